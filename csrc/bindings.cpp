@@ -1,0 +1,243 @@
+// torch op registrations (namespace "kgc") for the gfx950 HIP kernels.
+// Every op validates shapes/dtypes/devices on the host before launching: a bad
+// launch on the MI355X pool can fault the whole node, so nothing reaches a
+// kernel unless the kernel's indexing assumptions hold.
+#include <torch/library.h>
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+
+#include "kernels/launch.h"
+
+namespace {
+
+using at::Tensor;
+
+int dt_code(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kBFloat16: return kgc::DT_BF16;
+    case at::kHalf: return kgc::DT_F16;
+    case at::kFloat: return kgc::DT_F32;
+    default: TORCH_CHECK(false, "kgc: unsupported dtype ", t.scalar_type());
+  }
+  return -1;
+}
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
+
+void check_gpu(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "kgc: ", name, " must be a GPU tensor");
+}
+
+void check_same_dev(const Tensor& a, const Tensor& b, const char* name) {
+  TORCH_CHECK(a.device() == b.device(), "kgc: ", name, " on a different device");
+}
+
+int log2_exact(int64_t v, const char* what) {
+  int l = 0;
+  while ((int64_t(1) << l) < v) ++l;
+  TORCH_CHECK((int64_t(1) << l) == v, "kgc: ", what, " must be a power of two, got ", v);
+  return l;
+}
+
+void rms_norm(Tensor out, Tensor x, std::optional<Tensor> residual, Tensor w, double eps) {
+  check_gpu(x, "x");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  TORCH_CHECK(x.dim() == 2 && out.dim() == 2, "kgc.rms_norm: 2-D [rows, H] expected");
+  const int64_t rows = x.size(0), H = x.size(1);
+  TORCH_CHECK(H % 8 == 0 && H <= 8192, "kgc.rms_norm: H must be a multiple of 8 and <= 8192");
+  TORCH_CHECK(x.stride(1) == 1 && x.stride(0) % 8 == 0, "kgc.rms_norm: x rows must be dense, 16B aligned");
+  TORCH_CHECK(out.is_contiguous() && out.sizes() == x.sizes(), "kgc.rms_norm: out shape");
+  TORCH_CHECK(w.is_contiguous() && w.numel() == H && w.scalar_type() == x.scalar_type(), "kgc.rms_norm: weight");
+  TORCH_CHECK(out.scalar_type() == x.scalar_type(), "kgc.rms_norm: out dtype");
+  void* rp = nullptr;
+  if (residual.has_value()) {
+    TORCH_CHECK(residual->is_contiguous() && residual->sizes() == x.sizes() &&
+                residual->scalar_type() == x.scalar_type(), "kgc.rms_norm: residual");
+    TORCH_CHECK(x.is_contiguous(), "kgc.rms_norm: fused add needs contiguous x");
+    rp = residual->data_ptr();
+  }
+  kgc::launch_rms_norm(dt_code(x), out.data_ptr(), x.data_ptr(), rp, w.data_ptr(), (int)rows,
+                       (int)H, x.stride(0), (float)eps, stream());
+}
+
+void layer_norm(Tensor out, Tensor x, Tensor w, Tensor b, double eps) {
+  check_gpu(x, "x");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && out.is_contiguous() && out.sizes() == x.sizes(),
+              "kgc.layer_norm: contiguous 2-D");
+  const int64_t H = x.size(1);
+  TORCH_CHECK(H % 8 == 0 && H <= 8192, "kgc.layer_norm: H");
+  TORCH_CHECK(w.numel() == H && b.numel() == H, "kgc.layer_norm: weight/bias");
+  kgc::launch_layer_norm(dt_code(x), out.data_ptr(), x.data_ptr(), w.data_ptr(), b.data_ptr(),
+                         (int)x.size(0), (int)H, (float)eps, stream());
+}
+
+void silu_mul(Tensor out, Tensor x) {
+  check_gpu(x, "x");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && out.is_contiguous(), "kgc.silu_mul: contiguous 2-D");
+  const int64_t I = x.size(1) / 2;
+  TORCH_CHECK(x.size(1) % 16 == 0 && out.size(0) == x.size(0) && out.size(1) == I,
+              "kgc.silu_mul: shapes");
+  kgc::launch_silu_mul(dt_code(x), out.data_ptr(), x.data_ptr(), x.size(0), (int)I, stream());
+}
+
+void rope_kv_write(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor q_out, Tensor k_cache,
+                   Tensor v_cache, Tensor slot_mapping, std::optional<Tensor> q_norm_w,
+                   std::optional<Tensor> k_norm_w, int64_t nq, int64_t nkv, int64_t d,
+                   double eps, bool use_rope) {
+  check_gpu(qkv, "qkv");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
+  TORCH_CHECK(d % 16 == 0 && d <= 256, "kgc.rope_kv_write: head_dim");
+  const int64_t T = qkv.size(0);
+  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1 && qkv.size(1) >= (nq + 2 * nkv) * d &&
+              qkv.stride(0) % 8 == 0, "kgc.rope_kv_write: qkv [T, (nq+2nkv)*d]");
+  TORCH_CHECK(positions.scalar_type() == at::kLong && positions.numel() == T, "positions int64 [T]");
+  TORCH_CHECK(slot_mapping.scalar_type() == at::kLong && slot_mapping.numel() == T, "slot_mapping int64 [T]");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() && cos_sin.size(1) == d,
+              "cos_sin fp32 [max_pos, d]");
+  TORCH_CHECK(q_out.is_contiguous() && q_out.numel() == T * nq * d, "q_out [T, nq, d]");
+  TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && k_cache.dim() == 4 &&
+              k_cache.size(1) == nkv && k_cache.size(3) == d && v_cache.size(2) == d &&
+              v_cache.size(3) == k_cache.size(2), "kv cache layout");
+  TORCH_CHECK(k_cache.scalar_type() == qkv.scalar_type() && q_out.scalar_type() == qkv.scalar_type(),
+              "kgc.rope_kv_write: dtype");
+  const void* qn = nullptr;
+  const void* kn = nullptr;
+  if (q_norm_w.has_value()) {
+    TORCH_CHECK(k_norm_w.has_value() && q_norm_w->numel() == d && k_norm_w->numel() == d, "qk norm weights");
+    qn = q_norm_w->data_ptr();
+    kn = k_norm_w->data_ptr();
+  }
+  kgc::launch_rope_kv_write(dt_code(qkv), qkv.data_ptr(), qkv.stride(0),
+                            positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
+                            q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
+                            slot_mapping.data_ptr<int64_t>(), qn, kn, (int)T, (int)nq, (int)nkv,
+                            (int)d, (int)k_cache.size(2), (float)eps, use_rope, stream());
+}
+
+void check_kv(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, int64_t nq) {
+  TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 4 && k_cache.is_contiguous() &&
+              v_cache.is_contiguous(), "kv cache must be contiguous 4-D");
+  const int64_t nkv = k_cache.size(1), bs = k_cache.size(2), d = k_cache.size(3);
+  TORCH_CHECK(v_cache.size(0) == k_cache.size(0) && v_cache.size(1) == nkv &&
+              v_cache.size(2) == d && v_cache.size(3) == bs, "v_cache must be [nb, nkv, d, bs]");
+  TORCH_CHECK(d == 64 || d == 128, "head_dim must be 64 or 128");
+  TORCH_CHECK(nq % nkv == 0 && nq / nkv <= 16, "GQA group must be <= 16");
+  TORCH_CHECK(bs >= 16, "block_size must be >= 16");
+  TORCH_CHECK(q.scalar_type() == k_cache.scalar_type() && q.scalar_type() == v_cache.scalar_type(),
+              "q / cache dtype mismatch");
+  TORCH_CHECK(q.scalar_type() != at::kFloat, "attention kernels take bf16/f16");
+  check_same_dev(q, k_cache, "k_cache");
+  check_same_dev(q, v_cache, "v_cache");
+}
+
+void paged_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables,
+                  Tensor ctx_lens, Tensor max_logits, Tensor exp_sums, Tensor tmp_out,
+                  int64_t Z, double scale) {
+  check_gpu(q, "q");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
+  TORCH_CHECK(q.dim() == 3 && q.is_contiguous(), "q [B, nq, d] contiguous");
+  const int64_t B = q.size(0), nq = q.size(1), d = q.size(2);
+  check_kv(q, k_cache, v_cache, nq);
+  TORCH_CHECK(k_cache.size(3) == d, "head_dim mismatch");
+  TORCH_CHECK(out.is_contiguous() && out.sizes() == q.sizes() && out.scalar_type() == q.scalar_type(), "out");
+  TORCH_CHECK(block_tables.scalar_type() == at::kInt && block_tables.dim() == 2 &&
+              block_tables.size(0) >= B && block_tables.is_contiguous(), "block_tables int32 [B, max_blocks] contiguous");
+  TORCH_CHECK(ctx_lens.scalar_type() == at::kInt && ctx_lens.numel() >= B, "ctx_lens int32 [B]");
+  TORCH_CHECK(max_logits.scalar_type() == at::kFloat && exp_sums.scalar_type() == at::kFloat &&
+              tmp_out.scalar_type() == at::kFloat, "partials fp32");
+  const int64_t P_max = max_logits.size(-1);
+  TORCH_CHECK(max_logits.is_contiguous() && exp_sums.is_contiguous() && tmp_out.is_contiguous() &&
+              max_logits.numel() >= B * nq * P_max && exp_sums.numel() >= B * nq * P_max &&
+              tmp_out.numel() >= B * nq * P_max * d, "partials too small");
+  const int64_t bs = k_cache.size(2);
+  TORCH_CHECK(P_max * kgc::paged_decode_partition_size() >= block_tables.size(1) * bs,
+              "partials must cover block_tables capacity");
+  TORCH_CHECK(Z >= 1 && Z <= 65535, "Z");
+  kgc::launch_paged_decode(dt_code(q), out.data_ptr(), q.data_ptr(), k_cache.data_ptr(),
+                           v_cache.data_ptr(), block_tables.data_ptr<int>(),
+                           (int)block_tables.stride(0), ctx_lens.data_ptr<int>(),
+                           max_logits.data_ptr<float>(), exp_sums.data_ptr<float>(),
+                           tmp_out.data_ptr<float>(), (int)B, (int)nq, (int)k_cache.size(1),
+                           (int)d, log2_exact(bs, "block_size"), (int)P_max, (int)Z,
+                           (float)scale, stream());
+}
+
+void prefill_attention(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables,
+                       Tensor query_start_loc, Tensor seq_lens, Tensor work_seq,
+                       Tensor work_mblk, double scale) {
+  check_gpu(q, "q");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
+  TORCH_CHECK(q.dim() == 3 && q.is_contiguous(), "q [T, nq, d] contiguous");
+  const int64_t nq = q.size(1), d = q.size(2);
+  check_kv(q, k_cache, v_cache, nq);
+  TORCH_CHECK(k_cache.size(3) == d, "head_dim mismatch");
+  TORCH_CHECK(out.is_contiguous() && out.sizes() == q.sizes() && out.scalar_type() == q.scalar_type(), "out");
+  const int64_t P = seq_lens.numel();
+  TORCH_CHECK(block_tables.scalar_type() == at::kInt && block_tables.dim() == 2 &&
+              block_tables.size(0) >= P && block_tables.is_contiguous(), "block_tables contiguous");
+  TORCH_CHECK(query_start_loc.scalar_type() == at::kInt && query_start_loc.numel() == P + 1, "query_start_loc");
+  TORCH_CHECK(seq_lens.scalar_type() == at::kInt, "seq_lens int32");
+  TORCH_CHECK(work_seq.scalar_type() == at::kInt && work_mblk.scalar_type() == at::kInt &&
+              work_seq.numel() == work_mblk.numel(), "work list");
+  TORCH_CHECK(work_seq.numel() <= 2147483647 && nq <= 65535, "grid");
+  kgc::launch_prefill_attention(dt_code(q), q.data_ptr(), out.data_ptr(), k_cache.data_ptr(),
+                                v_cache.data_ptr(), block_tables.data_ptr<int>(),
+                                (int)block_tables.stride(0), query_start_loc.data_ptr<int>(),
+                                seq_lens.data_ptr<int>(), work_seq.data_ptr<int>(),
+                                work_mblk.data_ptr<int>(), (int)work_seq.numel(), (int)nq,
+                                (int)k_cache.size(1), (int)d,
+                                log2_exact(k_cache.size(2), "block_size"), (float)scale, stream());
+}
+
+void sample(Tensor out, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds) {
+  check_gpu(logits, "logits");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits [B, V] with dense rows");
+  const int64_t B = logits.size(0);
+  TORCH_CHECK(out.scalar_type() == at::kLong && out.numel() >= B, "out int64 [B]");
+  TORCH_CHECK(temperature.scalar_type() == at::kFloat && temperature.numel() >= B, "temperature fp32");
+  TORCH_CHECK(top_k.scalar_type() == at::kInt && top_k.numel() >= B, "top_k int32");
+  TORCH_CHECK(top_p.scalar_type() == at::kFloat && top_p.numel() >= B, "top_p fp32");
+  TORCH_CHECK(seeds.scalar_type() == at::kLong && seeds.numel() >= B, "seeds int64");
+  kgc::launch_sample(dt_code(logits), out.data_ptr<int64_t>(), logits.data_ptr(), logits.stride(0),
+                     (int)B, (int)logits.size(1), temperature.data_ptr<float>(),
+                     top_k.data_ptr<int>(), top_p.data_ptr<float>(), seeds.data_ptr<int64_t>(),
+                     stream());
+}
+
+int64_t decode_partition_size() { return kgc::paged_decode_partition_size(); }
+int64_t prefill_block_m() { return kgc::prefill_block_m(); }
+
+}  // namespace
+
+TORCH_LIBRARY(kgc, m) {
+  m.def("rms_norm(Tensor(a!) out, Tensor x, Tensor(b!)? residual, Tensor weight, float eps) -> ()");
+  m.def("layer_norm(Tensor(a!) out, Tensor x, Tensor weight, Tensor bias, float eps) -> ()");
+  m.def("silu_mul(Tensor(a!) out, Tensor x) -> ()");
+  m.def("rope_kv_write(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor(a!) q_out, "
+        "Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor slot_mapping, Tensor? q_norm_w, "
+        "Tensor? k_norm_w, int nq, int nkv, int d, float eps, bool use_rope) -> ()");
+  m.def("paged_decode(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
+        "Tensor block_tables, Tensor ctx_lens, Tensor(b!) max_logits, Tensor(c!) exp_sums, "
+        "Tensor(d!) tmp_out, int Z, float scale) -> ()");
+  m.def("prefill_attention(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
+        "Tensor block_tables, Tensor query_start_loc, Tensor seq_lens, Tensor work_seq, "
+        "Tensor work_mblk, float scale) -> ()");
+  m.def("sample(Tensor(a!) out, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, "
+        "Tensor seeds) -> ()");
+  m.def("decode_partition_size() -> int", &decode_partition_size);
+  m.def("prefill_block_m() -> int", &prefill_block_m);
+}
+
+TORCH_LIBRARY_IMPL(kgc, CUDA, m) {
+  m.impl("rms_norm", &rms_norm);
+  m.impl("layer_norm", &layer_norm);
+  m.impl("silu_mul", &silu_mul);
+  m.impl("rope_kv_write", &rope_kv_write);
+  m.impl("paged_decode", &paged_decode);
+  m.impl("prefill_attention", &prefill_attention);
+  m.impl("sample", &sample);
+}

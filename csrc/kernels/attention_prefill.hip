@@ -1,0 +1,259 @@
+// K2 varlen causal prefill attention over the paged KV cache (gfx950, bf16/f16).
+//
+// Each sequence contributes query rows [qsl[i], qsl[i+1]) at absolute positions
+// seq_len-qlen .. seq_len-1 and attends causally to cache positions [0, seq_len):
+// fresh prompts and chunked-prefill continuations run the same code.  The new
+// tokens' K/V were already scattered into the cache by rope_kv_write.
+//
+// Grid: (work items, q-heads); a work item = (sequence, 128-row query block), listed
+// heaviest-first by the host.  Workgroup = 4 waves x 32 query rows (two 16-row
+// q-tiles per wave).  K/V advance in 64-key tiles staged global->VGPR->LDS,
+// double-buffered, loads issued before the tile's MFMAs and written after them
+// (one barrier per tile).
+//
+// MFMA orientation (v_mfma_f32_16x16x32): S^T = K.Q^T and O^T = V^T.P^T, so the
+// query index is lane&15 in every accumulator: the online-softmax max/sum/rescale
+// are lane-local (+ xor 16/32), and S^T's accumulator is already the B operand of
+// the P.V product (row->key map key(m) = 8*(m>>2)+(m&3), +4 for the second tile of
+// each 32-key pair).
+// LDS images (16-byte chunk swizzles, conflict-free for the ds_read_b128 groups):
+//   K   [64 keys][D]   chunk c of key k stored at c ^ f(k), f(k) = (k&3)|((k>>3)&3)<<2
+//   V^T [D][64 keys]   chunk c of dim d stored at c ^ ((d>>1)&7)
+#include "common.h"
+#include "launch.h"
+
+namespace kgc {
+
+constexpr int PF_BM = 128;
+constexpr int PF_BN = 64;
+
+__device__ __forceinline__ int kswz(int k) { return (k & 3) | (((k >> 3) & 3) << 2); }
+
+template <typename T, int D>
+__global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
+    const T* __restrict__ q, T* __restrict__ out, const T* __restrict__ kc,
+    const T* __restrict__ vc, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ qsl, const int* __restrict__ seq_lens,
+    const int* __restrict__ work_seq, const int* __restrict__ work_mblk, int nq, int nkv,
+    int bs_log2, float scale_log2) {
+  typedef typename Vec8<T>::type V8;
+  constexpr int NCH = D / 8;                 // 16-byte chunks per K row
+  constexpr int KS = D / 32;                 // k-steps of QK^T
+  constexpr int DT = D / 16;                 // d-tiles of O^T
+  constexpr int KPT = PF_BN * NCH / 256;     // K chunks staged per thread
+  constexpr int VPT = D * (PF_BN / 8) / 256; // V chunks staged per thread
+  constexpr int TILE = PF_BN * D;            // elements per K (or V) image
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* lds = reinterpret_cast<T*>(smem);
+
+  const int seq = work_seq[blockIdx.x], mb = work_mblk[blockIdx.x];
+  const int hq = blockIdx.y;
+  const int h = hq / (nq / nkv);
+  const int q0 = qsl[seq];
+  const int qlen = qsl[seq + 1] - q0;
+  const int L = min(seq_lens[seq], bt_stride << bs_log2);  // never index past the table
+  const int ctx0 = L - qlen;
+  if (qlen <= 0 || ctx0 < 0) return;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r16 = lane & 15, qd = lane >> 4;
+  const int* bt = block_tables + (int64_t)seq * bt_stride;
+  const int bsm = (1 << bs_log2) - 1;
+  const int64_t hs = (int64_t)D << bs_log2;  // elements per (block, kv-head)
+
+  V8 qf[2][KS];
+  int qpos[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qi = mb * PF_BM + wave * 32 + qt * 16 + r16;
+    const int qc = min(qi, qlen - 1);
+    qpos[qt] = ctx0 + qc;
+    const T* qrow = q + ((int64_t)(q0 + qc) * nq + hq) * D;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      Pack8<T> t;
+      t.u = *reinterpret_cast<const u32x4*>(qrow + 32 * s + 8 * qd);
+      qf[qt][s] = t.v;
+    }
+  }
+  const int last_q = ctx0 + min((mb + 1) * PF_BM, qlen) - 1;
+  const int n_tiles = last_q / PF_BN + 1;
+
+  u32x4 kreg[KPT], vreg[VPT];
+  auto load_tile = [&](int kt) {
+#pragma unroll
+    for (int u = 0; u < KPT; ++u) {
+      const int ci = threadIdx.x + 256 * u;
+      const int key = ci / NCH, c = ci % NCH;
+      const int ka = min(kt * PF_BN + key, L - 1);
+      const T* src = kc + (int64_t)bt[ka >> bs_log2] * nkv * hs + h * hs +
+                     (int64_t)(ka & bsm) * D + c * 8;
+      kreg[u] = *reinterpret_cast<const u32x4*>(src);
+    }
+#pragma unroll
+    for (int u = 0; u < VPT; ++u) {
+      const int ci = threadIdx.x + 256 * u;
+      const int d = ci >> 3, c = ci & 7;
+      const int ka = min(kt * PF_BN + 8 * c, L - 1) & ~7;
+      const T* src = vc + (int64_t)bt[ka >> bs_log2] * nkv * hs + h * hs +
+                     ((int64_t)d << bs_log2) + (ka & bsm);
+      vreg[u] = *reinterpret_cast<const u32x4*>(src);
+    }
+  };
+  auto store_tile = [&](int buf) {
+    T* K = lds + buf * 2 * TILE;
+    T* V = K + TILE;
+#pragma unroll
+    for (int u = 0; u < KPT; ++u) {
+      const int ci = threadIdx.x + 256 * u;
+      const int key = ci / NCH, c = ci % NCH;
+      *reinterpret_cast<u32x4*>(K + key * D + ((c ^ (kswz(key) & (NCH - 1))) * 8)) = kreg[u];
+    }
+#pragma unroll
+    for (int u = 0; u < VPT; ++u) {
+      const int ci = threadIdx.x + 256 * u;
+      const int d = ci >> 3, c = ci & 7;
+      *reinterpret_cast<u32x4*>(V + d * PF_BN + ((c ^ ((d >> 1) & 7)) * 8)) = vreg[u];
+    }
+  };
+
+  f32x4 o[2][DT];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+    for (int t = 0; t < DT; ++t) o[qt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  const int keyA = 8 * (r16 >> 2) + (r16 & 3);
+  for (int kt = 0; kt < n_tiles; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < n_tiles) load_tile(kt + 1);
+    const T* K = lds + buf * 2 * TILE;
+    const T* V = K + TILE;
+    // ---- S^T tiles: [qt][a0, b0, a1, b1]
+    f32x4 s[2][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int key = (j >> 1) * 32 + keyA + 4 * (j & 1);
+      const T* krow = K + key * D;
+      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        Pack8<T> f;
+        f.u = *reinterpret_cast<const u32x4*>(krow + (((4 * ks + qd) ^ (r16 & (NCH - 1))) * 8));
+        a0 = mfma16x16x32(f.v, qf[0][ks], a0);
+        a1 = mfma16x16x32(f.v, qf[1][ks], a1);
+      }
+      s[0][j] = a0;
+      s[1][j] = a1;
+    }
+    // ---- causal mask + online softmax (query = lane&15: lane-local stats)
+    V8 pf[2][2];
+    const bool diag = (kt + 1) * PF_BN - 1 > ctx0 + mb * PF_BM + wave * 32;
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = kt * PF_BN + (j >> 1) * 32 + 8 * qd + 4 * (j & 1) + i;
+          float v = s[qt][j][i] * scale_log2;
+          if (diag && key > qpos[qt]) v = -INFINITY;
+          s[qt][j][i] = v;
+          tmax = fmaxf(tmax, v);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+      const float mn = fmaxf(m[qt], tmax);
+      const float alpha = exp2f(m[qt] - mn);
+      m[qt] = mn;
+      l[qt] *= alpha;
+#pragma unroll
+      for (int t = 0; t < DT; ++t) o[qt][t] *= alpha;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        Pack8<T> pk;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float pa = exp2f(s[qt][2 * kk][i] - mn);
+          const float pb = exp2f(s[qt][2 * kk + 1][i] - mn);
+          l[qt] += pa + pb;
+          pk.h[i] = from_f<T>(pa);
+          pk.h[4 + i] = from_f<T>(pb);
+        }
+        pf[qt][kk] = pk.v;
+      }
+    }
+    // ---- O^T += V^T . P^T
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      const int d = 16 * t + r16;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        Pack8<T> f;
+        f.u = *reinterpret_cast<const u32x4*>(V + d * PF_BN +
+                                              (((4 * kk + qd) ^ ((d >> 1) & 7)) * 8));
+        o[0][t] = mfma16x16x32(f.v, pf[0][kk], o[0][t]);
+        o[1][t] = mfma16x16x32(f.v, pf[1][kk], o[1][t]);
+      }
+    }
+    if (kt + 1 < n_tiles) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+  // ---- epilogue: O / l; lane holds O[query r16][16t + 4qd + i]
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    float tot = l[qt];
+    tot += __shfl_xor(tot, 16, 64);
+    tot += __shfl_xor(tot, 32, 64);
+    const float inv = 1.f / tot;
+    const int qi = mb * PF_BM + wave * 32 + qt * 16 + r16;
+    if (qi < qlen) {
+      T* orow = out + ((int64_t)(q0 + qi) * nq + hq) * D + 4 * qd;
+#pragma unroll
+      for (int t = 0; t < DT; ++t) {
+        Pack4<T> pk;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pk.h[i] = from_f<T>(o[qt][t][i] * inv);
+        *reinterpret_cast<u32x2*>(orow + 16 * t) = pk.u;
+      }
+    }
+  }
+}
+
+template <typename T, int D>
+static void prefill_dispatch(const void* q, void* out, const void* kc, const void* vc,
+                             const int* bt, int bt_stride, const int* qsl, const int* sl,
+                             const int* ws, const int* wm, int n_work, int nq, int nkv,
+                             int bs_log2, float scale_log2, hipStream_t s) {
+  const size_t lds = 2 * 2 * PF_BN * D * sizeof(T);
+  prefill_attn_kernel<T, D><<<dim3(n_work, nq), 256, lds, s>>>(
+      (const T*)q, (T*)out, (const T*)kc, (const T*)vc, bt, bt_stride, qsl, sl, ws, wm, nq,
+      nkv, bs_log2, scale_log2);
+}
+
+void launch_prefill_attention(int dtype, const void* q, void* out, const void* k_cache,
+                              const void* v_cache, const int* block_tables, int bt_stride,
+                              const int* query_start_loc, const int* seq_lens,
+                              const int* work_seq, const int* work_mblk, int n_work, int nq,
+                              int nkv, int D, int bs_log2, float scale, hipStream_t s) {
+  if (n_work == 0) return;
+  const float sl2 = scale * 1.4426950408889634f;
+#define KGC_PF(TT, DD)                                                                     \
+  prefill_dispatch<TT, DD>(q, out, k_cache, v_cache, block_tables, bt_stride,              \
+                           query_start_loc, seq_lens, work_seq, work_mblk, n_work, nq, nkv, \
+                           bs_log2, sl2, s)
+  if (dtype == DT_BF16) {
+    if (D == 128) KGC_PF(bf16, 128); else KGC_PF(bf16, 64);
+  } else {
+    if (D == 128) KGC_PF(f16, 128); else KGC_PF(f16, 64);
+  }
+#undef KGC_PF
+}
+
+int prefill_block_m() { return PF_BM; }
+
+}  // namespace kgc

@@ -1,0 +1,136 @@
+// K4 RMSNorm / fused residual-add + RMSNorm, K8 LayerNorm (OPT), K6 helper.
+// One workgroup per row; each thread owns up to MAXV 16-byte vectors of the row
+// held in registers between the reduction and the scale pass (single HBM read).
+#include "common.h"
+#include "launch.h"
+
+namespace kgc {
+
+constexpr int NORM_NT = 256;
+constexpr int NORM_MAXV = 4;  // 256 thr * 4 vec * 8 elems = 8192 = Llama-3-70B hidden
+
+template <typename T, bool ADD>
+__global__ __launch_bounds__(NORM_NT) void rms_norm_kernel(
+    T* __restrict__ out, const T* __restrict__ x, T* __restrict__ residual,
+    const T* __restrict__ w, int H, int64_t x_stride, float eps) {
+  __shared__ float scratch[NORM_NT / 64];
+  const int row = blockIdx.x;
+  const int nv = H >> 3;
+  const T* xr = x + row * x_stride;
+  T* rr = ADD ? residual + (int64_t)row * H : nullptr;
+  Pack8<T> v[NORM_MAXV];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NORM_MAXV; ++i) {
+    const int idx = threadIdx.x + i * NORM_NT;
+    if (idx < nv) {
+      v[i].u = *reinterpret_cast<const u32x4*>(xr + idx * 8);
+      if (ADD) {
+        Pack8<T> r;
+        r.u = *reinterpret_cast<const u32x4*>(rr + idx * 8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i].h[j] = from_f<T>(to_f(v[i].h[j]) + to_f(r.h[j]));
+        *reinterpret_cast<u32x4*>(rr + idx * 8) = v[i].u;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float f = to_f(v[i].h[j]);
+        ss += f * f;
+      }
+    }
+  }
+  ss = block_sum<NORM_NT>(ss, scratch);
+  const float inv = rsqrtf(ss / (float)H + eps);
+  T* orow = out + (int64_t)row * H;
+#pragma unroll
+  for (int i = 0; i < NORM_MAXV; ++i) {
+    const int idx = threadIdx.x + i * NORM_NT;
+    if (idx < nv) {
+      Pack8<T> wv, o;
+      wv.u = *reinterpret_cast<const u32x4*>(w + idx * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o.h[j] = from_f<T>(to_f(v[i].h[j]) * inv * to_f(wv.h[j]));
+      *reinterpret_cast<u32x4*>(orow + idx * 8) = o.u;
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NORM_NT) void layer_norm_kernel(
+    T* __restrict__ out, const T* __restrict__ x, const T* __restrict__ w,
+    const T* __restrict__ b, int H, float eps) {
+  __shared__ float scratch[NORM_NT / 64];
+  const int row = blockIdx.x;
+  const int nv = H >> 3;
+  const T* xr = x + (int64_t)row * H;
+  Pack8<T> v[NORM_MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NORM_MAXV; ++i) {
+    const int idx = threadIdx.x + i * NORM_NT;
+    if (idx < nv) {
+      v[i].u = *reinterpret_cast<const u32x4*>(xr + idx * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += to_f(v[i].h[j]);
+    }
+  }
+  const float mean = block_sum<NORM_NT>(s, scratch) / (float)H;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NORM_MAXV; ++i) {
+    const int idx = threadIdx.x + i * NORM_NT;
+    if (idx < nv) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = to_f(v[i].h[j]) - mean;
+        ss += d * d;
+      }
+    }
+  }
+  const float inv = rsqrtf(block_sum<NORM_NT>(ss, scratch) / (float)H + eps);
+  T* orow = out + (int64_t)row * H;
+#pragma unroll
+  for (int i = 0; i < NORM_MAXV; ++i) {
+    const int idx = threadIdx.x + i * NORM_NT;
+    if (idx < nv) {
+      Pack8<T> wv, bv, o;
+      wv.u = *reinterpret_cast<const u32x4*>(w + idx * 8);
+      bv.u = *reinterpret_cast<const u32x4*>(b + idx * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        o.h[j] = from_f<T>((to_f(v[i].h[j]) - mean) * inv * to_f(wv.h[j]) + to_f(bv.h[j]));
+      *reinterpret_cast<u32x4*>(orow + idx * 8) = o.u;
+    }
+  }
+}
+
+template <typename T>
+static void rms_dispatch(void* out, const void* x, void* res, const void* w, int rows, int H,
+                         int64_t xs, float eps, hipStream_t s) {
+  if (rows == 0) return;
+  if (res)
+    rms_norm_kernel<T, true><<<rows, NORM_NT, 0, s>>>((T*)out, (const T*)x, (T*)res,
+                                                      (const T*)w, H, xs, eps);
+  else
+    rms_norm_kernel<T, false><<<rows, NORM_NT, 0, s>>>((T*)out, (const T*)x, nullptr,
+                                                       (const T*)w, H, xs, eps);
+}
+
+void launch_rms_norm(int dtype, void* out, const void* x, void* residual, const void* w,
+                     int rows, int H, int64_t x_stride, float eps, hipStream_t s) {
+  if (dtype == DT_BF16) rms_dispatch<bf16>(out, x, residual, w, rows, H, x_stride, eps, s);
+  else rms_dispatch<f16>(out, x, residual, w, rows, H, x_stride, eps, s);
+}
+
+void launch_layer_norm(int dtype, void* out, const void* x, const void* w, const void* b,
+                       int rows, int H, float eps, hipStream_t s) {
+  if (rows == 0) return;
+  if (dtype == DT_BF16)
+    layer_norm_kernel<bf16><<<rows, NORM_NT, 0, s>>>((bf16*)out, (const bf16*)x,
+                                                     (const bf16*)w, (const bf16*)b, H, eps);
+  else
+    layer_norm_kernel<f16><<<rows, NORM_NT, 0, s>>>((f16*)out, (const f16*)x, (const f16*)w,
+                                                    (const f16*)b, H, eps);
+}
+
+}  // namespace kgc

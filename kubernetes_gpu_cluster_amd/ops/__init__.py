@@ -1,0 +1,206 @@
+"""Fused ops: gfx950 HIP kernels (``torch.ops.kgc``) for GPU tensors, the
+pure-PyTorch reference (``ops.reference``) for CPU tensors.
+
+There is exactly one GPU implementation per op.  If a GPU tensor reaches an op
+and the in-tree extension ``_kgc_ops.so`` is not loadable, the op raises: there
+is no silent eager fallback on the GPU path.
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import Optional
+
+import torch
+
+from . import reference as ref
+
+_SO = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_kgc_ops.so")
+_loaded: Optional[bool] = None
+_load_err: Optional[str] = None
+
+
+def load_extension(strict: bool = False) -> bool:
+    """Load the HIP kernel library once.  strict=True raises if unavailable."""
+    global _loaded, _load_err
+    if _loaded is None:
+        try:
+            if not os.path.exists(_SO):
+                raise FileNotFoundError(f"{_SO} not built (run `python csrc/build.py`)")
+            torch.ops.load_library(_SO)
+            _loaded = True
+        except Exception as e:  # noqa: BLE001 - report reason on use
+            _loaded, _load_err = False, f"{type(e).__name__}: {e}"
+    if strict and not _loaded:
+        raise RuntimeError(f"kgc HIP extension unavailable: {_load_err}")
+    return bool(_loaded)
+
+
+def extension_path() -> str:
+    return _SO
+
+
+def _k():
+    load_extension(strict=True)
+    return torch.ops.kgc
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+# ------------------------------------------------------------------ norms
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float,
+             out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if not _gpu(x):
+        r = ref.rms_norm(x, w, eps)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    x2 = x.reshape(-1, x.shape[-1]) if x.is_contiguous() else x
+    out = torch.empty(x2.shape, dtype=x.dtype, device=x.device) if out is None else out
+    _k().rms_norm(out.view(x2.shape), x2, None, w, eps)
+    return out.view(x.shape)
+
+
+def fused_add_rms_norm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
+                       eps: float) -> tuple[torch.Tensor, torch.Tensor]:
+    """In place: residual += x; x = rms_norm(residual) * w.  Returns (x, residual)."""
+    if not _gpu(x):
+        o, r = ref.fused_add_rms_norm(x, residual, w, eps)
+        x.copy_(o)
+        residual.copy_(r)
+        return x, residual
+    x2 = x.view(-1, x.shape[-1])
+    _k().rms_norm(x2, x2, residual.view(-1, x.shape[-1]), w, eps)
+    return x, residual
+
+
+def layer_norm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float = 1e-5):
+    if not _gpu(x):
+        return ref.layer_norm(x, w, b, eps)
+    x2 = x.reshape(-1, x.shape[-1]).contiguous()
+    out = torch.empty_like(x2)
+    _k().layer_norm(out, x2, w, b, eps)
+    return out.view(x.shape)
+
+
+def silu_mul(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if not _gpu(x):
+        return ref.silu_mul(x)
+    I = x.shape[-1] // 2
+    x2 = x.view(-1, x.shape[-1])
+    if out is None:
+        out = torch.empty(x2.shape[0], I, dtype=x.dtype, device=x.device)
+    _k().silu_mul(out, x2)
+    return out.view(*x.shape[:-1], I)
+
+
+# ------------------------------------------------------------------ rope + kv cache
+def rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor,
+                  k_cache: torch.Tensor, v_cache: torch.Tensor, slot_mapping: torch.Tensor,
+                  num_heads: int, num_kv_heads: int, head_dim: int,
+                  q_norm_w: Optional[torch.Tensor] = None,
+                  k_norm_w: Optional[torch.Tensor] = None, eps: float = 1e-6,
+                  use_rope: bool = True) -> torch.Tensor:
+    if not _gpu(qkv):
+        return ref.rope_qk_kv_write(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping,
+                                    num_heads, num_kv_heads, head_dim, q_norm_w, k_norm_w, eps,
+                                    use_rope)
+    T = qkv.shape[0]
+    q = torch.empty(T, num_heads, head_dim, dtype=qkv.dtype, device=qkv.device)
+    _k().rope_kv_write(qkv, positions, cos_sin, q, k_cache, v_cache, slot_mapping, q_norm_w,
+                       k_norm_w, num_heads, num_kv_heads, head_dim, eps, use_rope)
+    return q
+
+
+# ------------------------------------------------------------------ attention
+DECODE_PARTITION = 128
+PREFILL_BLOCK_M = 128
+
+
+def decode_partials(batch: int, num_heads: int, head_dim: int, max_blocks: int,
+                    block_size: int, device) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Workspace for the split-context decode kernel (static: graph-capturable)."""
+    P = math.ceil(max_blocks * block_size / DECODE_PARTITION)
+    ml = torch.empty(batch, num_heads, P, dtype=torch.float32, device=device)
+    es = torch.empty(batch, num_heads, P, dtype=torch.float32, device=device)
+    tmp = torch.empty(batch, num_heads, P, head_dim, dtype=torch.float32, device=device)
+    return ml, es, tmp
+
+
+def decode_grid_z(batch: int, num_kv_heads: int, max_ctx: int, target_waves: int = 4096) -> int:
+    """z-slices of the decode grid: enough waves to fill 256 CUs, bounded by the
+    number of 128-token partitions of the longest context."""
+    parts = max(1, math.ceil(max_ctx / DECODE_PARTITION))
+    want = math.ceil(target_waves / max(1, batch * num_kv_heads * 4))
+    return max(1, min(want, math.ceil(parts / 4)))
+
+
+def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                           block_tables: torch.Tensor, context_lens: torch.Tensor, scale: float,
+                           workspace=None, grid_z: int = 1,
+                           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if not _gpu(q):
+        return ref.paged_attention_decode(q, k_cache, v_cache, block_tables, context_lens, scale)
+    B, nq, d = q.shape
+    if out is None:
+        out = torch.empty_like(q)
+    if workspace is None:
+        workspace = decode_partials(B, nq, d, block_tables.shape[1], k_cache.shape[2], q.device)
+    ml, es, tmp = workspace
+    _k().paged_decode(out, q, k_cache, v_cache, block_tables, context_lens, ml, es, tmp,
+                      grid_z, scale)
+    return out
+
+
+def prefill_work_list(query_lens: list[int], seq_lens: list[int]) -> tuple[list[int], list[int]]:
+    """(seq, 128-row block) work items, heaviest (most keys) first."""
+    items = []
+    for i, (ql, sl) in enumerate(zip(query_lens, seq_lens)):
+        ctx0 = sl - ql
+        for mb in range((ql + PREFILL_BLOCK_M - 1) // PREFILL_BLOCK_M):
+            last = ctx0 + min((mb + 1) * PREFILL_BLOCK_M, ql)
+            items.append((-last, i, mb))
+    items.sort()
+    return [i for _, i, _ in items], [m for _, _, m in items]
+
+
+def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                      block_tables: torch.Tensor, query_start_loc: torch.Tensor,
+                      seq_lens: torch.Tensor, scale: float, work_seq: torch.Tensor = None,
+                      work_mblk: torch.Tensor = None,
+                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if not _gpu(q):
+        return ref.prefill_attention(q, k_cache, v_cache, block_tables, query_start_loc,
+                                     seq_lens, scale)
+    if work_seq is None:
+        qsl = query_start_loc.tolist()
+        ws, wm = prefill_work_list([qsl[i + 1] - qsl[i] for i in range(len(qsl) - 1)],
+                                   seq_lens.tolist())
+        work_seq = torch.tensor(ws, dtype=torch.int32, device=q.device)
+        work_mblk = torch.tensor(wm, dtype=torch.int32, device=q.device)
+    if out is None:
+        out = torch.empty_like(q)
+    _k().prefill_attention(out, q, k_cache, v_cache, block_tables, query_start_loc, seq_lens,
+                           work_seq, work_mblk, scale)
+    return out
+
+
+# ------------------------------------------------------------------ sampling
+def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
+           top_p: torch.Tensor, seeds: torch.Tensor,
+           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if not _gpu(logits):
+        return ref.sample(logits, temperature, top_k, top_p, seeds)
+    B = logits.shape[0]
+    if out is None:
+        out = torch.empty(B, dtype=torch.int64, device=logits.device)
+    _k().sample(out, logits, temperature, top_k, top_p, seeds)
+    return out
+
+
+__all__ = ["load_extension", "rms_norm", "fused_add_rms_norm", "layer_norm", "silu_mul",
+           "rope_kv_write", "paged_attention_decode", "prefill_attention", "sample",
+           "decode_partials", "decode_grid_z", "prefill_work_list", "ref"]
