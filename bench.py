@@ -1,0 +1,184 @@
+#!/usr/bin/env python3
+"""Headline benchmark: output tokens/s + p50 TTFT of the Llama-3-8B serving engine
+(BASELINE.json metric) on N MI355X GPUs of one node.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 the
+driver launches one rank per GPU with torch.distributed.run.  One *step* is one
+serving wave: ``--num-prompts`` requests (synthetic random token prompts of
+``--input-len`` tokens, ``--output-len`` generated tokens each, ignore_eos, temperature
+1.0 sampling) arrive at once and the continuous-batching engine runs until every
+request has finished -- the vLLM ``benchmark_serving`` request-rate=inf shape.
+TTFT is arrival -> first token of each request.
+
+Parallelism: ``dpN`` (default) runs one engine replica per GPU, like the reference's
+``replicaCount`` DP deployment behind the router (values-01-minimal-example2.yaml:10);
+per-GPU work is fixed, so scaling is weak.  ``--tp N`` runs one tensor-parallel
+engine over the N ranks (RCCL/xGMI all-reduce) instead.
+Weights are random-init bf16 of the real architecture (no checkpoints offline).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_METRIC = "output tokens/sec + p50 TTFT, Llama-3-8B K8s service at 1/2/4/8 MI355X"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="llama-3-8b")
+    ap.add_argument("--num-prompts", type=int, default=256, help="requests per wave per replica")
+    ap.add_argument("--input-len", type=int, default=512)
+    ap.add_argument("--output-len", type=int, default=256)
+    ap.add_argument("--max-num-seqs", type=int, default=256)
+    ap.add_argument("--max-num-batched-tokens", type=int, default=16384)
+    ap.add_argument("--max-model-len", type=int, default=4096)
+    ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--enforce-eager", action="store_true")
+    ap.add_argument("--gpu-memory-utilization", type=float, default=0.90)
+    ap.add_argument("--dtype", default="bfloat16")
+    ap.add_argument("--temperature", type=float, default=1.0)
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def run_wave(engine, args, wave: int, rank: int):
+    from kubernetes_gpu_cluster_amd.engine.sequence import SamplingParams
+    g = torch.Generator().manual_seed(1000 * wave + rank)
+    vocab = engine.mcfg.vocab_size
+    sp = SamplingParams(temperature=args.temperature, top_p=1.0, max_tokens=args.output_len,
+                        ignore_eos=True)
+    t0 = time.monotonic()
+    seqs = []
+    for i in range(args.num_prompts):
+        ids = torch.randint(100, vocab - 100, (args.input_len,), generator=g).tolist()
+        seqs.append(engine.add_request(ids, sp, request_id=f"w{wave}-r{rank}-{i}", arrival_time=t0))
+    steps = 0
+    while engine.has_unfinished():
+        engine.step()
+        steps += 1
+    t1 = time.monotonic()
+    out_toks = sum(len(s.output_token_ids) for s in seqs)
+    ttfts = [s.first_token_time - s.arrival_time for s in seqs]
+    tpots = [(s.last_token_time - s.first_token_time) / max(1, len(s.output_token_ids) - 1)
+             for s in seqs]
+    return out_toks, t1 - t0, ttfts, tpots, steps
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    n = world if world > 1 else 1
+    if args.gpus != n and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    assert torch.cuda.is_available(), "bench.py needs a GPU"
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    tp = args.tp
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    from kubernetes_gpu_cluster_amd.engine.config import EngineConfig
+    from kubernetes_gpu_cluster_amd.engine.llm_engine import LLMEngine
+    from kubernetes_gpu_cluster_amd.engine.worker import ExternalExecutor, Worker, worker_loop
+    cfg = EngineConfig(model=args.model, dtype=args.dtype, tensor_parallel_size=tp,
+                       max_model_len=args.max_model_len, max_num_seqs=args.max_num_seqs,
+                       max_num_batched_tokens=args.max_num_batched_tokens,
+                       gpu_memory_utilization=args.gpu_memory_utilization,
+                       enforce_eager=args.enforce_eager, random_init=True, seed=0, device="cuda")
+    engine = None
+    if tp > 1:
+        assert world % tp == 0
+        w = Worker(cfg, rank=rank, local_device=local_rank)
+        if w.ps.rank == 0:
+            engine = LLMEngine(cfg, ExternalExecutor(w))
+        else:
+            worker_loop(w)
+    else:
+        engine = LLMEngine(cfg)
+    replicas = world // tp
+    is_driver = engine is not None
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    res = None
+    if is_driver:
+        for wv in range(args.warmup):
+            run_wave(engine, args, -1 - wv, rank)
+    barrier() if tp == 1 else None
+    t0 = time.monotonic()
+    toks, ttfts, tpots, steps, wall = 0, [], [], 0, 0.0
+    if is_driver:
+        for wv in range(args.steps):
+            o, dt, tt, tp_, st = run_wave(engine, args, wv, rank)
+            toks += o
+            ttfts += tt
+            tpots += tp_
+            steps += st
+    if tp == 1:
+        barrier()
+    elapsed = time.monotonic() - t0
+    if is_driver and tp > 1:
+        engine.shutdown()
+    # aggregate over replicas (drivers) -- every rank participates in the collectives
+    if world > 1:
+        t = torch.tensor([elapsed if is_driver else 0.0, float(toks), float(steps)],
+                         dtype=torch.float64, device=dev)
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        elapsed, toks, steps = tmax[0].item(), int(t[1].item()), int(t[2].item())
+        gathered = [None] * world
+        dist.all_gather_object(gathered, (ttfts, tpots))
+        ttfts = [x for g in gathered for x in g[0]]
+        tpots = [x for g in gathered for x in g[1]]
+    if rank == 0:
+        value = toks / elapsed
+        p50_ttft = statistics.median(ttfts) * 1e3 if ttfts else None
+        out = {
+            "metric": BASELINE_METRIC, "value": round(value, 2), "unit": "output_tokens/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype if args.dtype != "bfloat16" else "bf16",
+            "data": "synthetic random-token prompts, random-init weights",
+            "p50_ttft_ms": round(p50_ttft, 2) if p50_ttft else None,
+            "p50_tpot_ms": round(statistics.median(tpots) * 1e3, 3) if tpots else None,
+            "engine_steps": steps,
+            "config": {"model": args.model, "global_batch": args.num_prompts * replicas,
+                       "seq_len": args.input_len + args.output_len, "input_len": args.input_len,
+                       "output_len": args.output_len,
+                       "parallelism": f"dp{replicas}" if tp == 1 else f"tp{tp}" + (f"xdp{replicas}" if replicas > 1 else ""),
+                       "max_num_seqs": args.max_num_seqs,
+                       "max_num_batched_tokens": args.max_num_batched_tokens,
+                       "cuda_graphs": not args.enforce_eager},
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

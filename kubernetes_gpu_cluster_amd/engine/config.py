@@ -1,0 +1,118 @@
+"""Engine configuration and the vLLM-compatible CLI flag surface.
+
+The reference passes engine flags through Helm ``vllmConfig`` keys and
+``extraArgs`` (``values-01-minimal-example8.yaml:23-38``):
+``--tensor-parallel-size``, ``--pipeline-parallel-size``, ``--max-model-len``,
+``--gpu-memory-utilization``, ``--dtype float16``, ``--disable-custom-all-reduce``,
+``--enforce-eager``, ``--trust-remote-code``, ``--kv-cache-dtype``.  All of them are
+accepted here with the same spelling (both ``--flag value`` and ``--flag=value``).
+"""
+from __future__ import annotations
+
+import argparse
+import dataclasses
+from typing import Optional
+
+import torch
+
+_DTYPES = {"auto": None, "bfloat16": torch.bfloat16, "bf16": torch.bfloat16,
+           "float16": torch.float16, "half": torch.float16, "fp16": torch.float16,
+           "float32": torch.float32, "float": torch.float32}
+
+
+@dataclasses.dataclass
+class EngineConfig:
+    model: str = "llama-3-8b"
+    served_model_name: Optional[str] = None
+    tokenizer: Optional[str] = None
+    dtype: str = "auto"
+    tensor_parallel_size: int = 1
+    pipeline_parallel_size: int = 1
+    max_model_len: Optional[int] = None
+    gpu_memory_utilization: float = 0.90
+    block_size: int = 32
+    max_num_seqs: int = 256
+    max_num_batched_tokens: Optional[int] = None
+    enable_chunked_prefill: bool = True
+    enforce_eager: bool = False
+    disable_custom_all_reduce: bool = False
+    trust_remote_code: bool = False
+    kv_cache_dtype: str = "auto"
+    seed: int = 0
+    random_init: bool = False
+    num_gpu_blocks_override: Optional[int] = None
+    device: str = "auto"                  # auto | cuda | cpu
+    moe_parallel: str = "tp"              # tp | ep  (Mixtral expert placement)
+    cuda_graph_max_bs: int = 256
+    async_output: bool = True             # overlap host bookkeeping with the next step
+    num_cpu_blocks: int = 0
+
+    def torch_dtype(self, model_default: torch.dtype = torch.bfloat16) -> torch.dtype:
+        d = _DTYPES.get(self.dtype.lower())
+        if self.dtype.lower() not in _DTYPES:
+            raise ValueError(f"unsupported --dtype {self.dtype}")
+        return model_default if d is None else d
+
+    def resolved_device(self) -> torch.device:
+        if self.device == "auto":
+            return torch.device("cuda" if torch.cuda.is_available() else "cpu")
+        return torch.device(self.device)
+
+    @property
+    def world_size(self) -> int:
+        return self.tensor_parallel_size * self.pipeline_parallel_size
+
+    def token_budget(self) -> int:
+        if self.max_num_batched_tokens:
+            return self.max_num_batched_tokens
+        return 16384 if self.enable_chunked_prefill else max(16384, self.max_model_len or 0)
+
+
+def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
+    a = p.add_argument
+    a("--model", type=str, default=None, help="preset name, local HF dir, or HF id")
+    a("--served-model-name", type=str, default=None)
+    a("--tokenizer", type=str, default=None)
+    a("--dtype", type=str, default="auto")
+    a("--tensor-parallel-size", "-tp", type=int, default=1)
+    a("--pipeline-parallel-size", "-pp", type=int, default=1)
+    a("--max-model-len", type=int, default=None)
+    a("--gpu-memory-utilization", type=float, default=0.90)
+    a("--block-size", type=int, default=32)
+    a("--max-num-seqs", type=int, default=256)
+    a("--max-num-batched-tokens", type=int, default=None)
+    a("--enable-chunked-prefill", dest="enable_chunked_prefill", action="store_true",
+      default=True)
+    a("--no-enable-chunked-prefill", dest="enable_chunked_prefill", action="store_false")
+    a("--enforce-eager", action="store_true")
+    a("--disable-custom-all-reduce", action="store_true")
+    a("--trust-remote-code", action="store_true")
+    a("--kv-cache-dtype", type=str, default="auto")
+    a("--seed", type=int, default=0)
+    a("--random-init", action="store_true", help="random weights (offline benchmarking)")
+    a("--load-format", type=str, default="auto", help="'dummy' == --random-init")
+    a("--num-gpu-blocks-override", type=int, default=None)
+    a("--device", type=str, default="auto")
+    a("--moe-parallel", type=str, default="tp", choices=["tp", "ep"])
+    a("--cuda-graph-max-bs", type=int, default=256)
+    a("--swap-space", type=float, default=0, help="accepted for compatibility (unused)")
+    a("--disable-log-requests", action="store_true")
+    a("--disable-log-stats", action="store_true")
+    return p
+
+
+def config_from_args(ns: argparse.Namespace) -> EngineConfig:
+    if ns.kv_cache_dtype not in ("auto", "bfloat16", "float16", "fp16", "bf16"):
+        raise ValueError(f"--kv-cache-dtype {ns.kv_cache_dtype} is not supported (auto/bf16/fp16)")
+    return EngineConfig(
+        model=ns.model, served_model_name=ns.served_model_name, tokenizer=ns.tokenizer,
+        dtype=ns.dtype, tensor_parallel_size=ns.tensor_parallel_size,
+        pipeline_parallel_size=ns.pipeline_parallel_size, max_model_len=ns.max_model_len,
+        gpu_memory_utilization=ns.gpu_memory_utilization, block_size=ns.block_size,
+        max_num_seqs=ns.max_num_seqs, max_num_batched_tokens=ns.max_num_batched_tokens,
+        enable_chunked_prefill=ns.enable_chunked_prefill, enforce_eager=ns.enforce_eager,
+        disable_custom_all_reduce=ns.disable_custom_all_reduce,
+        trust_remote_code=ns.trust_remote_code, kv_cache_dtype=ns.kv_cache_dtype, seed=ns.seed,
+        random_init=ns.random_init or ns.load_format == "dummy",
+        num_gpu_blocks_override=ns.num_gpu_blocks_override, device=ns.device,
+        moe_parallel=ns.moe_parallel, cuda_graph_max_bs=ns.cuda_graph_max_bs)

@@ -1,0 +1,162 @@
+"""LLMEngine: request intake, the schedule -> execute -> update step loop, and the
+offline ``LLM.generate`` API.
+
+One call to ``step()`` = one engine iteration (the serving hot loop of SURVEY.md
+§3.5): the scheduler picks a continuous batch (decodes + chunked prefills), the
+driver packs it into a StepPlan, every rank runs it, and sampled tokens are
+appended; stop conditions (EOS unless ignore_eos, stop_token_ids, max_tokens,
+max_model_len) finish sequences and free their KV blocks.
+"""
+from __future__ import annotations
+
+import itertools
+import logging
+import time
+from typing import Iterable, Optional, Union
+
+from ..models import resolve_model
+from ..utils.metrics import EngineMetrics
+from .block_manager import BlockManager
+from .config import EngineConfig
+from .scheduler import Scheduler
+from .sequence import RequestOutput, SamplingParams, Sequence
+from .worker import LocalExecutor, MultiprocExecutor, default_max_model_len
+
+log = logging.getLogger("kgc.engine")
+
+
+class LLMEngine:
+    def __init__(self, cfg: EngineConfig, executor=None):
+        self.cfg = cfg
+        self.mcfg, _ = resolve_model(cfg.model)
+        self.max_model_len = default_max_model_len(cfg)
+        if executor is None:
+            executor = LocalExecutor(cfg) if cfg.world_size == 1 else MultiprocExecutor(cfg)
+        self.executor = executor
+        t0 = time.time()
+        nb = executor.profile()
+        executor.init_cache(nb)
+        self.graph_s = executor.capture()
+        self.num_blocks = nb
+        runner = executor.runner
+        self.bm = BlockManager(nb, cfg.block_size, cfg.max_num_seqs, runner.max_blocks)
+        self.scheduler = Scheduler(self.bm, cfg.max_num_seqs, cfg.token_budget(),
+                                   self.max_model_len, cfg.enable_chunked_prefill)
+        self.seqs: dict[str, Sequence] = {}
+        self._ids = itertools.count()
+        self.metrics = EngineMetrics()
+        self.eos = self.mcfg.eos_token_id
+        self.init_s = time.time() - t0
+        log.info("engine ready: %d KV blocks x %d tokens, graphs %.1fs", nb, cfg.block_size,
+                 self.graph_s)
+
+    # ------------------------------------------------------------------ requests
+    def add_request(self, prompt_token_ids: list[int], params: Optional[SamplingParams] = None,
+                    request_id: Optional[str] = None, arrival_time: Optional[float] = None) -> Sequence:
+        params = params or SamplingParams()
+        rid = request_id if request_id is not None else f"req-{next(self._ids)}"
+        if not prompt_token_ids:
+            raise ValueError("empty prompt")
+        if len(prompt_token_ids) >= self.max_model_len:
+            raise ValueError(f"prompt of {len(prompt_token_ids)} tokens exceeds max_model_len "
+                             f"{self.max_model_len}")
+        if max(prompt_token_ids) >= self.mcfg.vocab_size or min(prompt_token_ids) < 0:
+            raise ValueError("prompt token id out of vocabulary range")
+        seq = Sequence(rid, prompt_token_ids, params, arrival_time, self.max_model_len)
+        self.seqs[rid] = seq
+        self.scheduler.add(seq)
+        self.metrics.on_arrival()
+        return seq
+
+    def abort(self, request_id: str) -> None:
+        s = self.scheduler.abort(request_id)
+        self.seqs.pop(request_id, None)
+        if s is not None:
+            self.metrics.on_finish(s)
+
+    def has_unfinished(self) -> bool:
+        return self.scheduler.has_work()
+
+    # ------------------------------------------------------------------ step
+    def step(self) -> list[RequestOutput]:
+        batch = self.scheduler.schedule()
+        if batch.is_empty:
+            return []
+        t0 = time.monotonic()
+        plan, samplers = self.executor.runner.build_plan(batch.prefills, batch.decodes, self.bm.table)
+        tokens = self.executor.execute(plan)
+        now = time.monotonic()
+        # advance computed counters
+        for seq, n in batch.prefills:
+            seq.num_computed += n
+        for seq in batch.decodes:
+            seq.num_computed += 1
+        outs: list[RequestOutput] = []
+        for seq, tok in zip(samplers, tokens):
+            seq.output_token_ids.append(tok)
+            if seq.first_token_time is None:
+                seq.first_token_time = now
+            seq.last_token_time = now
+            reason = self._check_stop(seq, tok)
+            if reason is not None:
+                seq.finish_time = now
+                self.scheduler.finish(seq, reason)
+                self.seqs.pop(seq.request_id, None)
+                self.metrics.on_finish(seq)
+            outs.append(RequestOutput(seq.request_id, seq.prompt_token_ids, [tok],
+                                      seq.output_token_ids, reason is not None, reason,
+                                      seq.arrival_time, seq.first_token_time, seq.finish_time,
+                                      seq.num_preemptions))
+        self.metrics.on_step(plan, now - t0, len(samplers), self.bm.usage(),
+                             len(self.scheduler.running), len(self.scheduler.waiting),
+                             len(batch.preempted))
+        return outs
+
+    def _check_stop(self, seq: Sequence, tok: int) -> Optional[str]:
+        p = seq.params
+        n = len(seq.output_token_ids)
+        if n >= seq.max_tokens:
+            return "length"
+        if seq.num_tokens >= self.max_model_len:
+            return "length"
+        if n < p.min_tokens:
+            return None
+        if not p.ignore_eos and tok == self.eos:
+            return "stop"
+        if tok in p.stop_token_ids:
+            return "stop"
+        return None
+
+    def shutdown(self) -> None:
+        self.executor.shutdown()
+
+
+class LLM:
+    """Offline batch generation (token ids in, token ids out; a tokenizer is used
+    when one is available locally)."""
+
+    def __init__(self, model: str = "llama-3-8b", **kw):
+        self.engine = LLMEngine(EngineConfig(model=model, **kw))
+        from ..utils.tokenizer import get_tokenizer
+        self.tokenizer = get_tokenizer(model, self.engine.mcfg)
+
+    def generate(self, prompts: Iterable[Union[str, list[int]]],
+                 params: Union[SamplingParams, list[SamplingParams], None] = None
+                 ) -> list[RequestOutput]:
+        prompts = list(prompts)
+        if not isinstance(params, list):
+            params = [params or SamplingParams()] * len(prompts)
+        ids = []
+        for i, (p, sp) in enumerate(zip(prompts, params)):
+            toks = self.tokenizer.encode(p) if isinstance(p, str) else p
+            self.engine.add_request(toks, sp, request_id=str(i))
+            ids.append(str(i))
+        final: dict[str, RequestOutput] = {}
+        while self.engine.has_unfinished():
+            for o in self.engine.step():
+                if o.finished:
+                    final[o.request_id] = o
+        return [final[i] for i in ids]
+
+    def shutdown(self):
+        self.engine.shutdown()

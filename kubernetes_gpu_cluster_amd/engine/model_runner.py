@@ -1,0 +1,377 @@
+"""Model runner: step packing, KV-cache sizing, hipGraph-captured decode, sampling.
+
+A step is described by a ``StepPlan``: a small header of counts plus three host
+blobs (int64 / int32 / fp32) at fixed offsets.  The driver builds it from the
+scheduler's batch; TP/PP workers receive only the plan (never Sequence objects).
+Each rank copies the blobs to static device buffers (3 H2D copies per step) and
+runs the forward; views into those static buffers are what the captured decode
+graphs read, so a graph replay needs no extra copies.
+
+Decode graphs are captured per batch bucket (1, 2, 4, 8, 16, 24, 32, ..., max);
+a pure-decode step pads to the next bucket (slot -1 = no KV write, ctx_len 0 =
+zero output).  Mixed / prefill steps run eagerly.  Sampling uses the counter-
+based HIP sampler, so every TP rank samples identical tokens from identical
+(all-gathered) logits without a broadcast.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.attention import AttnMetadata, ForwardContext
+from ..models.configs import ModelConfig
+from ..ops import reference as ref
+from ..parallel import comm
+from ..parallel.state import get_state
+from .sequence import Sequence
+
+
+def graph_buckets(max_bs: int) -> list[int]:
+    b = [1, 2, 4, 8, 16, 24, 32]
+    b += list(range(48, max_bs + 1, 16))
+    return sorted({x for x in b if x <= max_bs} | {max_bs})
+
+
+@dataclasses.dataclass
+class StepPlan:
+    T: int                 # tokens
+    Tp: int                # prefill tokens (first Tp of T)
+    P: int                 # prefill sequences
+    D: int                 # decode sequences
+    S: int                 # sampled rows
+    W: int                 # prefill attention work items
+    B: int                 # graph bucket (0 = eager)
+    max_ctx: int           # longest decode context
+    i64: np.ndarray
+    i32: np.ndarray
+    f32: np.ndarray
+
+    def header(self) -> list[int]:
+        return [self.T, self.Tp, self.P, self.D, self.S, self.W, self.B, self.max_ctx]
+
+
+class Layout:
+    """Fixed offsets of the step blobs."""
+
+    def __init__(self, max_tokens: int, max_seqs: int, max_blocks: int, block_m: int):
+        self.Tmax, self.Smax, self.mb = max_tokens, max_seqs, max_blocks
+        self.Wmax = max_tokens // block_m + max_seqs + 1
+        o = 0
+        self.ids, o = o, o + self.Tmax
+        self.pos, o = o, o + self.Tmax
+        self.slots, o = o, o + self.Tmax
+        self.seeds, o = o, o + self.Smax
+        self.lidx, o = o, o + self.Smax
+        self.n64 = o
+        o = 0
+        self.dbt, o = o, o + self.Smax * max_blocks
+        self.ctx, o = o, o + self.Smax
+        self.pbt, o = o, o + self.Smax * max_blocks
+        self.qsl, o = o, o + self.Smax + 1
+        self.sl, o = o, o + self.Smax
+        self.ws, o = o, o + self.Wmax
+        self.wm, o = o, o + self.Wmax
+        self.topk, o = o, o + self.Smax
+        self.n32 = o
+        self.temp, self.topp = 0, self.Smax
+        self.nf = 2 * self.Smax
+
+
+class ModelRunner:
+    def __init__(self, model, mcfg: ModelConfig, dtype: torch.dtype, device: torch.device,
+                 block_size: int, max_model_len: int, max_num_seqs: int, token_budget: int,
+                 enforce_eager: bool = False, graph_max_bs: int = 256):
+        self.model, self.mcfg, self.dtype, self.device = model, mcfg, dtype, device
+        self.bs = block_size
+        self.max_model_len = max_model_len
+        self.max_blocks = math.ceil(max_model_len / block_size)
+        self.max_num_seqs = max_num_seqs
+        self.token_budget = token_budget
+        self.is_gpu = device.type == "cuda"
+        self.use_graphs = self.is_gpu and not enforce_eager
+        self.graph_max_bs = min(graph_max_bs, max_num_seqs)
+        self.buckets = graph_buckets(self.graph_max_bs)
+        self.ps = get_state()
+        max_tokens = max(token_budget, max_num_seqs)
+        self.L = Layout(max_tokens, max_num_seqs, self.max_blocks, ops.PREFILL_BLOCK_M)
+        pin = self.is_gpu
+        self.h64 = torch.zeros(self.L.n64, dtype=torch.int64, pin_memory=pin)
+        self.h32 = torch.zeros(self.L.n32, dtype=torch.int32, pin_memory=pin)
+        self.hf = torch.zeros(self.L.nf, dtype=torch.float32, pin_memory=pin)
+        self.d64 = torch.zeros(self.L.n64, dtype=torch.int64, device=device)
+        self.d32 = torch.zeros(self.L.n32, dtype=torch.int32, device=device)
+        self.df = torch.zeros(self.L.nf, dtype=torch.float32, device=device)
+        rope_len = max(max_model_len, mcfg.max_position if mcfg.arch != "opt" else 1)
+        self.cos_sin = ref.rope_cos_sin_cache(mcfg.head_dim, rope_len + 1, mcfg.rope_theta,
+                                              mcfg.rope_scaling).to(device)
+        self.kv = None
+        self.kv_caches: list = []
+        self.workspace = None
+        self.graphs: dict[int, tuple] = {}
+        self.graph_pool = None
+        self.sample_out = torch.zeros(max_num_seqs, dtype=torch.int64, device=device)
+        self.stats = {"graph_steps": 0, "eager_steps": 0}
+
+    # ------------------------------------------------------------------ KV cache
+    def kv_bytes_per_block(self) -> int:
+        m = self.model
+        return (2 * m.num_local_layers * m.local_kv_heads() * self.mcfg.head_dim * self.bs *
+                torch.tensor([], dtype=self.dtype).element_size())
+
+    def profile_num_blocks(self, gpu_mem_util: float) -> int:
+        """Run a worst-case eager prefill, measure peak activation memory, and size the
+        KV pool to gpu_mem_util of total device memory (vLLM semantics)."""
+        if not self.is_gpu:
+            return max(64, (4 * self.max_num_seqs * self.max_blocks) // 4)
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats()
+        base = torch.cuda.memory_allocated()
+        self.init_kv_cache(16)
+        seqs = []
+        remaining = self.token_budget
+        while remaining > 0:
+            q = min(remaining, self.max_model_len)
+            seqs.append(q)
+            remaining -= q
+        self._dummy_prefill(seqs)
+        torch.cuda.synchronize()
+        peak = torch.cuda.max_memory_allocated() - base
+        self.kv = None
+        self.kv_caches = []
+        torch.cuda.empty_cache()
+        free, total = torch.cuda.mem_get_info()
+        used_now = total - free
+        reserve_graphs = 2 << 30 if self.use_graphs else 0
+        budget = total * gpu_mem_util - used_now - peak - reserve_graphs
+        nb = int(budget // self.kv_bytes_per_block())
+        return max(nb, 2)
+
+    def init_kv_cache(self, num_blocks: int) -> None:
+        m = self.model
+        L, nkv, d = m.num_local_layers, m.local_kv_heads(), self.mcfg.head_dim
+        # zero-init: stale slots of partially filled blocks must hold finite values
+        self.kv = torch.zeros(L, 2, num_blocks, nkv, self.bs, d, dtype=self.dtype,
+                              device=self.device)
+        self.kv_caches = [(self.kv[l, 0], self.kv[l, 1].view(num_blocks, nkv, d, self.bs))
+                          for l in range(L)]
+        self.num_blocks = num_blocks
+        nq = m.layers[0].self_attn.nq if hasattr(m.layers[0], "self_attn") else m.layers[0].qkv_proj.nq
+        if self.is_gpu:
+            self.workspace = ops.decode_partials(self.max_num_seqs, nq, d, self.max_blocks, self.bs,
+                                                 self.device)
+
+    def _dummy_prefill(self, qlens: list[int]) -> None:
+        """A prefill forward with slot -1 (no KV writes) over dummy block tables."""
+        T = sum(qlens)
+        P = len(qlens)
+        L = self.L
+        i64 = self.h64.numpy()
+        i32 = self.h32.numpy()
+        i64[L.ids:L.ids + T] = 0
+        i64[L.pos:L.pos + T] = np.concatenate([np.arange(q) for q in qlens])
+        i64[L.slots:L.slots + T] = -1
+        i32[L.pbt:L.pbt + P * self.max_blocks] = 0
+        qsl = np.concatenate([[0], np.cumsum(qlens)])
+        i32[L.qsl:L.qsl + P + 1] = qsl
+        i32[L.sl:L.sl + P] = qlens
+        ws, wm = ops.prefill_work_list(qlens, qlens)
+        i32[L.ws:L.ws + len(ws)] = ws
+        i32[L.wm:L.wm + len(wm)] = wm
+        i64[L.lidx:L.lidx + P] = qsl[1:] - 1
+        self.hf.numpy()[: 2 * self.L.Smax] = 1.0
+        plan = StepPlan(T, T, P, 0, P, len(ws), 0, 0, i64, i32, self.hf.numpy())
+        self.run(plan)
+
+    # ------------------------------------------------------------------ packing (driver)
+    def build_plan(self, prefills: list[tuple[Sequence, int]], decodes: list[Sequence],
+                   table: np.ndarray) -> tuple[StepPlan, list[Sequence]]:
+        """Pack a scheduled batch.  Returns the plan and the sequences that sample
+        (in sampled-row order)."""
+        L, bs, mb = self.L, self.bs, self.max_blocks
+        i64, i32, f32 = self.h64.numpy(), self.h32.numpy(), self.hf.numpy()
+        P, D = len(prefills), len(decodes)
+        samplers: list[Sequence] = []
+        lidx: list[int] = []
+        # ---- prefill chunks
+        off = 0
+        qlens, slens = [], []
+        for i, (seq, n) in enumerate(prefills):
+            a = seq.num_computed
+            pos = np.arange(a, a + n, dtype=np.int64)
+            i64[L.ids + off:L.ids + off + n] = seq.tokens_slice(a, a + n)
+            i64[L.pos + off:L.pos + off + n] = pos
+            row = table[seq.slot]
+            i64[L.slots + off:L.slots + off + n] = row[pos // bs].astype(np.int64) * bs + pos % bs
+            i32[L.pbt + i * mb:L.pbt + (i + 1) * mb] = row
+            qlens.append(n)
+            slens.append(a + n)
+            off += n
+            if a + n == seq.num_tokens:
+                samplers.append(seq)
+                lidx.append(off - 1)
+        Tp = off
+        W = 0
+        if P:
+            i32[L.qsl:L.qsl + P + 1] = np.concatenate([[0], np.cumsum(qlens)])
+            i32[L.sl:L.sl + P] = slens
+            ws, wm = ops.prefill_work_list(qlens, slens)
+            W = len(ws)
+            i32[L.ws:L.ws + W] = ws
+            i32[L.wm:L.wm + W] = wm
+        # ---- decodes (vectorised)
+        max_ctx = 0
+        B = 0
+        if D:
+            slots = np.fromiter((s.slot for s in decodes), dtype=np.int64, count=D)
+            pos = np.fromiter((s.num_computed for s in decodes), dtype=np.int64, count=D)
+            toks = [s.output_token_ids[-1] if s.output_token_ids else s.prompt_token_ids[-1]
+                    for s in decodes]
+            if self.use_graphs and P == 0 and D <= self.graph_max_bs:
+                B = next(b for b in self.buckets if b >= D)
+            n = max(D, B)
+            i64[L.ids + Tp:L.ids + Tp + D] = toks
+            i64[L.pos + Tp:L.pos + Tp + D] = pos
+            i64[L.slots + Tp:L.slots + Tp + D] = table[slots, pos // bs].astype(np.int64) * bs + pos % bs
+            dbt = i32[L.dbt:L.dbt + n * mb].reshape(n, mb)
+            dbt[:D] = table[slots]
+            i32[L.ctx:L.ctx + D] = pos + 1
+            if n > D:   # graph padding rows
+                i64[L.ids + Tp + D:L.ids + Tp + n] = 0
+                i64[L.pos + Tp + D:L.pos + Tp + n] = 0
+                i64[L.slots + Tp + D:L.slots + Tp + n] = -1
+                dbt[D:] = 0
+                i32[L.ctx + D:L.ctx + n] = 0
+            max_ctx = int(pos.max()) + 1
+            samplers.extend(decodes)
+            lidx.extend(range(Tp, Tp + D))
+        S = len(samplers)
+        T = Tp + D
+        # ---- sampling params
+        for j, s in enumerate(samplers):
+            p = s.params
+            f32[L.temp + j] = p.temperature
+            f32[L.topp + j] = p.top_p
+            i32[L.topk + j] = p.top_k
+            i64[L.seeds + j] = (s.seed & 0xFFFFFFFF) | (len(s.output_token_ids) << 32)
+        i64[L.lidx:L.lidx + S] = lidx
+        if B:
+            i64[L.lidx:L.lidx + B] = np.arange(B)   # graph rows index their own hidden row
+        return StepPlan(T, Tp, P, D, S, W, B, max_ctx, i64, i32, f32), samplers
+
+    # ------------------------------------------------------------------ execution (all ranks)
+    def _upload(self, plan: StepPlan) -> None:
+        if self.is_gpu:
+            self.d64.copy_(self.h64, non_blocking=True)
+            self.d32.copy_(self.h32, non_blocking=True)
+            self.df.copy_(self.hf, non_blocking=True)
+        else:
+            self.d64.copy_(torch.from_numpy(plan.i64))
+            self.d32.copy_(torch.from_numpy(plan.i32))
+            self.df.copy_(torch.from_numpy(plan.f32))
+
+    def _meta(self, T, Tp, P, D, W, max_ctx, z=None) -> AttnMetadata:
+        L, mb = self.L, self.max_blocks
+        d32 = self.d32
+        m = AttnMetadata(slot_mapping=self.d64[L.slots:L.slots + T], num_prefill_tokens=Tp,
+                         num_prefills=P, num_decodes=D)
+        if P:
+            m.prefill_block_tables = d32[L.pbt:L.pbt + P * mb].view(P, mb)
+            m.query_start_loc = d32[L.qsl:L.qsl + P + 1]
+            m.prefill_seq_lens = d32[L.sl:L.sl + P]
+            m.work_seq = d32[L.ws:L.ws + W]
+            m.work_mblk = d32[L.wm:L.wm + W]
+        if D:
+            m.decode_block_tables = d32[L.dbt:L.dbt + D * mb].view(D, mb)
+            m.decode_ctx_lens = d32[L.ctx:L.ctx + D]
+            m.decode_workspace = self.workspace
+            nkv = self.model.local_kv_heads()
+            m.decode_grid_z = z if z is not None else ops.decode_grid_z(D, nkv, max_ctx)
+        return m
+
+    def _forward(self, T, meta: AttnMetadata, hidden_in=None):
+        L = self.L
+        ctx = ForwardContext(meta, self.kv_caches, self.cos_sin)
+        ids = self.d64[L.ids:L.ids + T]
+        pos = self.d64[L.pos:L.pos + T]
+        if self.model.first:
+            return self.model(ids, pos, ctx)
+        h, r = hidden_in
+        return self.model(None, pos, ctx, hidden=h, residual=r)
+
+    @torch.inference_mode()
+    def run(self, plan: StepPlan) -> Optional[torch.Tensor]:
+        """Execute one step on this rank.  Returns sampled ids [S] (last PP stage)."""
+        self._upload(plan)
+        L = self.L
+        ps = self.ps
+        hidden_in = None
+        if not self.model.first:
+            shp = (plan.B or plan.T, self.mcfg.hidden_size)
+            hidden_in = comm.pp_recv([shp, shp], self.dtype, self.device)
+        if plan.B and plan.B in self.graphs and self.model.first and self.model.last:
+            g, logits = self.graphs[plan.B]
+            g.replay()
+            logits = logits[: plan.S]
+            self.stats["graph_steps"] += 1
+        else:
+            T = plan.T if not plan.B else plan.B
+            D = plan.D if not plan.B else plan.B
+            meta = self._meta(T, plan.Tp, plan.P, D, plan.W, plan.max_ctx)
+            out = self._forward(T, meta, hidden_in)
+            self.stats["eager_steps"] += 1
+            if not self.model.last:
+                comm.pp_send(list(out))
+                return None
+            idx = self.d64[L.lidx:L.lidx + plan.S]
+            logits = self.model.compute_logits(out.index_select(0, idx))
+        out = self.sample_out[: plan.S]
+        res = ops.sample(logits, self.df[L.temp:L.temp + plan.S], self.d32[L.topk:L.topk + plan.S],
+                         self.df[L.topp:L.topp + plan.S], self.d64[L.seeds:L.seeds + plan.S],
+                         out=out if self.is_gpu else None)
+        return res
+
+    # ------------------------------------------------------------------ hipGraph capture
+    @torch.inference_mode()
+    def capture_graphs(self) -> float:
+        """Capture decode forward + LM head for each batch bucket (largest first,
+        sharing one memory pool).  Returns seconds spent."""
+        self.buckets = graph_buckets(self.graph_max_bs)
+        if not self.use_graphs or not (self.model.first and self.model.last):
+            self.use_graphs = False
+            return 0.0
+        if self.ps.tp_size > 1 and comm.get_custom_allreduce() is None:
+            pass  # RCCL all-reduce is capturable on ROCm (torch registers the graph stream)
+        t0 = time.time()
+        L, mb = self.L, self.max_blocks
+        nkv = self.model.local_kv_heads()
+        # a valid idle decode state: ctx_len 0 rows (write zeros), slot -1
+        self.h64.zero_()
+        self.h32.zero_()
+        self.h64[L.slots:L.slots + self.graph_max_bs] = -1
+        self.h64[L.lidx:L.lidx + self.graph_max_bs] = torch.arange(self.graph_max_bs)
+        self.d64.copy_(self.h64)
+        self.d32.copy_(self.h32)
+        torch.cuda.synchronize()
+        self.graph_pool = torch.cuda.graph_pool_handle()
+        for B in sorted(self.buckets, reverse=True):
+            z = ops.decode_grid_z(B, nkv, self.max_model_len)
+            meta = self._meta(B, 0, 0, B, 0, self.max_model_len, z=z)
+            idx = self.d64[L.lidx:L.lidx + B]
+            for _ in range(2):   # warm up (allocator, library handles) outside capture
+                h = self._forward(B, meta)
+                self.model.compute_logits(h.index_select(0, idx))
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self.graph_pool):
+                h = self._forward(B, meta)
+                logits = self.model.compute_logits(h.index_select(0, idx))
+            self.graphs[B] = (g, logits)
+        torch.cuda.synchronize()
+        return time.time() - t0

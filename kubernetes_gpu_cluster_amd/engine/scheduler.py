@@ -1,0 +1,132 @@
+"""Continuous-batching scheduler with chunked prefill and recompute preemption.
+
+Each step has a token budget (``max_num_batched_tokens``) and a sequence cap
+(``max_num_seqs``).  Policy (decode-first, as in vLLM's V1 scheduler):
+
+1. Running sequences, FCFS: a decoding sequence takes 1 token; a sequence still in
+   (chunked) prefill takes min(remaining, budget).  If the KV pool cannot grow,
+   the newest running sequence is preempted (blocks freed, re-queued at the front
+   of the waiting queue, recomputed later) until the allocation fits.
+2. If nothing was preempted, waiting sequences are admitted FCFS while budget,
+   the sequence cap and free blocks (with a small watermark) allow.
+
+A scheduled unit is (sequence, n_tokens): tokens [num_computed, num_computed+n)
+are run; if that reaches the end of the sequence, a new token is sampled.
+"""
+from __future__ import annotations
+
+import collections
+import dataclasses
+from typing import Optional
+
+from .block_manager import BlockManager
+from .sequence import SeqStatus, Sequence
+
+
+@dataclasses.dataclass
+class ScheduledBatch:
+    prefills: list[tuple[Sequence, int]]      # (seq, n_tokens), n may be 1 for 1-token prompts
+    decodes: list[Sequence]                   # one token each
+    preempted: list[Sequence]
+
+    @property
+    def num_tokens(self) -> int:
+        return sum(n for _, n in self.prefills) + len(self.decodes)
+
+    @property
+    def is_empty(self) -> bool:
+        return not self.prefills and not self.decodes
+
+    def all_seqs(self) -> list[tuple[Sequence, int]]:
+        return self.prefills + [(s, 1) for s in self.decodes]
+
+
+class Scheduler:
+    def __init__(self, block_manager: BlockManager, max_num_seqs: int, token_budget: int,
+                 max_model_len: int, chunked_prefill: bool = True):
+        self.bm = block_manager
+        self.max_num_seqs = max_num_seqs
+        self.token_budget = token_budget
+        self.max_model_len = max_model_len
+        self.chunked = chunked_prefill
+        self.waiting: collections.deque[Sequence] = collections.deque()
+        self.running: list[Sequence] = []
+        self.num_preemptions = 0
+
+    def add(self, seq: Sequence) -> None:
+        self.waiting.append(seq)
+
+    def abort(self, request_id: str) -> Optional[Sequence]:
+        for q in (self.running, self.waiting):
+            for s in list(q):
+                if s.request_id == request_id:
+                    q.remove(s)
+                    self.bm.free_seq(s)
+                    s.status = SeqStatus.FINISHED
+                    s.finish_reason = "abort"
+                    return s
+        return None
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.running)
+
+    def _preempt(self, seq: Sequence) -> None:
+        self.bm.free_seq(seq)
+        seq.num_computed = 0
+        seq.status = SeqStatus.WAITING
+        seq.num_preemptions += 1
+        self.num_preemptions += 1
+        self.waiting.appendleft(seq)
+
+    def schedule(self) -> ScheduledBatch:
+        budget = self.token_budget
+        prefills: list[tuple[Sequence, int]] = []
+        decodes: list[Sequence] = []
+        preempted: list[Sequence] = []
+        i = 0
+        while i < len(self.running) and budget > 0:
+            seq = self.running[i]
+            remaining = seq.num_tokens - seq.num_computed
+            n = 1 if remaining == 1 else min(remaining, budget)
+            scheduled = True
+            while not self.bm.can_allocate(seq, seq.num_computed + n):
+                victim = self.running.pop()
+                self._preempt(victim)
+                preempted.append(victim)
+                if victim is seq:
+                    scheduled = False
+                    break
+            if not scheduled:
+                break
+            self.bm.allocate(seq, seq.num_computed + n)
+            if n == 1 and remaining == 1:
+                decodes.append(seq)
+            else:
+                prefills.append((seq, n))
+            budget -= n
+            i += 1
+        if not preempted:
+            while self.waiting and budget > 0 and len(self.running) < self.max_num_seqs:
+                seq = self.waiting[0]
+                remaining = seq.num_tokens - seq.num_computed
+                n = min(remaining, budget)
+                if n < remaining and not self.chunked:
+                    break
+                if not self.bm.can_allocate(seq, seq.num_computed + n, watermark=True):
+                    break
+                self.waiting.popleft()
+                self.bm.allocate(seq, seq.num_computed + n)
+                seq.status = SeqStatus.RUNNING
+                self.running.append(seq)
+                prefills.append((seq, n))
+                budget -= n
+        return ScheduledBatch(prefills, decodes, preempted)
+
+    def finish(self, seq: Sequence, reason: str) -> None:
+        seq.status = SeqStatus.FINISHED
+        seq.finish_reason = reason
+        self.bm.free_seq(seq)
+        try:
+            self.running.remove(seq)
+        except ValueError:
+            pass

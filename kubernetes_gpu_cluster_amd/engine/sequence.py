@@ -1,0 +1,121 @@
+"""Request / sequence state and sampling parameters (OpenAI semantics)."""
+from __future__ import annotations
+
+import dataclasses
+import enum
+import itertools
+import time
+from typing import Optional
+
+_seq_ids = itertools.count()
+
+
+@dataclasses.dataclass
+class SamplingParams:
+    temperature: float = 1.0
+    top_p: float = 1.0
+    top_k: int = -1
+    max_tokens: Optional[int] = 16
+    min_tokens: int = 0
+    stop_token_ids: list[int] = dataclasses.field(default_factory=list)
+    stop: list[str] = dataclasses.field(default_factory=list)
+    ignore_eos: bool = False
+    seed: Optional[int] = None
+    n: int = 1
+    logprobs: Optional[int] = None
+
+    def __post_init__(self):
+        if self.temperature < 0:
+            raise ValueError("temperature must be >= 0")
+        if not 0 < self.top_p <= 1:
+            raise ValueError("top_p must be in (0, 1]")
+        if self.top_k == 0 or self.top_k < -1:
+            raise ValueError("top_k must be -1 (disabled) or >= 1")
+        if self.max_tokens is not None and self.max_tokens < 1:
+            raise ValueError("max_tokens must be >= 1")
+        if self.n != 1:
+            raise ValueError("only n=1 is supported")
+
+
+class SeqStatus(enum.Enum):
+    WAITING = 0
+    RUNNING = 1
+    FINISHED = 2
+
+
+class Sequence:
+    __slots__ = ("seq_id", "request_id", "prompt_token_ids", "output_token_ids", "params",
+                 "status", "block_ids", "num_computed", "arrival_time", "first_token_time",
+                 "finish_time", "finish_reason", "seed", "num_preemptions", "max_tokens",
+                 "slot", "last_token_time", "token_times", "prompt_text", "stream")
+
+    def __init__(self, request_id: str, prompt_token_ids: list[int], params: SamplingParams,
+                 arrival_time: Optional[float] = None, max_model_len: int = 1 << 30):
+        self.seq_id = next(_seq_ids)
+        self.request_id = request_id
+        self.prompt_token_ids = list(prompt_token_ids)
+        self.output_token_ids: list[int] = []
+        self.params = params
+        self.status = SeqStatus.WAITING
+        self.block_ids: list[int] = []
+        self.num_computed = 0                 # tokens whose KV is in the cache
+        self.arrival_time = time.monotonic() if arrival_time is None else arrival_time
+        self.first_token_time: Optional[float] = None
+        self.last_token_time: Optional[float] = None
+        self.finish_time: Optional[float] = None
+        self.finish_reason: Optional[str] = None
+        self.seed = params.seed if params.seed is not None else (self.seq_id * 0x9E3779B1) & 0x7FFFFFFF
+        self.num_preemptions = 0
+        room = max_model_len - len(self.prompt_token_ids)
+        self.max_tokens = room if params.max_tokens is None else min(params.max_tokens, room)
+        self.slot = -1
+        self.token_times: list[float] = []
+        self.prompt_text: Optional[str] = None
+        self.stream = None
+
+    @property
+    def num_tokens(self) -> int:
+        return len(self.prompt_token_ids) + len(self.output_token_ids)
+
+    @property
+    def num_prompt(self) -> int:
+        return len(self.prompt_token_ids)
+
+    def token_at(self, i: int) -> int:
+        n = len(self.prompt_token_ids)
+        return self.prompt_token_ids[i] if i < n else self.output_token_ids[i - n]
+
+    def tokens_slice(self, a: int, b: int) -> list[int]:
+        n = len(self.prompt_token_ids)
+        if b <= n:
+            return self.prompt_token_ids[a:b]
+        if a >= n:
+            return self.output_token_ids[a - n:b - n]
+        return self.prompt_token_ids[a:] + self.output_token_ids[: b - n]
+
+    @property
+    def is_prefilling(self) -> bool:
+        return self.num_computed < self.num_tokens - 1 or (
+            self.num_computed < self.num_prompt)
+
+    @property
+    def finished(self) -> bool:
+        return self.status == SeqStatus.FINISHED
+
+
+@dataclasses.dataclass
+class RequestOutput:
+    request_id: str
+    prompt_token_ids: list[int]
+    new_token_ids: list[int]
+    output_token_ids: list[int]
+    finished: bool
+    finish_reason: Optional[str] = None
+    arrival_time: float = 0.0
+    first_token_time: Optional[float] = None
+    finish_time: Optional[float] = None
+    num_preemptions: int = 0
+
+    @property
+    def ttft(self) -> Optional[float]:
+        return None if self.first_token_time is None else self.first_token_time - self.arrival_time

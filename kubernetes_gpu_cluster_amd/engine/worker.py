@@ -1,0 +1,260 @@
+"""Workers and executors: one process per GPU, TP x PP inside a pod.
+
+The reference scales a model over GPUs by handing vLLM ``--tensor-parallel-size``
+/ ``--pipeline-parallel-size`` (and a Ray head for multi-pod PP:
+``values-01-minimal-example4.yaml:17-18,42-46``).  Here the driver process (rank 0)
+owns the scheduler; every rank owns one GPU and a ``Worker`` (model shard +
+``ModelRunner``).  Control commands (profile, init cache, capture, shutdown) and
+per-step ``StepPlan`` blobs travel over a gloo CPU group; activations and TP
+collectives go over RCCL/xGMI.
+
+Executors:
+  * LocalExecutor      TP = PP = 1, in-process.
+  * MultiprocExecutor  spawns ranks 1..N-1 (``torch.multiprocessing``, spawn) for
+                       the API server / offline LLM.
+  * ExternalExecutor   ranks already launched by torchrun (bench.py --tp N):
+                       rank 0 drives, the others call ``worker_loop``.
+"""
+from __future__ import annotations
+
+import os
+import pickle
+import socket
+import traceback
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .. import ops
+from ..models import load_model, resolve_model
+from ..models.moe import set_moe_mode
+from ..parallel import comm
+from ..parallel.state import destroy_parallel, get_state, init_parallel
+from .config import EngineConfig
+from .model_runner import ModelRunner, StepPlan
+
+CMD_STEP, CMD_PROFILE, CMD_INIT_CACHE, CMD_CAPTURE, CMD_EXIT = 1, 2, 3, 4, 5
+
+
+def default_max_model_len(cfg: EngineConfig) -> int:
+    mcfg, _ = resolve_model(cfg.model)
+    return cfg.max_model_len or mcfg.max_position
+
+
+class Worker:
+    def __init__(self, cfg: EngineConfig, rank: int = 0, local_device: Optional[int] = None):
+        self.cfg = cfg
+        dev = cfg.resolved_device()
+        if dev.type == "cuda":
+            idx = local_device if local_device is not None else int(os.environ.get("LOCAL_RANK", rank))
+            idx = idx % max(1, torch.cuda.device_count())
+            dev = torch.device("cuda", idx)
+            torch.cuda.set_device(dev)
+            ops.load_extension(strict=True)
+        self.device = dev
+        self.rank = rank
+        set_moe_mode(cfg.moe_parallel)
+        init_parallel(cfg.tensor_parallel_size, cfg.pipeline_parallel_size, device=dev)
+        self.ps = get_state()
+        mcfg, _ = resolve_model(cfg.model)
+        self.dtype = cfg.torch_dtype(torch.bfloat16 if mcfg.arch != "opt" else torch.float16)
+        if dev.type == "cpu" and self.dtype == torch.float16:
+            self.dtype = torch.float32       # CPU oracle path
+        self.max_model_len = default_max_model_len(cfg)
+        torch.manual_seed(cfg.seed)
+        self.mcfg, self.model = load_model(cfg.model, self.dtype, dev, cfg.random_init,
+                                           seed=cfg.seed)
+        if self.ps.tp_size > 1 and dev.type == "cuda" and not cfg.disable_custom_all_reduce:
+            from ..parallel.custom_allreduce import maybe_init_custom_allreduce
+            comm.set_custom_allreduce(maybe_init_custom_allreduce(self.ps, dev))
+        self.runner = ModelRunner(self.model, self.mcfg, self.dtype, dev, cfg.block_size,
+                                  self.max_model_len, cfg.max_num_seqs, cfg.token_budget(),
+                                  cfg.enforce_eager, cfg.cuda_graph_max_bs)
+
+    def profile(self) -> int:
+        if self.cfg.num_gpu_blocks_override:
+            return self.cfg.num_gpu_blocks_override
+        return self.runner.profile_num_blocks(self.cfg.gpu_memory_utilization)
+
+    def init_cache(self, nb: int) -> None:
+        self.runner.init_kv_cache(nb)
+
+    def capture(self) -> float:
+        return self.runner.capture_graphs()
+
+    def run(self, plan: StepPlan):
+        return self.runner.run(plan)
+
+
+# ---------------------------------------------------------------------- plan transport
+def _bcast_cmd(cmd: int, arg: int = 0, header: Optional[list[int]] = None) -> list[int]:
+    s = get_state()
+    h = torch.zeros(10, dtype=torch.int64)
+    if s.rank == 0:
+        h[0], h[1] = cmd, arg
+        if header:
+            h[2:2 + len(header)] = torch.tensor(header)
+    dist.broadcast(h, src=getattr(s, "global_base", 0), group=s.cpu_group)
+    return h.tolist()
+
+
+def _bcast_plan_blobs(runner: ModelRunner, plan_hdr: list[int]) -> None:
+    """Ship only the used prefixes of the blobs (the layout is fixed)."""
+    s = get_state()
+    src = getattr(s, "global_base", 0)
+    for t in (runner.h64, runner.h32, runner.hf):
+        dist.broadcast(t, src=src, group=s.cpu_group)
+
+
+def _send_tokens_to_driver(tokens: torch.Tensor) -> None:
+    s = get_state()
+    dist.send(tokens.cpu(), dst=getattr(s, "global_base", 0), group=s.cpu_group)
+
+
+def worker_loop(worker: Worker) -> None:
+    """Non-driver ranks: execute commands until CMD_EXIT."""
+    s = get_state()
+    last_pp_leader = s.is_last_pp and s.tp_rank == 0 and s.rank != 0
+    while True:
+        h = _bcast_cmd(0)
+        cmd, arg = h[0], h[1]
+        if cmd == CMD_EXIT:
+            break
+        if cmd == CMD_PROFILE:
+            nb = worker.profile()
+            comm.all_reduce_min_scalar(nb)
+        elif cmd == CMD_INIT_CACHE:
+            worker.init_cache(arg)
+        elif cmd == CMD_CAPTURE:
+            worker.capture()
+        elif cmd == CMD_STEP:
+            hdr = h[2:10]
+            _bcast_plan_blobs(worker.runner, hdr)
+            r = worker.runner
+            plan = StepPlan(*hdr, r.h64.numpy(), r.h32.numpy(), r.hf.numpy())
+            out = worker.run(plan)
+            if last_pp_leader and out is not None:
+                _send_tokens_to_driver(out)
+
+
+class LocalExecutor:
+    def __init__(self, cfg: EngineConfig):
+        self.worker = Worker(cfg)
+
+    @property
+    def runner(self) -> ModelRunner:
+        return self.worker.runner
+
+    def profile(self) -> int:
+        return self.worker.profile()
+
+    def init_cache(self, nb: int) -> None:
+        self.worker.init_cache(nb)
+
+    def capture(self) -> float:
+        return self.worker.capture()
+
+    def execute(self, plan: StepPlan) -> list[int]:
+        out = self.worker.run(plan)
+        return out.tolist()
+
+    def shutdown(self) -> None:
+        pass
+
+
+class _DistExecutorBase:
+    """Rank 0 side of the command protocol (shared by spawned / torchrun ranks)."""
+    worker: Worker
+
+    @property
+    def runner(self) -> ModelRunner:
+        return self.worker.runner
+
+    def profile(self) -> int:
+        _bcast_cmd(CMD_PROFILE)
+        nb = self.worker.profile()
+        return comm.all_reduce_min_scalar(nb)
+
+    def init_cache(self, nb: int) -> None:
+        _bcast_cmd(CMD_INIT_CACHE, nb)
+        self.worker.init_cache(nb)
+
+    def capture(self) -> float:
+        _bcast_cmd(CMD_CAPTURE)
+        return self.worker.capture()
+
+    def execute(self, plan: StepPlan) -> list[int]:
+        _bcast_cmd(CMD_STEP, 0, plan.header())
+        _bcast_plan_blobs(self.worker.runner, plan.header())
+        out = self.worker.run(plan)
+        s = get_state()
+        if s.pp_size > 1:
+            t = torch.empty(plan.S, dtype=torch.int64)
+            src = getattr(s, "global_base", 0) + (s.pp_size - 1) * s.tp_size
+            dist.recv(t, src=src, group=s.cpu_group)
+            return t.tolist()
+        return out.tolist()
+
+    def shutdown(self) -> None:
+        try:
+            _bcast_cmd(CMD_EXIT)
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class ExternalExecutor(_DistExecutorBase):
+    """All ranks launched externally (torchrun); call on rank 0 only."""
+
+    def __init__(self, worker: Worker):
+        self.worker = worker
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn_entry(rank: int, cfg: EngineConfig, env: dict) -> None:
+    os.environ.update(env)
+    os.environ["RANK"] = str(rank)
+    os.environ["LOCAL_RANK"] = str(rank)
+    try:
+        w = Worker(cfg, rank=rank, local_device=rank)
+        worker_loop(w)
+    except Exception:
+        traceback.print_exc()
+        raise
+    finally:
+        destroy_parallel()
+
+
+class MultiprocExecutor(_DistExecutorBase):
+    def __init__(self, cfg: EngineConfig):
+        import torch.multiprocessing as mp
+        ws = cfg.world_size
+        env = {"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(_free_port()),
+               "WORLD_SIZE": str(ws)}
+        for k in ("HSA_ENABLE_IPC_MODE_LEGACY",):
+            if k in os.environ:
+                env[k] = os.environ[k]
+        ctx = mp.get_context("spawn")
+        self.procs = []
+        for r in range(1, ws):
+            p = ctx.Process(target=_spawn_entry, args=(r, cfg, env), daemon=True)
+            p.start()
+            self.procs.append(p)
+        os.environ.update(env)
+        os.environ["RANK"] = "0"
+        os.environ["LOCAL_RANK"] = "0"
+        self.worker = Worker(cfg, rank=0, local_device=0)
+
+    def shutdown(self) -> None:
+        super().shutdown()
+        for p in self.procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.terminate()
+        destroy_parallel()

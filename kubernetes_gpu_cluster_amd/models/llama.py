@@ -1,0 +1,234 @@
+"""Llama-family decoder: Llama-3 (8B/70B), Mistral, Qwen2/2.5, Qwen3 (q/k norm),
+Qwen v1 (fused c_attn, ``--trust-remote-code`` arch) and Mixtral (MoE).
+
+Per layer:
+  fused_add_rms_norm (K4) -> QKV GEMM -> rope_kv_write (K3/K5/K6) -> paged attention
+  (K1/K2) -> O GEMM (+TP all-reduce C1) -> fused_add_rms_norm -> gate_up GEMM ->
+  silu_mul (K7) -> down GEMM (+TP all-reduce C2)   |  MoE: router -> topk-softmax (K13)
+  -> grouped expert MLP (K14) (+ all-reduce / all-to-all)
+Pipeline stages own a contiguous slice of layers; the first stage owns the
+embedding, the last the final norm and the LM head.
+"""
+from __future__ import annotations
+
+import re
+from typing import Iterable, Optional
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from ..parallel import comm
+from ..parallel.layers import (MergedColumnParallelLinear, ParallelLMHead, QKVParallelLinear,
+                               ReplicatedLinear, RowParallelLinear, VocabParallelEmbedding)
+from ..parallel.state import get_state
+from .attention import ForwardContext, PagedAttention
+from .configs import ModelConfig
+from .moe import MoEBlock
+
+
+def pp_layer_range(num_layers: int, pp_size: int, pp_rank: int) -> tuple[int, int]:
+    per = num_layers // pp_size
+    extra = num_layers % pp_size
+    start = pp_rank * per + min(pp_rank, extra)
+    return start, start + per + (1 if pp_rank < extra else 0)
+
+
+class RMSNorm(nn.Module):
+    def __init__(self, n: int, eps: float, dtype, device):
+        super().__init__()
+        self.weight = nn.Parameter(torch.ones(n, dtype=dtype, device=device), requires_grad=False)
+        self.eps = eps
+
+    def forward(self, x, residual=None):
+        if residual is None:
+            return ops.rms_norm(x, self.weight, self.eps)
+        return ops.fused_add_rms_norm(x, residual, self.weight, self.eps)
+
+
+class LlamaAttention(nn.Module):
+    def __init__(self, cfg: ModelConfig, layer_idx: int, dtype, device):
+        super().__init__()
+        self.cfg = cfg
+        self.qkv_proj = QKVParallelLinear(cfg.hidden_size, cfg.head_dim, cfg.num_heads,
+                                          cfg.num_kv_heads, bias=cfg.qkv_bias, dtype=dtype,
+                                          device=device)
+        self.nq, self.nkv = self.qkv_proj.nq, self.qkv_proj.nkv
+        self.o_proj = RowParallelLinear(cfg.num_heads * cfg.head_dim, cfg.hidden_size,
+                                        bias=cfg.o_bias, dtype=dtype, device=device)
+        if cfg.qk_norm:
+            self.q_norm = RMSNorm(cfg.head_dim, cfg.rms_eps, dtype, device)
+            self.k_norm = RMSNorm(cfg.head_dim, cfg.rms_eps, dtype, device)
+        else:
+            self.q_norm = self.k_norm = None
+        self.attn = PagedAttention(self.nq, self.nkv, cfg.head_dim, layer_idx)
+
+    def forward(self, positions, x, ctx: ForwardContext):
+        qkv = self.qkv_proj(x)
+        kc, vc = ctx.kv_caches[self.attn.layer_idx]
+        q = ops.rope_kv_write(qkv, positions, ctx.cos_sin, kc, vc, ctx.attn.slot_mapping,
+                              self.nq, self.nkv, self.cfg.head_dim,
+                              None if self.q_norm is None else self.q_norm.weight,
+                              None if self.k_norm is None else self.k_norm.weight,
+                              self.cfg.rms_eps)
+        return self.o_proj(self.attn(q, ctx))
+
+
+class LlamaMLP(nn.Module):
+    def __init__(self, cfg: ModelConfig, dtype, device):
+        super().__init__()
+        self.gate_up_proj = MergedColumnParallelLinear(cfg.hidden_size, [cfg.intermediate_size] * 2,
+                                                       dtype=dtype, device=device)
+        self.down_proj = RowParallelLinear(cfg.intermediate_size, cfg.hidden_size, dtype=dtype,
+                                           device=device)
+
+    def forward(self, x):
+        return self.down_proj(ops.silu_mul(self.gate_up_proj(x)))
+
+
+class LlamaDecoderLayer(nn.Module):
+    def __init__(self, cfg: ModelConfig, layer_idx: int, dtype, device):
+        super().__init__()
+        self.self_attn = LlamaAttention(cfg, layer_idx, dtype, device)
+        self.mlp = MoEBlock(cfg, dtype, device) if cfg.is_moe else LlamaMLP(cfg, dtype, device)
+        self.input_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_eps, dtype, device)
+        self.post_attention_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_eps, dtype, device)
+
+    def forward(self, positions, x, residual, ctx):
+        if residual is None:
+            residual = x
+            x = self.input_layernorm(x)
+        else:
+            x, residual = self.input_layernorm(x, residual)
+        x = self.self_attn(positions, x, ctx)
+        x, residual = self.post_attention_layernorm(x, residual)
+        return self.mlp(x), residual
+
+
+class LlamaForCausalLM(nn.Module):
+    def __init__(self, cfg: ModelConfig, dtype=torch.bfloat16, device=None):
+        super().__init__()
+        self.cfg = cfg
+        self.dtype = dtype
+        s = get_state()
+        self.start, self.end = pp_layer_range(cfg.num_layers, s.pp_size, s.pp_rank)
+        self.first, self.last = s.is_first_pp, s.is_last_pp
+        self.embed_tokens = (VocabParallelEmbedding(cfg.vocab_size, cfg.hidden_size, dtype, device)
+                             if self.first or (self.last and cfg.tie_embeddings) else None)
+        self.layers = nn.ModuleList([LlamaDecoderLayer(cfg, i - self.start, dtype, device)
+                                     for i in range(self.start, self.end)])
+        if self.last:
+            self.norm = RMSNorm(cfg.hidden_size, cfg.rms_eps, dtype, device)
+            tied = self.embed_tokens if cfg.tie_embeddings else None
+            self.lm_head = ParallelLMHead(cfg.vocab_size, cfg.hidden_size, dtype, device, tied)
+        else:
+            self.norm = self.lm_head = None
+
+    @property
+    def num_local_layers(self) -> int:
+        return self.end - self.start
+
+    def local_kv_heads(self) -> int:
+        return self.layers[0].self_attn.nkv if len(self.layers) else 0
+
+    def forward(self, input_ids: Optional[torch.Tensor], positions: torch.Tensor,
+                ctx: ForwardContext, hidden: Optional[torch.Tensor] = None,
+                residual: Optional[torch.Tensor] = None):
+        """First stage: input_ids -> ...; later stages take (hidden, residual) from the
+        previous stage.  Returns the final-normed hidden on the last stage, else
+        (hidden, residual) for the next stage."""
+        x = self.embed_tokens(input_ids) if self.first else hidden
+        for layer in self.layers:
+            x, residual = layer(positions, x, residual, ctx)
+        if not self.last:
+            return x, residual
+        if residual is None:
+            return self.norm(x)
+        x, _ = self.norm(x, residual)
+        return x
+
+    def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
+        return self.lm_head(hidden)
+
+    # ------------------------------------------------------------------ weights
+    def _hf_map(self, name: str):
+        """HF checkpoint name -> (local param, shard_id) or None if not on this rank."""
+        cfg = self.cfg
+        if cfg.arch == "qwen":
+            name = (name.replace("transformer.wte.", "model.embed_tokens.")
+                    .replace("transformer.ln_f.", "model.norm.")
+                    .replace("transformer.h.", "model.layers.")
+                    .replace(".ln_1.", ".input_layernorm.").replace(".ln_2.", ".post_attention_layernorm.")
+                    .replace(".attn.c_proj.", ".self_attn.o_proj.")
+                    .replace(".mlp.c_proj.", ".mlp.down_proj."))
+        m = re.match(r"model\.layers\.(\d+)\.(.*)", name)
+        if m is None:
+            if name.startswith("model.embed_tokens.") and self.embed_tokens is not None:
+                return self.embed_tokens.weight, None
+            if name.startswith("model.norm.") and self.norm is not None:
+                return self.norm.weight, None
+            if name.startswith("lm_head.") and self.lm_head is not None and self.lm_head.weight is not None:
+                return self.lm_head.weight, None
+            return None
+        li = int(m.group(1))
+        if not (self.start <= li < self.end):
+            return None
+        layer = self.layers[li - self.start]
+        rest = m.group(2)
+        sa = layer.self_attn
+        for sid in ("q", "k", "v"):
+            if rest.startswith(f"self_attn.{sid}_proj."):
+                p = sa.qkv_proj.weight if rest.endswith("weight") else sa.qkv_proj.bias
+                return p, sid
+        if rest.startswith("attn.c_attn."):      # qwen v1 fused qkv [3H, H]
+            return ("c_attn", sa.qkv_proj, rest.endswith("weight")), None
+        if rest.startswith("self_attn.o_proj."):
+            return (sa.o_proj.weight if rest.endswith("weight") else sa.o_proj.bias), None
+        if rest.startswith("self_attn.q_norm."):
+            return sa.q_norm.weight, None
+        if rest.startswith("self_attn.k_norm."):
+            return sa.k_norm.weight, None
+        if rest.startswith("input_layernorm."):
+            return layer.input_layernorm.weight, None
+        if rest.startswith("post_attention_layernorm."):
+            return layer.post_attention_layernorm.weight, None
+        mlp = layer.mlp
+        if cfg.arch == "qwen":
+            if rest.startswith("mlp.w2."):
+                return mlp.gate_up_proj.weight, 0
+            if rest.startswith("mlp.w1."):
+                return mlp.gate_up_proj.weight, 1
+        if rest.startswith("mlp.gate_proj."):
+            return mlp.gate_up_proj.weight, 0
+        if rest.startswith("mlp.up_proj."):
+            return mlp.gate_up_proj.weight, 1
+        if rest.startswith("mlp.down_proj."):
+            return mlp.down_proj.weight, None
+        if rest.startswith("block_sparse_moe."):
+            return mlp.map_weight(rest[len("block_sparse_moe."):])
+        return None
+
+    def load_weights(self, weights: Iterable[tuple[str, torch.Tensor]]) -> int:
+        n = 0
+        for name, w in weights:
+            tgt = self._hf_map(name)
+            if tgt is None:
+                continue
+            p, sid = tgt
+            if isinstance(p, tuple) and p[0] == "c_attn":
+                _, qkv, is_w = p
+                H = self.cfg.hidden_size
+                param = qkv.weight if is_w else qkv.bias
+                for i, s in enumerate(("q", "k", "v")):
+                    qkv._load(param, w.narrow(0, i * H, H), s)
+            elif isinstance(p, tuple) and p[0] == "moe":
+                p[1](w.to(self.dtype))
+            else:
+                loader = getattr(p, "weight_loader", None)
+                w = w.to(p.dtype)
+                if loader is None:
+                    p.data.copy_(w)
+                else:
+                    loader(p, w, sid) if sid is not None else loader(p, w)
+            n += 1
+        return n

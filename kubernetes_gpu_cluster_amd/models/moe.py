@@ -1,0 +1,143 @@
+"""Mixtral sparse-MoE block (K13 top-k softmax routing, K14 grouped expert MLP).
+
+Expert placement over the TP group (``--moe-parallel``):
+
+* ``tp`` (default): every rank holds all experts, each expert's intermediate dim
+  sharded like a dense MLP; the block ends with the TP all-reduce.
+* ``ep``: rank r owns experts [r*E/ep, (r+1)*E/ep) whole.  Tokens are dispatched
+  to the owning rank with an all-to-all (C7), processed by the local grouped
+  MLP, and the weighted results are returned with a second all-to-all.
+
+The grouped MLP sorts the (token, expert) pairs by expert and runs one GEMM pair
+per non-empty expert on contiguous row ranges (hipBLASLt), with the SiLU-mul
+(K7) in between and a weighted index_add combine.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from ..ops import reference as ref
+from ..parallel import comm
+from ..parallel.layers import ReplicatedLinear
+from ..parallel.state import get_state
+from .configs import ModelConfig
+
+MOE_MODE = {"mode": "tp"}
+
+
+def set_moe_mode(mode: str) -> None:
+    assert mode in ("tp", "ep")
+    MOE_MODE["mode"] = mode
+
+
+def grouped_expert_mlp(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor,
+                       topk_w: torch.Tensor, topk_ids: torch.Tensor,
+                       expert_offset: int = 0) -> torch.Tensor:
+    """x [T, H]; w13 [E_local, 2I, H]; w2 [E_local, H, I]; ids index global experts."""
+    T, H = x.shape
+    E = w13.shape[0]
+    k = topk_ids.shape[1]
+    flat = topk_ids.reshape(-1).long() - expert_offset
+    valid = (flat >= 0) & (flat < E)
+    order = torch.argsort(torch.where(valid, flat, E), stable=True)
+    counts = torch.bincount(flat[valid], minlength=E).tolist()
+    tok = order // k
+    out = torch.zeros(T, H, dtype=torch.float32, device=x.device)
+    start = 0
+    wflat = topk_w.reshape(-1)
+    for e, c in enumerate(counts):
+        if c == 0:
+            continue
+        idx = order[start:start + c]
+        t = tok[start:start + c]
+        h = ops.silu_mul(F.linear(x[t], w13[e]))
+        y = F.linear(h, w2[e])
+        out.index_add_(0, t, y.float() * wflat[idx, None])
+        start += c
+    return out.to(x.dtype)
+
+
+class MoEBlock(nn.Module):
+    def __init__(self, cfg: ModelConfig, dtype, device):
+        super().__init__()
+        s = get_state()
+        self.cfg = cfg
+        self.E, self.k = cfg.num_experts, cfg.top_k_experts
+        self.mode = MOE_MODE["mode"] if s.tp_size > 1 else "tp"
+        tp, r = s.tp_size, s.tp_rank
+        H, I = cfg.hidden_size, cfg.intermediate_size
+        self.gate = ReplicatedLinear(H, self.E, dtype=dtype, device=device)
+        if self.mode == "tp":
+            assert I % tp == 0
+            self.I_local, self.E_local, self.e0 = I // tp, self.E, 0
+        else:
+            assert self.E % tp == 0
+            self.I_local, self.E_local, self.e0 = I, self.E // tp, r * (self.E // tp)
+        self.w13 = nn.Parameter(torch.empty(self.E_local, 2 * self.I_local, H, dtype=dtype,
+                                            device=device), requires_grad=False)
+        self.w2 = nn.Parameter(torch.empty(self.E_local, H, self.I_local, dtype=dtype,
+                                           device=device), requires_grad=False)
+
+    def map_weight(self, rest: str):
+        """HF names under block_sparse_moe.: gate.weight, experts.{e}.w{1,2,3}.weight."""
+        if rest.startswith("gate."):
+            return self.gate.weight, None
+        parts = rest.split(".")
+        e, which = int(parts[1]), parts[2]
+        le = e - self.e0
+        if not (0 <= le < self.E_local):
+            return None
+        s = get_state()
+        r = s.tp_rank if self.mode == "tp" else 0
+        n = self.I_local
+
+        def load(w):
+            if which == "w1":
+                self.w13.data[le, :n].copy_(w.narrow(0, r * n, n))
+            elif which == "w3":
+                self.w13.data[le, n:].copy_(w.narrow(0, r * n, n))
+            else:
+                self.w2.data[le].copy_(w.narrow(1, r * n, n))
+        return ("moe", load), None
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        logits = self.gate(x)
+        topk_w, topk_ids = ref.moe_topk_softmax(logits, self.k)
+        if self.mode == "tp":
+            y = grouped_expert_mlp(x, self.w13, self.w2, topk_w, topk_ids)
+            return comm.tp_all_reduce(y)
+        return self._forward_ep(x, topk_w, topk_ids)
+
+    def _forward_ep(self, x, topk_w, topk_ids):
+        """All-to-all dispatch/combine (C7).  Each (token, slot) pair goes to the rank
+        owning its expert; the owner computes and sends the weighted row back."""
+        s = get_state()
+        tp = s.tp_size
+        T, H = x.shape
+        flat_ids = topk_ids.reshape(-1).long()
+        dest = flat_ids // self.E_local
+        order = torch.argsort(dest, stable=True)
+        send_counts = torch.bincount(dest, minlength=tp)
+        recv_counts = torch.empty_like(send_counts)
+        dist.all_to_all_single(recv_counts, send_counts, group=s.tp_group)
+        sc, rc = send_counts.tolist(), recv_counts.tolist()
+        tok = order // self.k
+        send_x = x[tok]
+        send_meta = torch.stack([flat_ids[order], torch.arange(order.numel(), device=x.device)], 1)
+        recv_x = torch.empty(sum(rc), H, dtype=x.dtype, device=x.device)
+        dist.all_to_all_single(recv_x, send_x, rc, sc, group=s.tp_group)
+        recv_ids = torch.empty(sum(rc), 2, dtype=send_meta.dtype, device=x.device)
+        dist.all_to_all_single(recv_ids, send_meta, rc, sc, group=s.tp_group)
+        ones = torch.ones(recv_x.shape[0], 1, dtype=torch.float32, device=x.device)
+        y = grouped_expert_mlp(recv_x, self.w13, self.w2, ones, recv_ids[:, :1].to(torch.int32),
+                               expert_offset=self.e0)
+        back = torch.empty(order.numel(), H, dtype=x.dtype, device=x.device)
+        dist.all_to_all_single(back, y, sc, rc, group=s.tp_group)
+        out = torch.zeros(T, H, dtype=torch.float32, device=x.device)
+        w = topk_w.reshape(-1)[order]
+        out.index_add_(0, tok, back.float() * w[:, None])
+        return out.to(x.dtype)

@@ -1,0 +1,95 @@
+"""Collectives used by the model (SURVEY.md §2.6 call sites C1-C8).
+
+All TP collectives go through RCCL (``torch.distributed`` backend ``nccl``) on the
+TP group, except decode-size all-reduces, which use the one-shot xGMI all-reduce
+(``parallel.custom_allreduce``) when it is registered for the group and the
+message fits its buffer; ``--disable-custom-all-reduce`` (reference
+``values-01-minimal-example8.yaml:32``) keeps everything on RCCL.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .state import get_state
+
+_custom_ar = None   # parallel.custom_allreduce.CustomAllReduce or None
+
+
+def set_custom_allreduce(car) -> None:
+    global _custom_ar
+    _custom_ar = car
+
+
+def get_custom_allreduce():
+    return _custom_ar
+
+
+def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
+    """C1/C2/C3: sum over the TP group (in place when possible)."""
+    s = get_state()
+    if s.tp_size == 1:
+        return x
+    car = _custom_ar
+    if car is not None and car.should_use(x):
+        return car.all_reduce(x)
+    dist.all_reduce(x, group=s.tp_group)
+    return x
+
+
+def tp_all_gather(x: torch.Tensor, dim: int = -1) -> torch.Tensor:
+    s = get_state()
+    if s.tp_size == 1:
+        return x
+    dim = dim % x.dim()
+    out = torch.empty((s.tp_size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x.contiguous(), group=s.tp_group)
+    return torch.cat(out.unbind(0), dim=dim)
+
+
+def tp_gather(x: torch.Tensor, dim: int = -1) -> Optional[torch.Tensor]:
+    """C4: gather vocab shards of the logits onto TP rank 0 (None elsewhere).
+    On RCCL a gather is an all-gather's cost; all ranks receive (cheap, and lets
+    every rank run the same sampler when needed)."""
+    return tp_all_gather(x, dim)
+
+
+def tp_broadcast(x: torch.Tensor, src_local: int = 0) -> torch.Tensor:
+    """C6: broadcast from a TP-local rank."""
+    s = get_state()
+    if s.tp_size == 1:
+        return x
+    base = getattr(s, "global_base", 0) + s.pp_rank * s.tp_size
+    dist.broadcast(x, src=base + src_local, group=s.tp_group)
+    return x
+
+
+def pp_send(tensors: list[torch.Tensor]) -> None:
+    """C5: stage boundary, hidden + residual to the next stage."""
+    s = get_state()
+    dst = getattr(s, "global_base", 0) + s.rank + s.tp_size
+    for t in tensors:
+        dist.send(t.contiguous(), dst=dst)
+
+
+def pp_recv(shapes: list[tuple], dtype: torch.dtype, device) -> list[torch.Tensor]:
+    s = get_state()
+    src = getattr(s, "global_base", 0) + s.rank - s.tp_size
+    out = []
+    for shp in shapes:
+        t = torch.empty(shp, dtype=dtype, device=device)
+        dist.recv(t, src=src)
+        out.append(t)
+    return out
+
+
+def all_reduce_min_scalar(v: int) -> int:
+    """C8: agree on the KV block count across all model ranks."""
+    s = get_state()
+    if s.world_size == 1 or not dist.is_initialized():
+        return v
+    t = torch.tensor([v], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=s.cpu_group)
+    return int(t.item())
