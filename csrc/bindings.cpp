@@ -99,8 +99,9 @@ void rope_kv_write(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor q_out, T
               "cos_sin fp32 [max_pos, d]");
   TORCH_CHECK(q_out.is_contiguous() && q_out.numel() == T * nq * d, "q_out [T, nq, d]");
   TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && k_cache.dim() == 4 &&
-              k_cache.size(1) == nkv && k_cache.size(3) == d && v_cache.size(2) == d &&
-              v_cache.size(3) == k_cache.size(2), "kv cache layout");
+              v_cache.dim() == 5 && k_cache.size(1) == nkv && k_cache.size(3) == d &&
+              v_cache.size(3) == d && v_cache.size(4) == 8 &&
+              v_cache.size(2) * 8 == k_cache.size(2), "kv cache layout");
   TORCH_CHECK(k_cache.scalar_type() == qkv.scalar_type() && q_out.scalar_type() == qkv.scalar_type(),
               "kgc.rope_kv_write: dtype");
   const void* qn = nullptr;
@@ -118,11 +119,12 @@ void rope_kv_write(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor q_out, T
 }
 
 void check_kv(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, int64_t nq) {
-  TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 4 && k_cache.is_contiguous() &&
-              v_cache.is_contiguous(), "kv cache must be contiguous 4-D");
+  TORCH_CHECK(k_cache.dim() == 4 && v_cache.dim() == 5 && k_cache.is_contiguous() &&
+              v_cache.is_contiguous(), "k_cache 4-D / v_cache 5-D contiguous");
   const int64_t nkv = k_cache.size(1), bs = k_cache.size(2), d = k_cache.size(3);
   TORCH_CHECK(v_cache.size(0) == k_cache.size(0) && v_cache.size(1) == nkv &&
-              v_cache.size(2) == d && v_cache.size(3) == bs, "v_cache must be [nb, nkv, d, bs]");
+              v_cache.size(2) * 8 == bs && v_cache.size(3) == d && v_cache.size(4) == 8,
+              "v_cache must be [nb, nkv, bs/8, d, 8]");
   TORCH_CHECK(d == 64 || d == 128, "head_dim must be 64 or 128");
   TORCH_CHECK(nq % nkv == 0 && nq / nkv <= 16, "GQA group must be <= 16");
   TORCH_CHECK(bs >= 16, "block_size must be >= 16");
@@ -148,20 +150,17 @@ void paged_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor b
   TORCH_CHECK(ctx_lens.scalar_type() == at::kInt && ctx_lens.numel() >= B, "ctx_lens int32 [B]");
   TORCH_CHECK(max_logits.scalar_type() == at::kFloat && exp_sums.scalar_type() == at::kFloat &&
               tmp_out.scalar_type() == at::kFloat, "partials fp32");
-  const int64_t P_max = max_logits.size(-1);
+  const int64_t Zmax = max_logits.size(-1);
   TORCH_CHECK(max_logits.is_contiguous() && exp_sums.is_contiguous() && tmp_out.is_contiguous() &&
-              max_logits.numel() >= B * nq * P_max && exp_sums.numel() >= B * nq * P_max &&
-              tmp_out.numel() >= B * nq * P_max * d, "partials too small");
-  const int64_t bs = k_cache.size(2);
-  TORCH_CHECK(P_max * kgc::paged_decode_partition_size() >= block_tables.size(1) * bs,
-              "partials must cover block_tables capacity");
-  TORCH_CHECK(Z >= 1 && Z <= 65535, "Z");
+              max_logits.numel() >= B * nq * Zmax && exp_sums.numel() >= B * nq * Zmax &&
+              tmp_out.numel() >= B * nq * Zmax * d, "partials too small");
+  TORCH_CHECK(Z >= 1 && Z <= Zmax && Z <= 65535, "kgc.paged_decode: need 1 <= Z <= partial slots");
   kgc::launch_paged_decode(dt_code(q), out.data_ptr(), q.data_ptr(), k_cache.data_ptr(),
                            v_cache.data_ptr(), block_tables.data_ptr<int>(),
                            (int)block_tables.stride(0), ctx_lens.data_ptr<int>(),
                            max_logits.data_ptr<float>(), exp_sums.data_ptr<float>(),
                            tmp_out.data_ptr<float>(), (int)B, (int)nq, (int)k_cache.size(1),
-                           (int)d, log2_exact(bs, "block_size"), (int)P_max, (int)Z,
+                           (int)d, log2_exact(k_cache.size(2), "block_size"), (int)Zmax, (int)Z,
                            (float)scale, stream());
 }
 

@@ -1,10 +1,14 @@
 // K1 paged-attention decode for gfx950 (CDNA4), bf16/f16, head_dim 64/128.
 //
-// Work decomposition: grid (num_seqs, num_kv_heads, Z); a 256-thread workgroup is
-// four independent waves; wave w of z-slice z owns the 128-token partitions
-// p = 4z + w, 4z + w + 4Z, ...  (Z is picked by the host so the grid fills the 256
-// CUs without depending on max_model_len, which keeps the launch hipGraph-static).
-// A second kernel merges the per-partition (max, sum, O) partials.
+// Work decomposition: grid (num_seqs, num_kv_heads, Z).  A 256-thread workgroup is
+// four waves; the 64-token partitions of the context are dealt round-robin to the
+// 4*Z waves of a (seq, kv-head): wave w of z-slice z owns p = z*4 + w, + 4Z, ...
+// Each wave carries an online softmax (m, l, O) across its partitions; the four
+// waves merge through LDS.  With Z == 1 (large batches: the host picks Z so the
+// grid fills the 256 CUs) the workgroup writes the normalised output directly --
+// no partials, no second kernel.  With Z > 1 it writes one (max, sum, O) partial per
+// z-slice and paged_decode_reduce_kernel merges the Z partials.  Z is a host choice
+// that does not depend on the batch's actual lengths, so the launch is hipGraph-static.
 //
 // Per 32-key chunk a wave runs two MFMA products, both v_mfma_f32_16x16x32:
 //   S^T[key][head] = K[key][:] . Q^T[:][head]       A = K rows straight from HBM
@@ -15,40 +19,42 @@
 // The two S^T tiles of a chunk use the row->key map  key(m) = 8*(m>>2) + (m&3) (+4 for
 // the second tile), so after QK^T lane l holds keys 8*(l>>4) + 0..7 of head l&15 --
 // exactly the B-operand fragment of the P.V MFMA: no LDS, no lane shuffles for P.
-// The head of every accumulator element is lane&15, so softmax statistics are
-// lane-local up to a 4-lane (xor 16/32) reduction.
-//
-// Softmax is two-pass per partition (all 128 scores stay in 32 VGPRs): no online
-// rescale.  Scores are kept in the log2 domain (scale * log2(e) folded in), exp2.
+// The head of every accumulator element is lane&15, so the softmax statistics and
+// the O rescale are lane-local up to a 4-lane (xor 16/32) reduction.
+// Scores are kept in the log2 domain (scale * log2(e) folded in), exp2.
 #include "common.h"
 #include "launch.h"
 
 namespace kgc {
 
-constexpr int DEC_PART = 128;    // tokens per partition (one wave)
+constexpr int DEC_PART = 64;     // tokens per partition (one wave-iteration)
 constexpr int DEC_CHUNKS = DEC_PART / 32;
 
 template <typename T, int D>
-__global__ __launch_bounds__(256) void paged_decode_kernel(
-    const T* __restrict__ q, const T* __restrict__ kc, const T* __restrict__ vc,
-    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ ctx_lens,
-    float* __restrict__ max_logits, float* __restrict__ exp_sums, float* __restrict__ tmp_out,
-    int nq, int nkv, int bs_log2, int P_max, float scale_log2) {
+__global__ __launch_bounds__(256, 3) void paged_decode_kernel(
+    T* __restrict__ out, const T* __restrict__ q, const T* __restrict__ kc,
+    const T* __restrict__ vc, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ ctx_lens, float* __restrict__ max_logits,
+    float* __restrict__ exp_sums, float* __restrict__ tmp_out, int nq, int nkv, int bs_log2,
+    int Zmax, float scale_log2) {
   typedef typename Vec8<T>::type V8;
   constexpr int KS = D / 32;      // k-steps of the QK^T product
   constexpr int DT = D / 16;      // 16-row d-tiles of O^T
+  __shared__ __attribute__((aligned(16))) float lds_o[4][16][D];
+  __shared__ float lds_m[4][16], lds_l[4][16];
   const int b = blockIdx.x, h = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r16 = lane & 15, qd = lane >> 4;
   const int G = nq / nkv;
   // clamp to the block-table capacity: a bad length gives wrong output, never a fault
   const int ctx = min(ctx_lens[b], bt_stride << bs_log2);
-  const int P = min((ctx + DEC_PART - 1) / DEC_PART, P_max);
-  const int first = blockIdx.z * 4 + wave;
-  if (first >= P) return;
+  const int P = (ctx + DEC_PART - 1) / DEC_PART;
   const int* bt = block_tables + (int64_t)b * bt_stride;
   const int bsm = (1 << bs_log2) - 1;
   const int64_t head_stride = (int64_t)D << bs_log2;   // elements per (block, kv-head)
+  const T* kbase = kc + h * head_stride;
+  const T* vbase = vc + h * head_stride;
+  const int64_t blk_stride = (int64_t)nkv * head_stride;
 
   V8 qf[KS];
   {
@@ -63,8 +69,12 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
     }
   }
   const int keyA = 8 * (r16 >> 2) + (r16 & 3);
+  float m_run = -INFINITY, l_run = 0.f;
+  f32x4 o[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int p = first; p < P; p += gridDim.z * 4) {
+  for (int p = blockIdx.z * 4 + wave; p < P; p += gridDim.z * 4) {
     const int base = p * DEC_PART;
     f32x4 sa[DEC_CHUNKS], sb[DEC_CHUNKS];
     // ---- S^T = K . Q^T
@@ -72,10 +82,8 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
     for (int c = 0; c < DEC_CHUNKS; ++c) {
       const int ta = min(base + c * 32 + keyA, ctx - 1);
       const int tb = min(base + c * 32 + keyA + 4, ctx - 1);
-      const T* ka = kc + (int64_t)bt[ta >> bs_log2] * nkv * head_stride + h * head_stride +
-                    (int64_t)(ta & bsm) * D + 8 * qd;
-      const T* kb = kc + (int64_t)bt[tb >> bs_log2] * nkv * head_stride + h * head_stride +
-                    (int64_t)(tb & bsm) * D + 8 * qd;
+      const T* ka = kbase + bt[ta >> bs_log2] * blk_stride + (int64_t)(ta & bsm) * D + 8 * qd;
+      const T* kb = kbase + bt[tb >> bs_log2] * blk_stride + (int64_t)(tb & bsm) * D + 8 * qd;
       f32x4 accA = {0.f, 0.f, 0.f, 0.f}, accB = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
@@ -88,8 +96,8 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
       sa[c] = accA;
       sb[c] = accB;
     }
-    // ---- mask + partition max (log2 domain)
-    float m = -INFINITY;
+    // ---- mask + partition max (log2 domain) + online rescale of the carry
+    float m = m_run;
 #pragma unroll
     for (int c = 0; c < DEC_CHUNKS; ++c) {
 #pragma unroll
@@ -102,91 +110,97 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(
     }
     m = fmaxf(m, __shfl_xor(m, 16, 64));
     m = fmaxf(m, __shfl_xor(m, 32, 64));
-    // ---- P = exp2(S - m), row sums, O^T = V^T . P^T
-    float l = 0.f;
-    f32x4 o[DT];
+    const float alpha = exp2f(m_run - m);     // 0 on the first partition
+    m_run = m;
+    l_run *= alpha;
 #pragma unroll
-    for (int t = 0; t < DT; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < DT; ++t) o[t] *= alpha;
+    // ---- P = exp2(S - m), O^T += V^T . P^T
 #pragma unroll
     for (int c = 0; c < DEC_CHUNKS; ++c) {
       Pack8<T> pf;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float pa = exp2f(sa[c][i] - m), pb = exp2f(sb[c][i] - m);
-        l += pa + pb;
+        l_run += pa + pb;
         pf.h[i] = from_f<T>(pa);
         pf.h[4 + i] = from_f<T>(pb);
       }
+      // V^T 8-key group of keys t0..t0+7: [(t0 & bsm) / 8][d][8]; 16 lanes = 256 B
       const int t0 = min(base + c * 32 + 8 * qd, ctx - 1) & ~7;
-      const T* vb = vc + (int64_t)bt[t0 >> bs_log2] * nkv * head_stride + h * head_stride +
-                    ((int64_t)r16 << bs_log2) + (t0 & bsm);
+      const T* vb = vbase + bt[t0 >> bs_log2] * blk_stride + ((t0 & bsm) >> 3) * (D * 8) + r16 * 8;
 #pragma unroll
       for (int t = 0; t < DT; ++t) {
         Pack8<T> vf;
-        vf.u = *reinterpret_cast<const u32x4*>(vb + ((int64_t)(16 * t) << bs_log2));
+        vf.u = *reinterpret_cast<const u32x4*>(vb + 16 * t * 8);
         o[t] = mfma16x16x32(vf.v, pf.v, o[t]);
       }
     }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    // ---- partials: lane (r16 = head in group, qd) holds O^T[16t + 4qd + i][r16]
-    if (r16 < G) {
-      const int64_t row = ((int64_t)b * nq + h * G + r16) * P_max + p;
-      float* dst = tmp_out + row * D + 4 * qd;
+  }
+  // ---- merge the 4 waves through LDS: lane (r16 = head, qd) holds O^T[16t+4qd+i][r16]
+  l_run += __shfl_xor(l_run, 16, 64);
+  l_run += __shfl_xor(l_run, 32, 64);
 #pragma unroll
-      for (int t = 0; t < DT; ++t) *reinterpret_cast<f32x4*>(dst + 16 * t) = o[t];
-      if (qd == 0) {
-        max_logits[row] = m;
-        exp_sums[row] = l;
+  for (int t = 0; t < DT; ++t)
+    *reinterpret_cast<f32x4*>(&lds_o[wave][r16][16 * t + 4 * qd]) = o[t];
+  if (qd == 0) {
+    lds_m[wave][r16] = m_run;
+    lds_l[wave][r16] = l_run;
+  }
+  __syncthreads();
+  const bool direct = gridDim.z == 1;
+  for (int e = threadIdx.x; e < G * D; e += 256) {
+    const int hh = e / D, d = e % D;
+    float M = fmaxf(fmaxf(lds_m[0][hh], lds_m[1][hh]), fmaxf(lds_m[2][hh], lds_m[3][hh]));
+    float acc = 0.f, L = 0.f;
+    if (M != -INFINITY) {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const float f = exp2f(lds_m[w][hh] - M);
+        acc += f * lds_o[w][hh][d];
+        L += f * lds_l[w][hh];
+      }
+    }
+    const int64_t row = (int64_t)b * nq + h * G + hh;
+    if (direct) {
+      out[row * D + d] = from_f<T>(L > 0.f ? acc / L : 0.f);
+    } else {
+      const int64_t prow = row * Zmax + blockIdx.z;
+      tmp_out[prow * D + d] = acc;
+      if (d == 0) {
+        max_logits[prow] = M;
+        exp_sums[prow] = L;
       }
     }
   }
 }
 
-// Merge partitions: one 64-thread wave per (seq, q-head).
+// Merge the Z z-slice partials: one 64-thread wave per (seq, q-head).
 template <typename T, int D>
 __global__ __launch_bounds__(64) void paged_decode_reduce_kernel(
     T* __restrict__ out, const float* __restrict__ max_logits,
     const float* __restrict__ exp_sums, const float* __restrict__ tmp_out,
-    const int* __restrict__ ctx_lens, int nq, int P_max) {
-  __shared__ float wts[1024];
+    const int* __restrict__ ctx_lens, int nq, int Z, int Zmax) {
   const int b = blockIdx.x, hq = blockIdx.y, tid = threadIdx.x;
-  const int ctx = max(ctx_lens[b], 0);
-  const int P = min((ctx + DEC_PART - 1) / DEC_PART, P_max);
   T* orow = out + ((int64_t)b * nq + hq) * D;
   constexpr int EPT = D / 64;
-  if (P == 0) {
-#pragma unroll
-    for (int e = 0; e < EPT; ++e) orow[tid * EPT + e] = from_f<T>(0.f);
-    return;
-  }
-  const int64_t base = ((int64_t)b * nq + hq) * P_max;
+  const int64_t base = ((int64_t)b * nq + hq) * Zmax;
   float m = -INFINITY;
-  for (int p = tid; p < P; p += 64) m = fmaxf(m, max_logits[base + p]);
-  m = wave_max(m);
+  for (int z = 0; z < Z; ++z) m = fmaxf(m, max_logits[base + z]);
   float acc[EPT];
 #pragma unroll
   for (int e = 0; e < EPT; ++e) acc[e] = 0.f;
   float tot = 0.f;
-  for (int p0 = 0; p0 < P; p0 += 1024) {
-    const int pn = min(1024, P - p0);
-    float part = 0.f;
-    for (int p = tid; p < pn; p += 64) {
-      const float w = exp2f(max_logits[base + p0 + p] - m);
-      wts[p] = w;
-      part += w * exp_sums[base + p0 + p];
-    }
-    tot += wave_sum(part);
-    __syncthreads();
-    for (int p = 0; p < pn; ++p) {
-      const float w = wts[p];
-      const float* src = tmp_out + (base + p0 + p) * D + tid * EPT;
+  if (ctx_lens[b] > 0 && m != -INFINITY) {
+    for (int z = 0; z < Z; ++z) {
+      const float w = exp2f(max_logits[base + z] - m);
+      tot += w * exp_sums[base + z];
+      const float* src = tmp_out + (base + z) * D + tid * EPT;
 #pragma unroll
       for (int e = 0; e < EPT; ++e) acc[e] += w * src[e];
     }
-    __syncthreads();
   }
-  const float inv = 1.f / tot;
+  const float inv = tot > 0.f ? 1.f / tot : 0.f;
 #pragma unroll
   for (int e = 0; e < EPT; ++e) orow[tid * EPT + e] = from_f<T>(acc[e] * inv);
 }
@@ -194,25 +208,26 @@ __global__ __launch_bounds__(64) void paged_decode_reduce_kernel(
 template <typename T, int D>
 static void decode_dispatch(void* out, const void* q, const void* kc, const void* vc,
                             const int* bt, int bt_stride, const int* ctx, float* ml, float* es,
-                            float* tmp, int B, int nq, int nkv, int bs_log2, int P_max, int Z,
+                            float* tmp, int B, int nq, int nkv, int bs_log2, int Zmax, int Z,
                             float scale_log2, hipStream_t s) {
   paged_decode_kernel<T, D><<<dim3(B, nkv, Z), 256, 0, s>>>(
-      (const T*)q, (const T*)kc, (const T*)vc, bt, bt_stride, ctx, ml, es, tmp, nq, nkv,
-      bs_log2, P_max, scale_log2);
-  paged_decode_reduce_kernel<T, D><<<dim3(B, nq), 64, 0, s>>>((T*)out, ml, es, tmp, ctx, nq,
-                                                              P_max);
+      (T*)out, (const T*)q, (const T*)kc, (const T*)vc, bt, bt_stride, ctx, ml, es, tmp, nq,
+      nkv, bs_log2, Zmax, scale_log2);
+  if (Z > 1)
+    paged_decode_reduce_kernel<T, D><<<dim3(B, nq), 64, 0, s>>>((T*)out, ml, es, tmp, ctx, nq,
+                                                                Z, Zmax);
 }
 
 void launch_paged_decode(int dtype, void* out, const void* q, const void* k_cache,
                          const void* v_cache, const int* block_tables, int bt_stride,
                          const int* ctx_lens, float* max_logits, float* exp_sums,
                          float* tmp_out, int B, int nq, int nkv, int D, int bs_log2,
-                         int P_max, int Z, float scale, hipStream_t s) {
+                         int Zmax, int Z, float scale, hipStream_t s) {
   if (B == 0) return;
   const float sl2 = scale * 1.4426950408889634f;
 #define KGC_DEC(TT, DD)                                                                   \
   decode_dispatch<TT, DD>(out, q, k_cache, v_cache, block_tables, bt_stride, ctx_lens,   \
-                          max_logits, exp_sums, tmp_out, B, nq, nkv, bs_log2, P_max, Z,  \
+                          max_logits, exp_sums, tmp_out, B, nq, nkv, bs_log2, Zmax, Z,   \
                           sl2, s)
   if (dtype == DT_BF16) {
     if (D == 128) KGC_DEC(bf16, 128); else KGC_DEC(bf16, 64);

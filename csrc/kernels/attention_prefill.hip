@@ -90,12 +90,12 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
       kreg[u] = *reinterpret_cast<const u32x4*>(src);
     }
 #pragma unroll
-    for (int u = 0; u < VPT; ++u) {
+    for (int u = 0; u < VPT; ++u) {       // 8-key group c of dim d: contiguous in d
       const int ci = threadIdx.x + 256 * u;
-      const int d = ci >> 3, c = ci & 7;
+      const int c = ci / D, d = ci % D;
       const int ka = min(kt * PF_BN + 8 * c, L - 1) & ~7;
       const T* src = vc + (int64_t)bt[ka >> bs_log2] * nkv * hs + h * hs +
-                     ((int64_t)d << bs_log2) + (ka & bsm);
+                     ((ka & bsm) >> 3) * (D * 8) + d * 8;
       vreg[u] = *reinterpret_cast<const u32x4*>(src);
     }
   };
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
 #pragma unroll
     for (int u = 0; u < VPT; ++u) {
       const int ci = threadIdx.x + 256 * u;
-      const int d = ci >> 3, c = ci & 7;
+      const int c = ci / D, d = ci % D;
       *reinterpret_cast<u32x4*>(V + d * PF_BN + ((c ^ ((d >> 1) & 7)) * 8)) = vreg[u];
     }
   };

@@ -22,7 +22,7 @@ void launch_paged_decode(int dtype, void* out, const void* q, const void* k_cach
                          const void* v_cache, const int* block_tables, int bt_stride,
                          const int* ctx_lens, float* max_logits, float* exp_sums,
                          float* tmp_out, int B, int nq, int nkv, int D, int bs_log2,
-                         int P_max, int Z, float scale, hipStream_t s);
+                         int Zmax, int Z, float scale, hipStream_t s);
 int paged_decode_partition_size();
 void launch_prefill_attention(int dtype, const void* q, void* out, const void* k_cache,
                               const void* v_cache, const int* block_tables, int bt_stride,

@@ -18,7 +18,12 @@ __global__ __launch_bounds__(NORM_NT) void rms_norm_kernel(
   const int nv = H >> 3;
   const T* xr = x + row * x_stride;
   T* rr = ADD ? residual + (int64_t)row * H : nullptr;
-  Pack8<T> v[NORM_MAXV];
+  Pack8<T> v[NORM_MAXV], wv[NORM_MAXV];
+#pragma unroll
+  for (int i = 0; i < NORM_MAXV; ++i) {   // weight loads issued before the reduction
+    const int idx = threadIdx.x + i * NORM_NT;
+    if (idx < nv) wv[i].u = *reinterpret_cast<const u32x4*>(w + idx * 8);
+  }
   float ss = 0.f;
 #pragma unroll
   for (int i = 0; i < NORM_MAXV; ++i) {
@@ -46,10 +51,9 @@ __global__ __launch_bounds__(NORM_NT) void rms_norm_kernel(
   for (int i = 0; i < NORM_MAXV; ++i) {
     const int idx = threadIdx.x + i * NORM_NT;
     if (idx < nv) {
-      Pack8<T> wv, o;
-      wv.u = *reinterpret_cast<const u32x4*>(w + idx * 8);
+      Pack8<T> o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o.h[j] = from_f<T>(to_f(v[i].h[j]) * inv * to_f(wv.h[j]));
+      for (int j = 0; j < 8; ++j) o.h[j] = from_f<T>(to_f(v[i].h[j]) * inv * to_f(wv[i].h[j]));
       *reinterpret_cast<u32x4*>(orow + idx * 8) = o.u;
     }
   }

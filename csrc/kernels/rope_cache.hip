@@ -1,17 +1,17 @@
 // K3 + K5 + K6 fused: split the fused QKV projection row, optional per-head q/k
 // RMSNorm (Qwen3), NeoX RoPE on q and k, write rotated q contiguous and scatter
-// k / v into the paged cache.  One workgroup per token; one thread owns the pair
+// k / v into the paged cache.  grid (tokens, item groups); one thread owns the pair
 // of 16-byte chunks (c, c + d/2) of one head so the rotation needs no exchange;
 // the head's TPH = d/16 threads are an aligned lane group for the q/k-norm sum.
 //
 // Cache layouts (see ops/reference.py):
-//   k_cache [nb, nkv, bs, d]    v_cache [nb, nkv, d, bs]  (V^T for the MFMA B operand)
+//   k_cache [nb, nkv, bs, d]    v_cache [nb, nkv, bs/8, d, 8]  (V^T in 8-key groups)
 #include "common.h"
 #include "launch.h"
 
 namespace kgc {
 
-constexpr int ROPE_NT = 256;
+constexpr int ROPE_NT = 128;
 
 template <typename T, bool NORM, bool ROPE>
 __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
@@ -20,25 +20,40 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
     T* __restrict__ v_cache, const int64_t* __restrict__ slot_mapping,
     const T* __restrict__ qn_w, const T* __restrict__ kn_w, int nq, int nkv, int d, int bs,
     float eps) {
+  // item space of one token: [q/k rotation items, padded to a wave] [v scatter items];
+  // gridDim.y workgroups of ROPE_NT items share a token (fills the CUs at decode).
   const int t = blockIdx.x;
-  const int64_t slot = slot_mapping[t];
-  const int64_t pos = positions[t];
   const int tph = d >> 4;               // threads per head (pairs of 8-elem chunks)
   const int half = d >> 1;
+  const int n_qk = (nq + nkv) * tph;
+  const int n_qk_pad = (n_qk + 63) & ~63;
+  const int it = blockIdx.y * ROPE_NT + threadIdx.x;
+  const int64_t slot = slot_mapping[t];
   const T* row = qkv + (int64_t)t * qkv_stride;
-  const float* cs = cos_sin + pos * d;
-  const int n_qk_items = (nq + nkv) * tph;
   const int64_t blk = slot >= 0 ? slot / bs : 0;
   const int off = slot >= 0 ? (int)(slot % bs) : 0;
-  // q and k heads: rotate (and optionally normalize)
-  for (int it = threadIdx.x; it < ((n_qk_items + 63) & ~63); it += ROPE_NT) {
-    const bool active = it < n_qk_items;
+  if (it < n_qk_pad) {                  // whole waves take this branch together
+    const bool active = it < n_qk;
     const int head = active ? it / tph : 0;     // 0..nq-1 = q, nq.. = k
     const int c = it % tph;                     // chunk index within the first half
     const T* src = row + head * d;
     Pack8<T> a, b;
     a.u = *reinterpret_cast<const u32x4*>(src + c * 8);
     b.u = *reinterpret_cast<const u32x4*>(src + half + c * 8);
+    float4 c0, c1, s0, s1;
+    if (ROPE) {
+      const float* cs = cos_sin + positions[t] * d;
+      c0 = *reinterpret_cast<const float4*>(cs + c * 8);
+      c1 = *reinterpret_cast<const float4*>(cs + c * 8 + 4);
+      s0 = *reinterpret_cast<const float4*>(cs + half + c * 8);
+      s1 = *reinterpret_cast<const float4*>(cs + half + c * 8 + 4);
+    }
+    Pack8<T> wa, wb;
+    if (NORM) {
+      const T* nw = head < nq ? qn_w : kn_w;
+      wa.u = *reinterpret_cast<const u32x4*>(nw + c * 8);
+      wb.u = *reinterpret_cast<const u32x4*>(nw + half + c * 8);
+    }
     float xa[8], xb[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) { xa[j] = to_f(a.h[j]); xb[j] = to_f(b.h[j]); }
@@ -48,10 +63,6 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
       for (int j = 0; j < 8; ++j) ss += xa[j] * xa[j] + xb[j] * xb[j];
       for (int o = 1; o < tph; o <<= 1) ss += __shfl_xor(ss, o, 64);
       const float inv = rsqrtf(ss / (float)d + eps);
-      const T* nw = head < nq ? qn_w : kn_w;
-      Pack8<T> wa, wb;
-      wa.u = *reinterpret_cast<const u32x4*>(nw + c * 8);
-      wb.u = *reinterpret_cast<const u32x4*>(nw + half + c * 8);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         // round through T like the unfused reference (norm output is stored in T)
@@ -59,19 +70,15 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
         xb[j] = to_f(from_f<T>(xb[j] * inv * to_f(wb.h[j])));
       }
     }
-    if (!active) continue;
+    if (!active) return;
     Pack8<T> oa, ob;
     if (ROPE) {
-      const float4 c0 = *reinterpret_cast<const float4*>(cs + c * 8);
-      const float4 c1 = *reinterpret_cast<const float4*>(cs + c * 8 + 4);
-      const float4 s0 = *reinterpret_cast<const float4*>(cs + half + c * 8);
-      const float4 s1 = *reinterpret_cast<const float4*>(cs + half + c * 8 + 4);
       const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-      const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        oa.h[j] = from_f<T>(xa[j] * cc[j] - xb[j] * ss[j]);
-        ob.h[j] = from_f<T>(xb[j] * cc[j] + xa[j] * ss[j]);
+        oa.h[j] = from_f<T>(xa[j] * cc[j] - xb[j] * sn[j]);
+        ob.h[j] = from_f<T>(xb[j] * cc[j] + xa[j] * sn[j]);
       }
     } else {
 #pragma unroll
@@ -87,19 +94,19 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
       *reinterpret_cast<u32x4*>(dst + c * 8) = oa.u;
       *reinterpret_cast<u32x4*>(dst + half + c * 8) = ob.u;
     }
+    return;
   }
-  if (slot < 0) return;
-  // v heads: transposed scatter (one element per 2-byte store, d*bs stride per dim)
-  const T* vsrc = row + (nq + nkv) * d;
-  const int n_v = nkv * (d >> 3);
-  for (int it = threadIdx.x; it < n_v; it += ROPE_NT) {
-    const int h = it / (d >> 3), c = it % (d >> 3);
-    Pack8<T> v;
-    v.u = *reinterpret_cast<const u32x4*>(vsrc + h * d + c * 8);
-    T* dst = v_cache + ((blk * nkv + h) * d + c * 8) * bs + off;
+  // v heads: transposed scatter into the 8-key group of this token (2-byte stores at
+  // a 16-byte stride: the 8 stores of a thread share one 128-byte line)
+  const int iv = it - n_qk_pad;
+  if (slot < 0 || iv >= nkv * (d >> 3)) return;
+  const int h = iv / (d >> 3), c = iv % (d >> 3);
+  Pack8<T> v;
+  v.u = *reinterpret_cast<const u32x4*>(row + (nq + nkv) * d + h * d + c * 8);
+  T* dst = v_cache + (blk * nkv + h) * (int64_t)bs * d + ((int64_t)(off >> 3) * d + c * 8) * 8 +
+           (off & 7);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dst[j * bs] = v.h[j];
-  }
+  for (int j = 0; j < 8; ++j) dst[j * 8] = v.h[j];
 }
 
 template <typename T>
@@ -109,8 +116,10 @@ static void rope_dispatch(const void* qkv, int64_t qkv_stride, const int64_t* po
                           int nq, int nkv, int d, int bs, float eps, bool rope,
                           hipStream_t s) {
   if (T_ == 0) return;
+  const int n_items = (((nq + nkv) * (d >> 4) + 63) & ~63) + nkv * (d >> 3);
+  const dim3 grid(T_, (n_items + ROPE_NT - 1) / ROPE_NT);
 #define KGC_ROPE_LAUNCH(N, R)                                                               \
-  rope_kv_kernel<T, N, R><<<T_, ROPE_NT, 0, s>>>((const T*)qkv, qkv_stride, pos, cs,       \
+  rope_kv_kernel<T, N, R><<<grid, ROPE_NT, 0, s>>>((const T*)qkv, qkv_stride, pos, cs,       \
                                                  (T*)q_out, (T*)kc, (T*)vc, slots,          \
                                                  (const T*)qn, (const T*)kn, nq, nkv, d,    \
                                                  bs, eps)

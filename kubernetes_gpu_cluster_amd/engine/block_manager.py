@@ -1,7 +1,7 @@
 """Paged KV-cache block allocator.
 
 Block ids index the per-layer cache tensors ``k_cache[nb, nkv, bs, d]`` /
-``v_cache[nb, nkv, d, bs]``.  Block 0 is reserved (never handed out) so padded
+``v_cache[nb, nkv, bs/8, d, 8]``.  Block 0 is reserved (never handed out) so padded
 block-table entries always point at valid memory.  Each running sequence owns a
 row ("slot") of a persistent int32 block table that is updated incrementally as
 blocks are appended, so building a step's block tables is a single row gather.

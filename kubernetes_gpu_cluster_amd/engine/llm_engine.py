@@ -19,10 +19,11 @@ from ..utils.metrics import EngineMetrics
 from .block_manager import BlockManager
 from .config import EngineConfig
 from .scheduler import Scheduler
-from .sequence import RequestOutput, SamplingParams, Sequence
+from .sequence import RequestOutput, SamplingParams, SeqStatus, Sequence
 from .worker import LocalExecutor, MultiprocExecutor, default_max_model_len
 
 log = logging.getLogger("kgc.engine")
+_PENDING = -1          # placeholder for a sampled token still on the GPU
 
 
 class LLMEngine:
@@ -46,6 +47,8 @@ class LLMEngine:
         self._ids = itertools.count()
         self.metrics = EngineMetrics()
         self.eos = self.mcfg.eos_token_id
+        self.async_mode = cfg.async_output and getattr(executor, "supports_async", False)
+        self._inflight = None
         self.init_s = time.time() - t0
         log.info("engine ready: %d KV blocks x %d tokens, graphs %.1fs", nb, cfg.block_size,
                  self.graph_s)
@@ -75,10 +78,78 @@ class LLMEngine:
             self.metrics.on_finish(s)
 
     def has_unfinished(self) -> bool:
-        return self.scheduler.has_work()
+        return self.scheduler.has_work() or self._inflight is not None
 
     # ------------------------------------------------------------------ step
     def step(self) -> list[RequestOutput]:
+        """One engine iteration.  In async mode (default, TP x PP with PP == 1) the
+        step launches batch N and then processes the tokens of batch N-1 while batch N
+        runs on the GPU: decode inputs come from the device-side last-token table, so
+        host bookkeeping (sampled-token append, stop checks, scheduling) overlaps GPU
+        execution.  EOS / stop-token finishes are therefore seen one step late (the
+        extra token is discarded); length finishes are exact."""
+        if not self.async_mode:
+            return self._step_sync()
+        launched = None
+        batch = self.scheduler.schedule()
+        if not batch.is_empty:
+            t0 = time.monotonic()
+            plan, samplers = self.executor.runner.build_plan(batch.prefills, batch.decodes,
+                                                             self.bm.table, device_tokens=True)
+            fut = self.executor.execute_async(plan)
+            for seq, n in batch.prefills:
+                seq.num_computed += n
+            for seq in batch.decodes:
+                seq.num_computed += 1
+            for seq in samplers:
+                seq.output_token_ids.append(_PENDING)
+                if len(seq.output_token_ids) >= seq.max_tokens or seq.num_tokens >= self.max_model_len:
+                    # finished by length: release now (stream order protects the KV
+                    # blocks still being written by the in-flight step)
+                    self.scheduler.finish(seq, "length")
+                    self.seqs.pop(seq.request_id, None)
+            launched = (fut, samplers, plan, t0, len(batch.preempted))
+        outs = self._process(self._inflight) if self._inflight is not None else []
+        self._inflight = launched
+        return outs
+
+    def _process(self, inflight) -> list[RequestOutput]:
+        fut, samplers, plan, t0, npre = inflight
+        tokens = fut.result()
+        now = time.monotonic()
+        outs: list[RequestOutput] = []
+        for seq, tok in zip(samplers, tokens):
+            if seq.finish_reason not in (None, "length"):
+                continue        # finished earlier (EOS seen one step late) or aborted
+            try:
+                idx = seq.output_token_ids.index(_PENDING)
+            except ValueError:
+                continue
+            seq.output_token_ids[idx] = tok
+            if seq.first_token_time is None:
+                seq.first_token_time = now
+            seq.last_token_time = now
+            reason = seq.finish_reason if seq.finished else self._check_stop(seq, tok)
+            if reason is not None and not seq.finished:
+                # EOS / stop token: drop tokens launched after this one
+                del seq.output_token_ids[idx + 1:]
+                self.scheduler.finish(seq, reason)
+                self.seqs.pop(seq.request_id, None)
+            if reason is not None and _PENDING not in seq.output_token_ids:
+                seq.finish_time = now
+                self.metrics.on_finish(seq)
+                done = True
+            else:
+                done = False
+            outs.append(RequestOutput(seq.request_id, seq.prompt_token_ids, [tok],
+                                      list(seq.output_token_ids), done, reason if done else None,
+                                      seq.arrival_time, seq.first_token_time, seq.finish_time,
+                                      seq.num_preemptions))
+        self.metrics.on_step(plan, now - t0, len(samplers), self.bm.usage(),
+                             len(self.scheduler.running), len(self.scheduler.waiting), npre)
+        return outs
+
+    def _step_sync(self) -> list[RequestOutput]:
         batch = self.scheduler.schedule()
         if batch.is_empty:
             return []
@@ -86,7 +157,6 @@ class LLMEngine:
         plan, samplers = self.executor.runner.build_plan(batch.prefills, batch.decodes, self.bm.table)
         tokens = self.executor.execute(plan)
         now = time.monotonic()
-        # advance computed counters
         for seq, n in batch.prefills:
             seq.num_computed += n
         for seq in batch.decodes:
@@ -104,7 +174,7 @@ class LLMEngine:
                 self.seqs.pop(seq.request_id, None)
                 self.metrics.on_finish(seq)
             outs.append(RequestOutput(seq.request_id, seq.prompt_token_ids, [tok],
-                                      seq.output_token_ids, reason is not None, reason,
+                                      list(seq.output_token_ids), reason is not None, reason,
                                       seq.arrival_time, seq.first_token_time, seq.finish_time,
                                       seq.num_preemptions))
         self.metrics.on_step(plan, now - t0, len(samplers), self.bm.usage(),

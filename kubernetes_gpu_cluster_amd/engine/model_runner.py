@@ -48,12 +48,14 @@ class StepPlan:
     W: int                 # prefill attention work items
     B: int                 # graph bucket (0 = eager)
     max_ctx: int           # longest decode context
+    dev_tok: int           # 1: decode input tokens come from the device-side last_tok table
     i64: np.ndarray
     i32: np.ndarray
     f32: np.ndarray
 
     def header(self) -> list[int]:
-        return [self.T, self.Tp, self.P, self.D, self.S, self.W, self.B, self.max_ctx]
+        return [self.T, self.Tp, self.P, self.D, self.S, self.W, self.B, self.max_ctx,
+                self.dev_tok]
 
 
 class Layout:
@@ -68,6 +70,8 @@ class Layout:
         self.slots, o = o, o + self.Tmax
         self.seeds, o = o, o + self.Smax
         self.lidx, o = o, o + self.Smax
+        self.dslots, o = o, o + self.Smax     # decode row -> seq slot (token gather)
+        self.sslots, o = o, o + self.Smax     # sampled row -> seq slot (token scatter)
         self.n64 = o
         o = 0
         self.dbt, o = o, o + self.Smax * max_blocks
@@ -116,6 +120,12 @@ class ModelRunner:
         self.graphs: dict[int, tuple] = {}
         self.graph_pool = None
         self.sample_out = torch.zeros(max_num_seqs, dtype=torch.int64, device=device)
+        # last sampled token per sequence slot: decode steps read their input token
+        # here, so the host can launch step N+1 before it has seen step N's tokens
+        self.last_tok = torch.zeros(max_num_seqs, dtype=torch.int64, device=device)
+        self.tok_host = [torch.zeros(max_num_seqs, dtype=torch.int64, pin_memory=self.is_gpu)
+                         for _ in range(2)]
+        self._tok_flip = 0
         self.stats = {"graph_steps": 0, "eager_steps": 0}
 
     # ------------------------------------------------------------------ KV cache
@@ -159,7 +169,7 @@ class ModelRunner:
         # zero-init: stale slots of partially filled blocks must hold finite values
         self.kv = torch.zeros(L, 2, num_blocks, nkv, self.bs, d, dtype=self.dtype,
                               device=self.device)
-        self.kv_caches = [(self.kv[l, 0], self.kv[l, 1].view(num_blocks, nkv, d, self.bs))
+        self.kv_caches = [(self.kv[l, 0], self.kv[l, 1].view(num_blocks, nkv, self.bs // 8, d, 8))
                           for l in range(L)]
         self.num_blocks = num_blocks
         nq = m.layers[0].self_attn.nq if hasattr(m.layers[0], "self_attn") else m.layers[0].qkv_proj.nq
@@ -186,14 +196,16 @@ class ModelRunner:
         i32[L.wm:L.wm + len(wm)] = wm
         i64[L.lidx:L.lidx + P] = qsl[1:] - 1
         self.hf.numpy()[: 2 * self.L.Smax] = 1.0
-        plan = StepPlan(T, T, P, 0, P, len(ws), 0, 0, i64, i32, self.hf.numpy())
+        i64[L.sslots:L.sslots + P] = 0
+        plan = StepPlan(T, T, P, 0, P, len(ws), 0, 0, 0, i64, i32, self.hf.numpy())
         self.run(plan)
 
     # ------------------------------------------------------------------ packing (driver)
     def build_plan(self, prefills: list[tuple[Sequence, int]], decodes: list[Sequence],
-                   table: np.ndarray) -> tuple[StepPlan, list[Sequence]]:
+                   table: np.ndarray, device_tokens: bool = False) -> tuple[StepPlan, list[Sequence]]:
         """Pack a scheduled batch.  Returns the plan and the sequences that sample
-        (in sampled-row order)."""
+        (in sampled-row order).  device_tokens: decode inputs are gathered on the GPU
+        from last_tok (async mode), so the host needs no sampled token values."""
         L, bs, mb = self.L, self.bs, self.max_blocks
         i64, i32, f32 = self.h64.numpy(), self.h32.numpy(), self.hf.numpy()
         P, D = len(prefills), len(decodes)
@@ -231,12 +243,16 @@ class ModelRunner:
         if D:
             slots = np.fromiter((s.slot for s in decodes), dtype=np.int64, count=D)
             pos = np.fromiter((s.num_computed for s in decodes), dtype=np.int64, count=D)
-            toks = [s.output_token_ids[-1] if s.output_token_ids else s.prompt_token_ids[-1]
-                    for s in decodes]
             if self.use_graphs and P == 0 and D <= self.graph_max_bs:
                 B = next(b for b in self.buckets if b >= D)
             n = max(D, B)
-            i64[L.ids + Tp:L.ids + Tp + D] = toks
+            if device_tokens:
+                i64[L.dslots:L.dslots + D] = slots
+                i64[L.dslots + D:L.dslots + n] = 0
+            else:
+                i64[L.ids + Tp:L.ids + Tp + D] = [
+                    s.output_token_ids[-1] if s.output_token_ids else s.prompt_token_ids[-1]
+                    for s in decodes]
             i64[L.pos + Tp:L.pos + Tp + D] = pos
             i64[L.slots + Tp:L.slots + Tp + D] = table[slots, pos // bs].astype(np.int64) * bs + pos % bs
             dbt = i32[L.dbt:L.dbt + n * mb].reshape(n, mb)
@@ -254,6 +270,7 @@ class ModelRunner:
         S = len(samplers)
         T = Tp + D
         # ---- sampling params
+        i64[L.sslots:L.sslots + S] = [s.slot for s in samplers]
         for j, s in enumerate(samplers):
             p = s.params
             f32[L.temp + j] = p.temperature
@@ -263,7 +280,8 @@ class ModelRunner:
         i64[L.lidx:L.lidx + S] = lidx
         if B:
             i64[L.lidx:L.lidx + B] = np.arange(B)   # graph rows index their own hidden row
-        return StepPlan(T, Tp, P, D, S, W, B, max_ctx, i64, i32, f32), samplers
+        return StepPlan(T, Tp, P, D, S, W, B, max_ctx, int(device_tokens and D > 0), i64, i32,
+                        f32), samplers
 
     # ------------------------------------------------------------------ execution (all ranks)
     def _upload(self, plan: StepPlan) -> None:
@@ -315,6 +333,10 @@ class ModelRunner:
         if not self.model.first:
             shp = (plan.B or plan.T, self.mcfg.hidden_size)
             hidden_in = comm.pp_recv([shp, shp], self.dtype, self.device)
+        elif plan.dev_tok:
+            n = max(plan.D, plan.B)
+            torch.index_select(self.last_tok, 0, self.d64[L.dslots:L.dslots + n],
+                               out=self.d64[L.ids + plan.Tp:L.ids + plan.Tp + n])
         if plan.B and plan.B in self.graphs and self.model.first and self.model.last:
             g, logits = self.graphs[plan.B]
             g.replay()
@@ -335,7 +357,21 @@ class ModelRunner:
         res = ops.sample(logits, self.df[L.temp:L.temp + plan.S], self.d32[L.topk:L.topk + plan.S],
                          self.df[L.topp:L.topp + plan.S], self.d64[L.seeds:L.seeds + plan.S],
                          out=out if self.is_gpu else None)
+        self.last_tok.index_copy_(0, self.d64[L.sslots:L.sslots + plan.S], res)
         return res
+
+    def tokens_to_host(self, res: torch.Tensor):
+        """Start the D2H copy of sampled ids into a pinned (double-buffered) host
+        buffer; returns (host view, event) -- read after event.synchronize()."""
+        buf = self.tok_host[self._tok_flip][: res.shape[0]]
+        self._tok_flip ^= 1
+        if not self.is_gpu:
+            buf.copy_(res)
+            return buf, None
+        buf.copy_(res, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return buf, ev
 
     # ------------------------------------------------------------------ hipGraph capture
     @torch.inference_mode()

@@ -91,7 +91,7 @@ class Worker:
 # ---------------------------------------------------------------------- plan transport
 def _bcast_cmd(cmd: int, arg: int = 0, header: Optional[list[int]] = None) -> list[int]:
     s = get_state()
-    h = torch.zeros(10, dtype=torch.int64)
+    h = torch.zeros(12, dtype=torch.int64)
     if s.rank == 0:
         h[0], h[1] = cmd, arg
         if header:
@@ -130,7 +130,7 @@ def worker_loop(worker: Worker) -> None:
         elif cmd == CMD_CAPTURE:
             worker.capture()
         elif cmd == CMD_STEP:
-            hdr = h[2:10]
+            hdr = h[2:11]
             _bcast_plan_blobs(worker.runner, hdr)
             r = worker.runner
             plan = StepPlan(*hdr, r.h64.numpy(), r.h32.numpy(), r.hf.numpy())
@@ -160,8 +160,30 @@ class LocalExecutor:
         out = self.worker.run(plan)
         return out.tolist()
 
+    def execute_async(self, plan: StepPlan) -> "TokenFuture":
+        out = self.worker.run(plan)
+        return TokenFuture(*self.runner.tokens_to_host(out))
+
+    @property
+    def supports_async(self) -> bool:
+        return True
+
     def shutdown(self) -> None:
         pass
+
+
+class TokenFuture:
+    """Sampled ids of a launched step; result() blocks until the D2H copy landed."""
+
+    def __init__(self, buf: torch.Tensor, ev=None, values: Optional[list[int]] = None):
+        self.buf, self.ev, self.values = buf, ev, values
+
+    def result(self) -> list[int]:
+        if self.values is None:
+            if self.ev is not None:
+                self.ev.synchronize()
+            self.values = self.buf.tolist()
+        return self.values
 
 
 class _DistExecutorBase:
@@ -184,6 +206,16 @@ class _DistExecutorBase:
     def capture(self) -> float:
         _bcast_cmd(CMD_CAPTURE)
         return self.worker.capture()
+
+    @property
+    def supports_async(self) -> bool:
+        return get_state().pp_size == 1
+
+    def execute_async(self, plan: StepPlan) -> TokenFuture:
+        _bcast_cmd(CMD_STEP, 0, plan.header())
+        _bcast_plan_blobs(self.worker.runner, plan.header())
+        out = self.worker.run(plan)
+        return TokenFuture(*self.runner.tokens_to_host(out))
 
     def execute(self, plan: StepPlan) -> list[int]:
         _bcast_cmd(CMD_STEP, 0, plan.header())

@@ -206,6 +206,8 @@ class LlamaForCausalLM(nn.Module):
             return mlp.down_proj.weight, None
         if rest.startswith("block_sparse_moe."):
             return mlp.map_weight(rest[len("block_sparse_moe."):])
+        if cfg.is_moe and rest.startswith("mlp."):
+            return mlp.map_weight(rest[len("mlp."):])
         return None
 
     def load_weights(self, weights: Iterable[tuple[str, torch.Tensor]]) -> int:

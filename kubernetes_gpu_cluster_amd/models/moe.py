@@ -83,9 +83,24 @@ class MoEBlock(nn.Module):
                                            device=device), requires_grad=False)
 
     def map_weight(self, rest: str):
-        """HF names under block_sparse_moe.: gate.weight, experts.{e}.w{1,2,3}.weight."""
+        """Checkpoint names under ``block_sparse_moe.``: gate.weight,
+        experts.{e}.w{1,2,3}.weight; or the fused transformers-v5 names under ``mlp.``:
+        gate.weight, experts.gate_up_proj [E, 2I, H], experts.down_proj [E, H, I]."""
         if rest.startswith("gate."):
             return self.gate.weight, None
+        if rest in ("experts.gate_up_proj", "experts.down_proj"):
+            s = get_state()
+            r = s.tp_rank if self.mode == "tp" else 0
+            n, I = self.I_local, self.cfg.intermediate_size
+            e0, e1 = self.e0, self.e0 + self.E_local
+
+            def load_fused(w):
+                if rest.endswith("gate_up_proj"):
+                    self.w13.data[:, :n].copy_(w[e0:e1, r * n:(r + 1) * n])
+                    self.w13.data[:, n:].copy_(w[e0:e1, I + r * n:I + (r + 1) * n])
+                else:
+                    self.w2.data.copy_(w[e0:e1, :, r * n:(r + 1) * n])
+            return ("moe", load_fused), None
         parts = rest.split(".")
         e, which = int(parts[1]), parts[2]
         le = e - self.e0

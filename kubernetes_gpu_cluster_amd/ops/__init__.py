@@ -116,23 +116,30 @@ def rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Ten
 
 
 # ------------------------------------------------------------------ attention
-DECODE_PARTITION = 128
+DECODE_PARTITION = 64        # tokens per wave-iteration of the decode kernel
 PREFILL_BLOCK_M = 128
+
+
+def decode_max_z(max_blocks: int, block_size: int) -> int:
+    parts = math.ceil(max_blocks * block_size / DECODE_PARTITION)
+    return max(1, math.ceil(parts / 4))
 
 
 def decode_partials(batch: int, num_heads: int, head_dim: int, max_blocks: int,
                     block_size: int, device) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-    """Workspace for the split-context decode kernel (static: graph-capturable)."""
-    P = math.ceil(max_blocks * block_size / DECODE_PARTITION)
-    ml = torch.empty(batch, num_heads, P, dtype=torch.float32, device=device)
-    es = torch.empty(batch, num_heads, P, dtype=torch.float32, device=device)
-    tmp = torch.empty(batch, num_heads, P, head_dim, dtype=torch.float32, device=device)
+    """Per-z-slice (max, sum, O) partials of the split-context decode kernel
+    (static: graph-capturable).  Unused when the grid has a single z-slice."""
+    Z = decode_max_z(max_blocks, block_size)
+    ml = torch.empty(batch, num_heads, Z, dtype=torch.float32, device=device)
+    es = torch.empty(batch, num_heads, Z, dtype=torch.float32, device=device)
+    tmp = torch.empty(batch, num_heads, Z, head_dim, dtype=torch.float32, device=device)
     return ml, es, tmp
 
 
 def decode_grid_z(batch: int, num_kv_heads: int, max_ctx: int, target_waves: int = 4096) -> int:
-    """z-slices of the decode grid: enough waves to fill 256 CUs, bounded by the
-    number of 128-token partitions of the longest context."""
+    """z-slices of the decode grid: enough waves to fill 256 CUs (3 resident waves
+    per SIMD), bounded by the 64-token partitions of the longest context.  Z == 1
+    (large batches) lets the kernel write its output directly."""
     parts = max(1, math.ceil(max_ctx / DECODE_PARTITION))
     want = math.ceil(target_waves / max(1, batch * num_kv_heads * 4))
     return max(1, min(want, math.ceil(parts / 4)))
@@ -150,6 +157,7 @@ def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torc
     if workspace is None:
         workspace = decode_partials(B, nq, d, block_tables.shape[1], k_cache.shape[2], q.device)
     ml, es, tmp = workspace
+    grid_z = min(grid_z, ml.shape[-1])
     _k().paged_decode(out, q, k_cache, v_cache, block_tables, context_lens, ml, es, tmp,
                       grid_z, scale)
     return out

@@ -7,8 +7,10 @@ written for clarity, in fp32, not speed.
 KV-cache layout (shared with the HIP kernels, chosen for CDNA4 MFMA operand
 loads, see csrc/kernels/attention_decode.hip):
   k_cache: [num_blocks, num_kv_heads, block_size, head_dim]   (key rows contiguous)
-  v_cache: [num_blocks, num_kv_heads, head_dim, block_size]   (V^T: 8 consecutive keys of
-                                                               one dim are 16 contiguous bytes)
+  v_cache: [num_blocks, num_kv_heads, block_size/8, head_dim, 8]
+           (V^T in 8-key groups: the 8 consecutive keys of one dim are 16 contiguous
+            bytes -- the MFMA A-operand fragment of O^T = V^T.P^T -- and the 16 dims
+            of one 16-row tile are 256 contiguous bytes)
 """
 from __future__ import annotations
 
@@ -113,7 +115,7 @@ def kv_cache_write(k: torch.Tensor, v: torch.Tensor, k_cache: torch.Tensor,
     sm = sm[valid]
     blk, off = sm // bs, sm % bs
     k_cache[blk, :, off, :] = k[valid].to(k_cache.dtype)
-    v_cache[blk, :, :, off] = v[valid].to(v_cache.dtype)
+    v_cache[blk, :, off // 8, :, off % 8] = v[valid].to(v_cache.dtype)
 
 
 # ---------------------------------------------------------------- attention
@@ -123,8 +125,8 @@ def _gather_kv(k_cache, v_cache, block_table, ctx_len):
     blocks = block_table[:nb].long()
     k = k_cache[blocks]                                   # [nb, nkv, bs, d]
     k = k.permute(0, 2, 1, 3).reshape(nb * bs, k.shape[1], k.shape[3])[:ctx_len]
-    v = v_cache[blocks]                                   # [nb, nkv, d, bs]
-    v = v.permute(0, 3, 1, 2).reshape(nb * bs, v.shape[1], v.shape[2])[:ctx_len]
+    v = v_cache[blocks]                                   # [nb, nkv, bs/8, d, 8]
+    v = v.permute(0, 2, 4, 1, 3).reshape(nb * bs, v.shape[1], v.shape[3])[:ctx_len]
     return k.float(), v.float()                           # [ctx, nkv, d]
 
 

@@ -1,0 +1,97 @@
+"""Engine-level checks on the MI355X: model parity through the HIP kernels,
+hipGraph decode replay == eager, async engine loop, Llama-3-8B-dims smoke."""
+import pytest
+import torch
+
+from kubernetes_gpu_cluster_amd.engine.config import EngineConfig
+from kubernetes_gpu_cluster_amd.engine.llm_engine import LLMEngine
+from kubernetes_gpu_cluster_amd.engine.sequence import SamplingParams
+from kubernetes_gpu_cluster_amd.models import PRESETS, build_model, full_state_dict_random
+from kubernetes_gpu_cluster_amd.engine.model_runner import ModelRunner
+from kubernetes_gpu_cluster_amd.parallel.state import ParallelState, set_state
+
+from test_model_parity import _engine_logits, _hf_model
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-qwen3", "tiny-qwen2", "tiny-mixtral"])
+def test_gpu_logits_match_hf(gpu, name):
+    cfg = PRESETS[name]
+    sd = full_state_dict_random(cfg, seed=2, std=0.05)
+    hf, _ = _hf_model(cfg, sd)
+    set_state(ParallelState(device=gpu))
+    model = build_model(cfg, torch.bfloat16, gpu)
+    model.load_weights(sd.items())
+    runner = ModelRunner(model, cfg, torch.bfloat16, gpu, block_size=16, max_model_len=256,
+                         max_num_seqs=4, token_budget=128, enforce_eager=True)
+    runner.init_kv_cache(48)
+    g = torch.Generator().manual_seed(0)
+    prompt = torch.randint(3, cfg.vocab_size, (70,), generator=g).tolist()
+    extra = torch.randint(3, cfg.vocab_size, (4,), generator=g).tolist()
+    with torch.no_grad():
+        ref = hf(torch.tensor([prompt + extra])).logits[0].float()
+    got = _engine_logits(model, runner, prompt, [33, 37], extra).float().cpu()
+    scale = ref.abs().max().item()
+    pos_err = (got - ref).abs().max(-1).values
+    cos = torch.nn.functional.cosine_similarity(got, ref, dim=-1)
+    ok = (pos_err < 0.03 * scale + 1e-3) & (cos > 0.999)
+    if cfg.is_moe:
+        # bf16 rounding can flip a top-2 expert choice at a near-tie (the same happens
+        # with the CPU reference in bf16): allow a few positions to route differently
+        assert ok.float().mean() >= 0.93, (pos_err.max(), ok.float().mean())
+    else:
+        assert bool(ok.all()), (pos_err.max().item(), scale, cos.min().item())
+
+
+def _tiny_engine(**kw):
+    PRESETS.setdefault("llama-3-8b-2l", PRESETS["llama-3-8b"].shrink(name="llama-3-8b-2l",
+                                                                     num_layers=2))
+    base = dict(model="llama-3-8b-2l", random_init=True, max_model_len=1024, max_num_seqs=16,
+                max_num_batched_tokens=2048, num_gpu_blocks_override=512, cuda_graph_max_bs=16)
+    base.update(kw)
+    return LLMEngine(EngineConfig(**base))
+
+
+def _run(eng, prompts, params):
+    seqs = [eng.add_request(p, sp) for p, sp in zip(prompts, params)]
+    while eng.has_unfinished():
+        eng.step()
+    return [s.output_token_ids for s in seqs]
+
+
+def test_graph_equals_eager_and_async_equals_sync(gpu):
+    g = torch.Generator().manual_seed(1)
+    prompts = [torch.randint(100, 128000, (n,), generator=g).tolist() for n in (5, 77, 300, 1)]
+    params = [SamplingParams(temperature=1.0, seed=i, max_tokens=12, ignore_eos=True)
+              for i in range(len(prompts))]
+    outs = {}
+    for eager in (True, False):
+        for am in (False, True):
+            eng = _tiny_engine(enforce_eager=eager, async_output=am)
+            outs[(eager, am)] = _run(eng, prompts, params)
+            if not eager:
+                assert eng.executor.runner.stats["graph_steps"] > 0
+            del eng
+            torch.cuda.empty_cache()
+    base = outs[(True, False)]
+    for k, v in outs.items():
+        # sampling noise is counter-based, so identical logits give identical tokens;
+        # hipBLASLt may pick a different kernel for a padded graph bucket, so allow a
+        # rare late divergence but require the first tokens to agree
+        for a, b in zip(v, base):
+            assert len(a) == len(b) == 12
+            assert a[:4] == b[:4], (k, a, b)
+
+
+def test_engine_preemption_recompute(gpu):
+    """A KV pool too small for the batch forces recompute preemption; every request
+    still completes with the requested length."""
+    eng = _tiny_engine(num_gpu_blocks_override=40, max_num_seqs=8, block_size=32)
+    g = torch.Generator().manual_seed(2)
+    prompts = [torch.randint(100, 128000, (200,), generator=g).tolist() for _ in range(8)]
+    params = [SamplingParams(max_tokens=60, ignore_eos=True, seed=i) for i in range(8)]
+    outs = _run(eng, prompts, params)
+    assert all(len(o) == 60 for o in outs)
+    assert eng.scheduler.num_preemptions > 0
+    assert eng.bm.num_free == eng.bm.num_blocks - 1

@@ -54,7 +54,7 @@ def test_silu_mul(gpu, dt):
 
 def _cache(nb, nkv, bs, d, dt, dev):
     kc = torch.zeros(nb, nkv, bs, d, dtype=dt, device=dev)
-    vc = torch.zeros(nb, nkv, d, bs, dtype=dt, device=dev)
+    vc = torch.zeros(nb, nkv, bs // 8, d, 8, dtype=dt, device=dev)
     return kc, vc
 
 
@@ -85,7 +85,7 @@ def _fill_random_cache(B, ctx_lens, nkv, bs, d, dt, dev, nb_extra=7):
     max_blocks = max(math.ceil(c / bs) for c in ctx_lens) + 1
     nb = sum(math.ceil(c / bs) for c in ctx_lens) + nb_extra
     kc = (torch.randn(nb, nkv, bs, d, device=dev) * 0.5).to(dt)
-    vc = torch.randn(nb, nkv, d, bs, device=dev).to(dt)
+    vc = torch.randn(nb, nkv, bs // 8, d, 8, device=dev).to(dt)
     perm = torch.randperm(nb).tolist()
     bt = torch.zeros(B, max_blocks, dtype=torch.int32)
     k = 0

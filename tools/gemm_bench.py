@@ -1,0 +1,73 @@
+"""Microbenchmark the projection GEMM shapes of the decode / prefill steps.
+
+    python tools/gemm_bench.py [--model llama-3-8b] [--ms 1,16,64,128,256,512] [--tunableop]
+
+Reports per shape: time, weight-streaming TB/s and TFLOP/s for F.linear
+(hipBLASLt) -- the baseline the hand-written decode GEMM must beat.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def shapes(model):
+    from kubernetes_gpu_cluster_amd.models.configs import PRESETS
+    c = PRESETS[model]
+    H, I, d = c.hidden_size, c.intermediate_size, c.head_dim
+    return {"qkv": ((c.num_heads + 2 * c.num_kv_heads) * d, H), "o": (H, c.num_heads * d),
+            "gate_up": (2 * I, H), "down": (H, I), "lm_head": (c.vocab_size, H)}
+
+
+def bench(fn, iters=50):
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    g.replay()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama-3-8b")
+    ap.add_argument("--ms", default="1,16,64,128,256,512,4096")
+    ap.add_argument("--backend", default="hipblaslt")
+    ap.add_argument("--custom", action="store_true", help="also time kgc.decode_gemm")
+    a = ap.parse_args()
+    if a.backend != "hipblaslt":
+        torch.backends.cuda.preferred_blas_library(a.backend)
+    dev = torch.device("cuda")
+    res = []
+    for name, (N, K) in shapes(a.model).items():
+        w = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
+        for M in [int(x) for x in a.ms.split(",")]:
+            x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+            t = bench(lambda: F.linear(x, w))
+            row = {"shape": name, "M": M, "N": N, "K": K, "backend": a.backend,
+                   "us": round(t * 1e6, 2), "w_TBps": round(N * K * 2 / t / 1e12, 2),
+                   "TFLOPs": round(2 * M * N * K / t / 1e12, 1)}
+            if a.custom:
+                from kubernetes_gpu_cluster_amd import ops
+                if ops.decode_gemm_supported(M, N, K):
+                    tc = bench(lambda: ops.decode_gemm(x, w))
+                    row["custom_us"] = round(tc * 1e6, 2)
+                    row["custom_TBps"] = round(N * K * 2 / tc / 1e12, 2)
+            print(json.dumps(row), flush=True)
+            res.append(row)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,63 @@
+"""Summarise a rocprofv3 kernel trace of a bench run.
+
+    python tools/trace_summary.py gpurun_out/prof2/runc/<pid>_kernel_trace.csv [--steps]
+
+Prints the per-kernel totals and, with --steps, the steady-state decode-step
+anatomy: per step (delimited by the sampler kernel) the span, GPU-busy time,
+host gap and the busy time per kernel family.
+"""
+import collections
+import csv
+import statistics
+import sys
+
+
+def family(name: str) -> str:
+    n = name
+    if "Cijk" in n or "gemm" in n.lower():
+        return "gemm(hipblaslt)"
+    for k in ("decode_gemm", "paged_decode_reduce", "paged_decode", "prefill_attn", "rms_norm",
+              "silu_mul", "rope_kv", "sample_kernel", "layer_norm", "allreduce", "nccl", "rccl"):
+        if k in n:
+            return k
+    return n[:60]
+
+
+def main():
+    path = sys.argv[1]
+    rows = list(csv.DictReader(open(path)))
+    ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
+    tot = collections.Counter()
+    cnt = collections.Counter()
+    for s, e, n in ev:
+        tot[family(n)] += e - s
+        cnt[family(n)] += 1
+    T = sum(tot.values())
+    print(f"{'family':40} {'ms':>9} {'%':>6} {'calls':>7}")
+    for k, v in tot.most_common(20):
+        print(f"{k:40} {v / 1e6:9.2f} {100 * v / T:6.1f} {cnt[k]:7}")
+    if "--steps" in sys.argv:
+        samp = [i for i, (s, e, n) in enumerate(ev) if "sample_kernel" in n]
+        steps = []
+        for a, b in zip(samp, samp[1:]):
+            seg = ev[a + 1:b + 1]
+            span = seg[-1][1] - ev[a][1]
+            busy = sum(e - s for s, e, n in seg)
+            fam = collections.Counter()
+            for s, e, n in seg:
+                fam[family(n)] += e - s
+            steps.append((span, busy, len(seg), fam))
+        nk = statistics.median([s[2] for s in steps])
+        dec = [s for s in steps if s[2] == nk]
+        print(f"\ndecode steps (kernels/step={nk}): {len(dec)}")
+        print(f"median span {statistics.median([s[0] for s in dec]) / 1e6:.3f} ms, "
+              f"busy {statistics.median([s[1] for s in dec]) / 1e6:.3f} ms")
+        agg = collections.Counter()
+        for s in dec:
+            agg.update(s[3])
+        for k, v in agg.most_common(12):
+            print(f"   {k:38} {v / len(dec) / 1e3:9.1f} us/step")
+
+
+if __name__ == "__main__":
+    main()
