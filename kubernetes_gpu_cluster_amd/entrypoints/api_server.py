@@ -1,0 +1,287 @@
+"""OpenAI-compatible HTTP server for the engine (the reference's serving pods run
+``vllm serve``).
+
+Routes: ``POST /v1/completions``, ``POST /v1/chat/completions`` (both with SSE
+streaming), ``GET /v1/models``, ``GET /health`` (liveness/readiness probes),
+``GET /metrics`` (Prometheus), ``GET /version``.
+
+    python -m kubernetes_gpu_cluster_amd.entrypoints.api_server --model llama-3-8b \\
+        --random-init --host 0.0.0.0 --port 8000 [--tensor-parallel-size 8 ...]
+
+Every engine flag of ``engine.config.add_engine_args`` is accepted, including
+the reference values files' ``extraArgs`` (``--dtype float16``,
+``--disable-custom-all-reduce``, ``--enforce-eager``, ``--trust-remote-code``, ...).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import time
+import uuid
+from typing import Any, Optional, Union
+
+from fastapi import FastAPI, Request
+from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
+from prometheus_client import generate_latest
+from pydantic import BaseModel, ConfigDict, Field
+
+from .. import __version__
+from ..engine.config import EngineConfig, add_engine_args, config_from_args
+from ..engine.sequence import SamplingParams
+from ..utils.tokenizer import get_tokenizer
+from .async_engine import AsyncLLMEngine, EngineDeadError
+
+log = logging.getLogger("kgc.api")
+
+
+class _Lenient(BaseModel):
+    model_config = ConfigDict(extra="allow")
+
+
+class CompletionRequest(_Lenient):
+    model: Optional[str] = None
+    prompt: Union[str, list[str], list[int], list[list[int]]]
+    max_tokens: Optional[int] = 16
+    temperature: Optional[float] = 1.0
+    top_p: Optional[float] = 1.0
+    top_k: Optional[int] = -1
+    n: int = 1
+    stream: bool = False
+    stop: Optional[Union[str, list[str]]] = None
+    stop_token_ids: Optional[list[int]] = None
+    seed: Optional[int] = None
+    ignore_eos: bool = False
+    min_tokens: int = 0
+    echo: bool = False
+    logprobs: Optional[int] = None
+    user: Optional[str] = None
+
+
+class ChatMessage(_Lenient):
+    role: str
+    content: Union[str, list[dict[str, Any]], None] = ""
+
+
+class ChatCompletionRequest(_Lenient):
+    model: Optional[str] = None
+    messages: list[ChatMessage]
+    max_tokens: Optional[int] = None
+    max_completion_tokens: Optional[int] = None
+    temperature: Optional[float] = 1.0
+    top_p: Optional[float] = 1.0
+    top_k: Optional[int] = -1
+    n: int = 1
+    stream: bool = False
+    stop: Optional[Union[str, list[str]]] = None
+    stop_token_ids: Optional[list[int]] = None
+    seed: Optional[int] = None
+    ignore_eos: bool = False
+    min_tokens: int = 0
+    user: Optional[str] = None
+
+
+def _err(status: int, msg: str, typ: str = "invalid_request_error") -> JSONResponse:
+    return JSONResponse({"object": "error", "message": msg, "type": typ, "code": status},
+                        status_code=status)
+
+
+class _Detok:
+    """Incremental detokenizer with stop-string truncation."""
+
+    def __init__(self, tok, stops: list[str]):
+        self.tok, self.stops = tok, [s for s in stops if s]
+        self.text = ""
+        self.stopped = False
+
+    def update(self, ids: list[int]) -> str:
+        full = self.tok.decode(ids)
+        for s in self.stops:
+            i = full.find(s)
+            if i >= 0:
+                full = full[:i]
+                self.stopped = True
+        delta = full[len(self.text):] if full.startswith(self.text) else full
+        self.text = full
+        return delta
+
+
+def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len: int) -> FastAPI:
+    app = FastAPI(title="kgc OpenAI-compatible server", version=__version__)
+    created = int(time.time())
+
+    def params_from(req, max_tokens: Optional[int]) -> SamplingParams:
+        stops = req.stop if isinstance(req.stop, list) else ([req.stop] if req.stop else [])
+        return SamplingParams(temperature=req.temperature if req.temperature is not None else 1.0,
+                              top_p=req.top_p if req.top_p is not None else 1.0,
+                              top_k=req.top_k if req.top_k not in (None, 0) else -1,
+                              max_tokens=max_tokens, min_tokens=req.min_tokens,
+                              stop_token_ids=list(req.stop_token_ids or []), stop=stops,
+                              ignore_eos=req.ignore_eos, seed=req.seed, n=req.n)
+
+    async def run(ids: list[int], sp: SamplingParams, rid: str, stream_fn, final_fn, stream: bool):
+        detok = _Detok(tokenizer, sp.stop)
+        gen = engine.generate(ids, sp, rid)
+        if stream:
+            async def sse():
+                try:
+                    async for out in gen:
+                        delta = detok.update(out.output_token_ids)
+                        reason = out.finish_reason if out.finished else None
+                        if detok.stopped:
+                            reason = "stop"
+                        if delta or reason:
+                            yield f"data: {json.dumps(stream_fn(delta, reason))}\n\n"
+                        if detok.stopped:
+                            await gen.aclose()
+                            break
+                except EngineDeadError as e:
+                    yield f"data: {json.dumps({'error': str(e)})}\n\n"
+                yield "data: [DONE]\n\n"
+            return StreamingResponse(sse(), media_type="text/event-stream")
+        last = None
+        async for out in gen:
+            last = out
+            detok.update(out.output_token_ids)
+            if detok.stopped:
+                await gen.aclose()
+                break
+        reason = "stop" if detok.stopped else (last.finish_reason if last else None)
+        return JSONResponse(final_fn(detok.text, reason, len(ids),
+                                     len(last.output_token_ids) if last else 0))
+
+    def prompt_ids(p) -> list[int]:
+        return tokenizer.encode(p) if isinstance(p, str) else [int(x) for x in p]
+
+    @app.post("/v1/completions")
+    async def completions(req: CompletionRequest):
+        if req.n != 1:
+            return _err(400, "only n=1 is supported")
+        prompts = req.prompt
+        if isinstance(prompts, list) and prompts and isinstance(prompts[0], (str, list)):
+            if len(prompts) != 1:
+                return _err(400, "batched prompts: send one request per prompt")
+            prompts = prompts[0]
+        ids = prompt_ids(prompts)
+        if len(ids) >= max_model_len:
+            return _err(400, f"prompt has {len(ids)} tokens; max_model_len is {max_model_len}")
+        try:
+            sp = params_from(req, req.max_tokens)
+        except ValueError as e:
+            return _err(400, str(e))
+        rid = f"cmpl-{uuid.uuid4().hex}"
+        prefix = (prompts if isinstance(prompts, str) else tokenizer.decode(ids)) if req.echo else ""
+
+        def chunk(delta, reason):
+            return {"id": rid, "object": "text_completion", "created": int(time.time()),
+                    "model": served_name,
+                    "choices": [{"index": 0, "text": delta, "logprobs": None,
+                                 "finish_reason": reason}]}
+
+        def final(text, reason, np_, nc):
+            return {"id": rid, "object": "text_completion", "created": int(time.time()),
+                    "model": served_name,
+                    "choices": [{"index": 0, "text": prefix + text, "logprobs": None,
+                                 "finish_reason": reason}],
+                    "usage": {"prompt_tokens": np_, "completion_tokens": nc,
+                              "total_tokens": np_ + nc}}
+        try:
+            return await run(ids, sp, rid, chunk, final, req.stream)
+        except EngineDeadError as e:
+            return _err(503, f"engine unavailable: {e}", "server_error")
+        except ValueError as e:
+            return _err(400, str(e))
+
+    @app.post("/v1/chat/completions")
+    async def chat(req: ChatCompletionRequest):
+        if req.n != 1:
+            return _err(400, "only n=1 is supported")
+        msgs = []
+        for m in req.messages:
+            c = m.content
+            if isinstance(c, list):
+                c = "".join(p.get("text", "") for p in c if isinstance(p, dict))
+            msgs.append({"role": m.role, "content": c or ""})
+        text = tokenizer.apply_chat_template(msgs, add_generation_prompt=True)
+        ids = tokenizer.encode(text)
+        if len(ids) >= max_model_len:
+            return _err(400, f"prompt has {len(ids)} tokens; max_model_len is {max_model_len}")
+        try:
+            sp = params_from(req, req.max_completion_tokens or req.max_tokens)
+        except ValueError as e:
+            return _err(400, str(e))
+        rid = f"chatcmpl-{uuid.uuid4().hex}"
+        first = [True]
+
+        def chunk(delta, reason):
+            d = {"content": delta}
+            if first[0]:
+                d["role"] = "assistant"
+                first[0] = False
+            return {"id": rid, "object": "chat.completion.chunk", "created": int(time.time()),
+                    "model": served_name,
+                    "choices": [{"index": 0, "delta": d, "finish_reason": reason}]}
+
+        def final(text, reason, np_, nc):
+            return {"id": rid, "object": "chat.completion", "created": int(time.time()),
+                    "model": served_name,
+                    "choices": [{"index": 0, "message": {"role": "assistant", "content": text},
+                                 "finish_reason": reason}],
+                    "usage": {"prompt_tokens": np_, "completion_tokens": nc,
+                              "total_tokens": np_ + nc}}
+        try:
+            return await run(ids, sp, rid, chunk, final, req.stream)
+        except EngineDeadError as e:
+            return _err(503, f"engine unavailable: {e}", "server_error")
+        except ValueError as e:
+            return _err(400, str(e))
+
+    @app.get("/v1/models")
+    async def models():
+        return {"object": "list", "data": [{"id": served_name, "object": "model",
+                                            "created": created, "owned_by": "kgc",
+                                            "max_model_len": max_model_len}]}
+
+    @app.get("/health")
+    async def health():
+        if not engine.is_alive:
+            return PlainTextResponse("engine dead", status_code=503)
+        return PlainTextResponse("ok")
+
+    @app.get("/metrics")
+    async def metrics():
+        return PlainTextResponse(generate_latest(engine.engine.metrics.registry).decode(),
+                                 media_type="text/plain; version=0.0.4")
+
+    @app.get("/version")
+    async def version():
+        return {"version": __version__}
+
+    return app
+
+
+def make_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description="kgc OpenAI-compatible server")
+    p.add_argument("model_tag", nargs="?", default=None, help="model (positional, like vllm serve)")
+    p.add_argument("--host", default="0.0.0.0")
+    p.add_argument("--port", type=int, default=8000)
+    p.add_argument("--uvicorn-log-level", default="info")
+    add_engine_args(p)
+    return p
+
+
+def main(argv=None) -> None:
+    import uvicorn
+    ns = make_parser().parse_args(argv)
+    ns.model = ns.model or ns.model_tag or "llama-3-8b"
+    cfg = config_from_args(ns)
+    logging.basicConfig(level=logging.INFO)
+    eng = AsyncLLMEngine(cfg)
+    tok = get_tokenizer(cfg.model, eng.engine.mcfg, cfg.tokenizer)
+    name = cfg.served_model_name or cfg.model
+    app = build_app(eng, tok, name, eng.engine.max_model_len)
+    uvicorn.run(app, host=ns.host, port=ns.port, log_level=ns.uvicorn_log_level)
+
+
+if __name__ == "__main__":
+    main()

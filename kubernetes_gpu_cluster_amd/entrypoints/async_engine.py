@@ -1,0 +1,119 @@
+"""Thread-backed async facade over LLMEngine for the HTTP server.
+
+The engine loop (schedule -> execute -> update) runs on one background thread;
+request submission, abort and per-request output streams cross to the asyncio
+loop through thread-safe queues (``loop.call_soon_threadsafe``).  GPU waits in the
+engine release the GIL, so the HTTP event loop keeps serving while a step runs.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import queue
+import threading
+import time
+import traceback
+from typing import AsyncIterator, Optional
+
+from ..engine.config import EngineConfig
+from ..engine.llm_engine import LLMEngine
+from ..engine.sequence import RequestOutput, SamplingParams
+
+log = logging.getLogger("kgc.async_engine")
+
+
+class EngineDeadError(RuntimeError):
+    pass
+
+
+class AsyncLLMEngine:
+    def __init__(self, cfg: EngineConfig, engine: Optional[LLMEngine] = None):
+        self.cfg = cfg
+        self.engine = engine or LLMEngine(cfg)
+        self._new: queue.Queue = queue.Queue()
+        self._aborts: queue.Queue = queue.Queue()
+        self._streams: dict[str, tuple[asyncio.AbstractEventLoop, asyncio.Queue]] = {}
+        self._wake = threading.Event()
+        self._stop = False
+        self.error: Optional[BaseException] = None
+        self.last_step_time = time.monotonic()
+        self._thread = threading.Thread(target=self._loop, name="kgc-engine", daemon=True)
+        self._thread.start()
+
+    # ------------------------------------------------------------------ engine thread
+    def _push(self, rid: str, item) -> None:
+        ent = self._streams.get(rid)
+        if ent is not None:
+            loop, q = ent
+            loop.call_soon_threadsafe(q.put_nowait, item)
+
+    def _loop(self) -> None:
+        eng = self.engine
+        try:
+            while not self._stop:
+                while True:
+                    try:
+                        rid, ids, params, t = self._new.get_nowait()
+                    except queue.Empty:
+                        break
+                    try:
+                        eng.add_request(ids, params, request_id=rid, arrival_time=t)
+                    except Exception as e:  # noqa: BLE001 - reported to the request
+                        self._push(rid, e)
+                while True:
+                    try:
+                        rid = self._aborts.get_nowait()
+                    except queue.Empty:
+                        break
+                    eng.abort(rid)
+                if eng.has_unfinished():
+                    for o in eng.step():
+                        self._push(o.request_id, o)
+                    self.last_step_time = time.monotonic()
+                else:
+                    self._wake.wait(0.05)
+                    self._wake.clear()
+        except BaseException as e:  # noqa: BLE001
+            self.error = e
+            log.error("engine loop died: %s", traceback.format_exc())
+            for rid in list(self._streams):
+                self._push(rid, EngineDeadError(str(e)))
+
+    # ------------------------------------------------------------------ asyncio side
+    @property
+    def is_alive(self) -> bool:
+        return self._thread.is_alive() and self.error is None
+
+    async def generate(self, prompt_ids: list[int], params: SamplingParams,
+                       request_id: str) -> AsyncIterator[RequestOutput]:
+        if not self.is_alive:
+            raise EngineDeadError(str(self.error))
+        loop = asyncio.get_running_loop()
+        q: asyncio.Queue = asyncio.Queue()
+        self._streams[request_id] = (loop, q)
+        self._new.put((request_id, prompt_ids, params, time.monotonic()))
+        self._wake.set()
+        finished = False
+        try:
+            while True:
+                item = await q.get()
+                if isinstance(item, BaseException):
+                    raise item
+                yield item
+                if item.finished:
+                    finished = True
+                    return
+        finally:
+            self._streams.pop(request_id, None)
+            if not finished:
+                self.abort(request_id)
+
+    def abort(self, request_id: str) -> None:
+        self._aborts.put(request_id)
+        self._wake.set()
+
+    def shutdown(self) -> None:
+        self._stop = True
+        self._wake.set()
+        self._thread.join(timeout=30)
+        self.engine.shutdown()

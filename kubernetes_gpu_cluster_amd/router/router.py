@@ -1,0 +1,313 @@
+"""Request router in front of the engine pods (the reference's production-stack
+router behind ``svc/vllm-router-service`` port 80; ``old_README.md:1175,1473-1476``).
+
+* Backend discovery: a static list (``--backends``), Kubernetes pod discovery
+  through the API server (``--k8s-label-selector``, in-cluster service-account
+  credentials; pods labelled ``app.kubernetes.io/component=serving-engine`` by the
+  chart), or DNS of a headless Service (``--dns-service``).
+* Model-aware routing: each backend's ``/v1/models`` is polled; a request goes to
+  a healthy backend serving its ``model`` (any backend if unspecified).
+* Policies: ``least-outstanding`` (default), ``round-robin``, ``session`` (sticky by
+  the ``x-session-id`` header / ``user`` field, consistent hashing).
+* Failure handling: periodic ``/health`` probes eject unhealthy backends; a
+  connection error or 5xx before any byte was relayed is retried on another
+  backend (failover); SSE streams are relayed chunk by chunk.
+* ``/v1/models`` (union), ``/health``, ``/metrics`` (router Prometheus metrics).
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import bisect
+import hashlib
+import itertools
+import json
+import logging
+import os
+import ssl
+import time
+from typing import Optional
+
+import aiohttp
+from aiohttp import web
+from prometheus_client import CollectorRegistry, Counter, Gauge, Histogram, generate_latest
+
+log = logging.getLogger("kgc.router")
+
+SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+
+
+class Backend:
+    def __init__(self, url: str):
+        self.url = url.rstrip("/")
+        self.healthy = True
+        self.outstanding = 0
+        self.models: set[str] = set()
+        self.fails = 0
+        self.last_ok = 0.0
+
+    def __repr__(self):
+        return f"Backend({self.url}, healthy={self.healthy}, out={self.outstanding})"
+
+
+class Router:
+    def __init__(self, backends: list[str], policy: str = "least-outstanding",
+                 health_interval: float = 5.0, fail_threshold: int = 2,
+                 k8s_selector: Optional[str] = None, k8s_namespace: Optional[str] = None,
+                 k8s_port: int = 8000, dns_service: Optional[str] = None, max_retries: int = 2,
+                 request_timeout: float = 3600.0):
+        self.backends: dict[str, Backend] = {u.rstrip("/"): Backend(u) for u in backends}
+        self.policy = policy
+        self.health_interval = health_interval
+        self.fail_threshold = fail_threshold
+        self.k8s_selector, self.k8s_namespace, self.k8s_port = k8s_selector, k8s_namespace, k8s_port
+        self.dns_service = dns_service
+        self.max_retries = max_retries
+        self.timeout = aiohttp.ClientTimeout(total=request_timeout, sock_connect=5)
+        self._rr = itertools.count()
+        self.session: Optional[aiohttp.ClientSession] = None
+        self._tasks: list[asyncio.Task] = []
+        r = self.registry = CollectorRegistry()
+        self.m_req = Counter("kgc_router_requests", "requests", ["backend", "status"], registry=r)
+        self.m_lat = Histogram("kgc_router_request_seconds", "latency", ["route"], registry=r)
+        self.m_out = Gauge("kgc_router_outstanding", "in-flight per backend", ["backend"], registry=r)
+        self.m_healthy = Gauge("kgc_router_healthy_backends", "healthy backends", registry=r)
+        self.m_retry = Counter("kgc_router_retries", "failover retries", registry=r)
+
+    # ------------------------------------------------------------------ lifecycle
+    async def start(self, app=None):
+        self.session = aiohttp.ClientSession(timeout=self.timeout)
+        await self.refresh_discovery()
+        await self.check_health()
+        self._tasks.append(asyncio.create_task(self._health_loop()))
+
+    async def stop(self, app=None):
+        for t in self._tasks:
+            t.cancel()
+        if self.session:
+            await self.session.close()
+
+    async def _health_loop(self):
+        while True:
+            await asyncio.sleep(self.health_interval)
+            try:
+                await self.refresh_discovery()
+                await self.check_health()
+            except Exception as e:  # noqa: BLE001
+                log.warning("health loop: %s", e)
+
+    # ------------------------------------------------------------------ discovery
+    async def refresh_discovery(self):
+        urls = None
+        if self.k8s_selector:
+            urls = await self._k8s_pods()
+        elif self.dns_service:
+            urls = await self._dns()
+        if urls is None:
+            return
+        for u in urls:
+            self.backends.setdefault(u, Backend(u))
+        for u in list(self.backends):
+            if u not in urls:
+                del self.backends[u]
+
+    async def _k8s_pods(self) -> Optional[list[str]]:
+        host = os.environ.get("KUBERNETES_SERVICE_HOST")
+        if not host or not os.path.exists(f"{SA_DIR}/token"):
+            return None
+        port = os.environ.get("KUBERNETES_SERVICE_PORT", "443")
+        ns = self.k8s_namespace or open(f"{SA_DIR}/namespace").read().strip()
+        token = open(f"{SA_DIR}/token").read().strip()
+        ctx = ssl.create_default_context(cafile=f"{SA_DIR}/ca.crt")
+        url = f"https://{host}:{port}/api/v1/namespaces/{ns}/pods"
+        async with self.session.get(url, params={"labelSelector": self.k8s_selector},
+                                    headers={"Authorization": f"Bearer {token}"}, ssl=ctx) as r:
+            data = await r.json()
+        return pods_to_urls(data, self.k8s_port)
+
+    async def _dns(self) -> Optional[list[str]]:
+        host, _, port = self.dns_service.partition(":")
+        loop = asyncio.get_running_loop()
+        try:
+            infos = await loop.getaddrinfo(host, int(port or 8000))
+        except OSError:
+            return []
+        return sorted({f"http://{i[4][0]}:{i[4][1]}" for i in infos})
+
+    # ------------------------------------------------------------------ health
+    async def _probe(self, b: Backend):
+        try:
+            async with self.session.get(b.url + "/health", timeout=aiohttp.ClientTimeout(total=3)) as r:
+                ok = r.status == 200
+            if ok and not b.models:
+                async with self.session.get(b.url + "/v1/models",
+                                            timeout=aiohttp.ClientTimeout(total=3)) as r:
+                    if r.status == 200:
+                        b.models = {m["id"] for m in (await r.json()).get("data", [])}
+        except Exception:  # noqa: BLE001
+            ok = False
+        if ok:
+            b.fails, b.healthy, b.last_ok = 0, True, time.monotonic()
+        else:
+            b.fails += 1
+            if b.fails >= self.fail_threshold:
+                b.healthy = False
+
+    async def check_health(self):
+        await asyncio.gather(*(self._probe(b) for b in list(self.backends.values())))
+        self.m_healthy.set(sum(b.healthy for b in self.backends.values()))
+
+    # ------------------------------------------------------------------ selection
+    def candidates(self, model: Optional[str]) -> list[Backend]:
+        hs = [b for b in self.backends.values() if b.healthy]
+        if model:
+            m = [b for b in hs if not b.models or model in b.models]
+            if m:
+                return m
+        return hs
+
+    def pick(self, model: Optional[str], session_key: Optional[str] = None,
+             exclude: set = frozenset()) -> Optional[Backend]:
+        cs = [b for b in self.candidates(model) if b.url not in exclude]
+        if not cs:
+            return None
+        if self.policy == "round-robin":
+            return cs[next(self._rr) % len(cs)]
+        if self.policy == "session" and session_key:
+            return consistent_pick(cs, session_key)
+        lo = min(b.outstanding for b in cs)
+        ties = [b for b in cs if b.outstanding == lo]
+        return ties[next(self._rr) % len(ties)]
+
+    # ------------------------------------------------------------------ proxy
+    async def proxy(self, request: web.Request) -> web.StreamResponse:
+        t0 = time.monotonic()
+        body = await request.read()
+        model = skey = None
+        try:
+            j = json.loads(body) if body else {}
+            model = j.get("model")
+            skey = request.headers.get("x-session-id") or j.get("user")
+        except (ValueError, AttributeError):
+            pass
+        tried: set = set()
+        for attempt in range(self.max_retries + 1):
+            b = self.pick(model, skey, tried)
+            if b is None:
+                return web.json_response({"error": "no healthy backend" + (f" for model {model}" if model else "")},
+                                         status=503)
+            tried.add(b.url)
+            b.outstanding += 1
+            self.m_out.labels(b.url).set(b.outstanding)
+            resp: Optional[web.StreamResponse] = None
+            try:
+                hdrs = {k: v for k, v in request.headers.items()
+                        if k.lower() not in ("host", "content-length", "transfer-encoding")}
+                async with self.session.request(request.method, b.url + request.path_qs,
+                                                data=body, headers=hdrs) as up:
+                    if up.status >= 500 and attempt < self.max_retries:
+                        b.fails += 1
+                        self.m_req.labels(b.url, str(up.status)).inc()
+                        self.m_retry.inc()
+                        continue
+                    resp = web.StreamResponse(status=up.status, headers={
+                        k: v for k, v in up.headers.items()
+                        if k.lower() in ("content-type", "cache-control")})
+                    await resp.prepare(request)
+                    async for chunk in up.content.iter_any():
+                        await resp.write(chunk)
+                    await resp.write_eof()
+                    self.m_req.labels(b.url, str(up.status)).inc()
+                    self.m_lat.labels(request.path).observe(time.monotonic() - t0)
+                    return resp
+            except (aiohttp.ClientConnectionError, asyncio.TimeoutError) as e:
+                self.m_req.labels(b.url, "conn_error").inc()
+                b.fails += 1
+                if b.fails >= self.fail_threshold:
+                    b.healthy = False
+                if resp is not None:       # bytes already relayed: cannot fail over
+                    return resp
+                self.m_retry.inc()
+                log.warning("backend %s failed (%s); failing over", b.url, e)
+            finally:
+                b.outstanding -= 1
+                self.m_out.labels(b.url).set(b.outstanding)
+        return web.json_response({"error": "all backends failed"}, status=502)
+
+    async def models(self, request: web.Request) -> web.Response:
+        seen, data = set(), []
+        for b in self.backends.values():
+            if not b.healthy:
+                continue
+            for m in sorted(b.models):
+                if m not in seen:
+                    seen.add(m)
+                    data.append({"id": m, "object": "model", "owned_by": "kgc"})
+        return web.json_response({"object": "list", "data": data})
+
+    async def health(self, request: web.Request) -> web.Response:
+        n = sum(b.healthy for b in self.backends.values())
+        return web.Response(text=f"ok ({n} healthy backends)", status=200 if n else 503)
+
+    async def metrics(self, request: web.Request) -> web.Response:
+        return web.Response(body=generate_latest(self.registry), content_type="text/plain")
+
+    def app(self) -> web.Application:
+        a = web.Application(client_max_size=64 << 20)
+        a.router.add_get("/v1/models", self.models)
+        a.router.add_get("/health", self.health)
+        a.router.add_get("/metrics", self.metrics)
+        a.router.add_route("*", "/v1/{tail:.*}", self.proxy)
+        a.on_startup.append(self.start)
+        a.on_cleanup.append(self.stop)
+        return a
+
+
+def pods_to_urls(pod_list: dict, port: int) -> list[str]:
+    """Ready, running pods with an IP -> base URLs."""
+    urls = []
+    for p in pod_list.get("items", []):
+        st = p.get("status", {})
+        if st.get("phase") != "Running" or not st.get("podIP"):
+            continue
+        conds = {c.get("type"): c.get("status") for c in st.get("conditions", [])}
+        if conds.get("Ready") == "False":
+            continue
+        urls.append(f"http://{st['podIP']}:{port}")
+    return sorted(urls)
+
+
+def consistent_pick(backends: list[Backend], key: str, vnodes: int = 64) -> Backend:
+    ring = []
+    for b in backends:
+        for v in range(vnodes):
+            h = int.from_bytes(hashlib.md5(f"{b.url}#{v}".encode()).digest()[:8], "big")
+            ring.append((h, b))
+    ring.sort(key=lambda x: x[0])
+    h = int.from_bytes(hashlib.md5(key.encode()).digest()[:8], "big")
+    i = bisect.bisect([r[0] for r in ring], h)
+    return ring[i % len(ring)][1]
+
+
+def main(argv=None):
+    p = argparse.ArgumentParser(description="kgc request router")
+    p.add_argument("--host", default="0.0.0.0")
+    p.add_argument("--port", type=int, default=8080)
+    p.add_argument("--backends", default="", help="comma-separated engine base URLs")
+    p.add_argument("--k8s-label-selector", default=None)
+    p.add_argument("--k8s-namespace", default=None)
+    p.add_argument("--k8s-port", type=int, default=8000)
+    p.add_argument("--dns-service", default=None, help="headless service host[:port]")
+    p.add_argument("--routing-logic", "--policy", dest="policy", default="least-outstanding",
+                   choices=["least-outstanding", "round-robin", "session"])
+    p.add_argument("--health-interval", type=float, default=5.0)
+    a = p.parse_args(argv)
+    logging.basicConfig(level=logging.INFO)
+    r = Router([u for u in a.backends.split(",") if u], a.policy, a.health_interval,
+               k8s_selector=a.k8s_label_selector, k8s_namespace=a.k8s_namespace,
+               k8s_port=a.k8s_port, dns_service=a.dns_service)
+    web.run_app(r.app(), host=a.host, port=a.port)
+
+
+if __name__ == "__main__":
+    main()

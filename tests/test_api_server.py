@@ -1,0 +1,71 @@
+"""OpenAI API server: schema, SSE streaming, stop strings, health/metrics/models
+(CPU engine with a tiny random model)."""
+import json
+
+import pytest
+from fastapi.testclient import TestClient
+
+from kubernetes_gpu_cluster_amd.engine.config import EngineConfig
+from kubernetes_gpu_cluster_amd.entrypoints.api_server import build_app
+from kubernetes_gpu_cluster_amd.entrypoints.async_engine import AsyncLLMEngine
+from kubernetes_gpu_cluster_amd.utils.tokenizer import get_tokenizer
+
+
+@pytest.fixture(scope="module")
+def client():
+    cfg = EngineConfig(model="tiny-llama", random_init=True, max_model_len=256, max_num_seqs=8,
+                       max_num_batched_tokens=128, device="cpu", dtype="float32")
+    eng = AsyncLLMEngine(cfg)
+    tok = get_tokenizer(cfg.model, eng.engine.mcfg)
+    app = build_app(eng, tok, "tiny-llama", eng.engine.max_model_len)
+    with TestClient(app) as c:
+        yield c
+    eng.shutdown()
+
+
+def test_models_health_metrics(client):
+    r = client.get("/v1/models")
+    assert r.status_code == 200 and r.json()["data"][0]["id"] == "tiny-llama"
+    assert client.get("/health").text == "ok"
+    client.post("/v1/completions", json={"prompt": "hi", "max_tokens": 2})
+    m = client.get("/metrics").text
+    assert "vllm:generation_tokens_total" in m and "vllm:time_to_first_token_seconds" in m
+
+
+def test_completion(client):
+    r = client.post("/v1/completions", json={"prompt": "hello world", "max_tokens": 7,
+                                             "temperature": 0, "ignore_eos": True})
+    j = r.json()
+    assert r.status_code == 200, j
+    assert j["object"] == "text_completion"
+    assert j["usage"]["completion_tokens"] == 7
+    assert j["choices"][0]["finish_reason"] == "length"
+    # token-id prompt + seeded sampling is reproducible
+    body = {"prompt": [5, 6, 7, 8], "max_tokens": 5, "seed": 11, "ignore_eos": True}
+    a = client.post("/v1/completions", json=body).json()["choices"][0]["text"]
+    b = client.post("/v1/completions", json=body).json()["choices"][0]["text"]
+    assert a == b
+
+
+def test_chat_and_stream(client):
+    r = client.post("/v1/chat/completions", json={
+        "messages": [{"role": "user", "content": "hi"}], "max_tokens": 4, "ignore_eos": True})
+    j = r.json()
+    assert j["object"] == "chat.completion" and j["choices"][0]["message"]["role"] == "assistant"
+    with client.stream("POST", "/v1/chat/completions", json={
+            "messages": [{"role": "user", "content": "hi"}], "max_tokens": 6, "stream": True,
+            "ignore_eos": True}) as s:
+        lines = [l for l in s.iter_lines() if l]
+    assert lines[-1] == "data: [DONE]"
+    chunks = [json.loads(l[6:]) for l in lines[:-1]]
+    assert chunks[0]["choices"][0]["delta"].get("role") == "assistant"
+    assert chunks[-1]["choices"][0]["finish_reason"] == "length"
+
+
+def test_errors(client):
+    r = client.post("/v1/completions", json={"prompt": "x" * 600, "max_tokens": 2})
+    assert r.status_code == 400
+    r = client.post("/v1/completions", json={"prompt": "x", "temperature": -1})
+    assert r.status_code == 400
+    r = client.post("/v1/completions", json={"prompt": "x", "n": 2})
+    assert r.status_code == 400

@@ -1,0 +1,102 @@
+"""Router: discovery, model-aware least-outstanding routing, failover, SSE relay."""
+import asyncio
+import json
+
+from aiohttp import web
+from aiohttp.test_utils import TestClient, TestServer
+
+from kubernetes_gpu_cluster_amd.router.router import Router, consistent_pick, pods_to_urls, Backend
+
+
+def fake_engine(name: str, model: str = "m", fail: bool = False):
+    app = web.Application()
+    app["hits"] = 0
+
+    async def health(r):
+        return web.Response(text="ok")
+
+    async def models(r):
+        return web.json_response({"data": [{"id": model}]})
+
+    async def comp(r):
+        app["hits"] += 1
+        if fail:
+            return web.Response(status=500, text="boom")
+        body = await r.json()
+        if body.get("stream"):
+            resp = web.StreamResponse(headers={"content-type": "text/event-stream"})
+            await resp.prepare(r)
+            for i in range(3):
+                await resp.write(f"data: {json.dumps({'i': i, 'be': name})}\n\n".encode())
+            await resp.write(b"data: [DONE]\n\n")
+            await resp.write_eof()
+            return resp
+        return web.json_response({"backend": name, "model": body.get("model")})
+
+    app.router.add_get("/health", health)
+    app.router.add_get("/v1/models", models)
+    app.router.add_post("/v1/completions", comp)
+    return app
+
+
+async def _scenario():
+    servers = [TestServer(fake_engine("a", "m1")), TestServer(fake_engine("b", "m1")),
+               TestServer(fake_engine("c", "m2")), TestServer(fake_engine("bad", "m1", fail=True))]
+    for s in servers:
+        await s.start_server()
+    urls = [str(s.make_url("")) for s in servers]
+    r = Router(urls, health_interval=3600)
+    client = TestClient(TestServer(r.app()))
+    await client.start_server()
+    try:
+        # model union
+        j = await (await client.get("/v1/models")).json()
+        assert {m["id"] for m in j["data"]} == {"m1", "m2"}
+        # m2 only on c
+        for _ in range(3):
+            j = await (await client.post("/v1/completions", json={"model": "m2", "prompt": "x"})).json()
+            assert j["backend"] == "c"
+        # m1 spread over a, b (and 'bad' fails over)
+        seen = set()
+        for _ in range(12):
+            resp = await client.post("/v1/completions", json={"model": "m1", "prompt": "x"})
+            assert resp.status == 200
+            seen.add((await resp.json())["backend"])
+        assert seen == {"a", "b"}
+        assert r.m_retry._value.get() > 0
+        # SSE relay
+        resp = await client.post("/v1/completions", json={"model": "m1", "stream": True})
+        text = await resp.text()
+        assert text.count("data: ") == 4 and text.strip().endswith("[DONE]")
+        # a dead backend is ejected by health probes
+        await servers[0].close()
+        await r.check_health()
+        await r.check_health()
+        assert not r.backends[urls[0].rstrip("/")].healthy
+        for _ in range(4):
+            j = await (await client.post("/v1/completions", json={"model": "m1"})).json()
+            assert j["backend"] == "b"
+        h = await client.get("/health")
+        assert h.status == 200
+        m = await (await client.get("/metrics")).text()
+        assert "kgc_router_requests_total" in m
+    finally:
+        await client.close()
+        for s in servers:
+            await s.close()
+
+
+def test_router_end_to_end():
+    asyncio.run(_scenario())
+
+
+def test_pods_to_urls_and_consistent_hash():
+    pods = {"items": [
+        {"status": {"phase": "Running", "podIP": "10.0.0.2", "conditions": [{"type": "Ready", "status": "True"}]}},
+        {"status": {"phase": "Pending", "podIP": "10.0.0.3"}},
+        {"status": {"phase": "Running", "podIP": "10.0.0.4", "conditions": [{"type": "Ready", "status": "False"}]}},
+    ]}
+    assert pods_to_urls(pods, 8000) == ["http://10.0.0.2:8000"]
+    bs = [Backend(f"http://h{i}:1") for i in range(4)]
+    picks = {k: consistent_pick(bs, k).url for k in ("u1", "u2", "u3")}
+    assert picks == {k: consistent_pick(bs, k).url for k in picks}   # stable
