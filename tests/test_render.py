@@ -1,0 +1,151 @@
+"""values-*.yaml -> manifests renderer (SURVEY.md §2.7 schema) and Helm chart parity."""
+import glob
+import os
+
+import pytest
+import yaml
+from hypothesis import given, settings, strategies as st
+
+from kubernetes_gpu_cluster_amd.k8s.render import ValuesError, render, to_yaml
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OURS = sorted(glob.glob(os.path.join(ROOT, "deploy/values/*.yaml")))
+REF = sorted(glob.glob("/root/reference/values-01-minimal-example*.yaml"))
+
+
+def _load(p):
+    with open(p) as f:
+        return yaml.safe_load(f)
+
+
+def _by_kind(objs, kind):
+    return [o for o in objs if o["kind"] == kind]
+
+
+def _check_invariants(objs, values):
+    deps = [d for d in _by_kind(objs, "Deployment") if d["metadata"]["name"].endswith("-deployment-vllm")]
+    assert len(deps) == len(values["servingEngineSpec"]["modelSpec"])
+    for d, ms in zip(deps, values["servingEngineSpec"]["modelSpec"]):
+        tpl = d["spec"]["template"]
+        lab = tpl["metadata"]["labels"]
+        assert lab["app.kubernetes.io/name"] == "vllm-stack"
+        assert lab["app.kubernetes.io/component"] == "serving-engine"
+        c = tpl["spec"]["containers"][0]
+        res = c["resources"]
+        assert "nvidia.com/gpu" not in str(res)
+        if int(ms.get("requestGPU", 1)):
+            assert int(res["limits"]["amd.com/gpu"]) >= int(ms.get("requestGPU", 1))
+        else:
+            assert "amd.com/gpu" not in res["limits"]
+            assert "--device" in c["args"]
+        shm = [m for m in c["volumeMounts"] if m["mountPath"] == "/dev/shm"]
+        assert len(shm) <= 1
+        names = [v["name"] for v in tpl["spec"]["volumes"]]
+        for m in c["volumeMounts"]:
+            assert m["name"] in names
+        assert d["spec"]["replicas"] == ms.get("replicaCount", 1)
+        assert c["args"][:2] == ["--model", str(ms["modelURL"])]
+    svc = [s for s in _by_kind(objs, "Service") if s["metadata"]["name"] == "vllm-router-service"]
+    assert svc and svc[0]["spec"]["ports"][0]["port"] == 80
+
+
+@pytest.mark.parametrize("path", OURS + REF, ids=[os.path.basename(os.path.dirname(p)) + "/" + os.path.basename(p) for p in OURS + REF])
+def test_render_all_values(path):
+    v = _load(path)
+    objs = render(v, release="vllm")
+    _check_invariants(objs, v)
+    yaml.safe_load_all(to_yaml(objs))     # round-trips
+
+
+def test_values8_mapping():
+    v = _load(os.path.join(ROOT, "deploy/values/values-01-minimal-example8.yaml"))
+    dep = render(v)[0]
+    c = dep["spec"]["template"]["spec"]["containers"][0]
+    a = c["args"]
+    assert a[a.index("--tensor-parallel-size") + 1] == "2"
+    assert a[a.index("--dtype") + 1] == "float16"
+    assert "--disable-custom-all-reduce" in a and "--enforce-eager" in a
+    assert c["resources"]["limits"]["amd.com/gpu"] == "2"
+    env = {e["name"]: e["value"] for e in c["env"]}
+    assert env["PYTORCH_HIP_ALLOC_CONF"] == "expandable_segments:True"
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    shm = [m for m in c["volumeMounts"] if m["mountPath"] == "/dev/shm"]
+    assert len(shm) == 1
+    assert dep["spec"]["template"]["spec"]["runtimeClassName"] == "crun"
+    assert dep["metadata"]["name"] == "vllm-qwen3-deployment-vllm"
+
+
+def test_pp_and_cpu():
+    v4 = _load(os.path.join(ROOT, "deploy/values/values-01-minimal-example4.yaml"))
+    c = render(v4)[0]["spec"]["template"]["spec"]["containers"][0]
+    assert c["resources"]["limits"]["amd.com/gpu"] == "2"      # PP=2 folded into the pod
+    vc = _load(os.path.join(ROOT, "deploy/values/values-opt125m-cpu.yaml"))
+    c = render(vc)[0]["spec"]["template"]["spec"]["containers"][0]
+    assert "amd.com/gpu" not in c["resources"]["requests"]
+    assert c["args"][c["args"].index("--device") + 1] == "cpu"
+
+
+def test_errors():
+    with pytest.raises(ValuesError):
+        render({})
+    with pytest.raises(ValuesError):
+        render({"servingEngineSpec": {"modelSpec": [{"name": "a"}]}})
+    with pytest.raises(ValuesError):
+        render({"servingEngineSpec": {"modelSpec": [{"name": "a", "modelURL": "x", "bogus": 1}]}})
+    with pytest.raises(ValuesError):
+        render({"servingEngineSpec": {"modelSpec": [{"name": "a", "modelURL": "x"},
+                                                    {"name": "A", "modelURL": "y"}]}})
+
+
+def test_golden_example2():
+    v = _load(os.path.join(ROOT, "deploy/values/values-01-minimal-example2.yaml"))
+    got = to_yaml(render(v, release="vllm"))
+    golden = os.path.join(ROOT, "tests/fixtures/golden_values2.yaml")
+    if not os.path.exists(golden):
+        with open(golden, "w") as f:
+            f.write(got)
+    assert got == open(golden).read()
+
+
+_name = st.text(alphabet="abcdefghijklmnopqrstuvwxyz0123456789-", min_size=1, max_size=20)
+
+
+@settings(max_examples=60, deadline=None)
+@given(st.lists(st.fixed_dictionaries(
+    {"name": _name, "modelURL": st.sampled_from(["meta-llama/Meta-Llama-3-8B", "/models/x"])},
+    optional={"replicaCount": st.integers(1, 8), "requestGPU": st.integers(0, 8),
+              "requestCPU": st.integers(1, 64), "shmSize": st.sampled_from(["1Gi", "10Gi"]),
+              "vllmConfig": st.fixed_dictionaries({}, optional={
+                  "tensorParallelSize": st.sampled_from([1, 2, 4, 8]),
+                  "pipelineParallelSize": st.sampled_from([1, 2]),
+                  "maxModelLen": st.integers(128, 131072),
+                  "extraArgs": st.lists(st.sampled_from(["--enforce-eager", "--trust-remote-code"]))})}),
+    min_size=1, max_size=3, unique_by=lambda d: d["name"].strip("-") or "x"))
+def test_render_fuzz(specs):
+    v = {"servingEngineSpec": {"runtimeClassName": "", "modelSpec": specs}}
+    try:
+        objs = render(v)
+    except ValuesError:
+        return    # e.g. names colliding after DNS-1123 normalisation
+    _check_invariants(objs, v)
+    for d, ms in zip([o for o in objs if o["kind"] == "Deployment"], specs):
+        vc = ms.get("vllmConfig") or {}
+        deg = vc.get("tensorParallelSize", 1) * vc.get("pipelineParallelSize", 1)
+        if ms.get("requestGPU", 1):
+            lim = int(d["spec"]["template"]["spec"]["containers"][0]["resources"]["limits"]["amd.com/gpu"])
+            assert lim == max(ms.get("requestGPU", 1), deg)
+
+
+def test_chart_parity():
+    """No helm binary offline: the chart must expose the same contract as the renderer."""
+    tpl = open(os.path.join(ROOT, "deploy/chart/kgc-stack/templates/engine.yaml")).read()
+    rt = open(os.path.join(ROOT, "deploy/chart/kgc-stack/templates/router.yaml")).read()
+    for key in ("servingEngineSpec.modelSpec", "replicaCount", "requestCPU", "requestMemory",
+                "amd.com/gpu", "tensorParallelSize", "pipelineParallelSize",
+                "gpuMemoryUtilization", "maxModelLen", "extraArgs", "shmSize", "nodeSelector",
+                "affinity", "topologySpreadConstraints", "tolerations", "runtimeClassName",
+                "extraVolumes", "extraVolumeMounts", "-deployment-vllm", "serving-engine",
+                "PYTORCH_HIP_ALLOC_CONF", "/health"):
+        assert key in tpl, key
+    assert "vllm-router-service" in rt and "port: 80" in rt and "pods" in rt
+    yaml.safe_load(open(os.path.join(ROOT, "deploy/chart/kgc-stack/Chart.yaml")))
