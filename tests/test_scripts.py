@@ -1,0 +1,135 @@
+"""Node bootstrap scripts under stub binaries (systemctl, kubeadm, apt-get, kubectl, ...)
+with every written file redirected under ROOT."""
+import os
+import subprocess
+
+import pytest
+
+from fake_node import make_node
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SCRIPTS = os.path.join(REPO, "deploy", "scripts")
+STUBS = ["systemctl", "kubeadm", "apt-get", "apt-mark", "modprobe", "sysctl", "ss", "curl",
+         "kubectl", "crio", "crictl", "swapoff", "udevadm", "tar", "crun", "conmon", "chown"]
+
+
+@pytest.fixture()
+def env(tmp_path):
+    stub = tmp_path / "stubs"
+    stub.mkdir()
+    log = tmp_path / "calls.log"
+    for s in STUBS:
+        body = f'#!/bin/bash\necho "{s} $*" >> "{log}"\n'
+        if s == "kubeadm":
+            body += ('if [[ "$1" == init ]]; then echo "kubeadm join 10.0.0.1:6443 --token abc.def '
+                     '--discovery-token-ca-cert-hash sha256:00"; fi\n')
+        (stub / s).write_text(body)
+        (stub / s).chmod(0o755)
+    root = tmp_path / "root"
+    (root / "etc").mkdir(parents=True)
+    (root / "etc" / "fstab").write_text("UUID=1 / ext4 defaults 0 1\n/swap.img none swap sw 0 0\n")
+    e = dict(os.environ, PATH=f"{stub}:{os.environ['PATH']}", ROOT=str(root), SUDO_USER="")
+    return e, root, log
+
+
+def sh(script, *args, env, check=True):
+    r = subprocess.run(["bash", os.path.join(SCRIPTS, script), *args], env=env,
+                       capture_output=True, text=True)
+    if check:
+        assert r.returncode == 0, r.stdout + r.stderr
+    return r
+
+
+def calls(log):
+    return log.read_text().splitlines() if log.exists() else []
+
+
+def test_control_plane(env):
+    e, root, log = env
+    sh("k8s_setup.sh", "--role", "control_plane", "--kube-version=v1.32.1", "--yes", "--untaint",
+       "--label-gpu", env=e)
+    c = calls(log)
+    init = [x for x in c if x.startswith("kubeadm init")][0]
+    assert "--cri-socket unix:///var/run/crio/crio.sock" in init
+    assert "--kubernetes-version v1.32.1" in init and "--pod-network-cidr 192.168.0.0/16" in init
+    assert "stable:/v1.32/deb" in (root / "etc/apt/sources.list.d/kubernetes.list").read_text()
+    assert "br_netfilter" in (root / "etc/modules-load.d/k8s.conf").read_text()
+    assert "ip_forward" in (root / "etc/sysctl.d/99-kubernetes-cri.conf").read_text()
+    assert "#/swap.img" in (root / "etc/fstab").read_text()
+    assert any("calico.yaml" in x for x in c)
+    assert any("taint nodes --all node-role.kubernetes.io/control-plane-" in x for x in c)
+    assert any("label node" in x and "gpu=true" in x for x in c)
+    assert any(x == "apt-get install -y kubelet kubeadm kubectl" for x in c)
+    assert list((root / "var/log").glob("kubeadm-init-*.log"))
+
+
+def test_ha_control_plane_endpoint(env):
+    e, root, log = env
+    sh("k8s_setup.sh", "--yes", "--role=cp", "--control-plane-endpoint=10.0.0.100:6443", env=e)
+    init = [x for x in calls(log) if x.startswith("kubeadm init")][0]
+    assert "--control-plane-endpoint 10.0.0.100:6443 --upload-certs" in init
+
+
+def test_worker_join_reference_form(env):
+    e, root, log = env
+    join = "kubeadm join 10.0.0.1:6443 --token abc --discovery-token-ca-cert-hash sha256:00"
+    sh("k8s_setup.sh", "--yes", "--role=node", f"--join={join}", env=e)
+    j = [x for x in calls(log) if x.startswith("kubeadm join")]
+    assert j and j[0].endswith("--cri-socket unix:///var/run/crio/crio.sock")
+
+
+def test_worker_join_honours_cri_socket_and_yes_anywhere(env):
+    e, root, log = env
+    sh("k8s_setup.sh", "--role", "worker", "--join", "kubeadm join 1.2.3.4:6443 --token t",
+       "--cri-socket", "unix:///run/containerd/containerd.sock", "--yes", env=e)
+    j = [x for x in calls(log) if x.startswith("kubeadm join")][0]
+    assert j.endswith("--cri-socket unix:///run/containerd/containerd.sock")
+
+
+def test_args_validated_before_destructive_steps(env):
+    e, root, log = env
+    r = sh("k8s_setup.sh", "--yes", env=e, check=False)
+    assert r.returncode != 0 and "--role" in r.stderr
+    r = sh("k8s_setup.sh", "--role=node", "--yes", env=e, check=False)
+    assert r.returncode != 0
+    r = sh("k8s_setup.sh", "--role=cp", "--kube-version=latest", "--yes", env=e, check=False)
+    assert r.returncode != 0
+    assert calls(log) == []          # nothing was reset or installed
+
+
+def test_dry_run_prints(env):
+    e, root, log = env
+    r = sh("k8s_setup.sh", "--role=cp", "--yes", "--dry-run", env=e)
+    assert "DRY: kubeadm init" in r.stdout and not any(x.startswith("kubeadm init") for x in calls(log))
+
+
+def test_crio_setup(env):
+    e, root, log = env
+    (root / "usr/local/bin").mkdir(parents=True)
+    sh("crio_setup.sh", "--crio-version", "v1.33", "--proxy=http://127.0.0.1:8118", env=e)
+    assert "isv:/cri-o:/stable:/v1.33" in (root / "etc/apt/sources.list.d/cri-o.list").read_text()
+    assert "HTTPS_PROXY=http://127.0.0.1:8118" in (root / "etc/systemd/system/crio.service.d/proxy.conf").read_text()
+    assert any(x == "apt-get install -y cri-o" for x in calls(log))
+
+
+def test_gpu_crio_setup(env):
+    e, root, log = env
+    subprocess.run(["bash", os.path.join(REPO, "native", "build.sh")], check=True)
+    make_node(str(root), n_gpus=8)
+    sh("gpu-crio-setup.sh", "--with-hook", "--skip-apt", env=e)
+    conf = (root / "etc/crio/crio.conf.d/99-amd.conf").read_text()
+    assert "[crio.runtime.runtimes.amd]" in conf and "default_runtime" not in conf
+    assert 'default_runtime = "crun"' in (root / "etc/crio/crio.conf.d/98-crun-default.conf").read_text()
+    cdi = (root / "etc/cdi/amd.yaml").read_text()
+    assert cdi.count("renderD") >= 16
+    assert (root / "usr/share/containers/oci/hooks.d/oci-amd-hook.json").exists()
+    assert "hooks_dir" in (root / "etc/crio/crio.conf.d/99-amd-hooks.conf").read_text()
+    assert (root / "usr/local/bin/amd-container-runtime").exists()
+    assert "render" in (root / "etc/udev/rules.d/70-amdgpu-kfd.rules").read_text()
+    c = calls(log)
+    assert "systemctl restart crio" in c
+    assert any("runtimeclasses.yaml" in x for x in c) and any("amd-gpu-device-plugin.yaml" in x for x in c)
+    # --set-default makes the amd handler the default runtime
+    sh("gpu-crio-setup.sh", "--set-default", "--skip-apt", "--no-kubectl", env=e)
+    assert 'default_runtime = "amd"' in (root / "etc/crio/crio.conf.d/99-amd.conf").read_text()
+    assert not (root / "etc/crio/crio.conf.d/98-crun-default.conf").exists()
