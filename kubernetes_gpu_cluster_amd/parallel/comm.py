@@ -44,9 +44,13 @@ def tp_all_gather(x: torch.Tensor, dim: int = -1) -> torch.Tensor:
     if s.tp_size == 1:
         return x
     dim = dim % x.dim()
-    out = torch.empty((s.tp_size,) + tuple(x.shape), dtype=x.dtype, device=x.device)
-    dist.all_gather_into_tensor(out, x.contiguous(), group=s.tp_group)
-    return torch.cat(out.unbind(0), dim=dim)
+    x = x.contiguous()
+    out = torch.empty((s.tp_size * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype,
+                      device=x.device)
+    dist.all_gather_into_tensor(out, x, group=s.tp_group)
+    if dim == 0:
+        return out
+    return torch.cat(out.view((s.tp_size,) + tuple(x.shape)).unbind(0), dim=dim)
 
 
 def tp_gather(x: torch.Tensor, dim: int = -1) -> Optional[torch.Tensor]:

@@ -1,0 +1,133 @@
+"""Multi-process (gloo, CPU) correctness of the parallel paths: TP=2 and PP=2
+logits == single process, Mixtral expert-parallel all-to-all == TP experts, and
+the multi-process engine (command/plan broadcast protocol) == single process."""
+import json
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from kubernetes_gpu_cluster_amd.models import PRESETS, full_state_dict_random
+
+from test_model_parity import _engine_logits
+
+WORLD_TIMEOUT = 240
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _child(rank, world, port, fn, args, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    res = fn(rank, *args)
+    if res is not None:
+        torch.save(res, os.path.join(outdir, f"r{rank}.pt"))
+
+
+def spawn(fn, world, *args):
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_child, args=(world, _port(), fn, args, d), nprocs=world,
+                           join=True, start_method="spawn")
+        return {int(f[1:-3]): torch.load(os.path.join(d, f)) for f in os.listdir(d)}
+
+
+def _logits(rank, name, tp, pp, moe_mode="tp"):
+    from kubernetes_gpu_cluster_amd.engine.block_manager import BlockManager
+    from kubernetes_gpu_cluster_amd.engine.model_runner import ModelRunner
+    from kubernetes_gpu_cluster_amd.engine.sequence import SamplingParams, Sequence
+    from kubernetes_gpu_cluster_amd.models import build_model
+    from kubernetes_gpu_cluster_amd.models.moe import set_moe_mode
+    from kubernetes_gpu_cluster_amd.parallel import comm
+    from kubernetes_gpu_cluster_amd.parallel.state import destroy_parallel, init_parallel
+    set_moe_mode(moe_mode)
+    s = init_parallel(tp, pp, backend="gloo", device=torch.device("cpu"))
+    cfg = PRESETS[name]
+    model = build_model(cfg, torch.float32, torch.device("cpu"))
+    model.load_weights(full_state_dict_random(cfg, seed=3, std=0.05).items())
+    runner = ModelRunner(model, cfg, torch.float32, torch.device("cpu"), 16, 256, 4, 128, True)
+    runner.init_kv_cache(48)
+    g = torch.Generator().manual_seed(0)
+    prompt = torch.randint(3, cfg.vocab_size, (29,), generator=g).tolist()
+    if pp == 1:
+        out = _engine_logits(model, runner, prompt, [13, 16], [7, 8])
+    else:
+        bm = BlockManager(48, 16, 4, runner.max_blocks)
+        seq = Sequence("0", prompt, SamplingParams())
+        bm.allocate(seq, len(prompt))
+        plan, _ = runner.build_plan([(seq, len(prompt))], [], bm.table)
+        runner._upload(plan)
+        meta = runner._meta(plan.T, plan.Tp, plan.P, plan.D, plan.W, plan.max_ctx)
+        with torch.inference_mode():
+            if s.is_first_pp:
+                h, r = runner._forward(plan.T, meta)
+                comm.pp_send([h, r])
+                out = None
+            else:
+                hin = comm.pp_recv([(plan.T, cfg.hidden_size)] * 2, torch.float32, torch.device("cpu"))
+                out = model.compute_logits(runner._forward(plan.T, meta, hin))
+    destroy_parallel()
+    return out
+
+
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-qwen2", "tiny-qwen3"])
+def test_tp2_matches_tp1(name):
+    ref = spawn(_logits, 1, name, 1, 1)[0]
+    got = spawn(_logits, 2, name, 2, 1)
+    torch.testing.assert_close(got[0], ref, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(got[1], ref, atol=1e-4, rtol=1e-4)   # identical on all ranks
+
+
+def test_pp2_matches_pp1():
+    ref = spawn(_logits, 1, "tiny-llama", 1, 1)[0]
+    got = spawn(_logits, 2, "tiny-llama", 1, 2)
+    torch.testing.assert_close(got[1], ref[:29], atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("mode", ["tp", "ep"])
+def test_moe_tp2(mode):
+    ref = spawn(_logits, 1, "tiny-mixtral", 1, 1)[0]
+    got = spawn(_logits, 2, "tiny-mixtral", 2, 1, mode)
+    torch.testing.assert_close(got[0], ref, atol=1e-4, rtol=1e-4)
+
+
+def _write_hf_dir(path, name):
+    from safetensors.torch import save_file
+    cfg = PRESETS[name]
+    os.makedirs(path, exist_ok=True)
+    save_file({k: v.contiguous() for k, v in full_state_dict_random(cfg, seed=5, std=0.05).items()},
+              os.path.join(path, "model.safetensors"))
+    json.dump({"model_type": "llama", "hidden_size": cfg.hidden_size,
+               "num_hidden_layers": cfg.num_layers, "num_attention_heads": cfg.num_heads,
+               "num_key_value_heads": cfg.num_kv_heads, "head_dim": cfg.head_dim,
+               "intermediate_size": cfg.intermediate_size, "vocab_size": cfg.vocab_size,
+               "max_position_embeddings": 512, "rope_theta": cfg.rope_theta,
+               "rms_norm_eps": cfg.rms_eps, "eos_token_id": 2, "bos_token_id": 1},
+              open(os.path.join(path, "config.json"), "w"))
+
+
+def test_engine_multiproc_tp2_and_pp2():
+    """LLM with TP=2 / PP=2 spawns worker processes; greedy output == TP=1 (weights
+    loaded from a local safetensors checkpoint, sliced per rank)."""
+    from kubernetes_gpu_cluster_amd.engine.llm_engine import LLM
+    from kubernetes_gpu_cluster_amd.engine.sequence import SamplingParams
+    with tempfile.TemporaryDirectory() as d:
+        _write_hf_dir(d, "tiny-llama")
+        prompts = [list(range(3, 40)), [5, 6, 7] * 20, [9]]
+        sp = [SamplingParams(temperature=0, max_tokens=8, ignore_eos=True)] * 3
+        outs = {}
+        for tp, pp in ((1, 1), (2, 1), (1, 2)):
+            llm = LLM(d, device="cpu", dtype="float32", tensor_parallel_size=tp,
+                      pipeline_parallel_size=pp, max_model_len=256, max_num_seqs=4,
+                      max_num_batched_tokens=64, num_gpu_blocks_override=64)
+            outs[(tp, pp)] = [o.output_token_ids for o in llm.generate(prompts, sp)]
+            llm.shutdown()
+        assert outs[(2, 1)] == outs[(1, 1)]
+        assert outs[(1, 2)] == outs[(1, 1)]
