@@ -63,6 +63,9 @@ class Worker:
         if dev.type == "cpu" and self.dtype == torch.float16:
             self.dtype = torch.float32       # CPU oracle path
         self.max_model_len = default_max_model_len(cfg)
+        if dev.type == "cuda":
+            from ..utils.gemm_tuning import enable_tuned_gemms
+            enable_tuned_gemms(mcfg.name, cfg.tensor_parallel_size)
         torch.manual_seed(cfg.seed)
         self.mcfg, self.model = load_model(cfg.model, self.dtype, dev, cfg.random_init,
                                            seed=cfg.seed)
