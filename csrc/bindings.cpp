@@ -207,6 +207,45 @@ void sample(Tensor out, Tensor logits, Tensor temperature, Tensor top_k, Tensor 
                      stream());
 }
 
+// ---- K12 xGMI all-reduce: IPC buffers are raw device pointers carried as int64
+int64_t ar_signal_bytes() { return (int64_t)kgc::allreduce_signal_bytes(); }
+int64_t ar_alloc(int64_t bytes) { return (int64_t)(intptr_t)kgc::ar_alloc(bytes); }
+void ar_free(int64_t p) { kgc::ar_free((void*)(intptr_t)p); }
+Tensor ar_get_handle(int64_t p) {
+  Tensor h = at::zeros({64}, at::TensorOptions().dtype(at::kByte));
+  kgc::ar_get_handle((void*)(intptr_t)p, h.data_ptr<uint8_t>());
+  return h;
+}
+int64_t ar_open_handle(Tensor h) {
+  TORCH_CHECK(h.device().is_cpu() && h.scalar_type() == at::kByte && h.numel() == 64,
+              "IPC handle: uint8[64] CPU tensor");
+  return (int64_t)(intptr_t)kgc::ar_open_handle(h.contiguous().data_ptr<uint8_t>());
+}
+void ar_close_handle(int64_t p) { kgc::ar_close_handle((void*)(intptr_t)p); }
+int64_t ar_read_err(int64_t sig) { return (int64_t)kgc::ar_read_err((void*)(intptr_t)sig); }
+
+void xgmi_allreduce(Tensor inout, std::vector<int64_t> data, std::vector<int64_t> sig, int64_t rank,
+                    int64_t cap_bytes, bool two_shot) {
+  check_gpu(inout, "inout");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(inout.device());
+  const int64_t nr = (int64_t)data.size();
+  TORCH_CHECK(nr == 2 || nr == 4 || nr == 8, "xgmi all-reduce: 2, 4 or 8 ranks");
+  TORCH_CHECK((int64_t)sig.size() == nr && rank >= 0 && rank < nr, "bad rank / pointer lists");
+  TORCH_CHECK(inout.is_contiguous(), "inout must be contiguous");
+  TORCH_CHECK(inout.scalar_type() == at::kBFloat16 || inout.scalar_type() == at::kHalf,
+              "bf16 / fp16 only");
+  const int64_t bytes = inout.numel() * inout.element_size();
+  TORCH_CHECK(bytes % (16 * nr) == 0, "message must be a multiple of 16 B x ranks");
+  TORCH_CHECK(bytes <= cap_bytes, "message larger than the IPC buffer");
+  kgc::ArPtrs P{};
+  for (int64_t r = 0; r < nr; ++r) {
+    P.data[r] = (void*)(intptr_t)data[r];
+    P.sig[r] = (void*)(intptr_t)sig[r];
+  }
+  kgc::launch_allreduce(dt_code(inout), P, (int)nr, (int)rank, inout.data_ptr(), bytes / 16,
+                        cap_bytes / 16, two_shot, stream());
+}
+
 int64_t decode_partition_size() { return kgc::paged_decode_partition_size(); }
 int64_t prefill_block_m() { return kgc::prefill_block_m(); }
 
@@ -228,6 +267,15 @@ TORCH_LIBRARY(kgc, m) {
   m.def("sample(Tensor(a!) out, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, "
         "Tensor seeds) -> ()");
   m.def("decode_partition_size() -> int", &decode_partition_size);
+  m.def("ar_signal_bytes() -> int", &ar_signal_bytes);
+  m.def("ar_alloc(int bytes) -> int", &ar_alloc);
+  m.def("ar_free(int ptr) -> ()", &ar_free);
+  m.def("ar_get_handle(int ptr) -> Tensor", &ar_get_handle);
+  m.def("ar_open_handle(Tensor handle) -> int", &ar_open_handle);
+  m.def("ar_close_handle(int ptr) -> ()", &ar_close_handle);
+  m.def("ar_read_err(int sig) -> int", &ar_read_err);
+  m.def("xgmi_allreduce(Tensor(a!) inout, int[] data, int[] sig, int rank, int cap_bytes, "
+        "bool two_shot) -> ()");
   m.def("prefill_block_m() -> int", &prefill_block_m);
 }
 
@@ -239,4 +287,5 @@ TORCH_LIBRARY_IMPL(kgc, CUDA, m) {
   m.impl("paged_decode", &paged_decode);
   m.impl("prefill_attention", &prefill_attention);
   m.impl("sample", &sample);
+  m.impl("xgmi_allreduce", &xgmi_allreduce);
 }

@@ -1,0 +1,209 @@
+// K12: one-shot / two-shot all-reduce over xGMI peer memory (SURVEY.md §2.5 K12;
+// the reference only toggles it: values-01-minimal-example8.yaml:32
+// `--disable-custom-all-reduce`).
+//
+// Every TP rank owns one uncached IPC buffer: [ArSignal][data parity 0][data parity 1].
+// The peers' buffers are mapped into each process (hipIpcOpenMemHandle), so a kernel
+// reads the other GPUs' HBM directly over the point-to-point xGMI links -- all 7 links
+// of an MI355X in parallel, instead of RCCL's ring that is bound by one link per step.
+//
+//  one-shot (small messages, latency bound): copy in -> flag barrier -> every rank
+//     sums all NR inputs (reads (NR-1) x bytes remote).
+//  two-shot (medium): copy in -> barrier -> rank r reduces segment r in place ->
+//     barrier -> every rank gathers the NR reduced segments (reads 2 (NR-1)/NR x bytes).
+//
+// Barriers are per workgroup: block b of every rank touches the same element set, so
+// block b only waits for block b of its peers.  The grid is ALWAYS AR_MAX_BLOCKS wide
+// (empty blocks still take part in the barrier): the per-block epoch parity protects
+// element v across calls only if v maps to the same block in every call (epoch flags, monotonically increasing,
+// never reset).  Data regions alternate by epoch parity so a slow peer still reading
+// epoch e never sees epoch e+1's copy-in.  The epoch counter lives in device memory, so
+// the launch is hipGraph-capturable (kernel arguments are frozen at capture).
+// Spins are bounded: a missing peer sets ArSignal::err (checked by the host) instead of
+// hanging the GPU.
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+#include "launch.h"
+
+namespace kgc {
+
+constexpr int AR_MAX_RANKS = 8;
+constexpr int AR_MAX_BLOCKS = 64;
+constexpr int AR_THREADS = 512;
+
+struct ArSignal {
+  uint32_t counter[AR_MAX_BLOCKS];                     // local: last epoch per block
+  uint32_t flag[2][AR_MAX_BLOCKS][AR_MAX_RANKS];       // written by peers
+  uint32_t err;
+  uint32_t pad[63];
+};
+
+size_t allreduce_signal_bytes() { return (sizeof(ArSignal) + 4095) & ~size_t(4095); }
+
+__device__ __forceinline__ void ar_store_flag(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t ar_load_flag(uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Publish this block's writes to every peer, then wait for every peer's block.
+template <int NR>
+__device__ __forceinline__ void ar_barrier(const ArPtrs& P, int rank, int phase,
+                                           uint32_t epoch) {
+  // every wave drains its own stores first (vmcnt is per wave; do not rely on the
+  // barrier's implicit wait), then one lane per peer releases at system scope
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x < NR) {
+    __threadfence_system();   // release: copy-in / reduced data visible system-wide
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ArSignal* peer = reinterpret_cast<ArSignal*>(P.sig[threadIdx.x]);
+    ar_store_flag(&peer->flag[phase][blockIdx.x][rank], epoch);
+    ArSignal* self = reinterpret_cast<ArSignal*>(P.sig[rank]);
+    uint32_t* f = &self->flag[phase][blockIdx.x][threadIdx.x];
+    int it = 0;
+    while ((int32_t)(ar_load_flag(f) - epoch) < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++it > (1 << 25)) {        // ~seconds: a peer is gone; fail loudly on the host
+        atomicOr(&self->err, 1u << threadIdx.x);
+        break;
+      }
+    }
+    __threadfence_system();   // acquire
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ u32x4 ld_peer(const void* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+}
+
+template <typename T, int NR, bool TWO>
+__global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArPtrs P, int rank, T* inout,
+                                                               int64_t nvec, int64_t cap_vec) {
+  ArSignal* self = reinterpret_cast<ArSignal*>(P.sig[rank]);
+  __shared__ uint32_t s_epoch;
+  if (threadIdx.x == 0) s_epoch = self->counter[blockIdx.x] + 1;
+  __syncthreads();
+  const uint32_t epoch = s_epoch;
+  const int64_t par_off = (int64_t)(epoch & 1) * cap_vec;
+  u32x4* io = reinterpret_cast<u32x4*>(inout);
+  u32x4* mine = reinterpret_cast<u32x4*>(P.data[rank]) + par_off;
+  const int64_t stride = (int64_t)gridDim.x * AR_THREADS;
+  const int64_t first = (int64_t)blockIdx.x * AR_THREADS + threadIdx.x;
+
+  for (int64_t v = first; v < nvec; v += stride) mine[v] = io[v];
+  ar_barrier<NR>(P, rank, 0, epoch);
+
+  auto reduce_at = [&](int64_t v) {
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    Pack8<T> in[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+      in[r].u = ld_peer(reinterpret_cast<const u32x4*>(P.data[r]) + par_off + v);
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += to_f<T>(in[r].h[j]);
+    Pack8<T> o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o.h[j] = from_f<T>(acc[j]);
+    return o.u;
+  };
+
+  if constexpr (!TWO) {
+    for (int64_t v = first; v < nvec; v += stride) io[v] = reduce_at(v);
+  } else {
+    const int64_t seg = nvec / NR;    // host guarantees nvec % NR == 0
+    const int64_t lo = (int64_t)rank * seg;
+    for (int64_t v = first; v < seg; v += stride) mine[lo + v] = reduce_at(lo + v);
+    ar_barrier<NR>(P, rank, 1, epoch);
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const u32x4* src = reinterpret_cast<const u32x4*>(P.data[r]) + par_off + (int64_t)r * seg;
+      u32x4* dst = io + (int64_t)r * seg;
+      for (int64_t v = first; v < seg; v += stride) dst[v] = ld_peer(src + v);
+    }
+  }
+  if (threadIdx.x == 0) self->counter[blockIdx.x] = epoch;
+}
+
+template <typename T, int NR>
+static void ar_dispatch(const ArPtrs& P, int rank, void* inout, int64_t nvec, int64_t cap_vec,
+                        bool two, hipStream_t s) {
+  constexpr int blocks = AR_MAX_BLOCKS;
+  if (two)
+    allreduce_kernel<T, NR, true><<<blocks, AR_THREADS, 0, s>>>(P, rank, (T*)inout, nvec, cap_vec);
+  else
+    allreduce_kernel<T, NR, false><<<blocks, AR_THREADS, 0, s>>>(P, rank, (T*)inout, nvec, cap_vec);
+}
+
+template <typename T>
+static void ar_by_ranks(int nranks, const ArPtrs& P, int rank, void* inout, int64_t nvec,
+                        int64_t cap_vec, bool two, hipStream_t s) {
+  switch (nranks) {
+    case 2: ar_dispatch<T, 2>(P, rank, inout, nvec, cap_vec, two, s); break;
+    case 4: ar_dispatch<T, 4>(P, rank, inout, nvec, cap_vec, two, s); break;
+    case 8: ar_dispatch<T, 8>(P, rank, inout, nvec, cap_vec, two, s); break;
+    default: break;
+  }
+}
+
+int allreduce_max_blocks() { return AR_MAX_BLOCKS; }
+
+void launch_allreduce(int dtype, const ArPtrs& P, int nranks, int rank, void* inout,
+                      int64_t nvec, int64_t cap_vec, bool two_shot, hipStream_t s) {
+  if (dtype == DT_BF16)
+    ar_by_ranks<bf16>(nranks, P, rank, inout, nvec, cap_vec, two_shot, s);
+  else
+    ar_by_ranks<f16>(nranks, P, rank, inout, nvec, cap_vec, two_shot, s);
+}
+
+// ---- IPC buffer management (host) ----------------------------------------------
+static void ar_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+void* ar_alloc(int64_t bytes) {
+  void* p = nullptr;
+  // uncached: flags and peer-written data must never sit stale in a local L2
+  ar_check(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached), "hipExtMallocWithFlags");
+  ar_check(hipMemset(p, 0, bytes), "hipMemset");
+  ar_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  return p;
+}
+
+void ar_free(void* p) { ar_check(hipFree(p), "hipFree"); }
+
+void ar_get_handle(void* p, uint8_t* out64) {
+  hipIpcMemHandle_t h;
+  ar_check(hipIpcGetMemHandle(&h, p), "hipIpcGetMemHandle");
+  static_assert(sizeof(h) <= 64, "IPC handle larger than 64 bytes");
+  memset(out64, 0, 64);
+  memcpy(out64, &h, sizeof(h));
+}
+
+void* ar_open_handle(const uint8_t* in64) {
+  hipIpcMemHandle_t h;
+  memcpy(&h, in64, sizeof(h));
+  void* p = nullptr;
+  ar_check(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
+  return p;
+}
+
+void ar_close_handle(void* p) { ar_check(hipIpcCloseMemHandle(p), "hipIpcCloseMemHandle"); }
+
+uint32_t ar_read_err(void* sig) {
+  uint32_t e = 0;
+  ar_check(hipMemcpy(&e, &reinterpret_cast<ArSignal*>(sig)->err, 4, hipMemcpyDeviceToHost),
+           "hipMemcpy");
+  return e;
+}
+
+}  // namespace kgc

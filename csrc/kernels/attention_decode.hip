@@ -30,7 +30,18 @@ namespace kgc {
 constexpr int DEC_PART = 64;     // tokens per partition (one wave-iteration)
 constexpr int DEC_CHUNKS = DEC_PART / 32;
 
-template <typename T, int D>
+__device__ __forceinline__ u32x4 ld16(const void* p) {
+  return *reinterpret_cast<const u32x4*>(p);
+}
+
+// PREF: false = load each K/V fragment right before its MFMA (116 VGPR, 4 waves/SIMD);
+// true = issue all 32 K and V loads of the partition before the first MFMA (132 VGPR,
+// 3 waves/SIMD).  Measured (tools/attn_bench.py, B=256 Llama-3-8B shapes): PREF is
+// 5-9 % faster when the grid is one workgroup per (seq, kv head) (Z == 1), ~6 % slower
+// at Z = 4 where fewer, longer-lived waves want occupancy.  Non-temporal K/V loads
+// and an MFMA-tiled K layout (1 KB contiguous per load) were measured too: -7 % and
+// +3 %, neither kept.
+template <typename T, int D, bool PREF>
 __global__ __launch_bounds__(256, 3) void paged_decode_kernel(
     T* __restrict__ out, const T* __restrict__ q, const T* __restrict__ kc,
     const T* __restrict__ vc, const int* __restrict__ block_tables, int bt_stride,
@@ -76,22 +87,48 @@ __global__ __launch_bounds__(256, 3) void paged_decode_kernel(
 
   for (int p = blockIdx.z * 4 + wave; p < P; p += gridDim.z * 4) {
     const int base = p * DEC_PART;
-    f32x4 sa[DEC_CHUNKS], sb[DEC_CHUNKS];
-    // ---- S^T = K . Q^T
+    const T* kaddr[DEC_CHUNKS][2];
+    const T* vaddr[DEC_CHUNKS];
 #pragma unroll
     for (int c = 0; c < DEC_CHUNKS; ++c) {
       const int ta = min(base + c * 32 + keyA, ctx - 1);
       const int tb = min(base + c * 32 + keyA + 4, ctx - 1);
-      const T* ka = kbase + bt[ta >> bs_log2] * blk_stride + (int64_t)(ta & bsm) * D + 8 * qd;
-      const T* kb = kbase + bt[tb >> bs_log2] * blk_stride + (int64_t)(tb & bsm) * D + 8 * qd;
+      kaddr[c][0] = kbase + bt[ta >> bs_log2] * blk_stride + (int64_t)(ta & bsm) * D + 8 * qd;
+      kaddr[c][1] = kbase + bt[tb >> bs_log2] * blk_stride + (int64_t)(tb & bsm) * D + 8 * qd;
+      // V^T 8-key group of keys t0..t0+7: [(t0 & bsm) / 8][d][8]; 16 lanes = 256 B
+      const int t0 = min(base + c * 32 + 8 * qd, ctx - 1) & ~7;
+      vaddr[c] = vbase + bt[t0 >> bs_log2] * blk_stride + ((t0 & bsm) >> 3) * (D * 8) + r16 * 8;
+    }
+    Pack8<T> kf[DEC_CHUNKS][2][KS];
+    Pack8<T> vf[PREF ? DEC_CHUNKS : 1][DT];
+    if constexpr (PREF) {
+#pragma unroll
+      for (int c = 0; c < DEC_CHUNKS; ++c)
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) {
+          kf[c][0][s2].u = ld16(kaddr[c][0] + 32 * s2);
+          kf[c][1][s2].u = ld16(kaddr[c][1] + 32 * s2);
+        }
+    }
+    if constexpr (PREF) {
+#pragma unroll
+      for (int c = 0; c < DEC_CHUNKS; ++c)
+#pragma unroll
+        for (int t = 0; t < DT; ++t) vf[PREF ? c : 0][t].u = ld16(vaddr[c] + 16 * t * 8);
+    }
+    f32x4 sa[DEC_CHUNKS], sb[DEC_CHUNKS];
+    // ---- S^T = K . Q^T
+#pragma unroll
+    for (int c = 0; c < DEC_CHUNKS; ++c) {
       f32x4 accA = {0.f, 0.f, 0.f, 0.f}, accB = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        Pack8<T> fa, fb;
-        fa.u = *reinterpret_cast<const u32x4*>(ka + 32 * s);
-        fb.u = *reinterpret_cast<const u32x4*>(kb + 32 * s);
-        accA = mfma16x16x32(fa.v, qf[s], accA);
-        accB = mfma16x16x32(fb.v, qf[s], accB);
+      for (int s2 = 0; s2 < KS; ++s2) {
+        if constexpr (!PREF) {
+          kf[c][0][s2].u = ld16(kaddr[c][0] + 32 * s2);
+          kf[c][1][s2].u = ld16(kaddr[c][1] + 32 * s2);
+        }
+        accA = mfma16x16x32(kf[c][0][s2].v, qf[s2], accA);
+        accB = mfma16x16x32(kf[c][1][s2].v, qf[s2], accB);
       }
       sa[c] = accA;
       sb[c] = accB;
@@ -126,14 +163,12 @@ __global__ __launch_bounds__(256, 3) void paged_decode_kernel(
         pf.h[i] = from_f<T>(pa);
         pf.h[4 + i] = from_f<T>(pb);
       }
-      // V^T 8-key group of keys t0..t0+7: [(t0 & bsm) / 8][d][8]; 16 lanes = 256 B
-      const int t0 = min(base + c * 32 + 8 * qd, ctx - 1) & ~7;
-      const T* vb = vbase + bt[t0 >> bs_log2] * blk_stride + ((t0 & bsm) >> 3) * (D * 8) + r16 * 8;
 #pragma unroll
       for (int t = 0; t < DT; ++t) {
-        Pack8<T> vf;
-        vf.u = *reinterpret_cast<const u32x4*>(vb + 16 * t * 8);
-        o[t] = mfma16x16x32(vf.v, pf.v, o[t]);
+        Pack8<T> v;
+        if constexpr (PREF) v = vf[PREF ? c : 0][t];
+        else v.u = ld16(vaddr[c] + 16 * t * 8);
+        o[t] = mfma16x16x32(v.v, pf.v, o[t]);
       }
     }
   }
@@ -210,7 +245,8 @@ static void decode_dispatch(void* out, const void* q, const void* kc, const void
                             const int* bt, int bt_stride, const int* ctx, float* ml, float* es,
                             float* tmp, int B, int nq, int nkv, int bs_log2, int Zmax, int Z,
                             float scale_log2, hipStream_t s) {
-  paged_decode_kernel<T, D><<<dim3(B, nkv, Z), 256, 0, s>>>(
+  auto kern = Z == 1 ? paged_decode_kernel<T, D, true> : paged_decode_kernel<T, D, false>;
+  kern<<<dim3(B, nkv, Z), 256, 0, s>>>(
       (T*)out, (const T*)q, (const T*)kc, (const T*)vc, bt, bt_stride, ctx, ml, es, tmp, nq,
       nkv, bs_log2, Zmax, scale_log2);
   if (Z > 1)

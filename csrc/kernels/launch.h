@@ -34,4 +34,20 @@ void launch_sample(int dtype, int64_t* out, const void* logits, int64_t row_stri
                    int V, const float* temperature, const int* top_k, const float* top_p,
                    const int64_t* seeds, hipStream_t s);
 
+// K12 xGMI all-reduce: per-rank [signal | data parity 0 | data parity 1] IPC buffers.
+struct ArPtrs {
+  void* data[8];
+  void* sig[8];
+};
+size_t allreduce_signal_bytes();
+int allreduce_max_blocks();
+void launch_allreduce(int dtype, const ArPtrs& P, int nranks, int rank, void* inout,
+                      int64_t nvec, int64_t cap_vec, bool two_shot, hipStream_t s);
+void* ar_alloc(int64_t bytes);
+void ar_free(void* p);
+void ar_get_handle(void* p, uint8_t* out64);
+void* ar_open_handle(const uint8_t* in64);
+void ar_close_handle(void* p);
+uint32_t ar_read_err(void* sig);
+
 }  // namespace kgc

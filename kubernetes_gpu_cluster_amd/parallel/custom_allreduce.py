@@ -1,0 +1,129 @@
+"""One-/two-shot all-reduce over xGMI peer memory for the decode-size TP all-reduces
+(call sites C1/C2 in §2.6).
+
+Why: inside one MI355X node every GPU pair has its own xGMI link (7 per GPU).  RCCL's
+ring all-reduce moves each byte over one link per step and pays a pipeline of 2(N-1)
+latency-bound hops; for the 0.06-4 MB messages of a decode step it is latency bound.
+Here every rank maps its TP peers' IPC buffers and one kernel (csrc/kernels/allreduce.hip)
+reads them all at once:
+
+* one-shot (<= ``one_shot_max`` bytes): each rank sums all N inputs itself;
+* two-shot (<= ``cap_bytes``): reduce-scatter into the owners' buffers, then
+  all-gather -- 2(N-1)/N of the bytes per rank, every link busy in parallel.
+
+Larger messages (prefill) fall back to RCCL.  The kernel's epoch counters live in
+device memory, so the all-reduce is captured into the decode hipGraphs like any
+other kernel.  ``--disable-custom-all-reduce`` (reference
+``values-01-minimal-example8.yaml:32``) or ``KGC_CUSTOM_AR=0`` turns it off.
+"""
+from __future__ import annotations
+
+import logging
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+log = logging.getLogger("kgc.allreduce")
+
+SUPPORTED_WORLD = (2, 4, 8)
+
+
+def _agree(ok: bool, group) -> bool:
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t[0]))
+
+
+class CustomAllReduce:
+    """Collective constructor: every rank of ``cpu_group`` must call it together.
+    Each step that can fail on one rank is followed by an agreement all-reduce, so a
+    failure raises on every rank instead of leaving peers blocked in a collective."""
+
+    def __init__(self, cpu_group, rank: int, world: int, device: torch.device,
+                 cap_bytes: int = 8 << 20, one_shot_max: Optional[int] = None):
+        if world not in SUPPORTED_WORLD:
+            raise ValueError(f"xGMI all-reduce supports {SUPPORTED_WORLD} ranks, not {world}")
+        self.rank, self.world, self.device = rank, world, device
+        self.cap = int(cap_bytes)
+        # one-shot reads (N-1) x bytes; two-shot 2(N-1)/N x bytes but two barriers
+        self.one_shot_max = one_shot_max if one_shot_max is not None else (
+            512 << 10 if world <= 2 else 256 << 10)
+        self._own, self._opened = 0, []
+        handle, err = None, None
+        try:
+            from .. import ops
+            ops.load_extension(strict=True)
+            k = torch.ops.kgc
+            with torch.cuda.device(device):
+                sig_bytes = int(k.ar_signal_bytes())
+                self._own = int(k.ar_alloc(sig_bytes + 2 * self.cap))
+                handle = k.ar_get_handle(self._own).tolist()
+        except Exception as e:  # noqa: BLE001
+            err = e
+        if not _agree(err is None, cpu_group):
+            self.close()
+            raise RuntimeError(f"xGMI all-reduce buffer allocation failed: {err}")
+        gathered: list = [None] * world
+        dist.all_gather_object(gathered, handle, group=cpu_group)
+        bases = []
+        try:
+            with torch.cuda.device(device):
+                for r, h in enumerate(gathered):
+                    if r == rank:
+                        bases.append(self._own)
+                    else:
+                        p = int(k.ar_open_handle(torch.tensor(h, dtype=torch.uint8)))
+                        self._opened.append(p)
+                        bases.append(p)
+        except Exception as e:  # noqa: BLE001
+            err = e
+        if not _agree(err is None, cpu_group):
+            self.close()
+            raise RuntimeError(f"xGMI all-reduce peer mapping failed: {err}")
+        self.sig = bases
+        self.data = [b + sig_bytes for b in bases]
+
+    def should_use(self, x: torch.Tensor) -> bool:
+        if not x.is_cuda or x.dtype not in (torch.bfloat16, torch.float16):
+            return False
+        nb = x.numel() * x.element_size()
+        return x.is_contiguous() and 0 < nb <= self.cap and nb % (16 * self.world) == 0
+
+    def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
+        nb = x.numel() * x.element_size()
+        torch.ops.kgc.xgmi_allreduce(x, self.data, self.sig, self.rank, self.cap,
+                                     nb > self.one_shot_max)
+        return x
+
+    def check(self) -> None:
+        """Raise if any barrier timed out waiting for a peer (see allreduce.hip)."""
+        err = int(torch.ops.kgc.ar_read_err(self.sig[self.rank]))
+        if err:
+            raise RuntimeError(f"xGMI all-reduce: peers {bin(err)} never arrived")
+
+    def close(self) -> None:
+        if self._own or self._opened:
+            torch.cuda.synchronize(self.device)
+            for p in self._opened:
+                torch.ops.kgc.ar_close_handle(p)
+            if self._own:
+                torch.ops.kgc.ar_free(self._own)
+            self._own = 0
+            self._opened = []
+
+
+def maybe_init_custom_allreduce(ps, device: torch.device) -> Optional[CustomAllReduce]:
+    """Build the xGMI all-reduce for this rank's TP group, or None (RCCL only).
+    All TP ranks agree: if any rank cannot set it up, none uses it."""
+    if os.environ.get("KGC_CUSTOM_AR", "1") == "0" or ps.tp_size not in SUPPORTED_WORLD:
+        return None
+    try:
+        car = CustomAllReduce(ps.tp_cpu_group, ps.tp_rank, ps.tp_size, device)
+    except RuntimeError as e:
+        log.warning("%s; using RCCL", e)
+        return None
+    log.info("xGMI all-reduce enabled: tp=%d cap=%d MiB one-shot<=%d KiB", ps.tp_size,
+             car.cap >> 20, car.one_shot_max >> 10)
+    return car

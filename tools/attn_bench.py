@@ -1,0 +1,73 @@
+"""Decode / prefill attention microbenchmark on realistic serving shapes.
+
+    python tools/attn_bench.py [--batch 256] [--ctx 640] [--nq 32 --nkv 8]
+
+Reports time per call and the KV bytes streamed per second (the decode kernel is
+HBM-bound: every cached K/V byte of every sequence is read once per step).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timeit(fn, iters=30):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    g.replay()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--ctx", type=int, default=640)
+    ap.add_argument("--nq", type=int, default=32)
+    ap.add_argument("--nkv", type=int, default=8)
+    ap.add_argument("--d", type=int, default=128)
+    ap.add_argument("--bs", type=int, default=32)
+    ap.add_argument("--max-len", type=int, default=4096)
+    a = ap.parse_args()
+    from kubernetes_gpu_cluster_amd import ops
+    dev = torch.device("cuda")
+    B, d, bs = a.batch, a.d, a.bs
+    nblk = math.ceil(a.ctx / bs)
+    NB = B * nblk + 16
+    kc = torch.randn(NB, a.nkv, bs, d, device=dev, dtype=torch.bfloat16)
+    vc = torch.randn(NB, a.nkv, bs // 8, d, 8, device=dev, dtype=torch.bfloat16)
+    maxb = math.ceil(a.max_len / bs)
+    perm = torch.randperm(NB - 1, device=dev)[: B * nblk] + 1
+    bt = torch.zeros(B, maxb, dtype=torch.int32, device=dev)
+    bt[:, :nblk] = perm.view(B, nblk).int()
+    # ragged contexts around --ctx (uniform +-25%)
+    ctx = (a.ctx * (0.75 + 0.25 * torch.rand(B, device=dev))).int().clamp(1, nblk * bs)
+    q = torch.randn(B, a.nq, d, device=dev, dtype=torch.bfloat16)
+    ws = ops.decode_partials(B, a.nq, d, maxb, bs, dev)
+    z = ops.decode_grid_z(B, a.nkv, a.max_len)
+    out = ops.paged_attention_decode(q, kc, vc, bt, ctx, d ** -0.5, ws, z)
+    from kubernetes_gpu_cluster_amd.ops import reference as R
+    n = min(B, 8)
+    ref = R.paged_attention_decode(q[:n].float(), kc.float(), vc.float(), bt[:n], ctx[:n], d ** -0.5)
+    err = (out[:n].float() - ref).abs().max().item()
+    t = timeit(lambda: ops.paged_attention_decode(q, kc, vc, bt, ctx, d ** -0.5, ws, z))
+    kv_bytes = int(ctx.sum()) * a.nkv * d * 2 * 2
+    print(json.dumps({"kernel": "paged_decode", "batch": B, "ctx_mean": float(ctx.float().mean()),
+                      "z": z, "max_err": round(err, 4), "us": round(t * 1e6, 2), "kv_TBps": round(kv_bytes / t / 1e12, 3)}))
+
+
+if __name__ == "__main__":
+    main()
