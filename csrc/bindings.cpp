@@ -207,6 +207,88 @@ void sample(Tensor out, Tensor logits, Tensor temperature, Tensor top_k, Tensor 
                      stream());
 }
 
+// ---- K13/K14 MoE
+void moe_route(Tensor topk_w, Tensor topk_ids, Tensor logits, bool renorm) {
+  check_gpu(logits, "logits");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "router logits [T, E] dense rows");
+  const int64_t T = logits.size(0), E = logits.size(1), k = topk_w.size(-1);
+  TORCH_CHECK(E >= 1 && E <= 64 && k >= 1 && k <= E, "1 <= k <= E <= 64");
+  TORCH_CHECK(topk_w.scalar_type() == at::kFloat && topk_w.is_contiguous() && topk_w.numel() == T * k,
+              "topk_w fp32 [T, k]");
+  TORCH_CHECK(topk_ids.scalar_type() == at::kInt && topk_ids.is_contiguous() &&
+              topk_ids.numel() == T * k, "topk_ids int32 [T, k]");
+  if (T == 0) return;
+  kgc::launch_moe_route(dt_code(logits), logits.data_ptr(), logits.stride(0), (int)T, (int)E,
+                        (int)k, renorm, topk_w.data_ptr<float>(), topk_ids.data_ptr<int>(), stream());
+}
+
+void moe_align(Tensor sorted_ids, Tensor block_expert, Tensor meta, Tensor topk_ids, int64_t e0,
+               int64_t E_local, int64_t bm) {
+  check_gpu(topk_ids, "topk_ids");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(topk_ids.device());
+  TORCH_CHECK(bm == 64 || bm == 128, "row block 64 or 128");
+  const int64_t npairs = topk_ids.numel();
+  const int64_t rows = sorted_ids.numel();
+  TORCH_CHECK(topk_ids.scalar_type() == at::kInt && topk_ids.is_contiguous(), "topk_ids int32");
+  TORCH_CHECK(E_local >= 1 && E_local <= 256, "1 <= local experts <= 256");
+  TORCH_CHECK(sorted_ids.scalar_type() == at::kInt && rows % bm == 0 &&
+              rows >= npairs + E_local * (bm - 1), "sorted_ids int32, >= pairs + E*(BM-1) rows");
+  TORCH_CHECK(block_expert.scalar_type() == at::kInt && block_expert.numel() >= rows / bm,
+              "block_expert int32 [rows / BM]");
+  TORCH_CHECK(meta.scalar_type() == at::kInt && meta.numel() >= 1, "meta int32");
+  kgc::launch_moe_align(topk_ids.data_ptr<int>(), (int)npairs, (int)e0, (int)E_local, (int)bm,
+                        (int)rows,
+                        sorted_ids.data_ptr<int>(), block_expert.data_ptr<int>(),
+                        meta.data_ptr<int>(), stream());
+}
+
+void moe_gemm(Tensor C, Tensor A, Tensor W, Tensor sorted_ids, Tensor block_expert, Tensor meta,
+              int64_t npairs, int64_t topk, int64_t bm, bool gather, bool scatter) {
+  check_gpu(A, "A");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(A.device());
+  TORCH_CHECK(bm == 64 || bm == 128, "row block 64 or 128");
+  TORCH_CHECK(W.dim() == 3 && W.is_contiguous(), "W [E, N, K] contiguous");
+  TORCH_CHECK(A.scalar_type() == W.scalar_type() && C.scalar_type() == W.scalar_type(),
+              "A, W, C share a dtype");
+  TORCH_CHECK(W.scalar_type() == at::kBFloat16 || W.scalar_type() == at::kHalf, "bf16 / fp16");
+  const int64_t N = W.size(1), K = W.size(2), rows = sorted_ids.numel();
+  TORCH_CHECK(N % kgc::moe_block_n() == 0 && K % kgc::moe_block_k() == 0,
+              "grouped GEMM needs N % 128 == 0 and K % 64 == 0");
+  TORCH_CHECK(A.dim() == 2 && A.size(1) == K && A.stride(1) == 1 && A.stride(0) % 8 == 0, "A [*, K]");
+  TORCH_CHECK(C.dim() == 2 && C.size(1) == N && C.stride(1) == 1 && C.stride(0) % 8 == 0, "C [*, N]");
+  TORCH_CHECK(rows % bm == 0 && block_expert.numel() >= rows / bm, "row blocks");
+  // every row index the kernel can touch must exist
+  if (gather) {
+    TORCH_CHECK(A.size(0) * topk >= npairs, "A has fewer token rows than pairs / k");
+  } else {
+    TORCH_CHECK(A.size(0) >= rows, "A must hold every padded row");
+  }
+  if (scatter) {
+    TORCH_CHECK(C.size(0) >= npairs, "C must hold every pair row");
+  } else {
+    TORCH_CHECK(C.size(0) >= rows, "C must hold every padded row");
+  }
+  if (rows == 0) return;
+  kgc::launch_moe_gemm(dt_code(W), (int)bm, C.data_ptr(), A.data_ptr(), W.data_ptr(),
+                       sorted_ids.data_ptr<int>(), block_expert.data_ptr<int>(), meta.data_ptr<int>(),
+                       (int)npairs, (int)topk, (int)N, (int)K, A.stride(0), C.stride(0),
+                       (int)(rows / bm), gather, scatter, stream());
+}
+
+void moe_combine(Tensor out, Tensor y, Tensor topk_w) {
+  check_gpu(y, "y");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(y.device());
+  const int64_t T = out.size(0), H = out.size(1), k = topk_w.size(-1);
+  TORCH_CHECK(out.is_contiguous() && y.is_contiguous() && H % 8 == 0, "contiguous, H % 8 == 0");
+  TORCH_CHECK(y.numel() >= T * k * H && topk_w.numel() == T * k && topk_w.scalar_type() == at::kFloat,
+              "y [T*k, H], topk_w fp32 [T, k]");
+  TORCH_CHECK(T <= 65535, "at most 65535 tokens per call");
+  if (T == 0) return;
+  kgc::launch_moe_combine(dt_code(out), out.data_ptr(), y.data_ptr(), topk_w.data_ptr<float>(),
+                          (int)T, (int)k, (int)H, stream());
+}
+
 // ---- K12 xGMI all-reduce: IPC buffers are raw device pointers carried as int64
 int64_t ar_signal_bytes() { return (int64_t)kgc::allreduce_signal_bytes(); }
 int64_t ar_alloc(int64_t bytes) { return (int64_t)(intptr_t)kgc::ar_alloc(bytes); }
@@ -267,6 +349,12 @@ TORCH_LIBRARY(kgc, m) {
   m.def("sample(Tensor(a!) out, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, "
         "Tensor seeds) -> ()");
   m.def("decode_partition_size() -> int", &decode_partition_size);
+  m.def("moe_route(Tensor(a!) topk_w, Tensor(b!) topk_ids, Tensor logits, bool renorm) -> ()");
+  m.def("moe_align(Tensor(a!) sorted_ids, Tensor(b!) block_expert, Tensor(c!) meta, "
+        "Tensor topk_ids, int e0, int E_local, int bm) -> ()");
+  m.def("moe_gemm(Tensor(a!) C, Tensor A, Tensor W, Tensor sorted_ids, Tensor block_expert, "
+        "Tensor meta, int npairs, int topk, int bm, bool gather, bool scatter) -> ()");
+  m.def("moe_combine(Tensor(a!) out, Tensor y, Tensor topk_w) -> ()");
   m.def("ar_signal_bytes() -> int", &ar_signal_bytes);
   m.def("ar_alloc(int bytes) -> int", &ar_alloc);
   m.def("ar_free(int ptr) -> ()", &ar_free);
@@ -288,4 +376,8 @@ TORCH_LIBRARY_IMPL(kgc, CUDA, m) {
   m.impl("prefill_attention", &prefill_attention);
   m.impl("sample", &sample);
   m.impl("xgmi_allreduce", &xgmi_allreduce);
+  m.impl("moe_route", &moe_route);
+  m.impl("moe_align", &moe_align);
+  m.impl("moe_gemm", &moe_gemm);
+  m.impl("moe_combine", &moe_combine);
 }

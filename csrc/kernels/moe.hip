@@ -1,0 +1,315 @@
+// K13 / K14: Mixtral sparse-MoE on gfx950 (reference model deployed
+// through values files, BASELINE config 4 "Mixtral 8x7B pod (MoE grouped GEMM ...)").
+//
+//   moe_route   : router logits [T, E] -> softmax -> top-k (renormalised) weights/ids.
+//                 One wave per token, experts on lanes (E <= 64).
+//   moe_align   : bucket the T*k (token, slot) pairs by expert, each bucket padded to
+//                 BM rows; emits sorted pair ids, the expert of every BM-row block
+//                 and the block count.  One workgroup, LDS counters -- all on device,
+//                 so the whole MoE block is hipGraph-capturable (no host sync).
+//   moe_gemm    : grouped GEMM over those row blocks.  Block (mb, nb) multiplies
+//                 BM rows of one expert by a MG_BN-column slice of that expert's
+//                 weight [N, K] on MFMA 16x16x32; A rows are gathered from the token
+//                 matrix (first GEMM) or read contiguously (second GEMM); the second
+//                 GEMM scatters rows back to pair order.  M-blocks run fastest in the
+//                 grid so the blocks sharing a weight slice run together (L2/MALL reuse).
+//   moe_combine : out[t] = sum_j w[t, j] * y[t*k + j]   (fp32 accumulation).
+#include "common.h"
+#include "launch.h"
+
+namespace kgc {
+
+constexpr int MG_BN = 128, MG_BK = 64, MG_THREADS = 256;
+// Row-block height: 64 or 128, chosen per call so that a decode step's typical bucket
+// (T*k/E rows) fits ONE block -- every extra block of an expert re-streams its weights.
+
+// ---------------------------------------------------------------------------- route
+template <typename T>
+__global__ __launch_bounds__(256) void moe_route_kernel(const T* __restrict__ logits,
+                                                        int64_t stride, int ntok, int E, int k,
+                                                        int renorm, float* __restrict__ topk_w,
+                                                        int* __restrict__ topk_ids) {
+  const int lane = threadIdx.x & 63;
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= ntok) return;
+  float v = lane < E ? to_f<T>(logits[(int64_t)t * stride + lane]) : -INFINITY;
+  const float m = wave_max(v);
+  float p = lane < E ? __expf(v - m) : 0.f;
+  const float s = wave_sum(p);
+  p = lane < E ? p / s : -1.f;
+  float wsel = 0.f, wsum = 0.f;
+  int isel = 0;
+  for (int j = 0; j < k; ++j) {
+    const float best = wave_max(p);
+    // lowest expert index among the maxima (torch.topk order for ties is unspecified;
+    // lowest-index is deterministic)
+    const uint64_t hit = __ballot(p == best);
+    const int e = __ffsll((unsigned long long)hit) - 1;
+    if (lane == j) {
+      wsel = best;
+      isel = e;
+    }
+    wsum += best;
+    if (lane == e) p = -1.f;
+  }
+  if (lane < k) {
+    topk_w[(int64_t)t * k + lane] = renorm ? wsel / wsum : wsel;
+    topk_ids[(int64_t)t * k + lane] = isel;
+  }
+}
+
+// ---------------------------------------------------------------------------- align
+// sorted_ids: [max_rows] pair ids (padding = npairs); block_expert: [max_rows / bm]
+// local expert per row block; meta[0] = number of row blocks in use.
+__global__ __launch_bounds__(1024) void moe_align_kernel(const int* __restrict__ topk_ids,
+                                                         int npairs, int e0, int E_local, int bm,
+                                                         int max_rows, int* __restrict__ sorted_ids,
+                                                         int* __restrict__ block_expert,
+                                                         int* __restrict__ meta) {
+  __shared__ int cnt[256], off[257], cur[256];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < E_local; e += blockDim.x) {
+    cnt[e] = 0;
+    cur[e] = 0;
+  }
+  for (int r = tid; r < max_rows; r += blockDim.x) sorted_ids[r] = npairs;
+  __syncthreads();
+  for (int p = tid; p < npairs; p += blockDim.x) {
+    const int e = topk_ids[p] - e0;
+    if (e >= 0 && e < E_local) atomicAdd(&cnt[e], 1);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int e = 0; e < E_local; ++e) {
+      off[e] = acc;
+      acc += (cnt[e] + bm - 1) / bm * bm;
+    }
+    off[E_local] = acc;
+    meta[0] = acc / bm;
+  }
+  __syncthreads();
+  const int nblk = off[E_local] / bm;
+  for (int b = tid; b < max_rows / bm; b += blockDim.x) {
+    int e = -1;
+    if (b < nblk) {
+      const int row = b * bm;
+      for (int q = 0; q < E_local; ++q)
+        if (row >= off[q] && row < off[q + 1]) e = q;
+    }
+    block_expert[b] = e;
+  }
+  __syncthreads();
+  for (int p = tid; p < npairs; p += blockDim.x) {
+    const int e = topk_ids[p] - e0;
+    if (e >= 0 && e < E_local) sorted_ids[off[e] + atomicAdd(&cur[e], 1)] = p;
+  }
+}
+
+// ---------------------------------------------------------------------------- grouped GEMM
+__device__ __forceinline__ int mg_swz(int row, int chunk) {   // 16-B chunk index in LDS row
+  return row * (MG_BK / 8) + (chunk ^ (row & 7));
+}
+
+// GATHER: A row r = x[sorted_ids[r] / topk]  (else A row r = A[r]);
+// SCATTER: C row sorted_ids[r] (skip padding)  (else C row r).
+template <typename T, int BM, bool GATHER, bool SCATTER>
+__global__ __launch_bounds__(MG_THREADS, 2) void moe_gemm_kernel(
+    T* __restrict__ C, const T* __restrict__ A, const T* __restrict__ W,
+    const int* __restrict__ sorted_ids, const int* __restrict__ block_expert,
+    const int* __restrict__ meta, int npairs, int topk, int N, int K, int64_t lda,
+    int64_t ldc) {
+  const int mb = blockIdx.x, nb = blockIdx.y;
+  if (mb >= meta[0]) return;
+  const int e = block_expert[mb];
+  if (e < 0) return;
+  constexpr int AC = BM / 32;     // A chunks per thread; also 16-row M tiles per wave
+  __shared__ u32x4 lds[2 * (BM + MG_BN) * (MG_BK / 8)];
+  u32x4* As = lds;                                   // [2][BM * 8]
+  u32x4* Bs = lds + 2 * BM * (MG_BK / 8);            // [2][MG_BN * 8]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, q4 = lane >> 4;
+
+  // global -> register staging assignment: A AC chunks/thread, B 4 chunks/thread
+  const int chunk = tid & 7;
+  const T* a_ptr[AC];
+#pragma unroll
+  for (int i = 0; i < AC; ++i) {
+    const int row = (tid >> 3) + 32 * i;
+    const int r = mb * BM + row;
+    int64_t arow;
+    if constexpr (GATHER) {
+      const int p = sorted_ids[r];
+      arow = p < npairs ? p / topk : 0;
+    } else {
+      arow = r;
+    }
+    a_ptr[i] = A + arow * lda + chunk * 8;
+  }
+  const T* w_ptr = W + ((int64_t)e * N + (int64_t)nb * MG_BN + (tid >> 3)) * K + chunk * 8;
+  u32x4 ra[AC], rb[4];
+  auto gload = [&](int kb) {
+    const int ko = kb * MG_BK;
+#pragma unroll
+    for (int i = 0; i < AC; ++i) ra[i] = *reinterpret_cast<const u32x4*>(a_ptr[i] + ko);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      rb[i] = *reinterpret_cast<const u32x4*>(w_ptr + (int64_t)32 * i * K + ko);
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < AC; ++i) As[buf * BM * 8 + mg_swz((tid >> 3) + 32 * i, chunk)] = ra[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) Bs[buf * MG_BN * 8 + mg_swz((tid >> 3) + 32 * i, chunk)] = rb[i];
+  };
+
+  const int wm = wave >> 1, wn = wave & 1;   // wave tile: BM/2 rows x 64 cols
+  f32x4 acc[AC][4];
+#pragma unroll
+  for (int i = 0; i < AC; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / MG_BK;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kb = 0; kb < nk; ++kb) {
+    const int buf = kb & 1;
+    if (kb + 1 < nk) gload(kb + 1);
+#pragma unroll
+    for (int ks = 0; ks < MG_BK / 32; ++ks) {
+      Pack8<T> af[AC], bf[4];
+#pragma unroll
+      for (int mt = 0; mt < AC; ++mt)
+        af[mt].u = As[buf * BM * 8 + mg_swz(wm * (BM / 2) + mt * 16 + r16, ks * 4 + q4)];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        bf[nt].u = Bs[buf * MG_BN * 8 + mg_swz(wn * 64 + nt * 16 + r16, ks * 4 + q4)];
+#pragma unroll
+      for (int mt = 0; mt < AC; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = mfma16x16x32(af[mt].v, bf[nt].v, acc[mt][nt]);
+    }
+    if (kb + 1 < nk) lstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane holds C[4*q4 + i][r16] of each 16x16 tile
+#pragma unroll
+  for (int mt = 0; mt < AC; ++mt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = mb * BM + wm * (BM / 2) + mt * 16 + 4 * q4 + i;
+      int64_t crow = r;
+      if constexpr (SCATTER) {
+        const int p = sorted_ids[r];
+        if (p >= npairs) continue;
+        crow = p;
+      }
+      T* crow_ptr = C + crow * ldc + (int64_t)nb * MG_BN + wn * 64 + r16;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) crow_ptr[nt * 16] = from_f<T>(acc[mt][nt][i]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- combine
+template <typename T>
+__global__ __launch_bounds__(256) void moe_combine_kernel(T* __restrict__ out,
+                                                          const T* __restrict__ y,
+                                                          const float* __restrict__ topk_w,
+                                                          int k, int H) {
+  const int t = blockIdx.y;
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c >= H) return;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < k; ++j) {
+    const float w = topk_w[(int64_t)t * k + j];
+    Pack8<T> v;
+    v.u = *reinterpret_cast<const u32x4*>(y + ((int64_t)t * k + j) * H + c);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] += w * to_f<T>(v.h[q]);
+  }
+  Pack8<T> o;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) o.h[q] = from_f<T>(acc[q]);
+  *reinterpret_cast<u32x4*>(out + (int64_t)t * H + c) = o.u;
+}
+
+// ---------------------------------------------------------------------------- launchers
+int moe_block_n() { return MG_BN; }
+int moe_block_k() { return MG_BK; }
+
+void launch_moe_route(int dtype, const void* logits, int64_t stride, int ntok, int E, int k,
+                      bool renorm, float* topk_w, int* topk_ids, hipStream_t s) {
+  const dim3 grid((ntok + 3) / 4);
+  if (dtype == DT_BF16)
+    moe_route_kernel<bf16><<<grid, 256, 0, s>>>((const bf16*)logits, stride, ntok, E, k, renorm,
+                                                topk_w, topk_ids);
+  else if (dtype == DT_F16)
+    moe_route_kernel<f16><<<grid, 256, 0, s>>>((const f16*)logits, stride, ntok, E, k, renorm,
+                                               topk_w, topk_ids);
+  else
+    moe_route_kernel<float><<<grid, 256, 0, s>>>((const float*)logits, stride, ntok, E, k, renorm,
+                                                 topk_w, topk_ids);
+}
+
+void launch_moe_align(const int* topk_ids, int npairs, int e0, int E_local, int bm, int max_rows,
+                      int* sorted_ids, int* block_expert, int* meta, hipStream_t s) {
+  moe_align_kernel<<<1, 1024, 0, s>>>(topk_ids, npairs, e0, E_local, bm, max_rows, sorted_ids,
+                                      block_expert, meta);
+}
+
+template <typename T, int BM>
+static void moe_gemm_bm(void* C, const void* A, const void* W, const int* sorted_ids,
+                        const int* block_expert, const int* meta, int npairs, int topk, int N,
+                        int K, int64_t lda, int64_t ldc, int max_mblocks, bool gather,
+                        bool scatter, hipStream_t s) {
+  const dim3 grid(max_mblocks, N / MG_BN);
+#define MG_LAUNCH(G, S)                                                                      \
+  moe_gemm_kernel<T, BM, G, S><<<grid, MG_THREADS, 0, s>>>((T*)C, (const T*)A, (const T*)W,   \
+                                                           sorted_ids, block_expert, meta,    \
+                                                           npairs, topk, N, K, lda, ldc)
+  if (gather && !scatter) MG_LAUNCH(true, false);
+  else if (!gather && scatter) MG_LAUNCH(false, true);
+  else if (gather && scatter) MG_LAUNCH(true, true);
+  else MG_LAUNCH(false, false);
+#undef MG_LAUNCH
+}
+
+template <typename T>
+static void moe_gemm_t(int bm, void* C, const void* A, const void* W, const int* sorted_ids,
+                       const int* block_expert, const int* meta, int npairs, int topk, int N,
+                       int K, int64_t lda, int64_t ldc, int max_mblocks, bool gather,
+                       bool scatter, hipStream_t s) {
+  if (bm == 128)
+    moe_gemm_bm<T, 128>(C, A, W, sorted_ids, block_expert, meta, npairs, topk, N, K, lda, ldc,
+                        max_mblocks, gather, scatter, s);
+  else
+    moe_gemm_bm<T, 64>(C, A, W, sorted_ids, block_expert, meta, npairs, topk, N, K, lda, ldc,
+                       max_mblocks, gather, scatter, s);
+}
+
+void launch_moe_gemm(int dtype, int bm, void* C, const void* A, const void* W,
+                     const int* sorted_ids, const int* block_expert, const int* meta, int npairs,
+                     int topk, int N, int K, int64_t lda, int64_t ldc, int max_mblocks,
+                     bool gather, bool scatter, hipStream_t s) {
+  if (dtype == DT_BF16)
+    moe_gemm_t<bf16>(bm, C, A, W, sorted_ids, block_expert, meta, npairs, topk, N, K, lda, ldc,
+                     max_mblocks, gather, scatter, s);
+  else
+    moe_gemm_t<f16>(bm, C, A, W, sorted_ids, block_expert, meta, npairs, topk, N, K, lda, ldc,
+                    max_mblocks, gather, scatter, s);
+}
+
+void launch_moe_combine(int dtype, void* out, const void* y, const float* topk_w, int ntok, int k,
+                        int H, hipStream_t s) {
+  const dim3 grid((H / 8 + 255) / 256, ntok);
+  if (dtype == DT_BF16)
+    moe_combine_kernel<bf16><<<grid, 256, 0, s>>>((bf16*)out, (const bf16*)y, topk_w, k, H);
+  else
+    moe_combine_kernel<f16><<<grid, 256, 0, s>>>((f16*)out, (const f16*)y, topk_w, k, H);
+}
+
+}  // namespace kgc

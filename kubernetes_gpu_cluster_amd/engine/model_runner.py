@@ -379,7 +379,8 @@ class ModelRunner:
         """Capture decode forward + LM head for each batch bucket (largest first,
         sharing one memory pool).  Returns seconds spent."""
         self.buckets = graph_buckets(self.graph_max_bs)
-        if not self.use_graphs or not (self.model.first and self.model.last):
+        if (not self.use_graphs or not (self.model.first and self.model.last)
+                or not getattr(self.model, "graph_safe", True)):
             self.use_graphs = False
             return 0.0
         if self.ps.tp_size > 1 and comm.get_custom_allreduce() is None:

@@ -128,6 +128,11 @@ class LlamaForCausalLM(nn.Module):
     def num_local_layers(self) -> int:
         return self.end - self.start
 
+    @property
+    def graph_safe(self) -> bool:
+        """False when a layer synchronises with the host (MoE ep mode / uncovered dims)."""
+        return all(getattr(l.mlp, "graph_safe", True) for l in self.layers)
+
     def local_kv_heads(self) -> int:
         return self.layers[0].self_attn.nkv if len(self.layers) else 0
 

@@ -8,11 +8,17 @@ Expert placement over the TP group (``--moe-parallel``):
   to the owning rank with an all-to-all (C7), processed by the local grouped
   MLP, and the weighted results are returned with a second all-to-all.
 
-The grouped MLP sorts the (token, expert) pairs by expert and runs one GEMM pair
-per non-empty expert on contiguous row ranges (hipBLASLt), with the SiLU-mul
-(K7) in between and a weighted index_add combine.
+On the GPU the whole block is native and host-sync free (so decode graphs capture
+it): router GEMM -> ``moe_route`` (K13) -> ``moe_align`` bucketing -> grouped MFMA
+GEMM (gate/up, rows gathered) -> silu_mul (K7) -> grouped GEMM (down, rows
+scattered back) -> weighted ``moe_combine`` (csrc/kernels/moe.hip).  The CPU path
+(and shapes the grouped-GEMM tiles do not cover) sorts the pairs by expert and runs
+one GEMM pair per non-empty expert; ``ep`` mode needs the per-rank counts on the
+host for the variable-size all-to-all, so it runs eagerly (no decode graphs).
 """
 from __future__ import annotations
+
+import logging
 
 import torch
 import torch.distributed as dist
@@ -20,12 +26,12 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from ..ops import reference as ref
 from ..parallel import comm
 from ..parallel.layers import ReplicatedLinear
 from ..parallel.state import get_state
 from .configs import ModelConfig
 
+log = logging.getLogger("kgc.moe")
 MOE_MODE = {"mode": "tp"}
 
 
@@ -81,6 +87,22 @@ class MoEBlock(nn.Module):
                                             device=device), requires_grad=False)
         self.w2 = nn.Parameter(torch.empty(self.E_local, H, self.I_local, dtype=dtype,
                                            device=device), requires_grad=False)
+        self.native = (torch.device(device).type == "cuda" and
+                       ops.moe_supported(2 * self.I_local, H) and ops.moe_supported(H, self.I_local))
+        if torch.device(device).type == "cuda" and not self.native:
+            log.warning("MoE dims (2I=%d, H=%d) not covered by the grouped GEMM tiles; "
+                        "using the per-expert path (no decode graphs)", 2 * self.I_local, H)
+        # decode hipGraphs need a block with no host synchronisation
+        self.graph_safe = self.native and self.mode == "tp"
+
+    def experts(self, x, topk_w, topk_ids, expert_offset: int = 0, all_local: bool = True):
+        # the grouped kernel streams each expert's weights once per row block: best at
+        # decode sizes; big prefill buckets run faster as one hipBLASLt GEMM per expert
+        # (host sync is fine there -- prefill is never graph-captured)
+        small = topk_ids.numel() <= ops.MOE_NATIVE_MAX_ROWS * self.E_local
+        if self.native and x.is_cuda and (small or torch.cuda.is_current_stream_capturing()):
+            return ops.fused_moe(x, self.w13, self.w2, topk_w, topk_ids, expert_offset, all_local)
+        return grouped_expert_mlp(x, self.w13, self.w2, topk_w, topk_ids, expert_offset)
 
     def map_weight(self, rest: str):
         """Checkpoint names under ``block_sparse_moe.``: gate.weight,
@@ -121,10 +143,9 @@ class MoEBlock(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         logits = self.gate(x)
-        topk_w, topk_ids = ref.moe_topk_softmax(logits, self.k)
+        topk_w, topk_ids = ops.moe_topk_softmax(logits, self.k)
         if self.mode == "tp":
-            y = grouped_expert_mlp(x, self.w13, self.w2, topk_w, topk_ids)
-            return comm.tp_all_reduce(y)
+            return comm.tp_all_reduce(self.experts(x, topk_w, topk_ids))
         return self._forward_ep(x, topk_w, topk_ids)
 
     def _forward_ep(self, x, topk_w, topk_ids):
@@ -148,8 +169,8 @@ class MoEBlock(nn.Module):
         recv_ids = torch.empty(sum(rc), 2, dtype=send_meta.dtype, device=x.device)
         dist.all_to_all_single(recv_ids, send_meta, rc, sc, group=s.tp_group)
         ones = torch.ones(recv_x.shape[0], 1, dtype=torch.float32, device=x.device)
-        y = grouped_expert_mlp(recv_x, self.w13, self.w2, ones, recv_ids[:, :1].to(torch.int32),
-                               expert_offset=self.e0)
+        y = self.experts(recv_x, ones, recv_ids[:, :1].to(torch.int32).contiguous(),
+                         expert_offset=self.e0)
         back = torch.empty(order.numel(), H, dtype=x.dtype, device=x.device)
         dist.all_to_all_single(back, y, sc, rc, group=s.tp_group)
         out = torch.zeros(T, H, dtype=torch.float32, device=x.device)

@@ -212,3 +212,56 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
 __all__ = ["load_extension", "rms_norm", "fused_add_rms_norm", "layer_norm", "silu_mul",
            "rope_kv_write", "paged_attention_decode", "prefill_attention", "sample",
            "decode_partials", "decode_grid_z", "prefill_work_list", "ref"]
+
+
+# ------------------------------------------------------------------ MoE (K13 / K14)
+MOE_NATIVE_MAX_ROWS = 128   # mean rows per expert above which hipBLASLt per expert wins
+
+
+def moe_supported(n: int, k: int) -> bool:
+    """Shapes the grouped GEMM tiles cover: N % 128 == 0 and K % 64 == 0."""
+    return n % 128 == 0 and k % 64 == 0
+
+
+def moe_topk_softmax(router_logits: torch.Tensor, k: int, renormalize: bool = True):
+    """K13: (weights fp32 [T, k], expert ids int32 [T, k])."""
+    if not _gpu(router_logits):
+        return ref.moe_topk_softmax(router_logits, k, renormalize)
+    T = router_logits.shape[0]
+    w = torch.empty(T, k, dtype=torch.float32, device=router_logits.device)
+    ids = torch.empty(T, k, dtype=torch.int32, device=router_logits.device)
+    _k().moe_route(w, ids, router_logits, renormalize)
+    return w, ids
+
+
+def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
+              topk_ids: torch.Tensor, expert_offset: int = 0,
+              all_local: bool = True) -> torch.Tensor:
+    """K14: sum_j topk_w[t, j] * MLP_{topk_ids[t, j]}(x[t]) for the experts held here
+    (global ids ``expert_offset .. expert_offset + w13.shape[0]``).  x [T, H];
+    w13 [E, 2I, H] (gate rows then up rows); w2 [E, H, I].  No host synchronisation:
+    bucket sizes stay on the device, so the block is captured in decode graphs."""
+    if not _gpu(x):
+        return ref.moe_mlp_local(x, w13, w2, topk_w, topk_ids, expert_offset)
+    k = _k()
+    T, H = x.shape
+    E, I2 = w13.shape[0], w13.shape[1]
+    topk = topk_ids.shape[1]
+    npairs = T * topk
+    bm = 64 if npairs <= 40 * E else 128   # one row block per expert at decode sizes
+    rows = (npairs + E * (bm - 1) + bm - 1) // bm * bm
+    dev = x.device
+    sorted_ids = torch.empty(rows, dtype=torch.int32, device=dev)
+    block_expert = torch.empty(rows // bm, dtype=torch.int32, device=dev)
+    meta = torch.empty(1, dtype=torch.int32, device=dev)
+    ids = topk_ids.contiguous()
+    k.moe_align(sorted_ids, block_expert, meta, ids, expert_offset, E, bm)
+    inter = torch.empty(rows, I2, dtype=x.dtype, device=dev)
+    k.moe_gemm(inter, x.contiguous(), w13, sorted_ids, block_expert, meta, npairs, topk, bm,
+               True, False)
+    act = silu_mul(inter)
+    y = (torch.empty if all_local else torch.zeros)(npairs, H, dtype=x.dtype, device=dev)
+    k.moe_gemm(y, act, w2, sorted_ids, block_expert, meta, npairs, topk, bm, False, True)
+    out = torch.empty(T, H, dtype=x.dtype, device=dev)
+    k.moe_combine(out, y, topk_w.contiguous().float())
+    return out

@@ -255,6 +255,23 @@ def moe_topk_softmax(router_logits: torch.Tensor, k: int, renormalize: bool = Tr
     return w, ids.to(torch.int32)
 
 
+def moe_mlp_local(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
+                  topk_ids: torch.Tensor, expert_offset: int = 0) -> torch.Tensor:
+    """K14 over the experts held locally (global ids offset by ``expert_offset``); pairs
+    routed elsewhere contribute nothing.  Expert outputs are rounded to x.dtype before
+    the fp32 weighted combine, like the kernel."""
+    T, H = x.shape
+    out = torch.zeros(T, H, dtype=torch.float32, device=x.device)
+    for e in range(w13.shape[0]):
+        tok, slot = torch.nonzero(topk_ids == e + expert_offset, as_tuple=True)
+        if tok.numel() == 0:
+            continue
+        h = silu_mul((x[tok].float() @ w13[e].float().t()).to(x.dtype).float())
+        y = (h.to(x.dtype).float() @ w2[e].float().t()).to(x.dtype)
+        out.index_add_(0, tok, y.float() * topk_w[tok, slot, None].float())
+    return out.to(x.dtype)
+
+
 def moe_mlp(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
             topk_ids: torch.Tensor) -> torch.Tensor:
     """K14: per-expert SwiGLU MLP, weighted combine.  w13 [E, 2I, H], w2 [E, H, I]."""

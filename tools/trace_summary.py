@@ -1,6 +1,7 @@
 """Summarise a rocprofv3 kernel trace of a bench run.
 
     python tools/trace_summary.py gpurun_out/prof2/runc/<pid>_kernel_trace.csv [--steps]
+    python tools/trace_summary.py gpurun_out/prof4/run_results.db [--steps]   (rocpd)
 
 Prints the per-kernel totals and, with --steps, the steady-state decode-step
 anatomy: per step (delimited by the sampler kernel) the span, GPU-busy time,
@@ -23,10 +24,21 @@ def family(name: str) -> str:
     return n[:60]
 
 
+def load(path: str):
+    """(start_ns, end_ns, kernel name) of every dispatch, from a rocprofv3 kernel-trace
+    CSV or a rocpd SQLite database (rocprofv3's default output format on ROCm 7)."""
+    if path.endswith(".db"):
+        import sqlite3
+        con = sqlite3.connect(path)
+        return sorted(con.execute("select start, end, name from kernels"))
+    rows = list(csv.DictReader(open(path)))
+    return sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
+                  for r in rows)
+
+
 def main():
     path = sys.argv[1]
-    rows = list(csv.DictReader(open(path)))
-    ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
+    ev = load(path)
     tot = collections.Counter()
     cnt = collections.Counter()
     for s, e, n in ev:
