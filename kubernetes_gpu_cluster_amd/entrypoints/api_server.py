@@ -87,23 +87,56 @@ def _err(status: int, msg: str, typ: str = "invalid_request_error") -> JSONRespo
 
 
 class _Detok:
-    """Incremental detokenizer with stop-string truncation."""
+    """Incremental detokenizer with stop-string truncation.
+
+    Decodes only a short window per update (tokens since the last emitted text, plus
+    a few before for merge context), so a streamed response costs O(n), not O(n^2)
+    full re-decodes.  A window ending in U+FFFD (an incomplete multi-byte sequence)
+    is held back until the next token completes it.  With stop strings, the last
+    ``max(len(stop)) - 1`` characters are withheld from the stream until they can no
+    longer start a stop string, so a stop string split over two updates is never
+    partially emitted; ``flush()`` releases them at the end."""
+
+    CONTEXT = 5
 
     def __init__(self, tok, stops: list[str]):
         self.tok, self.stops = tok, [s for s in stops if s]
-        self.text = ""
+        self.text = ""          # accepted text (truncated at a stop string)
         self.stopped = False
+        self._emitted = 0       # characters of self.text already returned
+        self._hold = max((len(s) for s in self.stops), default=1) - 1
+        self._prefix = 0        # window start (context tokens already decoded)
+        self._read = 0          # tokens whose text is already in self.text
 
     def update(self, ids: list[int]) -> str:
-        full = self.tok.decode(ids)
-        for s in self.stops:
-            i = full.find(s)
-            if i >= 0:
-                full = full[:i]
+        if self.stopped or len(ids) <= self._read:
+            return ""
+        before = self.tok.decode(ids[self._prefix:self._read]) if self._read > self._prefix else ""
+        after = self.tok.decode(ids[self._prefix:])
+        if after.endswith("\ufffd") or not after.startswith(before):
+            return ""
+        self._read = len(ids)
+        self._prefix = max(0, self._read - self.CONTEXT)
+        old = len(self.text)
+        self.text += after[len(before):]
+        if self.stops:
+            start = max(0, old - self._hold)      # a stop may straddle old text and delta
+            hits = [i for i in (self.text.find(s, start) for s in self.stops) if i >= 0]
+            if hits:
+                self.text = self.text[:min(hits)]
                 self.stopped = True
-        delta = full[len(self.text):] if full.startswith(self.text) else full
-        self.text = full
-        return delta
+                return self.flush()
+        end = len(self.text) - self._hold
+        if end <= self._emitted:
+            return ""
+        out = self.text[self._emitted:end]
+        self._emitted = end
+        return out
+
+    def flush(self) -> str:
+        out = self.text[self._emitted:]
+        self._emitted = len(self.text)
+        return out
 
 
 def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len: int) -> FastAPI:
@@ -130,6 +163,8 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
                         reason = out.finish_reason if out.finished else None
                         if detok.stopped:
                             reason = "stop"
+                        elif reason:
+                            delta += detok.flush()
                         if delta or reason:
                             yield f"data: {json.dumps(stream_fn(delta, reason))}\n\n"
                         if detok.stopped:

@@ -301,8 +301,11 @@ def main(argv=None):
     p.add_argument("--routing-logic", "--policy", dest="policy", default="least-outstanding",
                    choices=["least-outstanding", "round-robin", "session"])
     p.add_argument("--health-interval", type=float, default=5.0)
+    p.add_argument("--access-log", action="store_true", help="log every proxied request")
     a = p.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
+    if not a.access_log:
+        logging.getLogger("aiohttp.access").setLevel(logging.WARNING)
     r = Router([u for u in a.backends.split(",") if u], a.policy, a.health_interval,
                k8s_selector=a.k8s_label_selector, k8s_namespace=a.k8s_namespace,
                k8s_port=a.k8s_port, dns_service=a.dns_service)

@@ -69,3 +69,30 @@ def test_errors(client):
     assert r.status_code == 400
     r = client.post("/v1/completions", json={"prompt": "x", "n": 2})
     assert r.status_code == 400
+
+
+class _ByteTok:
+    """ids are UTF-8 bytes; decode like a byte-level BPE (invalid tails -> U+FFFD)."""
+
+    def decode(self, ids):
+        return bytes(ids).decode("utf-8", errors="replace")
+
+
+def test_incremental_detok_matches_full_decode():
+    from kubernetes_gpu_cluster_amd.entrypoints.api_server import _Detok
+    text = "héllo wörld — ünïcode ✓ end"
+    ids = list(text.encode())
+    d = _Detok(_ByteTok(), [])
+    out = "".join(d.update(ids[:i]) for i in range(1, len(ids) + 1)) + d.flush()
+    assert out == text == d.text
+    d2 = _Detok(_ByteTok(), ["zz", "longer-stop"])   # holdback, no stop hit
+    out2 = "".join(d2.update(ids[:i]) for i in range(1, len(ids) + 1)) + d2.flush()
+    assert out2 == text and not d2.stopped
+
+
+def test_incremental_detok_stop_straddles_updates():
+    from kubernetes_gpu_cluster_amd.entrypoints.api_server import _Detok
+    ids = list("abc STOP def".encode())
+    d = _Detok(_ByteTok(), ["STOP"])
+    out = "".join(d.update(ids[:i]) for i in range(1, len(ids) + 1))
+    assert d.stopped and out == "abc " and d.text == "abc "
