@@ -113,6 +113,10 @@ def launch(a) -> list[subprocess.Popen]:
                "--uvicorn-log-level", "warning"] + a.engine_args
         procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
         backends.append(f"http://127.0.0.1:{port}")
+    if a.no_router:
+        asyncio.run(wait_healthy(backends, a.startup_timeout))
+        a.base_url = backends[0]
+        return procs
     cmd = [sys.executable, "-m", "kubernetes_gpu_cluster_amd.router.router", "--host", "127.0.0.1",
            "--port", str(a.router_port), "--backends", ",".join(backends)]
     procs.append(subprocess.Popen(cmd, env=env0, start_new_session=True))
@@ -136,6 +140,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--engine-port", type=int, default=8100)
     ap.add_argument("--router-port", type=int, default=8080)
+    ap.add_argument("--no-router", action="store_true", help="--launch: hit engine 0 directly")
     ap.add_argument("--max-num-seqs", type=int, default=256)
     ap.add_argument("--max-model-len", type=int, default=4096)
     ap.add_argument("--startup-timeout", type=float, default=900)

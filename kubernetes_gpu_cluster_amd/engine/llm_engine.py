@@ -103,6 +103,7 @@ class LLMEngine:
                 seq.num_computed += 1
             for seq in samplers:
                 seq.output_token_ids.append(_PENDING)
+                seq.num_pending += 1
                 if len(seq.output_token_ids) >= seq.max_tokens or seq.num_tokens >= self.max_model_len:
                     # finished by length: release now (stream order protects the KV
                     # blocks still being written by the in-flight step)
@@ -121,10 +122,10 @@ class LLMEngine:
         for seq, tok in zip(samplers, tokens):
             if seq.finish_reason not in (None, "length"):
                 continue        # finished earlier (EOS seen one step late) or aborted
-            try:
-                idx = seq.output_token_ids.index(_PENDING)
-            except ValueError:
+            if seq.num_pending == 0:
                 continue
+            idx = len(seq.output_token_ids) - seq.num_pending
+            seq.num_pending -= 1
             seq.output_token_ids[idx] = tok
             if seq.first_token_time is None:
                 seq.first_token_time = now
@@ -133,16 +134,17 @@ class LLMEngine:
             if reason is not None and not seq.finished:
                 # EOS / stop token: drop tokens launched after this one
                 del seq.output_token_ids[idx + 1:]
+                seq.num_pending = 0
                 self.scheduler.finish(seq, reason)
                 self.seqs.pop(seq.request_id, None)
-            if reason is not None and _PENDING not in seq.output_token_ids:
+            if reason is not None and seq.num_pending == 0:
                 seq.finish_time = now
                 self.metrics.on_finish(seq)
                 done = True
             else:
                 done = False
             outs.append(RequestOutput(seq.request_id, seq.prompt_token_ids, [tok],
-                                      list(seq.output_token_ids), done, reason if done else None,
+                                      seq.output_token_ids, idx + 1, done, reason if done else None,
                                       seq.arrival_time, seq.first_token_time, seq.finish_time,
                                       seq.num_preemptions))
         self.metrics.on_step(plan, now - t0, len(samplers), self.bm.usage(),
@@ -174,7 +176,8 @@ class LLMEngine:
                 self.seqs.pop(seq.request_id, None)
                 self.metrics.on_finish(seq)
             outs.append(RequestOutput(seq.request_id, seq.prompt_token_ids, [tok],
-                                      list(seq.output_token_ids), reason is not None, reason,
+                                      seq.output_token_ids, len(seq.output_token_ids),
+                                      reason is not None, reason,
                                       seq.arrival_time, seq.first_token_time, seq.finish_time,
                                       seq.num_preemptions))
         self.metrics.on_step(plan, now - t0, len(samplers), self.bm.usage(),

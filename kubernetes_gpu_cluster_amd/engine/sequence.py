@@ -47,7 +47,8 @@ class Sequence:
     __slots__ = ("seq_id", "request_id", "prompt_token_ids", "output_token_ids", "params",
                  "status", "block_ids", "num_computed", "arrival_time", "first_token_time",
                  "finish_time", "finish_reason", "seed", "num_preemptions", "max_tokens",
-                 "slot", "last_token_time", "token_times", "prompt_text", "stream")
+                 "slot", "last_token_time", "token_times", "prompt_text", "stream",
+                 "num_pending")
 
     def __init__(self, request_id: str, prompt_token_ids: list[int], params: SamplingParams,
                  arrival_time: Optional[float] = None, max_model_len: int = 1 << 30):
@@ -72,6 +73,7 @@ class Sequence:
         self.token_times: list[float] = []
         self.prompt_text: Optional[str] = None
         self.stream = None
+        self.num_pending = 0                  # trailing sampled tokens still on the GPU
 
     @property
     def num_tokens(self) -> int:
@@ -105,16 +107,24 @@ class Sequence:
 
 @dataclasses.dataclass
 class RequestOutput:
+    """Per-step output of one request.  ``output_token_ids`` is a view of the
+    sequence's token list cut at the tokens resolved so far (no O(n) copy per step;
+    the list only grows past ``num_output_tokens`` or is truncated beyond it)."""
     request_id: str
     prompt_token_ids: list[int]
     new_token_ids: list[int]
-    output_token_ids: list[int]
+    _ids: list[int]
+    num_output_tokens: int
     finished: bool
     finish_reason: Optional[str] = None
     arrival_time: float = 0.0
     first_token_time: Optional[float] = None
     finish_time: Optional[float] = None
     num_preemptions: int = 0
+
+    @property
+    def output_token_ids(self) -> list[int]:
+        return self._ids[:self.num_output_tokens]
 
     @property
     def ttft(self) -> Optional[float]:

@@ -76,7 +76,10 @@ class Router:
 
     # ------------------------------------------------------------------ lifecycle
     async def start(self, app=None):
-        self.session = aiohttp.ClientSession(timeout=self.timeout)
+        # no connection cap: aiohttp's default (100 total) would silently queue every
+        # request past the 100th, starving an engine that batches 256+ sequences
+        conn = aiohttp.TCPConnector(limit=0, limit_per_host=0, keepalive_timeout=60)
+        self.session = aiohttp.ClientSession(timeout=self.timeout, connector=conn)
         await self.refresh_discovery()
         await self.check_health()
         self._tasks.append(asyncio.create_task(self._health_loop()))

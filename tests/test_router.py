@@ -100,3 +100,57 @@ def test_pods_to_urls_and_consistent_hash():
     bs = [Backend(f"http://h{i}:1") for i in range(4)]
     picks = {k: consistent_pick(bs, k).url for k in ("u1", "u2", "u3")}
     assert picks == {k: consistent_pick(bs, k).url for k in picks}   # stable
+
+
+async def _concurrency_scenario(n=300):
+    """More concurrent streams than aiohttp's default connector cap (100): all must be
+    in flight at the backend at the same time, none queued in the router."""
+    app = web.Application()
+    state = {"live": 0, "peak": 0}
+    gate = asyncio.Event()
+
+    async def health(r):
+        return web.Response(text="ok")
+
+    async def models(r):
+        return web.json_response({"data": [{"id": "m"}]})
+
+    async def comp(r):
+        state["live"] += 1
+        state["peak"] = max(state["peak"], state["live"])
+        if state["live"] >= n:
+            gate.set()
+        resp = web.StreamResponse(headers={"content-type": "text/event-stream"})
+        await resp.prepare(r)
+        await asyncio.wait_for(gate.wait(), 30)
+        await resp.write(b"data: {}\n\ndata: [DONE]\n\n")
+        await resp.write_eof()
+        state["live"] -= 1
+        return resp
+
+    app.router.add_get("/health", health)
+    app.router.add_get("/v1/models", models)
+    app.router.add_post("/v1/completions", comp)
+    be = TestServer(app)
+    await be.start_server()
+    r = Router([str(be.make_url(""))], health_interval=3600)
+    client = TestClient(TestServer(r.app()))
+    await client.start_server()
+    import aiohttp
+    sess = aiohttp.ClientSession(connector=aiohttp.TCPConnector(limit=0))
+    try:
+        async def one():
+            async with sess.post(client.make_url("/v1/completions"),
+                                 json={"model": "m", "stream": True}) as resp:
+                return await resp.text()
+        outs = await asyncio.gather(*[one() for _ in range(n)])
+        assert all(o.endswith("[DONE]\n\n") for o in outs)
+        assert state["peak"] == n
+    finally:
+        await sess.close()
+        await client.close()
+        await be.close()
+
+
+def test_router_has_no_connection_cap():
+    asyncio.run(_concurrency_scenario())
