@@ -23,7 +23,6 @@ from typing import Any, Optional, Union
 
 from fastapi import FastAPI, Request
 from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
-from prometheus_client import generate_latest
 from pydantic import BaseModel, ConfigDict, Field
 
 from .. import __version__
@@ -285,7 +284,7 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
 
     @app.get("/metrics")
     async def metrics():
-        return PlainTextResponse(generate_latest(engine.engine.metrics.registry).decode(),
+        return PlainTextResponse(await engine.metrics_text(),
                                  media_type="text/plain; version=0.0.4")
 
     @app.get("/version")
@@ -301,6 +300,9 @@ def make_parser() -> argparse.ArgumentParser:
     p.add_argument("--host", default="0.0.0.0")
     p.add_argument("--port", type=int, default=8000)
     p.add_argument("--uvicorn-log-level", default="info")
+    p.add_argument("--engine-in-process", action="store_true",
+                   help="run the engine loop on a thread of this process instead of a "
+                        "separate engine-core process")
     add_engine_args(p)
     return p
 
@@ -311,11 +313,18 @@ def main(argv=None) -> None:
     ns.model = ns.model or ns.model_tag or "llama-3-8b"
     cfg = config_from_args(ns)
     logging.basicConfig(level=logging.INFO)
-    eng = AsyncLLMEngine(cfg)
+    if ns.engine_in_process:
+        eng = AsyncLLMEngine(cfg)
+    else:
+        from .engine_core import EngineCoreClient
+        eng = EngineCoreClient(cfg)
     tok = get_tokenizer(cfg.model, eng.engine.mcfg, cfg.tokenizer)
     name = cfg.served_model_name or cfg.model
     app = build_app(eng, tok, name, eng.engine.max_model_len)
-    uvicorn.run(app, host=ns.host, port=ns.port, log_level=ns.uvicorn_log_level)
+    try:
+        uvicorn.run(app, host=ns.host, port=ns.port, log_level=ns.uvicorn_log_level)
+    finally:
+        eng.shutdown()
 
 
 if __name__ == "__main__":

@@ -135,6 +135,10 @@ class AsyncLLMEngine:
         self._aborts.put(request_id)
         self._wake.set()
 
+    async def metrics_text(self) -> str:
+        from prometheus_client import generate_latest
+        return generate_latest(self.engine.metrics.registry).decode()
+
     def shutdown(self) -> None:
         self._stop = True
         self._wake.set()

@@ -1,0 +1,219 @@
+"""Engine core in its own process, for the HTTP server.
+
+With the engine loop on a thread of the API-server process, the scheduler and
+plan building (~1-2 ms per step at batch 256) compete for one GIL with request
+parsing, detokenisation and SSE writes for 256 streams.  Once that Python work
+exceeds a decode step, the GPU idles.  ``EngineCoreClient`` starts
+``LLMEngine`` in a separate spawned process.  The API process never touches the
+GPU, so spawning stays safe.  The two talk over one duplex pipe:
+
+* API -> core: ``add`` / ``abort`` / ``metrics`` / ``shutdown`` messages, non-blocking
+  for the event loop;
+* core -> API: ONE ``out`` message per engine step, carrying every request's newly
+  resolved tokens.  A reader thread delivers it to the event loop with one
+  thread-safe call.
+
+The interface matches ``AsyncLLMEngine``: ``generate``, ``abort``, ``is_alive``,
+``shutdown``, ``metrics_text``, ``mcfg``, ``max_model_len``.  ``build_app`` therefore
+accepts either.  ``--engine-in-process`` selects the thread-backed engine instead.
+"""
+from __future__ import annotations
+
+import asyncio
+import itertools
+import logging
+import multiprocessing as mp
+import threading
+import traceback
+from typing import AsyncIterator, Optional
+
+from ..engine.config import EngineConfig
+from ..engine.sequence import RequestOutput, SamplingParams
+from .async_engine import EngineDeadError, _deliver
+
+log = logging.getLogger("kgc.engine_core")
+
+
+# ---------------------------------------------------------------------------- core process
+def _core_main(cfg: EngineConfig, conn) -> None:
+    logging.basicConfig(level=logging.INFO)
+    try:
+        from ..engine.llm_engine import LLMEngine
+        eng = LLMEngine(cfg)
+    except BaseException:  # noqa: BLE001
+        conn.send(("dead", traceback.format_exc()))
+        return
+    conn.send(("ready", {"mcfg": eng.mcfg, "max_model_len": eng.max_model_len}))
+    try:
+        running = True
+        while running:
+            idle = not eng.has_unfinished()
+            # drain the inbox; block briefly only when there is nothing to run
+            while conn.poll(0.05 if idle else 0):
+                msg = conn.recv()
+                kind = msg[0]
+                if kind == "add":
+                    _, rid, ids, params, arrival = msg
+                    try:
+                        eng.add_request(ids, params, request_id=rid, arrival_time=arrival)
+                    except Exception as e:  # noqa: BLE001 - reported to that request
+                        conn.send(("reject", rid, f"{type(e).__name__}: {e}"))
+                elif kind == "abort":
+                    eng.abort(msg[1])
+                elif kind == "metrics":
+                    from prometheus_client import generate_latest
+                    conn.send(("metrics", msg[1], generate_latest(eng.metrics.registry).decode()))
+                elif kind == "shutdown":
+                    running = False
+                    break
+                idle = False
+            if running and eng.has_unfinished():
+                outs = eng.step()
+                if outs:
+                    conn.send(("out", [(o.request_id, o.new_token_ids, o.finished, o.finish_reason,
+                                        o.arrival_time, o.first_token_time, o.finish_time,
+                                        o.num_preemptions) for o in outs]))
+    except BaseException:  # noqa: BLE001
+        tb = traceback.format_exc()
+        log.error("engine core died: %s", tb)
+        try:
+            conn.send(("dead", tb))
+        except OSError:
+            pass
+    finally:
+        eng.shutdown()
+
+
+# ---------------------------------------------------------------------------- API side
+class _Stream:
+    __slots__ = ("loop", "q", "prompt", "ids")
+
+    def __init__(self, loop, q, prompt):
+        self.loop, self.q, self.prompt, self.ids = loop, q, prompt, []
+
+
+class EngineCoreClient:
+    def __init__(self, cfg: EngineConfig, startup_timeout: float = 3600.0):
+        self.cfg = cfg
+        ctx = mp.get_context("spawn")
+        self._conn, child = ctx.Pipe(duplex=True)
+        self._proc = ctx.Process(target=_core_main, args=(cfg, child), name="kgc-engine-core")
+        self._proc.start()
+        child.close()
+        if not self._conn.poll(startup_timeout):
+            self._proc.kill()
+            raise RuntimeError("engine core did not start in time")
+        kind, info = self._conn.recv()
+        if kind != "ready":
+            self._proc.join(10)
+            raise RuntimeError(f"engine core failed to start:\n{info}")
+        self.mcfg = info["mcfg"]
+        self.max_model_len = info["max_model_len"]
+        self.error: Optional[str] = None
+        self._streams: dict[str, _Stream] = {}
+        self._send_lock = threading.Lock()
+        self._metrics_waiters: dict[int, tuple] = {}
+        self._tokens = itertools.count()
+        self._reader = threading.Thread(target=self._read_loop, name="kgc-core-reader", daemon=True)
+        self._reader.start()
+
+    # the api server reads these through ``engine.engine`` in thread mode
+    @property
+    def engine(self):
+        return self
+
+    def _send(self, msg) -> None:
+        with self._send_lock:
+            self._conn.send(msg)
+
+    def _read_loop(self) -> None:
+        try:
+            while True:
+                msg = self._conn.recv()
+                kind = msg[0]
+                if kind == "out":
+                    by_loop: dict = {}
+                    for rid, new, fin, reason, arr, ftt, ft, npre in msg[1]:
+                        st = self._streams.get(rid)
+                        if st is None:
+                            continue
+                        st.ids.extend(new)
+                        o = RequestOutput(rid, st.prompt, new, st.ids, len(st.ids), fin, reason,
+                                          arr, ftt, ft, npre)
+                        by_loop.setdefault(st.loop, []).append((st.q, o))
+                    for loop, items in by_loop.items():
+                        loop.call_soon_threadsafe(_deliver, items)
+                elif kind == "reject":
+                    st = self._streams.get(msg[1])
+                    if st is not None:
+                        st.loop.call_soon_threadsafe(st.q.put_nowait, ValueError(msg[2]))
+                elif kind == "metrics":
+                    w = self._metrics_waiters.pop(msg[1], None)
+                    if w is not None:
+                        loop, fut = w
+                        loop.call_soon_threadsafe(fut.set_result, msg[2])
+                elif kind == "dead":
+                    self.error = msg[1]
+                    break
+        except (EOFError, OSError) as e:
+            self.error = self.error or f"engine core connection lost: {e}"
+        log.error("engine core is gone: %s", self.error)
+        err = EngineDeadError("engine core died")
+        for st in list(self._streams.values()):
+            st.loop.call_soon_threadsafe(st.q.put_nowait, err)
+
+    @property
+    def is_alive(self) -> bool:
+        return self.error is None and self._proc.is_alive()
+
+    async def generate(self, prompt_ids: list[int], params: SamplingParams,
+                       request_id: str) -> AsyncIterator[RequestOutput]:
+        if not self.is_alive:
+            raise EngineDeadError(str(self.error))
+        import time
+        loop = asyncio.get_running_loop()
+        q: asyncio.Queue = asyncio.Queue()
+        self._streams[request_id] = _Stream(loop, q, list(prompt_ids))
+        self._send(("add", request_id, list(prompt_ids), params, time.monotonic()))
+        finished = False
+        try:
+            while True:
+                item = await q.get()
+                while not isinstance(item, BaseException) and not item.finished and not q.empty():
+                    nxt = q.get_nowait()          # coalesce when the stream lags
+                    if not isinstance(nxt, BaseException):
+                        nxt.new_token_ids = item.new_token_ids + nxt.new_token_ids
+                    item = nxt
+                if isinstance(item, BaseException):
+                    raise item
+                yield item
+                if item.finished:
+                    finished = True
+                    return
+        finally:
+            self._streams.pop(request_id, None)
+            if not finished and self.is_alive:
+                self.abort(request_id)
+
+    def abort(self, request_id: str) -> None:
+        try:
+            self._send(("abort", request_id))
+        except OSError:
+            pass
+
+    async def metrics_text(self) -> str:
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        tok = next(self._tokens)
+        self._metrics_waiters[tok] = (loop, fut)
+        self._send(("metrics", tok))
+        return await asyncio.wait_for(fut, 10)
+
+    def shutdown(self) -> None:
+        try:
+            self._send(("shutdown",))
+        except OSError:
+            pass
+        self._proc.join(60)
+        if self._proc.is_alive():
+            self._proc.kill()

@@ -11,11 +11,19 @@ from kubernetes_gpu_cluster_amd.entrypoints.async_engine import AsyncLLMEngine
 from kubernetes_gpu_cluster_amd.utils.tokenizer import get_tokenizer
 
 
-@pytest.fixture(scope="module")
-def client():
-    cfg = EngineConfig(model="tiny-llama", random_init=True, max_model_len=256, max_num_seqs=8,
-                       max_num_batched_tokens=128, device="cpu", dtype="float32")
-    eng = AsyncLLMEngine(cfg)
+def _cfg():
+    return EngineConfig(model="tiny-llama", random_init=True, max_model_len=256, max_num_seqs=8,
+                        max_num_batched_tokens=128, device="cpu", dtype="float32")
+
+
+@pytest.fixture(scope="module", params=["thread", "core-process"])
+def client(request):
+    cfg = _cfg()
+    if request.param == "thread":
+        eng = AsyncLLMEngine(cfg)
+    else:
+        from kubernetes_gpu_cluster_amd.entrypoints.engine_core import EngineCoreClient
+        eng = EngineCoreClient(cfg)
     tok = get_tokenizer(cfg.model, eng.engine.mcfg)
     app = build_app(eng, tok, "tiny-llama", eng.engine.max_model_len)
     with TestClient(app) as c:
@@ -96,3 +104,25 @@ def test_incremental_detok_stop_straddles_updates():
     d = _Detok(_ByteTok(), ["STOP"])
     out = "".join(d.update(ids[:i]) for i in range(1, len(ids) + 1))
     assert d.stopped and out == "abc " and d.text == "abc "
+
+
+def test_engine_core_death_is_reported():
+    """The engine-core process dies -> /health 503 (pod restart) and requests fail fast."""
+    from kubernetes_gpu_cluster_amd.entrypoints.engine_core import EngineCoreClient
+    eng = EngineCoreClient(_cfg())
+    tok = get_tokenizer("tiny-llama", eng.mcfg)
+    app = build_app(eng, tok, "tiny-llama", eng.max_model_len)
+    with TestClient(app) as c:
+        assert c.get("/health").status_code == 200
+        assert c.post("/v1/completions", json={"prompt": [5, 6], "max_tokens": 2}).status_code == 200
+        eng._proc.kill()
+        eng._proc.join(10)
+        import time
+        for _ in range(50):
+            if not eng.is_alive:
+                break
+            time.sleep(0.1)
+        assert c.get("/health").status_code == 503
+        r = c.post("/v1/completions", json={"prompt": [5, 6], "max_tokens": 2})
+        assert r.status_code == 503
+    eng.shutdown()
