@@ -116,6 +116,13 @@ def _send_tokens_to_driver(tokens: torch.Tensor) -> None:
     dist.send(tokens.cpu(), dst=getattr(s, "global_base", 0), group=s.cpu_group)
 
 
+def _release_custom_allreduce() -> None:
+    car = comm.get_custom_allreduce()
+    if car is not None:
+        comm.set_custom_allreduce(None)
+        car.close()
+
+
 def worker_loop(worker: Worker) -> None:
     """Non-driver ranks: execute commands until CMD_EXIT."""
     s = get_state()
@@ -124,6 +131,7 @@ def worker_loop(worker: Worker) -> None:
         h = _bcast_cmd(0)
         cmd, arg = h[0], h[1]
         if cmd == CMD_EXIT:
+            _release_custom_allreduce()
             break
         if cmd == CMD_PROFILE:
             nb = worker.profile()
@@ -237,6 +245,7 @@ class _DistExecutorBase:
             _bcast_cmd(CMD_EXIT)
         except Exception:  # noqa: BLE001
             pass
+        _release_custom_allreduce()
 
 
 class ExternalExecutor(_DistExecutorBase):

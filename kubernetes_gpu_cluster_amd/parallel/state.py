@@ -81,7 +81,10 @@ def init_parallel(tp: int = 1, pp: int = 1, backend: Optional[str] = None,
         rank = int(os.environ.get("RANK", 0)) if rank is None else rank
         world_size = int(os.environ.get("WORLD_SIZE", ws)) if world_size is None else world_size
         if backend is None:
-            backend = "nccl" if (device is not None and device.type == "cuda") else "gloo"
+            # KGC_DIST_BACKEND=gloo lets several TP ranks share ONE GPU (RCCL refuses
+            # duplicate devices): a correctness harness for the TP path on a 1-GPU box
+            backend = os.environ.get("KGC_DIST_BACKEND") or (
+                "nccl" if (device is not None and device.type == "cuda") else "gloo")
         if device is not None and device.type == "cuda":
             torch.cuda.set_device(device)
         kw = {}
