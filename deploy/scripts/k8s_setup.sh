@@ -8,7 +8,9 @@
 # work; --join honours --cri-socket; the apt repo follows --kube-version.
 # Extra flags: --control-plane-endpoint=VIP:6443 (HA, multi-cp.md:290),
 #   --pod-network-cidr, --cni=calico|none, --untaint, --label-gpu, --skip-reset,
-#   --proxy=http://host:port (optional egress proxy for apt/CRI-O), --dry-run.
+#   --proxy=http://host:port (optional egress proxy for apt/CRI-O), --dry-run,
+#   --fix-coredns (run CoreDNS AppArmor-unconfined: the fix that made CoreDNS start
+#   on the reference's nodes, old_README.md:780-836).
 set -euo pipefail
 HERE="$(cd "$(dirname "${BASH_SOURCE[0]}")" && pwd)"
 source "$HERE/lib.sh"
@@ -24,6 +26,7 @@ CALICO_VERSION="v3.28.0"
 UNTAINT=0
 LABEL_GPU=0
 SKIP_RESET=0
+FIX_COREDNS=0
 PROXY="${PROXY:-}"
 
 usage() { sed -n '2,14p' "$0"; exit "${1:-0}"; }
@@ -33,7 +36,7 @@ parse_args() {
     local arg="$1" val=""
     case "$arg" in
       --*=*) val="${arg#*=}"; arg="${arg%%=*}" ;;
-      --yes|-y|--untaint|--label-gpu|--skip-reset|--dry-run|-h|--help) ;;
+      --yes|-y|--untaint|--label-gpu|--skip-reset|--fix-coredns|--dry-run|-h|--help) ;;
       --*) [[ $# -ge 2 ]] || die "$arg needs a value"; val="$2"; shift ;;
     esac
     case "$arg" in
@@ -53,6 +56,7 @@ parse_args() {
       --untaint) UNTAINT=1 ;;
       --label-gpu) LABEL_GPU=1 ;;
       --skip-reset) SKIP_RESET=1 ;;
+      --fix-coredns) FIX_COREDNS=1 ;;
       --proxy) PROXY="$val" ;;
       --dry-run) DRY_RUN=1 ;;
       -h|--help) usage 0 ;;
@@ -183,6 +187,14 @@ init_control_plane() {
   fi
   if [[ "$LABEL_GPU" == "1" ]]; then
     run "${kc[@]}" label node "$(hostname)" gpu=true --overwrite || true
+  fi
+  if [[ "$FIX_COREDNS" == "1" ]]; then
+    # AppArmor-confined CoreDNS crash-looped on the reference's hosts; the pod-level
+    # appArmorProfile field (k8s >= 1.30) replaces the deprecated annotation
+    run "${kc[@]}" -n kube-system patch deployment coredns --type=strategic -p \
+      '{"spec":{"template":{"spec":{"securityContext":{"appArmorProfile":{"type":"Unconfined"}}}}}}' \
+      || warn "coredns patch failed"
+    run "${kc[@]}" -n kube-system rollout restart deployment coredns || true
   fi
 }
 

@@ -63,6 +63,15 @@ def test_control_plane(env):
     assert list((root / "var/log").glob("kubeadm-init-*.log"))
 
 
+def test_fix_coredns(env):
+    e, root, log = env
+    sh("k8s_setup.sh", "--yes", "--role=cp", "--fix-coredns", env=e)
+    c = calls(log)
+    patch = [x for x in c if "patch deployment coredns" in x]
+    assert patch and '"appArmorProfile":{"type":"Unconfined"}' in patch[0]
+    assert any("rollout restart deployment coredns" in x for x in c)
+
+
 def test_ha_control_plane_endpoint(env):
     e, root, log = env
     sh("k8s_setup.sh", "--yes", "--role=cp", "--control-plane-endpoint=10.0.0.100:6443", env=e)
@@ -133,3 +142,52 @@ def test_gpu_crio_setup(env):
     sh("gpu-crio-setup.sh", "--set-default", "--skip-apt", "--no-kubectl", env=e)
     assert 'default_runtime = "amd"' in (root / "etc/crio/crio.conf.d/99-amd.conf").read_text()
     assert not (root / "etc/crio/crio.conf.d/98-crun-default.conf").exists()
+
+
+def test_ha_setup_systemd(env):
+    e, root, log = env
+    sh("ha_setup.sh", "--vip=10.0.0.100", "--interface", "eth0", "--state=master",
+       "--peer=cp1=10.0.0.11", "--peer", "cp2=10.0.0.12", "--peer=cp3=10.0.0.13", "--yes", env=e)
+    ka = (root / "etc/keepalived/keepalived.conf").read_text()
+    assert "state MASTER" in ka and "priority 101" in ka and "interface eth0" in ka
+    assert "10.0.0.100" in ka and "fall 10" in ka and "rise 2" in ka and "interval 3" in ka
+    chk = root / "etc/keepalived/check_apiserver.sh"
+    assert os.access(chk, os.X_OK) and "127.0.0.1:8443/healthz" in chk.read_text()
+    hp = (root / "etc/haproxy/haproxy.cfg").read_text()
+    assert "bind *:8443" in hp and "uri /healthz" in hp
+    for i in (1, 2, 3):
+        assert f"server cp{i} 10.0.0.1{i}:6443 check" in hp
+    c = calls(log)
+    assert "apt-get install -y keepalived haproxy" in c
+    assert "systemctl enable --now keepalived" in c and "systemctl enable --now haproxy" in c
+    r = subprocess.run(["bash", "-n", str(chk)], capture_output=True)
+    assert r.returncode == 0
+
+
+def test_ha_setup_static_pods_and_validation(env):
+    e, root, log = env
+    sh("ha_setup.sh", "--vip=10.0.0.100", "--interface=ens5", "--peer=a=10.0.0.2",
+       "--mode=static-pods", "--yes", env=e)
+    assert "state BACKUP" in (root / "etc/keepalived/keepalived.conf").read_text()
+    man = (root / "etc/kubernetes/manifests/haproxy.yaml").read_text()
+    assert "path: /etc/haproxy/haproxy.cfg" in man and "mountPath: /usr/local/etc/haproxy/haproxy.cfg" in man
+    assert (root / "etc/kubernetes/manifests/keepalived.yaml").exists()
+    assert not any(x.startswith("systemctl") for x in calls(log))
+    for bad in (["--interface=eth0", "--peer=a=1.2.3.4"],                     # no vip
+                ["--vip=10.0.0.1", "--peer=a=1.2.3.4"],                       # no interface
+                ["--vip=10.0.0.1", "--interface=eth0"],                       # no peers
+                ["--vip=10.0.0.1", "--interface=eth0", "--peer=a=1.2.3.4", "--lb-port=6443"]):
+        r = sh("ha_setup.sh", *bad, env=e, check=False)
+        assert r.returncode != 0
+
+
+def test_proxy_setup(env):
+    e, root, log = env
+    sh("proxy_setup.sh", "--socks=127.0.0.1:1080", "--ssh-tunnel", "me@bastion", env=e)
+    conf = (root / "etc/privoxy/config").read_text()
+    assert "listen-address  127.0.0.1:8118" in conf and "forward-socks5  /  127.0.0.1:1080" in conf
+    unit = (root / "etc/systemd/system/kgc-socks-tunnel.service").read_text()
+    assert "ssh -N -D 127.0.0.1:1080" in unit and "Restart=always" in unit and "me@bastion" in unit
+    c = calls(log)
+    assert "systemctl restart privoxy" in c and "apt-get install -y privoxy" in c
+    assert sh("proxy_setup.sh", env=e, check=False).returncode != 0
