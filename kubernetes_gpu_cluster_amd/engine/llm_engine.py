@@ -20,7 +20,7 @@ from .block_manager import BlockManager
 from .config import EngineConfig
 from .scheduler import Scheduler
 from .sequence import RequestOutput, SamplingParams, SeqStatus, Sequence
-from .worker import LocalExecutor, MultiprocExecutor, default_max_model_len
+from .worker import TokenFuture, LocalExecutor, MultiprocExecutor, default_max_model_len
 
 log = logging.getLogger("kgc.engine")
 _PENDING = -1          # placeholder for a sampled token still on the GPU
@@ -117,9 +117,10 @@ class LLMEngine:
     def _process(self, inflight) -> list[RequestOutput]:
         fut, samplers, plan, t0, npre = inflight
         tokens = fut.result()
+        lps = fut.logprobs() if plan.lp else {}
         now = time.monotonic()
         outs: list[RequestOutput] = []
-        for seq, tok in zip(samplers, tokens):
+        for row, (seq, tok) in enumerate(zip(samplers, tokens)):
             if seq.finish_reason not in (None, "length"):
                 continue        # finished earlier (EOS seen one step late) or aborted
             if seq.num_pending == 0:
@@ -143,10 +144,13 @@ class LLMEngine:
                 done = True
             else:
                 done = False
-            outs.append(RequestOutput(seq.request_id, seq.prompt_token_ids, [tok],
-                                      seq.output_token_ids, idx + 1, done, reason if done else None,
-                                      seq.arrival_time, seq.first_token_time, seq.finish_time,
-                                      seq.num_preemptions))
+            o = RequestOutput(seq.request_id, seq.prompt_token_ids, [tok],
+                              seq.output_token_ids, idx + 1, done, reason if done else None,
+                              seq.arrival_time, seq.first_token_time, seq.finish_time,
+                              seq.num_preemptions)
+            if row in lps:
+                o.logprobs = [(tok, lps[row][0], lps[row][1])]
+            outs.append(o)
         self.metrics.on_step(plan, now - t0, len(samplers), self.bm.usage(),
                              len(self.scheduler.running), len(self.scheduler.waiting), npre)
         return outs
@@ -158,13 +162,14 @@ class LLMEngine:
         t0 = time.monotonic()
         plan, samplers = self.executor.runner.build_plan(batch.prefills, batch.decodes, self.bm.table)
         tokens = self.executor.execute(plan)
+        lps = TokenFuture(None, lp=self.executor.runner.take_logprobs()).logprobs() if plan.lp else {}
         now = time.monotonic()
         for seq, n in batch.prefills:
             seq.num_computed += n
         for seq in batch.decodes:
             seq.num_computed += 1
         outs: list[RequestOutput] = []
-        for seq, tok in zip(samplers, tokens):
+        for row, (seq, tok) in enumerate(zip(samplers, tokens)):
             seq.output_token_ids.append(tok)
             if seq.first_token_time is None:
                 seq.first_token_time = now
@@ -175,11 +180,14 @@ class LLMEngine:
                 self.scheduler.finish(seq, reason)
                 self.seqs.pop(seq.request_id, None)
                 self.metrics.on_finish(seq)
-            outs.append(RequestOutput(seq.request_id, seq.prompt_token_ids, [tok],
-                                      seq.output_token_ids, len(seq.output_token_ids),
-                                      reason is not None, reason,
-                                      seq.arrival_time, seq.first_token_time, seq.finish_time,
-                                      seq.num_preemptions))
+            o = RequestOutput(seq.request_id, seq.prompt_token_ids, [tok],
+                              seq.output_token_ids, len(seq.output_token_ids),
+                              reason is not None, reason,
+                              seq.arrival_time, seq.first_token_time, seq.finish_time,
+                              seq.num_preemptions)
+            if row in lps:
+                o.logprobs = [(tok, lps[row][0], lps[row][1])]
+            outs.append(o)
         self.metrics.on_step(plan, now - t0, len(samplers), self.bm.usage(),
                              len(self.scheduler.running), len(self.scheduler.waiting),
                              len(batch.preempted))
@@ -225,10 +233,15 @@ class LLM:
             self.engine.add_request(toks, sp, request_id=str(i))
             ids.append(str(i))
         final: dict[str, RequestOutput] = {}
+        lps: dict[str, list] = {}
         while self.engine.has_unfinished():
             for o in self.engine.step():
+                if o.logprobs:
+                    lps.setdefault(o.request_id, []).extend(o.logprobs)
                 if o.finished:
                     final[o.request_id] = o
+        for rid, o in final.items():
+            o.logprobs = lps.get(rid)
         return [final[i] for i in ids]
 
     def shutdown(self):

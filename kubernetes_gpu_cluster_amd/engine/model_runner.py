@@ -52,6 +52,7 @@ class StepPlan:
     i64: np.ndarray
     i32: np.ndarray
     f32: np.ndarray
+    lp: Optional[list] = None   # driver only: [(sampled row, top-k)] for logprobs requests
 
     def header(self) -> list[int]:
         return [self.T, self.Tp, self.P, self.D, self.S, self.W, self.B, self.max_ctx,
@@ -280,8 +281,10 @@ class ModelRunner:
         i64[L.lidx:L.lidx + S] = lidx
         if B:
             i64[L.lidx:L.lidx + B] = np.arange(B)   # graph rows index their own hidden row
+        lp = [(j, s.params.logprobs) for j, s in enumerate(samplers)
+              if s.params.logprobs is not None] or None
         return StepPlan(T, Tp, P, D, S, W, B, max_ctx, int(device_tokens and D > 0), i64, i32,
-                        f32), samplers
+                        f32, lp), samplers
 
     # ------------------------------------------------------------------ execution (all ranks)
     def _upload(self, plan: StepPlan) -> None:
@@ -358,7 +361,23 @@ class ModelRunner:
                          self.df[L.topp:L.topp + plan.S], self.d64[L.seeds:L.seeds + plan.S],
                          out=out if self.is_gpu else None)
         self.last_tok.index_copy_(0, self.d64[L.sslots:L.sslots + plan.S], res)
+        self._last_lp = self._logprobs(plan.lp, logits, res) if plan.lp else None
         return res
+
+    def _logprobs(self, lp: list, logits: torch.Tensor, res: torch.Tensor):
+        """log-softmax of the raw logits for the rows that asked for logprobs: the
+        sampled token's logprob and the top-k alternatives (device tensors; copied to
+        the host only when the step's tokens are read)."""
+        rows = torch.tensor([r for r, _ in lp], device=logits.device)
+        kmax = max(1, max(k for _, k in lp))
+        lsm = torch.log_softmax(logits.index_select(0, rows).float(), dim=-1)
+        chosen = lsm.gather(1, res.index_select(0, rows).view(-1, 1)).view(-1)
+        topv, topi = lsm.topk(min(kmax, lsm.shape[-1]), dim=-1)
+        return lp, chosen, topv, topi
+
+    def take_logprobs(self):
+        lp, self._last_lp = getattr(self, "_last_lp", None), None
+        return lp
 
     def tokens_to_host(self, res: torch.Tensor):
         """Start the D2H copy of sampled ids into a pinned (double-buffered) host

@@ -121,6 +121,9 @@ class RequestOutput:
     first_token_time: Optional[float] = None
     finish_time: Optional[float] = None
     num_preemptions: int = 0
+    # per new token, when the request asked for logprobs:
+    # (token id, logprob, [(alternative id, logprob)] top-k)
+    logprobs: Optional[list] = None
 
     @property
     def output_token_ids(self) -> list[int]:

@@ -173,7 +173,7 @@ class LocalExecutor:
 
     def execute_async(self, plan: StepPlan) -> "TokenFuture":
         out = self.worker.run(plan)
-        return TokenFuture(*self.runner.tokens_to_host(out))
+        return TokenFuture(*self.runner.tokens_to_host(out), lp=self.runner.take_logprobs())
 
     @property
     def supports_async(self) -> bool:
@@ -184,10 +184,12 @@ class LocalExecutor:
 
 
 class TokenFuture:
-    """Sampled ids of a launched step; result() blocks until the D2H copy landed."""
+    """Sampled ids of a launched step; result() blocks until the D2H copy landed.
+    ``logprobs()`` -> {sampled row: (logprob of the sampled token, [(id, logprob)] top-k)}
+    for the rows whose requests asked for logprobs."""
 
-    def __init__(self, buf: torch.Tensor, ev=None, values: Optional[list[int]] = None):
-        self.buf, self.ev, self.values = buf, ev, values
+    def __init__(self, buf: torch.Tensor, ev=None, values: Optional[list[int]] = None, lp=None):
+        self.buf, self.ev, self.values, self._lp = buf, ev, values, lp
 
     def result(self) -> list[int]:
         if self.values is None:
@@ -195,6 +197,14 @@ class TokenFuture:
                 self.ev.synchronize()
             self.values = self.buf.tolist()
         return self.values
+
+    def logprobs(self) -> dict:
+        if self._lp is None:
+            return {}
+        rows, chosen, topv, topi = self._lp
+        chosen, topv, topi = chosen.tolist(), topv.tolist(), topi.tolist()
+        return {r: (chosen[i], list(zip(topi[i][:k], topv[i][:k])))
+                for i, (r, k) in enumerate(rows)}
 
 
 class _DistExecutorBase:
@@ -226,7 +236,7 @@ class _DistExecutorBase:
         _bcast_cmd(CMD_STEP, 0, plan.header())
         _bcast_plan_blobs(self.worker.runner, plan.header())
         out = self.worker.run(plan)
-        return TokenFuture(*self.runner.tokens_to_host(out))
+        return TokenFuture(*self.runner.tokens_to_host(out), lp=self.runner.take_logprobs())
 
     def execute(self, plan: StepPlan) -> list[int]:
         _bcast_cmd(CMD_STEP, 0, plan.header())

@@ -77,7 +77,12 @@ class ChatCompletionRequest(_Lenient):
     seed: Optional[int] = None
     ignore_eos: bool = False
     min_tokens: int = 0
+    logprobs: bool = False
+    top_logprobs: Optional[int] = None
     user: Optional[str] = None
+
+
+MAX_LOGPROBS = 20
 
 
 def _err(status: int, msg: str, typ: str = "invalid_request_error") -> JSONResponse:
@@ -142,14 +147,20 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
     app = FastAPI(title="kgc OpenAI-compatible server", version=__version__)
     created = int(time.time())
 
-    def params_from(req, max_tokens: Optional[int]) -> SamplingParams:
+    def params_from(req, max_tokens: Optional[int], logprobs: Optional[int] = None) -> SamplingParams:
         stops = req.stop if isinstance(req.stop, list) else ([req.stop] if req.stop else [])
+        if logprobs is not None and not 0 <= logprobs <= MAX_LOGPROBS:
+            raise ValueError(f"logprobs must be in [0, {MAX_LOGPROBS}]")
         return SamplingParams(temperature=req.temperature if req.temperature is not None else 1.0,
                               top_p=req.top_p if req.top_p is not None else 1.0,
                               top_k=req.top_k if req.top_k not in (None, 0) else -1,
                               max_tokens=max_tokens, min_tokens=req.min_tokens,
                               stop_token_ids=list(req.stop_token_ids or []), stop=stops,
-                              ignore_eos=req.ignore_eos, seed=req.seed, n=req.n)
+                              ignore_eos=req.ignore_eos, seed=req.seed, n=req.n,
+                              logprobs=logprobs)
+
+    def tok_str(t: int) -> str:
+        return tokenizer.decode([t])
 
     async def run(ids: list[int], sp: SamplingParams, rid: str, stream_fn, final_fn, stream: bool):
         detok = _Detok(tokenizer, sp.stop)
@@ -164,8 +175,8 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
                             reason = "stop"
                         elif reason:
                             delta += detok.flush()
-                        if delta or reason:
-                            yield f"data: {json.dumps(stream_fn(delta, reason))}\n\n"
+                        if delta or reason or out.logprobs:
+                            yield f"data: {json.dumps(stream_fn(delta, reason, out.logprobs))}\n\n"
                         if detok.stopped:
                             await gen.aclose()
                             break
@@ -174,15 +185,44 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
                 yield "data: [DONE]\n\n"
             return StreamingResponse(sse(), media_type="text/event-stream")
         last = None
+        lps: list = []
         async for out in gen:
             last = out
+            if out.logprobs:
+                lps.extend(out.logprobs)
             detok.update(out.output_token_ids)
             if detok.stopped:
                 await gen.aclose()
                 break
         reason = "stop" if detok.stopped else (last.finish_reason if last else None)
         return JSONResponse(final_fn(detok.text, reason, len(ids),
-                                     len(last.output_token_ids) if last else 0))
+                                     len(last.output_token_ids) if last else 0,
+                                     lps if sp.logprobs is not None else None))
+
+    def completion_logprobs(lps, offset0: int = 0):
+        """legacy completions shape: tokens / token_logprobs / top_logprobs / text_offset"""
+        if lps is None:
+            return None
+        toks, vals, tops, offs = [], [], [], []
+        off = offset0
+        for t, lp, top in lps:
+            s = tok_str(t)
+            toks.append(s)
+            vals.append(lp)
+            tops.append({tok_str(a): v for a, v in top})
+            offs.append(off)
+            off += len(s)
+        return {"tokens": toks, "token_logprobs": vals, "top_logprobs": tops, "text_offset": offs}
+
+    def chat_logprobs(lps):
+        if lps is None:
+            return None
+
+        def ent(t, lp):
+            s = tok_str(t)
+            return {"token": s, "logprob": lp, "bytes": list(s.encode("utf-8"))}
+        return {"content": [dict(ent(t, lp), top_logprobs=[ent(a, v) for a, v in top])
+                            for t, lp, top in lps]}
 
     def prompt_ids(p) -> list[int]:
         return tokenizer.encode(p) if isinstance(p, str) else [int(x) for x in p]
@@ -200,22 +240,25 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
         if len(ids) >= max_model_len:
             return _err(400, f"prompt has {len(ids)} tokens; max_model_len is {max_model_len}")
         try:
-            sp = params_from(req, req.max_tokens)
+            sp = params_from(req, req.max_tokens, req.logprobs)
         except ValueError as e:
             return _err(400, str(e))
         rid = f"cmpl-{uuid.uuid4().hex}"
         prefix = (prompts if isinstance(prompts, str) else tokenizer.decode(ids)) if req.echo else ""
+        want_lp = req.logprobs is not None
 
-        def chunk(delta, reason):
+        def chunk(delta, reason, lps=None):
             return {"id": rid, "object": "text_completion", "created": int(time.time()),
                     "model": served_name,
-                    "choices": [{"index": 0, "text": delta, "logprobs": None,
+                    "choices": [{"index": 0, "text": delta,
+                                 "logprobs": completion_logprobs(lps or []) if want_lp else None,
                                  "finish_reason": reason}]}
 
-        def final(text, reason, np_, nc):
+        def final(text, reason, np_, nc, lps=None):
             return {"id": rid, "object": "text_completion", "created": int(time.time()),
                     "model": served_name,
-                    "choices": [{"index": 0, "text": prefix + text, "logprobs": None,
+                    "choices": [{"index": 0, "text": prefix + text,
+                                 "logprobs": completion_logprobs(lps, len(prefix)),
                                  "finish_reason": reason}],
                     "usage": {"prompt_tokens": np_, "completion_tokens": nc,
                               "total_tokens": np_ + nc}}
@@ -241,25 +284,29 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
         if len(ids) >= max_model_len:
             return _err(400, f"prompt has {len(ids)} tokens; max_model_len is {max_model_len}")
         try:
-            sp = params_from(req, req.max_completion_tokens or req.max_tokens)
+            sp = params_from(req, req.max_completion_tokens or req.max_tokens,
+                             (req.top_logprobs or 0) if req.logprobs else None)
         except ValueError as e:
             return _err(400, str(e))
         rid = f"chatcmpl-{uuid.uuid4().hex}"
         first = [True]
 
-        def chunk(delta, reason):
+        def chunk(delta, reason, lps=None):
             d = {"content": delta}
             if first[0]:
                 d["role"] = "assistant"
                 first[0] = False
+            c = {"index": 0, "delta": d, "finish_reason": reason}
+            if req.logprobs:
+                c["logprobs"] = chat_logprobs(lps or [])
             return {"id": rid, "object": "chat.completion.chunk", "created": int(time.time()),
-                    "model": served_name,
-                    "choices": [{"index": 0, "delta": d, "finish_reason": reason}]}
+                    "model": served_name, "choices": [c]}
 
-        def final(text, reason, np_, nc):
+        def final(text, reason, np_, nc, lps=None):
             return {"id": rid, "object": "chat.completion", "created": int(time.time()),
                     "model": served_name,
                     "choices": [{"index": 0, "message": {"role": "assistant", "content": text},
+                                 "logprobs": chat_logprobs(lps),
                                  "finish_reason": reason}],
                     "usage": {"prompt_tokens": np_, "completion_tokens": nc,
                               "total_tokens": np_ + nc}}

@@ -26,6 +26,13 @@ class EngineDeadError(RuntimeError):
     pass
 
 
+def _merge(prev, nxt) -> None:
+    """Fold an earlier (undelivered) step output into the next one of the same request."""
+    nxt.new_token_ids = prev.new_token_ids + nxt.new_token_ids
+    if prev.logprobs or nxt.logprobs:
+        nxt.logprobs = (prev.logprobs or []) + (nxt.logprobs or [])
+
+
 def _deliver(items) -> None:
     for q, o in items:
         q.put_nowait(o)
@@ -118,7 +125,7 @@ class AsyncLLMEngine:
                 while not isinstance(item, BaseException) and not item.finished and not q.empty():
                     nxt = q.get_nowait()
                     if not isinstance(nxt, BaseException):
-                        nxt.new_token_ids = item.new_token_ids + nxt.new_token_ids
+                        _merge(item, nxt)
                     item = nxt
                 if isinstance(item, BaseException):
                     raise item

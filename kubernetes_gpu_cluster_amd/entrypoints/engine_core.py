@@ -29,7 +29,7 @@ from typing import AsyncIterator, Optional
 
 from ..engine.config import EngineConfig
 from ..engine.sequence import RequestOutput, SamplingParams
-from .async_engine import EngineDeadError, _deliver
+from .async_engine import EngineDeadError, _deliver, _merge
 
 log = logging.getLogger("kgc.engine_core")
 
@@ -72,7 +72,7 @@ def _core_main(cfg: EngineConfig, conn) -> None:
                 if outs:
                     conn.send(("out", [(o.request_id, o.new_token_ids, o.finished, o.finish_reason,
                                         o.arrival_time, o.first_token_time, o.finish_time,
-                                        o.num_preemptions) for o in outs]))
+                                        o.num_preemptions, o.logprobs) for o in outs]))
     except BaseException:  # noqa: BLE001
         tb = traceback.format_exc()
         log.error("engine core died: %s", tb)
@@ -133,13 +133,13 @@ class EngineCoreClient:
                 kind = msg[0]
                 if kind == "out":
                     by_loop: dict = {}
-                    for rid, new, fin, reason, arr, ftt, ft, npre in msg[1]:
+                    for rid, new, fin, reason, arr, ftt, ft, npre, lps in msg[1]:
                         st = self._streams.get(rid)
                         if st is None:
                             continue
                         st.ids.extend(new)
                         o = RequestOutput(rid, st.prompt, new, st.ids, len(st.ids), fin, reason,
-                                          arr, ftt, ft, npre)
+                                          arr, ftt, ft, npre, lps)
                         by_loop.setdefault(st.loop, []).append((st.q, o))
                     for loop, items in by_loop.items():
                         loop.call_soon_threadsafe(_deliver, items)
@@ -182,7 +182,7 @@ class EngineCoreClient:
                 while not isinstance(item, BaseException) and not item.finished and not q.empty():
                     nxt = q.get_nowait()          # coalesce when the stream lags
                     if not isinstance(nxt, BaseException):
-                        nxt.new_token_ids = item.new_token_ids + nxt.new_token_ids
+                        _merge(item, nxt)
                     item = nxt
                 if isinstance(item, BaseException):
                     raise item

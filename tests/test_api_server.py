@@ -126,3 +126,27 @@ def test_engine_core_death_is_reported():
         r = c.post("/v1/completions", json={"prompt": [5, 6], "max_tokens": 2})
         assert r.status_code == 503
     eng.shutdown()
+
+
+def test_completion_logprobs(client):
+    r = client.post("/v1/completions", json={"prompt": [5, 6, 7], "max_tokens": 4, "logprobs": 3,
+                                             "temperature": 0, "ignore_eos": True})
+    lp = r.json()["choices"][0]["logprobs"]
+    assert len(lp["tokens"]) == 4 and len(lp["token_logprobs"]) == 4
+    for v, top in zip(lp["token_logprobs"], lp["top_logprobs"]):
+        assert v <= 0 and 1 <= len(top) <= 3
+        # greedy: the chosen token is the most likely one (token strings may collide in
+        # the legacy dict format, so compare against the listed maxima)
+        assert v >= max(top.values()) - 1e-4
+    assert lp["text_offset"] == sorted(lp["text_offset"])
+    assert client.post("/v1/completions", json={"prompt": "x", "logprobs": 99}).status_code == 400
+
+
+def test_chat_logprobs_stream(client):
+    with client.stream("POST", "/v1/chat/completions", json={
+            "messages": [{"role": "user", "content": "hi"}], "max_tokens": 3, "stream": True,
+            "ignore_eos": True, "logprobs": True, "top_logprobs": 2}) as s:
+        lines = [l for l in s.iter_lines() if l and l != "data: [DONE]"]
+    content = [c for l in lines for c in (json.loads(l[6:])["choices"][0].get("logprobs") or {}).get("content", [])]
+    assert len(content) == 3
+    assert all(len(c["top_logprobs"]) == 2 and c["logprob"] <= 0 for c in content)

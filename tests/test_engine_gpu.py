@@ -138,3 +138,20 @@ def test_tp2_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch):
     same = sum(a == b for x, y in zip(outs[1], outs[2]) for a, b in zip(x, y))
     assert all(x[0] == y[0] for x, y in zip(outs[1], outs[2])), outs
     assert same >= 0.8 * sum(len(x) for x in outs[1]), outs
+
+
+def test_logprobs_through_decode_graphs(gpu):
+    """logprobs come from the graph's static logits buffer: greedy -> the sampled token
+    is the top-1 alternative, every value is a log-probability."""
+    from kubernetes_gpu_cluster_amd.engine.llm_engine import LLM
+    llm = LLM("tiny-llama", device="cuda", dtype="bfloat16", random_init=True, max_model_len=256,
+              max_num_seqs=8, max_num_batched_tokens=256)
+    outs = llm.generate([[5, 6, 7, 8], [9, 10]],
+                        [SamplingParams(temperature=0, max_tokens=6, ignore_eos=True, logprobs=3)] * 2)
+    assert llm.engine.executor.runner.stats["graph_steps"] > 0
+    for o in outs:
+        assert len(o.logprobs) == 6
+        for tok, lp, top in o.logprobs:
+            assert lp <= 1e-6 and len(top) == 3
+            assert top[0][0] == tok or abs(top[0][1] - lp) < 1e-3
+    llm.shutdown()

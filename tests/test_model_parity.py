@@ -110,3 +110,38 @@ def test_logits_match_hf(name):
         ref = hf(torch.tensor([prompt + extra])).logits[0].float()
     got = _engine_logits(model, runner, prompt, [16, 21], extra)   # chunked prefill + 5 decodes
     torch.testing.assert_close(got, ref[: len(prompt) + len(extra)], atol=2e-4, rtol=2e-4)
+
+
+def test_engine_logprobs_match_log_softmax(tmp_path):
+    """Sampled-token logprob and top-k from the runner == log_softmax of the logits
+    the model produces for the same prefix (raw logits, before temperature)."""
+    import json
+    import os
+    from safetensors.torch import save_file
+    from kubernetes_gpu_cluster_amd.engine.llm_engine import LLM
+    from kubernetes_gpu_cluster_amd.engine.sequence import SamplingParams as SP
+    cfg = PRESETS["tiny-llama"]
+    sd = full_state_dict_random(cfg, seed=4, std=0.1)
+    save_file({k: v.contiguous() for k, v in sd.items()}, str(tmp_path / "model.safetensors"))
+    json.dump({"model_type": "llama", "hidden_size": cfg.hidden_size,
+               "num_hidden_layers": cfg.num_layers, "num_attention_heads": cfg.num_heads,
+               "num_key_value_heads": cfg.num_kv_heads, "head_dim": cfg.head_dim,
+               "intermediate_size": cfg.intermediate_size, "vocab_size": cfg.vocab_size,
+               "max_position_embeddings": 512, "rope_theta": cfg.rope_theta,
+               "rms_norm_eps": cfg.rms_eps, "eos_token_id": 2, "bos_token_id": 1},
+              open(tmp_path / "config.json", "w"))
+    llm = LLM(str(tmp_path), device="cpu", dtype="float32", max_model_len=128, max_num_seqs=2,
+              max_num_batched_tokens=64, num_gpu_blocks_override=32)
+    prompt = [5, 9, 13, 17]
+    out = llm.generate([prompt], [SP(temperature=0.7, max_tokens=3, ignore_eos=True, logprobs=4,
+                                     seed=3)])[0]
+    llm.shutdown()
+    assert len(out.logprobs) == 3
+    model, runner = _ours(cfg, sd)
+    full = prompt + out.output_token_ids
+    logits = _engine_logits(model, runner, full, [len(full)], [])
+    for i, (tok, lp, top) in enumerate(out.logprobs):
+        assert tok == out.output_token_ids[i]
+        ref = torch.log_softmax(logits[len(prompt) - 1 + i].float(), -1)
+        assert abs(ref[tok].item() - lp) < 1e-3
+        assert [a for a, _ in top] == ref.topk(4).indices.tolist()
