@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--dtype", default="bfloat16")
     ap.add_argument("--temperature", type=float, default=1.0)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: run the same harness on the fp32 CPU path (gloo) -- a test "
+                         "harness for the multi-rank logic, not a measurement")
     return ap.parse_args()
 
 
@@ -87,12 +90,20 @@ def main():
     n = world if world > 1 else 1
     if args.gpus != n and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    assert torch.cuda.is_available(), "bench.py needs a GPU"
-    dev = torch.device("cuda", local_rank)
-    torch.cuda.set_device(dev)
+    cpu = args.device == "cpu"
+    if cpu:
+        dev = torch.device("cpu")
+        args.dtype = "float32"
+    else:
+        assert torch.cuda.is_available(), "bench.py needs a GPU (or --device cpu)"
+        dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev)
     tp = args.tp
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if cpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     from kubernetes_gpu_cluster_amd.engine.config import EngineConfig
     from kubernetes_gpu_cluster_amd.engine.llm_engine import LLMEngine
     from kubernetes_gpu_cluster_amd.engine.worker import ExternalExecutor, Worker, worker_loop
@@ -100,7 +111,8 @@ def main():
                        max_model_len=args.max_model_len, max_num_seqs=args.max_num_seqs,
                        max_num_batched_tokens=args.max_num_batched_tokens,
                        gpu_memory_utilization=args.gpu_memory_utilization,
-                       enforce_eager=args.enforce_eager, random_init=True, seed=0, device="cuda")
+                       enforce_eager=args.enforce_eager, random_init=True, seed=0,
+                       device=args.device)
     engine = None
     if tp > 1:
         assert world % tp == 0
@@ -115,7 +127,8 @@ def main():
     is_driver = engine is not None
 
     def barrier():
-        torch.cuda.synchronize()
+        if not cpu:
+            torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
 
@@ -157,7 +170,8 @@ def main():
             "metric": BASELINE_METRIC, "value": round(value, 2), "unit": "output_tokens/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype if args.dtype != "bfloat16" else "bf16",
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": {"bfloat16": "bf16", "float16": "fp16", "float32": "fp32"}.get(args.dtype, args.dtype),
             "data": "synthetic random-token prompts, random-init weights",
             "p50_ttft_ms": round(p50_ttft, 2) if p50_ttft else None,
             "p50_tpot_ms": round(statistics.median(tpots) * 1e3, 3) if tpots else None,
