@@ -63,8 +63,25 @@ class BlockManager:
             seq.slot = -1
         seq.block_ids = []
 
-    def check_invariants(self) -> None:
-        """Debug: no block is both free and owned; block 0 never handed out."""
+    def check_invariants(self, seqs=()) -> None:
+        """Debug (KGC_DEBUG=1 checks this every engine step): no block is both free and
+        owned or owned twice; block 0 is never handed out; every block is accounted
+        for; each owner's block-table row mirrors its block list."""
         fs = set(self.free)
         assert len(fs) == len(self.free), "duplicate free block"
-        assert 0 not in fs
+        assert 0 not in fs, "reserved block 0 on the free list"
+        owned: set = set()
+        for s in seqs:
+            if not s.block_ids:
+                continue
+            b = set(s.block_ids)
+            assert len(b) == len(s.block_ids), f"{s.request_id} holds a block twice"
+            assert 0 not in b, f"{s.request_id} holds reserved block 0"
+            assert not (b & fs), f"{s.request_id} holds a free block"
+            assert not (b & owned), f"{s.request_id} shares a block with another sequence"
+            owned |= b
+            assert s.slot >= 0, f"{s.request_id} owns blocks but no table slot"
+            row = self.table[s.slot, : len(s.block_ids)]
+            assert row.tolist() == s.block_ids, f"{s.request_id} block-table row is stale"
+        if seqs:
+            assert len(owned) + len(fs) == self.num_blocks - 1, "leaked KV blocks"

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import itertools
 import logging
+import os
 import time
 from typing import Iterable, Optional, Union
 
@@ -24,6 +25,40 @@ from .worker import TokenFuture, LocalExecutor, MultiprocExecutor, default_max_m
 
 log = logging.getLogger("kgc.engine")
 _PENDING = -1          # placeholder for a sampled token still on the GPU
+
+
+class _StepProfiler:
+    """``KGC_TORCH_PROFILE=dir[:start[:steps]]``: record engine steps start..start+steps
+    with torch.profiler (CPU + HIP activity) and write a Chrome trace into dir."""
+
+    def __init__(self, out_dir: str, start: int, steps: int):
+        self.dir, self.start, self.stop, self.n, self.p = out_dir, start, start + steps, 0, None
+
+    @classmethod
+    def from_env(cls):
+        spec = os.environ.get("KGC_TORCH_PROFILE")
+        if not spec:
+            return None
+        parts = spec.split(":")
+        return cls(parts[0], int(parts[1]) if len(parts) > 1 else 20,
+                   int(parts[2]) if len(parts) > 2 else 10)
+
+    def tick(self) -> None:
+        import torch
+        if self.n == self.start:
+            acts = [torch.profiler.ProfilerActivity.CPU]
+            if torch.cuda.is_available():
+                acts.append(torch.profiler.ProfilerActivity.CUDA)
+            self.p = torch.profiler.profile(activities=acts, record_shapes=False)
+            self.p.__enter__()
+        elif self.n == self.stop and self.p is not None:
+            self.p.__exit__(None, None, None)
+            os.makedirs(self.dir, exist_ok=True)
+            path = os.path.join(self.dir, f"engine_steps_{self.start}_{self.stop}.json")
+            self.p.export_chrome_trace(path)
+            log.info("torch profiler trace: %s", path)
+            self.p = None
+        self.n += 1
 
 
 class LLMEngine:
@@ -49,6 +84,8 @@ class LLMEngine:
         self.eos = self.mcfg.eos_token_id
         self.async_mode = cfg.async_output and getattr(executor, "supports_async", False)
         self._inflight = None
+        self._debug = os.environ.get("KGC_DEBUG", "0") == "1"
+        self._prof = _StepProfiler.from_env()
         self.init_s = time.time() - t0
         log.info("engine ready: %d KV blocks x %d tokens, graphs %.1fs", nb, cfg.block_size,
                  self.graph_s)
@@ -88,6 +125,10 @@ class LLMEngine:
         host bookkeeping (sampled-token append, stop checks, scheduling) overlaps GPU
         execution.  EOS / stop-token finishes are therefore seen one step late (the
         extra token is discarded); length finishes are exact."""
+        if self._debug:
+            self.bm.check_invariants(list(self.scheduler.running))
+        if self._prof is not None:
+            self._prof.tick()
         if not self.async_mode:
             return self._step_sync()
         launched = None

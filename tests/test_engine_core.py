@@ -1,0 +1,182 @@
+"""Engine core on the CPU: block manager, continuous-batching scheduler
+(decode-first, chunked prefill, recompute preemption, aborts, max-model-len), and
+the engine loop end to end with KGC_DEBUG invariants and the torch-profiler hook."""
+import os
+
+import numpy as np
+import pytest
+
+from kubernetes_gpu_cluster_amd.engine.block_manager import BlockManager
+from kubernetes_gpu_cluster_amd.engine.scheduler import Scheduler
+from kubernetes_gpu_cluster_amd.engine.sequence import SamplingParams, Sequence
+
+
+def _seq(rid, n, max_tokens=8):
+    return Sequence(rid, list(range(3, 3 + n)), SamplingParams(max_tokens=max_tokens))
+
+
+# ---------------------------------------------------------------------------- block manager
+def test_block_manager_alloc_free_and_table():
+    bm = BlockManager(num_blocks=9, block_size=4, max_seqs=3, max_blocks_per_seq=4)
+    a, b = _seq("a", 5), _seq("b", 3)
+    assert bm.can_allocate(a, 5)
+    bm.allocate(a, 5)                 # 2 blocks
+    bm.allocate(b, 3)                 # 1 block
+    assert len(a.block_ids) == 2 and len(b.block_ids) == 1 and 0 not in a.block_ids + b.block_ids
+    assert bm.table[a.slot, :2].tolist() == a.block_ids
+    bm.check_invariants([a, b])
+    assert bm.num_free == 8 - 3
+    bm.allocate(a, 8)                 # still 2 blocks
+    assert len(a.block_ids) == 2
+    assert not bm.can_allocate(a, 17)             # > max_blocks_per_seq
+    bm.free_seq(a)
+    assert a.slot == -1 and a.block_ids == [] and bm.num_free == 7
+    bm.check_invariants([b])
+    assert np.all(bm.table[0] == 0) or np.all(bm.table[1] == 0)
+
+
+def test_block_manager_invariants_catch_corruption():
+    bm = BlockManager(6, 4, 2, 4)
+    a, b = _seq("a", 8), _seq("b", 4)
+    bm.allocate(a, 8)
+    bm.allocate(b, 4)
+    b.block_ids.append(a.block_ids[0])            # shared block
+    with pytest.raises(AssertionError):
+        bm.check_invariants([a, b])
+    b.block_ids.pop()
+    bm.free.append(a.block_ids[0])                # owned and free
+    with pytest.raises(AssertionError):
+        bm.check_invariants([a, b])
+    bm.free.pop()
+    bm.free.pop()                                 # leaked block
+    with pytest.raises(AssertionError):
+        bm.check_invariants([a, b])
+
+
+# ---------------------------------------------------------------------------- scheduler
+def _drive(sched, seqs, steps):
+    """Fake model runner: every scheduled unit completes; samplers get one token."""
+    trace = []
+    for _ in range(steps):
+        batch = sched.schedule()
+        trace.append(batch)
+        for seq, n in batch.prefills:
+            seq.num_computed += n
+            if seq.num_computed == seq.num_tokens:
+                seq.output_token_ids.append(7)
+        for seq in batch.decodes:
+            seq.num_computed += 1
+            seq.output_token_ids.append(7)
+        for seq in list(sched.running):
+            if len(seq.output_token_ids) >= seq.max_tokens:
+                sched.finish(seq, "length")
+        sched.bm.check_invariants(sched.running)
+        if not sched.has_work():
+            break
+    return trace
+
+
+def test_chunked_prefill_respects_budget_and_decode_first():
+    bm = BlockManager(64, 4, 4, 16)
+    sched = Scheduler(bm, max_num_seqs=4, token_budget=10, max_model_len=64)
+    long, short = _seq("long", 23, 3), _seq("short", 4, 3)
+    sched.add(long)
+    sched.add(short)
+    trace = _drive(sched, [long, short], 50)
+    assert all(b.num_tokens <= 10 for b in trace)
+    first = trace[0]
+    assert first.prefills == [(long, 10)]          # chunk of the long prompt only
+    # once the long prompt samples, later steps put its decode first
+    for b in trace:
+        if b.decodes and b.prefills:
+            assert b.decodes[0] is long or long not in [s for s, _ in b.prefills]
+    assert len(long.output_token_ids) == 3 and len(short.output_token_ids) == 3
+    assert not sched.has_work() and bm.num_free == 63
+
+
+def test_preemption_recompute_when_kv_runs_out():
+    bm = BlockManager(num_blocks=7, block_size=4, max_seqs=4, max_blocks_per_seq=8)   # 6 usable
+    sched = Scheduler(bm, max_num_seqs=4, token_budget=64, max_model_len=64)
+    seqs = [_seq(f"s{i}", 7, 12) for i in range(3)]
+    for s in seqs:
+        sched.add(s)
+    trace = _drive(sched, seqs, 200)
+    assert sched.num_preemptions > 0
+    assert any(b.preempted for b in trace)
+    assert all(len(s.output_token_ids) == 12 for s in seqs)
+    assert bm.num_free == 6
+
+
+def test_abort_and_max_seqs():
+    bm = BlockManager(64, 4, 2, 16)
+    sched = Scheduler(bm, max_num_seqs=2, token_budget=100, max_model_len=64)
+    a, b, c = _seq("a", 5), _seq("b", 5), _seq("c", 5)
+    for s in (a, b, c):
+        sched.add(s)
+    batch = sched.schedule()
+    assert len(batch.prefills) == 2 and len(sched.waiting) == 1   # cap of 2 running
+    assert sched.abort("b") is b and b.finish_reason == "abort" and b.block_ids == []
+    assert sched.abort("zzz") is None
+    bm.check_invariants(sched.running)
+
+
+# ---------------------------------------------------------------------------- engine loop
+def _llm(**kw):
+    from kubernetes_gpu_cluster_amd.engine.llm_engine import LLM
+    base = dict(device="cpu", dtype="float32", random_init=True, max_model_len=128,
+                max_num_seqs=4, max_num_batched_tokens=48, seed=1)
+    base.update(kw)
+    return LLM("tiny-llama", **base)
+
+
+def test_engine_preemption_matches_ample_kv(monkeypatch):
+    """Greedy outputs are identical with a KV pool so small that sequences get
+    preempted and recomputed; KGC_DEBUG checks block invariants every step."""
+    monkeypatch.setenv("KGC_DEBUG", "1")
+    prompts = [[5 + i, 6, 7, 8, 9, 10, 11] * 3 for i in range(4)]
+    sp = SamplingParams(temperature=0, max_tokens=20, ignore_eos=True)
+    ample = _llm(num_gpu_blocks_override=64, block_size=16)
+    ref = [o.output_token_ids for o in ample.generate(prompts, sp)]
+    ample.shutdown()
+    tight = _llm(num_gpu_blocks_override=6, block_size=16)
+    got = [o.output_token_ids for o in tight.generate(prompts, sp)]
+    npre = tight.engine.scheduler.num_preemptions
+    tight.shutdown()
+    assert npre > 0
+    assert got == ref
+
+
+def test_engine_async_equals_sync():
+    prompts = [[5, 6, 7], [9] * 30, [11, 12]]
+    sp = [SamplingParams(temperature=0.8, seed=s, max_tokens=9, ignore_eos=True) for s in (1, 2, 3)]
+    outs = []
+    for async_output in (True, False):
+        llm = _llm(num_gpu_blocks_override=64, block_size=16, async_output=async_output)
+        assert llm.engine.async_mode == async_output
+        outs.append([o.output_token_ids for o in llm.generate(prompts, sp)])
+        llm.shutdown()
+    assert outs[0] == outs[1]
+
+
+def test_engine_stop_tokens_and_max_model_len():
+    llm = _llm(num_gpu_blocks_override=64, block_size=16)
+    o = llm.generate([[5, 6, 7]], SamplingParams(temperature=0, max_tokens=30, ignore_eos=True))[0]
+    stop_tok = o.output_token_ids[4]
+    first = o.output_token_ids.index(stop_tok)
+    o2 = llm.generate([[5, 6, 7]], SamplingParams(temperature=0, max_tokens=30,
+                                                  stop_token_ids=[stop_tok]))[0]
+    assert o2.finish_reason == "stop" and o2.output_token_ids == o.output_token_ids[:first + 1]
+    with pytest.raises(ValueError):
+        llm.engine.add_request(list(range(200)), SamplingParams())
+    o3 = llm.generate([list(range(3, 123))], SamplingParams(max_tokens=50, ignore_eos=True))[0]
+    assert len(o3.output_token_ids) == 128 - 120 and o3.finish_reason == "length"
+    llm.shutdown()
+
+
+def test_torch_profiler_hook(tmp_path, monkeypatch):
+    monkeypatch.setenv("KGC_TORCH_PROFILE", f"{tmp_path}:1:3")
+    llm = _llm(num_gpu_blocks_override=64, block_size=16)
+    llm.generate([[5, 6, 7]], SamplingParams(max_tokens=8, ignore_eos=True))
+    llm.shutdown()
+    files = os.listdir(tmp_path)
+    assert files == ["engine_steps_1_4.json"]
