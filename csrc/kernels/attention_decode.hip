@@ -59,7 +59,6 @@ __global__ __launch_bounds__(256, 3) void paged_decode_kernel(
   const int G = nq / nkv;
   // clamp to the block-table capacity: a bad length gives wrong output, never a fault
   const int ctx = min(ctx_lens[b], bt_stride << bs_log2);
-  const int P = (ctx + DEC_PART - 1) / DEC_PART;
   const int* bt = block_tables + (int64_t)b * bt_stride;
   const int bsm = (1 << bs_log2) - 1;
   const int64_t head_stride = (int64_t)D << bs_log2;   // elements per (block, kv-head)
@@ -85,18 +84,29 @@ __global__ __launch_bounds__(256, 3) void paged_decode_kernel(
 #pragma unroll
   for (int t = 0; t < DT; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int p = blockIdx.z * 4 + wave; p < P; p += gridDim.z * 4) {
-    const int base = p * DEC_PART;
+  // Balanced split: the ctx's 32-token chunks are divided evenly over the Z x 4 waves
+  // (sizes differ by at most one chunk), so no wave of a workgroup idles while a
+  // sibling processes one more 64-token partition (whole-partition round-robin left
+  // up to 25 % of wave time idle at ctx ~ 600).  A wave's last step may hold one
+  // chunk; the other chunk's loads clamp to the wave's last token (cache hits) and
+  // its scores are masked.
+  const int nchunk = (ctx + 31) >> 5;
+  const int nwk = gridDim.z * 4, wk = blockIdx.z * 4 + wave;
+  const int c0 = (int)(((int64_t)nchunk * wk) / nwk);
+  const int c1 = (int)(((int64_t)nchunk * (wk + 1)) / nwk);
+  const int end = min(ctx, c1 << 5);       // this wave's token range is [c0*32, end)
+  for (int ci = c0; ci < c1; ci += DEC_CHUNKS) {
+    const int base = ci << 5;
     const T* kaddr[DEC_CHUNKS][2];
     const T* vaddr[DEC_CHUNKS];
 #pragma unroll
     for (int c = 0; c < DEC_CHUNKS; ++c) {
-      const int ta = min(base + c * 32 + keyA, ctx - 1);
-      const int tb = min(base + c * 32 + keyA + 4, ctx - 1);
+      const int ta = min(base + c * 32 + keyA, end - 1);
+      const int tb = min(base + c * 32 + keyA + 4, end - 1);
       kaddr[c][0] = kbase + bt[ta >> bs_log2] * blk_stride + (int64_t)(ta & bsm) * D + 8 * qd;
       kaddr[c][1] = kbase + bt[tb >> bs_log2] * blk_stride + (int64_t)(tb & bsm) * D + 8 * qd;
       // V^T 8-key group of keys t0..t0+7: [(t0 & bsm) / 8][d][8]; 16 lanes = 256 B
-      const int t0 = min(base + c * 32 + 8 * qd, ctx - 1) & ~7;
+      const int t0 = min(base + c * 32 + 8 * qd, end - 1) & ~7;
       vaddr[c] = vbase + bt[t0 >> bs_log2] * blk_stride + ((t0 & bsm) >> 3) * (D * 8) + r16 * 8;
     }
     Pack8<T> kf[DEC_CHUNKS][2][KS];
@@ -140,8 +150,8 @@ __global__ __launch_bounds__(256, 3) void paged_decode_kernel(
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int tok = base + c * 32 + 8 * qd + i;
-        sa[c][i] = tok < ctx ? sa[c][i] * scale_log2 : -INFINITY;
-        sb[c][i] = tok + 4 < ctx ? sb[c][i] * scale_log2 : -INFINITY;
+        sa[c][i] = tok < end ? sa[c][i] * scale_log2 : -INFINITY;
+        sb[c][i] = tok + 4 < end ? sb[c][i] * scale_log2 : -INFINITY;
         m = fmaxf(m, fmaxf(sa[c][i], sb[c][i]));
       }
     }
