@@ -46,6 +46,13 @@ class EngineConfig:
     cuda_graph_max_bs: int = 256
     async_output: bool = True             # overlap host bookkeeping with the next step
     num_cpu_blocks: int = 0
+    # one engine spread over several nodes / pods (TP x PP ranks split evenly):
+    # node 0 runs the API server and ranks [0, g); node k runs ranks [k*g, (k+1)*g)
+    # via entrypoints.worker_node; rendezvous at master_addr:master_port
+    nnodes: int = 1
+    node_rank: int = 0
+    master_addr: Optional[str] = None
+    master_port: int = 29500
 
     def torch_dtype(self, model_default: torch.dtype = torch.bfloat16) -> torch.dtype:
         d = _DTYPES.get(self.dtype.lower())
@@ -61,6 +68,19 @@ class EngineConfig:
     @property
     def world_size(self) -> int:
         return self.tensor_parallel_size * self.pipeline_parallel_size
+
+    @property
+    def ranks_per_node(self) -> int:
+        if self.world_size % self.nnodes:
+            raise ValueError(f"tp*pp={self.world_size} does not split over {self.nnodes} nodes")
+        return self.world_size // self.nnodes
+
+    def dist_env(self) -> dict:
+        """Rendezvous env shared by every rank of this engine."""
+        if self.nnodes > 1 and not self.master_addr:
+            raise ValueError("--nnodes > 1 needs --master-addr (node 0's address)")
+        return {"MASTER_ADDR": self.master_addr or "127.0.0.1", "MASTER_PORT": str(self.master_port),
+                "WORLD_SIZE": str(self.world_size)}
 
     def token_budget(self) -> int:
         if self.max_num_batched_tokens:
@@ -95,6 +115,10 @@ def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     a("--device", type=str, default="auto")
     a("--moe-parallel", type=str, default="tp", choices=["tp", "ep"])
     a("--cuda-graph-max-bs", type=int, default=256)
+    a("--nnodes", type=int, default=1, help="nodes (pods) one engine spans")
+    a("--node-rank", type=int, default=0)
+    a("--master-addr", type=str, default=None, help="address of node 0 (multi-node)")
+    a("--master-port", type=int, default=29500)
     a("--swap-space", type=float, default=0, help="accepted for compatibility (unused)")
     a("--disable-log-requests", action="store_true")
     a("--disable-log-stats", action="store_true")
@@ -115,4 +139,6 @@ def config_from_args(ns: argparse.Namespace) -> EngineConfig:
         trust_remote_code=ns.trust_remote_code, kv_cache_dtype=ns.kv_cache_dtype, seed=ns.seed,
         random_init=ns.random_init or ns.load_format == "dummy",
         num_gpu_blocks_override=ns.num_gpu_blocks_override, device=ns.device,
-        moe_parallel=ns.moe_parallel, cuda_graph_max_bs=ns.cuda_graph_max_bs)
+        moe_parallel=ns.moe_parallel, cuda_graph_max_bs=ns.cuda_graph_max_bs,
+        nnodes=ns.nnodes, node_rank=ns.node_rank, master_addr=ns.master_addr,
+        master_port=ns.master_port)

@@ -271,12 +271,13 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _spawn_entry(rank: int, cfg: EngineConfig, env: dict) -> None:
+def _spawn_entry(rank: int, cfg: EngineConfig, env: dict, local: Optional[int] = None) -> None:
+    local = rank if local is None else local
     os.environ.update(env)
     os.environ["RANK"] = str(rank)
-    os.environ["LOCAL_RANK"] = str(rank)
+    os.environ["LOCAL_RANK"] = str(local)
     try:
-        w = Worker(cfg, rank=rank, local_device=rank)
+        w = Worker(cfg, rank=rank, local_device=local)
         worker_loop(w)
     except Exception:
         traceback.print_exc()
@@ -285,21 +286,35 @@ def _spawn_entry(rank: int, cfg: EngineConfig, env: dict) -> None:
         destroy_parallel()
 
 
+def spawn_local_ranks(cfg: EngineConfig, env: dict, first: int, last: int, daemon: bool = True):
+    """Start ranks [first, last) of this node as worker processes (local device =
+    rank - node_rank * ranks_per_node)."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    base = cfg.node_rank * cfg.ranks_per_node
+    procs = []
+    for r in range(first, last):
+        p = ctx.Process(target=_spawn_entry, args=(r, cfg, env, r - base), daemon=daemon)
+        p.start()
+        procs.append(p)
+    return procs
+
+
 class MultiprocExecutor(_DistExecutorBase):
+    """Rank 0 (the driver) plus this node's other ranks as spawned processes; with
+    ``cfg.nnodes > 1`` the remaining nodes run ``entrypoints.worker_node`` and join
+    the same rendezvous."""
+
     def __init__(self, cfg: EngineConfig):
-        import torch.multiprocessing as mp
-        ws = cfg.world_size
-        env = {"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(_free_port()),
-               "WORLD_SIZE": str(ws)}
-        for k in ("HSA_ENABLE_IPC_MODE_LEGACY",):
+        if cfg.node_rank != 0:
+            raise ValueError("the engine (driver) runs on node 0; use entrypoints.worker_node")
+        env = cfg.dist_env()
+        if cfg.nnodes == 1 and not cfg.master_addr:
+            env["MASTER_PORT"] = str(_free_port())
+        for k in ("HSA_ENABLE_IPC_MODE_LEGACY", "KGC_DIST_BACKEND"):
             if k in os.environ:
                 env[k] = os.environ[k]
-        ctx = mp.get_context("spawn")
-        self.procs = []
-        for r in range(1, ws):
-            p = ctx.Process(target=_spawn_entry, args=(r, cfg, env), daemon=True)
-            p.start()
-            self.procs.append(p)
+        self.procs = spawn_local_ranks(cfg, env, 1, cfg.ranks_per_node)
         os.environ.update(env)
         os.environ["RANK"] = "0"
         os.environ["LOCAL_RANK"] = "0"

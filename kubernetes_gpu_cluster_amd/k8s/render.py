@@ -19,6 +19,13 @@ MI355X-specific mapping:
   spread selectors (``values-01-minimal-example2.yaml:23-49``) bind.
 * ``PYTORCH_CUDA_ALLOC_CONF`` is mirrored to ``PYTORCH_HIP_ALLOC_CONF``.
 * ``lmcacheConfig`` is accepted and ignored.
+* ``vllmConfig.nnodes: N`` (extension) spreads one engine replica over N pods, the
+  in-house replacement for the reference's KubeRay multi-pod pipeline
+  (``values-01-minimal-example4.yaml:42-46``): a leader StatefulSet (API server +
+  driver, node 0; ``component: serving-engine``, so the router discovers only it) and
+  a worker StatefulSet of N-1 pods (``entrypoints.worker_node``, node rank = pod index
+  + 1), rendezvousing at the leader's stable headless-service DNS name.  Each pod gets
+  ``requestGPU`` GPUs, or ``tp*pp/N`` when that is larger.
 
     python -m kubernetes_gpu_cluster_amd.k8s.render -f values.yaml --release vllm | kubectl apply -f -
 """
@@ -187,6 +194,10 @@ def render_engine(ms: dict, release: str, namespace: str, engine_image: str, eng
     dep_name = f"{release}-{name}-deployment-vllm"
     sel = {"app.kubernetes.io/instance": release, "model": name,
            "app.kubernetes.io/component": "serving-engine"}
+    nnodes = int((ms.get("vllmConfig") or {}).get("nnodes", 1) or 1)
+    if nnodes > 1:
+        return _render_multinode(ms, name, release, namespace, nnodes, degree, labels, sel,
+                                 spec, container)
     dep = {"apiVersion": "apps/v1", "kind": "Deployment",
            "metadata": {"name": dep_name, "namespace": namespace, "labels": labels,
                         "annotations": dict(ms.get("annotations") or {})},
@@ -200,6 +211,83 @@ def render_engine(ms: dict, release: str, namespace: str, engine_image: str, eng
            "spec": {"selector": sel, "ports": [{"name": "http", "port": ENGINE_PORT,
                                                 "targetPort": ENGINE_PORT}]}}
     return [dep, svc]
+
+
+MULTINODE_PORT = 29500
+
+
+def _render_multinode(ms, name, release, namespace, nnodes, degree, labels, sel, spec,
+                      container) -> list[dict]:
+    """Leader + worker StatefulSets for one engine spread over ``nnodes`` pods."""
+    if degree % nnodes:
+        raise ValuesError(f"modelSpec {name}: tp*pp={degree} does not split over nnodes={nnodes}")
+    per_pod = max(int(ms.get("requestGPU", 1) or 0), degree // nnodes)
+    if int(ms.get("requestGPU", 1) or 0) == 0:
+        raise ValuesError(f"modelSpec {name}: nnodes > 1 needs GPU pods")
+    for obj in (container["resources"]["requests"], container["resources"]["limits"]):
+        obj["amd.com/gpu"] = str(per_pod)
+    out = []
+    reps = int(ms.get("replicaCount", 1))
+    for r in range(reps):
+        sfx = f"-r{r}" if reps > 1 else ""
+        leader, worker = f"{release}-{name}{sfx}-leader", f"{release}-{name}{sfx}-worker"
+        group = {"kgc.amd.com/engine-group": f"{name}{sfx}"}
+        master = f"{leader}-0.{leader}.{namespace}.svc.cluster.local"
+        dist = ["--nnodes", str(nnodes), "--master-addr", master,
+                "--master-port", str(MULTINODE_PORT)]
+        lead_c = copy.deepcopy(container)
+        lead_c["args"] = list(container["args"]) + ["--node-rank", "0"] + dist
+        lead_c["ports"] = lead_c["ports"] + [{"name": "dist", "containerPort": MULTINODE_PORT}]
+        wk_c = copy.deepcopy(container)
+        wk_args, skip = [], False
+        for a in container["args"]:          # api-server-only flags
+            if skip:
+                skip = False
+                continue
+            if a in ("--host", "--port"):
+                skip = True
+                continue
+            wk_args.append(a)
+        wk_c["command"] = ["python3", "-m", "kubernetes_gpu_cluster_amd.entrypoints.worker_node"]
+        wk_c["args"] = wk_args + dist + ["--node-rank-offset", "1", "--health-port", str(ENGINE_PORT)]
+        wk_c["env"] = wk_c["env"] + [{"name": "POD_INDEX", "valueFrom": {"fieldRef": {
+            "fieldPath": "metadata.labels['apps.kubernetes.io/pod-index']"}}}]
+        wk_c["ports"] = [{"name": "health", "containerPort": ENGINE_PORT}]
+        lead_labels = dict(labels, **group)
+        wk_labels = dict(labels, **group)
+        wk_labels["app.kubernetes.io/component"] = "engine-worker"
+        lead_sel = dict(sel, **group)
+        wk_sel = dict(sel, **group)
+        wk_sel["app.kubernetes.io/component"] = "engine-worker"
+
+        def sts(nm, lbl, sl, c, replicas):
+            pod_spec = copy.deepcopy(spec)
+            pod_spec["containers"] = [c]
+            return {"apiVersion": "apps/v1", "kind": "StatefulSet",
+                    "metadata": {"name": nm, "namespace": namespace, "labels": lbl,
+                                 "annotations": dict(ms.get("annotations") or {})},
+                    "spec": {"serviceName": nm, "replicas": replicas,
+                             "podManagementPolicy": "Parallel",
+                             "selector": {"matchLabels": sl},
+                             "template": {"metadata": {"labels": lbl}, "spec": pod_spec}}}
+
+        def headless(nm, lbl, sl, ports):
+            return {"apiVersion": "v1", "kind": "Service",
+                    "metadata": {"name": nm, "namespace": namespace, "labels": lbl},
+                    "spec": {"clusterIP": "None", "publishNotReadyAddresses": True,
+                             "selector": sl, "ports": ports}}
+        out += [headless(leader, lead_labels, lead_sel,
+                         [{"name": "dist", "port": MULTINODE_PORT},
+                          {"name": "http", "port": ENGINE_PORT}]),
+                headless(worker, wk_labels, wk_sel, [{"name": "health", "port": ENGINE_PORT}]),
+                sts(leader, lead_labels, lead_sel, lead_c, 1),
+                sts(worker, wk_labels, wk_sel, wk_c, nnodes - 1)]
+    out.append({"apiVersion": "v1", "kind": "Service",
+                "metadata": {"name": f"{release}-{name}-engine-service", "namespace": namespace,
+                             "labels": labels},
+                "spec": {"selector": sel, "ports": [{"name": "http", "port": ENGINE_PORT,
+                                                     "targetPort": ENGINE_PORT}]}})
+    return out
 
 
 def render_router(release: str, namespace: str, engine_image: str, engine_tag: str,

@@ -131,3 +131,43 @@ def test_engine_multiproc_tp2_and_pp2():
             llm.shutdown()
         assert outs[(2, 1)] == outs[(1, 1)]
         assert outs[(1, 2)] == outs[(1, 1)]
+
+
+def test_engine_two_nodes_matches_single_node(tmp_path):
+    """One TP=2 engine over two "nodes": the driver (node 0, in this process) and
+    entrypoints.worker_node as a separate process (node 1) rendezvous over TCP; greedy
+    output == TP=1.  The CPU/gloo rehearsal of the multi-pod StatefulSet layout."""
+    import subprocess
+    import sys
+    from kubernetes_gpu_cluster_amd.engine.llm_engine import LLM
+    from kubernetes_gpu_cluster_amd.engine.sequence import SamplingParams
+    d = str(tmp_path / "m")
+    _write_hf_dir(d, "tiny-llama")
+    prompts = [list(range(3, 40)), [5, 6, 7] * 20]
+    sp = [SamplingParams(temperature=0, max_tokens=8, ignore_eos=True)] * 2
+    common = dict(device="cpu", dtype="float32", max_model_len=256, max_num_seqs=4,
+                  max_num_batched_tokens=64, num_gpu_blocks_override=64)
+    ref_llm = LLM(d, **common)
+    ref = [o.output_token_ids for o in ref_llm.generate(prompts, sp)]
+    ref_llm.shutdown()
+    port = _port()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    worker = subprocess.Popen(
+        [sys.executable, "-m", "kubernetes_gpu_cluster_amd.entrypoints.worker_node", d,
+         "--tensor-parallel-size", "2", "--nnodes", "2", "--node-rank", "1",
+         "--master-addr", "127.0.0.1", "--master-port", str(port), "--device", "cpu",
+         "--dtype", "float32", "--max-model-len", "256", "--max-num-seqs", "4",
+         "--max-num-batched-tokens", "64", "--num-gpu-blocks-override", "64"],
+        cwd=root, env=dict(os.environ, PYTHONPATH=root), stdout=subprocess.PIPE,
+        stderr=subprocess.STDOUT, text=True)
+    try:
+        llm = LLM(d, tensor_parallel_size=2, nnodes=2, node_rank=0, master_addr="127.0.0.1",
+                  master_port=port, **common)
+        got = [o.output_token_ids for o in llm.generate(prompts, sp)]
+        llm.shutdown()
+        rc = worker.wait(timeout=120)
+    finally:
+        if worker.poll() is None:
+            worker.kill()
+    assert rc == 0, worker.stdout.read()[-3000:]
+    assert got == ref

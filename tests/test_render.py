@@ -149,3 +149,40 @@ def test_chart_parity():
         assert key in tpl, key
     assert "vllm-router-service" in rt and "port: 80" in rt and "pods" in rt
     yaml.safe_load(open(os.path.join(ROOT, "deploy/chart/kgc-stack/Chart.yaml")))
+
+
+def test_multinode_leader_worker_statefulsets():
+    v = _load(os.path.join(ROOT, "deploy/values/multinode/values-llama3-70b-2nodes-pp2.yaml"))
+    objs = render(v, release="vllm", namespace="ml")
+    sts = {o["metadata"]["name"]: o for o in _by_kind(objs, "StatefulSet")}
+    assert set(sts) == {"vllm-llama3-70b-2n-leader", "vllm-llama3-70b-2n-worker"}
+    assert not [d for d in _by_kind(objs, "Deployment") if "-deployment-vllm" in d["metadata"]["name"]]
+    lead, wk = sts["vllm-llama3-70b-2n-leader"], sts["vllm-llama3-70b-2n-worker"]
+    assert lead["spec"]["replicas"] == 1 and wk["spec"]["replicas"] == 1
+    lc = lead["spec"]["template"]["spec"]["containers"][0]
+    wc = wk["spec"]["template"]["spec"]["containers"][0]
+    master = "vllm-llama3-70b-2n-leader-0.vllm-llama3-70b-2n-leader.ml.svc.cluster.local"
+    for c in (lc, wc):
+        a = c["args"]
+        assert a[a.index("--nnodes") + 1] == "2" and a[a.index("--master-addr") + 1] == master
+        assert c["resources"]["limits"]["amd.com/gpu"] == "4"
+    assert lc["command"][-1].endswith("api_server") and "--node-rank" in lc["args"]
+    assert wc["command"][-1].endswith("worker_node")
+    assert "--host" not in wc["args"] and "--port" not in wc["args"]
+    assert any(e["name"] == "POD_INDEX" for e in wc["env"])
+    # the router discovers only the leader; the engine Service targets only the leader
+    assert lead["spec"]["template"]["metadata"]["labels"]["app.kubernetes.io/component"] == "serving-engine"
+    assert wk["spec"]["template"]["metadata"]["labels"]["app.kubernetes.io/component"] == "engine-worker"
+    heads = [s for s in _by_kind(objs, "Service") if s["spec"].get("clusterIP") == "None"]
+    assert {s["metadata"]["name"] for s in heads} == set(sts)
+    # the rendered argv parse with each entrypoint's own parser
+    from kubernetes_gpu_cluster_amd.entrypoints.api_server import make_parser as api_parser
+    from kubernetes_gpu_cluster_amd.entrypoints.worker_node import make_parser as wk_parser
+    ns = wk_parser().parse_args(wc["args"])
+    assert ns.nnodes == 2 and ns.node_rank_offset == 1 and ns.pipeline_parallel_size == 2
+    ns = api_parser().parse_args(lc["args"])
+    assert ns.nnodes == 2 and ns.node_rank == 0 and ns.tensor_parallel_size == 4
+    bad = dict(v)
+    bad["servingEngineSpec"]["modelSpec"][0]["vllmConfig"]["nnodes"] = 3
+    with pytest.raises(ValuesError):
+        render(bad)
