@@ -1,6 +1,7 @@
 """values-*.yaml -> manifests renderer (SURVEY.md §2.7 schema) and Helm chart parity."""
 import glob
 import os
+import re
 
 import pytest
 import yaml
@@ -148,6 +149,14 @@ def test_chart_parity():
                 "PYTORCH_HIP_ALLOC_CONF", "/health"):
         assert key in tpl, key
     assert "vllm-router-service" in rt and "port: 80" in rt and "pods" in rt
+    mn = open(os.path.join(ROOT, "deploy/chart/kgc-stack/templates/engine-multinode.yaml")).read()
+    for key in ("StatefulSet", "worker_node", "--nnodes", "--master-addr", "--node-rank-offset",
+                "apps.kubernetes.io/pod-index", "clusterIP: None", "engine-worker"):
+        assert key in mn, key
+    # template actions balance (no helm binary: a cheap structural check)
+    for t in (tpl, mn):
+        opens = len(re.findall(r"{{-?\s*(if|range|with|define)\b", t))
+        assert opens == len(re.findall(r"{{-?\s*end\s*-?}}", t))
     yaml.safe_load(open(os.path.join(ROOT, "deploy/chart/kgc-stack/Chart.yaml")))
 
 

@@ -22,6 +22,10 @@ def main():
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--max-bs", type=int, default=256)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--prefill-m", type=int, nargs="*", default=[],
+                    help="also tune these token counts (full chunked-prefill steps run exactly "
+                         "--max-num-batched-tokens tokens)")
+    ap.add_argument("--append", action="store_true", help="keep the rows already in --out")
     a = ap.parse_args()
     from kubernetes_gpu_cluster_amd.utils.gemm_tuning import default_table_path
     out = a.out or default_table_path(a.model, a.tp)
@@ -30,6 +34,8 @@ def main():
     torch.cuda.tunable.enable(True)
     torch.cuda.tunable.tuning_enable(True)
     torch.cuda.tunable.set_filename(out, insert_device_ordinal=False)
+    if a.append and os.path.exists(out):
+        torch.cuda.tunable.read_file(out)
     torch.cuda.tunable.set_max_tuning_duration(60)
     import torch.nn.functional as F
     from kubernetes_gpu_cluster_amd.engine.model_runner import graph_buckets
@@ -44,7 +50,7 @@ def main():
     dev = torch.device("cuda")
     for name, (N, K) in shapes.items():
         w = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
-        for M in graph_buckets(a.max_bs):
+        for M in list(graph_buckets(a.max_bs)) + [m for m in a.prefill_m if name != "lm_head"]:
             x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
             F.linear(x, w)
             torch.cuda.synchronize()
