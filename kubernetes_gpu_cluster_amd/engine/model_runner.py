@@ -29,6 +29,7 @@ from ..models.configs import ModelConfig
 from ..ops import reference as ref
 from ..parallel import comm
 from ..parallel.state import get_state
+from .logits_processor import LogitsProcessor, needs_counts
 from .sequence import Sequence
 
 
@@ -49,14 +50,17 @@ class StepPlan:
     B: int                 # graph bucket (0 = eager)
     max_ctx: int           # longest decode context
     dev_tok: int           # 1: decode input tokens come from the device-side last_tok table
+    tok_bcast: int         # 1: TP ranks take the driver's sampled ids (driver-side logits processing)
     i64: np.ndarray
     i32: np.ndarray
     f32: np.ndarray
     lp: Optional[list] = None   # driver only: [(sampled row, top-k)] for logprobs requests
+    proc: Optional[list] = None  # driver only: [(sampled row, slot, params)] penalties/bias/min_p
+    proc_init: Optional[list] = None  # driver only: [(slot, prompt ids, output ids)]
 
     def header(self) -> list[int]:
         return [self.T, self.Tp, self.P, self.D, self.S, self.W, self.B, self.max_ctx,
-                self.dev_tok]
+                self.dev_tok, self.tok_bcast]
 
 
 class Layout:
@@ -121,6 +125,7 @@ class ModelRunner:
         self.graphs: dict[int, tuple] = {}
         self.graph_pool = None
         self.sample_out = torch.zeros(max_num_seqs, dtype=torch.int64, device=device)
+        self.processor = LogitsProcessor(max_num_seqs, mcfg.vocab_size, device)
         # last sampled token per sequence slot: decode steps read their input token
         # here, so the host can launch step N+1 before it has seen step N's tokens
         self.last_tok = torch.zeros(max_num_seqs, dtype=torch.int64, device=device)
@@ -198,7 +203,7 @@ class ModelRunner:
         i64[L.lidx:L.lidx + P] = qsl[1:] - 1
         self.hf.numpy()[: 2 * self.L.Smax] = 1.0
         i64[L.sslots:L.sslots + P] = 0
-        plan = StepPlan(T, T, P, 0, P, len(ws), 0, 0, 0, i64, i32, self.hf.numpy())
+        plan = StepPlan(T, T, P, 0, P, len(ws), 0, 0, 0, 0, i64, i32, self.hf.numpy())
         self.run(plan)
 
     # ------------------------------------------------------------------ packing (driver)
@@ -283,8 +288,17 @@ class ModelRunner:
             i64[L.lidx:L.lidx + B] = np.arange(B)   # graph rows index their own hidden row
         lp = [(j, s.params.logprobs) for j, s in enumerate(samplers)
               if s.params.logprobs is not None] or None
-        return StepPlan(T, Tp, P, D, S, W, B, max_ctx, int(device_tokens and D > 0), i64, i32,
-                        f32, lp), samplers
+        proc, proc_init = None, None
+        if any(s.params.needs_proc for s in samplers):
+            proc = [(j, s.slot, s.params) for j, s in enumerate(samplers) if s.params.needs_proc]
+            proc_init = [(s.slot, s.prompt_token_ids, list(s.output_token_ids))
+                         for s in samplers if needs_counts(s.params) and s.proc_slot != s.slot] or None
+            for s in samplers:
+                if needs_counts(s.params):
+                    s.proc_slot = s.slot
+        bcast = int(proc is not None and self.ps.tp_size > 1)
+        return StepPlan(T, Tp, P, D, S, W, B, max_ctx, int(device_tokens and D > 0), bcast,
+                        i64, i32, f32, lp, proc, proc_init), samplers
 
     # ------------------------------------------------------------------ execution (all ranks)
     def _upload(self, plan: StepPlan) -> None:
@@ -356,23 +370,43 @@ class ModelRunner:
                 return None
             idx = self.d64[L.lidx:L.lidx + plan.S]
             logits = self.model.compute_logits(out.index_select(0, idx))
+        pre_lp = None
+        if plan.proc and self.model.last:
+            if plan.lp:       # logprobs report the raw distribution, before processing
+                pre_lp = self._logprobs_pre(plan.lp, logits)
+            if plan.proc_init:
+                for slot, prompt, output in plan.proc_init:
+                    self.processor.init_slot(slot, prompt, output)
+            self.processor.apply(logits, plan.proc)
         out = self.sample_out[: plan.S]
         res = ops.sample(logits, self.df[L.temp:L.temp + plan.S], self.d32[L.topk:L.topk + plan.S],
                          self.df[L.topp:L.topp + plan.S], self.d64[L.seeds:L.seeds + plan.S],
                          out=out if self.is_gpu else None)
+        if plan.tok_bcast:
+            comm.tp_broadcast(res, 0)          # every TP rank continues with the driver's ids
+        if plan.proc and self.model.last:
+            self.processor.update(plan.proc, res)
         self.last_tok.index_copy_(0, self.d64[L.sslots:L.sslots + plan.S], res)
-        self._last_lp = self._logprobs(plan.lp, logits, res) if plan.lp else None
+        if plan.lp:
+            self._last_lp = self._logprobs_post(pre_lp or self._logprobs_pre(plan.lp, logits), res)
+        else:
+            self._last_lp = None
         return res
 
-    def _logprobs(self, lp: list, logits: torch.Tensor, res: torch.Tensor):
-        """log-softmax of the raw logits for the rows that asked for logprobs: the
-        sampled token's logprob and the top-k alternatives (device tensors; copied to
-        the host only when the step's tokens are read)."""
+    def _logprobs_pre(self, lp: list, logits: torch.Tensor):
+        """log-softmax of the raw logits for the rows that asked for logprobs and their
+        top-k alternatives (device tensors; copied to the host only when the step's
+        tokens are read)."""
         rows = torch.tensor([r for r, _ in lp], device=logits.device)
         kmax = max(1, max(k for _, k in lp))
         lsm = torch.log_softmax(logits.index_select(0, rows).float(), dim=-1)
-        chosen = lsm.gather(1, res.index_select(0, rows).view(-1, 1)).view(-1)
         topv, topi = lsm.topk(min(kmax, lsm.shape[-1]), dim=-1)
+        return lp, rows, lsm, topv, topi
+
+    @staticmethod
+    def _logprobs_post(pre, res: torch.Tensor):
+        lp, rows, lsm, topv, topi = pre
+        chosen = lsm.gather(1, res.index_select(0, rows).view(-1, 1)).view(-1)
         return lp, chosen, topv, topi
 
     def take_logprobs(self):

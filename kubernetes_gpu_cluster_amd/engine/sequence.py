@@ -23,6 +23,12 @@ class SamplingParams:
     seed: Optional[int] = None
     n: int = 1
     logprobs: Optional[int] = None
+    presence_penalty: float = 0.0
+    frequency_penalty: float = 0.0
+    repetition_penalty: float = 1.0
+    min_p: float = 0.0
+    logit_bias: Optional[dict] = None
+    needs_proc: bool = dataclasses.field(default=False, init=False, repr=False)
 
     def __post_init__(self):
         if self.temperature < 0:
@@ -33,8 +39,23 @@ class SamplingParams:
             raise ValueError("top_k must be -1 (disabled) or >= 1")
         if self.max_tokens is not None and self.max_tokens < 1:
             raise ValueError("max_tokens must be >= 1")
-        if self.n != 1:
-            raise ValueError("only n=1 is supported")
+        if self.n < 1:
+            raise ValueError("n must be >= 1")
+        if not -2.0 <= self.presence_penalty <= 2.0 or not -2.0 <= self.frequency_penalty <= 2.0:
+            raise ValueError("presence_penalty / frequency_penalty must be in [-2, 2]")
+        if self.repetition_penalty <= 0:
+            raise ValueError("repetition_penalty must be > 0")
+        if not 0.0 <= self.min_p <= 1.0:
+            raise ValueError("min_p must be in [0, 1]")
+        if self.logit_bias:
+            for k, v in self.logit_bias.items():
+                if not -100 <= float(v) <= 100:
+                    raise ValueError("logit_bias values must be in [-100, 100]")
+                int(k)
+        # penalties / bias / min_p need the driver-side logits processor
+        self.needs_proc = bool(self.presence_penalty or self.frequency_penalty
+                               or self.repetition_penalty != 1.0 or self.logit_bias
+                               or self.min_p > 0.0)
 
 
 class SeqStatus(enum.Enum):
@@ -48,7 +69,7 @@ class Sequence:
                  "status", "block_ids", "num_computed", "arrival_time", "first_token_time",
                  "finish_time", "finish_reason", "seed", "num_preemptions", "max_tokens",
                  "slot", "last_token_time", "token_times", "prompt_text", "stream",
-                 "num_pending")
+                 "num_pending", "proc_slot")
 
     def __init__(self, request_id: str, prompt_token_ids: list[int], params: SamplingParams,
                  arrival_time: Optional[float] = None, max_model_len: int = 1 << 30):
@@ -74,6 +95,7 @@ class Sequence:
         self.prompt_text: Optional[str] = None
         self.stream = None
         self.num_pending = 0                  # trailing sampled tokens still on the GPU
+        self.proc_slot = -1                   # slot whose penalty statistics are built
 
     @property
     def num_tokens(self) -> int:

@@ -141,7 +141,7 @@ def worker_loop(worker: Worker) -> None:
         elif cmd == CMD_CAPTURE:
             worker.capture()
         elif cmd == CMD_STEP:
-            hdr = h[2:11]
+            hdr = h[2:12]
             _bcast_plan_blobs(worker.runner, hdr)
             r = worker.runner
             plan = StepPlan(*hdr, r.h64.numpy(), r.h32.numpy(), r.hf.numpy())

@@ -15,6 +15,8 @@ the reference values files' ``extraArgs`` (``--dtype float16``,
 from __future__ import annotations
 
 import argparse
+import asyncio
+import dataclasses
 import json
 import logging
 import time
@@ -54,6 +56,11 @@ class CompletionRequest(_Lenient):
     min_tokens: int = 0
     echo: bool = False
     logprobs: Optional[int] = None
+    presence_penalty: Optional[float] = 0.0
+    frequency_penalty: Optional[float] = 0.0
+    repetition_penalty: Optional[float] = 1.0
+    min_p: Optional[float] = 0.0
+    logit_bias: Optional[dict[str, float]] = None
     user: Optional[str] = None
 
 
@@ -79,6 +86,11 @@ class ChatCompletionRequest(_Lenient):
     min_tokens: int = 0
     logprobs: bool = False
     top_logprobs: Optional[int] = None
+    presence_penalty: Optional[float] = 0.0
+    frequency_penalty: Optional[float] = 0.0
+    repetition_penalty: Optional[float] = 1.0
+    min_p: Optional[float] = 0.0
+    logit_bias: Optional[dict[str, float]] = None
     user: Optional[str] = None
 
 
@@ -157,16 +169,30 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
                               max_tokens=max_tokens, min_tokens=req.min_tokens,
                               stop_token_ids=list(req.stop_token_ids or []), stop=stops,
                               ignore_eos=req.ignore_eos, seed=req.seed, n=req.n,
-                              logprobs=logprobs)
+                              logprobs=logprobs,
+                              presence_penalty=req.presence_penalty or 0.0,
+                              frequency_penalty=req.frequency_penalty or 0.0,
+                              repetition_penalty=req.repetition_penalty or 1.0,
+                              min_p=req.min_p or 0.0,
+                              logit_bias={int(k): float(v) for k, v in (req.logit_bias or {}).items()}
+                              or None)
 
     def tok_str(t: int) -> str:
         return tokenizer.decode([t])
 
     async def run(ids: list[int], sp: SamplingParams, rid: str, stream_fn, final_fn, stream: bool):
-        detok = _Detok(tokenizer, sp.stop)
-        gen = engine.generate(ids, sp, rid)
+        """One engine request per choice (n > 1 fans out with seeds seed+i); choices stream
+        interleaved, each chunk tagged with its choice index."""
+        n = sp.n
+        subs = [dataclasses.replace(sp, n=1, seed=None if sp.seed is None else sp.seed + i)
+                for i in range(n)]
+        rids = [rid if n == 1 else f"{rid}-{i}" for i in range(n)]
         if stream:
-            async def sse():
+            q: asyncio.Queue = asyncio.Queue()
+
+            async def pump(i):
+                detok = _Detok(tokenizer, subs[i].stop)
+                gen = engine.generate(ids, subs[i], rids[i])
                 try:
                     async for out in gen:
                         delta = detok.update(out.output_token_ids)
@@ -176,28 +202,63 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
                         elif reason:
                             delta += detok.flush()
                         if delta or reason or out.logprobs:
-                            yield f"data: {json.dumps(stream_fn(delta, reason, out.logprobs))}\n\n"
+                            await q.put((i, delta, reason, out.logprobs))
                         if detok.stopped:
                             await gen.aclose()
                             break
                 except EngineDeadError as e:
-                    yield f"data: {json.dumps({'error': str(e)})}\n\n"
-                yield "data: [DONE]\n\n"
+                    await q.put((i, None, None, e))
+                finally:
+                    await q.put((i, None, "__done__", None))
+
+            async def sse():
+                tasks = [asyncio.create_task(pump(i)) for i in range(n)]
+                done = 0
+                try:
+                    while done < n:
+                        i, delta, reason, lps = await q.get()
+                        if reason == "__done__":
+                            done += 1
+                            continue
+                        if isinstance(lps, BaseException):
+                            yield f"data: {json.dumps({'error': str(lps)})}\n\n"
+                            continue
+                        c = stream_fn(delta, reason, lps)
+                        c["choices"][0]["index"] = i
+                        yield f"data: {json.dumps(c)}\n\n"
+                    yield "data: [DONE]\n\n"
+                finally:
+                    for t in tasks:
+                        t.cancel()
             return StreamingResponse(sse(), media_type="text/event-stream")
-        last = None
-        lps: list = []
-        async for out in gen:
-            last = out
-            if out.logprobs:
-                lps.extend(out.logprobs)
-            detok.update(out.output_token_ids)
-            if detok.stopped:
-                await gen.aclose()
-                break
-        reason = "stop" if detok.stopped else (last.finish_reason if last else None)
-        return JSONResponse(final_fn(detok.text, reason, len(ids),
-                                     len(last.output_token_ids) if last else 0,
-                                     lps if sp.logprobs is not None else None))
+
+        async def one(i):
+            detok = _Detok(tokenizer, subs[i].stop)
+            gen = engine.generate(ids, subs[i], rids[i])
+            last, lps = None, []
+            async for out in gen:
+                last = out
+                if out.logprobs:
+                    lps.extend(out.logprobs)
+                detok.update(out.output_token_ids)
+                if detok.stopped:
+                    await gen.aclose()
+                    break
+            reason = "stop" if detok.stopped else (last.finish_reason if last else None)
+            return detok.text, reason, (len(last.output_token_ids) if last else 0), lps
+        res = await asyncio.gather(*[one(i) for i in range(n)])
+        text, reason, nc, lps = res[0]
+        body = final_fn(text, reason, len(ids), sum(r[2] for r in res),
+                        lps if sp.logprobs is not None else None)
+        if n > 1:
+            choices = []
+            for i, (t_i, r_i, _, l_i) in enumerate(res):
+                one_body = final_fn(t_i, r_i, len(ids), 0, l_i if sp.logprobs is not None else None)
+                c = one_body["choices"][0]
+                c["index"] = i
+                choices.append(c)
+            body["choices"] = choices
+        return JSONResponse(body)
 
     def completion_logprobs(lps, offset0: int = 0):
         """legacy completions shape: tokens / token_logprobs / top_logprobs / text_offset"""
@@ -229,8 +290,8 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
 
     @app.post("/v1/completions")
     async def completions(req: CompletionRequest):
-        if req.n != 1:
-            return _err(400, "only n=1 is supported")
+        if not 1 <= req.n <= 16:
+            return _err(400, "n must be in [1, 16]")
         prompts = req.prompt
         if isinstance(prompts, list) and prompts and isinstance(prompts[0], (str, list)):
             if len(prompts) != 1:
@@ -271,8 +332,8 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
 
     @app.post("/v1/chat/completions")
     async def chat(req: ChatCompletionRequest):
-        if req.n != 1:
-            return _err(400, "only n=1 is supported")
+        if not 1 <= req.n <= 16:
+            return _err(400, "n must be in [1, 16]")
         msgs = []
         for m in req.messages:
             c = m.content

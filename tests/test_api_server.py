@@ -75,7 +75,7 @@ def test_errors(client):
     assert r.status_code == 400
     r = client.post("/v1/completions", json={"prompt": "x", "temperature": -1})
     assert r.status_code == 400
-    r = client.post("/v1/completions", json={"prompt": "x", "n": 2})
+    r = client.post("/v1/completions", json={"prompt": "x", "n": 0})
     assert r.status_code == 400
 
 
@@ -150,3 +150,22 @@ def test_chat_logprobs_stream(client):
     content = [c for l in lines for c in (json.loads(l[6:])["choices"][0].get("logprobs") or {}).get("content", [])]
     assert len(content) == 3
     assert all(len(c["top_logprobs"]) == 2 and c["logprob"] <= 0 for c in content)
+
+
+def test_n_choices_and_penalties(client):
+    r = client.post("/v1/completions", json={"prompt": [5, 6, 7], "max_tokens": 4, "n": 3,
+                                             "seed": 7, "ignore_eos": True,
+                                             "presence_penalty": 0.5, "frequency_penalty": 0.2,
+                                             "logit_bias": {"9": 2.0}, "min_p": 0.01})
+    j = r.json()
+    assert r.status_code == 200, j
+    assert [c["index"] for c in j["choices"]] == [0, 1, 2]
+    assert j["usage"]["completion_tokens"] == 12
+    with client.stream("POST", "/v1/chat/completions", json={
+            "messages": [{"role": "user", "content": "hi"}], "max_tokens": 3, "n": 2,
+            "stream": True, "ignore_eos": True}) as s:
+        lines = [l for l in s.iter_lines() if l and l != "data: [DONE]"]
+    idx = {json.loads(l[6:])["choices"][0]["index"] for l in lines}
+    assert idx == {0, 1}
+    assert client.post("/v1/completions", json={"prompt": "x", "n": 99}).status_code == 400
+    assert client.post("/v1/completions", json={"prompt": "x", "presence_penalty": 5}).status_code == 400

@@ -171,3 +171,24 @@ def test_engine_two_nodes_matches_single_node(tmp_path):
             worker.kill()
     assert rc == 0, worker.stdout.read()[-3000:]
     assert got == ref
+
+
+def test_engine_tp2_logits_processing_matches_tp1(tmp_path):
+    """Penalties / bias run on the driver only; TP ranks adopt its sampled ids
+    (tok_bcast), so TP=2 output == TP=1 output."""
+    from kubernetes_gpu_cluster_amd.engine.llm_engine import LLM
+    from kubernetes_gpu_cluster_amd.engine.sequence import SamplingParams
+    d = str(tmp_path / "m")
+    _write_hf_dir(d, "tiny-llama")
+    prompts = [list(range(3, 20)), [5, 6, 7] * 5]
+    sp = [SamplingParams(temperature=0, max_tokens=10, ignore_eos=True, presence_penalty=1.5,
+                         repetition_penalty=1.2),
+          SamplingParams(temperature=0.9, seed=4, max_tokens=10, ignore_eos=True,
+                         logit_bias={11: 3.0, 12: 3.0})]
+    outs = {}
+    for tp in (1, 2):
+        llm = LLM(d, device="cpu", dtype="float32", tensor_parallel_size=tp, max_model_len=256,
+                  max_num_seqs=4, max_num_batched_tokens=64, num_gpu_blocks_override=64)
+        outs[tp] = [o.output_token_ids for o in llm.generate(prompts, sp)]
+        llm.shutdown()
+    assert outs[2] == outs[1]
