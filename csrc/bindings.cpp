@@ -83,10 +83,18 @@ void silu_mul(Tensor out, Tensor x) {
   kgc::launch_silu_mul(dt_code(x), out.data_ptr(), x.data_ptr(), x.size(0), (int)I, stream());
 }
 
+// KV cache element type: the activation dtype, or fp8 e4m3 (--kv-cache-dtype fp8)
+bool kv_is_fp8(const Tensor& k_cache, const Tensor& v_cache, at::ScalarType act) {
+  TORCH_CHECK(k_cache.scalar_type() == v_cache.scalar_type(), "k/v cache dtype mismatch");
+  if (k_cache.scalar_type() == at::kFloat8_e4m3fn) return true;
+  TORCH_CHECK(k_cache.scalar_type() == act, "kv cache dtype must be the activation dtype or fp8_e4m3fn");
+  return false;
+}
+
 void rope_kv_write(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor q_out, Tensor k_cache,
                    Tensor v_cache, Tensor slot_mapping, std::optional<Tensor> q_norm_w,
                    std::optional<Tensor> k_norm_w, int64_t nq, int64_t nkv, int64_t d,
-                   double eps, bool use_rope) {
+                   double eps, bool use_rope, double k_scale, double v_scale) {
   check_gpu(qkv, "qkv");
   c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
   TORCH_CHECK(d % 16 == 0 && d <= 256, "kgc.rope_kv_write: head_dim");
@@ -102,8 +110,9 @@ void rope_kv_write(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor q_out, T
               v_cache.dim() == 5 && k_cache.size(1) == nkv && k_cache.size(3) == d &&
               v_cache.size(3) == d && v_cache.size(4) == 8 &&
               v_cache.size(2) * 8 == k_cache.size(2), "kv cache layout");
-  TORCH_CHECK(k_cache.scalar_type() == qkv.scalar_type() && q_out.scalar_type() == qkv.scalar_type(),
-              "kgc.rope_kv_write: dtype");
+  const bool kv8 = kv_is_fp8(k_cache, v_cache, qkv.scalar_type());
+  TORCH_CHECK(q_out.scalar_type() == qkv.scalar_type(), "kgc.rope_kv_write: dtype");
+  TORCH_CHECK(k_scale > 0 && v_scale > 0, "kv scales must be > 0");
   const void* qn = nullptr;
   const void* kn = nullptr;
   if (q_norm_w.has_value()) {
@@ -115,7 +124,8 @@ void rope_kv_write(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor q_out, T
                             positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
                             q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                             slot_mapping.data_ptr<int64_t>(), qn, kn, (int)T, (int)nq, (int)nkv,
-                            (int)d, (int)k_cache.size(2), (float)eps, use_rope, stream());
+                            (int)d, (int)k_cache.size(2), (float)eps, use_rope, kv8,
+                            (float)k_scale, (float)v_scale, stream());
 }
 
 void check_kv(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, int64_t nq) {
@@ -128,8 +138,7 @@ void check_kv(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, int
   TORCH_CHECK(d == 64 || d == 128, "head_dim must be 64 or 128");
   TORCH_CHECK(nq % nkv == 0 && nq / nkv <= 16, "GQA group must be <= 16");
   TORCH_CHECK(bs >= 16, "block_size must be >= 16");
-  TORCH_CHECK(q.scalar_type() == k_cache.scalar_type() && q.scalar_type() == v_cache.scalar_type(),
-              "q / cache dtype mismatch");
+  kv_is_fp8(k_cache, v_cache, q.scalar_type());
   TORCH_CHECK(q.scalar_type() != at::kFloat, "attention kernels take bf16/f16");
   check_same_dev(q, k_cache, "k_cache");
   check_same_dev(q, v_cache, "v_cache");
@@ -137,7 +146,7 @@ void check_kv(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, int
 
 void paged_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables,
                   Tensor ctx_lens, Tensor max_logits, Tensor exp_sums, Tensor tmp_out,
-                  int64_t Z, double scale) {
+                  int64_t Z, double scale, double k_scale, double v_scale) {
   check_gpu(q, "q");
   c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   TORCH_CHECK(q.dim() == 3 && q.is_contiguous(), "q [B, nq, d] contiguous");
@@ -161,12 +170,13 @@ void paged_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor b
                            max_logits.data_ptr<float>(), exp_sums.data_ptr<float>(),
                            tmp_out.data_ptr<float>(), (int)B, (int)nq, (int)k_cache.size(1),
                            (int)d, log2_exact(k_cache.size(2), "block_size"), (int)Zmax, (int)Z,
-                           (float)scale, stream());
+                           (float)scale, k_cache.scalar_type() == at::kFloat8_e4m3fn,
+                           (float)k_scale, (float)v_scale, stream());
 }
 
 void prefill_attention(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables,
                        Tensor query_start_loc, Tensor seq_lens, Tensor work_seq,
-                       Tensor work_mblk, double scale) {
+                       Tensor work_mblk, double scale, double k_scale, double v_scale) {
   check_gpu(q, "q");
   c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   TORCH_CHECK(q.dim() == 3 && q.is_contiguous(), "q [T, nq, d] contiguous");
@@ -188,7 +198,9 @@ void prefill_attention(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Ten
                                 seq_lens.data_ptr<int>(), work_seq.data_ptr<int>(),
                                 work_mblk.data_ptr<int>(), (int)work_seq.numel(), (int)nq,
                                 (int)k_cache.size(1), (int)d,
-                                log2_exact(k_cache.size(2), "block_size"), (float)scale, stream());
+                                log2_exact(k_cache.size(2), "block_size"), (float)scale,
+                                k_cache.scalar_type() == at::kFloat8_e4m3fn, (float)k_scale,
+                                (float)v_scale, stream());
 }
 
 void sample(Tensor out, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds) {
@@ -339,13 +351,14 @@ TORCH_LIBRARY(kgc, m) {
   m.def("silu_mul(Tensor(a!) out, Tensor x) -> ()");
   m.def("rope_kv_write(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor(a!) q_out, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor slot_mapping, Tensor? q_norm_w, "
-        "Tensor? k_norm_w, int nq, int nkv, int d, float eps, bool use_rope) -> ()");
+        "Tensor? k_norm_w, int nq, int nkv, int d, float eps, bool use_rope, float k_scale=1.0, "
+        "float v_scale=1.0) -> ()");
   m.def("paged_decode(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
         "Tensor block_tables, Tensor ctx_lens, Tensor(b!) max_logits, Tensor(c!) exp_sums, "
-        "Tensor(d!) tmp_out, int Z, float scale) -> ()");
+        "Tensor(d!) tmp_out, int Z, float scale, float k_scale=1.0, float v_scale=1.0) -> ()");
   m.def("prefill_attention(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
         "Tensor block_tables, Tensor query_start_loc, Tensor seq_lens, Tensor work_seq, "
-        "Tensor work_mblk, float scale) -> ()");
+        "Tensor work_mblk, float scale, float k_scale=1.0, float v_scale=1.0) -> ()");
   m.def("sample(Tensor(a!) out, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, "
         "Tensor seeds) -> ()");
   m.def("decode_partition_size() -> int", &decode_partition_size);

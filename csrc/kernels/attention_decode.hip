@@ -24,6 +24,7 @@
 // Scores are kept in the log2 domain (scale * log2(e) folded in), exp2.
 #include "common.h"
 #include "launch.h"
+#include <type_traits>
 
 namespace kgc {
 
@@ -41,14 +42,23 @@ __device__ __forceinline__ u32x4 ld16(const void* p) {
 // at Z = 4 where fewer, longer-lived waves want occupancy.  Non-temporal K/V loads
 // and an MFMA-tiled K layout (1 KB contiguous per load) were measured too: -7 % and
 // +3 %, neither kept.
-template <typename T, int D, bool PREF>
+// KV8: fp8 e4m3 cache (8-byte fragment loads widened in registers); the K scale is
+// folded into scale_log2 by the launcher, the V scale (v_scale) into the output.
+template <typename T, int D, bool PREF, bool KV8>
 __global__ __launch_bounds__(256, 3) void paged_decode_kernel(
-    T* __restrict__ out, const T* __restrict__ q, const T* __restrict__ kc,
-    const T* __restrict__ vc, const int* __restrict__ block_tables, int bt_stride,
+    T* __restrict__ out, const T* __restrict__ q, const void* __restrict__ kc_,
+    const void* __restrict__ vc_, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ ctx_lens, float* __restrict__ max_logits,
     float* __restrict__ exp_sums, float* __restrict__ tmp_out, int nq, int nkv, int bs_log2,
-    int Zmax, float scale_log2) {
+    int Zmax, float scale_log2, float v_scale) {
   typedef typename Vec8<T>::type V8;
+  typedef std::conditional_t<KV8, uint8_t, T> C;   // cache element
+  const C* __restrict__ kc = reinterpret_cast<const C*>(kc_);
+  const C* __restrict__ vc = reinterpret_cast<const C*>(vc_);
+  auto ldf = [](const C* p) -> u32x4 {
+    if constexpr (KV8) return fp8x8_widen<T>(*reinterpret_cast<const u32x2*>(p));
+    else return *reinterpret_cast<const u32x4*>(p);
+  };
   constexpr int KS = D / 32;      // k-steps of the QK^T product
   constexpr int DT = D / 16;      // 16-row d-tiles of O^T
   __shared__ __attribute__((aligned(16))) float lds_o[4][16][D];
@@ -62,8 +72,8 @@ __global__ __launch_bounds__(256, 3) void paged_decode_kernel(
   const int* bt = block_tables + (int64_t)b * bt_stride;
   const int bsm = (1 << bs_log2) - 1;
   const int64_t head_stride = (int64_t)D << bs_log2;   // elements per (block, kv-head)
-  const T* kbase = kc + h * head_stride;
-  const T* vbase = vc + h * head_stride;
+  const C* kbase = kc + h * head_stride;
+  const C* vbase = vc + h * head_stride;
   const int64_t blk_stride = (int64_t)nkv * head_stride;
 
   V8 qf[KS];
@@ -97,8 +107,8 @@ __global__ __launch_bounds__(256, 3) void paged_decode_kernel(
   const int end = min(ctx, c1 << 5);       // this wave's token range is [c0*32, end)
   for (int ci = c0; ci < c1; ci += DEC_CHUNKS) {
     const int base = ci << 5;
-    const T* kaddr[DEC_CHUNKS][2];
-    const T* vaddr[DEC_CHUNKS];
+    const C* kaddr[DEC_CHUNKS][2];
+    const C* vaddr[DEC_CHUNKS];
 #pragma unroll
     for (int c = 0; c < DEC_CHUNKS; ++c) {
       const int ta = min(base + c * 32 + keyA, end - 1);
@@ -116,15 +126,15 @@ __global__ __launch_bounds__(256, 3) void paged_decode_kernel(
       for (int c = 0; c < DEC_CHUNKS; ++c)
 #pragma unroll
         for (int s2 = 0; s2 < KS; ++s2) {
-          kf[c][0][s2].u = ld16(kaddr[c][0] + 32 * s2);
-          kf[c][1][s2].u = ld16(kaddr[c][1] + 32 * s2);
+          kf[c][0][s2].u = ldf(kaddr[c][0] + 32 * s2);
+          kf[c][1][s2].u = ldf(kaddr[c][1] + 32 * s2);
         }
     }
     if constexpr (PREF) {
 #pragma unroll
       for (int c = 0; c < DEC_CHUNKS; ++c)
 #pragma unroll
-        for (int t = 0; t < DT; ++t) vf[PREF ? c : 0][t].u = ld16(vaddr[c] + 16 * t * 8);
+        for (int t = 0; t < DT; ++t) vf[PREF ? c : 0][t].u = ldf(vaddr[c] + 16 * t * 8);
     }
     f32x4 sa[DEC_CHUNKS], sb[DEC_CHUNKS];
     // ---- S^T = K . Q^T
@@ -134,8 +144,8 @@ __global__ __launch_bounds__(256, 3) void paged_decode_kernel(
 #pragma unroll
       for (int s2 = 0; s2 < KS; ++s2) {
         if constexpr (!PREF) {
-          kf[c][0][s2].u = ld16(kaddr[c][0] + 32 * s2);
-          kf[c][1][s2].u = ld16(kaddr[c][1] + 32 * s2);
+          kf[c][0][s2].u = ldf(kaddr[c][0] + 32 * s2);
+          kf[c][1][s2].u = ldf(kaddr[c][1] + 32 * s2);
         }
         accA = mfma16x16x32(kf[c][0][s2].v, qf[s2], accA);
         accB = mfma16x16x32(kf[c][1][s2].v, qf[s2], accB);
@@ -177,7 +187,7 @@ __global__ __launch_bounds__(256, 3) void paged_decode_kernel(
       for (int t = 0; t < DT; ++t) {
         Pack8<T> v;
         if constexpr (PREF) v = vf[PREF ? c : 0][t];
-        else v.u = ld16(vaddr[c] + 16 * t * 8);
+        else v.u = ldf(vaddr[c] + 16 * t * 8);
         o[t] = mfma16x16x32(v.v, pf.v, o[t]);
       }
     }
@@ -208,10 +218,10 @@ __global__ __launch_bounds__(256, 3) void paged_decode_kernel(
     }
     const int64_t row = (int64_t)b * nq + h * G + hh;
     if (direct) {
-      out[row * D + d] = from_f<T>(L > 0.f ? acc / L : 0.f);
+      out[row * D + d] = from_f<T>(L > 0.f ? acc / L * v_scale : 0.f);
     } else {
       const int64_t prow = row * Zmax + blockIdx.z;
-      tmp_out[prow * D + d] = acc;
+      tmp_out[prow * D + d] = acc * v_scale;
       if (d == 0) {
         max_logits[prow] = M;
         exp_sums[prow] = L;
@@ -250,15 +260,15 @@ __global__ __launch_bounds__(64) void paged_decode_reduce_kernel(
   for (int e = 0; e < EPT; ++e) orow[tid * EPT + e] = from_f<T>(acc[e] * inv);
 }
 
-template <typename T, int D>
+template <typename T, int D, bool KV8>
 static void decode_dispatch(void* out, const void* q, const void* kc, const void* vc,
                             const int* bt, int bt_stride, const int* ctx, float* ml, float* es,
                             float* tmp, int B, int nq, int nkv, int bs_log2, int Zmax, int Z,
-                            float scale_log2, hipStream_t s) {
-  auto kern = Z == 1 ? paged_decode_kernel<T, D, true> : paged_decode_kernel<T, D, false>;
+                            float scale_log2, float v_scale, hipStream_t s) {
+  auto kern = Z == 1 ? paged_decode_kernel<T, D, true, KV8> : paged_decode_kernel<T, D, false, KV8>;
   kern<<<dim3(B, nkv, Z), 256, 0, s>>>(
-      (T*)out, (const T*)q, (const T*)kc, (const T*)vc, bt, bt_stride, ctx, ml, es, tmp, nq,
-      nkv, bs_log2, Zmax, scale_log2);
+      (T*)out, (const T*)q, kc, vc, bt, bt_stride, ctx, ml, es, tmp, nq,
+      nkv, bs_log2, Zmax, scale_log2, v_scale);
   if (Z > 1)
     paged_decode_reduce_kernel<T, D><<<dim3(B, nq), 64, 0, s>>>((T*)out, ml, es, tmp, ctx, nq,
                                                                 Z, Zmax);
@@ -268,18 +278,22 @@ void launch_paged_decode(int dtype, void* out, const void* q, const void* k_cach
                          const void* v_cache, const int* block_tables, int bt_stride,
                          const int* ctx_lens, float* max_logits, float* exp_sums,
                          float* tmp_out, int B, int nq, int nkv, int D, int bs_log2,
-                         int Zmax, int Z, float scale, hipStream_t s) {
+                         int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
+                         float v_scale, hipStream_t s) {
   if (B == 0) return;
-  const float sl2 = scale * 1.4426950408889634f;
-#define KGC_DEC(TT, DD)                                                                   \
-  decode_dispatch<TT, DD>(out, q, k_cache, v_cache, block_tables, bt_stride, ctx_lens,   \
-                          max_logits, exp_sums, tmp_out, B, nq, nkv, bs_log2, Zmax, Z,   \
-                          sl2, s)
+  const float sl2 = scale * k_scale * 1.4426950408889634f;
+#define KGC_DEC(TT, DD, K8)                                                               \
+  decode_dispatch<TT, DD, K8>(out, q, k_cache, v_cache, block_tables, bt_stride, ctx_lens, \
+                              max_logits, exp_sums, tmp_out, B, nq, nkv, bs_log2, Zmax, Z, \
+                              sl2, v_scale, s)
+#define KGC_DEC_D(TT, K8) \
+  if (D == 128) KGC_DEC(TT, 128, K8); else KGC_DEC(TT, 64, K8)
   if (dtype == DT_BF16) {
-    if (D == 128) KGC_DEC(bf16, 128); else KGC_DEC(bf16, 64);
+    if (kv_fp8) { KGC_DEC_D(bf16, true); } else { KGC_DEC_D(bf16, false); }
   } else {
-    if (D == 128) KGC_DEC(f16, 128); else KGC_DEC(f16, 64);
+    if (kv_fp8) { KGC_DEC_D(f16, true); } else { KGC_DEC_D(f16, false); }
   }
+#undef KGC_DEC_D
 #undef KGC_DEC
 }
 

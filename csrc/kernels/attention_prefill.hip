@@ -21,6 +21,7 @@
 //   V^T [D][64 keys]   chunk c of dim d stored at c ^ ((d>>1)&7)
 #include "common.h"
 #include "launch.h"
+#include <type_traits>
 
 namespace kgc {
 
@@ -29,14 +30,25 @@ constexpr int PF_BN = 64;
 
 __device__ __forceinline__ int kswz(int k) { return (k & 3) | (((k >> 3) & 3) << 2); }
 
-template <typename T, int D>
+// KV8: fp8 e4m3 cache; staged as 8-byte loads, widened to T on the way into LDS (the
+// LDS image and everything after it is unchanged).  K scale folded into scale_log2,
+// V scale applied in the epilogue.
+template <typename T, int D, bool KV8>
 __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
-    const T* __restrict__ q, T* __restrict__ out, const T* __restrict__ kc,
-    const T* __restrict__ vc, const int* __restrict__ block_tables, int bt_stride,
+    const T* __restrict__ q, T* __restrict__ out, const void* __restrict__ kc_,
+    const void* __restrict__ vc_, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ qsl, const int* __restrict__ seq_lens,
     const int* __restrict__ work_seq, const int* __restrict__ work_mblk, int nq, int nkv,
-    int bs_log2, float scale_log2) {
+    int bs_log2, float scale_log2, float v_scale) {
   typedef typename Vec8<T>::type V8;
+  typedef std::conditional_t<KV8, uint8_t, T> C;   // cache element
+  typedef std::conditional_t<KV8, u32x2, u32x4> R; // staged raw fragment (8 elements)
+  const C* __restrict__ kc = reinterpret_cast<const C*>(kc_);
+  const C* __restrict__ vc = reinterpret_cast<const C*>(vc_);
+  auto widen = [](R r) -> u32x4 {
+    if constexpr (KV8) return fp8x8_widen<T>(r);
+    else return r;
+  };
   constexpr int NCH = D / 8;                 // 16-byte chunks per K row
   constexpr int KS = D / 32;                 // k-steps of QK^T
   constexpr int DT = D / 16;                 // d-tiles of O^T
@@ -78,25 +90,25 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
   const int last_q = ctx0 + min((mb + 1) * PF_BM, qlen) - 1;
   const int n_tiles = last_q / PF_BN + 1;
 
-  u32x4 kreg[KPT], vreg[VPT];
+  R kreg[KPT], vreg[VPT];
   auto load_tile = [&](int kt) {
 #pragma unroll
     for (int u = 0; u < KPT; ++u) {
       const int ci = threadIdx.x + 256 * u;
       const int key = ci / NCH, c = ci % NCH;
       const int ka = min(kt * PF_BN + key, L - 1);
-      const T* src = kc + (int64_t)bt[ka >> bs_log2] * nkv * hs + h * hs +
+      const C* src = kc + (int64_t)bt[ka >> bs_log2] * nkv * hs + h * hs +
                      (int64_t)(ka & bsm) * D + c * 8;
-      kreg[u] = *reinterpret_cast<const u32x4*>(src);
+      kreg[u] = *reinterpret_cast<const R*>(src);
     }
 #pragma unroll
     for (int u = 0; u < VPT; ++u) {       // 8-key group c of dim d: contiguous in d
       const int ci = threadIdx.x + 256 * u;
       const int c = ci / D, d = ci % D;
       const int ka = min(kt * PF_BN + 8 * c, L - 1) & ~7;
-      const T* src = vc + (int64_t)bt[ka >> bs_log2] * nkv * hs + h * hs +
+      const C* src = vc + (int64_t)bt[ka >> bs_log2] * nkv * hs + h * hs +
                      ((ka & bsm) >> 3) * (D * 8) + d * 8;
-      vreg[u] = *reinterpret_cast<const u32x4*>(src);
+      vreg[u] = *reinterpret_cast<const R*>(src);
     }
   };
   auto store_tile = [&](int buf) {
@@ -106,13 +118,13 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
     for (int u = 0; u < KPT; ++u) {
       const int ci = threadIdx.x + 256 * u;
       const int key = ci / NCH, c = ci % NCH;
-      *reinterpret_cast<u32x4*>(K + key * D + ((c ^ (kswz(key) & (NCH - 1))) * 8)) = kreg[u];
+      *reinterpret_cast<u32x4*>(K + key * D + ((c ^ (kswz(key) & (NCH - 1))) * 8)) = widen(kreg[u]);
     }
 #pragma unroll
     for (int u = 0; u < VPT; ++u) {
       const int ci = threadIdx.x + 256 * u;
       const int c = ci / D, d = ci % D;
-      *reinterpret_cast<u32x4*>(V + d * PF_BN + ((c ^ ((d >> 1) & 7)) * 8)) = vreg[u];
+      *reinterpret_cast<u32x4*>(V + d * PF_BN + ((c ^ ((d >> 1) & 7)) * 8)) = widen(vreg[u]);
     }
   };
 
@@ -209,7 +221,7 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
     float tot = l[qt];
     tot += __shfl_xor(tot, 16, 64);
     tot += __shfl_xor(tot, 32, 64);
-    const float inv = 1.f / tot;
+    const float inv = v_scale / tot;
     const int qi = mb * PF_BM + wave * 32 + qt * 16 + r16;
     if (qi < qlen) {
       T* orow = out + ((int64_t)(q0 + qi) * nq + hq) * D + 4 * qd;
@@ -224,33 +236,37 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
   }
 }
 
-template <typename T, int D>
+template <typename T, int D, bool KV8>
 static void prefill_dispatch(const void* q, void* out, const void* kc, const void* vc,
                              const int* bt, int bt_stride, const int* qsl, const int* sl,
                              const int* ws, const int* wm, int n_work, int nq, int nkv,
-                             int bs_log2, float scale_log2, hipStream_t s) {
+                             int bs_log2, float scale_log2, float v_scale, hipStream_t s) {
   const size_t lds = 2 * 2 * PF_BN * D * sizeof(T);
-  prefill_attn_kernel<T, D><<<dim3(n_work, nq), 256, lds, s>>>(
-      (const T*)q, (T*)out, (const T*)kc, (const T*)vc, bt, bt_stride, qsl, sl, ws, wm, nq,
-      nkv, bs_log2, scale_log2);
+  prefill_attn_kernel<T, D, KV8><<<dim3(n_work, nq), 256, lds, s>>>(
+      (const T*)q, (T*)out, kc, vc, bt, bt_stride, qsl, sl, ws, wm, nq,
+      nkv, bs_log2, scale_log2, v_scale);
 }
 
 void launch_prefill_attention(int dtype, const void* q, void* out, const void* k_cache,
                               const void* v_cache, const int* block_tables, int bt_stride,
                               const int* query_start_loc, const int* seq_lens,
                               const int* work_seq, const int* work_mblk, int n_work, int nq,
-                              int nkv, int D, int bs_log2, float scale, hipStream_t s) {
+                              int nkv, int D, int bs_log2, float scale, bool kv_fp8,
+                              float k_scale, float v_scale, hipStream_t s) {
   if (n_work == 0) return;
-  const float sl2 = scale * 1.4426950408889634f;
-#define KGC_PF(TT, DD)                                                                     \
-  prefill_dispatch<TT, DD>(q, out, k_cache, v_cache, block_tables, bt_stride,              \
-                           query_start_loc, seq_lens, work_seq, work_mblk, n_work, nq, nkv, \
-                           bs_log2, sl2, s)
+  const float sl2 = scale * k_scale * 1.4426950408889634f;
+#define KGC_PF(TT, DD, K8)                                                                 \
+  prefill_dispatch<TT, DD, K8>(q, out, k_cache, v_cache, block_tables, bt_stride,          \
+                               query_start_loc, seq_lens, work_seq, work_mblk, n_work, nq, \
+                               nkv, bs_log2, sl2, v_scale, s)
+#define KGC_PF_D(TT, K8) \
+  if (D == 128) KGC_PF(TT, 128, K8); else KGC_PF(TT, 64, K8)
   if (dtype == DT_BF16) {
-    if (D == 128) KGC_PF(bf16, 128); else KGC_PF(bf16, 64);
+    if (kv_fp8) { KGC_PF_D(bf16, true); } else { KGC_PF_D(bf16, false); }
   } else {
-    if (D == 128) KGC_PF(f16, 128); else KGC_PF(f16, 64);
+    if (kv_fp8) { KGC_PF_D(f16, true); } else { KGC_PF_D(f16, false); }
   }
+#undef KGC_PF_D
 #undef KGC_PF
 }
 

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 namespace kgc {
 
@@ -89,5 +90,53 @@ __device__ __forceinline__ float block_max(float v, float* scratch) {
 }
 
 __device__ __forceinline__ float fast_exp(float x) { return __expf(x); }
+
+// ---- fp8 (OCP e4m3, gfx950) KV cache ---------------------------------------------
+// Values are stored as fp8(x / scale) with the per-tensor scale folded into the
+// attention math by the kernels (K: softmax scale, V: output), so dequantisation is
+// the exact e4m3 -> bf16/f16 widening (every e4m3 value is representable in both).
+constexpr float FP8_MAX = 448.f;
+
+__device__ __forceinline__ uint32_t fp8x4(float a, float b, float c, float d) {
+  a = fminf(fmaxf(a, -FP8_MAX), FP8_MAX);
+  b = fminf(fmaxf(b, -FP8_MAX), FP8_MAX);
+  c = fminf(fmaxf(c, -FP8_MAX), FP8_MAX);
+  d = fminf(fmaxf(d, -FP8_MAX), FP8_MAX);
+  const int lo = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(c, d, lo, true);
+}
+
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+
+// bytes [2*HI, 2*HI+1] of w -> 2 T packed in 32 bits
+template <typename T, bool HI> __device__ __forceinline__ uint32_t fp8x2_widen(uint32_t w) {
+  if constexpr (std::is_same_v<T, bf16>) {
+    union { bf16x2_t v; uint32_t u; } r;
+    r.v = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w, 1.0f, HI);
+    return r.u;
+  } else {
+    union { f16x2_t v; uint32_t u; } r;
+    r.v = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(w, 1.0f, HI);
+    return r.u;
+  }
+}
+
+// 8 fp8 bytes -> 8 T (one MFMA operand fragment)
+template <typename T>
+__device__ __forceinline__ u32x4 fp8x8_widen(u32x2 raw) {
+  return u32x4{fp8x2_widen<T, false>(raw.x), fp8x2_widen<T, true>(raw.x),
+               fp8x2_widen<T, false>(raw.y), fp8x2_widen<T, true>(raw.y)};
+}
+
+// Load one 8-element fragment from a cache row: 16 B of T, or 8 B of fp8 widened.
+template <typename T, bool KV8>
+__device__ __forceinline__ u32x4 ld_frag8(const void* base, int64_t elem) {
+  if constexpr (KV8)
+    return fp8x8_widen<T>(*reinterpret_cast<const u32x2*>(
+        reinterpret_cast<const uint8_t*>(base) + elem));
+  else
+    return *reinterpret_cast<const u32x4*>(reinterpret_cast<const T*>(base) + elem);
+}
 
 }  // namespace kgc

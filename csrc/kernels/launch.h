@@ -17,18 +17,21 @@ void launch_rope_kv_write(int dtype, const void* qkv, int64_t qkv_stride,
                           const int64_t* positions, const float* cos_sin, void* q_out,
                           void* k_cache, void* v_cache, const int64_t* slot_mapping,
                           const void* q_norm_w, const void* k_norm_w, int T, int nq, int nkv,
-                          int d, int bs, float eps, bool use_rope, hipStream_t s);
+                          int d, int bs, float eps, bool use_rope, bool kv_fp8, float k_scale,
+                          float v_scale, hipStream_t s);
 void launch_paged_decode(int dtype, void* out, const void* q, const void* k_cache,
                          const void* v_cache, const int* block_tables, int bt_stride,
                          const int* ctx_lens, float* max_logits, float* exp_sums,
                          float* tmp_out, int B, int nq, int nkv, int D, int bs_log2,
-                         int Zmax, int Z, float scale, hipStream_t s);
+                         int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
+                         float v_scale, hipStream_t s);
 int paged_decode_partition_size();
 void launch_prefill_attention(int dtype, const void* q, void* out, const void* k_cache,
                               const void* v_cache, const int* block_tables, int bt_stride,
                               const int* query_start_loc, const int* seq_lens,
                               const int* work_seq, const int* work_mblk, int n_work, int nq,
-                              int nkv, int D, int bs_log2, float scale, hipStream_t s);
+                              int nkv, int D, int bs_log2, float scale, bool kv_fp8,
+                              float k_scale, float v_scale, hipStream_t s);
 int prefill_block_m();
 void launch_sample(int dtype, int64_t* out, const void* logits, int64_t row_stride, int B,
                    int V, const float* temperature, const int* top_k, const float* top_p,

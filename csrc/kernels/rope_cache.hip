@@ -6,6 +6,8 @@
 //
 // Cache layouts (see ops/reference.py):
 //   k_cache [nb, nkv, bs, d]    v_cache [nb, nkv, bs/8, d, 8]  (V^T in 8-key groups)
+// KV8: the cache holds fp8 e4m3 of (value / scale) (--kv-cache-dtype fp8); the value
+// quantised is the T-rounded one, exactly what a T cache would store.
 #include "common.h"
 #include "launch.h"
 
@@ -13,13 +15,13 @@ namespace kgc {
 
 constexpr int ROPE_NT = 128;
 
-template <typename T, bool NORM, bool ROPE>
+template <typename T, bool NORM, bool ROPE, bool KV8>
 __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
     const T* __restrict__ qkv, int64_t qkv_stride, const int64_t* __restrict__ positions,
-    const float* __restrict__ cos_sin, T* __restrict__ q_out, T* __restrict__ k_cache,
-    T* __restrict__ v_cache, const int64_t* __restrict__ slot_mapping,
+    const float* __restrict__ cos_sin, T* __restrict__ q_out, void* __restrict__ k_cache,
+    void* __restrict__ v_cache, const int64_t* __restrict__ slot_mapping,
     const T* __restrict__ qn_w, const T* __restrict__ kn_w, int nq, int nkv, int d, int bs,
-    float eps) {
+    float eps, float k_inv, float v_inv) {
   // item space of one token: [q/k rotation items, padded to a wave] [v scatter items];
   // gridDim.y workgroups of ROPE_NT items share a token (fills the CUs at decode).
   const int t = blockIdx.x;
@@ -90,9 +92,21 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
       *reinterpret_cast<u32x4*>(dst + half + c * 8) = ob.u;
     } else if (slot >= 0) {
       const int kh = head - nq;
-      T* dst = k_cache + ((blk * nkv + kh) * bs + off) * d;
-      *reinterpret_cast<u32x4*>(dst + c * 8) = oa.u;
-      *reinterpret_cast<u32x4*>(dst + half + c * 8) = ob.u;
+      const int64_t e = ((blk * nkv + kh) * bs + off) * d;
+      if constexpr (KV8) {
+        uint8_t* dst = reinterpret_cast<uint8_t*>(k_cache) + e;
+        float fa[8], fb[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { fa[j] = to_f(oa.h[j]) * k_inv; fb[j] = to_f(ob.h[j]) * k_inv; }
+        *reinterpret_cast<u32x2*>(dst + c * 8) =
+            u32x2{fp8x4(fa[0], fa[1], fa[2], fa[3]), fp8x4(fa[4], fa[5], fa[6], fa[7])};
+        *reinterpret_cast<u32x2*>(dst + half + c * 8) =
+            u32x2{fp8x4(fb[0], fb[1], fb[2], fb[3]), fp8x4(fb[4], fb[5], fb[6], fb[7])};
+      } else {
+        T* dst = reinterpret_cast<T*>(k_cache) + e;
+        *reinterpret_cast<u32x4*>(dst + c * 8) = oa.u;
+        *reinterpret_cast<u32x4*>(dst + half + c * 8) = ob.u;
+      }
     }
     return;
   }
@@ -103,26 +117,39 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
   const int h = iv / (d >> 3), c = iv % (d >> 3);
   Pack8<T> v;
   v.u = *reinterpret_cast<const u32x4*>(row + (nq + nkv) * d + h * d + c * 8);
-  T* dst = v_cache + (blk * nkv + h) * (int64_t)bs * d + ((int64_t)(off >> 3) * d + c * 8) * 8 +
-           (off & 7);
+  const int64_t e = (blk * nkv + h) * (int64_t)bs * d + ((int64_t)(off >> 3) * d + c * 8) * 8 +
+                    (off & 7);
+  if constexpr (KV8) {
+    uint8_t* dst = reinterpret_cast<uint8_t*>(v_cache) + e;
+    const uint32_t w0 = fp8x4(to_f(v.h[0]) * v_inv, to_f(v.h[1]) * v_inv, to_f(v.h[2]) * v_inv,
+                              to_f(v.h[3]) * v_inv);
+    const uint32_t w1 = fp8x4(to_f(v.h[4]) * v_inv, to_f(v.h[5]) * v_inv, to_f(v.h[6]) * v_inv,
+                              to_f(v.h[7]) * v_inv);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) dst[j * 8] = v.h[j];
+    for (int j = 0; j < 4; ++j) {
+      dst[j * 8] = (uint8_t)(w0 >> (8 * j));
+      dst[(j + 4) * 8] = (uint8_t)(w1 >> (8 * j));
+    }
+  } else {
+    T* dst = reinterpret_cast<T*>(v_cache) + e;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dst[j * 8] = v.h[j];
+  }
 }
 
-template <typename T>
+template <typename T, bool KV8>
 static void rope_dispatch(const void* qkv, int64_t qkv_stride, const int64_t* pos,
                           const float* cs, void* q_out, void* kc, void* vc,
                           const int64_t* slots, const void* qn, const void* kn, int T_,
-                          int nq, int nkv, int d, int bs, float eps, bool rope,
-                          hipStream_t s) {
+                          int nq, int nkv, int d, int bs, float eps, bool rope, float k_inv,
+                          float v_inv, hipStream_t s) {
   if (T_ == 0) return;
   const int n_items = (((nq + nkv) * (d >> 4) + 63) & ~63) + nkv * (d >> 3);
   const dim3 grid(T_, (n_items + ROPE_NT - 1) / ROPE_NT);
 #define KGC_ROPE_LAUNCH(N, R)                                                               \
-  rope_kv_kernel<T, N, R><<<grid, ROPE_NT, 0, s>>>((const T*)qkv, qkv_stride, pos, cs,       \
-                                                 (T*)q_out, (T*)kc, (T*)vc, slots,          \
-                                                 (const T*)qn, (const T*)kn, nq, nkv, d,    \
-                                                 bs, eps)
+  rope_kv_kernel<T, N, R, KV8><<<grid, ROPE_NT, 0, s>>>(                                    \
+      (const T*)qkv, qkv_stride, pos, cs, (T*)q_out, kc, vc, slots, (const T*)qn,           \
+      (const T*)kn, nq, nkv, d, bs, eps, k_inv, v_inv)
   const bool norm = qn != nullptr;
   if (norm && rope) KGC_ROPE_LAUNCH(true, true);
   else if (norm) KGC_ROPE_LAUNCH(true, false);
@@ -135,13 +162,18 @@ void launch_rope_kv_write(int dtype, const void* qkv, int64_t qkv_stride,
                           const int64_t* positions, const float* cos_sin, void* q_out,
                           void* k_cache, void* v_cache, const int64_t* slot_mapping,
                           const void* q_norm_w, const void* k_norm_w, int T, int nq, int nkv,
-                          int d, int bs, float eps, bool use_rope, hipStream_t s) {
-  if (dtype == DT_BF16)
-    rope_dispatch<bf16>(qkv, qkv_stride, positions, cos_sin, q_out, k_cache, v_cache,
-                        slot_mapping, q_norm_w, k_norm_w, T, nq, nkv, d, bs, eps, use_rope, s);
-  else
-    rope_dispatch<f16>(qkv, qkv_stride, positions, cos_sin, q_out, k_cache, v_cache,
-                       slot_mapping, q_norm_w, k_norm_w, T, nq, nkv, d, bs, eps, use_rope, s);
+                          int d, int bs, float eps, bool use_rope, bool kv_fp8, float k_scale,
+                          float v_scale, hipStream_t s) {
+#define KGC_ROPE_TYPES(TT, K8)                                                               \
+  rope_dispatch<TT, K8>(qkv, qkv_stride, positions, cos_sin, q_out, k_cache, v_cache,       \
+                        slot_mapping, q_norm_w, k_norm_w, T, nq, nkv, d, bs, eps, use_rope, \
+                        1.f / k_scale, 1.f / v_scale, s)
+  if (dtype == DT_BF16) {
+    if (kv_fp8) KGC_ROPE_TYPES(bf16, true); else KGC_ROPE_TYPES(bf16, false);
+  } else {
+    if (kv_fp8) KGC_ROPE_TYPES(f16, true); else KGC_ROPE_TYPES(f16, false);
+  }
+#undef KGC_ROPE_TYPES
 }
 
 }  // namespace kgc

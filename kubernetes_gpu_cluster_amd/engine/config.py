@@ -20,6 +20,9 @@ _DTYPES = {"auto": None, "bfloat16": torch.bfloat16, "bf16": torch.bfloat16,
            "float32": torch.float32, "float": torch.float32}
 
 
+KV_CACHE_DTYPES = ("auto", "bfloat16", "bf16", "float16", "fp16", "fp8", "fp8_e4m3")
+
+
 @dataclasses.dataclass
 class EngineConfig:
     model: str = "llama-3-8b"
@@ -59,6 +62,12 @@ class EngineConfig:
         if self.dtype.lower() not in _DTYPES:
             raise ValueError(f"unsupported --dtype {self.dtype}")
         return model_default if d is None else d
+
+    def kv_torch_dtype(self, act: torch.dtype) -> torch.dtype:
+        """Cache element type: fp8 e4m3 for --kv-cache-dtype fp8, else the activations'."""
+        if self.kv_cache_dtype in ("fp8", "fp8_e4m3"):
+            return torch.float8_e4m3fn
+        return act
 
     def resolved_device(self) -> torch.device:
         if self.device == "auto":
@@ -107,7 +116,8 @@ def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     a("--enforce-eager", action="store_true")
     a("--disable-custom-all-reduce", action="store_true")
     a("--trust-remote-code", action="store_true")
-    a("--kv-cache-dtype", type=str, default="auto")
+    a("--kv-cache-dtype", type=str, default="auto",
+      help="auto (activation dtype) or fp8 / fp8_e4m3 (half the KV bytes)")
     a("--seed", type=int, default=0)
     a("--random-init", action="store_true", help="random weights (offline benchmarking)")
     a("--load-format", type=str, default="auto", help="'dummy' == --random-init")
@@ -126,8 +136,9 @@ def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
 
 
 def config_from_args(ns: argparse.Namespace) -> EngineConfig:
-    if ns.kv_cache_dtype not in ("auto", "bfloat16", "float16", "fp16", "bf16"):
-        raise ValueError(f"--kv-cache-dtype {ns.kv_cache_dtype} is not supported (auto/bf16/fp16)")
+    if ns.kv_cache_dtype not in KV_CACHE_DTYPES:
+        raise ValueError(f"--kv-cache-dtype {ns.kv_cache_dtype} is not supported "
+                         f"({'/'.join(KV_CACHE_DTYPES)})")
     return EngineConfig(
         model=ns.model, served_model_name=ns.served_model_name, tokenizer=ns.tokenizer,
         dtype=ns.dtype, tensor_parallel_size=ns.tensor_parallel_size,

@@ -95,8 +95,13 @@ class Layout:
 class ModelRunner:
     def __init__(self, model, mcfg: ModelConfig, dtype: torch.dtype, device: torch.device,
                  block_size: int, max_model_len: int, max_num_seqs: int, token_budget: int,
-                 enforce_eager: bool = False, graph_max_bs: int = 256):
+                 enforce_eager: bool = False, graph_max_bs: int = 256,
+                 kv_dtype: Optional[torch.dtype] = None, kv_scales: tuple = (1.0, 1.0)):
         self.model, self.mcfg, self.dtype, self.device = model, mcfg, dtype, device
+        # KV cache element type: the activation dtype, or fp8 e4m3 (--kv-cache-dtype fp8:
+        # half the bytes per cached token, twice the tokens per GB)
+        self.kv_dtype = kv_dtype or dtype
+        self.kv_scales = kv_scales
         self.bs = block_size
         self.max_model_len = max_model_len
         self.max_blocks = math.ceil(max_model_len / block_size)
@@ -138,7 +143,7 @@ class ModelRunner:
     def kv_bytes_per_block(self) -> int:
         m = self.model
         return (2 * m.num_local_layers * m.local_kv_heads() * self.mcfg.head_dim * self.bs *
-                torch.tensor([], dtype=self.dtype).element_size())
+                torch.tensor([], dtype=self.kv_dtype).element_size())
 
     def profile_num_blocks(self, gpu_mem_util: float) -> int:
         """Run a worst-case eager prefill, measure peak activation memory, and size the
@@ -173,7 +178,7 @@ class ModelRunner:
         m = self.model
         L, nkv, d = m.num_local_layers, m.local_kv_heads(), self.mcfg.head_dim
         # zero-init: stale slots of partially filled blocks must hold finite values
-        self.kv = torch.zeros(L, 2, num_blocks, nkv, self.bs, d, dtype=self.dtype,
+        self.kv = torch.zeros(L, 2, num_blocks, nkv, self.bs, d, dtype=self.kv_dtype,
                               device=self.device)
         self.kv_caches = [(self.kv[l, 0], self.kv[l, 1].view(num_blocks, nkv, self.bs // 8, d, 8))
                           for l in range(L)]
@@ -332,7 +337,7 @@ class ModelRunner:
 
     def _forward(self, T, meta: AttnMetadata, hidden_in=None):
         L = self.L
-        ctx = ForwardContext(meta, self.kv_caches, self.cos_sin)
+        ctx = ForwardContext(meta, self.kv_caches, self.cos_sin, *self.kv_scales)
         ids = self.d64[L.ids:L.ids + T]
         pos = self.d64[L.pos:L.pos + T]
         if self.model.first:

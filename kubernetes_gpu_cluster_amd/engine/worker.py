@@ -74,7 +74,8 @@ class Worker:
             comm.set_custom_allreduce(maybe_init_custom_allreduce(self.ps, dev))
         self.runner = ModelRunner(self.model, self.mcfg, self.dtype, dev, cfg.block_size,
                                   self.max_model_len, cfg.max_num_seqs, cfg.token_budget(),
-                                  cfg.enforce_eager, cfg.cuda_graph_max_bs)
+                                  cfg.enforce_eager, cfg.cuda_graph_max_bs,
+                                  kv_dtype=cfg.kv_torch_dtype(self.dtype))
 
     def profile(self) -> int:
         if self.cfg.num_gpu_blocks_override:

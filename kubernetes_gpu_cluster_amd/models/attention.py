@@ -41,6 +41,8 @@ class ForwardContext:
     attn: AttnMetadata
     kv_caches: list                                    # per local layer: (k_cache, v_cache)
     cos_sin: Optional[torch.Tensor] = None
+    k_scale: float = 1.0                               # fp8 KV: cache holds fp8(x / scale)
+    v_scale: float = 1.0
 
 
 class PagedAttention(nn.Module):
@@ -60,14 +62,15 @@ class PagedAttention(nn.Module):
         if tp:
             o = ops.prefill_attention(q[:tp], kc, vc, m.prefill_block_tables, m.query_start_loc,
                                       m.prefill_seq_lens, self.scale, m.work_seq, m.work_mblk,
-                                      out=out[:tp])
+                                      out=out[:tp], k_scale=ctx.k_scale, v_scale=ctx.v_scale)
             if o.data_ptr() != out.data_ptr():
                 out[:tp].copy_(o)
         if m.num_decodes:
             dst = out[tp:tp + m.num_decodes]
             o = ops.paged_attention_decode(q[tp:tp + m.num_decodes], kc, vc,
                                            m.decode_block_tables, m.decode_ctx_lens, self.scale,
-                                           m.decode_workspace, m.decode_grid_z, out=dst)
+                                           m.decode_workspace, m.decode_grid_z, out=dst,
+                                           k_scale=ctx.k_scale, v_scale=ctx.v_scale)
             if o.data_ptr() != dst.data_ptr():
                 dst.copy_(o)
         return out.view(q.shape[0], self.nq * self.d)

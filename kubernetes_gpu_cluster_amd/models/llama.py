@@ -70,7 +70,7 @@ class LlamaAttention(nn.Module):
                               self.nq, self.nkv, self.cfg.head_dim,
                               None if self.q_norm is None else self.q_norm.weight,
                               None if self.k_norm is None else self.k_norm.weight,
-                              self.cfg.rms_eps)
+                              self.cfg.rms_eps, k_scale=ctx.k_scale, v_scale=ctx.v_scale)
         return self.o_proj(self.attn(q, ctx))
 
 

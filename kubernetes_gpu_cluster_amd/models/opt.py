@@ -52,7 +52,7 @@ class OPTLayer(nn.Module):
         kc, vc = ctx.kv_caches[self.attn.layer_idx]
         q = ops.rope_kv_write(qkv, positions, ctx.cos_sin, kc, vc, ctx.attn.slot_mapping,
                               self.qkv_proj.nq, self.qkv_proj.nkv, self.cfg.head_dim,
-                              use_rope=False)
+                              use_rope=False, k_scale=ctx.k_scale, v_scale=ctx.v_scale)
         x = x + self.out_proj(self.attn(q, ctx))
         h = self.final_layer_norm(x)
         return x + self.fc2(F.relu(self.fc1(h)))

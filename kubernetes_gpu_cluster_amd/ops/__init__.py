@@ -103,15 +103,19 @@ def rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Ten
                   num_heads: int, num_kv_heads: int, head_dim: int,
                   q_norm_w: Optional[torch.Tensor] = None,
                   k_norm_w: Optional[torch.Tensor] = None, eps: float = 1e-6,
-                  use_rope: bool = True) -> torch.Tensor:
+                  use_rope: bool = True, k_scale: float = 1.0,
+                  v_scale: float = 1.0) -> torch.Tensor:
+    """k_cache / v_cache may be fp8 (torch.float8_e4m3fn): values are stored as
+    fp8(x / scale)."""
     if not _gpu(qkv):
         return ref.rope_qk_kv_write(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping,
                                     num_heads, num_kv_heads, head_dim, q_norm_w, k_norm_w, eps,
-                                    use_rope)
+                                    use_rope, k_scale, v_scale)
     T = qkv.shape[0]
     q = torch.empty(T, num_heads, head_dim, dtype=qkv.dtype, device=qkv.device)
     _k().rope_kv_write(qkv, positions, cos_sin, q, k_cache, v_cache, slot_mapping, q_norm_w,
-                       k_norm_w, num_heads, num_kv_heads, head_dim, eps, use_rope)
+                       k_norm_w, num_heads, num_kv_heads, head_dim, eps, use_rope, k_scale,
+                       v_scale)
     return q
 
 
@@ -148,9 +152,11 @@ def decode_grid_z(batch: int, num_kv_heads: int, max_ctx: int, target_waves: int
 def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                            block_tables: torch.Tensor, context_lens: torch.Tensor, scale: float,
                            workspace=None, grid_z: int = 1,
-                           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                           out: Optional[torch.Tensor] = None, k_scale: float = 1.0,
+                           v_scale: float = 1.0) -> torch.Tensor:
     if not _gpu(q):
-        return ref.paged_attention_decode(q, k_cache, v_cache, block_tables, context_lens, scale)
+        return ref.paged_attention_decode(q, k_cache, v_cache, block_tables, context_lens, scale,
+                                          k_scale, v_scale)
     B, nq, d = q.shape
     if out is None:
         out = torch.empty_like(q)
@@ -159,7 +165,7 @@ def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torc
     ml, es, tmp = workspace
     grid_z = min(grid_z, ml.shape[-1])
     _k().paged_decode(out, q, k_cache, v_cache, block_tables, context_lens, ml, es, tmp,
-                      grid_z, scale)
+                      grid_z, scale, k_scale, v_scale)
     return out
 
 
@@ -179,10 +185,11 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
                       block_tables: torch.Tensor, query_start_loc: torch.Tensor,
                       seq_lens: torch.Tensor, scale: float, work_seq: torch.Tensor = None,
                       work_mblk: torch.Tensor = None,
-                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                      out: Optional[torch.Tensor] = None, k_scale: float = 1.0,
+                      v_scale: float = 1.0) -> torch.Tensor:
     if not _gpu(q):
         return ref.prefill_attention(q, k_cache, v_cache, block_tables, query_start_loc,
-                                     seq_lens, scale)
+                                     seq_lens, scale, k_scale, v_scale)
     if work_seq is None:
         qsl = query_start_loc.tolist()
         ws, wm = prefill_work_list([qsl[i + 1] - qsl[i] for i in range(len(qsl) - 1)],
@@ -192,7 +199,7 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
     if out is None:
         out = torch.empty_like(q)
     _k().prefill_attention(out, q, k_cache, v_cache, block_tables, query_start_loc, seq_lens,
-                           work_seq, work_mblk, scale)
+                           work_seq, work_mblk, scale, k_scale, v_scale)
     return out
 
 

@@ -86,7 +86,8 @@ def rope_qk_kv_write(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.
                      num_heads: int, num_kv_heads: int, head_dim: int,
                      q_norm_w: Optional[torch.Tensor] = None,
                      k_norm_w: Optional[torch.Tensor] = None, eps: float = 1e-6,
-                     use_rope: bool = True) -> torch.Tensor:
+                     use_rope: bool = True, k_scale: float = 1.0,
+                     v_scale: float = 1.0) -> torch.Tensor:
     """K3+K5(+K6): split fused qkv [T, (nq+2nkv)*d], optional per-head q/k RMSNorm,
     RoPE on q,k, scatter k,v into the paged cache at slot_mapping (-1 = skip).
     Returns rotated q as a contiguous [T, nq, d] tensor."""
@@ -101,12 +102,24 @@ def rope_qk_kv_write(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.
     if use_rope:
         q = apply_rope(q, positions, cos_sin)
         k = apply_rope(k, positions, cos_sin)
-    kv_cache_write(k, v, k_cache, v_cache, slot_mapping)
+    kv_cache_write(k, v, k_cache, v_cache, slot_mapping, k_scale, v_scale)
     return q.contiguous()
 
 
+FP8_MAX = 448.0
+
+
+def to_cache(x: torch.Tensor, cache_dtype: torch.dtype, scale: float = 1.0) -> torch.Tensor:
+    """Value -> cache element: the cache dtype itself, or fp8 e4m3 of (x / scale) with
+    saturation (the kernels clamp to +-448 before the hardware conversion)."""
+    if cache_dtype == torch.float8_e4m3fn:
+        return (x.float() / scale).clamp(-FP8_MAX, FP8_MAX).to(cache_dtype)
+    return x.to(cache_dtype)
+
+
 def kv_cache_write(k: torch.Tensor, v: torch.Tensor, k_cache: torch.Tensor,
-                   v_cache: torch.Tensor, slot_mapping: torch.Tensor) -> None:
+                   v_cache: torch.Tensor, slot_mapping: torch.Tensor,
+                   k_scale: float = 1.0, v_scale: float = 1.0) -> None:
     bs = k_cache.shape[2]
     sm = slot_mapping.long()
     valid = sm >= 0
@@ -114,12 +127,13 @@ def kv_cache_write(k: torch.Tensor, v: torch.Tensor, k_cache: torch.Tensor,
         return
     sm = sm[valid]
     blk, off = sm // bs, sm % bs
-    k_cache[blk, :, off, :] = k[valid].to(k_cache.dtype)
-    v_cache[blk, :, off // 8, :, off % 8] = v[valid].to(v_cache.dtype)
+    # an fp8 cache stores the activation-dtype-rounded value, quantised
+    k_cache[blk, :, off, :] = to_cache(k[valid].to(k.dtype), k_cache.dtype, k_scale)
+    v_cache[blk, :, off // 8, :, off % 8] = to_cache(v[valid].to(v.dtype), v_cache.dtype, v_scale)
 
 
 # ---------------------------------------------------------------- attention
-def _gather_kv(k_cache, v_cache, block_table, ctx_len):
+def _gather_kv(k_cache, v_cache, block_table, ctx_len, k_scale=1.0, v_scale=1.0):
     bs = k_cache.shape[2]
     nb = (ctx_len + bs - 1) // bs
     blocks = block_table[:nb].long()
@@ -127,12 +141,12 @@ def _gather_kv(k_cache, v_cache, block_table, ctx_len):
     k = k.permute(0, 2, 1, 3).reshape(nb * bs, k.shape[1], k.shape[3])[:ctx_len]
     v = v_cache[blocks]                                   # [nb, nkv, bs/8, d, 8]
     v = v.permute(0, 2, 4, 1, 3).reshape(nb * bs, v.shape[1], v.shape[3])[:ctx_len]
-    return k.float(), v.float()                           # [ctx, nkv, d]
+    return k.float() * k_scale, v.float() * v_scale      # [ctx, nkv, d]
 
 
 def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                            block_tables: torch.Tensor, context_lens: torch.Tensor,
-                           scale: float) -> torch.Tensor:
+                           scale: float, k_scale: float = 1.0, v_scale: float = 1.0) -> torch.Tensor:
     """K1: q [B, nq, d] -> out [B, nq, d], one query token per sequence."""
     B, nq, d = q.shape
     nkv = k_cache.shape[1]
@@ -140,7 +154,7 @@ def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torc
     out = torch.empty_like(q)
     for b in range(B):
         L = int(context_lens[b])
-        k, v = _gather_kv(k_cache, v_cache, block_tables[b], L)
+        k, v = _gather_kv(k_cache, v_cache, block_tables[b], L, k_scale, v_scale)
         qb = q[b].float().view(nkv, g, d)
         s = torch.einsum("hgd,lhd->hgl", qb, k) * scale
         p = torch.softmax(s, dim=-1)
@@ -151,7 +165,8 @@ def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torc
 
 def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
                       block_tables: torch.Tensor, query_start_loc: torch.Tensor,
-                      seq_lens: torch.Tensor, scale: float) -> torch.Tensor:
+                      seq_lens: torch.Tensor, scale: float, k_scale: float = 1.0,
+                      v_scale: float = 1.0) -> torch.Tensor:
     """K2: varlen causal attention for packed prompt chunks.  Sequence i owns query
     rows [qsl[i], qsl[i+1]); its keys are cache positions [0, seq_lens[i]) and its
     queries sit at absolute positions seq_lens[i]-qlen .. seq_lens[i]-1."""
@@ -164,7 +179,7 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
         ql, L = b - a, int(seq_lens[i])
         if ql == 0:
             continue
-        k, v = _gather_kv(k_cache, v_cache, block_tables[i], L)
+        k, v = _gather_kv(k_cache, v_cache, block_tables[i], L, k_scale, v_scale)
         qi = q[a:b].float().view(ql, nkv, g, d)
         s = torch.einsum("qhgd,lhd->hgql", qi, k) * scale
         qpos = torch.arange(L - ql, L)[:, None]

@@ -180,3 +180,24 @@ def test_torch_profiler_hook(tmp_path, monkeypatch):
     llm.shutdown()
     files = os.listdir(tmp_path)
     assert files == ["engine_steps_1_4.json"]
+
+
+def test_engine_fp8_kv_cache_cpu():
+    """--kv-cache-dtype fp8: the cache holds float8_e4m3fn, twice the blocks fit in the
+    same bytes, and greedy output stays close to the bf16/fp32-cache engine (e4m3 keeps
+    3 mantissa bits, so a late near-tie may flip)."""
+    import torch
+    prompts = [[5 + i, 6, 7, 8, 9, 10, 11] * 3 for i in range(3)]
+    sp = SamplingParams(temperature=0, max_tokens=12, ignore_eos=True)
+    ref = _llm(num_gpu_blocks_override=64, block_size=16)
+    a = [o.output_token_ids for o in ref.generate(prompts, sp)]
+    bpb = ref.engine.executor.runner.kv_bytes_per_block()
+    ref.shutdown()
+    f8 = _llm(num_gpu_blocks_override=64, block_size=16, kv_cache_dtype="fp8")
+    r = f8.engine.executor.runner
+    assert r.kv.dtype == torch.float8_e4m3fn and r.kv_bytes_per_block() * 4 == bpb  # fp32 -> fp8
+    b = [o.output_token_ids for o in f8.generate(prompts, sp)]
+    f8.shutdown()
+    assert all(x[0] == y[0] for x, y in zip(a, b))
+    same = sum(p == q for x, y in zip(a, b) for p, q in zip(x, y))
+    assert same >= 0.6 * sum(len(x) for x in a)

@@ -155,3 +155,21 @@ def test_logprobs_through_decode_graphs(gpu):
             assert lp <= 1e-6 and len(top) == 3
             assert top[0][0] == tok or abs(top[0][1] - lp) < 1e-3
     llm.shutdown()
+
+
+def test_fp8_kv_engine_graphs(gpu):
+    """--kv-cache-dtype fp8 through the whole engine (graph decode + chunked prefill)."""
+    from kubernetes_gpu_cluster_amd.engine.llm_engine import LLM
+    prompts = [[5 + i, 6, 7, 8, 9] * 9 for i in range(3)]
+    sp = SamplingParams(temperature=0, max_tokens=12, ignore_eos=True)
+    outs = []
+    for kvd in ("auto", "fp8"):
+        llm = LLM("tiny-llama", device="cuda", dtype="bfloat16", random_init=True, seed=2,
+                  max_model_len=256, max_num_seqs=4, max_num_batched_tokens=64,
+                  kv_cache_dtype=kvd)
+        if kvd == "fp8":
+            assert llm.engine.executor.runner.kv.dtype == torch.float8_e4m3fn
+        outs.append([o.output_token_ids for o in llm.generate(prompts, sp)])
+        assert llm.engine.executor.runner.stats["graph_steps"] > 0
+        llm.shutdown()
+    assert all(a[0] == b[0] for a, b in zip(*outs))

@@ -248,3 +248,75 @@ def test_fused_moe_graph_capture(gpu):
         g.replay()
         exp = ref.moe_mlp_local(x.cpu(), w13.cpu(), w2.cpu(), tw.cpu(), tid.cpu())
         torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(torch.bfloat16))
+
+
+# ------------------------------------------------------------------ fp8 KV cache
+FP8 = torch.float8_e4m3fn
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("scales", [(1.0, 1.0), (0.5, 2.0)])
+def test_rope_kv_write_fp8(gpu, dt, scales):
+    """Quantised cache bytes == torch's RNE fp8 conversion of the T-rounded values."""
+    torch.manual_seed(12)
+    T, nq, nkv, bs, nb, d = 40, 8, 2, 16, 12, 128
+    qkv = (torch.randn(T, (nq + 2 * nkv) * d) * 4).to(dt).to(gpu)
+    pos = torch.randint(0, 500, (T,), device=gpu)
+    slots = torch.randperm(nb * bs, device=gpu)[:T]
+    cs = ref.rope_cos_sin_cache(d, 1024, 5e5).to(gpu)
+    kc = torch.zeros(nb, nkv, bs, d, dtype=FP8, device=gpu)
+    vc = torch.zeros(nb, nkv, bs // 8, d, 8, dtype=FP8, device=gpu)
+    kc2, vc2 = kc.cpu().clone(), vc.cpu().clone()
+    ks, vs = scales
+    q = ops.rope_kv_write(qkv, pos, cs, kc, vc, slots, nq, nkv, d, k_scale=ks, v_scale=vs)
+    qr = ref.rope_qk_kv_write(qkv.cpu(), pos.cpu(), cs.cpu(), kc2, vc2, slots.cpu(), nq, nkv, d,
+                              k_scale=ks, v_scale=vs)
+    torch.testing.assert_close(q.cpu().float(), qr.float(), **_tol(dt))
+    # V is a pure copy -> bit-exact; K passes through RoPE in fp32 first, so allow a
+    # one-step (one fp8 ulp) disagreement on rounding ties of slightly different fp32
+    assert torch.equal(vc.cpu().view(torch.uint8), vc2.view(torch.uint8))
+    kd = (kc.cpu().view(torch.uint8).int() - kc2.view(torch.uint8).int()).abs()
+    assert (kd > 1).sum() == 0 and (kd == 1).float().mean() < 0.01
+
+
+def _fp8_cache(kc, vc, ks, vs):
+    return (ref.to_cache(kc, FP8, ks), ref.to_cache(vc, FP8, vs))
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("d,nq,nkv", [(128, 32, 8), (64, 12, 12)])
+def test_paged_decode_fp8(gpu, dt, d, nq, nkv):
+    torch.manual_seed(13)
+    ctx = [1, 33, 300, 1000, 2049]
+    B, bs = len(ctx), 32
+    kc, vc, bt = _fill_random_cache(B, ctx, nkv, bs, d, dt, gpu)
+    ks, vs = 0.5, 2.0
+    kc8, vc8 = _fp8_cache(kc, vc, ks, vs)
+    q = torch.randn(B, nq, d, dtype=dt, device=gpu)
+    cl = torch.tensor(ctx, dtype=torch.int32, device=gpu)
+    for z in (1, 3):
+        out = ops.paged_attention_decode(q, kc8, vc8, bt, cl, d ** -0.5, grid_z=z, k_scale=ks,
+                                         v_scale=vs)
+        exp = ref.paged_attention_decode(q.cpu(), kc8.cpu(), vc8.cpu(), bt.cpu(), cl.cpu(),
+                                         d ** -0.5, ks, vs)
+        torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(dt))
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_prefill_attention_fp8(gpu, dt):
+    torch.manual_seed(14)
+    d, nq, nkv, bs = 128, 32, 8, 16
+    seq_lens, query_lens = [5, 300, 700], [5, 100, 257]
+    kc, vc, bt = _fill_random_cache(len(seq_lens), seq_lens, nkv, bs, d, dt, gpu)
+    ks, vs = 1.0, 0.25
+    kc8, vc8 = _fp8_cache(kc, vc, ks, vs)
+    qsl = [0]
+    for ql in query_lens:
+        qsl.append(qsl[-1] + ql)
+    q = torch.randn(qsl[-1], nq, d, dtype=dt, device=gpu)
+    qsl_t = torch.tensor(qsl, dtype=torch.int32, device=gpu)
+    sl_t = torch.tensor(seq_lens, dtype=torch.int32, device=gpu)
+    out = ops.prefill_attention(q, kc8, vc8, bt, qsl_t, sl_t, d ** -0.5, k_scale=ks, v_scale=vs)
+    exp = ref.prefill_attention(q.cpu(), kc8.cpu(), vc8.cpu(), bt.cpu(), qsl_t.cpu(), sl_t.cpu(),
+                                d ** -0.5, ks, vs)
+    torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(dt))
