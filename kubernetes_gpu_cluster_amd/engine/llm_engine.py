@@ -71,6 +71,15 @@ class LLMEngine:
         self.executor = executor
         t0 = time.time()
         nb = executor.profile()
+        # like vLLM: refuse to start when not even one max-length sequence fits
+        # (otherwise requests would wait forever for blocks that never free up)
+        cap = (nb - 1) * cfg.block_size
+        if cap < self.max_model_len:
+            executor.shutdown()
+            raise ValueError(
+                f"KV cache holds {max(cap, 0)} tokens ({nb} blocks of {cfg.block_size}), less than "
+                f"max_model_len={self.max_model_len}: raise --gpu-memory-utilization, lower "
+                f"--max-model-len, use --kv-cache-dtype fp8, or add tensor parallelism")
         executor.init_cache(nb)
         self.graph_s = executor.capture()
         self.num_blocks = nb

@@ -174,6 +174,20 @@ class ModelRunner:
         nb = int(budget // self.kv_bytes_per_block())
         return max(nb, 2)
 
+    def release(self) -> None:
+        """Drop the KV arena, decode graphs and workspaces (engine shutdown): a process
+        that builds a second engine must get the memory back."""
+        self.graphs = {}
+        self.graph_pool = None
+        self.kv = None
+        self.kv_caches = []
+        self.workspace = None
+        if self.is_gpu:
+            import gc
+            gc.collect()
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+
     def init_kv_cache(self, num_blocks: int) -> None:
         m = self.model
         L, nkv, d = m.num_local_layers, m.local_kv_heads(), self.mcfg.head_dim

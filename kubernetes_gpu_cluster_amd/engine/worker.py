@@ -91,6 +91,9 @@ class Worker:
     def run(self, plan: StepPlan):
         return self.runner.run(plan)
 
+    def release(self) -> None:
+        self.runner.release()
+
 
 # ---------------------------------------------------------------------- plan transport
 def _bcast_cmd(cmd: int, arg: int = 0, header: Optional[list[int]] = None) -> list[int]:
@@ -133,6 +136,7 @@ def worker_loop(worker: Worker) -> None:
         cmd, arg = h[0], h[1]
         if cmd == CMD_EXIT:
             _release_custom_allreduce()
+            worker.release()
             break
         if cmd == CMD_PROFILE:
             nb = worker.profile()
@@ -181,7 +185,7 @@ class LocalExecutor:
         return True
 
     def shutdown(self) -> None:
-        pass
+        self.worker.runner.release()
 
 
 class TokenFuture:
@@ -327,4 +331,5 @@ class MultiprocExecutor(_DistExecutorBase):
             p.join(timeout=30)
             if p.is_alive():
                 p.terminate()
+        self.worker.runner.release()
         destroy_parallel()

@@ -135,10 +135,10 @@ def test_engine_preemption_matches_ample_kv(monkeypatch):
     monkeypatch.setenv("KGC_DEBUG", "1")
     prompts = [[5 + i, 6, 7, 8, 9, 10, 11] * 3 for i in range(4)]
     sp = SamplingParams(temperature=0, max_tokens=20, ignore_eos=True)
-    ample = _llm(num_gpu_blocks_override=64, block_size=16)
+    ample = _llm(num_gpu_blocks_override=64, block_size=16, max_model_len=64)
     ref = [o.output_token_ids for o in ample.generate(prompts, sp)]
     ample.shutdown()
-    tight = _llm(num_gpu_blocks_override=6, block_size=16)
+    tight = _llm(num_gpu_blocks_override=6, block_size=16, max_model_len=64)
     got = [o.output_token_ids for o in tight.generate(prompts, sp)]
     npre = tight.engine.scheduler.num_preemptions
     tight.shutdown()
@@ -201,3 +201,8 @@ def test_engine_fp8_kv_cache_cpu():
     assert all(x[0] == y[0] for x, y in zip(a, b))
     same = sum(p == q for x, y in zip(a, b) for p, q in zip(x, y))
     assert same >= 0.6 * sum(len(x) for x in a)
+
+
+def test_engine_refuses_kv_smaller_than_one_sequence():
+    with pytest.raises(ValueError, match="max_model_len"):
+        _llm(num_gpu_blocks_override=4, block_size=16, max_model_len=128)
