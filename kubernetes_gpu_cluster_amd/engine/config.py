@@ -37,6 +37,7 @@ class EngineConfig:
     max_num_seqs: int = 256
     max_num_batched_tokens: Optional[int] = None
     enable_chunked_prefill: bool = True
+    enable_prefix_caching: bool = True    # vLLM V1 default: reuse cached KV of shared prefixes
     enforce_eager: bool = False
     disable_custom_all_reduce: bool = False
     trust_remote_code: bool = False
@@ -113,6 +114,8 @@ def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     a("--enable-chunked-prefill", dest="enable_chunked_prefill", action="store_true",
       default=True)
     a("--no-enable-chunked-prefill", dest="enable_chunked_prefill", action="store_false")
+    a("--enable-prefix-caching", dest="enable_prefix_caching", action="store_true", default=True)
+    a("--no-enable-prefix-caching", dest="enable_prefix_caching", action="store_false")
     a("--enforce-eager", action="store_true")
     a("--disable-custom-all-reduce", action="store_true")
     a("--trust-remote-code", action="store_true")
@@ -146,6 +149,7 @@ def config_from_args(ns: argparse.Namespace) -> EngineConfig:
         gpu_memory_utilization=ns.gpu_memory_utilization, block_size=ns.block_size,
         max_num_seqs=ns.max_num_seqs, max_num_batched_tokens=ns.max_num_batched_tokens,
         enable_chunked_prefill=ns.enable_chunked_prefill, enforce_eager=ns.enforce_eager,
+        enable_prefix_caching=ns.enable_prefix_caching,
         disable_custom_all_reduce=ns.disable_custom_all_reduce,
         trust_remote_code=ns.trust_remote_code, kv_cache_dtype=ns.kv_cache_dtype, seed=ns.seed,
         random_init=ns.random_init or ns.load_format == "dummy",

@@ -84,7 +84,8 @@ class LLMEngine:
         self.graph_s = executor.capture()
         self.num_blocks = nb
         runner = executor.runner
-        self.bm = BlockManager(nb, cfg.block_size, cfg.max_num_seqs, runner.max_blocks)
+        self.bm = BlockManager(nb, cfg.block_size, cfg.max_num_seqs, runner.max_blocks,
+                               enable_prefix_caching=cfg.enable_prefix_caching)
         self.scheduler = Scheduler(self.bm, cfg.max_num_seqs, cfg.token_budget(),
                                    self.max_model_len, cfg.enable_chunked_prefill)
         self.seqs: dict[str, Sequence] = {}
@@ -154,6 +155,10 @@ class LLMEngine:
             for seq in samplers:
                 seq.output_token_ids.append(_PENDING)
                 seq.num_pending += 1
+            if self.bm.prefix_caching:      # publish blocks whose token ids are all known
+                for seq, _ in batch.prefills:
+                    self.bm.register_full_blocks(seq, seq.num_tokens - seq.num_pending)
+            for seq in samplers:
                 if len(seq.output_token_ids) >= seq.max_tokens or seq.num_tokens >= self.max_model_len:
                     # finished by length: release now (stream order protects the KV
                     # blocks still being written by the in-flight step)
@@ -178,6 +183,8 @@ class LLMEngine:
             idx = len(seq.output_token_ids) - seq.num_pending
             seq.num_pending -= 1
             seq.output_token_ids[idx] = tok
+            if self.bm.prefix_caching and seq.slot >= 0:
+                self.bm.register_full_blocks(seq, seq.num_tokens - seq.num_pending)
             if seq.first_token_time is None:
                 seq.first_token_time = now
             seq.last_token_time = now
@@ -203,6 +210,8 @@ class LLMEngine:
             outs.append(o)
         self.metrics.on_step(plan, now - t0, len(samplers), self.bm.usage(),
                              len(self.scheduler.running), len(self.scheduler.waiting), npre)
+        if self.bm.prefix_caching:
+            self.metrics.on_prefix_cache(self.bm.query_tokens, self.bm.hit_tokens)
         return outs
 
     def _step_sync(self) -> list[RequestOutput]:
@@ -219,8 +228,13 @@ class LLMEngine:
         for seq in batch.decodes:
             seq.num_computed += 1
         outs: list[RequestOutput] = []
+        if self.bm.prefix_caching:
+            for seq, _ in batch.prefills:
+                self.bm.register_full_blocks(seq, seq.num_tokens)
         for row, (seq, tok) in enumerate(zip(samplers, tokens)):
             seq.output_token_ids.append(tok)
+            if self.bm.prefix_caching:
+                self.bm.register_full_blocks(seq, seq.num_tokens)
             if seq.first_token_time is None:
                 seq.first_token_time = now
             seq.last_token_time = now

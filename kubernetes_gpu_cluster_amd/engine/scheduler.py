@@ -11,7 +11,9 @@ Each step has a token budget (``max_num_batched_tokens``) and a sequence cap
    the sequence cap and free blocks (with a small watermark) allow.
 
 A scheduled unit is (sequence, n_tokens): tokens [num_computed, num_computed+n)
-are run; if that reaches the end of the sequence, a new token is sampled.
+are run; if that reaches the end of the sequence, a new token is sampled.  With
+prefix caching, an admitted sequence first takes the cached blocks of its longest
+cached prefix and starts computing after them.
 """
 from __future__ import annotations
 
@@ -106,15 +108,23 @@ class Scheduler:
             budget -= n
             i += 1
         if not preempted:
+            bs = self.bm.block_size
             while self.waiting and budget > 0 and len(self.running) < self.max_num_seqs:
                 seq = self.waiting[0]
-                remaining = seq.num_tokens - seq.num_computed
+                # prefix caching: leading full blocks already in the cache are not recomputed
+                hits = self.bm.cached_prefix_blocks(seq) if self.bm.prefix_caching else []
+                start = seq.num_computed + len(hits) * bs
+                remaining = seq.num_tokens - start
                 n = min(remaining, budget)
                 if n < remaining and not self.chunked:
                     break
-                if not self.bm.can_allocate(seq, seq.num_computed + n, watermark=True):
+                if not self.bm.can_admit(seq, start + n, hits):
                     break
                 self.waiting.popleft()
+                if self.bm.prefix_caching:
+                    self.bm.note_query(seq)
+                    if hits:
+                        seq.num_computed += self.bm.take_prefix(seq, hits)
                 self.bm.allocate(seq, seq.num_computed + n)
                 seq.status = SeqStatus.RUNNING
                 self.running.append(seq)

@@ -38,6 +38,13 @@ class EngineMetrics:
                                 registry=r)
         self.step_time = Histogram("kgc:engine_step_seconds", "engine step wall time", lab,
                                    buckets=_LAT, registry=r)
+        self.prefix_queries = Counter("vllm:prefix_cache_queries", "prompt tokens looked up in "
+                                      "the prefix cache", lab, registry=r)
+        self.prefix_hits = Counter("vllm:prefix_cache_hits", "prompt tokens served from the "
+                                   "prefix cache", lab, registry=r)
+        self.prefix_rate = Gauge("vllm:gpu_prefix_cache_hit_rate", "prefix cache hit rate",
+                                 lab, registry=r)
+        self._pq = self._ph = 0
         self.model = model_name
         self.total_gen = 0
         self.total_prompt = 0
@@ -68,6 +75,15 @@ class EngineMetrics:
             self._trace.append({"name": f"step T={plan.T} P={plan.P} D={plan.D} B={plan.B}",
                                 "ph": "X", "ts": now - dt * 1e6, "dur": dt * 1e6, "pid": 0,
                                 "tid": 0})
+
+    def on_prefix_cache(self, queries: int, hits: int) -> None:
+        """Cumulative token counts from the block manager."""
+        m = self.model
+        if queries > self._pq:
+            self.prefix_queries.labels(m).inc(queries - self._pq)
+            self.prefix_hits.labels(m).inc(hits - self._ph)
+            self._pq, self._ph = queries, hits
+            self.prefix_rate.labels(m).set(hits / queries)
 
     def on_finish(self, seq) -> None:
         m = self.model

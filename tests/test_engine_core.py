@@ -206,3 +206,70 @@ def test_engine_fp8_kv_cache_cpu():
 def test_engine_refuses_kv_smaller_than_one_sequence():
     with pytest.raises(ValueError, match="max_model_len"):
         _llm(num_gpu_blocks_override=4, block_size=16, max_model_len=128)
+
+
+# ---------------------------------------------------------------------------- prefix caching
+def test_prefix_cache_block_manager():
+    bm = BlockManager(16, 4, 4, 8, enable_prefix_caching=True)
+    a = _seq("a", 10)                       # blocks: [0..3] [4..7] [8..9]
+    bm.allocate(a, 10)
+    a.num_computed = 10
+    bm.register_full_blocks(a, a.num_tokens)
+    assert a.num_registered == 2
+    b = Sequence("b", list(range(3, 13)) + [99], SamplingParams())   # same first 10 tokens
+    hits = bm.cached_prefix_blocks(b)
+    assert hits == a.block_ids[:2]
+    assert bm.can_admit(b, 11, hits)
+    assert bm.take_prefix(b, hits) == 8
+    bm.allocate(b, 11)
+    bm.check_invariants([a, b])
+    assert bm.ref[hits[0]] == 2
+    bm.free_seq(a)
+    assert bm.ref[hits[0]] == 1 and not bm.evictable   # b still holds the shared blocks
+    bm.check_invariants([b])
+    bm.free_seq(b)
+    assert len(bm.evictable) == 2                      # cached contents kept for reuse
+    bm.check_invariants([])
+    # allocation drains never-cached blocks first, then evicts LRU cached blocks
+    c = _seq("c", 4 * 8)
+    bm.allocate(c, 4 * 8)
+    d = _seq("d", 4 * 7)
+    assert bm.can_allocate(d, 28)
+    bm.allocate(d, 28)
+    assert not bm.evictable and not bm.block_of     # both cached blocks evicted
+    bm.check_invariants([c, d])
+
+
+def test_engine_prefix_cache_hits_and_parity(monkeypatch):
+    """Shared-prefix prompts: the second wave reuses cached blocks (fewer computed
+    tokens) and produces exactly the tokens of an engine without prefix caching."""
+    monkeypatch.setenv("KGC_DEBUG", "1")
+    shared = list(range(7, 7 + 40))
+    prompts = [shared + [100 + i, 101 + i, 102] for i in range(3)]
+    sp = SamplingParams(temperature=0, max_tokens=10, ignore_eos=True)
+    off = _llm(num_gpu_blocks_override=64, block_size=16, enable_prefix_caching=False)
+    ref = [o.output_token_ids for o in off.generate(prompts, sp)]
+    off.shutdown()
+    on = _llm(num_gpu_blocks_override=64, block_size=16, enable_prefix_caching=True)
+    first = [o.output_token_ids for o in on.generate(prompts[:1], sp)]
+    rest = [o.output_token_ids for o in on.generate(prompts, sp)]
+    bm = on.engine.bm
+    assert bm.hit_tokens >= 3 * 32        # every prompt of wave 2 reused 2 full blocks
+    on.shutdown()
+    assert first[0] == ref[0]
+    assert rest == ref
+
+
+def test_engine_prefix_cache_with_preemption(monkeypatch):
+    monkeypatch.setenv("KGC_DEBUG", "1")
+    prompts = [[5 + i, 6, 7, 8, 9, 10, 11] * 3 for i in range(4)]
+    sp = SamplingParams(temperature=0, max_tokens=20, ignore_eos=True)
+    a = _llm(num_gpu_blocks_override=64, block_size=16, max_model_len=64,
+             enable_prefix_caching=False)
+    ref = [o.output_token_ids for o in a.generate(prompts, sp)]
+    a.shutdown()
+    b = _llm(num_gpu_blocks_override=6, block_size=16, max_model_len=64, enable_prefix_caching=True)
+    got = [o.output_token_ids for o in b.generate(prompts, sp)]
+    assert b.engine.scheduler.num_preemptions > 0
+    b.shutdown()
+    assert got == ref
