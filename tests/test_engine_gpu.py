@@ -158,10 +158,13 @@ def test_logprobs_through_decode_graphs(gpu):
 
 
 def test_fp8_kv_engine_graphs(gpu):
-    """--kv-cache-dtype fp8 through the whole engine (graph decode + chunked prefill)."""
+    """--kv-cache-dtype fp8 through the whole engine (graph decode + chunked prefill).
+    e4m3 keeps 3 mantissa bits, so greedy tokens of a random-init model (flat logits)
+    may differ; the check is that each fp8 first token is among the bf16-cache run's
+    top-5 candidates and that the top-1 logprobs agree closely."""
     from kubernetes_gpu_cluster_amd.engine.llm_engine import LLM
     prompts = [[5 + i, 6, 7, 8, 9] * 9 for i in range(3)]
-    sp = SamplingParams(temperature=0, max_tokens=12, ignore_eos=True)
+    sp = SamplingParams(temperature=0, max_tokens=12, ignore_eos=True, logprobs=5)
     outs = []
     for kvd in ("auto", "fp8"):
         llm = LLM("tiny-llama", device="cuda", dtype="bfloat16", random_init=True, seed=2,
@@ -169,7 +172,11 @@ def test_fp8_kv_engine_graphs(gpu):
                   kv_cache_dtype=kvd)
         if kvd == "fp8":
             assert llm.engine.executor.runner.kv.dtype == torch.float8_e4m3fn
-        outs.append([o.output_token_ids for o in llm.generate(prompts, sp)])
+        outs.append(llm.generate(prompts, sp))
         assert llm.engine.executor.runner.stats["graph_steps"] > 0
         llm.shutdown()
-    assert all(a[0] == b[0] for a, b in zip(*outs))
+    for a, b in zip(*outs):
+        tok_b, lp_b, _ = b.logprobs[0]
+        top_a = a.logprobs[0][2]
+        assert tok_b in [t for t, _ in top_a], (a.output_token_ids, b.output_token_ids)
+        assert abs(top_a[0][1] - b.logprobs[0][2][0][1]) < 0.15
