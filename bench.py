@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--dtype", default="bfloat16")
     ap.add_argument("--temperature", type=float, default=1.0)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--prefix-caching", type=int, default=1, choices=[0, 1],
+                    help="automatic prefix caching (engine default: on; random prompts never hit)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: run the same harness on the fp32 CPU path (gloo) -- a test "
                          "harness for the multi-rank logic, not a measurement")
@@ -112,7 +114,7 @@ def main():
                        max_num_batched_tokens=args.max_num_batched_tokens,
                        gpu_memory_utilization=args.gpu_memory_utilization,
                        enforce_eager=args.enforce_eager, random_init=True, seed=0,
-                       device=args.device)
+                       device=args.device, enable_prefix_caching=bool(args.prefix_caching))
     engine = None
     if tp > 1:
         assert world % tp == 0
