@@ -1,6 +1,6 @@
 """Microbenchmark the projection GEMM shapes of the decode / prefill steps.
 
-    python tools/gemm_bench.py [--model llama-3-8b] [--ms 1,16,64,128,256,512] [--tunableop]
+    python tools/gemm_bench.py [--model llama-3-8b] [--ms 1,16,64,128,256,512] [--table CSV]
 
 Reports per shape: time, weight-streaming TB/s and TFLOP/s for F.linear
 (hipBLASLt) -- the baseline the hand-written decode GEMM must beat.
@@ -45,10 +45,15 @@ def main():
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--ms", default="1,16,64,128,256,512,4096")
     ap.add_argument("--backend", default="hipblaslt")
-    ap.add_argument("--custom", action="store_true", help="also time kgc.decode_gemm")
+    ap.add_argument("--table", default=None, help="TunableOp results CSV to apply (read-only)")
     a = ap.parse_args()
     if a.backend != "hipblaslt":
         torch.backends.cuda.preferred_blas_library(a.backend)
+    if a.table:
+        torch.cuda.tunable.enable(True)
+        torch.cuda.tunable.tuning_enable(False)
+        torch.cuda.tunable.set_filename(a.table, insert_device_ordinal=False)
+        assert torch.cuda.tunable.read_file(a.table), a.table
     dev = torch.device("cuda")
     res = []
     for name, (N, K) in shapes(a.model).items():
@@ -56,15 +61,10 @@ def main():
         for M in [int(x) for x in a.ms.split(",")]:
             x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
             t = bench(lambda: F.linear(x, w))
-            row = {"shape": name, "M": M, "N": N, "K": K, "backend": a.backend,
+            row = {"shape": name, "M": M, "N": N, "K": K,
+                   "backend": "tunableop-table" if a.table else a.backend,
                    "us": round(t * 1e6, 2), "w_TBps": round(N * K * 2 / t / 1e12, 2),
                    "TFLOPs": round(2 * M * N * K / t / 1e12, 1)}
-            if a.custom:
-                from kubernetes_gpu_cluster_amd import ops
-                if ops.decode_gemm_supported(M, N, K):
-                    tc = bench(lambda: ops.decode_gemm(x, w))
-                    row["custom_us"] = round(tc * 1e6, 2)
-                    row["custom_TBps"] = round(N * K * 2 / tc / 1e12, 2)
             print(json.dumps(row), flush=True)
             res.append(row)
 
