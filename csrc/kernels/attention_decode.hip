@@ -35,17 +35,20 @@ __device__ __forceinline__ u32x4 ld16(const void* p) {
   return *reinterpret_cast<const u32x4*>(p);
 }
 
-// PREF: false = load each K/V fragment right before its MFMA (116 VGPR, 4 waves/SIMD);
-// true = issue all 32 K and V loads of the partition before the first MFMA (132 VGPR,
-// 3 waves/SIMD).  Measured (tools/attn_bench.py, B=256 Llama-3-8B shapes): PREF is
-// 5-9 % faster when the grid is one workgroup per (seq, kv head) (Z == 1), ~6 % slower
-// at Z = 4 where fewer, longer-lived waves want occupancy.  Non-temporal K/V loads
+// PREF: true = issue all K and V loads of a wave-iteration before its first MFMA;
+// false = load each fragment right before its MFMA.  NCH = 32-token chunks per
+// wave-iteration, OCC = waves per SIMD.  Shipped: PREF, NCH = 1, OCC = 4 (<= 128 VGPR).
+// Measured (tools/attn_bench.py, profiles/attn_decode_microbench.jsonl) against the
+// previous PREF/NCH=2/OCC=3 (134 VGPR): +4 % at B=256 ctx 640 (5.36 vs 5.14 TB/s),
+// +9 % at B=32 ctx 2600 (Z=4), +4 % at B=64 (Z=2); the per-fragment-load form at
+// OCC 4 is 3-8 % slower than both.  At B=256 the grid is 2048 workgroups: OCC 4 runs
+// them in 2 full rounds of 1024 instead of 2.67 rounds of 768.  Non-temporal K/V loads
 // and an MFMA-tiled K layout (1 KB contiguous per load) were measured too: -7 % and
 // +3 %, neither kept.
 // KV8: fp8 e4m3 cache (8-byte fragment loads widened in registers); the K scale is
 // folded into scale_log2 by the launcher, the V scale (v_scale) into the output.
-template <typename T, int D, bool PREF, bool KV8>
-__global__ __launch_bounds__(256, 3) void paged_decode_kernel(
+template <typename T, int D, bool PREF, bool KV8, int OCC = 3, int NCH = DEC_CHUNKS>
+__global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
     T* __restrict__ out, const T* __restrict__ q, const void* __restrict__ kc_,
     const void* __restrict__ vc_, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ ctx_lens, float* __restrict__ max_logits,
@@ -105,12 +108,12 @@ __global__ __launch_bounds__(256, 3) void paged_decode_kernel(
   const int c0 = (int)(((int64_t)nchunk * wk) / nwk);
   const int c1 = (int)(((int64_t)nchunk * (wk + 1)) / nwk);
   const int end = min(ctx, c1 << 5);       // this wave's token range is [c0*32, end)
-  for (int ci = c0; ci < c1; ci += DEC_CHUNKS) {
+  for (int ci = c0; ci < c1; ci += NCH) {
     const int base = ci << 5;
-    const C* kaddr[DEC_CHUNKS][2];
-    const C* vaddr[DEC_CHUNKS];
+    const C* kaddr[NCH][2];
+    const C* vaddr[NCH];
 #pragma unroll
-    for (int c = 0; c < DEC_CHUNKS; ++c) {
+    for (int c = 0; c < NCH; ++c) {
       const int ta = min(base + c * 32 + keyA, end - 1);
       const int tb = min(base + c * 32 + keyA + 4, end - 1);
       kaddr[c][0] = kbase + bt[ta >> bs_log2] * blk_stride + (int64_t)(ta & bsm) * D + 8 * qd;
@@ -119,11 +122,11 @@ __global__ __launch_bounds__(256, 3) void paged_decode_kernel(
       const int t0 = min(base + c * 32 + 8 * qd, end - 1) & ~7;
       vaddr[c] = vbase + bt[t0 >> bs_log2] * blk_stride + ((t0 & bsm) >> 3) * (D * 8) + r16 * 8;
     }
-    Pack8<T> kf[DEC_CHUNKS][2][KS];
-    Pack8<T> vf[PREF ? DEC_CHUNKS : 1][DT];
+    Pack8<T> kf[NCH][2][KS];
+    Pack8<T> vf[PREF ? NCH : 1][DT];
     if constexpr (PREF) {
 #pragma unroll
-      for (int c = 0; c < DEC_CHUNKS; ++c)
+      for (int c = 0; c < NCH; ++c)
 #pragma unroll
         for (int s2 = 0; s2 < KS; ++s2) {
           kf[c][0][s2].u = ldf(kaddr[c][0] + 32 * s2);
@@ -132,14 +135,14 @@ __global__ __launch_bounds__(256, 3) void paged_decode_kernel(
     }
     if constexpr (PREF) {
 #pragma unroll
-      for (int c = 0; c < DEC_CHUNKS; ++c)
+      for (int c = 0; c < NCH; ++c)
 #pragma unroll
         for (int t = 0; t < DT; ++t) vf[PREF ? c : 0][t].u = ldf(vaddr[c] + 16 * t * 8);
     }
-    f32x4 sa[DEC_CHUNKS], sb[DEC_CHUNKS];
+    f32x4 sa[NCH], sb[NCH];
     // ---- S^T = K . Q^T
 #pragma unroll
-    for (int c = 0; c < DEC_CHUNKS; ++c) {
+    for (int c = 0; c < NCH; ++c) {
       f32x4 accA = {0.f, 0.f, 0.f, 0.f}, accB = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s2 = 0; s2 < KS; ++s2) {
@@ -156,7 +159,7 @@ __global__ __launch_bounds__(256, 3) void paged_decode_kernel(
     // ---- mask + partition max (log2 domain) + online rescale of the carry
     float m = m_run;
 #pragma unroll
-    for (int c = 0; c < DEC_CHUNKS; ++c) {
+    for (int c = 0; c < NCH; ++c) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int tok = base + c * 32 + 8 * qd + i;
@@ -174,7 +177,7 @@ __global__ __launch_bounds__(256, 3) void paged_decode_kernel(
     for (int t = 0; t < DT; ++t) o[t] *= alpha;
     // ---- P = exp2(S - m), O^T += V^T . P^T
 #pragma unroll
-    for (int c = 0; c < DEC_CHUNKS; ++c) {
+    for (int c = 0; c < NCH; ++c) {
       Pack8<T> pf;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -265,7 +268,7 @@ static void decode_dispatch(void* out, const void* q, const void* kc, const void
                             const int* bt, int bt_stride, const int* ctx, float* ml, float* es,
                             float* tmp, int B, int nq, int nkv, int bs_log2, int Zmax, int Z,
                             float scale_log2, float v_scale, hipStream_t s) {
-  auto kern = Z == 1 ? paged_decode_kernel<T, D, true, KV8> : paged_decode_kernel<T, D, false, KV8>;
+  auto kern = paged_decode_kernel<T, D, true, KV8, 4, 1>;
   kern<<<dim3(B, nkv, Z), 256, 0, s>>>(
       (T*)out, (const T*)q, kc, vc, bt, bt_stride, ctx, ml, es, tmp, nq,
       nkv, bs_log2, Zmax, scale_log2, v_scale);

@@ -41,6 +41,9 @@ def main():
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--bs", type=int, default=32)
     ap.add_argument("--max-len", type=int, default=4096)
+    ap.add_argument("--ragged", type=float, default=0.25,
+                    help="context lengths uniform in [ctx*(1-r), ctx] (0: all equal, as in bench.py)")
+    ap.add_argument("--z", type=int, default=0, help="force the z-split (0: engine heuristic)")
     a = ap.parse_args()
     from kubernetes_gpu_cluster_amd import ops
     dev = torch.device("cuda")
@@ -54,10 +57,10 @@ def main():
     bt = torch.zeros(B, maxb, dtype=torch.int32, device=dev)
     bt[:, :nblk] = perm.view(B, nblk).int()
     # ragged contexts around --ctx (uniform +-25%)
-    ctx = (a.ctx * (0.75 + 0.25 * torch.rand(B, device=dev))).int().clamp(1, nblk * bs)
+    ctx = (a.ctx * (1 - a.ragged + a.ragged * torch.rand(B, device=dev))).int().clamp(1, nblk * bs)
     q = torch.randn(B, a.nq, d, device=dev, dtype=torch.bfloat16)
     ws = ops.decode_partials(B, a.nq, d, maxb, bs, dev)
-    z = ops.decode_grid_z(B, a.nkv, a.max_len)
+    z = a.z or ops.decode_grid_z(B, a.nkv, a.max_len)
     out = ops.paged_attention_decode(q, kc, vc, bt, ctx, d ** -0.5, ws, z)
     from kubernetes_gpu_cluster_amd.ops import reference as R
     n = min(B, 8)
@@ -66,7 +69,8 @@ def main():
     t = timeit(lambda: ops.paged_attention_decode(q, kc, vc, bt, ctx, d ** -0.5, ws, z))
     kv_bytes = int(ctx.sum()) * a.nkv * d * 2 * 2
     print(json.dumps({"kernel": "paged_decode", "batch": B, "ctx_mean": float(ctx.float().mean()),
-                      "z": z, "max_err": round(err, 4), "us": round(t * 1e6, 2), "kv_TBps": round(kv_bytes / t / 1e12, 3)}))
+                      "z": z, "max_err": round(err, 4), "us": round(t * 1e6, 2), "kv_TBps": round(kv_bytes / t / 1e12, 3),
+                      "variant": os.environ.get("KGC_DEC_VARIANT", "0")}))
 
 
 if __name__ == "__main__":
