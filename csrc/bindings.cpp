@@ -340,6 +340,42 @@ void xgmi_allreduce(Tensor inout, std::vector<int64_t> data, std::vector<int64_t
                         cap_bytes / 16, two_shot, stream());
 }
 
+void skinny_gemm(Tensor C, Tensor X, Tensor W, std::optional<Tensor> bias, int64_t mt,
+                 int64_t nt, int64_t nw, bool ntl) {
+  check_gpu(X, "X");
+  check_same_dev(X, W, "W");
+  check_same_dev(X, C, "C");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(X.device());
+  TORCH_CHECK(X.dim() == 2 && W.dim() == 2 && C.dim() == 2, "kgc.skinny_gemm: 2-D operands");
+  TORCH_CHECK(X.scalar_type() == W.scalar_type() && C.scalar_type() == X.scalar_type() &&
+              (X.scalar_type() == at::kBFloat16 || X.scalar_type() == at::kHalf),
+              "kgc.skinny_gemm: bf16/f16 operands of one dtype");
+  TORCH_CHECK(mt == 1 || mt == 2 || mt == 4, "kgc.skinny_gemm: mt in {1,2,4}");
+  TORCH_CHECK(nt == 1 || nt == 2, "kgc.skinny_gemm: nt in {1,2}");
+  TORCH_CHECK(nw == 4 || nw == 8 || nw == 16, "kgc.skinny_gemm: nw in {4,8,16}");
+  const int64_t M = X.size(0), K = X.size(1), N = W.size(0);
+  TORCH_CHECK(M >= 1 && M <= 16 * mt, "kgc.skinny_gemm: M must be in [1, 16*mt]");
+  TORCH_CHECK(W.size(1) == K && W.is_contiguous(), "kgc.skinny_gemm: W [N, K] contiguous");
+  TORCH_CHECK(N % (16 * nt) == 0, "kgc.skinny_gemm: N % (16*nt) != 0");
+  TORCH_CHECK(K % (32 * nw) == 0, "kgc.skinny_gemm: K % (32*nw) != 0");
+  TORCH_CHECK(X.stride(1) == 1 && X.stride(0) % 8 == 0 && X.stride(0) >= K,
+              "kgc.skinny_gemm: X rows dense, 16B aligned");
+  TORCH_CHECK(C.size(0) == M && C.size(1) == N && C.stride(1) == 1, "kgc.skinny_gemm: C [M, N]");
+  TORCH_CHECK(N <= INT32_MAX && K <= INT32_MAX, "kgc.skinny_gemm: dims overflow");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(X.data_ptr()) % 16 == 0 &&
+              reinterpret_cast<uintptr_t>(W.data_ptr()) % 16 == 0, "kgc.skinny_gemm: alignment");
+  const void* bp = nullptr;
+  if (bias.has_value()) {
+    TORCH_CHECK(bias->is_contiguous() && bias->numel() == N &&
+                bias->scalar_type() == X.scalar_type(), "kgc.skinny_gemm: bias [N]");
+    check_same_dev(X, *bias, "bias");
+    bp = bias->data_ptr();
+  }
+  kgc::launch_skinny_gemm(dt_code(X), (int)mt, (int)nt, (int)nw, ntl, C.data_ptr(), X.data_ptr(),
+                          W.data_ptr(), bp, (int)M, (int)N, (int)K, X.stride(0), C.stride(0),
+                          stream());
+}
+
 int64_t decode_partition_size() { return kgc::paged_decode_partition_size(); }
 int64_t prefill_block_m() { return kgc::prefill_block_m(); }
 
@@ -378,6 +414,8 @@ TORCH_LIBRARY(kgc, m) {
   m.def("xgmi_allreduce(Tensor(a!) inout, int[] data, int[] sig, int rank, int cap_bytes, "
         "bool two_shot) -> ()");
   m.def("prefill_block_m() -> int", &prefill_block_m);
+  m.def("skinny_gemm(Tensor(a!) C, Tensor X, Tensor W, Tensor? bias, int mt, int nt, int nw, "
+        "bool ntl) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(kgc, CUDA, m) {
@@ -393,4 +431,5 @@ TORCH_LIBRARY_IMPL(kgc, CUDA, m) {
   m.impl("moe_align", &moe_align);
   m.impl("moe_gemm", &moe_gemm);
   m.impl("moe_combine", &moe_combine);
+  m.impl("skinny_gemm", &skinny_gemm);
 }

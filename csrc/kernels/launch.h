@@ -37,6 +37,11 @@ void launch_sample(int dtype, int64_t* out, const void* logits, int64_t row_stri
                    int V, const float* temperature, const int* top_k, const float* top_p,
                    const int64_t* seeds, hipStream_t s);
 
+// K9 skinny (small-M decode) GEMM: C[M, N] = X[M, K] . W[N, K]^T (+ bias), M <= 16*mt.
+void launch_skinny_gemm(int dtype, int mt, int nt, int nw, bool ntl, void* C, const void* X,
+                        const void* W, const void* bias, int M, int N, int K, int64_t ldx,
+                        int64_t ldc, hipStream_t s);
+
 // K13/K14 MoE: routing, expert bucketing, grouped MFMA GEMM, weighted combine.
 int moe_block_n();
 int moe_block_k();

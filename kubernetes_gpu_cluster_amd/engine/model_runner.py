@@ -451,6 +451,12 @@ class ModelRunner:
         """Capture decode forward + LM head for each batch bucket (largest first,
         sharing one memory pool).  Returns seconds spent."""
         self.buckets = graph_buckets(self.graph_max_bs)
+        if self.is_gpu:
+            # K9: per decode bucket and weight shape, hipBLASLt or the skinny GEMM --
+            # whichever measured faster on this model's weights (ops/gemm.py)
+            from ..ops import gemm
+            gemm.tune_skinny([p for p in self.model.parameters() if p.dim() == 2],
+                             self.buckets)
         if (not self.use_graphs or not (self.model.first and self.model.last)
                 or not getattr(self.model, "graph_safe", True)):
             self.use_graphs = False

@@ -1,8 +1,8 @@
 """Tensor-parallel layers (Megatron column/row sharding) over the TP group.
 
-GEMMs are ``torch.nn.functional.linear`` (hipBLASLt on ROCm) on weights stored
-[out, in] so the reduction dim is contiguous for both the library GEMM and the
-decode path.  Sharding:
+GEMMs are ``ops.gemm.linear``: hipBLASLt, or the K9 skinny GEMM for the small-batch
+decode shapes where the engine-start tuner measured it faster, on weights stored
+[out, in] so the reduction dim is contiguous for both.  Sharding:
 
 * ColumnParallelLinear     weight rows split; no communication.
 * MergedColumnParallelLinear  fused gate_up: each logical output split separately
@@ -25,6 +25,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.gemm import linear
 from . import comm
 from .state import get_state
 
@@ -53,7 +54,7 @@ class ReplicatedLinear(nn.Module):
         self.bias = _param((out_f,), dtype, device, _default_loader) if bias else None
 
     def forward(self, x):
-        return F.linear(x, self.weight, self.bias)
+        return linear(x, self.weight, self.bias)
 
 
 class ColumnParallelLinear(nn.Module):
@@ -72,7 +73,7 @@ class ColumnParallelLinear(nn.Module):
         param.data.copy_(w.narrow(0, r * self.out_per, self.out_per))
 
     def forward(self, x):
-        y = F.linear(x, self.weight, self.bias)
+        y = linear(x, self.weight, self.bias)
         return comm.tp_all_gather(y, -1) if self.gather_output else y
 
 
@@ -94,7 +95,7 @@ class MergedColumnParallelLinear(nn.Module):
         param.data.narrow(0, self.offsets[shard_id], n).copy_(w.narrow(0, r * n, n))
 
     def forward(self, x):
-        return F.linear(x, self.weight, self.bias)
+        return linear(x, self.weight, self.bias)
 
 
 class QKVParallelLinear(nn.Module):
@@ -130,7 +131,7 @@ class QKVParallelLinear(nn.Module):
                 w.narrow(0, self.kv_start * d, self.kv_size))
 
     def forward(self, x):
-        return F.linear(x, self.weight, self.bias)
+        return linear(x, self.weight, self.bias)
 
 
 class RowParallelLinear(nn.Module):
@@ -149,7 +150,7 @@ class RowParallelLinear(nn.Module):
         param.data.copy_(w.narrow(1, r * self.in_per, self.in_per))
 
     def forward(self, x):
-        y = F.linear(x, self.weight)
+        y = linear(x, self.weight)
         if self.reduce_results:
             y = comm.tp_all_reduce(y)
         if self.bias is not None:
@@ -218,7 +219,7 @@ class ParallelLMHead(nn.Module):
         return self.emb.weight if self.emb is not None else self.weight
 
     def forward(self, h: torch.Tensor) -> torch.Tensor:
-        logits = F.linear(h, self.get_weight())
+        logits = linear(h, self.get_weight())
         tp, _ = _tp()
         if tp > 1:
             logits = comm.tp_all_gather(logits, -1)

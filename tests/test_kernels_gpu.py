@@ -320,3 +320,52 @@ def test_prefill_attention_fp8(gpu, dt):
     exp = ref.prefill_attention(q.cpu(), kc8.cpu(), vc8.cpu(), bt.cpu(), qsl_t.cpu(), sl_t.cpu(),
                                 d ** -0.5, ks, vs)
     torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(dt))
+
+
+# ------------------------------------------------------------------ K9 skinny GEMM
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("M,N,K", [(1, 6144, 4096), (7, 4096, 14336), (16, 512, 1024),
+                                   (24, 1024, 2048), (33, 2048, 512), (64, 256, 4096)])
+def test_skinny_gemm(gpu, dt, M, N, K):
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, dtype=dt, device=gpu)
+    w = torch.randn(N, K, dtype=dt, device=gpu) * K ** -0.5
+    b = torch.randn(N, dtype=dt, device=gpu)
+    exp = x.float().cpu() @ w.float().cpu().t()
+    mt = 1 if M <= 16 else (2 if M <= 32 else 4)
+    for nt in (1, 2):
+        for nw in (4, 8, 16):
+            for ntl in (True, False):
+                cfg = (mt, nt, nw, ntl)
+                if not gemm.skinny_ok(M, N, K, cfg):
+                    continue
+                got = gemm.skinny_gemm(x, w, None, cfg)
+                torch.testing.assert_close(got.float().cpu(), exp, atol=3e-2, rtol=2e-2)
+                gotb = gemm.skinny_gemm(x, w, b, cfg)
+                torch.testing.assert_close(gotb.float().cpu(), exp + b.float().cpu(), atol=3e-2,
+                                           rtol=2e-2)
+
+
+def test_skinny_gemm_strided_x(gpu):
+    """X may be a row-strided view (e.g. a slice of a wider activation)."""
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    torch.manual_seed(3)
+    big = torch.randn(8, 3072, dtype=torch.bfloat16, device=gpu)
+    x = big[:, :1024]
+    w = torch.randn(512, 1024, dtype=torch.bfloat16, device=gpu) * 0.03
+    got = gemm.skinny_gemm(x, w, None, (1, 1, 4, True))
+    exp = x.float().cpu() @ w.float().cpu().t()
+    torch.testing.assert_close(got.float().cpu(), exp, atol=3e-2, rtol=2e-2)
+
+
+def test_linear_uses_tuned_plan(gpu):
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    torch.manual_seed(4)
+    ws = [torch.randn(1024, 2048, dtype=torch.bfloat16, device=gpu) * 0.02 for _ in range(4)]
+    res = gemm.tune_skinny(ws, [1, 8, 64])
+    assert set(res) == {(1, 1024, 2048), (8, 1024, 2048), (64, 1024, 2048)}
+    x = torch.randn(8, 2048, dtype=torch.bfloat16, device=gpu)
+    torch.testing.assert_close(gemm.linear(x, ws[0]).float(), (x @ ws[0].t()).float(),
+                               atol=3e-2, rtol=2e-2)
+    gemm.clear_plan()
