@@ -54,10 +54,17 @@ def parse():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--prefix-caching", type=int, default=1, choices=[0, 1],
                     help="automatic prefix caching (engine default: on; random prompts never hit)")
+    ap.add_argument("--log-level", default="WARNING",
+                    help="python logging level on stderr (INFO shows the GEMM tuner's choices)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: run the same harness on the fp32 CPU path (gloo) -- a test "
                          "harness for the multi-rank logic, not a measurement")
     return ap.parse_args()
+
+
+def _k9_plan() -> dict:
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    return gemm.plan()
 
 
 def run_wave(engine, args, wave: int, rank: int):
@@ -85,6 +92,9 @@ def run_wave(engine, args, wave: int, rank: int):
 
 def main():
     args = parse()
+    import logging
+    logging.basicConfig(level=getattr(logging, args.log_level.upper(), logging.WARNING),
+                        format="%(asctime)s %(name)s %(levelname)s %(message)s")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -178,6 +188,7 @@ def main():
             "p50_ttft_ms": round(p50_ttft, 2) if p50_ttft else None,
             "p50_tpot_ms": round(statistics.median(tpots) * 1e3, 3) if tpots else None,
             "engine_steps": steps,
+            "k9_skinny_gemm_shapes": len(_k9_plan()),
             "config": {"model": args.model, "global_batch": args.num_prompts * replicas,
                        "seq_len": args.input_len + args.output_len, "input_len": args.input_len,
                        "output_len": args.output_len,

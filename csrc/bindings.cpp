@@ -163,7 +163,8 @@ void paged_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor b
   TORCH_CHECK(max_logits.is_contiguous() && exp_sums.is_contiguous() && tmp_out.is_contiguous() &&
               max_logits.numel() >= B * nq * Zmax && exp_sums.numel() >= B * nq * Zmax &&
               tmp_out.numel() >= B * nq * Zmax * d, "partials too small");
-  TORCH_CHECK(Z >= 1 && Z <= Zmax && Z <= 65535, "kgc.paged_decode: need 1 <= Z <= partial slots");
+  TORCH_CHECK(Z >= 1 && Z <= Zmax && Z <= 1024,
+              "kgc.paged_decode: need 1 <= Z <= min(partial slots, 1024)");
   kgc::launch_paged_decode(dt_code(q), out.data_ptr(), q.data_ptr(), k_cache.data_ptr(),
                            v_cache.data_ptr(), block_tables.data_ptr<int>(),
                            (int)block_tables.stride(0), ctx_lens.data_ptr<int>(),

@@ -30,6 +30,7 @@ namespace kgc {
 
 constexpr int DEC_PART = 64;     // tokens per partition (one wave-iteration)
 constexpr int DEC_CHUNKS = DEC_PART / 32;
+constexpr int DEC_MAX_Z = 1024;  // z-slices the reduce kernel merges (host-checked)
 
 __device__ __forceinline__ u32x4 ld16(const void* p) {
   return *reinterpret_cast<const u32x4*>(p);
@@ -239,20 +240,32 @@ __global__ __launch_bounds__(64) void paged_decode_reduce_kernel(
     T* __restrict__ out, const float* __restrict__ max_logits,
     const float* __restrict__ exp_sums, const float* __restrict__ tmp_out,
     const int* __restrict__ ctx_lens, int nq, int Z, int Zmax) {
+  // The slice statistics are read in parallel (lane z), the weights staged in LDS,
+  // and empty slices (a short context in a grid sized for max_model_len: weight 0)
+  // are skipped -- the previous serial per-slice loop cost ~7 us per call at B = 1.
+  __shared__ float wz[DEC_MAX_Z];
   const int b = blockIdx.x, hq = blockIdx.y, tid = threadIdx.x;
   T* orow = out + ((int64_t)b * nq + hq) * D;
   constexpr int EPT = D / 64;
   const int64_t base = ((int64_t)b * nq + hq) * Zmax;
   float m = -INFINITY;
-  for (int z = 0; z < Z; ++z) m = fmaxf(m, max_logits[base + z]);
+  for (int z = tid; z < Z; z += 64) m = fmaxf(m, max_logits[base + z]);
+  m = wave_max(m);
   float acc[EPT];
 #pragma unroll
   for (int e = 0; e < EPT; ++e) acc[e] = 0.f;
   float tot = 0.f;
   if (ctx_lens[b] > 0 && m != -INFINITY) {
-    for (int z = 0; z < Z; ++z) {
+    for (int z = tid; z < Z; z += 64) {
       const float w = exp2f(max_logits[base + z] - m);
+      wz[z] = w;
       tot += w * exp_sums[base + z];
+    }
+    tot = wave_sum(tot);
+    __syncthreads();
+    for (int z = 0; z < Z; ++z) {
+      const float w = wz[z];
+      if (w == 0.f) continue;
       const float* src = tmp_out + (base + z) * D + tid * EPT;
 #pragma unroll
       for (int e = 0; e < EPT; ++e) acc[e] += w * src[e];

@@ -141,12 +141,13 @@ def decode_partials(batch: int, num_heads: int, head_dim: int, max_blocks: int,
 
 
 def decode_grid_z(batch: int, num_kv_heads: int, max_ctx: int, target_waves: int = 4096) -> int:
-    """z-slices of the decode grid: enough waves to fill 256 CUs (3 resident waves
-    per SIMD), bounded by the 64-token partitions of the longest context.  Z == 1
-    (large batches) lets the kernel write its output directly."""
+    """z-slices of the decode grid: enough waves to fill 256 CUs (4 resident waves
+    per SIMD), bounded by the 64-token partitions of the longest context and by the
+    1024 slices the reduce kernel merges.  Z == 1 (large batches) lets the kernel
+    write its output directly."""
     parts = max(1, math.ceil(max_ctx / DECODE_PARTITION))
     want = math.ceil(target_waves / max(1, batch * num_kv_heads * 4))
-    return max(1, min(want, math.ceil(parts / 4)))
+    return max(1, min(want, math.ceil(parts / 4), 1024))
 
 
 def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,

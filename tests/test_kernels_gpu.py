@@ -369,3 +369,4 @@ def test_linear_uses_tuned_plan(gpu):
     torch.testing.assert_close(gemm.linear(x, ws[0]).float(), (x @ ws[0].t()).float(),
                                atol=3e-2, rtol=2e-2)
     gemm.clear_plan()
+

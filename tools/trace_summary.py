@@ -15,6 +15,10 @@ import sys
 
 def family(name: str) -> str:
     n = name
+    if "skinny_gemm" in n:
+        return "skinny_gemm(K9)"
+    if "moe_gemm" in n:
+        return "moe_gemm(K14)"
     if "Cijk" in n or "gemm" in n.lower():
         return "gemm(hipblaslt)"
     for k in ("decode_gemm", "paged_decode_reduce", "paged_decode", "prefill_attn", "rms_norm",
