@@ -19,6 +19,9 @@ import asyncio
 import dataclasses
 import json
 import logging
+import os
+import socket
+import threading
 import time
 import uuid
 from typing import Any, Optional, Union
@@ -187,6 +190,30 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
         subs = [dataclasses.replace(sp, n=1, seed=None if sp.seed is None else sp.seed + i)
                 for i in range(n)]
         rids = [rid if n == 1 else f"{rid}-{i}" for i in range(n)]
+        if stream and n == 1:
+            # one coroutine per stream: engine output -> detok -> SSE bytes, no task or
+            # queue hop (the per-token path dominates the API process at 256 streams)
+            async def sse1():
+                detok = _Detok(tokenizer, sp.stop)
+                gen = engine.generate(ids, subs[0], rid)
+                try:
+                    async for out in gen:
+                        delta = detok.update(out.output_token_ids)
+                        reason = out.finish_reason if out.finished else None
+                        if detok.stopped:
+                            reason = "stop"
+                        elif reason:
+                            delta += detok.flush()
+                        if delta or reason or out.logprobs:
+                            yield stream_fn(delta, reason, out.logprobs, 0)
+                        if detok.stopped:
+                            break
+                except EngineDeadError as e:
+                    yield f"data: {json.dumps({'error': str(e)})}\n\n"
+                finally:
+                    await gen.aclose()
+                yield "data: [DONE]\n\n"
+            return StreamingResponse(sse1(), media_type="text/event-stream")
         if stream:
             q: asyncio.Queue = asyncio.Queue()
 
@@ -223,9 +250,7 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
                         if isinstance(lps, BaseException):
                             yield f"data: {json.dumps({'error': str(lps)})}\n\n"
                             continue
-                        c = stream_fn(delta, reason, lps)
-                        c["choices"][0]["index"] = i
-                        yield f"data: {json.dumps(c)}\n\n"
+                        yield stream_fn(delta, reason, lps, i)
                     yield "data: [DONE]\n\n"
                 finally:
                     for t in tasks:
@@ -308,12 +333,15 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
         prefix = (prompts if isinstance(prompts, str) else tokenizer.decode(ids)) if req.echo else ""
         want_lp = req.logprobs is not None
 
-        def chunk(delta, reason, lps=None):
-            return {"id": rid, "object": "text_completion", "created": int(time.time()),
-                    "model": served_name,
-                    "choices": [{"index": 0, "text": delta,
-                                 "logprobs": completion_logprobs(lps or []) if want_lp else None,
-                                 "finish_reason": reason}]}
+        head = f'data: {{"id": "{rid}", "object": "text_completion", "created": '
+        model_js = json.dumps(served_name)
+
+        def chunk(delta, reason, lps=None, index=0):
+            """One SSE event; the constant head is formatted once per request."""
+            lp = json.dumps(completion_logprobs(lps or [])) if want_lp else "null"
+            return (f'{head}{int(time.time())}, "model": {model_js}, "choices": [{{"index": '
+                    f'{index}, "text": {json.dumps(delta)}, "logprobs": {lp}, "finish_reason": '
+                    f'{json.dumps(reason)}}}]}}\n\n')
 
         def final(text, reason, np_, nc, lps=None):
             return {"id": rid, "object": "text_completion", "created": int(time.time()),
@@ -352,16 +380,17 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
         rid = f"chatcmpl-{uuid.uuid4().hex}"
         first = [True]
 
-        def chunk(delta, reason, lps=None):
+        def chunk(delta, reason, lps=None, index=0):
             d = {"content": delta}
             if first[0]:
                 d["role"] = "assistant"
                 first[0] = False
-            c = {"index": 0, "delta": d, "finish_reason": reason}
+            c = {"index": index, "delta": d, "finish_reason": reason}
             if req.logprobs:
                 c["logprobs"] = chat_logprobs(lps or [])
-            return {"id": rid, "object": "chat.completion.chunk", "created": int(time.time()),
-                    "model": served_name, "choices": [c]}
+            return "data: " + json.dumps({"id": rid, "object": "chat.completion.chunk",
+                                          "created": int(time.time()), "model": served_name,
+                                          "choices": [c]}) + "\n\n"
 
         def final(text, reason, np_, nc, lps=None):
             return {"id": rid, "object": "chat.completion", "created": int(time.time()),
@@ -411,28 +440,84 @@ def make_parser() -> argparse.ArgumentParser:
     p.add_argument("--engine-in-process", action="store_true",
                    help="run the engine loop on a thread of this process instead of a "
                         "separate engine-core process")
+    p.add_argument("--api-server-count", type=int, default=0,
+                   help="API processes sharing the port (SO_REUSEPORT) in front of one "
+                        "engine core; >1 spreads detokenisation / SSE of many concurrent "
+                        "streams over several CPUs (0: min(4, CPUs / 4))")
     add_engine_args(p)
     return p
 
 
-def main(argv=None) -> None:
+def _reuseport_socket(host: str, port: int) -> socket.socket:
+    s = socket.socket(socket.AF_INET6 if ":" in host else socket.AF_INET, socket.SOCK_STREAM)
+    s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    s.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEPORT, 1)
+    s.bind((host, port))
+    return s
+
+
+def _serve(ns, cfg: EngineConfig, connect=None, core_proc=None, sock=None) -> None:
+    """One API process: an engine (private core, shared core at ``connect``, or
+    in-process thread) behind uvicorn; with a shared core it exits when the core does."""
     import uvicorn
-    ns = make_parser().parse_args(argv)
-    ns.model = ns.model or ns.model_tag or "llama-3-8b"
-    cfg = config_from_args(ns)
     logging.basicConfig(level=logging.INFO)
     if ns.engine_in_process:
         eng = AsyncLLMEngine(cfg)
     else:
         from .engine_core import EngineCoreClient
-        eng = EngineCoreClient(cfg)
+        eng = EngineCoreClient(cfg, connect=connect, core_proc=core_proc)
     tok = get_tokenizer(cfg.model, eng.engine.mcfg, cfg.tokenizer)
     name = cfg.served_model_name or cfg.model
     app = build_app(eng, tok, name, eng.engine.max_model_len)
+    server = uvicorn.Server(uvicorn.Config(app, host=ns.host, port=ns.port,
+                                           log_level=ns.uvicorn_log_level))
+    if connect is not None:
+        def watchdog():
+            while not server.should_exit:
+                time.sleep(1.0)
+                if not eng.is_alive:
+                    server.should_exit = True
+        threading.Thread(target=watchdog, name="kgc-api-watchdog", daemon=True).start()
     try:
-        uvicorn.run(app, host=ns.host, port=ns.port, log_level=ns.uvicorn_log_level)
+        server.run(sockets=[sock] if sock is not None else None)
     finally:
         eng.shutdown()
+
+
+def _serve_worker(ns, cfg: EngineConfig, connect) -> None:
+    _serve(ns, cfg, connect=connect, sock=_reuseport_socket(ns.host, ns.port))
+
+
+def main(argv=None) -> None:
+    ns = make_parser().parse_args(argv)
+    ns.model = ns.model or ns.model_tag or "llama-3-8b"
+    cfg = config_from_args(ns)
+    n = ns.api_server_count or min(4, max(1, (os.cpu_count() or 1) // 4))
+    if n == 1 or ns.engine_in_process:
+        _serve(ns, cfg)
+        return
+    import multiprocessing as mp
+    import secrets
+    import shutil
+    import tempfile
+    from .engine_core import start_core
+    tmp = tempfile.mkdtemp(prefix="kgc-core-")
+    connect = (os.path.join(tmp, "core.sock"), secrets.token_bytes(32))
+    core = start_core(cfg, connect[0], connect[1], n)
+    ctx = mp.get_context("spawn")
+    workers = [ctx.Process(target=_serve_worker, args=(ns, cfg, connect), name=f"kgc-api-{i}")
+               for i in range(1, n)]
+    for w in workers:
+        w.start()
+    try:
+        _serve(ns, cfg, connect=connect, core_proc=core,
+               sock=_reuseport_socket(ns.host, ns.port))
+    finally:
+        for w in workers:
+            w.join(30)
+            if w.is_alive():
+                w.terminate()
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 if __name__ == "__main__":

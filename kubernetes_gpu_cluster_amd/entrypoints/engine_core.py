@@ -13,6 +13,12 @@ GPU, so spawning stays safe.  The two talk over one duplex pipe:
   resolved tokens.  A reader thread delivers it to the event loop with one
   thread-safe call.
 
+At 256 concurrent streams one API process is itself CPU-bound (detokenisation,
+JSON and SSE writes for every token of every stream each ~11 ms step), so
+``--api-server-count N`` runs N API processes on one port (SO_REUSEPORT) in front of
+ONE engine core: the core accepts N connections on a unix socket and sends each
+frontend only the outputs of the requests it submitted.
+
 The interface matches ``AsyncLLMEngine``: ``generate``, ``abort``, ``is_alive``,
 ``shutdown``, ``metrics_text``, ``mcfg``, ``max_model_len``.  ``build_app`` therefore
 accepts either.  ``--engine-in-process`` selects the thread-backed engine instead.
@@ -23,8 +29,11 @@ import asyncio
 import itertools
 import logging
 import multiprocessing as mp
+import os
 import threading
+import time
 import traceback
+from multiprocessing.connection import wait as mp_wait
 from typing import AsyncIterator, Optional
 
 from ..engine.config import EngineConfig
@@ -35,53 +44,120 @@ log = logging.getLogger("kgc.engine_core")
 
 
 # ---------------------------------------------------------------------------- core process
-def _core_main(cfg: EngineConfig, conn) -> None:
+def _make_engine(cfg: EngineConfig):
+    if os.environ.get("KGC_FAKE_ENGINE"):
+        # GPU-free timing model of the engine (engine/fake.py): load-tests the
+        # API / router / client path above the engine on a CPU-only machine
+        from ..engine.fake import FakeEngine
+        return FakeEngine(cfg)
+    from ..engine.llm_engine import LLMEngine
+    return LLMEngine(cfg)
+
+
+def _core_main(cfg: EngineConfig, conn, listen: Optional[tuple] = None) -> None:
+    """``conn``: the pipe to a single frontend; or, with ``listen = (address, authkey,
+    n)``, accept ``n`` frontend connections (``--api-server-count``) and route every
+    request's outputs back to the frontend that submitted it."""
     logging.basicConfig(level=logging.INFO)
+    conns = [conn] if conn is not None else []
+    listener = None
+    if listen is not None:
+        from multiprocessing.connection import Listener
+        listener = Listener(listen[0], authkey=listen[1])
     try:
-        from ..engine.llm_engine import LLMEngine
-        eng = LLMEngine(cfg)
+        eng = _make_engine(cfg)
     except BaseException:  # noqa: BLE001
-        conn.send(("dead", traceback.format_exc()))
+        tb = traceback.format_exc()
+        if listener is not None:
+            for _ in range(listen[2]):
+                try:
+                    listener.accept().send(("dead", tb))
+                except OSError:
+                    break
+        else:
+            conn.send(("dead", tb))
         return
-    conn.send(("ready", {"mcfg": eng.mcfg, "max_model_len": eng.max_model_len}))
+    ready_msg = ("ready", {"mcfg": eng.mcfg, "max_model_len": eng.max_model_len})
+    if listener is not None:
+        for _ in range(listen[2]):        # each frontend may start serving once attached
+            conns.append(listener.accept())
+            conns[-1].send(ready_msg)
+        listener.close()
+    else:
+        conn.send(ready_msg)
+    owner: dict = {}          # request id -> connection of the frontend that submitted it
     try:
         running = True
-        while running:
+        while running and conns:
             idle = not eng.has_unfinished()
-            # drain the inbox; block briefly only when there is nothing to run
-            while conn.poll(0.05 if idle else 0):
-                msg = conn.recv()
-                kind = msg[0]
-                if kind == "add":
-                    _, rid, ids, params, arrival = msg
+            # drain every inbox; block briefly only when there is nothing to run
+            ready = mp_wait(conns, 0.05 if idle else 0)
+            while ready and running:
+                for c in ready:
                     try:
-                        eng.add_request(ids, params, request_id=rid, arrival_time=arrival)
-                    except Exception as e:  # noqa: BLE001 - reported to that request
-                        conn.send(("reject", rid, f"{type(e).__name__}: {e}"))
-                elif kind == "abort":
-                    eng.abort(msg[1])
-                elif kind == "metrics":
-                    from prometheus_client import generate_latest
-                    conn.send(("metrics", msg[1], generate_latest(eng.metrics.registry).decode()))
-                elif kind == "shutdown":
-                    running = False
-                    break
-                idle = False
+                        msg = c.recv()
+                    except (EOFError, OSError):
+                        conns.remove(c)        # a frontend went away: drop its requests
+                        for rid in [r for r, oc in owner.items() if oc is c]:
+                            owner.pop(rid)
+                            eng.abort(rid)
+                        continue
+                    kind = msg[0]
+                    if kind == "add":
+                        _, rid, ids, params, arrival = msg
+                        try:
+                            eng.add_request(ids, params, request_id=rid, arrival_time=arrival)
+                            owner[rid] = c
+                        except Exception as e:  # noqa: BLE001 - reported to that request
+                            c.send(("reject", rid, f"{type(e).__name__}: {e}"))
+                    elif kind == "abort":
+                        owner.pop(msg[1], None)
+                        eng.abort(msg[1])
+                    elif kind == "metrics":
+                        from prometheus_client import generate_latest
+                        c.send(("metrics", msg[1], generate_latest(eng.metrics.registry).decode()))
+                    elif kind == "shutdown":
+                        running = False
+                        break
+                ready = mp_wait(conns, 0) if running and conns else []
             if running and eng.has_unfinished():
-                outs = eng.step()
-                if outs:
-                    conn.send(("out", [(o.request_id, o.new_token_ids, o.finished, o.finish_reason,
-                                        o.arrival_time, o.first_token_time, o.finish_time,
-                                        o.num_preemptions, o.logprobs) for o in outs]))
+                by_conn: dict = {}
+                for o in eng.step():
+                    c = owner.get(o.request_id)
+                    if c is None:
+                        continue
+                    if o.finished:
+                        owner.pop(o.request_id, None)
+                    by_conn.setdefault(c, []).append(
+                        (o.request_id, o.new_token_ids, o.finished, o.finish_reason,
+                         o.arrival_time, o.first_token_time, o.finish_time,
+                         o.num_preemptions, o.logprobs))
+                for c, items in by_conn.items():
+                    try:
+                        c.send(("out", items))
+                    except OSError:
+                        pass
     except BaseException:  # noqa: BLE001
         tb = traceback.format_exc()
         log.error("engine core died: %s", tb)
-        try:
-            conn.send(("dead", tb))
-        except OSError:
-            pass
+        for c in conns:
+            try:
+                c.send(("dead", tb))
+            except OSError:
+                pass
     finally:
         eng.shutdown()
+
+
+def start_core(cfg: EngineConfig, address: str, authkey: bytes, n_frontends: int):
+    """Start an engine core serving ``n_frontends`` API processes over the unix socket
+    ``address`` (``--api-server-count``); each attaches with
+    ``EngineCoreClient(cfg, connect=(address, authkey))``."""
+    ctx = mp.get_context("spawn")
+    proc = ctx.Process(target=_core_main, args=(cfg, None, (address, authkey, n_frontends)),
+                       name="kgc-engine-core")
+    proc.start()
+    return proc
 
 
 # ---------------------------------------------------------------------------- API side
@@ -93,19 +169,38 @@ class _Stream:
 
 
 class EngineCoreClient:
-    def __init__(self, cfg: EngineConfig, startup_timeout: float = 3600.0):
+    def __init__(self, cfg: EngineConfig, startup_timeout: float = 3600.0,
+                 connect: Optional[tuple] = None, core_proc=None):
+        """Spawn a private engine core (default), or attach to a shared one at
+        ``connect = (address, authkey)``; ``core_proc`` is given in the process that
+        started the shared core (liveness and shutdown)."""
         self.cfg = cfg
-        ctx = mp.get_context("spawn")
-        self._conn, child = ctx.Pipe(duplex=True)
-        self._proc = ctx.Process(target=_core_main, args=(cfg, child), name="kgc-engine-core")
-        self._proc.start()
-        child.close()
+        if connect is None:
+            ctx = mp.get_context("spawn")
+            self._conn, child = ctx.Pipe(duplex=True)
+            self._proc = ctx.Process(target=_core_main, args=(cfg, child), name="kgc-engine-core")
+            self._proc.start()
+            child.close()
+        else:
+            from multiprocessing.connection import Client
+            self._proc = core_proc
+            deadline = time.monotonic() + startup_timeout
+            while True:              # the core binds its socket before loading weights
+                try:
+                    self._conn = Client(connect[0], authkey=connect[1])
+                    break
+                except (FileNotFoundError, ConnectionRefusedError):
+                    if time.monotonic() > deadline:
+                        raise RuntimeError("engine core socket never appeared")
+                    time.sleep(0.2)
         if not self._conn.poll(startup_timeout):
-            self._proc.kill()
+            if self._proc is not None:
+                self._proc.kill()
             raise RuntimeError("engine core did not start in time")
         kind, info = self._conn.recv()
         if kind != "ready":
-            self._proc.join(10)
+            if self._proc is not None:
+                self._proc.join(10)
             raise RuntimeError(f"engine core failed to start:\n{info}")
         self.mcfg = info["mcfg"]
         self.max_model_len = info["max_model_len"]
@@ -164,13 +259,12 @@ class EngineCoreClient:
 
     @property
     def is_alive(self) -> bool:
-        return self.error is None and self._proc.is_alive()
+        return self.error is None and (self._proc is None or self._proc.is_alive())
 
     async def generate(self, prompt_ids: list[int], params: SamplingParams,
                        request_id: str) -> AsyncIterator[RequestOutput]:
         if not self.is_alive:
             raise EngineDeadError(str(self.error))
-        import time
         loop = asyncio.get_running_loop()
         q: asyncio.Queue = asyncio.Queue()
         self._streams[request_id] = _Stream(loop, q, list(prompt_ids))
@@ -210,6 +304,12 @@ class EngineCoreClient:
         return await asyncio.wait_for(fut, 10)
 
     def shutdown(self) -> None:
+        if self._proc is None:            # attached to a shared core: just detach
+            try:
+                self._conn.close()
+            except OSError:
+                pass
+            return
         try:
             self._send(("shutdown",))
         except OSError:

@@ -169,3 +169,35 @@ def test_n_choices_and_penalties(client):
     assert idx == {0, 1}
     assert client.post("/v1/completions", json={"prompt": "x", "n": 99}).status_code == 400
     assert client.post("/v1/completions", json={"prompt": "x", "presence_penalty": 5}).status_code == 400
+
+
+def test_shared_core_serves_two_frontends(tmp_path):
+    """--api-server-count: one engine core, two attached frontends; each frontend gets
+    exactly its own requests' outputs, and a detached frontend leaves the core running."""
+    import asyncio
+
+    from kubernetes_gpu_cluster_amd.engine.sequence import SamplingParams
+    from kubernetes_gpu_cluster_amd.entrypoints.engine_core import EngineCoreClient, start_core
+    cfg = _cfg()
+    addr, key = str(tmp_path / "core.sock"), b"k" * 32
+    core = start_core(cfg, addr, key, 2)
+    a = EngineCoreClient(cfg, connect=(addr, key), core_proc=core)
+    b = EngineCoreClient(cfg, connect=(addr, key))
+    sp = SamplingParams(max_tokens=5, ignore_eos=True, temperature=0.0)
+
+    async def run(cl, rid, prompt):
+        toks = []
+        async for o in cl.generate(prompt, sp, rid):
+            toks = list(o.output_token_ids)
+        return toks
+
+    async def go():
+        return await asyncio.gather(run(a, "a1", [5, 6, 7]), run(b, "b1", [5, 6, 7]),
+                                    run(a, "a2", [8, 9]), run(b, "b2", [8, 9]))
+    ra1, rb1, ra2, rb2 = asyncio.run(go())
+    assert len(ra1) == 5 and ra1 == rb1 and ra2 == rb2
+    b.shutdown()                       # detach one frontend; the core keeps serving
+    assert asyncio.run(run(a, "a3", [5, 6, 7])) == ra1
+    a.shutdown()
+    core.join(30)
+    assert not core.is_alive()
