@@ -79,7 +79,8 @@ def engine_args(ms: dict) -> list[str]:
                ("gpuMemoryUtilization", "--gpu-memory-utilization"),
                ("maxModelLen", "--max-model-len"), ("dtype", "--dtype"),
                ("maxNumSeqs", "--max-num-seqs"), ("blockSize", "--block-size"),
-               ("maxNumBatchedTokens", "--max-num-batched-tokens")]
+               ("maxNumBatchedTokens", "--max-num-batched-tokens"),
+               ("apiServerCount", "--api-server-count")]
     for key, flag in mapping:
         if key in vc and vc[key] is not None and not _flag_present(extra, flag):
             args += [flag, str(vc[key])]
