@@ -214,8 +214,14 @@ void sample(Tensor out, Tensor logits, Tensor temperature, Tensor top_k, Tensor 
   TORCH_CHECK(top_k.scalar_type() == at::kInt && top_k.numel() >= B, "top_k int32");
   TORCH_CHECK(top_p.scalar_type() == at::kFloat && top_p.numel() >= B, "top_p fp32");
   TORCH_CHECK(seeds.scalar_type() == at::kLong && seeds.numel() >= B, "seeds int64");
-  kgc::launch_sample(dt_code(logits), out.data_ptr<int64_t>(), logits.data_ptr(), logits.stride(0),
-                     (int)B, (int)logits.size(1), temperature.data_ptr<float>(),
+  TORCH_CHECK(B <= 65535 * 256 && logits.size(1) < INT32_MAX, "kgc.sample: shape");
+  if (B == 0) return;
+  // per-(row, vocab split) candidates; from the caching allocator, so graph capture
+  // gives the workspace a fixed address like any other captured temporary
+  Tensor partial = at::empty({B * kgc::sample_splits((int)B)}, logits.options().dtype(at::kLong));
+  kgc::launch_sample(dt_code(logits), out.data_ptr<int64_t>(),
+                     reinterpret_cast<uint64_t*>(partial.data_ptr<int64_t>()), logits.data_ptr(),
+                     logits.stride(0), (int)B, (int)logits.size(1), temperature.data_ptr<float>(),
                      top_k.data_ptr<int>(), top_p.data_ptr<float>(), seeds.data_ptr<int64_t>(),
                      stream());
 }

@@ -33,9 +33,10 @@ void launch_prefill_attention(int dtype, const void* q, void* out, const void* k
                               int nkv, int D, int bs_log2, float scale, bool kv_fp8,
                               float k_scale, float v_scale, hipStream_t s);
 int prefill_block_m();
-void launch_sample(int dtype, int64_t* out, const void* logits, int64_t row_stride, int B,
-                   int V, const float* temperature, const int* top_k, const float* top_p,
-                   const int64_t* seeds, hipStream_t s);
+int sample_splits(int B);   // vocabulary splits per row; partial holds B * splits words
+void launch_sample(int dtype, int64_t* out, uint64_t* partial, const void* logits,
+                   int64_t row_stride, int B, int V, const float* temperature, const int* top_k,
+                   const float* top_p, const int64_t* seeds, hipStream_t s);
 
 // K9 skinny (small-M decode) GEMM: C[M, N] = X[M, K] . W[N, K]^T (+ bias), M <= 16*mt.
 void launch_skinny_gemm(int dtype, int mt, int nt, int nw, bool ntl, void* C, const void* X,

@@ -1,4 +1,5 @@
-// K10 sampler: one 1024-thread workgroup per row of logits [B, V].
+// K10 sampler: 1024-thread workgroups over the rows of logits [B, V] (a row's vocabulary
+// split over several workgroups at small batch), then a per-row merge.
 //   temperature <= 1e-5        -> argmax (first index on ties)
 //   otherwise x = logit / temp -> optional top-k threshold (4-pass radix select on the
 //                                 order-preserving uint32 image of x), optional top-p
@@ -8,10 +9,13 @@
 // ops/reference.uniform_noise, so sampled ids are reproducible per request seed.
 #include "common.h"
 #include "launch.h"
+#include <algorithm>
 
 namespace kgc {
 
 constexpr int SMP_NT = 1024;
+constexpr int SMP_NBIN = 2048;   // distance-from-max bins of the top-k / top-p pre-pass
+constexpr int SMP_DB = 64;       // bins per nat of logit distance
 
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x ^= x >> 16;
@@ -33,22 +37,71 @@ __device__ __forceinline__ float key_val(uint32_t k) {
 template <typename T>
 __device__ __forceinline__ float load_logit(const T* row, int i) { return to_f(row[i]); }
 
+// Inclusive prefix sum of one value per thread over a SMP_NT-thread block: wave64
+// shuffle scans, then the wave totals (scratch: SMP_NT / 64 floats).
+__device__ __forceinline__ float block_scan_incl(float v, float* wtot) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  if (lane == 63) wtot[w] = v;
+  __syncthreads();
+  float off = 0.f;
+  for (int j = 0; j < w; ++j) off += wtot[j];
+  __syncthreads();
+  return v + off;
+}
+
+// f(i, logit) over row[lo, hi) by a SMP_NT-thread block.  16-bit rows are read as
+// 16-byte vectors (8 logits per load, 2 loads in flight per thread): every pass over
+// a 128K-entry row is then ~16 dependent round trips per thread instead of ~125.
+template <typename T, typename F>
+__device__ __forceinline__ void visit_row(const T* __restrict__ row, int lo, int hi, int tid,
+                                          F&& f) {
+  if constexpr (sizeof(T) == 2) {
+    const int a = min(hi, (lo + 7) & ~7);
+    const int e = max(a, hi & ~7);
+    if ((reinterpret_cast<uintptr_t>(row) & 15) == 0) {
+      for (int i = lo + tid; i < a; i += SMP_NT) f(i, to_f(row[i]));
+#pragma unroll 2
+      for (int v = a + 8 * tid; v < e; v += 8 * SMP_NT) {
+        Pack8<T> p;
+        p.u = *reinterpret_cast<const u32x4*>(row + v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f(v + j, to_f(p.h[j]));
+      }
+      for (int i = e + tid; i < hi; i += SMP_NT) f(i, to_f(row[i]));
+      return;
+    }
+  }
+  for (int i = lo + tid; i < hi; i += SMP_NT) f(i, to_f(row[i]));
+}
+
 __device__ __forceinline__ void argmax_merge(float& v, int& i, float v2, int i2) {
   if (v2 > v || (v2 == v && i2 < i)) { v = v2; i = i2; }
 }
 
+// Grid (B, S): the S blocks of a row split its vocabulary for the (Gumbel-)argmax pass,
+// the expensive one (two logs and two hashes per logit).  A row with a top-k / top-p
+// threshold has every block compute that threshold over the whole row first (cheap
+// vectorised passes, run in parallel), so no single block walks the row alone.
+// Each block writes its (value, index) candidate packed into one uint64 (value's
+// order-preserving image high, inverted index low: max = larger value, then lower
+// index) and sample_merge_kernel reduces the S candidates of a row.
 template <typename T>
 __global__ __launch_bounds__(SMP_NT) void sample_kernel(
-    int64_t* __restrict__ out, const T* __restrict__ logits, int64_t row_stride, int V,
+    uint64_t* __restrict__ partial, const T* __restrict__ logits, int64_t row_stride, int V,
     const float* __restrict__ temperature, const int* __restrict__ top_k,
     const float* __restrict__ top_p, const int64_t* __restrict__ seeds) {
   __shared__ float red_v[SMP_NT / 64];
   __shared__ int red_i[SMP_NT / 64];
   __shared__ float hist_f[256];
-  __shared__ uint32_t hist_u[256];
+  __shared__ float hist_d[SMP_NBIN];
+  __shared__ float scan_w[SMP_NT / 64];
   __shared__ uint32_t sel_bin;
   __shared__ float sel_f;
-  __shared__ uint32_t sel_u;
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const T* row = logits + (int64_t)b * row_stride;
   const float temp = temperature[b];
@@ -57,78 +110,112 @@ __global__ __launch_bounds__(SMP_NT) void sample_kernel(
   const float p = greedy ? 1.f : top_p[b];
   const bool use_k = k > 0 && k < V;
   const bool use_p = p < 1.f;
+  const int S = gridDim.y, y = blockIdx.y;
+  const int i_lo = (int)((int64_t)V * y / S);
+  const int i_hi = (int)((int64_t)V * (y + 1) / S);
 
-  auto xval = [&](int i) -> float { return greedy ? load_logit(row, i) : load_logit(row, i) / temp; };
+  auto xv = [&](float raw) -> float { return greedy ? raw : raw / temp; };
 
   // ---------- thresholds (kept support = x >= thr)
+  // Both selects first bin the row by distance from its max (SMP_DB bins per nat, so
+  // a row spreads over hundreds of bins), then resolve the bin holding the k-th value
+  // / the p-mass crossing exactly with radix passes restricted to that bin's few
+  // elements.  Every "where does the running total cross the target" search is a
+  // block-parallel prefix sum: a serial scan by one thread cost ~100 cycles per bin
+  // (~300 us per top-p row with the 2048 + 4 x 256 bins).
+  // The selects run on the raw logits: x = raw / temp is order-preserving (temp > 0),
+  // so "raw >= thr" keeps exactly the tokens "x >= thr * ..." would, and no pass but
+  // the final one pays the fp32 division (the masses use raw * (1 / temp)).
   float thr = -INFINITY;
   if (use_k || use_p) {
+    float mx = -INFINITY;
+    visit_row(row, 0, V, tid, [&](int, float r) { mx = fmaxf(mx, r); });
+    mx = block_max<SMP_NT>(mx, red_v);
+    const float it = 1.f / temp;                   // x = raw * it for the softmax mass
+    auto dbin = [&](float x) -> int {
+      const float d = (mx - x) * it * (float)SMP_DB;
+      return d < (float)(SMP_NBIN - 1) ? (int)d : SMP_NBIN - 1;   // -inf / NaN -> last
+    };
+    // distance bins in value order (bin 0 = largest values): first bin whose running
+    // total reaches `target` -> sel_bin, the total before it -> sel_f; 2 bins / thread
+    auto cross_dist = [&](float target) {
+      if (tid == 0) { sel_bin = SMP_NBIN - 1; sel_f = 0.f; }
+      const float h0 = hist_d[2 * tid], h1 = hist_d[2 * tid + 1];
+      const float incl = block_scan_incl(h0 + h1, scan_w);
+      const float excl = incl - h0 - h1;
+      if (excl < target && excl + h0 >= target) { sel_bin = 2 * tid; sel_f = excl; }
+      else if (excl + h0 < target && incl >= target) { sel_bin = 2 * tid + 1; sel_f = excl + h0; }
+      __syncthreads();
+    };
+    // radix bins visited from 255 down to `lowest`: first one whose running total
+    // (starting at `start`) reaches `target` -> sel_bin, the total before it -> sel_f;
+    // none -> bin `fallback`, the total over the visited bins
+    auto cross_radix = [&](const float* h, float start, float target, int lowest, int fallback) {
+      const int pos = tid, bin = 255 - pos;
+      const float v = (pos < 256 && bin >= lowest) ? h[bin] : 0.f;
+      const float incl = start + block_scan_incl(v, scan_w);
+      const float excl = incl - v;
+      if (tid == SMP_NT - 1) { sel_bin = fallback; sel_f = incl; }
+      __syncthreads();
+      if (pos < 256 && bin >= lowest && excl < target && incl >= target) {
+        sel_bin = bin;
+        sel_f = excl;
+      }
+      __syncthreads();
+    };
     if (use_k) {
+      for (int j = tid; j < SMP_NBIN; j += SMP_NT) hist_d[j] = 0.f;
+      __syncthreads();
+      visit_row(row, 0, V, tid, [&](int, float r) { atomicAdd(&hist_d[dbin(r)], 1.f); });
+      __syncthreads();
+      cross_dist((float)k);
+      const int kbin = (int)sel_bin;
       uint32_t prefix = 0, mask = 0;
-      int remaining = k;
+      float remaining = (float)k - sel_f;       // counts: exact in fp32 up to 2^24
       for (int shift = 24; shift >= 0; shift -= 8) {
-        if (tid < 256) hist_u[tid] = 0;
+        if (tid < 256) hist_f[tid] = 0.f;
         __syncthreads();
-        for (int i = tid; i < V; i += SMP_NT) {
-          const uint32_t kk = ord_key(xval(i));
-          if ((kk & mask) == prefix) atomicAdd(&hist_u[(kk >> shift) & 255], 1u);
-        }
+        visit_row(row, 0, V, tid, [&](int, float r) {
+          const uint32_t kk = ord_key(r);
+          if (dbin(r) == kbin && (kk & mask) == prefix) atomicAdd(&hist_f[(kk >> shift) & 255], 1.f);
+        });
         __syncthreads();
-        if (tid == 0) {
-          int acc = 0, bin = 0;
-          for (bin = 255; bin >= 0; --bin) {
-            if (acc + (int)hist_u[bin] >= remaining) break;
-            acc += hist_u[bin];
-          }
-          sel_bin = (uint32_t)max(bin, 0);
-          sel_u = (uint32_t)acc;
-        }
-        __syncthreads();
-        remaining -= (int)sel_u;
+        cross_radix(hist_f, 0.f, remaining, 0, 0);
+        remaining -= sel_f;
         prefix |= sel_bin << shift;
         mask |= 255u << shift;
       }
       thr = key_val(prefix);
     }
     if (use_p) {
-      // max and normaliser over the current support
-      float mx = -INFINITY;
-      for (int i = tid; i < V; i += SMP_NT) {
-        const float x = xval(i);
-        if (x >= thr) mx = fmaxf(mx, x);
-      }
-      mx = block_max<SMP_NT>(mx, red_v);
+      // normaliser and p-mass histogram over the current support (mx is still its max)
+      for (int j = tid; j < SMP_NBIN; j += SMP_NT) hist_d[j] = 0.f;
+      __syncthreads();
       float z = 0.f;
-      for (int i = tid; i < V; i += SMP_NT) {
-        const float x = xval(i);
-        if (x >= thr) z += __expf(x - mx);
-      }
+      visit_row(row, 0, V, tid, [&](int, float r) {
+        if (r >= thr) {
+          const float e = __expf((r - mx) * it);
+          z += e;
+          atomicAdd(&hist_d[dbin(r)], e);
+        }
+      });
       z = block_sum<SMP_NT>(z, red_v);
       const float target = p * z;
+      cross_dist(target);
+      const int pbin = (int)sel_bin;
       uint32_t prefix = 0, mask = 0;
-      float above = 0.f;
+      float above = sel_f;
       const uint32_t kthr = ord_key(thr);
       for (int shift = 24; shift >= 0; shift -= 8) {
         if (tid < 256) hist_f[tid] = 0.f;
         __syncthreads();
-        for (int i = tid; i < V; i += SMP_NT) {
-          const float x = xval(i);
-          const uint32_t kk = ord_key(x);
-          if (kk >= kthr && (kk & mask) == prefix)
-            atomicAdd(&hist_f[(kk >> shift) & 255], __expf(x - mx));
-        }
+        visit_row(row, 0, V, tid, [&](int, float r) {
+          const uint32_t kk = ord_key(r);
+          if (kk >= kthr && dbin(r) == pbin && (kk & mask) == prefix)
+            atomicAdd(&hist_f[(kk >> shift) & 255], __expf((r - mx) * it));
+        });
         __syncthreads();
-        if (tid == 0) {
-          float acc = above;
-          int bin;
-          for (bin = 255; bin > 0; --bin) {
-            if (acc + hist_f[bin] >= target) break;
-            acc += hist_f[bin];
-          }
-          sel_bin = (uint32_t)bin;
-          sel_f = acc;
-        }
-        __syncthreads();
+        cross_radix(hist_f, above, target, 1, 0);
         above = sel_f;
         prefix |= sel_bin << shift;
         mask |= 255u << shift;
@@ -143,16 +230,16 @@ __global__ __launch_bounds__(SMP_NT) void sample_kernel(
   const uint32_t hi = (uint32_t)(seed >> 32);
   float best = -INFINITY;
   int besti = 0x7fffffff;
-  for (int i = tid; i < V; i += SMP_NT) {
-    float x = xval(i);
+  visit_row(row, i_lo, i_hi, tid, [&](int i, float r) {
+    float x = xv(r);
     if (!greedy) {
-      if (x < thr) continue;
+      if (r < thr) return;
       const uint32_t h = mix32(mix32(key ^ (uint32_t)(i * 0x9E3779B9u)) + hi);
       const float u = ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
       x += -logf(-logf(u));
     }
     argmax_merge(best, besti, x, i);
-  }
+  });
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float v2 = __shfl_xor(best, o, 64);
@@ -165,23 +252,42 @@ __global__ __launch_bounds__(SMP_NT) void sample_kernel(
     float bv = red_v[0];
     int bi = red_i[0];
     for (int j = 1; j < SMP_NT / 64; ++j) argmax_merge(bv, bi, red_v[j], red_i[j]);
-    out[b] = bi == 0x7fffffff ? 0 : bi;
+    partial[(int64_t)b * S + y] = ((uint64_t)ord_key(bv) << 32) | (uint32_t)(~(uint32_t)bi);
   }
 }
 
-void launch_sample(int dtype, int64_t* out, const void* logits, int64_t row_stride, int B,
-                   int V, const float* temperature, const int* top_k, const float* top_p,
-                   const int64_t* seeds, hipStream_t s) {
+// One thread per row: the largest packed candidate of the row's S blocks.
+__global__ __launch_bounds__(256) void sample_merge_kernel(int64_t* __restrict__ out,
+                                                           const uint64_t* __restrict__ partial,
+                                                           int B, int S) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  uint64_t best = 0;
+  for (int y = 0; y < S; ++y) best = max(best, partial[(int64_t)b * S + y]);
+  const uint32_t idx = ~(uint32_t)(best & 0xffffffffu);
+  out[b] = (best == 0 || idx >= 0x7fffffffu) ? 0 : (int64_t)idx;
+}
+
+int sample_splits(int B) {
+  // enough 1024-thread blocks to cover the chip at small batch; 1 block/row at large
+  return B >= 512 ? 1 : std::min(32, (512 + B - 1) / B);
+}
+
+void launch_sample(int dtype, int64_t* out, uint64_t* partial, const void* logits,
+                   int64_t row_stride, int B, int V, const float* temperature, const int* top_k,
+                   const float* top_p, const int64_t* seeds, hipStream_t s) {
   if (B == 0) return;
+  const dim3 grid(B, sample_splits(B));
   if (dtype == DT_BF16)
-    sample_kernel<bf16><<<B, SMP_NT, 0, s>>>(out, (const bf16*)logits, row_stride, V,
-                                             temperature, top_k, top_p, seeds);
+    sample_kernel<bf16><<<grid, SMP_NT, 0, s>>>(partial, (const bf16*)logits, row_stride, V,
+                                                temperature, top_k, top_p, seeds);
   else if (dtype == DT_F16)
-    sample_kernel<f16><<<B, SMP_NT, 0, s>>>(out, (const f16*)logits, row_stride, V,
-                                            temperature, top_k, top_p, seeds);
+    sample_kernel<f16><<<grid, SMP_NT, 0, s>>>(partial, (const f16*)logits, row_stride, V,
+                                               temperature, top_k, top_p, seeds);
   else
-    sample_kernel<float><<<B, SMP_NT, 0, s>>>(out, (const float*)logits, row_stride, V,
-                                              temperature, top_k, top_p, seeds);
+    sample_kernel<float><<<grid, SMP_NT, 0, s>>>(partial, (const float*)logits, row_stride, V,
+                                                 temperature, top_k, top_p, seeds);
+  sample_merge_kernel<<<(B + 255) / 256, 256, 0, s>>>(out, partial, B, grid.y);
 }
 
 }  // namespace kgc
