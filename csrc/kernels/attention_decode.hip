@@ -241,8 +241,9 @@ __global__ __launch_bounds__(64) void paged_decode_reduce_kernel(
     const float* __restrict__ exp_sums, const float* __restrict__ tmp_out,
     const int* __restrict__ ctx_lens, int nq, int Z, int Zmax) {
   // The slice statistics are read in parallel (lane z), the weights staged in LDS,
-  // and empty slices (a short context in a grid sized for max_model_len: weight 0)
-  // are skipped -- the previous serial per-slice loop cost ~7 us per call at B = 1.
+  // and the partial rows loaded 8 slices at a time: the previous per-slice loop was a
+  // chain of dependent L2 round trips (~7 us per call at B = 1; decode + reduce for
+  // B = 1, ctx 565, Z = 16 went 13.0 -> 9.3 us).
   __shared__ float wz[DEC_MAX_Z];
   const int b = blockIdx.x, hq = blockIdx.y, tid = threadIdx.x;
   T* orow = out + ((int64_t)b * nq + hq) * D;
@@ -263,12 +264,22 @@ __global__ __launch_bounds__(64) void paged_decode_reduce_kernel(
     }
     tot = wave_sum(tot);
     __syncthreads();
-    for (int z = 0; z < Z; ++z) {
-      const float w = wz[z];
-      if (w == 0.f) continue;
-      const float* src = tmp_out + (base + z) * D + tid * EPT;
+    // 8 slices' partial rows in flight per step (every slice wrote its row, empty
+    // ones with weight 0), instead of one dependent L2 round trip per slice
+    for (int z0 = 0; z0 < Z; z0 += 8) {
+      float v[8][EPT], wv[8];
 #pragma unroll
-      for (int e = 0; e < EPT; ++e) acc[e] += w * src[e];
+      for (int j = 0; j < 8; ++j) {
+        const int z = min(z0 + j, Z - 1);
+        wv[j] = z0 + j < Z ? wz[z] : 0.f;
+        const float* src = tmp_out + (base + z) * D + tid * EPT;
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) v[j][e] = src[e];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) acc[e] += wv[j] * v[j][e];
     }
   }
   const float inv = tot > 0.f ? 1.f / tot : 0.f;
