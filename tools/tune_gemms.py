@@ -26,6 +26,11 @@ def main():
                     help="also tune these token counts (full chunked-prefill steps run exactly "
                          "--max-num-batched-tokens tokens)")
     ap.add_argument("--append", action="store_true", help="keep the rows already in --out")
+    ap.add_argument("--min-bs", type=int, default=1, help="only tune buckets >= this")
+    ap.add_argument("--rotating-mb", type=int, default=0,
+                    help="TunableOp rotating input buffers of this many MB: > 256 MB (the "
+                         "Infinity Cache) times every candidate on cold weights, as a decode "
+                         "graph runs them")
     a = ap.parse_args()
     from kubernetes_gpu_cluster_amd.utils.gemm_tuning import default_table_path
     out = a.out or default_table_path(a.model, a.tp)
@@ -37,6 +42,8 @@ def main():
     if a.append and os.path.exists(out):
         torch.cuda.tunable.read_file(out)
     torch.cuda.tunable.set_max_tuning_duration(60)
+    if a.rotating_mb:
+        torch.cuda.tunable.set_rotating_buffer_size(a.rotating_mb)
     import torch.nn.functional as F
     from kubernetes_gpu_cluster_amd.engine.model_runner import graph_buckets
     from kubernetes_gpu_cluster_amd.models.configs import PRESETS
@@ -50,7 +57,8 @@ def main():
     dev = torch.device("cuda")
     for name, (N, K) in shapes.items():
         w = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
-        for M in list(graph_buckets(a.max_bs)) + [m for m in a.prefill_m if name != "lm_head"]:
+        ms = [m for m in graph_buckets(a.max_bs) if m >= a.min_bs]
+        for M in ms + [m for m in a.prefill_m if name != "lm_head"]:
             x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
             F.linear(x, w)
             torch.cuda.synchronize()
