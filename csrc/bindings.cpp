@@ -263,19 +263,26 @@ void moe_align(Tensor sorted_ids, Tensor block_expert, Tensor meta, Tensor topk_
 }
 
 void moe_gemm(Tensor C, Tensor A, Tensor W, Tensor sorted_ids, Tensor block_expert, Tensor meta,
-              int64_t npairs, int64_t topk, int64_t bm, bool gather, bool scatter) {
+              int64_t npairs, int64_t topk, int64_t bm, bool gather, bool scatter, int64_t splitk) {
   check_gpu(A, "A");
   c10::hip::HIPGuardMasqueradingAsCUDA g(A.device());
   TORCH_CHECK(bm == 64 || bm == 128, "row block 64 or 128");
   TORCH_CHECK(W.dim() == 3 && W.is_contiguous(), "W [E, N, K] contiguous");
-  TORCH_CHECK(A.scalar_type() == W.scalar_type() && C.scalar_type() == W.scalar_type(),
-              "A, W, C share a dtype");
+  TORCH_CHECK(splitk >= 1 && splitk <= 16, "1 <= splitk <= 16");
+  TORCH_CHECK(splitk == 1 || (scatter && !gather), "split-K only for the scattering second GEMM");
+  TORCH_CHECK(A.scalar_type() == W.scalar_type() &&
+              C.scalar_type() == (splitk > 1 ? at::kFloat : W.scalar_type()),
+              "A, W share a dtype; C too (fp32 split-K slices when splitk > 1)");
   TORCH_CHECK(W.scalar_type() == at::kBFloat16 || W.scalar_type() == at::kHalf, "bf16 / fp16");
   const int64_t N = W.size(1), K = W.size(2), rows = sorted_ids.numel();
   TORCH_CHECK(N % kgc::moe_block_n() == 0 && K % kgc::moe_block_k() == 0,
               "grouped GEMM needs N % 128 == 0 and K % 64 == 0");
   TORCH_CHECK(A.dim() == 2 && A.size(1) == K && A.stride(1) == 1 && A.stride(0) % 8 == 0, "A [*, K]");
-  TORCH_CHECK(C.dim() == 2 && C.size(1) == N && C.stride(1) == 1 && C.stride(0) % 8 == 0, "C [*, N]");
+  // split-K: C [S, rows, N] contiguous fp32 slices; else C [*, N]
+  const Tensor C2 = splitk > 1 ? C.select(0, 0) : C;
+  TORCH_CHECK(splitk == 1 || (C.dim() == 3 && C.size(0) == splitk && C.is_contiguous()),
+              "split-K output: contiguous fp32 [splitk, rows, N]");
+  TORCH_CHECK(C2.dim() == 2 && C2.size(1) == N && C2.stride(1) == 1 && C2.stride(0) % 8 == 0, "C [*, N]");
   TORCH_CHECK(rows % bm == 0 && block_expert.numel() >= rows / bm, "row blocks");
   // every row index the kernel can touch must exist
   if (gather) {
@@ -284,15 +291,16 @@ void moe_gemm(Tensor C, Tensor A, Tensor W, Tensor sorted_ids, Tensor block_expe
     TORCH_CHECK(A.size(0) >= rows, "A must hold every padded row");
   }
   if (scatter) {
-    TORCH_CHECK(C.size(0) >= npairs, "C must hold every pair row");
+    TORCH_CHECK(C2.size(0) >= npairs, "C must hold every pair row");
   } else {
-    TORCH_CHECK(C.size(0) >= rows, "C must hold every padded row");
+    TORCH_CHECK(C2.size(0) >= rows, "C must hold every padded row");
   }
   if (rows == 0) return;
   kgc::launch_moe_gemm(dt_code(W), (int)bm, C.data_ptr(), A.data_ptr(), W.data_ptr(),
                        sorted_ids.data_ptr<int>(), block_expert.data_ptr<int>(), meta.data_ptr<int>(),
-                       (int)npairs, (int)topk, (int)N, (int)K, A.stride(0), C.stride(0),
-                       (int)(rows / bm), gather, scatter, stream());
+                       (int)npairs, (int)topk, (int)N, (int)K, A.stride(0), C2.stride(0),
+                       (int)(rows / bm), gather, scatter, (int)splitk,
+                       splitk > 1 ? C.stride(0) : 0, stream());
 }
 
 void moe_combine(Tensor out, Tensor y, Tensor topk_w) {
@@ -300,12 +308,17 @@ void moe_combine(Tensor out, Tensor y, Tensor topk_w) {
   c10::hip::HIPGuardMasqueradingAsCUDA g(y.device());
   const int64_t T = out.size(0), H = out.size(1), k = topk_w.size(-1);
   TORCH_CHECK(out.is_contiguous() && y.is_contiguous() && H % 8 == 0, "contiguous, H % 8 == 0");
-  TORCH_CHECK(y.numel() >= T * k * H && topk_w.numel() == T * k && topk_w.scalar_type() == at::kFloat,
-              "y [T*k, H], topk_w fp32 [T, k]");
+  // y: [T*k, H] in out's dtype, or fp32 split-K slices [S, rows >= T*k, H]
+  const bool slices = y.dim() == 3;
+  TORCH_CHECK(slices ? (y.scalar_type() == at::kFloat && y.size(2) == H && y.size(1) >= T * k)
+                     : (y.scalar_type() == out.scalar_type() && y.numel() >= T * k * H),
+              "y [T*k, H] or fp32 [S, >= T*k, H]");
+  TORCH_CHECK(topk_w.numel() == T * k && topk_w.scalar_type() == at::kFloat, "topk_w fp32 [T, k]");
   TORCH_CHECK(T <= 65535, "at most 65535 tokens per call");
   if (T == 0) return;
   kgc::launch_moe_combine(dt_code(out), out.data_ptr(), y.data_ptr(), topk_w.data_ptr<float>(),
-                          (int)T, (int)k, (int)H, stream());
+                          (int)T, (int)k, (int)H, slices ? (int)y.size(0) : 1,
+                          slices ? y.stride(0) : 0, stream());
 }
 
 // ---- K12 xGMI all-reduce: IPC buffers are raw device pointers carried as int64
@@ -409,7 +422,7 @@ TORCH_LIBRARY(kgc, m) {
   m.def("moe_align(Tensor(a!) sorted_ids, Tensor(b!) block_expert, Tensor(c!) meta, "
         "Tensor topk_ids, int e0, int E_local, int bm) -> ()");
   m.def("moe_gemm(Tensor(a!) C, Tensor A, Tensor W, Tensor sorted_ids, Tensor block_expert, "
-        "Tensor meta, int npairs, int topk, int bm, bool gather, bool scatter) -> ()");
+        "Tensor meta, int npairs, int topk, int bm, bool gather, bool scatter, int splitk=1) -> ()");
   m.def("moe_combine(Tensor(a!) out, Tensor y, Tensor topk_w) -> ()");
   m.def("ar_signal_bytes() -> int", &ar_signal_bytes);
   m.def("ar_alloc(int bytes) -> int", &ar_alloc);

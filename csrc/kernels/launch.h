@@ -50,12 +50,13 @@ void launch_moe_route(int dtype, const void* logits, int64_t stride, int ntok, i
                       bool renorm, float* topk_w, int* topk_ids, hipStream_t s);
 void launch_moe_align(const int* topk_ids, int npairs, int e0, int E_local, int bm, int max_rows,
                       int* sorted_ids, int* block_expert, int* meta, hipStream_t s);
+// splitk > 1 (scatter only): C is S fp32 slices of slice_stride elements each
 void launch_moe_gemm(int dtype, int bm, void* C, const void* A, const void* W,
                      const int* sorted_ids, const int* block_expert, const int* meta, int npairs,
                      int topk, int N, int K, int64_t lda, int64_t ldc, int max_mblocks,
-                     bool gather, bool scatter, hipStream_t s);
+                     bool gather, bool scatter, int splitk, int64_t slice_stride, hipStream_t s);
 void launch_moe_combine(int dtype, void* out, const void* y, const float* topk_w, int ntok, int k,
-                        int H, hipStream_t s);
+                        int H, int splitk, int64_t slice_stride, hipStream_t s);
 
 // K12 xGMI all-reduce: per-rank [signal | data parity 0 | data parity 1] IPC buffers.
 struct ArPtrs {

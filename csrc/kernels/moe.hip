@@ -113,12 +113,16 @@ __device__ __forceinline__ int mg_swz(int row, int chunk) {   // 16-B chunk inde
 
 // GATHER: A row r = x[sorted_ids[r] / topk]  (else A row r = A[r]);
 // SCATTER: C row sorted_ids[r] (skip padding)  (else C row r).
-template <typename T, int BM, bool GATHER, bool SCATTER>
+// PARTIAL (split-K, with SCATTER): grid z = S slices of K; slice z writes its fp32 sum
+// to Cf[z][row][:] and moe_combine adds the S slices.  At decode sizes the down
+// projection has only (experts x N/128) = 256 workgroups, each walking K = 14336 alone;
+// splitting K 4 ways fills the chip.
+template <typename T, int BM, bool GATHER, bool SCATTER, bool PARTIAL>
 __global__ __launch_bounds__(MG_THREADS, 2) void moe_gemm_kernel(
-    T* __restrict__ C, const T* __restrict__ A, const T* __restrict__ W,
+    void* __restrict__ Cv, const T* __restrict__ A, const T* __restrict__ W,
     const int* __restrict__ sorted_ids, const int* __restrict__ block_expert,
     const int* __restrict__ meta, int npairs, int topk, int N, int K, int64_t lda,
-    int64_t ldc) {
+    int64_t ldc, int64_t slice_stride) {
   const int mb = blockIdx.x, nb = blockIdx.y;
   if (mb >= meta[0]) return;
   const int e = block_expert[mb];
@@ -170,12 +174,14 @@ __global__ __launch_bounds__(MG_THREADS, 2) void moe_gemm_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = K / MG_BK;
-  gload(0);
+  const int nk_all = K / MG_BK;
+  const int kb0 = (int)((int64_t)nk_all * blockIdx.z / gridDim.z);
+  const int nk = (int)((int64_t)nk_all * (blockIdx.z + 1) / gridDim.z);
+  gload(kb0);
   lstore(0);
   __syncthreads();
-  for (int kb = 0; kb < nk; ++kb) {
-    const int buf = kb & 1;
+  for (int kb = kb0; kb < nk; ++kb) {
+    const int buf = (kb - kb0) & 1;
     if (kb + 1 < nk) gload(kb + 1);
 #pragma unroll
     for (int ks = 0; ks < MG_BK / 32; ++ks) {
@@ -207,29 +213,52 @@ __global__ __launch_bounds__(MG_THREADS, 2) void moe_gemm_kernel(
         if (p >= npairs) continue;
         crow = p;
       }
-      T* crow_ptr = C + crow * ldc + (int64_t)nb * MG_BN + wn * 64 + r16;
+      const int64_t off = crow * ldc + (int64_t)nb * MG_BN + wn * 64 + r16;
+      if constexpr (PARTIAL) {
+        float* cp = reinterpret_cast<float*>(Cv) + blockIdx.z * slice_stride + off;
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) crow_ptr[nt * 16] = from_f<T>(acc[mt][nt][i]);
+        for (int nt = 0; nt < 4; ++nt) cp[nt * 16] = acc[mt][nt][i];
+      } else {
+        T* cp = reinterpret_cast<T*>(Cv) + off;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) cp[nt * 16] = from_f<T>(acc[mt][nt][i]);
+      }
     }
   }
 }
 
 // ---------------------------------------------------------------------------- combine
+// y: [T*k, H] in T, or (S > 0) S fp32 split-K slices [S][T*k, H] summed here.
 template <typename T>
 __global__ __launch_bounds__(256) void moe_combine_kernel(T* __restrict__ out,
-                                                          const T* __restrict__ y,
+                                                          const void* __restrict__ y,
                                                           const float* __restrict__ topk_w,
-                                                          int k, int H) {
+                                                          int k, int H, int S,
+                                                          int64_t slice_stride) {
   const int t = blockIdx.y;
   const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
   if (c >= H) return;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int j = 0; j < k; ++j) {
     const float w = topk_w[(int64_t)t * k + j];
-    Pack8<T> v;
-    v.u = *reinterpret_cast<const u32x4*>(y + ((int64_t)t * k + j) * H + c);
+    const int64_t row = ((int64_t)t * k + j) * H + c;
+    if (S == 0) {
+      Pack8<T> v;
+      v.u = *reinterpret_cast<const u32x4*>(reinterpret_cast<const T*>(y) + row);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) acc[q] += w * to_f<T>(v.h[q]);
+      for (int q = 0; q < 8; ++q) acc[q] += w * to_f<T>(v.h[q]);
+    } else {
+      for (int z = 0; z < S; ++z) {
+        const float* src = reinterpret_cast<const float*>(y) + z * slice_stride + row;
+        const f32x4 a = *reinterpret_cast<const f32x4*>(src);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(src + 4);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc[q] += w * a[q];
+          acc[4 + q] += w * b[q];
+        }
+      }
+    }
   }
   Pack8<T> o;
 #pragma unroll
@@ -265,16 +294,18 @@ template <typename T, int BM>
 static void moe_gemm_bm(void* C, const void* A, const void* W, const int* sorted_ids,
                         const int* block_expert, const int* meta, int npairs, int topk, int N,
                         int K, int64_t lda, int64_t ldc, int max_mblocks, bool gather,
-                        bool scatter, hipStream_t s) {
-  const dim3 grid(max_mblocks, N / MG_BN);
-#define MG_LAUNCH(G, S)                                                                      \
-  moe_gemm_kernel<T, BM, G, S><<<grid, MG_THREADS, 0, s>>>((T*)C, (const T*)A, (const T*)W,   \
-                                                           sorted_ids, block_expert, meta,    \
-                                                           npairs, topk, N, K, lda, ldc)
-  if (gather && !scatter) MG_LAUNCH(true, false);
-  else if (!gather && scatter) MG_LAUNCH(false, true);
-  else if (gather && scatter) MG_LAUNCH(true, true);
-  else MG_LAUNCH(false, false);
+                        bool scatter, int splitk, int64_t slice_stride, hipStream_t s) {
+  const dim3 grid(max_mblocks, N / MG_BN, splitk);
+#define MG_LAUNCH(G, S, P)                                                                   \
+  moe_gemm_kernel<T, BM, G, S, P><<<grid, MG_THREADS, 0, s>>>(C, (const T*)A, (const T*)W,   \
+                                                              sorted_ids, block_expert, meta, \
+                                                              npairs, topk, N, K, lda, ldc,   \
+                                                              slice_stride)
+  if (splitk > 1) MG_LAUNCH(false, true, true);          // host-checked: scatter, !gather
+  else if (gather && !scatter) MG_LAUNCH(true, false, false);
+  else if (!gather && scatter) MG_LAUNCH(false, true, false);
+  else if (gather && scatter) MG_LAUNCH(true, true, false);
+  else MG_LAUNCH(false, false, false);
 #undef MG_LAUNCH
 }
 
@@ -282,34 +313,35 @@ template <typename T>
 static void moe_gemm_t(int bm, void* C, const void* A, const void* W, const int* sorted_ids,
                        const int* block_expert, const int* meta, int npairs, int topk, int N,
                        int K, int64_t lda, int64_t ldc, int max_mblocks, bool gather,
-                       bool scatter, hipStream_t s) {
+                       bool scatter, int splitk, int64_t slice_stride, hipStream_t s) {
   if (bm == 128)
     moe_gemm_bm<T, 128>(C, A, W, sorted_ids, block_expert, meta, npairs, topk, N, K, lda, ldc,
-                        max_mblocks, gather, scatter, s);
+                        max_mblocks, gather, scatter, splitk, slice_stride, s);
   else
     moe_gemm_bm<T, 64>(C, A, W, sorted_ids, block_expert, meta, npairs, topk, N, K, lda, ldc,
-                       max_mblocks, gather, scatter, s);
+                       max_mblocks, gather, scatter, splitk, slice_stride, s);
 }
 
 void launch_moe_gemm(int dtype, int bm, void* C, const void* A, const void* W,
                      const int* sorted_ids, const int* block_expert, const int* meta, int npairs,
                      int topk, int N, int K, int64_t lda, int64_t ldc, int max_mblocks,
-                     bool gather, bool scatter, hipStream_t s) {
+                     bool gather, bool scatter, int splitk, int64_t slice_stride, hipStream_t s) {
   if (dtype == DT_BF16)
     moe_gemm_t<bf16>(bm, C, A, W, sorted_ids, block_expert, meta, npairs, topk, N, K, lda, ldc,
-                     max_mblocks, gather, scatter, s);
+                     max_mblocks, gather, scatter, splitk, slice_stride, s);
   else
     moe_gemm_t<f16>(bm, C, A, W, sorted_ids, block_expert, meta, npairs, topk, N, K, lda, ldc,
-                    max_mblocks, gather, scatter, s);
+                    max_mblocks, gather, scatter, splitk, slice_stride, s);
 }
 
 void launch_moe_combine(int dtype, void* out, const void* y, const float* topk_w, int ntok, int k,
-                        int H, hipStream_t s) {
+                        int H, int splitk, int64_t slice_stride, hipStream_t s) {
   const dim3 grid((H / 8 + 255) / 256, ntok);
+  const int S = splitk > 1 ? splitk : 0;
   if (dtype == DT_BF16)
-    moe_combine_kernel<bf16><<<grid, 256, 0, s>>>((bf16*)out, (const bf16*)y, topk_w, k, H);
+    moe_combine_kernel<bf16><<<grid, 256, 0, s>>>((bf16*)out, y, topk_w, k, H, S, slice_stride);
   else
-    moe_combine_kernel<f16><<<grid, 256, 0, s>>>((f16*)out, (const f16*)y, topk_w, k, H);
+    moe_combine_kernel<f16><<<grid, 256, 0, s>>>((f16*)out, y, topk_w, k, H, S, slice_stride);
 }
 
 }  // namespace kgc

@@ -242,6 +242,19 @@ def moe_topk_softmax(router_logits: torch.Tensor, k: int, renormalize: bool = Tr
     return w, ids
 
 
+def moe_splitk(npairs: int, E: int, N: int, K: int, bm: int) -> int:
+    """K-slices for the down projection: enough workgroups to fill 256 CUs twice over,
+    each slice still >= 16 K-tiles of 64.  The row-block count is bounded without a host
+    sync (at most npairs/bm + E blocks carry rows)."""
+    if os.environ.get("KGC_MOE_SPLITK") is not None:
+        return max(1, int(os.environ["KGC_MOE_SPLITK"]))
+    wgs = min((npairs + bm - 1) // bm + E, npairs) * (N // 128)
+    S = 1
+    while S < 8 and wgs * S < 1024 and K // 64 // (2 * S) >= 16:
+        S *= 2
+    return S
+
+
 def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
               topk_ids: torch.Tensor, expert_offset: int = 0,
               all_local: bool = True) -> torch.Tensor:
@@ -268,8 +281,13 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     k.moe_gemm(inter, x.contiguous(), w13, sorted_ids, block_expert, meta, npairs, topk, bm,
                True, False)
     act = silu_mul(inter)
-    y = (torch.empty if all_local else torch.zeros)(npairs, H, dtype=x.dtype, device=dev)
-    k.moe_gemm(y, act, w2, sorted_ids, block_expert, meta, npairs, topk, bm, False, True)
+    S = moe_splitk(npairs, E, H, w2.shape[2], bm)
+    alloc = torch.empty if all_local else torch.zeros   # EP: pairs of remote experts add 0
+    if S > 1:
+        y = alloc(S, npairs, H, dtype=torch.float32, device=dev)
+    else:
+        y = alloc(npairs, H, dtype=x.dtype, device=dev)
+    k.moe_gemm(y, act, w2, sorted_ids, block_expert, meta, npairs, topk, bm, False, True, S)
     out = torch.empty(T, H, dtype=x.dtype, device=dev)
     k.moe_combine(out, y, topk_w.contiguous().float())
     return out

@@ -232,6 +232,20 @@ def test_fused_moe_expert_subset(gpu):
     torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(torch.bfloat16))
 
 
+@pytest.mark.parametrize("S", [1, 3, 8])
+@pytest.mark.parametrize("T,all_local", [(5, True), (300, True), (40, False)])
+def test_fused_moe_splitk(gpu, monkeypatch, S, T, all_local):
+    """Down projection split over S K-slices (fp32 slices summed in moe_combine); S = 3
+    leaves uneven slices of the 16 K-tiles."""
+    monkeypatch.setenv("KGC_MOE_SPLITK", str(S))
+    x, w13, w2, tw, tid = _moe_case(torch.bfloat16, T, 8, 2, 256, 1024, gpu, seed=5)
+    lo = 0 if all_local else 2
+    out = ops.fused_moe(x, w13[lo:].contiguous(), w2[lo:].contiguous(), tw, tid,
+                        expert_offset=lo, all_local=all_local)
+    exp = ref.moe_mlp_local(x.cpu(), w13[lo:].cpu(), w2[lo:].cpu(), tw.cpu(), tid.cpu(), lo)
+    torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(torch.bfloat16))
+
+
 def test_fused_moe_graph_capture(gpu):
     """No host sync inside: the block captures into a hipGraph and replays with new routes."""
     x, w13, w2, tw, tid = _moe_case(torch.bfloat16, 64, 8, 2, 256, 256, gpu, seed=4)
