@@ -269,7 +269,7 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     E, I2 = w13.shape[0], w13.shape[1]
     topk = topk_ids.shape[1]
     npairs = T * topk
-    bm = 64 if npairs <= 40 * E else 128   # one row block per expert at decode sizes
+    bm = int(os.environ.get("KGC_MOE_BM", 0)) or (64 if npairs <= 40 * E else 128)
     rows = (npairs + E * (bm - 1) + bm - 1) // bm * bm
     dev = x.device
     sorted_ids = torch.empty(rows, dtype=torch.int32, device=dev)

@@ -46,6 +46,9 @@ def main():
     ap.add_argument("--ms", default="1,16,64,128,256,512,4096")
     ap.add_argument("--backend", default="hipblaslt")
     ap.add_argument("--table", default=None, help="TunableOp results CSV to apply (read-only)")
+    ap.add_argument("--copies", type=int, default=1,
+                    help="rotate over this many weight copies (>1: weights stream from HBM, "
+                         "not the 256 MB Infinity Cache, as in a decode step)")
     a = ap.parse_args()
     if a.backend != "hipblaslt":
         torch.backends.cuda.preferred_blas_library(a.backend)
@@ -57,16 +60,22 @@ def main():
     dev = torch.device("cuda")
     res = []
     for name, (N, K) in shapes(a.model).items():
-        w = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
+        ws = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) for _ in range(a.copies)]
         for M in [int(x) for x in a.ms.split(",")]:
             x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
-            t = bench(lambda: F.linear(x, w))
+
+            def run():
+                for w in ws:
+                    F.linear(x, w)
+            t = bench(run, iters=max(1, 50 // a.copies)) / a.copies
             row = {"shape": name, "M": M, "N": N, "K": K,
                    "backend": "tunableop-table" if a.table else a.backend,
                    "us": round(t * 1e6, 2), "w_TBps": round(N * K * 2 / t / 1e12, 2),
                    "TFLOPs": round(2 * M * N * K / t / 1e12, 1)}
             print(json.dumps(row), flush=True)
             res.append(row)
+        del ws
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":

@@ -45,8 +45,9 @@ def main():
         t_loop = timeit(lambda: grouped_expert_mlp(x, w13, w2, tw, tid))
         flops = 2 * T * a.k * 3 * a.H * a.I
         npairs = T * a.k
-        S = ops.moe_splitk(npairs, a.E, a.H, a.I, 64 if npairs <= 40 * a.E else 128)
-        print(json.dumps({"T": T, "splitk": S, "native_us": round(t_nat * 1e6, 1),
+        bm = int(os.environ.get("KGC_MOE_BM", 0)) or (64 if npairs <= 40 * a.E else 128)
+        S = ops.moe_splitk(npairs, a.E, a.H, a.I, bm)
+        print(json.dumps({"T": T, "bm": bm, "splitk": S, "native_us": round(t_nat * 1e6, 1),
                           "loop_us": round(t_loop * 1e6, 1),
                           "native_TFLOPs": round(flops / t_nat / 1e12, 1),
                           "native_w_TBps": round(wbytes / t_nat / 1e12, 2)}), flush=True)

@@ -62,6 +62,7 @@ def main():
             x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
             F.linear(x, w)
             torch.cuda.synchronize()
+            print(f"  {name} M={M}", flush=True)   # progress (a long silent run looks hung)
         print(f"tuned {name} N={N} K={K} for {len(graph_buckets(a.max_bs))} buckets", flush=True)
     print(out)   # TunableOp writes the results file at process exit
 
