@@ -361,7 +361,8 @@ void xgmi_allreduce(Tensor inout, std::vector<int64_t> data, std::vector<int64_t
 }
 
 void skinny_gemm(Tensor C, Tensor X, Tensor W, std::optional<Tensor> bias, int64_t mt,
-                 int64_t nt, int64_t nw, bool ntl) {
+                 int64_t nt, int64_t nw, bool ntl, int64_t epi, std::optional<Tensor> gamma,
+                 double eps) {
   check_gpu(X, "X");
   check_same_dev(X, W, "W");
   check_same_dev(X, C, "C");
@@ -391,9 +392,19 @@ void skinny_gemm(Tensor C, Tensor X, Tensor W, std::optional<Tensor> bias, int64
     check_same_dev(X, *bias, "bias");
     bp = bias->data_ptr();
   }
-  kgc::launch_skinny_gemm(dt_code(X), (int)mt, (int)nt, (int)nw, ntl, C.data_ptr(), X.data_ptr(),
-                          W.data_ptr(), bp, (int)M, (int)N, (int)K, X.stride(0), C.stride(0),
-                          stream());
+  TORCH_CHECK(epi >= 0 && epi <= 2, "kgc.skinny_gemm: epi in {0 plain, 1 norm, 2 accumulate}");
+  const void* gp = nullptr;
+  if (epi == 1) {
+    TORCH_CHECK(gamma.has_value() && gamma->is_contiguous() && gamma->numel() == K &&
+                gamma->scalar_type() == X.scalar_type(), "kgc.skinny_gemm: norm needs gamma [K]");
+    check_same_dev(X, *gamma, "gamma");
+    gp = gamma->data_ptr();
+  }
+  if (epi == 2)   // C is read and rewritten in place: it must not overlap the input rows
+    TORCH_CHECK(C.data_ptr() != X.data_ptr(), "kgc.skinny_gemm: accumulate target aliases X");
+  kgc::launch_skinny_gemm(dt_code(X), (int)mt, (int)nt, (int)nw, ntl, (int)epi, C.data_ptr(),
+                          X.data_ptr(), W.data_ptr(), bp, gp, (float)eps, (int)M, (int)N, (int)K,
+                          X.stride(0), C.stride(0), stream());
 }
 
 int64_t decode_partition_size() { return kgc::paged_decode_partition_size(); }
@@ -435,7 +446,7 @@ TORCH_LIBRARY(kgc, m) {
         "bool two_shot) -> ()");
   m.def("prefill_block_m() -> int", &prefill_block_m);
   m.def("skinny_gemm(Tensor(a!) C, Tensor X, Tensor W, Tensor? bias, int mt, int nt, int nw, "
-        "bool ntl) -> ()");
+        "bool ntl, int epi=0, Tensor? gamma=None, float eps=1e-6) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(kgc, CUDA, m) {

@@ -20,18 +20,34 @@
 // Shapes the kernel takes (checked on the host): N % (16*NT) == 0, K % (32*NW) == 0,
 // 16-byte aligned rows.  Which (M, N, K) run here and which on hipBLASLt is decided at
 // engine start by timing both on the model's own weights (ops/gemm.py).
+//
+// Fused epilogues for the decode layer at small M (the layer then runs no RMSNorm
+// kernel: 2 of its ~10 launches at the ~4.7 us small-kernel floor disappear):
+//   SK_NORM: X rows are RMS-normalised on the fly, C = rms(x)^-1 * ((x * gamma) W^T).
+//            Each lane squares the X elements it loads anyway; the per-row sums of
+//            squares meet in LDS with the partial products, and 1/rms scales the merged
+//            row (one factor per row, so it commutes with the K-sum).  ~15 VALU cycles
+//            per X element: only the one-m-tile (M <= 16) form is used by the model.
+//   SK_ACC:  C += X W^T (+ bias) -- the residual add of o_proj / down_proj.
 #include "common.h"
 #include "launch.h"
 
 namespace kgc {
 
-template <typename T, int MT, int NT, int NW, bool NTL>
+enum { SK_PLAIN = 0, SK_NORM = 1, SK_ACC = 2 };
+
+template <typename T, int MT, int NT, int NW, bool NTL, int EPI>
 __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
     T* __restrict__ C, const T* __restrict__ X, const T* __restrict__ W,
-    const T* __restrict__ bias, int M, int K, int64_t ldx, int64_t ldc) {
-  typedef typename Vec8<T>::type V8;
-  constexpr int U = (MT + NT) <= 2 ? 8 : 4;     // k-steps of loads in flight per batch
+    const T* __restrict__ bias, const T* __restrict__ gamma, float eps, int M, int K,
+    int64_t ldx, int64_t ldc) {
+  constexpr bool NORM = EPI == SK_NORM, ACC = EPI == SK_ACC;
+  // k-steps of loads in flight per batch (SK_NORM: gamma fragments ride along, so the
+  // batch is halved to keep the register sets -- and the waves per SIMD -- as they were)
+  constexpr int U = (!NORM && (MT + NT) <= 2) ? 8 : 4;
   __shared__ __attribute__((aligned(16))) float red[NW][MT][NT][64][4];
+  __shared__ float ssr[NORM ? NW : 1][MT][64];  // per-lane partial sums of squares
+  __shared__ float inv_s[16 * MT];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r16 = lane & 15, q4 = lane >> 4;
   const int64_t n0 = (int64_t)blockIdx.x * (16 * NT);
@@ -44,16 +60,37 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
   const T* xrow[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) xrow[mt] = X + (int64_t)min(16 * mt + r16, M - 1) * ldx + 8 * q4;
+  const T* grow = NORM ? gamma + 8 * q4 : nullptr;
 
   f32x4 acc[MT][NT];
+  float ss[MT];
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
+  for (int mt = 0; mt < MT; ++mt) {
+    ss[mt] = 0.f;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   auto ldw = [](const T* p) -> u32x4 {
     if constexpr (NTL) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
     else return *reinterpret_cast<const u32x4*>(p);
+  };
+  // one k-step of MFMAs; with NORM the X fragment is squared into ss and scaled by gamma
+  auto step = [&](const Pack8<T>* wf, const Pack8<T>* xf, const Pack8<T>& gf) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      Pack8<T> xv = xf[mt];
+      if constexpr (NORM) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float a = to_f<T>(xf[mt].h[j]);
+          ss[mt] += a * a;
+          xv.h[j] = from_f<T>(a * to_f<T>(gf.h[j]));
+        }
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(wf[nt].v, xv.v, acc[mt][nt]);
+    }
   };
 
   // Two register sets (A, B) of U k-steps each: batch b+1's loads are in flight while
@@ -61,7 +98,8 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
   // to two batches of W outstanding instead of draining to zero between batches.
   typedef Pack8<T> WSet[U][NT];
   typedef Pack8<T> XSet[U][MT];
-  auto load = [&](WSet& wf, XSet& xf, int k) {
+  typedef Pack8<T> GSet[NORM ? U : 1];
+  auto load = [&](WSet& wf, XSet& xf, GSet& gf, int k) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -71,52 +109,64 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
         xf[u][mt].u = *reinterpret_cast<const u32x4*>(xrow[mt] + k + 32 * u);
+    if constexpr (NORM) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) gf[u].u = *reinterpret_cast<const u32x4*>(grow + k + 32 * u);
+    }
   };
-  auto compute = [&](const WSet& wf, const XSet& xf) {
+  auto compute = [&](const WSet& wf, const XSet& xf, const GSet& gf) {
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-          acc[mt][nt] = mfma16x16x32(wf[u][nt].v, xf[u][mt].v, acc[mt][nt]);
+    for (int u = 0; u < U; ++u) step(wf[u], xf[u], gf[NORM ? u : 0]);
   };
   const int nb = (kend - kbeg) / (32 * U);
   int k = kbeg;
   WSet wa, wb;
   XSet xa, xb;
-  if (nb > 0) load(wa, xa, k);
+  GSet ga, gb;
+  if (nb > 0) load(wa, xa, ga, k);
   for (int b = 0; b < nb; b += 2) {
-    if (b + 1 < nb) load(wb, xb, k + 32 * U);
-    compute(wa, xa);
+    if (b + 1 < nb) load(wb, xb, gb, k + 32 * U);
+    compute(wa, xa, ga);
     if (b + 1 < nb) {
-      if (b + 2 < nb) load(wa, xa, k + 64 * U);
-      compute(wb, xb);
+      if (b + 2 < nb) load(wa, xa, ga, k + 64 * U);
+      compute(wb, xb, gb);
     }
     k += 64 * U;
   }
   k = kbeg + nb * 32 * U;
   for (; k < kend; k += 32) {     // K-range not a multiple of 32*U
-    Pack8<T> wf[NT], xf[MT];
+    Pack8<T> wf[NT], xf[MT], gf;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) wf[nt].u = ldw(wrow[nt] + k);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) xf[mt].u = *reinterpret_cast<const u32x4*>(xrow[mt] + k);
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma16x16x32(wf[nt].v, xf[mt].v, acc[mt][nt]);
+    if constexpr (NORM) gf.u = *reinterpret_cast<const u32x4*>(grow + k);
+    step(wf, xf, gf);
   }
 
   // ---- merge the NW K-slices: lane (r16, q4) of wave w holds C^T[16nt+4q4+i][16mt+r16]
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
+  for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
       *reinterpret_cast<f32x4*>(&red[wave][mt][nt][lane][0]) = acc[mt][nt];
+    if constexpr (NORM) ssr[wave][mt][lane] = ss[mt];
+  }
   __syncthreads();
   constexpr int TN = 16 * NT;
   const int rows = min(M, 16 * MT);
+  if constexpr (NORM) {
+    // row m's sum of squares: its 4 lanes (q4) in each of the NW waves
+    if (threadIdx.x < rows) {
+      const int m = threadIdx.x, mt = m >> 4, r = m & 15;
+      float t = 0.f;
+      for (int w = 0; w < NW; ++w)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t += ssr[w][mt][q * 16 + r];
+      inv_s[m] = rsqrtf(t / (float)K + eps);
+    }
+    __syncthreads();
+  }
   for (int e = threadIdx.x; e < rows * TN; e += NW * 64) {
     const int m = e / TN, n = e % TN;
     const int mt = m >> 4, nt = n >> 4, nn = n & 15;
@@ -124,49 +174,62 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
     float s = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) s += red[w][mt][nt][l][i];
+    if constexpr (NORM) s *= inv_s[m];
     if (bias != nullptr) s += to_f<T>(bias[n0 + n]);
-    C[(int64_t)m * ldc + n0 + n] = from_f<T>(s);
+    T* c = C + (int64_t)m * ldc + n0 + n;
+    if constexpr (ACC) s += to_f<T>(*c);
+    *c = from_f<T>(s);
   }
+}
+
+template <typename T, int MT, int NT, int NW, bool NTL>
+static void sk_launch(int epi, dim3 grid, hipStream_t s, void* C, const void* X, const void* W,
+                      const void* bias, const void* gamma, float eps, int M, int K,
+                      int64_t ldx, int64_t ldc) {
+#define SK_GO(E)                                                                              \
+  skinny_gemm_kernel<T, MT, NT, NW, NTL, E><<<grid, NW * 64, 0, s>>>(                        \
+      (T*)C, (const T*)X, (const T*)W, (const T*)bias, (const T*)gamma, eps, M, K, ldx, ldc)
+  if (epi == SK_NORM) SK_GO(SK_NORM);
+  else if (epi == SK_ACC) SK_GO(SK_ACC);
+  else SK_GO(SK_PLAIN);
+#undef SK_GO
 }
 
 template <typename T, int MT, int NT>
-static void skinny_nw(int nw, bool ntl, void* C, const void* X, const void* W, const void* bias,
-                      int M, int N, int K, int64_t ldx, int64_t ldc, hipStream_t s) {
+static void skinny_nw(int nw, bool ntl, int epi, void* C, const void* X, const void* W,
+                      const void* bias, const void* gamma, float eps, int M, int N, int K,
+                      int64_t ldx, int64_t ldc, hipStream_t s) {
   const dim3 grid(N / (16 * NT));
-#define SK_LAUNCH(NW_, NTL_)                                                                  \
-  skinny_gemm_kernel<T, MT, NT, NW_, NTL_><<<grid, NW_ * 64, 0, s>>>(                        \
-      (T*)C, (const T*)X, (const T*)W, (const T*)bias, M, K, ldx, ldc)
-  if (nw == 16) {
-    if (ntl) SK_LAUNCH(16, true); else SK_LAUNCH(16, false);
-  } else if (nw == 8) {
-    if (ntl) SK_LAUNCH(8, true); else SK_LAUNCH(8, false);
-  } else {
-    if (ntl) SK_LAUNCH(4, true); else SK_LAUNCH(4, false);
-  }
-#undef SK_LAUNCH
+#define SK_NW(NW_)                                                                            \
+  if (ntl) sk_launch<T, MT, NT, NW_, true>(epi, grid, s, C, X, W, bias, gamma, eps, M, K, ldx, ldc); \
+  else sk_launch<T, MT, NT, NW_, false>(epi, grid, s, C, X, W, bias, gamma, eps, M, K, ldx, ldc)
+  if (nw == 16) { SK_NW(16); }
+  else if (nw == 8) { SK_NW(8); }
+  else { SK_NW(4); }
+#undef SK_NW
 }
 
 template <typename T>
-static void skinny_t(int mt, int nt, int nw, bool ntl, void* C, const void* X, const void* W,
-                     const void* bias, int M, int N, int K, int64_t ldx, int64_t ldc,
-                     hipStream_t s) {
+static void skinny_t(int mt, int nt, int nw, bool ntl, int epi, void* C, const void* X,
+                     const void* W, const void* bias, const void* gamma, float eps, int M, int N,
+                     int K, int64_t ldx, int64_t ldc, hipStream_t s) {
 #define SK_MT(MT_)                                                                            \
-  if (nt == 2) skinny_nw<T, MT_, 2>(nw, ntl, C, X, W, bias, M, N, K, ldx, ldc, s);           \
-  else skinny_nw<T, MT_, 1>(nw, ntl, C, X, W, bias, M, N, K, ldx, ldc, s)
+  if (nt == 2) skinny_nw<T, MT_, 2>(nw, ntl, epi, C, X, W, bias, gamma, eps, M, N, K, ldx, ldc, s); \
+  else skinny_nw<T, MT_, 1>(nw, ntl, epi, C, X, W, bias, gamma, eps, M, N, K, ldx, ldc, s)
   if (mt == 1) { SK_MT(1); }
   else if (mt == 2) { SK_MT(2); }
   else { SK_MT(4); }
 #undef SK_MT
 }
 
-void launch_skinny_gemm(int dtype, int mt, int nt, int nw, bool ntl, void* C, const void* X,
-                        const void* W, const void* bias, int M, int N, int K, int64_t ldx,
-                        int64_t ldc, hipStream_t s) {
+void launch_skinny_gemm(int dtype, int mt, int nt, int nw, bool ntl, int epi, void* C,
+                        const void* X, const void* W, const void* bias, const void* gamma,
+                        float eps, int M, int N, int K, int64_t ldx, int64_t ldc, hipStream_t s) {
   if (M == 0 || N == 0) return;
   if (dtype == DT_BF16)
-    skinny_t<bf16>(mt, nt, nw, ntl, C, X, W, bias, M, N, K, ldx, ldc, s);
+    skinny_t<bf16>(mt, nt, nw, ntl, epi, C, X, W, bias, gamma, eps, M, N, K, ldx, ldc, s);
   else
-    skinny_t<f16>(mt, nt, nw, ntl, C, X, W, bias, M, N, K, ldx, ldc, s);
+    skinny_t<f16>(mt, nt, nw, ntl, epi, C, X, W, bias, gamma, eps, M, N, K, ldx, ldc, s);
 }
 
 }  // namespace kgc

@@ -39,9 +39,10 @@ void launch_sample(int dtype, int64_t* out, uint64_t* partial, const void* logit
                    const float* top_p, const int64_t* seeds, hipStream_t s);
 
 // K9 skinny (small-M decode) GEMM: C[M, N] = X[M, K] . W[N, K]^T (+ bias), M <= 16*mt.
-void launch_skinny_gemm(int dtype, int mt, int nt, int nw, bool ntl, void* C, const void* X,
-                        const void* W, const void* bias, int M, int N, int K, int64_t ldx,
-                        int64_t ldc, hipStream_t s);
+// epi: 0 plain, 1 RMS-normalise X rows on the fly (gamma [K], eps), 2 accumulate into C
+void launch_skinny_gemm(int dtype, int mt, int nt, int nw, bool ntl, int epi, void* C,
+                        const void* X, const void* W, const void* bias, const void* gamma,
+                        float eps, int M, int N, int K, int64_t ldx, int64_t ldc, hipStream_t s);
 
 // K13/K14 MoE: routing, expert bucketing, grouped MFMA GEMM, weighted combine.
 int moe_block_n();

@@ -455,8 +455,9 @@ class ModelRunner:
             # K9: per decode bucket and weight shape, hipBLASLt or the skinny GEMM --
             # whichever measured faster on this model's weights (ops/gemm.py)
             from ..ops import gemm
+            ns = getattr(self.model, "fused_norm_shapes", lambda: set())()
             gemm.tune_skinny([p for p in self.model.parameters() if p.dim() == 2],
-                             self.buckets)
+                             self.buckets, norm_shapes=ns)
         if (not self.use_graphs or not (self.model.first and self.model.last)
                 or not getattr(self.model, "graph_safe", True)):
             self.use_graphs = False

@@ -64,14 +64,17 @@ class LlamaAttention(nn.Module):
         self.attn = PagedAttention(self.nq, self.nkv, cfg.head_dim, layer_idx)
 
     def forward(self, positions, x, ctx: ForwardContext):
-        qkv = self.qkv_proj(x)
+        return self.o_proj(self.attend(positions, self.qkv_proj(x), ctx))
+
+    def attend(self, positions, qkv, ctx: ForwardContext):
+        """RoPE + KV-cache write + paged attention on a QKV projection -> [T, nq*d]."""
         kc, vc = ctx.kv_caches[self.attn.layer_idx]
         q = ops.rope_kv_write(qkv, positions, ctx.cos_sin, kc, vc, ctx.attn.slot_mapping,
                               self.nq, self.nkv, self.cfg.head_dim,
                               None if self.q_norm is None else self.q_norm.weight,
                               None if self.k_norm is None else self.k_norm.weight,
                               self.cfg.rms_eps, k_scale=ctx.k_scale, v_scale=ctx.v_scale)
-        return self.o_proj(self.attn(q, ctx))
+        return self.attn(q, ctx)
 
 
 class LlamaMLP(nn.Module):
@@ -142,6 +145,10 @@ class LlamaForCausalLM(nn.Module):
         """First stage: input_ids -> ...; later stages take (hidden, residual) from the
         previous stage.  Returns the final-normed hidden on the last stage, else
         (hidden, residual) for the next stage."""
+        if hidden is None and residual is None:
+            cfgs = self._fused_cfgs(input_ids.shape[0])
+            if cfgs is not None:
+                return self._forward_fused(input_ids, positions, ctx, cfgs)
         x = self.embed_tokens(input_ids) if self.first else hidden
         for layer in self.layers:
             x, residual = layer(positions, x, residual, ctx)
@@ -151,6 +158,61 @@ class LlamaForCausalLM(nn.Module):
             return self.norm(x)
         x, _ = self.norm(x, residual)
         return x
+
+    # ------------------------------------------------------------------ fused small-M decode
+    def _fused_cfgs(self, M: int):
+        """K9 configurations (qkv, o, gate_up, down) when this step runs the fused layer:
+        one GPU (TP = PP = 1), a dense MLP, and start-up tuning measured the fused layer
+        faster at this M (ops/gemm.py fused_norm_plan).  None: the regular path runs."""
+        if (M > 16 or not self._fusable or not self.layers
+                or not self.layers[0].input_layernorm.weight.is_cuda):
+            return None
+        from ..ops import gemm
+        norm_ws, acc_ws = self._fused_weights()
+        p = gemm.fused_norm_plan(M, [tuple(w.shape) for w in norm_ws],
+                                 [tuple(w.shape) for w in acc_ws])
+        if p is None:
+            return None
+        (c_qkv, c_gu), (c_o, c_dn) = p
+        return [c_qkv, c_o, c_gu, c_dn]
+
+    def _fused_weights(self):
+        l0 = self.layers[0]
+        return ((l0.self_attn.qkv_proj.weight, l0.mlp.gate_up_proj.weight),
+                (l0.self_attn.o_proj.weight, l0.mlp.down_proj.weight))
+
+    def fused_norm_shapes(self) -> set:
+        """(N, K) of the GEMMs whose input RMSNorm the fused layer absorbs (tuned at start)."""
+        if not self._fusable or not self.layers:
+            return set()
+        return {tuple(w.shape) for w in self._fused_weights()[0]}
+
+    @property
+    def _fusable(self) -> bool:
+        s = get_state()
+        return (self.first and self.last and s.tp_size == 1 and not self.cfg.is_moe
+                and ops.fused_small_m_enabled())
+
+    def _forward_fused(self, input_ids, positions, ctx, cfgs):
+        """The decoder at small M with the residual stream kept in one buffer: every
+        RMSNorm runs inside the GEMM that consumes it (K9 SK_NORM) and every residual add
+        inside the GEMM that produces it (K9 SK_ACC) -- 8 launches per layer instead of
+        10.  Same math as the regular path: residual += o; x = norm(residual) ..."""
+        from ..ops import gemm
+        c_qkv, c_o, c_gu, c_dn = cfgs
+        res = self.embed_tokens(input_ids)
+        for layer in self.layers:
+            at, mlp = layer.self_attn, layer.mlp
+            ln1, ln2 = layer.input_layernorm, layer.post_attention_layernorm
+            qkv = gemm.skinny_norm(res, at.qkv_proj.weight, at.qkv_proj.bias, ln1.weight,
+                                   ln1.eps, c_qkv)
+            gemm.skinny_accum(res, at.attend(positions, qkv, ctx), at.o_proj.weight,
+                              at.o_proj.bias, c_o)
+            gu = gemm.skinny_norm(res, mlp.gate_up_proj.weight, mlp.gate_up_proj.bias,
+                                  ln2.weight, ln2.eps, c_gu)
+            gemm.skinny_accum(res, ops.silu_mul(gu), mlp.down_proj.weight, mlp.down_proj.bias,
+                              c_dn)
+        return self.norm(res)
 
     def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
         return self.lm_head(hidden)

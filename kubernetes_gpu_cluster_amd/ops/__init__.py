@@ -49,6 +49,11 @@ def _gpu(t: torch.Tensor) -> bool:
     return t.is_cuda
 
 
+def fused_small_m_enabled() -> bool:
+    """KGC_FUSED_SMALL_M=0 turns off the fused small-batch decoder layer (models/llama.py)."""
+    return os.environ.get("KGC_FUSED_SMALL_M", "1") != "0"
+
+
 # ------------------------------------------------------------------ norms
 def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float,
              out: Optional[torch.Tensor] = None) -> torch.Tensor:

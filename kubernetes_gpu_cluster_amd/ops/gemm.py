@@ -25,6 +25,11 @@ _CONFIGS = [(mt, nt, nw, ntl) for mt in (1, 2, 4) for nt in (1, 2) for nw in (4,
             for ntl in (True, False)]
 
 _plan: dict[tuple[int, int, int], tuple[int, int, int, bool]] = {}
+# (M, N, K) -> (cfg, us) of the fastest SK_NORM variant, and (M, N, K) -> us of the path
+# the plain plan runs (hipBLASLt or skinny); (M, K) -> us of a separate rms_norm.
+_plan_norm: dict[tuple[int, int, int], tuple[tuple, float]] = {}
+_chosen_us: dict[tuple[int, int, int], float] = {}
+_rms_us: dict[tuple[int, int], float] = {}
 _enabled = os.environ.get("KGC_SKINNY_GEMM", "1") != "0"
 
 
@@ -51,7 +56,48 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return F.linear(x, w, bias)
 
 
+def skinny_cfg(M: int, N: int, K: int):
+    """The tuned skinny configuration for (M, N, K), or None where hipBLASLt runs."""
+    return _plan.get((M, N, K))
+
+
+def skinny_norm(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor],
+                gamma: torch.Tensor, eps: float, cfg) -> torch.Tensor:
+    """rms_norm(x) * gamma, then the GEMM, in one launch (K9 SK_NORM epilogue)."""
+    from . import _k
+    out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
+    _k().skinny_gemm(out, x, w, bias, *cfg, 1, gamma, eps)
+    return out
+
+
+def skinny_accum(out: torch.Tensor, x: torch.Tensor, w: torch.Tensor,
+                 bias: Optional[torch.Tensor], cfg) -> torch.Tensor:
+    """out += x W^T (+ bias) in one launch (K9 SK_ACC epilogue: the residual add)."""
+    from . import _k
+    _k().skinny_gemm(out, x, w, bias, *cfg, 2, None, 1e-6)
+    return out
+
+
+def fused_norm_plan(M: int, norm_shapes, acc_shapes):
+    """Configurations for a decoder layer whose RMSNorms run inside the GEMMs that
+    consume them (SK_NORM on ``norm_shapes``) and whose residual adds run in the GEMMs
+    that produce them (SK_ACC on ``acc_shapes``) -- or None unless tuning measured the
+    SK_NORM GEMMs to cost less than the plain GEMMs plus the separate norm launches."""
+    try:
+        norm = [_plan_norm[(M, N, K)] for N, K in norm_shapes]
+        acc = [_plan[(M, N, K)] for N, K in acc_shapes]
+        plain = sum(_chosen_us[(M, N, K)] + _rms_us[(M, K)] for N, K in norm_shapes)
+    except KeyError:
+        return None
+    if sum(t for _, t in norm) >= 0.98 * plain:
+        return None
+    return [c for c, _ in norm], acc
+
+
 def clear_plan() -> None:
+    _plan_norm.clear()
+    _chosen_us.clear()
+    _rms_us.clear()
     _plan.clear()
 
 
@@ -73,7 +119,7 @@ def _time(fn, reps: int) -> float:
 
 @torch.inference_mode()
 def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: float = 0.97,
-                reps: int = 3) -> dict:
+                reps: int = 3, norm_shapes=(), norm_max_m: int = 16) -> dict:
     """Time hipBLASLt against every skinny configuration for each weight shape and
     batch size M (decode buckets <= SKINNY_MAX_M) and record the skinny kernel where it
     is faster by more than ``1 - margin``.  Each timing sweeps ALL weights of the shape
@@ -112,9 +158,41 @@ def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: floa
             best = sk_cfg if sk_t < lib_t * margin else None
             n = len(ws)
             res[(M, N, K)] = (best, lib_t * 1e3 / n, sk_t * 1e3 / n, sk_cfg)
+            _chosen_us[(M, N, K)] = (sk_t if best is not None else lib_t) * 1e3 / n
             if best is not None:
                 _plan[(M, N, K)] = best
+            if (N, K) in norm_shapes and M <= norm_max_m:
+                _tune_norm(ws, x, out, M, N, K, reps)
             log.info("gemm M=%d N=%d K=%d: hipBLASLt %.1f us, skinny %s %.1f us -> %s", M, N, K,
                      lib_t * 1e3 / n, sk_cfg, sk_t * 1e3 / n, "skinny" if best else "hipBLASLt")
     log.info("skinny GEMM tuning: %d shapes in %.1f s", len(res), time.time() - t0)
     return res
+
+
+def _tune_norm(ws, x, out, M: int, N: int, K: int, reps: int) -> None:
+    """Time the SK_NORM variants (one m-tile) and a separate rms_norm launch at (M, K)."""
+    from . import _k, rms_norm
+    gamma = torch.ones(K, dtype=x.dtype, device=x.device)
+    best_t, best_cfg = float("inf"), None
+    for cfg in _CONFIGS:
+        if cfg[0] != 1 or not skinny_ok(M, N, K, cfg):
+            continue
+
+        def fn(cfg=cfg):
+            for w in ws:
+                _k().skinny_gemm(out, x, w, None, *cfg, 1, gamma, 1e-6)
+        t = _time(fn, reps)
+        if t < best_t:
+            best_t, best_cfg = t, cfg
+    if best_cfg is not None:
+        _plan_norm[(M, N, K)] = (best_cfg, best_t * 1e3 / len(ws))
+    if (M, K) not in _rms_us:
+        # inside a graph, as in the decode step: eager launches of a ~2 us kernel would
+        # time the host's launch rate instead
+        xn = torch.empty_like(x)
+        rms_norm(x, gamma, 1e-6, xn)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(32):
+                rms_norm(x, gamma, 1e-6, xn)
+        _rms_us[(M, K)] = _time(g.replay, reps) * 1e3 / 32

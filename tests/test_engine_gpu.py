@@ -44,6 +44,48 @@ def test_gpu_logits_match_hf(gpu, name):
         assert bool(ok.all()), (pos_err.max().item(), scale, cos.min().item())
 
 
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-qwen2", "tiny-qwen3"])
+def test_gpu_logits_match_hf_fused_small_m(gpu, name):
+    """The fused small-M decoder (norms inside the skinny GEMMs, residual adds in their
+    epilogues) against HF: prefill chunks of 13 and 7 tokens and 1-token decode steps
+    all take the fused path once the skinny plan covers every projection."""
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    cfg = PRESETS[name]
+    sd = full_state_dict_random(cfg, seed=3, std=0.05)
+    hf, _ = _hf_model(cfg, sd)
+    set_state(ParallelState(device=gpu))
+    model = build_model(cfg, torch.bfloat16, gpu)
+    model.load_weights(sd.items())
+    runner = ModelRunner(model, cfg, torch.bfloat16, gpu, block_size=16, max_model_len=256,
+                         max_num_seqs=4, token_budget=128, enforce_eager=True)
+    runner.init_kv_cache(48)
+    norm_ws, acc_ws = model._fused_weights()
+    gemm.clear_plan()
+    try:
+        for M in (13, 7, 1):      # a plan as if tuning had measured the fused layer faster
+            for w in norm_ws:
+                N, K = w.shape
+                gemm._plan_norm[(M, N, K)] = ((1, 1, 4, True), 1.0)
+                gemm._chosen_us[(M, N, K)] = 2.0
+                gemm._rms_us[(M, K)] = 1.0
+            for w in acc_ws:
+                gemm._plan[(M, *w.shape)] = (1, 1, 4, True)
+            assert model._fused_cfgs(M) is not None
+        g = torch.Generator().manual_seed(1)
+        prompt = torch.randint(3, cfg.vocab_size, (20,), generator=g).tolist()
+        extra = torch.randint(3, cfg.vocab_size, (4,), generator=g).tolist()
+        with torch.no_grad():
+            ref = hf(torch.tensor([prompt + extra])).logits[0].float()
+        got = _engine_logits(model, runner, prompt, [13, 7], extra).float().cpu()
+    finally:
+        gemm.clear_plan()
+    scale = ref.abs().max().item()
+    pos_err = (got - ref).abs().max(-1).values
+    cos = torch.nn.functional.cosine_similarity(got, ref, dim=-1)
+    assert bool(((pos_err < 0.03 * scale + 1e-3) & (cos > 0.999)).all()), \
+        (pos_err.max().item(), scale, cos.min().item())
+
+
 def _tiny_engine(**kw):
     PRESETS.setdefault("llama-3-8b-2l", PRESETS["llama-3-8b"].shrink(name="llama-3-8b-2l",
                                                                      num_layers=2))

@@ -373,6 +373,31 @@ def test_skinny_gemm_strided_x(gpu):
     torch.testing.assert_close(got.float().cpu(), exp, atol=3e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("M", [1, 5, 16])
+@pytest.mark.parametrize("nw", [4, 16])
+def test_skinny_gemm_norm_and_accumulate(gpu, M, nw):
+    """K9 epilogues: SK_NORM == rms_norm(x) * gamma then the GEMM (+ bias);
+    SK_ACC == C + x W^T (+ bias), in place."""
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    torch.manual_seed(M * 7 + nw)
+    K, N, eps = 2048, 512, 1e-5
+    x = torch.randn(M, K, dtype=torch.bfloat16, device=gpu) * 3
+    w = torch.randn(N, K, dtype=torch.bfloat16, device=gpu) * K ** -0.5
+    g = (torch.rand(K, device=gpu) + 0.5).to(torch.bfloat16)
+    b = torch.randn(N, dtype=torch.bfloat16, device=gpu)
+    cfg = (1, 2, nw, True)
+    xf, wf = x.float().cpu(), w.float().cpu()
+    xn = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * g.float().cpu()
+    got = gemm.skinny_norm(x, w, b, g, eps, cfg)
+    torch.testing.assert_close(got.float().cpu(), xn @ wf.t() + b.float().cpu(), atol=3e-2,
+                               rtol=2e-2)
+    c0 = torch.randn(M, N, dtype=torch.bfloat16, device=gpu)
+    exp = c0.float().cpu() + xf @ wf.t() + b.float().cpu()
+    c = c0.clone()
+    assert gemm.skinny_accum(c, x, w, b, cfg) is c
+    torch.testing.assert_close(c.float().cpu(), exp, atol=6e-2, rtol=2e-2)
+
+
 def test_linear_uses_tuned_plan(gpu):
     from kubernetes_gpu_cluster_amd.ops import gemm
     torch.manual_seed(4)
