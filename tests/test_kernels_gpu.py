@@ -114,6 +114,31 @@ def test_paged_decode(gpu, dt, d, nq, nkv, bs):
         torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(dt))
 
 
+def test_paged_decode_workspace_reuse(gpu):
+    """One static partials workspace serves launches of any Z (incl. an empty context),
+    eager or replayed from a graph."""
+    torch.manual_seed(13)
+    dt, d, nq, nkv, bs = torch.bfloat16, 128, 32, 8, 32
+    ctx = [1, 700, 2049, 64, 0, 333]
+    B = len(ctx)
+    kc, vc, bt = _fill_random_cache(B, [max(c, 1) for c in ctx], nkv, bs, d, dt, gpu)
+    q = torch.randn(B, nq, d, dtype=dt, device=gpu)
+    cl = torch.tensor(ctx, dtype=torch.int32, device=gpu)
+    ws = ops.decode_partials(B, nq, d, bt.shape[1], bs, gpu)
+    exp = ref.paged_attention_decode(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cl.cpu(), d ** -0.5)
+    for z in (7, 1, 16, 3, 16):
+        out = ops.paged_attention_decode(q, kc, vc, bt, cl, d ** -0.5, workspace=ws, grid_z=z)
+        torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(dt))
+    out = torch.empty_like(q)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ops.paged_attention_decode(q, kc, vc, bt, cl, d ** -0.5, workspace=ws, grid_z=5, out=out)
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(dt))
+
+
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("d,nq,nkv", [(128, 32, 8), (64, 4, 4), (128, 8, 1)])
 def test_prefill_attention(gpu, dt, d, nq, nkv):
