@@ -67,6 +67,11 @@ def _k9_plan() -> dict:
     return gemm.plan()
 
 
+def _splitk_plan() -> dict:
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    return gemm.splitk_plan()
+
+
 def run_wave(engine, args, wave: int, rank: int):
     from kubernetes_gpu_cluster_amd.engine.sequence import SamplingParams
     g = torch.Generator().manual_seed(1000 * wave + rank)
@@ -189,6 +194,7 @@ def main():
             "p50_tpot_ms": round(statistics.median(tpots) * 1e3, 3) if tpots else None,
             "engine_steps": steps,
             "k9_skinny_gemm_shapes": len(_k9_plan()),
+            "splitk_gemm_shapes": len(_splitk_plan()),
             "config": {"model": args.model, "global_batch": args.num_prompts * replicas,
                        "seq_len": args.input_len + args.output_len, "input_len": args.input_len,
                        "output_len": args.output_len,

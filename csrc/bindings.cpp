@@ -321,6 +321,40 @@ void moe_combine(Tensor out, Tensor y, Tensor topk_w) {
                           slices ? y.stride(0) : 0, stream());
 }
 
+// Dense split-K decode GEMM on the grouped-GEMM tiles (XCD-mapped K-slices) + its reduction.
+void dense_gemm_splitk(Tensor Cs, Tensor A, Tensor W, int64_t bm) {
+  check_gpu(A, "A");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(A.device());
+  TORCH_CHECK(bm == 64 || bm == 128, "row block 64 or 128");
+  TORCH_CHECK(W.dim() == 2 && W.is_contiguous(), "W [N, K] contiguous");
+  TORCH_CHECK(W.scalar_type() == at::kBFloat16 || W.scalar_type() == at::kHalf, "bf16 / fp16");
+  const int64_t N = W.size(0), K = W.size(1);
+  TORCH_CHECK(A.scalar_type() == W.scalar_type() && A.dim() == 2 && A.size(1) == K &&
+              A.stride(1) == 1 && A.stride(0) % 8 == 0, "A [M, K] in W's dtype");
+  const int64_t M = A.size(0);
+  TORCH_CHECK(N % kgc::moe_block_n() == 0 && K % kgc::moe_block_k() == 0, "N % 128, K % 64");
+  TORCH_CHECK(Cs.scalar_type() == at::kFloat && Cs.dim() == 3 && Cs.is_contiguous() &&
+              Cs.size(1) == M && Cs.size(2) == N, "Cs fp32 contiguous [S, M, N]");
+  const int64_t S = Cs.size(0);
+  TORCH_CHECK(S >= 1 && S <= 16 && K / kgc::moe_block_k() >= S, "1 <= S <= 16, S <= K / 64");
+  if (M == 0) return;
+  kgc::launch_dense_gemm_splitk(dt_code(W), (int)bm, Cs.data_ptr<float>(), A.data_ptr(),
+                                W.data_ptr(), (int)M, (int)N, (int)K, A.stride(0), (int)S,
+                                stream());
+}
+
+void splitk_reduce(Tensor out, Tensor Cs) {
+  check_gpu(Cs, "Cs");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(Cs.device());
+  TORCH_CHECK(Cs.scalar_type() == at::kFloat && Cs.dim() == 3 && Cs.is_contiguous(), "Cs fp32 [S, M, N]");
+  TORCH_CHECK(out.is_contiguous() && out.numel() == Cs.size(1) * Cs.size(2) && out.numel() % 8 == 0,
+              "out [M, N] contiguous, numel % 8 == 0");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kHalf, "bf16 / fp16");
+  if (out.numel() == 0) return;
+  kgc::launch_splitk_reduce(dt_code(out), out.data_ptr(), Cs.data_ptr<float>(), (int)Cs.size(0),
+                            out.numel(), Cs.stride(0), stream());
+}
+
 // ---- K12 xGMI all-reduce: IPC buffers are raw device pointers carried as int64
 int64_t ar_signal_bytes() { return (int64_t)kgc::allreduce_signal_bytes(); }
 int64_t ar_alloc(int64_t bytes) { return (int64_t)(intptr_t)kgc::ar_alloc(bytes); }
@@ -435,6 +469,8 @@ TORCH_LIBRARY(kgc, m) {
   m.def("moe_gemm(Tensor(a!) C, Tensor A, Tensor W, Tensor sorted_ids, Tensor block_expert, "
         "Tensor meta, int npairs, int topk, int bm, bool gather, bool scatter, int splitk=1) -> ()");
   m.def("moe_combine(Tensor(a!) out, Tensor y, Tensor topk_w) -> ()");
+  m.def("dense_gemm_splitk(Tensor(a!) Cs, Tensor A, Tensor W, int bm) -> ()");
+  m.def("splitk_reduce(Tensor(a!) out, Tensor Cs) -> ()");
   m.def("ar_signal_bytes() -> int", &ar_signal_bytes);
   m.def("ar_alloc(int bytes) -> int", &ar_alloc);
   m.def("ar_free(int ptr) -> ()", &ar_free);
@@ -462,5 +498,7 @@ TORCH_LIBRARY_IMPL(kgc, CUDA, m) {
   m.impl("moe_align", &moe_align);
   m.impl("moe_gemm", &moe_gemm);
   m.impl("moe_combine", &moe_combine);
+  m.impl("dense_gemm_splitk", &dense_gemm_splitk);
+  m.impl("splitk_reduce", &splitk_reduce);
   m.impl("skinny_gemm", &skinny_gemm);
 }

@@ -56,6 +56,11 @@ void launch_moe_gemm(int dtype, int bm, void* C, const void* A, const void* W,
                      const int* sorted_ids, const int* block_expert, const int* meta, int npairs,
                      int topk, int N, int K, int64_t lda, int64_t ldc, int max_mblocks,
                      bool gather, bool scatter, int splitk, int64_t slice_stride, hipStream_t s);
+// dense split-K decode GEMM: Cs [splitk, M, N] fp32 = A [M, K] x W [N, K]^T, XCD-mapped slices
+void launch_dense_gemm_splitk(int dtype, int bm, float* Cs, const void* A, const void* W, int M,
+                              int N, int K, int64_t lda, int splitk, hipStream_t s);
+void launch_splitk_reduce(int dtype, void* out, const float* Cs, int S, int64_t numel,
+                          int64_t slice_stride, hipStream_t s);
 void launch_moe_combine(int dtype, void* out, const void* y, const float* topk_w, int ntok, int k,
                         int H, int splitk, int64_t slice_stride, hipStream_t s);
 

@@ -117,16 +117,37 @@ __device__ __forceinline__ int mg_swz(int row, int chunk) {   // 16-B chunk inde
 // to Cf[z][row][:] and moe_combine adds the S slices.  At decode sizes the down
 // projection has only (experts x N/128) = 256 workgroups, each walking K = 14336 alone;
 // splitting K 4 ways fills the chip.
-template <typename T, int BM, bool GATHER, bool SCATTER, bool PARTIAL>
+// DENSE (dense split-K decode GEMM, one weight matrix, no row maps): a 1-D grid of
+// MB * NB * S workgroups, slice z = linear id % S.  Workgroups are dispatched round-robin
+// over the 8 XCDs, so with S = 8 every XCD owns one K-slice: its [M, K/8] activation slice
+// stays in that XCD's L2 for all N-tiles while the weights stream from HBM once, and the
+// M-blocks sharing an N-tile run back to back on the same XCD.
+template <typename T, int BM, bool GATHER, bool SCATTER, bool PARTIAL, bool DENSE = false>
 __global__ __launch_bounds__(MG_THREADS, 2) void moe_gemm_kernel(
     void* __restrict__ Cv, const T* __restrict__ A, const T* __restrict__ W,
     const int* __restrict__ sorted_ids, const int* __restrict__ block_expert,
     const int* __restrict__ meta, int npairs, int topk, int N, int K, int64_t lda,
-    int64_t ldc, int64_t slice_stride) {
-  const int mb = blockIdx.x, nb = blockIdx.y;
-  if (mb >= meta[0]) return;
-  const int e = block_expert[mb];
-  if (e < 0) return;
+    int64_t ldc, int64_t slice_stride, int dense_m) {
+  int mb, nb, z, S, e;
+  if constexpr (DENSE) {
+    // npairs = number of M-blocks, topk = number of K-slices (reused scalar args);
+    // rows >= dense_m of the last M-block load row dense_m - 1 and store nothing
+    S = topk;
+    const int L = blockIdx.x;
+    z = L % S;
+    const int j = L / S;
+    mb = j % npairs;
+    nb = j / npairs;
+    e = 0;
+  } else {
+    mb = blockIdx.x;
+    nb = blockIdx.y;
+    z = blockIdx.z;
+    S = gridDim.z;
+    if (mb >= meta[0]) return;
+    e = block_expert[mb];
+    if (e < 0) return;
+  }
   constexpr int AC = BM / 32;     // A chunks per thread; also 16-row M tiles per wave
   __shared__ u32x4 lds[2 * (BM + MG_BN) * (MG_BK / 8)];
   u32x4* As = lds;                                   // [2][BM * 8]
@@ -145,6 +166,8 @@ __global__ __launch_bounds__(MG_THREADS, 2) void moe_gemm_kernel(
     if constexpr (GATHER) {
       const int p = sorted_ids[r];
       arow = p < npairs ? p / topk : 0;
+    } else if constexpr (DENSE) {
+      arow = r < dense_m ? r : dense_m - 1;
     } else {
       arow = r;
     }
@@ -175,8 +198,8 @@ __global__ __launch_bounds__(MG_THREADS, 2) void moe_gemm_kernel(
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk_all = K / MG_BK;
-  const int kb0 = (int)((int64_t)nk_all * blockIdx.z / gridDim.z);
-  const int nk = (int)((int64_t)nk_all * (blockIdx.z + 1) / gridDim.z);
+  const int kb0 = (int)((int64_t)nk_all * z / S);
+  const int nk = (int)((int64_t)nk_all * (z + 1) / S);
   gload(kb0);
   lstore(0);
   __syncthreads();
@@ -208,6 +231,9 @@ __global__ __launch_bounds__(MG_THREADS, 2) void moe_gemm_kernel(
     for (int i = 0; i < 4; ++i) {
       const int r = mb * BM + wm * (BM / 2) + mt * 16 + 4 * q4 + i;
       int64_t crow = r;
+      if constexpr (DENSE) {
+        if (r >= dense_m) continue;
+      }
       if constexpr (SCATTER) {
         const int p = sorted_ids[r];
         if (p >= npairs) continue;
@@ -215,7 +241,7 @@ __global__ __launch_bounds__(MG_THREADS, 2) void moe_gemm_kernel(
       }
       const int64_t off = crow * ldc + (int64_t)nb * MG_BN + wn * 64 + r16;
       if constexpr (PARTIAL) {
-        float* cp = reinterpret_cast<float*>(Cv) + blockIdx.z * slice_stride + off;
+        float* cp = reinterpret_cast<float*>(Cv) + z * slice_stride + off;
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) cp[nt * 16] = acc[mt][nt][i];
       } else {
@@ -225,6 +251,28 @@ __global__ __launch_bounds__(MG_THREADS, 2) void moe_gemm_kernel(
       }
     }
   }
+}
+
+// out[m, n] = sum_z Cs[z, m, n]  (+ residual)  -- split-K reduction of the dense GEMM.
+template <typename T>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(T* __restrict__ out,
+                                                            const float* __restrict__ Cs, int S,
+                                                            int64_t n8, int64_t slice_stride) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n8) return;
+  f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, b = a;
+  for (int z = 0; z < S; ++z) {
+    const float* src = Cs + z * slice_stride + i * 8;
+    a += *reinterpret_cast<const f32x4*>(src);
+    b += *reinterpret_cast<const f32x4*>(src + 4);
+  }
+  Pack8<T> o;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    o.h[q] = from_f<T>(a[q]);
+    o.h[4 + q] = from_f<T>(b[q]);
+  }
+  *reinterpret_cast<u32x4*>(out + i * 8) = o.u;
 }
 
 // ---------------------------------------------------------------------------- combine
@@ -300,7 +348,7 @@ static void moe_gemm_bm(void* C, const void* A, const void* W, const int* sorted
   moe_gemm_kernel<T, BM, G, S, P><<<grid, MG_THREADS, 0, s>>>(C, (const T*)A, (const T*)W,   \
                                                               sorted_ids, block_expert, meta, \
                                                               npairs, topk, N, K, lda, ldc,   \
-                                                              slice_stride)
+                                                              slice_stride, 0)
   if (splitk > 1) MG_LAUNCH(false, true, true);          // host-checked: scatter, !gather
   else if (gather && !scatter) MG_LAUNCH(true, false, false);
   else if (!gather && scatter) MG_LAUNCH(false, true, false);
@@ -332,6 +380,34 @@ void launch_moe_gemm(int dtype, int bm, void* C, const void* A, const void* W,
   else
     moe_gemm_t<f16>(bm, C, A, W, sorted_ids, block_expert, meta, npairs, topk, N, K, lda, ldc,
                     max_mblocks, gather, scatter, splitk, slice_stride, s);
+}
+
+void launch_dense_gemm_splitk(int dtype, int bm, float* Cs, const void* A, const void* W, int M,
+                              int N, int K, int64_t lda, int splitk, hipStream_t s) {
+  const int MB = (M + bm - 1) / bm;
+  const dim3 grid(MB * (N / MG_BN) * splitk);
+  const int64_t ss = (int64_t)M * N;
+#define DG_LAUNCH(T, BMV)                                                                     \
+  moe_gemm_kernel<T, BMV, false, false, true, true><<<grid, MG_THREADS, 0, s>>>(             \
+      Cs, (const T*)A, (const T*)W, nullptr, nullptr, nullptr, MB, splitk, N, K, lda, N, ss, M)
+  if (dtype == DT_BF16) {
+    if (bm == 128) DG_LAUNCH(bf16, 128);
+    else DG_LAUNCH(bf16, 64);
+  } else {
+    if (bm == 128) DG_LAUNCH(f16, 128);
+    else DG_LAUNCH(f16, 64);
+  }
+#undef DG_LAUNCH
+}
+
+void launch_splitk_reduce(int dtype, void* out, const float* Cs, int S, int64_t numel,
+                          int64_t slice_stride, hipStream_t s) {
+  const int64_t n8 = numel / 8;
+  const dim3 grid((unsigned)((n8 + 255) / 256));
+  if (dtype == DT_BF16)
+    splitk_reduce_kernel<bf16><<<grid, 256, 0, s>>>((bf16*)out, Cs, S, n8, slice_stride);
+  else
+    splitk_reduce_kernel<f16><<<grid, 256, 0, s>>>((f16*)out, Cs, S, n8, slice_stride);
 }
 
 void launch_moe_combine(int dtype, void* out, const void* y, const float* topk_w, int ntok, int k,

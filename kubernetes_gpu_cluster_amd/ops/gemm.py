@@ -1,5 +1,9 @@
-"""Linear layers on the GPU: hipBLASLt (``F.linear``) or the hand-written K9 skinny
-GEMM (``csrc/kernels/gemm_skinny.hip``) for small-batch decode.
+"""Linear layers on the GPU: hipBLASLt (``F.linear``), the hand-written K9 skinny
+GEMM (``csrc/kernels/gemm_skinny.hip``) for small-batch decode, or the dense split-K
+MFMA GEMM (``dense_gemm_splitk`` in ``csrc/kernels/moe.hip``: the K14 tiles with one
+K-slice per XCD, fp32 slices summed by ``splitk_reduce``) for mid-size decode batches,
+where hipBLASLt's few output tiles leave the long-K projections (the MLP down
+projection, K = 14336) at ~1.8 TB/s.
 
 Which one runs is a per-(M, N, K) decision made once at engine start by timing
 both on the model's own weights (``tune_skinny``), never guessed: at M <= 64 the GEMM
@@ -32,6 +36,34 @@ _chosen_us: dict[tuple[int, int, int], float] = {}
 _rms_us: dict[tuple[int, int], float] = {}
 _enabled = os.environ.get("KGC_SKINNY_GEMM", "1") != "0"
 
+# dense split-K: (M, N, K) -> (bm, S) where it measured faster than hipBLASLt
+SPLITK_MAX_M = 512
+_SK_CONFIGS = [(bm, S) for bm in (64, 128) for S in (2, 4, 8)]
+_plan_sk: dict[tuple[int, int, int], tuple[int, int]] = {}
+_sk_enabled = os.environ.get("KGC_SPLITK_GEMM", "1") != "0"
+
+
+def splitk_ok(M: int, N: int, K: int, cfg) -> bool:
+    bm, S = cfg
+    return 1 <= M <= SPLITK_MAX_M and N % 128 == 0 and K % 64 == 0 and K // 64 >= S
+
+
+def splitk_gemm(x: torch.Tensor, w: torch.Tensor, cfg,
+                out: Optional[torch.Tensor] = None,
+                ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x W^T as S fp32 K-slices (one per XCD group) plus a reduction to x's dtype."""
+    from . import _k
+    bm, S = cfg
+    M, N = x.shape[0], w.shape[0]
+    if ws is None:
+        ws = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
+    if out is None:
+        out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    k = _k()
+    k.dense_gemm_splitk(ws, x, w, bm)
+    k.splitk_reduce(out, ws)
+    return out
+
 
 def skinny_ok(M: int, N: int, K: int, cfg) -> bool:
     mt, nt, nw, _ = cfg
@@ -53,6 +85,11 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         cfg = _plan.get((x.shape[0], w.shape[0], w.shape[1]))
         if cfg is not None and x.stride(1) == 1:
             return skinny_gemm(x, w, bias, cfg)
+    if (_plan_sk and bias is None and x.is_cuda and x.dim() == 2 and x.stride(1) == 1
+            and x.stride(0) % 8 == 0):
+        cfg = _plan_sk.get((x.shape[0], w.shape[0], w.shape[1]))
+        if cfg is not None:
+            return splitk_gemm(x, w, cfg)
     return F.linear(x, w, bias)
 
 
@@ -95,6 +132,7 @@ def fused_norm_plan(M: int, norm_shapes, acc_shapes):
 
 
 def clear_plan() -> None:
+    _plan_sk.clear()
     _plan_norm.clear()
     _chosen_us.clear()
     _rms_us.clear()
@@ -103,6 +141,10 @@ def clear_plan() -> None:
 
 def plan() -> dict:
     return dict(_plan)
+
+
+def splitk_plan() -> dict:
+    return dict(_plan_sk)
 
 
 def _time(fn, reps: int) -> float:
@@ -165,8 +207,46 @@ def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: floa
                 _tune_norm(ws, x, out, M, N, K, reps)
             log.info("gemm M=%d N=%d K=%d: hipBLASLt %.1f us, skinny %s %.1f us -> %s", M, N, K,
                      lib_t * 1e3 / n, sk_cfg, sk_t * 1e3 / n, "skinny" if best else "hipBLASLt")
-    log.info("skinny GEMM tuning: %d shapes in %.1f s", len(res), time.time() - t0)
+        if _sk_enabled:
+            _tune_splitk(ws, N, K, [m for m in ms if SKINNY_MAX_M < m <= SPLITK_MAX_M], margin,
+                         reps, res)
+    log.info("GEMM tuning: %d shapes in %.1f s", len(res), time.time() - t0)
     return res
+
+
+def _tune_splitk(ws, N: int, K: int, ms, margin: float, reps: int, res: dict) -> None:
+    """hipBLASLt vs every dense split-K configuration at each M in ``ms``, over all
+    weights of the shape (HBM-resident, as in a decode step)."""
+    for M in sorted(set(ms)):
+        if not splitk_ok(M, N, K, (64, 1)):
+            continue
+        x = torch.randn(M, K, dtype=ws[0].dtype, device=ws[0].device)
+        out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+
+        def lib():
+            for w in ws:
+                F.linear(x, w)
+        lib_t = _time(lib, reps)
+        best_t, best_cfg = float("inf"), None
+        for cfg in _SK_CONFIGS:
+            if not splitk_ok(M, N, K, cfg) or (cfg[0] == 128 and M <= 64):
+                continue
+            buf = torch.empty(cfg[1], M, N, dtype=torch.float32, device=x.device)
+
+            def sk(cfg=cfg, buf=buf):
+                for w in ws:
+                    splitk_gemm(x, w, cfg, out, buf)
+            t = _time(sk, reps)
+            if t < best_t:
+                best_t, best_cfg = t, cfg
+        n = len(ws)
+        chosen = best_cfg if best_t < lib_t * margin else None
+        if chosen is not None:
+            _plan_sk[(M, N, K)] = chosen
+        res[(M, N, K)] = (chosen, lib_t * 1e3 / n, best_t * 1e3 / n, best_cfg)
+        log.info("gemm M=%d N=%d K=%d: hipBLASLt %.1f us, split-K %s %.1f us -> %s", M, N, K,
+                 lib_t * 1e3 / n, best_cfg, best_t * 1e3 / n,
+                 "split-K" if chosen else "hipBLASLt")
 
 
 def _tune_norm(ws, x, out, M: int, N: int, K: int, reps: int) -> None:

@@ -423,6 +423,36 @@ def test_skinny_gemm_norm_and_accumulate(gpu, M, nw):
     torch.testing.assert_close(c.float().cpu(), exp, atol=6e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("M,N,K,bm,S", [(256, 1024, 4096, 128, 8), (80, 768, 2048, 64, 4),
+                                        (144, 512, 1024, 128, 2), (33, 256, 8192, 64, 8)])
+def test_dense_gemm_splitk_matches_fp32(gpu, M, N, K, bm, S):
+    """Dense split-K decode GEMM (XCD-mapped K-slices) + reduction vs an fp32 matmul,
+    including M not a multiple of the row block (clamped loads, masked stores)."""
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, dtype=torch.bfloat16, device=gpu)
+    w = torch.randn(N, K, dtype=torch.bfloat16, device=gpu) * 0.02
+    ref = x.float().cpu() @ w.float().cpu().t()
+    ws = torch.full((S, M, N), float("nan"), dtype=torch.float32, device=gpu)
+    got = gemm.splitk_gemm(x, w, (bm, S), ws=ws)
+    torch.testing.assert_close(got.float().cpu(), ref, atol=3e-2, rtol=2e-2)
+    # every slice row was written (no NaN left from the fill), and slices sum to the result
+    torch.testing.assert_close(ws.sum(0).cpu(), ref, atol=2e-3, rtol=2e-3)
+
+
+def test_linear_uses_splitk_plan(gpu):
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    torch.manual_seed(5)
+    w = torch.randn(1024, 4096, dtype=torch.bfloat16, device=gpu) * 0.02
+    x = torch.randn(96, 4096, dtype=torch.bfloat16, device=gpu)
+    gemm._plan_sk[(96, 1024, 4096)] = (64, 4)
+    try:
+        got = gemm.linear(x, w)
+    finally:
+        gemm.clear_plan()
+    torch.testing.assert_close(got.float(), (x.float() @ w.float().t()), atol=3e-2, rtol=2e-2)
+
+
 def test_linear_uses_tuned_plan(gpu):
     from kubernetes_gpu_cluster_amd.ops import gemm
     torch.manual_seed(4)
