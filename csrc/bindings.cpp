@@ -355,6 +355,37 @@ void splitk_reduce(Tensor out, Tensor Cs) {
                             out.numel(), Cs.stride(0), stream());
 }
 
+void splitk_reduce_silu(Tensor out, Tensor Cs) {
+  check_gpu(Cs, "Cs");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(Cs.device());
+  TORCH_CHECK(Cs.scalar_type() == at::kFloat && Cs.dim() == 3 && Cs.is_contiguous(), "Cs fp32 [S, M, 2I]");
+  const int64_t M = Cs.size(1), I = Cs.size(2) / 2;
+  TORCH_CHECK(Cs.size(2) % 16 == 0, "2I % 16 == 0");
+  TORCH_CHECK(out.dim() == 2 && out.is_contiguous() && out.size(0) == M && out.size(1) == I,
+              "out [M, I] contiguous");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kHalf, "bf16 / fp16");
+  if (M == 0) return;
+  kgc::launch_splitk_reduce_silu(dt_code(out), out.data_ptr(), Cs.data_ptr<float>(), (int)Cs.size(0),
+                                 (int)M, (int)I, Cs.stride(0), stream());
+}
+
+void splitk_add_rms_norm(Tensor out, Tensor Cs, Tensor residual, Tensor w, double eps) {
+  check_gpu(Cs, "Cs");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(Cs.device());
+  TORCH_CHECK(Cs.scalar_type() == at::kFloat && Cs.dim() == 3 && Cs.is_contiguous(), "Cs fp32 [S, M, H]");
+  const int64_t M = Cs.size(1), H = Cs.size(2);
+  TORCH_CHECK(H % 8 == 0 && H <= 8192, "H % 8 == 0, H <= 8192");
+  for (const Tensor* t : {&out, &residual})
+    TORCH_CHECK(t->dim() == 2 && t->is_contiguous() && t->size(0) == M && t->size(1) == H &&
+                t->scalar_type() == out.scalar_type(), "out / residual [M, H] contiguous");
+  TORCH_CHECK(w.is_contiguous() && w.numel() == H && w.scalar_type() == out.scalar_type(), "w [H]");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kHalf, "bf16 / fp16");
+  if (M == 0) return;
+  kgc::launch_splitk_add_rms_norm(dt_code(out), out.data_ptr(), Cs.data_ptr<float>(),
+                                  residual.data_ptr(), w.data_ptr(), (int)M, (int)H,
+                                  (int)Cs.size(0), Cs.stride(0), (float)eps, stream());
+}
+
 // ---- K12 xGMI all-reduce: IPC buffers are raw device pointers carried as int64
 int64_t ar_signal_bytes() { return (int64_t)kgc::allreduce_signal_bytes(); }
 int64_t ar_alloc(int64_t bytes) { return (int64_t)(intptr_t)kgc::ar_alloc(bytes); }
@@ -471,6 +502,8 @@ TORCH_LIBRARY(kgc, m) {
   m.def("moe_combine(Tensor(a!) out, Tensor y, Tensor topk_w) -> ()");
   m.def("dense_gemm_splitk(Tensor(a!) Cs, Tensor A, Tensor W, int bm) -> ()");
   m.def("splitk_reduce(Tensor(a!) out, Tensor Cs) -> ()");
+  m.def("splitk_reduce_silu(Tensor(a!) out, Tensor Cs) -> ()");
+  m.def("splitk_add_rms_norm(Tensor(a!) out, Tensor Cs, Tensor(b!) residual, Tensor w, float eps) -> ()");
   m.def("ar_signal_bytes() -> int", &ar_signal_bytes);
   m.def("ar_alloc(int bytes) -> int", &ar_alloc);
   m.def("ar_free(int ptr) -> ()", &ar_free);
@@ -500,5 +533,7 @@ TORCH_LIBRARY_IMPL(kgc, CUDA, m) {
   m.impl("moe_combine", &moe_combine);
   m.impl("dense_gemm_splitk", &dense_gemm_splitk);
   m.impl("splitk_reduce", &splitk_reduce);
+  m.impl("splitk_reduce_silu", &splitk_reduce_silu);
+  m.impl("splitk_add_rms_norm", &splitk_add_rms_norm);
   m.impl("skinny_gemm", &skinny_gemm);
 }

@@ -59,8 +59,15 @@ void launch_moe_gemm(int dtype, int bm, void* C, const void* A, const void* W,
 // dense split-K decode GEMM: Cs [splitk, M, N] fp32 = A [M, K] x W [N, K]^T, XCD-mapped slices
 void launch_dense_gemm_splitk(int dtype, int bm, float* Cs, const void* A, const void* W, int M,
                               int N, int K, int64_t lda, int splitk, hipStream_t s);
+// residual += sum_z Cs[z] (rounded to dtype); out = rms_norm(residual) * w, one WG per row
+void launch_splitk_add_rms_norm(int dtype, void* out, const float* Cs, void* residual,
+                                const void* w, int rows, int H, int S, int64_t slice_stride,
+                                float eps, hipStream_t s);
 void launch_splitk_reduce(int dtype, void* out, const float* Cs, int S, int64_t numel,
                           int64_t slice_stride, hipStream_t s);
+// silu(gate) * up of the summed gate_up split-K slices: Cs [S, M, 2I] -> out [M, I]
+void launch_splitk_reduce_silu(int dtype, void* out, const float* Cs, int S, int M, int I,
+                               int64_t slice_stride, hipStream_t s);
 void launch_moe_combine(int dtype, void* out, const void* y, const float* topk_w, int ntok, int k,
                         int H, int splitk, int64_t slice_stride, hipStream_t s);
 

@@ -275,6 +275,36 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(T* __restrict__ out,
   *reinterpret_cast<u32x4*>(out + i * 8) = o.u;
 }
 
+// K7 fused into the gate_up split-K reduction: out[m, i] = silu(g) * u with
+// g = sum_z Cs[z, m, i], u = sum_z Cs[z, m, I + i].  The [M, 2I] bf16 gate_up output
+// is never written, and the separate silu_mul launch disappears from the decode step.
+// grid (ceil(I/8/256), M): one 8-wide column group per thread, no index division.
+template <typename T>
+__global__ __launch_bounds__(256) void splitk_reduce_silu_kernel(T* __restrict__ out,
+                                                                 const float* __restrict__ Cs,
+                                                                 int S, int I,
+                                                                 int64_t slice_stride) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c >= I) return;
+  const int64_t m = blockIdx.y;
+  const float* row = Cs + m * 2 * I + c;
+  f32x4 g0 = f32x4{0.f, 0.f, 0.f, 0.f}, g1 = g0, u0 = g0, u1 = g0;
+  for (int z = 0; z < S; ++z) {
+    const float* src = row + z * slice_stride;
+    g0 += *reinterpret_cast<const f32x4*>(src);
+    g1 += *reinterpret_cast<const f32x4*>(src + 4);
+    u0 += *reinterpret_cast<const f32x4*>(src + I);
+    u1 += *reinterpret_cast<const f32x4*>(src + I + 4);
+  }
+  Pack8<T> o;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    o.h[q] = from_f<T>(g0[q] / (1.f + __expf(-g0[q])) * u0[q]);
+    o.h[4 + q] = from_f<T>(g1[q] / (1.f + __expf(-g1[q])) * u1[q]);
+  }
+  *reinterpret_cast<u32x4*>(out + m * I + c) = o.u;
+}
+
 // ---------------------------------------------------------------------------- combine
 // y: [T*k, H] in T, or (S > 0) S fp32 split-K slices [S][T*k, H] summed here.
 template <typename T>
@@ -408,6 +438,21 @@ void launch_splitk_reduce(int dtype, void* out, const float* Cs, int S, int64_t 
     splitk_reduce_kernel<bf16><<<grid, 256, 0, s>>>((bf16*)out, Cs, S, n8, slice_stride);
   else
     splitk_reduce_kernel<f16><<<grid, 256, 0, s>>>((f16*)out, Cs, S, n8, slice_stride);
+}
+
+void launch_splitk_reduce_silu(int dtype, void* out, const float* Cs, int S, int M, int I,
+                               int64_t slice_stride, hipStream_t s) {
+  for (int m0 = 0; m0 < M; m0 += 65535) {   // gridDim.y <= 65535
+    const int n = std::min(M - m0, 65535);
+    const dim3 grid((unsigned)((I / 8 + 255) / 256), (unsigned)n);
+    const float* c = Cs + (int64_t)m0 * 2 * I;
+    if (dtype == DT_BF16)
+      splitk_reduce_silu_kernel<bf16><<<grid, 256, 0, s>>>((bf16*)out + (int64_t)m0 * I, c, S, I,
+                                                          slice_stride);
+    else
+      splitk_reduce_silu_kernel<f16><<<grid, 256, 0, s>>>((f16*)out + (int64_t)m0 * I, c, S, I,
+                                                         slice_stride);
+  }
 }
 
 void launch_moe_combine(int dtype, void* out, const void* y, const float* topk_w, int ntok, int k,

@@ -59,6 +59,67 @@ __global__ __launch_bounds__(NORM_NT) void rms_norm_kernel(
   }
 }
 
+// Split-K reduction fused into the residual add + RMSNorm that consumes a row-parallel
+// projection (o_proj -> post-attention norm, down_proj -> next layer's input norm):
+//   h = sum_z Cs[z, row, :] (rounded to T, as the unfused reduce stores it)
+//   residual += h;  out = rms_norm(residual) * w
+// The [M, H] projection output is never written and one launch per projection goes.
+template <typename T>
+__global__ __launch_bounds__(NORM_NT) void splitk_add_rms_norm_kernel(
+    T* __restrict__ out, const float* __restrict__ Cs, T* __restrict__ residual,
+    const T* __restrict__ w, int H, int S, int64_t slice_stride, float eps) {
+  __shared__ float scratch[NORM_NT / 64];
+  const int row = blockIdx.x;
+  const int nv = H >> 3;
+  const float* cr = Cs + (int64_t)row * H;
+  T* rr = residual + (int64_t)row * H;
+  Pack8<T> v[NORM_MAXV], wv[NORM_MAXV];
+#pragma unroll
+  for (int i = 0; i < NORM_MAXV; ++i) {
+    const int idx = threadIdx.x + i * NORM_NT;
+    if (idx < nv) wv[i].u = *reinterpret_cast<const u32x4*>(w + idx * 8);
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NORM_MAXV; ++i) {
+    const int idx = threadIdx.x + i * NORM_NT;
+    if (idx < nv) {
+      f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, b = a;
+      for (int z = 0; z < S; ++z) {
+        const float* src = cr + z * slice_stride + idx * 8;
+        a += *reinterpret_cast<const f32x4*>(src);
+        b += *reinterpret_cast<const f32x4*>(src + 4);
+      }
+      Pack8<T> r;
+      r.u = *reinterpret_cast<const u32x4*>(rr + idx * 8);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[i].h[q] = from_f<T>(to_f(from_f<T>(a[q])) + to_f(r.h[q]));
+        v[i].h[4 + q] = from_f<T>(to_f(from_f<T>(b[q])) + to_f(r.h[4 + q]));
+      }
+      *reinterpret_cast<u32x4*>(rr + idx * 8) = v[i].u;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float f = to_f(v[i].h[j]);
+        ss += f * f;
+      }
+    }
+  }
+  ss = block_sum<NORM_NT>(ss, scratch);
+  const float inv = rsqrtf(ss / (float)H + eps);
+  T* orow = out + (int64_t)row * H;
+#pragma unroll
+  for (int i = 0; i < NORM_MAXV; ++i) {
+    const int idx = threadIdx.x + i * NORM_NT;
+    if (idx < nv) {
+      Pack8<T> o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o.h[j] = from_f<T>(to_f(v[i].h[j]) * inv * to_f(wv[i].h[j]));
+      *reinterpret_cast<u32x4*>(orow + idx * 8) = o.u;
+    }
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(NORM_NT) void layer_norm_kernel(
     T* __restrict__ out, const T* __restrict__ x, const T* __restrict__ w,
@@ -124,6 +185,18 @@ void launch_rms_norm(int dtype, void* out, const void* x, void* residual, const 
                      int rows, int H, int64_t x_stride, float eps, hipStream_t s) {
   if (dtype == DT_BF16) rms_dispatch<bf16>(out, x, residual, w, rows, H, x_stride, eps, s);
   else rms_dispatch<f16>(out, x, residual, w, rows, H, x_stride, eps, s);
+}
+
+void launch_splitk_add_rms_norm(int dtype, void* out, const float* Cs, void* residual,
+                                const void* w, int rows, int H, int S, int64_t slice_stride,
+                                float eps, hipStream_t s) {
+  if (rows == 0) return;
+  if (dtype == DT_BF16)
+    splitk_add_rms_norm_kernel<bf16><<<rows, NORM_NT, 0, s>>>(
+        (bf16*)out, Cs, (bf16*)residual, (const bf16*)w, H, S, slice_stride, eps);
+  else
+    splitk_add_rms_norm_kernel<f16><<<rows, NORM_NT, 0, s>>>(
+        (f16*)out, Cs, (f16*)residual, (const f16*)w, H, S, slice_stride, eps);
 }
 
 void launch_layer_norm(int dtype, void* out, const void* x, const void* w, const void* b,

@@ -11,6 +11,7 @@ embedding, the last the final norm and the LM head.
 """
 from __future__ import annotations
 
+import os
 import re
 from typing import Iterable, Optional
 
@@ -18,6 +19,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
+from ..ops import gemm
 from ..parallel import comm
 from ..parallel.layers import (MergedColumnParallelLinear, ParallelLMHead, QKVParallelLinear,
                                ReplicatedLinear, RowParallelLinear, VocabParallelEmbedding)
@@ -32,6 +34,9 @@ def pp_layer_range(num_layers: int, pp_size: int, pp_rank: int) -> tuple[int, in
     extra = num_layers % pp_size
     start = pp_rank * per + min(pp_rank, extra)
     return start, start + per + (1 if pp_rank < extra else 0)
+
+
+_tail_fusion_enabled = os.environ.get("KGC_TAIL_FUSION", "1") != "0"
 
 
 class RMSNorm(nn.Module):
@@ -86,7 +91,9 @@ class LlamaMLP(nn.Module):
                                            device=device)
 
     def forward(self, x):
-        return self.down_proj(ops.silu_mul(self.gate_up_proj(x)))
+        # gate_up -> silu_mul, fused into the split-K reduction where that runs (ops/gemm.py)
+        gu = self.gate_up_proj
+        return self.down_proj(gemm.linear_silu(x, gu.weight, gu.bias))
 
 
 class LlamaDecoderLayer(nn.Module):
@@ -150,6 +157,8 @@ class LlamaForCausalLM(nn.Module):
             if cfgs is not None:
                 return self._forward_fused(input_ids, positions, ctx, cfgs)
         x = self.embed_tokens(input_ids) if self.first else hidden
+        if self._tail_fusable(x):
+            return self._forward_tail_fused(positions, x, ctx)
         for layer in self.layers:
             x, residual = layer(positions, x, residual, ctx)
         if not self.last:
@@ -157,6 +166,40 @@ class LlamaForCausalLM(nn.Module):
         if residual is None:
             return self.norm(x)
         x, _ = self.norm(x, residual)
+        return x
+
+    # ------------------------------------------------------------------ fused projection tails
+    def _tail_fusable(self, x) -> bool:
+        """One GPU, whole model, dense bias-free MLP / o_proj, and a split-K plan at this M:
+        the o / down projections then run with their reduction fused into the next norm."""
+        if not (x.is_cuda and self.first and self.last and self.layers and not self.cfg.is_moe
+                and get_state().tp_size == 1 and gemm.splitk_plan_has_m(x.shape[0])
+                and _tail_fusion_enabled):
+            return False
+        l0 = self.layers[0]
+        return (l0.self_attn.o_proj.bias is None and l0.mlp.down_proj.bias is None
+                and l0.mlp.gate_up_proj.bias is None)
+
+    def _forward_tail_fused(self, positions, x, ctx):
+        """The regular layer loop with each row-parallel projection handed to the norm that
+        consumes it (``gemm.linear_add_rms``): o_proj -> post-attention norm, down_proj ->
+        the next layer's input norm (the last one -> the final norm).  Same math and
+        rounding points as ``LlamaDecoderLayer.forward``."""
+        residual, h, prev = x, None, None
+        for layer in self.layers:
+            ln1 = layer.input_layernorm
+            if prev is None:
+                x = ln1(x)
+            else:
+                x, residual = gemm.linear_add_rms(h, prev.mlp.down_proj.weight, residual,
+                                                  ln1.weight, ln1.eps)
+            at, ln2 = layer.self_attn, layer.post_attention_layernorm
+            a = at.attend(positions, at.qkv_proj(x), ctx)
+            x, residual = gemm.linear_add_rms(a, at.o_proj.weight, residual, ln2.weight, ln2.eps)
+            h = gemm.linear_silu(x, layer.mlp.gate_up_proj.weight)
+            prev = layer
+        x, _ = gemm.linear_add_rms(h, prev.mlp.down_proj.weight, residual, self.norm.weight,
+                                   self.norm.eps)
         return x
 
     # ------------------------------------------------------------------ fused small-M decode
@@ -180,6 +223,11 @@ class LlamaForCausalLM(nn.Module):
         l0 = self.layers[0]
         return ((l0.self_attn.qkv_proj.weight, l0.mlp.gate_up_proj.weight),
                 (l0.self_attn.o_proj.weight, l0.mlp.down_proj.weight))
+
+    def silu_shapes(self) -> set:
+        """(N, K) of the merged gate_up weights (their split-K reduction carries silu_mul)."""
+        return {tuple(l.mlp.gate_up_proj.weight.shape) for l in self.layers
+                if isinstance(getattr(l, "mlp", None), LlamaMLP)}
 
     def fused_norm_shapes(self) -> set:
         """(N, K) of the GEMMs whose input RMSNorm the fused layer absorbs (tuned at start)."""

@@ -65,6 +65,58 @@ def splitk_gemm(x: torch.Tensor, w: torch.Tensor, cfg,
     return out
 
 
+def splitk_gemm_silu(x: torch.Tensor, w: torch.Tensor, cfg,
+                     out: Optional[torch.Tensor] = None,
+                     ws: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """silu(x Wg^T) * (x Wu^T) for a merged [gate; up] weight: the split-K slices are
+    summed and activated in one pass (``splitk_reduce_silu``), so the [M, 2I] gate_up
+    output is never materialised and no separate silu_mul runs."""
+    from . import _k
+    bm, S = cfg
+    M, N = x.shape[0], w.shape[0]
+    if ws is None:
+        ws = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
+    if out is None:
+        out = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
+    k = _k()
+    k.dense_gemm_splitk(ws, x, w, bm)
+    k.splitk_reduce_silu(out, ws)
+    return out
+
+
+def linear_silu(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """silu_mul(linear(x, w, bias)) over a merged gate_up weight, with the activation
+    folded into the split-K reduction where the plan runs split-K at this (M, N, K)."""
+    from . import silu_mul
+    if (_plan_sk and bias is None and x.is_cuda and x.dim() == 2 and x.stride(1) == 1
+            and x.stride(0) % 8 == 0 and w.shape[0] % 16 == 0):
+        cfg = _plan_sk.get((x.shape[0], w.shape[0], w.shape[1]))
+        if cfg is not None:
+            return splitk_gemm_silu(x, w, cfg)
+    return silu_mul(linear(x, w, bias))
+
+
+def linear_add_rms(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor,
+                   gamma: torch.Tensor, eps: float) -> tuple[torch.Tensor, torch.Tensor]:
+    """residual += x W^T; returns (rms_norm(residual) * gamma, residual) -- a row-parallel
+    projection (o / down, TP = 1) and the fused add + RMSNorm that consumes it.  Where the
+    plan runs split-K at this (M, N, K), the slice reduction, residual add and norm are one
+    kernel (``splitk_add_rms_norm``); otherwise the GEMM and ``fused_add_rms_norm`` run."""
+    from . import _k, fused_add_rms_norm
+    if (_plan_sk and x.is_cuda and x.dim() == 2 and x.stride(1) == 1 and x.stride(0) % 8 == 0
+            and w.shape[0] <= 8192 and residual.is_contiguous()):
+        cfg = _plan_sk.get((x.shape[0], w.shape[0], w.shape[1]))
+        if cfg is not None:
+            bm, S = cfg
+            ws = torch.empty(S, x.shape[0], w.shape[0], dtype=torch.float32, device=x.device)
+            out = torch.empty_like(residual)
+            k = _k()
+            k.dense_gemm_splitk(ws, x, w, bm)
+            k.splitk_add_rms_norm(out, ws, residual, gamma, eps)
+            return out, residual
+    return fused_add_rms_norm(linear(x, w), residual, gamma, eps)
+
+
 def skinny_ok(M: int, N: int, K: int, cfg) -> bool:
     mt, nt, nw, _ = cfg
     return 1 <= M <= 16 * mt and N % (16 * nt) == 0 and K % (32 * nw) == 0
@@ -147,6 +199,10 @@ def splitk_plan() -> dict:
     return dict(_plan_sk)
 
 
+def splitk_plan_has_m(M: int) -> bool:
+    return _sk_enabled and any(k[0] == M for k in _plan_sk)
+
+
 def _time(fn, reps: int) -> float:
     fn()
     torch.cuda.synchronize()
@@ -161,13 +217,15 @@ def _time(fn, reps: int) -> float:
 
 @torch.inference_mode()
 def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: float = 0.97,
-                reps: int = 3, norm_shapes=(), norm_max_m: int = 16) -> dict:
+                reps: int = 3, norm_shapes=(), norm_max_m: int = 16, silu_shapes=()) -> dict:
     """Time hipBLASLt against every skinny configuration for each weight shape and
     batch size M (decode buckets <= SKINNY_MAX_M) and record the skinny kernel where it
     is faster by more than ``1 - margin``.  Each timing sweeps ALL weights of the shape
     (every layer's copy) so the weights stream from HBM as in a real decode step,
     not from the 256 MB Infinity Cache.  Returns {(M, N, K): (chosen cfg or None,
-    hipBLASLt us, best skinny us, best skinny cfg)}, times per GEMM call."""
+    hipBLASLt us, best skinny us, best skinny cfg)}, times per GEMM call.
+    ``silu_shapes``: (N, K) of merged gate_up weights, whose split-K candidates are timed
+    with the fused SiLU reduction against hipBLASLt + silu_mul (``linear_silu``)."""
     if not _enabled:
         return {}
     by_shape: dict[tuple[int, int], list[torch.Tensor]] = {}
@@ -209,25 +267,32 @@ def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: floa
                      lib_t * 1e3 / n, sk_cfg, sk_t * 1e3 / n, "skinny" if best else "hipBLASLt")
         if _sk_enabled:
             _tune_splitk(ws, N, K, [m for m in ms if SKINNY_MAX_M < m <= SPLITK_MAX_M], margin,
-                         reps, res)
+                         reps, res, silu=(N, K) in silu_shapes)
     log.info("GEMM tuning: %d shapes in %.1f s", len(res), time.time() - t0)
     return res
 
 
-def _tune_splitk(ws, N: int, K: int, ms, margin: float, reps: int, res: dict) -> None:
+def _tune_splitk(ws, N: int, K: int, ms, margin: float, reps: int, res: dict,
+                 silu: bool = False) -> None:
     """hipBLASLt vs every dense split-K configuration at each M in ``ms``, over all
-    weights of the shape (HBM-resident, as in a decode step)."""
+    weights of the shape (HBM-resident, as in a decode step).  ``silu``: both sides
+    include the SiLU-and-mul that follows a gate_up projection."""
+    from . import silu_mul
     for M in sorted(set(ms)):
         if not splitk_ok(M, N, K, (64, 1)):
             continue
         x = torch.randn(M, K, dtype=ws[0].dtype, device=ws[0].device)
-        out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+        out = torch.empty(M, N // 2 if silu else N, dtype=x.dtype, device=x.device)
+        act = torch.empty(M, N // 2, dtype=x.dtype, device=x.device) if silu else None
 
         def lib():
             for w in ws:
-                F.linear(x, w)
+                y = F.linear(x, w)
+                if silu:
+                    silu_mul(y, act)
         lib_t = _time(lib, reps)
         best_t, best_cfg = float("inf"), None
+        sk_fn = splitk_gemm_silu if silu else splitk_gemm
         for cfg in _SK_CONFIGS:
             if not splitk_ok(M, N, K, cfg) or (cfg[0] == 128 and M <= 64):
                 continue
@@ -235,7 +300,7 @@ def _tune_splitk(ws, N: int, K: int, ms, margin: float, reps: int, res: dict) ->
 
             def sk(cfg=cfg, buf=buf):
                 for w in ws:
-                    splitk_gemm(x, w, cfg, out, buf)
+                    sk_fn(x, w, cfg, out, buf)
             t = _time(sk, reps)
             if t < best_t:
                 best_t, best_cfg = t, cfg
@@ -244,8 +309,8 @@ def _tune_splitk(ws, N: int, K: int, ms, margin: float, reps: int, res: dict) ->
         if chosen is not None:
             _plan_sk[(M, N, K)] = chosen
         res[(M, N, K)] = (chosen, lib_t * 1e3 / n, best_t * 1e3 / n, best_cfg)
-        log.info("gemm M=%d N=%d K=%d: hipBLASLt %.1f us, split-K %s %.1f us -> %s", M, N, K,
-                 lib_t * 1e3 / n, best_cfg, best_t * 1e3 / n,
+        log.info("gemm M=%d N=%d K=%d%s: hipBLASLt %.1f us, split-K %s %.1f us -> %s", M, N, K,
+                 " +silu" if silu else "", lib_t * 1e3 / n, best_cfg, best_t * 1e3 / n,
                  "split-K" if chosen else "hipBLASLt")
 
 

@@ -464,3 +464,88 @@ def test_linear_uses_tuned_plan(gpu):
                                atol=3e-2, rtol=2e-2)
     gemm.clear_plan()
 
+
+
+@pytest.mark.parametrize("M,N,K,bm,S", [(256, 2048, 4096, 128, 4), (80, 1536, 2048, 64, 8),
+                                        (33, 512, 1024, 64, 2)])
+def test_splitk_gemm_silu_matches_fp32(gpu, M, N, K, bm, S):
+    """gate_up split-K GEMM with SiLU-and-mul folded into the slice reduction vs an fp32
+    silu(g) * u reference (N = 2I, merged [gate; up] weight)."""
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    torch.manual_seed(M + N + 1)
+    x = torch.randn(M, K, dtype=torch.bfloat16, device=gpu)
+    w = torch.randn(N, K, dtype=torch.bfloat16, device=gpu) * 0.03
+    y = x.float().cpu() @ w.float().cpu().t()
+    g, u = y[:, : N // 2], y[:, N // 2:]
+    ref = torch.nn.functional.silu(g) * u
+    got = gemm.splitk_gemm_silu(x, w, (bm, S))
+    assert got.shape == (M, N // 2)
+    torch.testing.assert_close(got.float().cpu(), ref, atol=3e-2, rtol=2e-2)
+    # through the dispatcher: linear_silu takes the plan's split-K path
+    gemm._plan_sk[(M, N, K)] = (bm, S)
+    try:
+        got2 = gemm.linear_silu(x, w)
+    finally:
+        gemm.clear_plan()
+    torch.testing.assert_close(got2, got)
+
+
+@pytest.mark.parametrize("M,N,K,bm,S", [(256, 4096, 4096, 64, 4), (96, 4096, 14336, 64, 8),
+                                        (40, 1024, 2048, 128, 2)])
+def test_linear_add_rms_splitk_matches_fp32(gpu, M, N, K, bm, S):
+    """Split-K reduction fused into residual add + RMSNorm vs an fp32 reference of
+    residual += x W^T; out = rms_norm(residual) * gamma."""
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    torch.manual_seed(M + K)
+    x = torch.randn(M, K, dtype=torch.bfloat16, device=gpu)
+    w = torch.randn(N, K, dtype=torch.bfloat16, device=gpu) * 0.02
+    res = torch.randn(M, N, dtype=torch.bfloat16, device=gpu)
+    gamma = torch.rand(N, dtype=torch.bfloat16, device=gpu) + 0.5
+    r32 = res.float().cpu() + (x.float().cpu() @ w.float().cpu().t())
+    exp = r32 * torch.rsqrt(r32.pow(2).mean(-1, keepdim=True) + 1e-5) * gamma.float().cpu()
+    gemm._plan_sk[(M, N, K)] = (bm, S)
+    try:
+        out, r = gemm.linear_add_rms(x, w, res, gamma, 1e-5)
+    finally:
+        gemm.clear_plan()
+    assert r.data_ptr() == res.data_ptr()   # residual updated in place
+    torch.testing.assert_close(r.float().cpu(), r32, atol=5e-2, rtol=2e-2)
+    torch.testing.assert_close(out.float().cpu(), exp, atol=5e-2, rtol=2e-2)
+
+
+def test_tail_fused_model_matches_regular_path(gpu):
+    """Whole-model forward with o/down reductions fused into the norms (forced split-K
+    plan) vs the regular layer loop on the same weights."""
+    from kubernetes_gpu_cluster_amd.models import configs
+    from kubernetes_gpu_cluster_amd.models.llama import LlamaForCausalLM
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    from kubernetes_gpu_cluster_amd.models import llama as llama_mod
+    cfg = configs.PRESETS["llama-3-8b"].shrink(name="tail-fuse", num_layers=2)
+    torch.manual_seed(0)
+    model = LlamaForCausalLM(cfg, torch.bfloat16, gpu)
+    for p in model.parameters():
+        p.data.normal_(0, 0.02) if p.dim() == 2 else p.data.fill_(1.0)
+    M = 96
+    ids = torch.randint(0, cfg.vocab_size, (M,), device=gpu)
+    x = model.embed_tokens(ids)
+
+    class _Ctx:
+        pass
+    # exercise the projection tail only: attention replaced by an identity-shaped stub
+    for l in model.layers:
+        l.self_attn.attend = (lambda positions, qkv, ctx, nq=l.self_attn.nq * cfg.head_dim:
+                              qkv[:, :nq].contiguous())
+    ref_out = None
+    try:
+        llama_mod._tail_fusion_enabled = False
+        ref_out = model(ids, None, _Ctx())
+        for l in model.layers:
+            for w in (l.self_attn.o_proj.weight, l.mlp.down_proj.weight):
+                gemm._plan_sk[(M, w.shape[0], w.shape[1])] = (64, 4)
+        llama_mod._tail_fusion_enabled = True
+        assert model._tail_fusable(x)
+        got = model(ids, None, _Ctx())
+    finally:
+        gemm.clear_plan()
+        llama_mod._tail_fusion_enabled = True
+    torch.testing.assert_close(got.float(), ref_out.float(), atol=6e-2, rtol=3e-2)
