@@ -1,0 +1,43 @@
+"""CPU checks of the GEMM dispatch helpers in ops/gemm.py: with no tuned plan (or on
+CPU tensors) ``linear_silu`` and ``linear_add_rms`` are exactly the unfused layer math
+(``silu_mul(linear)`` / ``fused_add_rms_norm(linear)``), and the tail-fused model path is
+never taken off the GPU.  The fused GPU kernels are checked against fp32 references in
+test_kernels_gpu.py."""
+import torch
+
+from kubernetes_gpu_cluster_amd import ops
+from kubernetes_gpu_cluster_amd.ops import gemm
+
+
+def test_linear_silu_fallback_matches_layer_math():
+    torch.manual_seed(0)
+    x = torch.randn(5, 64)
+    w = torch.randn(96, 64) * 0.1
+    y = x @ w.t()
+    exp = torch.nn.functional.silu(y[:, :48]) * y[:, 48:]
+    torch.testing.assert_close(gemm.linear_silu(x, w), exp, atol=1e-5, rtol=1e-5)
+
+
+def test_linear_add_rms_fallback_matches_layer_math():
+    torch.manual_seed(1)
+    x = torch.randn(7, 32)
+    w = torch.randn(48, 32) * 0.1
+    res = torch.randn(7, 48)
+    gamma = torch.rand(48) + 0.5
+    r_exp = res + x @ w.t()
+    o_exp = ops.reference.rms_norm(r_exp, gamma, 1e-6)
+    o, r = gemm.linear_add_rms(x, w, res.clone(), gamma, 1e-6)
+    torch.testing.assert_close(r, r_exp, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(o, o_exp, atol=1e-5, rtol=1e-5)
+
+
+def test_tail_fusion_not_taken_on_cpu():
+    from kubernetes_gpu_cluster_amd.models import configs
+    from kubernetes_gpu_cluster_amd.models.llama import LlamaForCausalLM
+    cfg = configs.PRESETS["tiny-llama"]
+    m = LlamaForCausalLM(cfg, torch.float32, torch.device("cpu"))
+    gemm._plan_sk[(4, 1, 1)] = (64, 2)
+    try:
+        assert not m._tail_fusable(torch.zeros(4, cfg.hidden_size))
+    finally:
+        gemm.clear_plan()
