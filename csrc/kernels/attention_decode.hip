@@ -65,7 +65,9 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
   };
   constexpr int KS = D / 32;      // k-steps of the QK^T product
   constexpr int DT = D / 16;      // 16-row d-tiles of O^T
-  __shared__ __attribute__((aligned(16))) float lds_o[4][16][D];
+  // rows padded by 4 floats: the b128 stores of lanes (head r16, qd) land in (r16 + qd) mod 16
+  // bank groups, 4 lanes each (the b128 minimum), instead of 16 heads on one group
+  __shared__ __attribute__((aligned(16))) float lds_o[4][16][D + 4];
   __shared__ float lds_m[4][16], lds_l[4][16];
   const int b = blockIdx.x, h = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
