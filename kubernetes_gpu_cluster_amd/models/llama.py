@@ -229,6 +229,15 @@ class LlamaForCausalLM(nn.Module):
         return {tuple(l.mlp.gate_up_proj.weight.shape) for l in self.layers
                 if isinstance(getattr(l, "mlp", None), LlamaMLP)}
 
+    def tail_shapes(self) -> set:
+        """(N, K) of the o / down projections whose split-K reduction the following
+        residual add + RMSNorm absorbs (``_forward_tail_fused``), when that path can run."""
+        if not (self.first and self.last and self.layers and not self.cfg.is_moe
+                and get_state().tp_size == 1 and _tail_fusion_enabled):
+            return set()
+        l0 = self.layers[0]
+        return {tuple(l0.self_attn.o_proj.weight.shape), tuple(l0.mlp.down_proj.weight.shape)}
+
     def fused_norm_shapes(self) -> set:
         """(N, K) of the GEMMs whose input RMSNorm the fused layer absorbs (tuned at start)."""
         if not self._fusable or not self.layers:

@@ -217,7 +217,8 @@ def _time(fn, reps: int) -> float:
 
 @torch.inference_mode()
 def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: float = 0.97,
-                reps: int = 3, norm_shapes=(), norm_max_m: int = 16, silu_shapes=()) -> dict:
+                reps: int = 3, norm_shapes=(), norm_max_m: int = 16, silu_shapes=(),
+                tail_shapes=()) -> dict:
     """Time hipBLASLt against every skinny configuration for each weight shape and
     batch size M (decode buckets <= SKINNY_MAX_M) and record the skinny kernel where it
     is faster by more than ``1 - margin``.  Each timing sweeps ALL weights of the shape
@@ -225,7 +226,9 @@ def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: floa
     not from the 256 MB Infinity Cache.  Returns {(M, N, K): (chosen cfg or None,
     hipBLASLt us, best skinny us, best skinny cfg)}, times per GEMM call.
     ``silu_shapes``: (N, K) of merged gate_up weights, whose split-K candidates are timed
-    with the fused SiLU reduction against hipBLASLt + silu_mul (``linear_silu``)."""
+    with the fused SiLU reduction against hipBLASLt + silu_mul (``linear_silu``).
+    ``tail_shapes``: (N, K) of row-parallel projections feeding a residual add + RMSNorm
+    (``linear_add_rms``), timed with that norm on both sides."""
     if not _enabled:
         return {}
     by_shape: dict[tuple[int, int], list[torch.Tensor]] = {}
@@ -267,32 +270,42 @@ def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: floa
                      lib_t * 1e3 / n, sk_cfg, sk_t * 1e3 / n, "skinny" if best else "hipBLASLt")
         if _sk_enabled:
             _tune_splitk(ws, N, K, [m for m in ms if SKINNY_MAX_M < m <= SPLITK_MAX_M], margin,
-                         reps, res, silu=(N, K) in silu_shapes)
+                         reps, res, silu=(N, K) in silu_shapes, tail=(N, K) in tail_shapes)
     log.info("GEMM tuning: %d shapes in %.1f s", len(res), time.time() - t0)
     return res
 
 
 def _tune_splitk(ws, N: int, K: int, ms, margin: float, reps: int, res: dict,
-                 silu: bool = False) -> None:
+                 silu: bool = False, tail: bool = False) -> None:
     """hipBLASLt vs every dense split-K configuration at each M in ``ms``, over all
     weights of the shape (HBM-resident, as in a decode step).  ``silu``: both sides
-    include the SiLU-and-mul that follows a gate_up projection."""
-    from . import silu_mul
+    include the SiLU-and-mul that follows a gate_up projection; ``tail``: both sides
+    include the residual add + RMSNorm that consumes an o / down projection."""
+    from . import _k, fused_add_rms_norm, silu_mul
     for M in sorted(set(ms)):
         if not splitk_ok(M, N, K, (64, 1)):
             continue
         x = torch.randn(M, K, dtype=ws[0].dtype, device=ws[0].device)
         out = torch.empty(M, N // 2 if silu else N, dtype=x.dtype, device=x.device)
         act = torch.empty(M, N // 2, dtype=x.dtype, device=x.device) if silu else None
+        tail = tail and not silu and N <= 8192
+        res_t = torch.zeros(M, N, dtype=x.dtype, device=x.device) if tail else None
+        gamma = torch.ones(N, dtype=x.dtype, device=x.device) if tail else None
 
         def lib():
             for w in ws:
                 y = F.linear(x, w)
                 if silu:
                     silu_mul(y, act)
+                elif tail:
+                    fused_add_rms_norm(y, res_t, gamma, 1e-6)
         lib_t = _time(lib, reps)
         best_t, best_cfg = float("inf"), None
-        sk_fn = splitk_gemm_silu if silu else splitk_gemm
+
+        def sk_tail(x, w, cfg, out, buf):
+            _k().dense_gemm_splitk(buf, x, w, cfg[0])
+            _k().splitk_add_rms_norm(out, buf, res_t, gamma, 1e-6)
+        sk_fn = splitk_gemm_silu if silu else (sk_tail if tail else splitk_gemm)
         for cfg in _SK_CONFIGS:
             if not splitk_ok(M, N, K, cfg) or (cfg[0] == 128 and M <= 64):
                 continue
@@ -310,8 +323,8 @@ def _tune_splitk(ws, N: int, K: int, ms, margin: float, reps: int, res: dict,
             _plan_sk[(M, N, K)] = chosen
         res[(M, N, K)] = (chosen, lib_t * 1e3 / n, best_t * 1e3 / n, best_cfg)
         log.info("gemm M=%d N=%d K=%d%s: hipBLASLt %.1f us, split-K %s %.1f us -> %s", M, N, K,
-                 " +silu" if silu else "", lib_t * 1e3 / n, best_cfg, best_t * 1e3 / n,
-                 "split-K" if chosen else "hipBLASLt")
+                 " +silu" if silu else (" +add_rms" if tail else ""), lib_t * 1e3 / n,
+                 best_cfg, best_t * 1e3 / n, "split-K" if chosen else "hipBLASLt")
 
 
 def _tune_norm(ws, x, out, M: int, N: int, K: int, reps: int) -> None:
