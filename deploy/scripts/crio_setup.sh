@@ -25,14 +25,14 @@ while [[ $# -gt 0 ]]; do
 done
 
 require_root
-KEYRING=/etc/apt/keyrings/cri-o-apt-keyring.gpg
+KEYRING=/etc/apt/keyrings/cri-o-apt-keyring.asc   # armoured key; apt accepts .asc as-is
 write_file /etc/apt/sources.list.d/cri-o.list \
   "deb [signed-by=$KEYRING] https://download.opensuse.org/repositories/isv:/cri-o:/stable:/$CRIO_VERSION/deb/ /
 "
 mkdir -p "${ROOT}/etc/apt/keyrings"
 run curl -fsSL ${PROXY:+--proxy "$PROXY"} \
   "https://download.opensuse.org/repositories/isv:/cri-o:/stable:/$CRIO_VERSION/deb/Release.key" \
-  -o "${ROOT}/etc/apt/keyrings/cri-o-apt-keyring.asc" || warn "could not fetch the CRI-O key"
+  -o "${ROOT}${KEYRING}" || warn "could not fetch the CRI-O key"
 if [[ -n "$PROXY" ]]; then
   write_file /etc/apt/apt.conf.d/95kgc-proxy "Acquire::http::Proxy \"$PROXY\";
 Acquire::https::Proxy \"$PROXY\";

@@ -1,7 +1,9 @@
 #!/usr/bin/env bash
 # MI355X GPU enablement for a CRI-O node (replaces the reference's NVIDIA
 # gpu-crio-setup.sh:138-154).  One injection mechanism, no runtime conflicts:
-#   1. conmon + crun present (crun >= 1.21, the version the reference needed)
+#   1. conmon + crun >= 1.21 (the version the reference needed): the newest crun found
+#      (/usr/local first, then PATH), else apt, else a source build of crun 1.21;
+#      the detected path goes into the crun runtime handler and the shim's environment
 #   2. amd node tools installed: amd-container-runtime (OCI shim), amd-container-hook,
 #      amd-ctk, amdgpu-topo, libamdgpu_topo.so (built by native/build.sh)
 #   3. CRI-O runtime handler "amd" -> amd-container-runtime (amd-ctk runtime configure);
@@ -46,10 +48,47 @@ apt_install() {
   run apt-get install -y "$@"
 }
 
+CRUN_MIN=1.21               # older distro crun broke pods ("unknown version specified",
+CRUN_PATH=""                # reference old_README.md:774,1186-1199; gpu-crio-setup.sh:43-56)
+
+# version_ge A B: A >= B in version order
+version_ge() { [[ "$(printf '%s\n%s\n' "$2" "$1" | sort -V | head -n1)" == "$2" ]]; }
+
+crun_version() {    # "crun version 1.21" -> 1.21 (empty when crun is missing / unparsable)
+  local c="${1:-crun}"
+  "$c" --version 2>/dev/null | awk 'NR==1 && $2=="version" {print $3}'
+}
+
+find_crun() {       # newest usable crun: the source build in /usr/local wins over the distro's
+  local c
+  for c in /usr/local/bin/crun "$(command -v crun 2>/dev/null)"; do
+    [[ -n "$c" && -x "$c" ]] || continue
+    local v; v=$(crun_version "$c")
+    if [[ -n "$v" ]] && version_ge "$v" "$CRUN_MIN"; then CRUN_PATH="$c"; return 0; fi
+  done
+  return 1
+}
+
+build_crun() {      # source build of crun $CRUN_MIN into /usr/local (cwd untouched)
+  local src="${CRUN_SRC_DIR:-/usr/local/src/crun-$CRUN_MIN}"
+  log "building crun $CRUN_MIN from source in $src"
+  apt_install git make gcc automake autoconf libtool pkg-config libsystemd-dev libcap-dev \
+    libseccomp-dev libyajl-dev go-md2man python3 || warn "crun build deps not installed"
+  run rm -rf "$src"
+  run git clone --depth 1 --branch "$CRUN_MIN" https://github.com/containers/crun.git "$src" \
+    || return 1
+  run bash -c "cd '$src' && ./autogen.sh && ./configure --prefix=/usr/local && make -j\$(nproc) && make install"
+}
+
 install_runtime_deps() {
   have_cmd conmon || apt_install conmon || warn "conmon missing"
-  if ! have_cmd crun; then
-    apt_install crun || warn "crun missing: build crun >= 1.21 from source"
+  find_crun && { log "crun $(crun_version "$CRUN_PATH") at $CRUN_PATH"; return 0; }
+  apt_install crun || true
+  find_crun && { log "crun $(crun_version "$CRUN_PATH") at $CRUN_PATH"; return 0; }
+  build_crun || warn "crun $CRUN_MIN source build failed"
+  if ! find_crun; then
+    CRUN_PATH=$(command -v crun 2>/dev/null || echo /usr/local/bin/crun)
+    warn "no crun >= $CRUN_MIN found; configuring $CRUN_PATH anyway"
   fi
 }
 
@@ -70,13 +109,16 @@ CTK() { run "$BIN_SRC/amd-ctk" "$@"; }
 configure_crio() {
   local args=(runtime configure --runtime=crio --config="${ROOT}/etc/crio/crio.conf.d/99-amd.conf"
               --runtime-path="$PREFIX/bin/amd-container-runtime")
+  # the shim execs this crun (not whatever crun is first in CRI-O's PATH)
+  write_file /etc/default/amd-container-runtime "AMD_CONTAINER_RUNTIME_LOWLEVEL=$CRUN_PATH
+"
   [[ "$SET_DEFAULT" == "1" ]] && args+=(--set-as-default)
   CTK "${args[@]}"
   write_file /etc/crio/crio.conf.d/98-crun-default.conf '[crio.runtime]
 default_runtime = "crun"
 
 [crio.runtime.runtimes.crun]
-runtime_path = "/usr/bin/crun"
+runtime_path = "'"$CRUN_PATH"'"
 runtime_type = "oci"
 runtime_root = "/run/crun"
 '

@@ -133,12 +133,15 @@ $'net.bridge.bridge-nf-call-iptables  = 1\nnet.bridge.bridge-nf-call-ip6tables =
 install_k8s_apt() {
   local minor; minor=$(kube_minor "$KUBE_VERSION")
   log "installing kubelet/kubeadm/kubectl from pkgs.k8s.io $minor"
+  # apt reads an ASCII-armoured key directly when the file ends in .asc, so the key is
+  # stored exactly where signed-by points (no gpg --dearmor step to get out of sync)
+  local keyring=/etc/apt/keyrings/kubernetes-apt-keyring.asc
   write_file /etc/apt/sources.list.d/kubernetes.list \
-    "deb [signed-by=/etc/apt/keyrings/kubernetes-apt-keyring.gpg] https://pkgs.k8s.io/core:/stable:/${minor}/deb/ /
+    "deb [signed-by=${keyring}] https://pkgs.k8s.io/core:/stable:/${minor}/deb/ /
 "
   mkdir -p "${ROOT}/etc/apt/keyrings"
   run curl -fsSL ${PROXY:+--proxy "$PROXY"} "https://pkgs.k8s.io/core:/stable:/${minor}/deb/Release.key" \
-    -o "${ROOT}/etc/apt/keyrings/kubernetes-apt-keyring.asc" || warn "could not fetch the k8s apt key"
+    -o "${ROOT}${keyring}" || warn "could not fetch the k8s apt key"
   run apt-get update -y || warn "apt-get update failed"
   run apt-get install -y kubelet kubeadm kubectl || die "installing kubeadm failed"
   run apt-mark hold kubelet kubeadm kubectl || true
@@ -173,10 +176,13 @@ init_control_plane() {
               --pod-network-cidr "$POD_CIDR")
   [[ -n "$CP_ENDPOINT" ]] && args+=(--control-plane-endpoint "$CP_ENDPOINT" --upload-certs)
   log "kubeadm ${args[*]}"
-  if [[ "$DRY_RUN" == "1" ]]; then run kubeadm "${args[@]}"; return 0; fi
-  kubeadm "${args[@]}" 2>&1 | tee "$logf"
-  grep -qE 'kubeadm join .* --token' "$logf" || die "kubeadm init did not print a join command (see $logf)"
-  post_init_kubeconfig
+  if [[ "$DRY_RUN" == "1" ]]; then
+    run kubeadm "${args[@]}"       # and keep going: the dry run prints the post-init calls too
+  else
+    kubeadm "${args[@]}" 2>&1 | tee "$logf"
+    grep -qE 'kubeadm join .* --token' "$logf" || die "kubeadm init did not print a join command (see $logf)"
+    post_init_kubeconfig
+  fi
   local kc=(kubectl --kubeconfig "${ROOT}/etc/kubernetes/admin.conf")
   if [[ "$CNI" == "calico" ]]; then
     run "${kc[@]}" apply -f "https://raw.githubusercontent.com/projectcalico/calico/${CALICO_VERSION}/manifests/calico.yaml" \

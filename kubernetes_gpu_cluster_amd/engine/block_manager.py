@@ -7,8 +7,13 @@ Block ids index the per-layer cache tensors ``k_cache[nb, nkv, bs, d]`` /
 - Sized for 288 GB HBM: block tables are int32 (up to 2^31 blocks), and the free list is a stack (O(1) allocate/free).
 
 Prefix caching (vLLM's automatic prefix caching, on by default in its V1 engine):
-- A FULL block whose token ids are all known is content-addressed. Its key is
-  ``hash((parent block's key, its block_size token ids))``, so one key names a whole prefix.
+- A FULL block whose token ids are all known is content-addressed. Its key is a 128-bit
+  keyed BLAKE2b of (parent block's key, its block_size token ids), so one key names a whole
+  prefix. The BLAKE2b key is a random per-process salt: keys cannot be precomputed by a
+  client, unlike Python's unseeded ``hash()`` of an int tuple (the vLLM CVE-2025-25183 class).
+- A hit is verified, not trusted: every cached block keeps its parent key and token ids, and
+  a lookup whose stored (parent key, tokens) differ from the sequence's stops there and the
+  rest of the prompt is recomputed.
 - Blocks are reference counted.
   - A sequence admitted with a prompt whose leading full blocks are cached takes references on those blocks. It starts computing after them, and the prefill kernel reads them as context, exactly like a chunked-prefill continuation.
   - A block whose last reference goes away keeps its contents and its key. It moves to an LRU list of evictable blocks.
@@ -18,6 +23,8 @@ Prefix caching (vLLM's automatic prefix caching, on by default in its V1 engine)
 from __future__ import annotations
 
 import collections
+import hashlib
+import os
 
 import numpy as np
 
@@ -37,11 +44,14 @@ class BlockManager:
         self.free_slots: list[int] = list(range(max_seqs - 1, -1, -1))
         self.prefix_caching = enable_prefix_caching
         self.ref = np.zeros(num_blocks, dtype=np.int32) if enable_prefix_caching else None
-        self.key_of: dict[int, int] = {}                       # cached block -> prefix key
-        self.block_of: dict[int, int] = {}                     # prefix key -> cached block
+        self.key_of: dict[int, bytes] = {}                     # cached block -> prefix key
+        self.block_of: dict[bytes, int] = {}                   # prefix key -> cached block
+        self.content_of: dict[int, tuple] = {}                 # cached block -> (parent key, toks)
+        self._salt = os.urandom(16)
         self.evictable: collections.OrderedDict[int, None] = collections.OrderedDict()
         self.hit_tokens = 0                                    # prefix-cache statistics
         self.query_tokens = 0
+        self.collisions = 0
 
     # ---------------------------------------------------------------- capacity
     @property
@@ -67,6 +77,7 @@ class BlockManager:
             return self.free.pop()
         b, _ = self.evictable.popitem(last=False)          # least recently freed
         key = self.key_of.pop(b)
+        self.content_of.pop(b, None)
         if self.block_of.get(key) == b:
             del self.block_of[key]
         return b
@@ -106,7 +117,12 @@ class BlockManager:
         seq.num_registered = 0
 
     # ---------------------------------------------------------------- prefix caching
-    def _keys(self, seq: Sequence, n_full: int) -> list[int]:
+    def block_key(self, parent: bytes, toks) -> bytes:
+        h = hashlib.blake2b(parent, digest_size=16, key=self._salt)
+        h.update(np.asarray(toks, dtype=np.int64).tobytes())
+        return h.digest()
+
+    def _keys(self, seq: Sequence, n_full: int) -> list[bytes]:
         """Prefix keys of seq's first n_full blocks (memoised on the sequence; its token
         ids never change, so the keys stay valid across preemptions)."""
         keys = seq.block_keys
@@ -114,7 +130,7 @@ class BlockManager:
         while len(keys) < n_full:
             i = len(keys)
             toks = seq.tokens_slice(i * bs, (i + 1) * bs)
-            keys.append(hash((keys[-1] if keys else None, tuple(toks))))
+            keys.append(self.block_key(keys[-1] if keys else b"", toks))
         return keys[:n_full]
 
     def cached_prefix_blocks(self, seq: Sequence) -> list[int]:
@@ -125,9 +141,15 @@ class BlockManager:
         # never key over a token id still pending on the GPU
         n_full = min(seq.num_tokens - 1, seq.num_tokens - seq.num_pending) // self.block_size
         hits = []
-        for key in self._keys(seq, n_full):
+        bs = self.block_size
+        keys = self._keys(seq, n_full)
+        for i, key in enumerate(keys):
             b = self.block_of.get(key)
             if b is None:
+                break
+            parent = keys[i - 1] if i else b""
+            if self.content_of.get(b) != (parent, tuple(seq.tokens_slice(i * bs, (i + 1) * bs))):
+                self.collisions += 1          # key matched, content did not: recompute
                 break
             hits.append(b)
         return hits
@@ -169,12 +191,15 @@ class BlockManager:
         if n_full <= seq.num_registered:
             return
         keys = self._keys(seq, n_full)
+        bs = self.block_size
         for i in range(seq.num_registered, n_full):
             b = seq.block_ids[i]
             if b in self.key_of or keys[i] in self.block_of:
                 continue        # a prefix hit (already published), or the same content elsewhere
             self.key_of[b] = keys[i]
             self.block_of[keys[i]] = b
+            self.content_of[b] = (keys[i - 1] if i else b"",
+                                  tuple(seq.tokens_slice(i * bs, (i + 1) * bs)))
         seq.num_registered = n_full
 
     def hit_rate(self) -> float:

@@ -96,7 +96,7 @@ class Sequence:
         self.stream = None
         self.num_pending = 0                  # trailing sampled tokens still on the GPU
         self.proc_slot = -1                   # slot whose penalty statistics are built
-        self.block_keys: list[int] = []       # prefix-cache keys of its full blocks
+        self.block_keys: list[bytes] = []       # prefix-cache keys of its full blocks
         self.num_registered = 0               # leading blocks published to the prefix cache
 
     @property

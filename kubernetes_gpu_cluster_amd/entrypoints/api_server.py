@@ -466,7 +466,8 @@ def _serve(ns, cfg: EngineConfig, connect=None, core_proc=None, sock=None) -> No
     else:
         from .engine_core import EngineCoreClient
         eng = EngineCoreClient(cfg, connect=connect, core_proc=core_proc)
-    tok = get_tokenizer(cfg.model, eng.engine.mcfg, cfg.tokenizer)
+    tok = get_tokenizer(cfg.model, eng.engine.mcfg, cfg.tokenizer,
+                        allow_synthetic=cfg.random_init)
     name = cfg.served_model_name or cfg.model
     app = build_app(eng, tok, name, eng.engine.max_model_len)
     server = uvicorn.Server(uvicorn.Config(app, host=ns.host, port=ns.port,
@@ -492,6 +493,10 @@ def main(argv=None) -> None:
     ns = make_parser().parse_args(argv)
     ns.model = ns.model or ns.model_tag or "llama-3-8b"
     cfg = config_from_args(ns)
+    # fail before any engine process or GPU is touched: a missing hostPath checkpoint
+    # exits non-zero so the pod crash-loops instead of serving random tokens
+    from ..models import check_weights
+    check_weights(cfg.model, cfg.random_init)
     n = ns.api_server_count or min(4, max(1, (os.cpu_count() or 1) // 4))
     if n == 1 or ns.engine_in_process:
         _serve(ns, cfg)

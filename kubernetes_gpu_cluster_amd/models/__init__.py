@@ -126,13 +126,38 @@ def iter_safetensors(path: str) -> Iterator[tuple[str, torch.Tensor]]:
                 yield k, fh.get_tensor(k)
 
 
+class WeightsNotFoundError(FileNotFoundError):
+    """The model names a checkpoint that is not there and random weights were not asked for.
+
+    A pod whose hostPath mount failed (``values-01-minimal-example3.yaml:22-30``) must
+    crash-loop, not serve random tokens with HTTP 200."""
+
+
+def check_weights(model_name: str, random_weights: bool) -> Optional[str]:
+    """Resolve the weights directory; raise unless it holds safetensors or random
+    weights were requested (``--load-format dummy`` / ``--random-init``)."""
+    _, wdir = resolve_model(model_name)
+    if random_weights:
+        return wdir
+    if wdir is None:
+        raise WeightsNotFoundError(
+            f"model {model_name!r} resolves to a built-in architecture preset with no "
+            f"checkpoint: pass --load-format dummy (or --random-init) for random weights, "
+            f"or point the model at a directory with config.json + *.safetensors")
+    if not glob.glob(os.path.join(wdir, "*.safetensors")):
+        raise WeightsNotFoundError(f"no *.safetensors under {wdir!r} (and random weights were "
+                                   f"not requested)")
+    return wdir
+
+
 def load_model(model_name: str, dtype=torch.bfloat16, device=None, random_weights: bool = False,
                seed: int = 0, cfg_override: Optional[dict] = None):
-    cfg, wdir = resolve_model(model_name)
+    cfg, _ = resolve_model(model_name)
+    wdir = check_weights(model_name, random_weights)
     if cfg_override:
         cfg = cfg.shrink(**cfg_override)
     model = build_model(cfg, dtype, device)
-    if random_weights or wdir is None or not glob.glob(os.path.join(wdir, "*.safetensors")):
+    if random_weights:
         random_init(model, seed)
     else:
         model.load_weights(iter_safetensors(wdir))
@@ -141,4 +166,5 @@ def load_model(model_name: str, dtype=torch.bfloat16, device=None, random_weight
 
 
 __all__ = ["PRESETS", "ModelConfig", "resolve_model", "build_model", "random_init",
-           "full_state_dict_random", "load_model", "iter_safetensors"]
+           "full_state_dict_random", "load_model", "iter_safetensors", "check_weights",
+           "WeightsNotFoundError"]

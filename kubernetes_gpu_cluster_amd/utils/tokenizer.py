@@ -79,8 +79,14 @@ class HFTokenizer:
         return SyntheticTokenizer.apply_chat_template(self, messages, add_generation_prompt)
 
 
-def get_tokenizer(model: str, mcfg, tokenizer: Optional[str] = None):
+def get_tokenizer(model: str, mcfg, tokenizer: Optional[str] = None,
+                  allow_synthetic: bool = True):
+    """``allow_synthetic=False`` (the API server with a real checkpoint) raises instead of
+    falling back to the byte-level tokenizer, so a half-mounted model dir fails loudly."""
     for path in (tokenizer, model):
         if path and os.path.isfile(os.path.join(path, "tokenizer.json")):
             return HFTokenizer(path)
+    if not allow_synthetic:
+        raise FileNotFoundError(f"no tokenizer.json in {tokenizer or model!r}; pass --tokenizer "
+                                f"DIR or --load-format dummy for a synthetic byte tokenizer")
     return SyntheticTokenizer(mcfg.vocab_size, mcfg.eos_token_id, mcfg.bos_token_id)

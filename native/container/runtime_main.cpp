@@ -57,9 +57,22 @@ std::string find_in_path(const std::string& name) {
   return "";
 }
 
+// KEY=VALUE lines of the node defaults file written by gpu-crio-setup.sh (CRI-O starts
+// runtimes with its own environment, so the detected crun >= 1.21 path lives here).
+std::string node_default(const std::string& key) {
+  const char* f = std::getenv("AMD_CONTAINER_RUNTIME_DEFAULTS");
+  std::ifstream in(f && *f ? f : "/etc/default/amd-container-runtime");
+  std::string line;
+  while (std::getline(in, line))
+    if (line.rfind(key + "=", 0) == 0) return line.substr(key.size() + 1);
+  return "";
+}
+
 std::string lowlevel_runtime() {
   if (const char* e = std::getenv("AMD_CONTAINER_RUNTIME_LOWLEVEL"))
     if (*e) return e;
+  const std::string d = node_default("AMD_CONTAINER_RUNTIME_LOWLEVEL");
+  if (!d.empty() && ::access(d.c_str(), X_OK) == 0) return d;
   for (const char* r : {"crun", "runc"}) {
     const std::string p = find_in_path(r);
     if (!p.empty()) return p;

@@ -240,6 +240,52 @@ def test_prefix_cache_block_manager():
     bm.check_invariants([c, d])
 
 
+def test_prefix_cache_forced_collision_recomputes():
+    """Every key collides: a prompt with different tokens must not reuse another
+    prompt's KV (verified hit), and the same prompt still hits."""
+    bm = BlockManager(16, 4, 4, 8, enable_prefix_caching=True)
+    bm.block_key = lambda parent, toks: b"\x00" * 16          # worst case: one key for all
+    a = _seq("a", 10)
+    bm.allocate(a, 10)
+    a.num_computed = 10
+    bm.register_full_blocks(a, a.num_tokens)
+    other = Sequence("o", list(range(50, 61)), SamplingParams())
+    assert bm.cached_prefix_blocks(other) == []
+    assert bm.collisions == 1
+    same = Sequence("s", list(range(3, 7)) + [99] * 7, SamplingParams())
+    assert bm.cached_prefix_blocks(same) == a.block_ids[:1]   # block 0 matches, block 1 not
+
+
+def test_prefix_cache_keys_are_salted_per_process():
+    a = BlockManager(8, 4, 2, 4, enable_prefix_caching=True)
+    b = BlockManager(8, 4, 2, 4, enable_prefix_caching=True)
+    assert a.block_key(b"", [1, 2, 3, 4]) != b.block_key(b"", [1, 2, 3, 4])
+    assert len(a.block_key(b"", [1, 2, 3, 4])) == 16
+
+
+def test_missing_weights_refuse_to_start(tmp_path):
+    """No silent random init: a preset name, a preset-basename path that does not exist
+    (failed hostPath mount) or a dir without safetensors all fail unless random weights
+    are requested explicitly (--load-format dummy)."""
+    from kubernetes_gpu_cluster_amd.models import WeightsNotFoundError, check_weights
+    from kubernetes_gpu_cluster_amd.entrypoints import api_server
+    for name in ("qwen3-0.6b", "/models/Qwen3-0.6B", "meta-llama/Meta-Llama-3-8B"):
+        with pytest.raises(WeightsNotFoundError):
+            check_weights(name, random_weights=False)
+        check_weights(name, random_weights=True)
+    (tmp_path / "config.json").write_text('{"model_type": "llama", "num_hidden_layers": 1, '
+                                          '"hidden_size": 64, "num_attention_heads": 2, '
+                                          '"intermediate_size": 128, "vocab_size": 256}')
+    with pytest.raises(WeightsNotFoundError):
+        check_weights(str(tmp_path), random_weights=False)
+    with pytest.raises(WeightsNotFoundError):          # the server exits before any engine
+        api_server.main(["/models/Qwen3-0.6B", "--device", "cpu"])
+    with pytest.raises(WeightsNotFoundError):
+        _llm_plain = __import__("kubernetes_gpu_cluster_amd.engine.llm_engine",
+                                fromlist=["LLM"]).LLM
+        _llm_plain("tiny-llama", device="cpu", dtype="float32", max_model_len=64)
+
+
 def test_engine_prefix_cache_hits_and_parity(monkeypatch):
     """Shared-prefix prompts: the second wave reuses cached blocks (fewer computed
     tokens) and produces exactly the tokens of an engine without prefix caching."""

@@ -125,11 +125,21 @@ def test_hook_dry_run(tmp_path):
     r = run("amd-container-hook", "prestart", "--root", root, "--dry-run",
             input=json.dumps({"ociVersion": "1.0.2", "id": "c", "pid": 1, "bundle": b}))
     lines = r.stdout.strip().splitlines()
-    assert lines[0].endswith("/rootfs/dev/kfd c 235 0")
-    assert len(lines) == 5
+    # the container /dev tmpfs only exists in the container's mount namespace: the hook
+    # enters it (state.pid) before creating any node
+    assert lines[0] == "setns /proc/1/ns/mnt"
+    assert lines[1].endswith("/rootfs/dev/kfd c 235 0")
+    assert len(lines) == 6
+    r = run("amd-container-hook", "createContainer", "--root", root, "--dry-run",
+            input=json.dumps({"pid": 7, "bundle": b}))
+    assert not r.stdout.startswith("setns")      # already in the container namespace
     r = run("amd-container-hook", "prestart", "--root", root, "--dry-run",
             input=json.dumps({"bundle": make_bundle(str(tmp_path / "b2"))}))
     assert r.stdout == ""
+    # a GPU container without a pid cannot be served: fail instead of a silent no-op
+    r = subprocess.run([os.path.join(BIN, "amd-container-hook"), "prestart", "--root", root],
+                       input=json.dumps({"bundle": b}), capture_output=True, text=True)
+    assert r.returncode != 0 and "pid" in r.stderr
 
 
 def test_ctk(tmp_path):
@@ -146,6 +156,16 @@ def test_ctk(tmp_path):
     t = conf.read_text()
     assert 'default_runtime = "amd"' in t and "[crio.runtime.runtimes.amd]" in t
     assert 'runtime_path = "/usr/local/bin/amd-container-runtime"' in t
+    import tomli
+    run("amd-ctk", "runtime", "configure", "--runtime=crio", f"--config={conf}",
+        "--set-as-default", "--cdi.enabled=true")
+    doc = tomli.loads(conf.read_text())                    # a duplicate table would raise
+    rt = doc["crio"]["runtime"]
+    assert rt["enable_cdi"] is True and rt["default_runtime"] == "amd"
+    assert rt["runtimes"]["amd"]["runtime_type"] == "oci"
+    hooks = tmp_path / "99-amd-hooks.conf"
+    run("amd-ctk", "crio", "hooks-dir", f"--config={hooks}")
+    assert tomli.loads(hooks.read_text())["crio"]["runtime"]["hooks_dir"]
     run("amd-ctk", "hook", "install", "--hooks-dir", str(tmp_path / "hooks.d"))
     h = json.load(open(tmp_path / "hooks.d" / "oci-amd-hook.json"))
     assert h["stages"] == ["prestart"] and h["hook"]["args"] == ["amd-container-hook", "prestart"]

@@ -1,6 +1,7 @@
 """Node bootstrap scripts under stub binaries (systemctl, kubeadm, apt-get, kubectl, ...)
 with every written file redirected under ROOT."""
 import os
+import sys
 import subprocess
 
 import pytest
@@ -10,7 +11,8 @@ from fake_node import make_node
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SCRIPTS = os.path.join(REPO, "deploy", "scripts")
 STUBS = ["systemctl", "kubeadm", "apt-get", "apt-mark", "modprobe", "sysctl", "ss", "curl",
-         "kubectl", "crio", "crictl", "swapoff", "udevadm", "tar", "crun", "conmon", "chown"]
+         "kubectl", "crio", "crictl", "swapoff", "udevadm", "tar", "crun", "conmon", "chown",
+         "git"]
 
 
 @pytest.fixture()
@@ -20,6 +22,9 @@ def env(tmp_path):
     log = tmp_path / "calls.log"
     for s in STUBS:
         body = f'#!/bin/bash\necho "{s} $*" >> "{log}"\n'
+        if s == "curl":   # honour -o so the files the scripts download exist under ROOT
+            body += ('prev=""; for a in "$@"; do [[ "$prev" == "-o" ]] && '
+                     'echo "-----BEGIN PGP PUBLIC KEY BLOCK-----" > "$a"; prev="$a"; done\n')
         if s == "kubeadm":
             body += ('if [[ "$1" == init ]]; then echo "kubeadm join 10.0.0.1:6443 --token abc.def '
                      '--discovery-token-ca-cert-hash sha256:00"; fi\n')
@@ -126,6 +131,9 @@ def test_gpu_crio_setup(env):
     subprocess.run(["bash", os.path.join(REPO, "native", "build.sh")], check=True)
     make_node(str(root), n_gpus=8)
     sh("gpu-crio-setup.sh", "--with-hook", "--skip-apt", env=e)
+    import tomli
+    for f in (root / "etc/crio/crio.conf.d").iterdir():     # every drop-in must parse
+        tomli.loads(f.read_text())
     conf = (root / "etc/crio/crio.conf.d/99-amd.conf").read_text()
     assert "[crio.runtime.runtimes.amd]" in conf and "default_runtime" not in conf
     assert 'default_runtime = "crun"' in (root / "etc/crio/crio.conf.d/98-crun-default.conf").read_text()
@@ -191,3 +199,106 @@ def test_proxy_setup(env):
     c = calls(log)
     assert "systemctl restart privoxy" in c and "apt-get install -y privoxy" in c
     assert sh("proxy_setup.sh", env=e, check=False).returncode != 0
+
+
+def _signed_by(list_file):
+    import re
+    m = re.search(r"signed-by=([^\]\s]+)", list_file.read_text())
+    assert m, list_file.read_text()
+    return m.group(1)
+
+
+def test_apt_signed_by_keys_exist(env):
+    """apt rejects a repo whose signed-by file is missing: every list must point at the
+    exact file the script downloaded the key to."""
+    e, root, log = env
+    sh("k8s_setup.sh", "--yes", "--role=cp", env=e)
+    sh("crio_setup.sh", env=e)
+    for lst in ("kubernetes.list", "cri-o.list"):
+        key = _signed_by(root / "etc/apt/sources.list.d" / lst)
+        assert (root / key.lstrip("/")).is_file(), f"{lst}: signed-by {key} not written"
+        assert key.endswith(".asc")   # armoured key: apt needs the .asc suffix to read it
+
+
+def _fake_crun(dir_, version):
+    dir_.mkdir(parents=True, exist_ok=True)
+    c = dir_ / "crun"
+    c.write_text(f'#!/bin/bash\n[[ "$1" == --version ]] && echo "crun version {version}"\n')
+    c.chmod(0o755)
+    return c
+
+
+def test_gpu_crio_crun_version_gate(env, tmp_path):
+    """crun >= 1.21 is used where it is found (its path goes into the crun handler and the
+    shim's defaults); an older crun triggers the source build of 1.21 (reference
+    gpu-crio-setup.sh:43-56) with the caller's cwd untouched."""
+    e, root, log = env
+    new = _fake_crun(tmp_path / "newbin", "1.22")
+    e2 = dict(e, PATH=f"{new.parent}:{e['PATH']}")
+    sh("gpu-crio-setup.sh", "--skip-apt", "--no-kubectl", env=e2)
+    conf = (root / "etc/crio/crio.conf.d/98-crun-default.conf").read_text()
+    import tomli
+    assert tomli.loads(conf)["crio"]["runtime"]["runtimes"]["crun"]["runtime_path"] == str(new)
+    assert f"AMD_CONTAINER_RUNTIME_LOWLEVEL={new}" in \
+        (root / "etc/default/amd-container-runtime").read_text()
+    assert not any(x.startswith("git clone") for x in calls(log))
+    old = _fake_crun(tmp_path / "oldbin", "1.14.1")
+    e3 = dict(e, PATH=f"{old.parent}:{e['PATH']}", CRUN_SRC_DIR=str(tmp_path / "crun-src"))
+    r = sh("gpu-crio-setup.sh", "--skip-apt", "--no-kubectl", env=e3)
+    clone = [x for x in calls(log) if x.startswith("git clone")]
+    assert clone and "--branch 1.21" in clone[0] and "containers/crun" in clone[0]
+    assert "no crun >= 1.21" in r.stderr                 # stub build produced nothing
+
+
+def test_bringup_dry_run_full_ordered_log(env):
+    """bringup.sh --dry-run: every step of the single-node bring-up, in order."""
+    e, root, log = env
+    r = sh("bringup.sh", "--single-node", "--dry-run",
+           "--values=" + os.path.join(REPO, "deploy/values/values-llama3-8b-tp1.yaml"), env=e)
+    out = r.stdout
+    order = ["step 1: CRI-O", "apt-get install -y cri-o",
+             "step 2: Kubernetes", "kubeadm init", "taint nodes --all",
+             "step 3: native", "native/build.sh",
+             "step 4: GPU enablement", "amd-ctk runtime configure",
+             "step 5:", "wait for amd.com/gpu on the node",
+             "step 6:", "k8s.render -f", "| kubectl apply -f -",
+             "step 7:", "wait for serving-engine Deployments", "wait for vllm-router-service",
+             "step 8:", "port-forward svc/vllm-router-service 30080:80",
+             "curl -sf http://127.0.0.1:30080/v1/models", "bring-up complete"]
+    pos = 0
+    for needle in order:
+        i = out.find(needle, pos)
+        assert i >= 0, f"{needle!r} missing or out of order in:\n{out}"
+        pos = i
+    assert calls(log) == [] or not any(c.startswith("kubeadm init") for c in calls(log))
+
+
+def test_bringup_waits_and_smokes(env, tmp_path):
+    """Deploy + wait + smoke against stub kubectl/curl (node already bootstrapped)."""
+    e, root, log = env
+    stub = tmp_path / "stubs2"
+    stub.mkdir()
+    (stub / "kubectl").write_text(f'''#!/bin/bash
+echo "kubectl $*" >> "{log}"
+case "$*" in
+  *"get nodes"*) echo 8 ;;
+  *"get endpoints"*) echo 10.0.0.5 ;;
+  "apply -f -") cat > "{tmp_path}/applied.yaml" ;;
+  *port-forward*) sleep 30 ;;
+esac
+''')
+    (stub / "curl").write_text(f'''#!/bin/bash
+echo "curl $*" >> "{log}"
+prev=""; for a in "$@"; do [[ "$prev" == "-o" ]] && echo '{{"data": [{{"id": "llama-3-8b"}}]}}' > "$a"; prev="$a"; done
+exit 0
+''')
+    for f in stub.iterdir():
+        f.chmod(0o755)
+    e2 = dict(e, PATH=f"{stub}:{e['PATH']}", WAIT_INTERVAL="0", PYTHON=sys.executable)
+    r = sh("bringup.sh", "--skip-node-setup", "--port=31999", env=e2)
+    assert "serving model: llama-3-8b" in r.stdout
+    applied = (tmp_path / "applied.yaml").read_text()
+    assert "vllm-router-service" in applied and "amd.com/gpu" in applied
+    c = calls(log)
+    assert any("rollout status deployment" in x for x in c)
+    assert any("/v1/completions" in x for x in c)
