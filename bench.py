@@ -67,9 +67,9 @@ def _k9_plan() -> dict:
     return gemm.plan()
 
 
-def _splitk_plan() -> dict:
+def _k9m_plan() -> dict:
     from kubernetes_gpu_cluster_amd.ops import gemm
-    return gemm.splitk_plan()
+    return gemm.dgemm_plan()
 
 
 def run_wave(engine, args, wave: int, rank: int):
@@ -194,7 +194,7 @@ def main():
             "p50_tpot_ms": round(statistics.median(tpots) * 1e3, 3) if tpots else None,
             "engine_steps": steps,
             "k9_skinny_gemm_shapes": len(_k9_plan()),
-            "splitk_gemm_shapes": len(_splitk_plan()),
+            "k9m_gemm_shapes": len(_k9m_plan()),
             "config": {"model": args.model, "global_batch": args.num_prompts * replicas,
                        "seq_len": args.input_len + args.output_len, "input_len": args.input_len,
                        "output_len": args.output_len,

@@ -91,6 +91,7 @@ bool kv_is_fp8(const Tensor& k_cache, const Tensor& v_cache, at::ScalarType act)
   return false;
 }
 
+// qkv: [T, >= (nq+2nkv)*d] in q_out's dtype, or the K9m split-K slices fp32 [S, T, N]
 void rope_kv_write(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor q_out, Tensor k_cache,
                    Tensor v_cache, Tensor slot_mapping, std::optional<Tensor> q_norm_w,
                    std::optional<Tensor> k_norm_w, int64_t nq, int64_t nkv, int64_t d,
@@ -98,9 +99,24 @@ void rope_kv_write(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor q_out, T
   check_gpu(qkv, "qkv");
   c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
   TORCH_CHECK(d % 16 == 0 && d <= 256, "kgc.rope_kv_write: head_dim");
-  const int64_t T = qkv.size(0);
-  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1 && qkv.size(1) >= (nq + 2 * nkv) * d &&
-              qkv.stride(0) % 8 == 0, "kgc.rope_kv_write: qkv [T, (nq+2nkv)*d]");
+  const bool slices = qkv.dim() == 3;
+  const int64_t T = slices ? qkv.size(1) : qkv.size(0);
+  int64_t S = 0, ss = 0, stride;
+  if (slices) {
+    TORCH_CHECK(qkv.scalar_type() == at::kFloat && qkv.is_contiguous() &&
+                qkv.size(2) >= (nq + 2 * nkv) * d && qkv.size(2) % 8 == 0 && qkv.size(0) >= 1,
+                "kgc.rope_kv_write: slices fp32 [S, T, (nq+2nkv)*d] contiguous");
+    S = qkv.size(0);
+    ss = qkv.stride(0);
+    stride = qkv.stride(1);
+  } else {
+    TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1 && qkv.size(1) >= (nq + 2 * nkv) * d &&
+                qkv.stride(0) % 8 == 0, "kgc.rope_kv_write: qkv [T, (nq+2nkv)*d]");
+    TORCH_CHECK(q_out.scalar_type() == qkv.scalar_type(), "kgc.rope_kv_write: dtype");
+    stride = qkv.stride(0);
+  }
+  TORCH_CHECK(q_out.scalar_type() == at::kBFloat16 || q_out.scalar_type() == at::kHalf,
+              "q_out bf16 / fp16");
   TORCH_CHECK(positions.scalar_type() == at::kLong && positions.numel() == T, "positions int64 [T]");
   TORCH_CHECK(slot_mapping.scalar_type() == at::kLong && slot_mapping.numel() == T, "slot_mapping int64 [T]");
   TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() && cos_sin.size(1) == d,
@@ -110,8 +126,7 @@ void rope_kv_write(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor q_out, T
               v_cache.dim() == 5 && k_cache.size(1) == nkv && k_cache.size(3) == d &&
               v_cache.size(3) == d && v_cache.size(4) == 8 &&
               v_cache.size(2) * 8 == k_cache.size(2), "kv cache layout");
-  const bool kv8 = kv_is_fp8(k_cache, v_cache, qkv.scalar_type());
-  TORCH_CHECK(q_out.scalar_type() == qkv.scalar_type(), "kgc.rope_kv_write: dtype");
+  const bool kv8 = kv_is_fp8(k_cache, v_cache, q_out.scalar_type());
   TORCH_CHECK(k_scale > 0 && v_scale > 0, "kv scales must be > 0");
   const void* qn = nullptr;
   const void* kn = nullptr;
@@ -120,7 +135,7 @@ void rope_kv_write(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor q_out, T
     qn = q_norm_w->data_ptr();
     kn = k_norm_w->data_ptr();
   }
-  kgc::launch_rope_kv_write(dt_code(qkv), qkv.data_ptr(), qkv.stride(0),
+  kgc::launch_rope_kv_write(dt_code(q_out), qkv.data_ptr(), stride, (int)S, ss,
                             positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
                             q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                             slot_mapping.data_ptr<int64_t>(), qn, kn, (int)T, (int)nq, (int)nkv,
@@ -343,6 +358,97 @@ void dense_gemm_splitk(Tensor Cs, Tensor A, Tensor W, int64_t bm) {
                                 stream());
 }
 
+// K9m mid-batch decode GEMM (LDS-DMA ring, XCD-mapped split-K, fused epilogues).
+// W: [N, K] for the row-major configs, [N/128, K/64, 8192] (dgemm_pack) for packed ones.
+static void dgemm_shape(const Tensor& W, bool packed, int64_t* N, int64_t* K) {
+  if (packed) {
+    TORCH_CHECK(W.dim() == 3 && W.is_contiguous() && W.size(2) == 128 * kgc::dgemm_block_k(),
+                "packed W [N/128, K/64, 8192] contiguous");
+    *N = W.size(0) * 128;
+    *K = W.size(1) * kgc::dgemm_block_k();
+  } else {
+    TORCH_CHECK(W.dim() == 2 && W.is_contiguous(), "W [N, K] contiguous");
+    *N = W.size(0);
+    *K = W.size(1);
+  }
+}
+
+void dgemm(Tensor C, Tensor X, Tensor W, int64_t cfg, int64_t epi) {
+  check_gpu(X, "X");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(X.device());
+  TORCH_CHECK(cfg >= 0 && cfg < kgc::dgemm_num_cfgs(), "unknown dgemm tile config");
+  int bm, bn, packed;
+  kgc::dgemm_cfg_info((int)cfg, &bm, &bn, &packed);
+  TORCH_CHECK(epi >= 0 && epi <= 2, "epi 0 (fp32 slices), 1 (out), 2 (silu pairs)");
+  TORCH_CHECK(W.scalar_type() == at::kBFloat16 || W.scalar_type() == at::kHalf, "bf16 / fp16");
+  int64_t N, K;
+  dgemm_shape(W, packed, &N, &K);
+  const int64_t bk = kgc::dgemm_block_k();
+  TORCH_CHECK(X.scalar_type() == W.scalar_type() && X.dim() == 2 && X.size(1) == K &&
+              X.stride(1) == 1 && X.stride(0) % 8 == 0 &&
+              reinterpret_cast<uintptr_t>(X.data_ptr()) % 16 == 0, "X [M, K] in W's dtype, "
+              "16-B aligned rows");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(W.data_ptr()) % 16 == 0, "W 16-B aligned");
+  const int64_t M = X.size(0);
+  TORCH_CHECK(N % bn == 0 && K % bk == 0 && K >= bk, "N % BN == 0, K % 64 == 0");
+  TORCH_CHECK(M <= (int64_t)1 << 20 && N < ((int64_t)1 << 31) / 4, "size limits");
+  int64_t S = 1, ss = 0;
+  if (epi == 0) {
+    TORCH_CHECK(C.scalar_type() == at::kFloat && C.dim() == 3 && C.is_contiguous() &&
+                C.size(1) == M && C.size(2) == N, "C fp32 contiguous [S, M, N]");
+    S = C.size(0);
+    ss = C.stride(0);
+    TORCH_CHECK(S >= 1 && S <= 32 && S <= K / bk, "1 <= S <= min(32, K / 64)");
+  } else {
+    TORCH_CHECK(C.scalar_type() == W.scalar_type() && C.dim() == 2 && C.is_contiguous() &&
+                C.size(0) == M && C.size(1) == (epi == 2 ? N / 2 : N),
+                "C [M, N] (epi 1) or [M, N/2] (epi 2), contiguous, W's dtype");
+  }
+  TORCH_CHECK((M + bm - 1) / bm * (N / bn) * S < ((int64_t)1 << 31), "grid too large");
+  if (M == 0) return;
+  kgc::launch_dgemm(dt_code(W), (int)cfg, (int)epi, C.data_ptr(), X.data_ptr(), W.data_ptr(),
+                    (int)M, (int)N, (int)K, X.stride(0), (int)S, ss, stream());
+}
+
+// P [N/128, K/64, 8192] <- W [N, K] re-laid out for the packed K9m configs
+void dgemm_pack(Tensor P, Tensor W, bool silu) {
+  check_gpu(W, "W");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(W.device());
+  TORCH_CHECK(W.dim() == 2 && W.is_contiguous(), "W [N, K] contiguous");
+  TORCH_CHECK(W.scalar_type() == at::kBFloat16 || W.scalar_type() == at::kHalf, "bf16 / fp16");
+  const int64_t N = W.size(0), K = W.size(1), bk = kgc::dgemm_block_k();
+  TORCH_CHECK(N % 128 == 0 && K % bk == 0 && (!silu || (N / 2) % 64 == 0), "N % 128, K % 64");
+  TORCH_CHECK(P.scalar_type() == W.scalar_type() && P.dim() == 3 && P.is_contiguous() &&
+              P.size(0) == N / 128 && P.size(1) == K / bk && P.size(2) == 128 * bk,
+              "P [N/128, K/64, 8192] contiguous, W's dtype");
+  TORCH_CHECK(P.device() == W.device(), "same device");
+  kgc::launch_dgemm_pack(dt_code(W), silu, P.data_ptr(), W.data_ptr(), (int)N, (int)K,
+                         stream());
+}
+
+std::vector<int64_t> dgemm_cfg_info(int64_t cfg) {
+  TORCH_CHECK(cfg >= 0 && cfg < kgc::dgemm_num_cfgs(), "unknown dgemm tile config");
+  int bm, bn, packed;
+  kgc::dgemm_cfg_info((int)cfg, &bm, &bn, &packed);
+  return {bm, bn, packed};
+}
+int64_t dgemm_num_cfgs() { return kgc::dgemm_num_cfgs(); }
+
+// profiling only: the packed 256 x 128 tile with its MFMAs / DMAs / one operand's DMAs removed
+void dgemm_ablate(Tensor C, Tensor X, Tensor W, int64_t mode) {
+  check_gpu(X, "X");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(X.device());
+  TORCH_CHECK(W.scalar_type() == at::kBFloat16 && X.scalar_type() == at::kBFloat16, "bf16");
+  int64_t N, K;
+  dgemm_shape(W, true, &N, &K);
+  const int64_t M = X.size(0);
+  TORCH_CHECK(X.dim() == 2 && X.is_contiguous() && X.size(1) == K, "X [M, K] contiguous");
+  TORCH_CHECK(C.scalar_type() == at::kFloat && C.dim() == 3 && C.is_contiguous() &&
+              C.size(1) == M && C.size(2) == N && C.size(0) <= K / 64, "C fp32 [S, M, N]");
+  kgc::launch_dgemm_ablate((int)mode, C.data_ptr<float>(), X.data_ptr(), W.data_ptr(), (int)M,
+                           (int)N, (int)K, X.stride(0), (int)C.size(0), C.stride(0), stream());
+}
+
 void splitk_reduce(Tensor out, Tensor Cs) {
   check_gpu(Cs, "Cs");
   c10::hip::HIPGuardMasqueradingAsCUDA g(Cs.device());
@@ -502,6 +608,11 @@ TORCH_LIBRARY(kgc, m) {
   m.def("moe_combine(Tensor(a!) out, Tensor y, Tensor topk_w) -> ()");
   m.def("dense_gemm_splitk(Tensor(a!) Cs, Tensor A, Tensor W, int bm) -> ()");
   m.def("splitk_reduce(Tensor(a!) out, Tensor Cs) -> ()");
+  m.def("dgemm(Tensor(a!) C, Tensor X, Tensor W, int cfg, int epi) -> ()");
+  m.def("dgemm_cfg_info(int cfg) -> int[]", &dgemm_cfg_info);
+  m.def("dgemm_num_cfgs() -> int", &dgemm_num_cfgs);
+  m.def("dgemm_ablate(Tensor(a!) C, Tensor X, Tensor W, int mode) -> ()");
+  m.def("dgemm_pack(Tensor(a!) P, Tensor W, bool silu) -> ()");
   m.def("splitk_reduce_silu(Tensor(a!) out, Tensor Cs) -> ()");
   m.def("splitk_add_rms_norm(Tensor(a!) out, Tensor Cs, Tensor(b!) residual, Tensor w, float eps) -> ()");
   m.def("ar_signal_bytes() -> int", &ar_signal_bytes);
@@ -532,6 +643,9 @@ TORCH_LIBRARY_IMPL(kgc, CUDA, m) {
   m.impl("moe_gemm", &moe_gemm);
   m.impl("moe_combine", &moe_combine);
   m.impl("dense_gemm_splitk", &dense_gemm_splitk);
+  m.impl("dgemm", &dgemm);
+  m.impl("dgemm_ablate", &dgemm_ablate);
+  m.impl("dgemm_pack", &dgemm_pack);
   m.impl("splitk_reduce", &splitk_reduce);
   m.impl("splitk_reduce_silu", &splitk_reduce_silu);
   m.impl("splitk_add_rms_norm", &splitk_add_rms_norm);

@@ -1,0 +1,520 @@
+// K9m: mid-batch decode GEMM for gfx950 (M = 65..512 rows, the batch-256 decode step).
+//
+//   C[M, N] = X[M, K] . W[N, K]^T      bf16 / f16 in, fp32 MFMA accumulation
+//
+// At M = 256 a decode projection sits at the HBM/MFMA ridge: every weight byte feeds 256
+// MACs, so the weights (read once, from HBM), the activation tile (re-read from L2 by
+// every column tile) and the MFMA pipe must all run near their rates at once.
+//   * 512-thread workgroups (8 waves, 4 (M) x 2 (N)), one per CU, BM = 128 / 256 rows x
+//     BN = 64 / 128 columns x BK = 64, mfma_f32_16x16x32 (the shape gfx950 clocks higher).
+//   * Both operands go HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave
+//     instruction) into a 3-slot ring, two K-steps in flight behind the one consumed; the
+//     ring is retired with a counted `s_waitcnt vmcnt(N)` and a raw s_barrier (never
+//     __syncthreads(), whose implicit vmcnt(0) would drain the ring every step).
+//   * LDS rows are 128 B (BK bf16) with a 16-B-chunk XOR swizzle (chunk ^ row % 8) applied
+//     on the SOURCE address (the DMA writes lane-linear) and on the ds_read_b128 address:
+//     conflict-free fragment reads for both operands.
+//   * PACKED weights (PK): the weight matrix is re-laid out once at load time as
+//     [N / BN][K / BK][BN x BK] tiles with the swizzle baked in, so each K-step of a
+//     column tile is ONE contiguous 16 KB block.  Measured (tools/dma_probe.hip): the
+//     row-major tile walk (128 rows x 128 B, rows 8 KB apart) streams HBM at ~4.4 TB/s,
+//     contiguous blocks at ~5.8 TB/s.
+//   * Each workgroup starts its K walk at its own step (wrapping), so the workgroups of an
+//     XCD do not all fetch the same activation lines at once (-5..9 % time at S = 1).
+//   * Split-K over a 1-D grid: workgroup L takes K-slice z = L % S, so with S | 8 every
+//     XCD (workgroups L, L+8, ... share one) streams ONE K-slice of X, which stays in that
+//     XCD's L2 for all its column tiles, while the weights stream from HBM exactly once.
+//   * Epilogues: EPI_PARTIAL writes fp32 slice z of [S, M, N] (summed by the consumer:
+//     splitk_add_rms_norm for o/down, splitk_reduce); EPI_OUT writes the tile in X's dtype
+//     (S = 1); EPI_SILU (S = 1) takes a merged [gate; up] weight whose tile rows alternate
+//     16-row groups of gate and up, so each lane holds gate and up of the same output
+//     column and writes silu(g) * u: the [M, 2I] gate_up activation never exists.
+// What did not pay (profiles/README.md, "K9m"): 32-deep K slots with a 6-slot ring (the
+// per-step barrier costs more than the deeper ring buys), 256 x 256 tiles, and activations
+// loaded straight into registers beside a 5-slot weight ring.
+// Reference parity: SURVEY.md §2.5 K9 (decode GEMMs of the vLLM image the reference
+// deploys, /root/reference/values-01-minimal-example2.yaml:6-7).
+#include "common.h"
+#include "launch.h"
+
+namespace kgc {
+
+namespace {
+
+constexpr int DG_THREADS = 512;     // 8 waves: 4 along M x 2 along N
+constexpr int DG_BK = 64, DG_NS = 3, DG_ROWB = 128;
+
+enum { EPI_PARTIAL = 0, EPI_OUT = 1, EPI_SILU = 2 };
+// ablation builds (tools/dgemm_bench.py --ablate): one K-step without its MFMAs, without
+// its DMAs, or without one operand's DMAs
+enum { ABL_NONE = 0, ABL_NO_MFMA = 1, ABL_NO_DMA = 2, ABL_NO_A = 3, ABL_NO_B = 4 };
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
+
+// AUX = 2: non-temporal (the weight stream, read once by one CU, must not evict the
+// activation slice every column tile of the XCD re-reads from L2)
+template <int AUX>
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)lds_wave_base, 16, 0, AUX);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait until at most min(D, younger) steps of L DMAs each are still in flight
+template <int L, int D>
+__device__ __forceinline__ void wait_younger(int younger) {
+  if (younger >= D) { wait_vm<D * L>(); return; }
+  if constexpr (D > 3) if (younger == 3) { wait_vm<3 * L>(); return; }
+  if constexpr (D > 2) if (younger == 2) { wait_vm<2 * L>(); return; }
+  if constexpr (D > 1) if (younger == 1) { wait_vm<L>(); return; }
+  wait_vm<0>();
+}
+
+__device__ __forceinline__ float silu_f(float g) { return g / (1.f + __expf(-g)); }
+
+// 16-B chunk position of (row, chunk) in a 128-B LDS row
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ (row & 7); }
+
+// weight row of B-tile row r (0..BN-1) for column tile nb; EPI_SILU interleaves gate / up
+template <int BN, int EPI>
+__device__ __forceinline__ int64_t weight_row(int nb, int r, int N) {
+  if constexpr (EPI == EPI_SILU) {
+    const int g = r >> 4;
+    return (int64_t)((g & 1) ? (N >> 1) : 0) + nb * (BN / 2) + (g >> 1) * 16 + (r & 15);
+  } else {
+    return (int64_t)nb * BN + r;
+  }
+}
+
+// LDW = 4: four extra loader waves issue every DMA and the 8 MFMA waves never stall on
+// DMA issue (one s_barrier per step for all 12 waves); LDW = 0: the MFMA waves issue too.
+template <typename T, int BM, int BN, int EPI, bool PK, int ABL = ABL_NONE, int LDW = 0>
+__global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
+    void* __restrict__ Cv, const T* __restrict__ X, const T* __restrict__ W, int M, int N,
+    int K, int64_t ldx, int S, int MB, int64_t slice_stride) {
+  constexpr int MT = BM / 4 / 16;                 // 16-row MFMA tiles per wave
+  constexpr int NT = BN / 2 / 16;                 // 16-col MFMA tiles per wave
+  constexpr int NIW = LDW > 0 ? LDW : 8;          // waves issuing DMAs
+  constexpr int LA = BM / 8 / NIW, LB = BN / 8 / NIW;   // 1-KiB DMAs per issuing wave per step
+  static_assert(LA * 8 * NIW == BM && LB * 8 * NIW == BN, "DMA split");
+  constexpr int L = LA + LB;
+  constexpr int A_BYTES = BM * DG_ROWB, SLOT_BYTES = (BM + BN) * DG_ROWB;
+  static_assert(DG_NS * SLOT_BYTES <= 163840, "LDS ring exceeds 160 KiB");
+  // ONE shared array for the whole ring (a second __shared__ object can make hipcc emit a
+  // vmcnt(0) before the first ds_read of every step)
+  __shared__ __attribute__((aligned(16))) char lds[DG_NS * SLOT_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool loader = LDW > 0 && wave >= 8;
+  const bool consumer = LDW == 0 || wave < 8;
+  const int iw = LDW > 0 ? wave - 8 : wave;       // index among the issuing waves
+  const int wm = (wave >> 1) & 3, wn = wave & 1;
+  const int z = blockIdx.x % S;
+  const int j = blockIdx.x / S;
+  const int mb = j % MB, nb = j / MB;
+  const int m0 = mb * BM;
+
+  // ---- DMA sources: lane l of instruction i fills LDS row 8i + l/8, 16-B slot l%8 with
+  // global chunk (l%8) ^ (row%8)  (row%8 == l/8): the swizzle lives in the source address
+  const int drow = lane >> 3, dchunk = (lane & 7) ^ drow;
+  const T* a_src[LA];
+#pragma unroll
+  for (int t = 0; t < LA; ++t) {
+    int r = m0 + (iw * LA + t) * 8 + drow;
+    r = r < M ? r : M - 1;                        // padded rows re-read the last row
+    a_src[t] = X + (int64_t)r * ldx + dchunk * 8;
+  }
+  const int nk_all = K / DG_BK;
+  const T* b_src[LB];
+#pragma unroll
+  for (int t = 0; t < LB; ++t) {
+    if constexpr (PK) {
+      // packed [N/BN][K/BK][BN*BK], swizzle baked in: linear 1-KiB pieces of the tile
+      b_src[t] = W + (int64_t)nb * nk_all * (BN * DG_BK) + (iw * LB + t) * 512 + lane * 8;
+    } else {
+      const int r = (iw * LB + t) * 8 + drow;
+      b_src[t] = W + weight_row<BN, EPI>(nb, r, N) * K + dchunk * 8;
+    }
+  }
+
+  const int kb0 = (int)((int64_t)nk_all * z / S);
+  const int nk = (int)((int64_t)nk_all * (z + 1) / S) - kb0;
+  // each workgroup starts its walk at its own step
+  const int rot = nk >= 4 ? (int)(((int64_t)j * 37) % nk) : 0;
+
+  auto issue = [&](int slot, int step) {
+    if constexpr (ABL == ABL_NO_DMA) return;
+    if (LDW > 0 && !loader) return;
+    char* sa = lds + slot * SLOT_BYTES;
+    char* sb = sa + A_BYTES;
+    int st = step + rot;
+    st = st >= nk ? st - nk : st;
+    const int kb = kb0 + st;
+    if constexpr (ABL != ABL_NO_A) {
+#pragma unroll
+      for (int t = 0; t < LA; ++t)
+        glds16<0>(a_src[t] + kb * DG_BK, sa + (iw * LA + t) * 1024);
+    }
+    if constexpr (ABL != ABL_NO_B) {
+      const int64_t bo = PK ? (int64_t)kb * (BN * DG_BK) : (int64_t)kb * DG_BK;
+#pragma unroll
+      for (int t = 0; t < LB; ++t) glds16<2>(b_src[t] + bo, sb + (iw * LB + t) * 1024);
+    }
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const int a_row0 = wm * (BM / 4) + fr;
+  const int b_row0 = wn * (BN / 2) + fr;
+
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  int slot = 0;
+  for (int it = 0; it < nk; ++it) {
+    // step `it` must have landed; step it + 1 (if issued) may stay in flight
+    if (LDW > 0 && !loader) {
+      // MFMA waves have no DMAs of their own: the barrier below orders them after the
+      // loaders' waits
+    } else if constexpr (ABL == ABL_NO_A) {
+      if (it + 1 < nk) wait_vm<LB>(); else wait_vm<0>();
+    } else if constexpr (ABL == ABL_NO_B) {
+      if (it + 1 < nk) wait_vm<LA>(); else wait_vm<0>();
+    } else if constexpr (ABL != ABL_NO_DMA) {
+      if (it + 1 < nk) wait_vm<L>(); else wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (it + 2 < nk) issue(slot == 0 ? 2 : slot - 1, it + 2);
+    const char* sa = lds + slot * SLOT_BYTES;
+    const char* sb = sa + A_BYTES;
+    slot = slot == DG_NS - 1 ? 0 : slot + 1;
+    if constexpr (ABL == ABL_NO_MFMA) continue;
+    if (!consumer) continue;
+#pragma unroll
+    for (int ks = 0; ks < DG_BK / 32; ++ks) {
+      const int c = ks * 4 + fq;
+      Pack8<T> af[MT], bfr[NT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int r = a_row0 + i * 16;
+        af[i].u = *reinterpret_cast<const u32x4*>(sa + r * DG_ROWB + (swz(r, c) << 4));
+      }
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const int r = b_row0 + n * 16;
+        bfr[n].u = *reinterpret_cast<const u32x4*>(sb + r * DG_ROWB + (swz(r, c) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[i][n] = mfma16x16x32(af[i].v, bfr[n].v, acc[i][n]);
+    }
+  }
+
+  // ---- epilogue: lane holds C[4*fq + e][fr] of every 16x16 tile
+  if (!consumer) return;
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = m0 + wm * (BM / 4) + i * 16 + fq * 4 + e;
+      if (row >= M) continue;
+      if constexpr (EPI == EPI_PARTIAL) {
+        float* cp = reinterpret_cast<float*>(Cv) + z * slice_stride + (int64_t)row * N +
+                    nb * BN + wn * (BN / 2) + fr;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) cp[n * 16] = acc[i][n][e];
+      } else if constexpr (EPI == EPI_OUT) {
+        T* cp = reinterpret_cast<T*>(Cv) + (int64_t)row * N + nb * BN + wn * (BN / 2) + fr;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) cp[n * 16] = from_f<T>(acc[i][n][e]);
+      } else {
+        const int I = N >> 1;
+        T* cp = reinterpret_cast<T*>(Cv) + (int64_t)row * I + nb * (BN / 2) + wn * (BN / 4) + fr;
+#pragma unroll
+        for (int n = 0; n < NT; n += 2)
+          cp[(n >> 1) * 16] = from_f<T>(silu_f(acc[i][n][e]) * acc[i][n + 1][e]);
+      }
+    }
+  }
+}
+
+// Split-loader variant (packed weights only).  With every DMA of a step in one in-order
+// queue, the activation pieces (L2 hits) wait behind the weight pieces (HBM misses), so a
+// 3-slot ring of 48 KB caps the per-CU intake at ~96 KB per HBM latency (~48 GB/s, what
+// the single-queue kernels measure).  Here the queues are separate waves:
+//   waves 0-7   MFMA consumers (as dgemm_kernel),
+//   waves 8-11  activation loaders: a 3-slot A ring (one step in flight behind the read),
+//   waves 12-13 weight loaders: an NB-slot B ring (NB - 2 steps in flight: 32-48 KB of
+//               HBM reads per CU at all times);
+// each loader group waits only on its own vmcnt, and one s_barrier per step joins all 14.
+template <typename T, int BM, int BN, int EPI, int NB>
+__global__ __launch_bounds__(896, 1) void dgemm_sl_kernel(
+    void* __restrict__ Cv, const T* __restrict__ X, const T* __restrict__ W, int M, int N,
+    int K, int64_t ldx, int S, int MB, int64_t slice_stride) {
+  constexpr int MT = BM / 4 / 16, NT = BN / 2 / 16;
+  constexpr int NA = 3;
+  constexpr int LA = BM / 8 / 4, LB = BN / 8 / 2;   // DMAs per A / B loader wave per step
+  constexpr int A_SLOT = BM * DG_ROWB, B_SLOT = BN * DG_ROWB;
+  static_assert(NA * A_SLOT + NB * B_SLOT <= 163840, "LDS rings exceed 160 KiB");
+  __shared__ __attribute__((aligned(16))) char lds[NA * A_SLOT + NB * B_SLOT];
+  char* const ring_a = lds;
+  char* const ring_b = lds + NA * A_SLOT;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int z = blockIdx.x % S;
+  const int j = blockIdx.x / S;
+  const int mb = j % MB, nb = j / MB;
+  const int m0 = mb * BM;
+  const int nk_all = K / DG_BK;
+  const int kb0 = (int)((int64_t)nk_all * z / S);
+  const int nk = (int)((int64_t)nk_all * (z + 1) / S) - kb0;
+  const int rot = nk >= 4 ? (int)(((int64_t)j * 37) % nk) : 0;
+  auto kstep = [&](int step) {
+    int st = step + rot;
+    return kb0 + (st >= nk ? st - nk : st);
+  };
+
+  if (wave >= 8) {
+    // ------------------------------------------------------------------ loaders
+    const bool is_a = wave < 12;
+    const int iw = is_a ? wave - 8 : wave - 12;
+    const int drow = lane >> 3, dchunk = (lane & 7) ^ drow;
+    const T* src[LA > LB ? LA : LB];
+    if (is_a) {
+#pragma unroll
+      for (int t = 0; t < LA; ++t) {
+        int r = m0 + (iw * LA + t) * 8 + drow;
+        r = r < M ? r : M - 1;
+        src[t] = X + (int64_t)r * ldx + dchunk * 8;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < LB; ++t)
+        src[t] = W + (int64_t)nb * nk_all * (BN * DG_BK) + (iw * LB + t) * 512 + lane * 8;
+    }
+    auto issue_a = [&](int step) {
+      char* d = ring_a + (step % NA) * A_SLOT + iw * LA * 1024;
+      const int ko = kstep(step) * DG_BK;
+#pragma unroll
+      for (int t = 0; t < LA; ++t) glds16<0>(src[t] + ko, d + t * 1024);
+    };
+    auto issue_b = [&](int step) {
+      char* d = ring_b + (step % NB) * B_SLOT + iw * LB * 1024;
+      const int64_t bo = (int64_t)kstep(step) * (BN * DG_BK);
+#pragma unroll
+      for (int t = 0; t < LB; ++t) glds16<2>(src[t] + bo, d + t * 1024);
+    };
+    if (is_a) {
+      for (int p = 0; p < NA - 1 && p < nk; ++p) issue_a(p);
+    } else {
+      for (int p = 0; p < NB - 1 && p < nk; ++p) issue_b(p);
+    }
+    for (int it = 0; it < nk; ++it) {
+      if (is_a) {
+        wait_younger<LA, NA - 2>(nk - 1 - it);
+      } else {
+        wait_younger<LB, NB - 2>(nk - 1 - it);
+      }
+      __builtin_amdgcn_s_barrier();
+      if (is_a) {
+        if (it + NA - 1 < nk) issue_a(it + NA - 1);
+      } else {
+        if (it + NB - 1 < nk) issue_b(it + NB - 1);
+      }
+    }
+    return;
+  }
+
+  // -------------------------------------------------------------------- MFMA waves
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int a_row0 = wm * (BM / 4) + fr;
+  const int b_row0 = wn * (BN / 2) + fr;
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int it = 0; it < nk; ++it) {
+    __builtin_amdgcn_s_barrier();
+    const char* sa = ring_a + (it % NA) * A_SLOT;
+    const char* sb = ring_b + (it % NB) * B_SLOT;
+#pragma unroll
+    for (int ks = 0; ks < DG_BK / 32; ++ks) {
+      const int c = ks * 4 + fq;
+      Pack8<T> af[MT], bfr[NT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int r = a_row0 + i * 16;
+        af[i].u = *reinterpret_cast<const u32x4*>(sa + r * DG_ROWB + (swz(r, c) << 4));
+      }
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const int r = b_row0 + n * 16;
+        bfr[n].u = *reinterpret_cast<const u32x4*>(sb + r * DG_ROWB + (swz(r, c) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[i][n] = mfma16x16x32(af[i].v, bfr[n].v, acc[i][n]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = m0 + wm * (BM / 4) + i * 16 + fq * 4 + e;
+      if (row >= M) continue;
+      if constexpr (EPI == EPI_PARTIAL) {
+        float* cp = reinterpret_cast<float*>(Cv) + z * slice_stride + (int64_t)row * N +
+                    nb * BN + wn * (BN / 2) + fr;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) cp[n * 16] = acc[i][n][e];
+      } else if constexpr (EPI == EPI_OUT) {
+        T* cp = reinterpret_cast<T*>(Cv) + (int64_t)row * N + nb * BN + wn * (BN / 2) + fr;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) cp[n * 16] = from_f<T>(acc[i][n][e]);
+      } else {
+        const int I = N >> 1;
+        T* cp = reinterpret_cast<T*>(Cv) + (int64_t)row * I + nb * (BN / 2) + wn * (BN / 4) + fr;
+#pragma unroll
+        for (int n = 0; n < NT; n += 2)
+          cp[(n >> 1) * 16] = from_f<T>(silu_f(acc[i][n][e]) * acc[i][n + 1][e]);
+      }
+    }
+  }
+}
+
+template <typename T, int BM, int BN, int NB>
+void dgemm_sl_cfg(int epi, void* C, const void* X, const void* W, int M, int N, int K,
+                  int64_t ldx, int S, int64_t ss, hipStream_t s) {
+  const int MB = (M + BM - 1) / BM;
+  const dim3 grid((unsigned)(MB * (N / BN) * S));
+#define DG_SL(E)                                                                       \
+  dgemm_sl_kernel<T, BM, BN, E, NB><<<grid, 896, 0, s>>>(C, (const T*)X, (const T*)W, M, \
+                                                          N, K, ldx, S, MB, ss)
+  if (epi == EPI_PARTIAL) DG_SL(EPI_PARTIAL);
+  else if (epi == EPI_OUT) DG_SL(EPI_OUT);
+  else DG_SL(EPI_SILU);
+#undef DG_SL
+}
+
+// Re-layout W [N, K] (EPI_SILU: merged [gate; up]) into the packed tiles the PK kernels
+// stream: P[nb][kb][r][pos] (16-B chunks) = W[weight_row(nb, r)][kb*64 + (pos ^ r%8)*8 ..]
+template <typename T, int BN, int EPI>
+__global__ __launch_bounds__(256) void dgemm_pack_kernel(T* __restrict__ P,
+                                                         const T* __restrict__ W, int N,
+                                                         int K) {
+  const int nk_all = K / DG_BK;
+  const int64_t chunk = (int64_t)blockIdx.x * 256 + threadIdx.x;   // one 16-B chunk
+  const int64_t total = (int64_t)N * K / 8;
+  if (chunk >= total) return;
+  const int pos = (int)(chunk & 7);
+  const int64_t rowi = chunk >> 3;                 // (nb, kb, r) flattened
+  const int r = (int)(rowi % BN);
+  const int64_t t = rowi / BN;
+  const int kb = (int)(t % nk_all);
+  const int nb = (int)(t / nk_all);
+  const int64_t src = weight_row<BN, EPI>(nb, r, N) * K + kb * DG_BK + swz(r, pos) * 8;
+  reinterpret_cast<u32x4*>(P)[chunk] = *reinterpret_cast<const u32x4*>(W + src);
+}
+
+// Tile table: id -> (BM, BN, packed weights); ids 6, 7 = 4, 5 with 4 loader waves;
+// ids 8, 9 = split loaders (dgemm_sl_kernel) 256 x 128 with a 4- / 128 x 128 with a 6-slot
+// weight ring
+constexpr int kNumCfgs = 10;
+static const int kCfg[kNumCfgs][3] = {{256, 128, 0}, {256, 64, 0},  {128, 128, 0}, {128, 64, 0},
+                                      {256, 128, 1}, {128, 128, 1}, {256, 128, 1}, {128, 128, 1},
+                                      {256, 128, 1}, {128, 128, 1}};
+
+template <typename T, int BM, int BN, bool PK, int LDW = 0>
+void dgemm_cfg(int epi, void* C, const void* X, const void* W, int M, int N, int K, int64_t ldx,
+               int S, int64_t ss, hipStream_t s) {
+  const int MB = (M + BM - 1) / BM;
+  const dim3 grid((unsigned)(MB * (N / BN) * S));
+#define DG_LAUNCH(E)                                                             \
+  dgemm_kernel<T, BM, BN, E, PK, ABL_NONE, LDW><<<grid, DG_THREADS + LDW * 64, 0, s>>>( \
+      C, (const T*)X, (const T*)W, M, N, K, ldx, S, MB, ss)
+  if (epi == EPI_PARTIAL) DG_LAUNCH(EPI_PARTIAL);
+  else if (epi == EPI_OUT) DG_LAUNCH(EPI_OUT);
+  else DG_LAUNCH(EPI_SILU);
+#undef DG_LAUNCH
+}
+
+template <typename T>
+void dgemm_t(int cfg, int epi, void* C, const void* X, const void* W, int M, int N, int K,
+             int64_t ldx, int S, int64_t ss, hipStream_t s) {
+  switch (cfg) {
+    case 0: dgemm_cfg<T, 256, 128, false>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
+    case 1: dgemm_cfg<T, 256, 64, false>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
+    case 2: dgemm_cfg<T, 128, 128, false>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
+    case 3: dgemm_cfg<T, 128, 64, false>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
+    case 4: dgemm_cfg<T, 256, 128, true>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
+    case 5: dgemm_cfg<T, 128, 128, true>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
+    case 6: dgemm_cfg<T, 256, 128, true, 4>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
+    case 7: dgemm_cfg<T, 128, 128, true, 4>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
+    case 8: dgemm_sl_cfg<T, 256, 128, 4>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
+    default: dgemm_sl_cfg<T, 128, 128, 6>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
+  }
+}
+
+}  // namespace
+
+int dgemm_num_cfgs() { return kNumCfgs; }
+void dgemm_cfg_info(int cfg, int* bm, int* bn, int* packed) {
+  *bm = kCfg[cfg][0];
+  *bn = kCfg[cfg][1];
+  *packed = kCfg[cfg][2];
+}
+int dgemm_block_k() { return DG_BK; }
+
+void launch_dgemm(int dtype, int cfg, int epi, void* C, const void* X, const void* W, int M,
+                  int N, int K, int64_t ldx, int S, int64_t slice_stride, hipStream_t s) {
+  if (dtype == DT_BF16) dgemm_t<bf16>(cfg, epi, C, X, W, M, N, K, ldx, S, slice_stride, s);
+  else dgemm_t<f16>(cfg, epi, C, X, W, M, N, K, ldx, S, slice_stride, s);
+}
+
+void launch_dgemm_pack(int dtype, bool silu, void* P, const void* W, int N, int K,
+                       hipStream_t s) {
+  const int64_t chunks = (int64_t)N * K / 8;
+  const dim3 grid((unsigned)((chunks + 255) / 256));
+#define PACK(T, E) \
+  dgemm_pack_kernel<T, 128, E><<<grid, 256, 0, s>>>((T*)P, (const T*)W, N, K)
+  if (dtype == DT_BF16) {
+    if (silu) PACK(bf16, EPI_SILU);
+    else PACK(bf16, EPI_OUT);
+  } else {
+    if (silu) PACK(f16, EPI_SILU);
+    else PACK(f16, EPI_OUT);
+  }
+#undef PACK
+}
+
+// 256 x 128 packed tile with one part removed, fp32 slices (profiling only)
+void launch_dgemm_ablate(int mode, float* C, const void* X, const void* W, int M, int N, int K,
+                         int64_t ldx, int S, int64_t ss, hipStream_t s) {
+  const int MB = (M + 255) / 256;
+  const dim3 grid((unsigned)(MB * (N / 128) * S));
+#define AB(MODE)                                                                     \
+  dgemm_kernel<bf16, 256, 128, EPI_PARTIAL, true, MODE><<<grid, DG_THREADS, 0, s>>>( \
+      C, (const bf16*)X, (const bf16*)W, M, N, K, ldx, S, MB, ss)
+  switch (mode) {
+    case ABL_NO_MFMA: AB(ABL_NO_MFMA); break;
+    case ABL_NO_DMA: AB(ABL_NO_DMA); break;
+    case ABL_NO_A: AB(ABL_NO_A); break;
+    case ABL_NO_B: AB(ABL_NO_B); break;
+    default: AB(ABL_NONE); break;
+  }
+#undef AB
+}
+
+}  // namespace kgc

@@ -13,8 +13,9 @@ void launch_rms_norm(int dtype, void* out, const void* x, void* residual, const 
 void launch_layer_norm(int dtype, void* out, const void* x, const void* w, const void* b,
                        int rows, int H, float eps, hipStream_t s);
 void launch_silu_mul(int dtype, void* out, const void* x, int64_t rows, int I, hipStream_t s);
-void launch_rope_kv_write(int dtype, const void* qkv, int64_t qkv_stride,
-                          const int64_t* positions, const float* cos_sin, void* q_out,
+// S > 0: qkv is S fp32 split-K slices [S, T, qkv_stride] (slice_stride apart), summed here
+void launch_rope_kv_write(int dtype, const void* qkv, int64_t qkv_stride, int S,
+                          int64_t slice_stride, const int64_t* positions, const float* cos_sin, void* q_out,
                           void* k_cache, void* v_cache, const int64_t* slot_mapping,
                           const void* q_norm_w, const void* k_norm_w, int T, int nq, int nkv,
                           int d, int bs, float eps, bool use_rope, bool kv_fp8, float k_scale,
@@ -59,6 +60,20 @@ void launch_moe_gemm(int dtype, int bm, void* C, const void* A, const void* W,
 // dense split-K decode GEMM: Cs [splitk, M, N] fp32 = A [M, K] x W [N, K]^T, XCD-mapped slices
 void launch_dense_gemm_splitk(int dtype, int bm, float* Cs, const void* A, const void* W, int M,
                               int N, int K, int64_t lda, int splitk, hipStream_t s);
+// K9m mid-batch decode GEMM (gemm_decode.hip): X [M, K] . W^T with tile config `cfg`
+// (dgemm_cfg_info: BM x BN, and whether W is the packed [N/128][K/64][128*64] layout of
+// launch_dgemm_pack rather than [N, K]).  epi 0: fp32 split-K slice z of C [S, M, N];
+// 1: C [M, N] in X's dtype (S = 1); 2: silu(gate) * up of a merged [gate; up] W into
+// C [M, N/2] (S = 1; a packed W must have been packed with silu = true)
+int dgemm_num_cfgs();
+void dgemm_cfg_info(int cfg, int* bm, int* bn, int* packed);
+int dgemm_block_k();
+void launch_dgemm(int dtype, int cfg, int epi, void* C, const void* X, const void* W, int M,
+                  int N, int K, int64_t ldx, int S, int64_t slice_stride, hipStream_t s);
+void launch_dgemm_pack(int dtype, bool silu, void* P, const void* W, int N, int K,
+                       hipStream_t s);
+void launch_dgemm_ablate(int mode, float* C, const void* X, const void* W, int M, int N, int K,
+                         int64_t ldx, int S, int64_t ss, hipStream_t s);
 // residual += sum_z Cs[z] (rounded to dtype); out = rms_norm(residual) * w, one WG per row
 void launch_splitk_add_rms_norm(int dtype, void* out, const float* Cs, void* residual,
                                 const void* w, int rows, int H, int S, int64_t slice_stride,

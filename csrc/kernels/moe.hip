@@ -254,13 +254,15 @@ __global__ __launch_bounds__(MG_THREADS, 2) void moe_gemm_kernel(
 }
 
 // out[m, n] = sum_z Cs[z, m, n]  (+ residual)  -- split-K reduction of the dense GEMM.
-template <typename T>
+template <typename T, int SK>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(T* __restrict__ out,
-                                                            const float* __restrict__ Cs, int S,
+                                                            const float* __restrict__ Cs, int S_,
                                                             int64_t n8, int64_t slice_stride) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n8) return;
+  const int S = SK > 0 ? SK : S_;     // SK > 0: all slice loads issued up front
   f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, b = a;
+#pragma unroll
   for (int z = 0; z < S; ++z) {
     const float* src = Cs + z * slice_stride + i * 8;
     a += *reinterpret_cast<const f32x4*>(src);
@@ -279,16 +281,18 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(T* __restrict__ out,
 // g = sum_z Cs[z, m, i], u = sum_z Cs[z, m, I + i].  The [M, 2I] bf16 gate_up output
 // is never written, and the separate silu_mul launch disappears from the decode step.
 // grid (ceil(I/8/256), M): one 8-wide column group per thread, no index division.
-template <typename T>
+template <typename T, int SK>
 __global__ __launch_bounds__(256) void splitk_reduce_silu_kernel(T* __restrict__ out,
                                                                  const float* __restrict__ Cs,
-                                                                 int S, int I,
+                                                                 int S_, int I,
                                                                  int64_t slice_stride) {
+  const int S = SK > 0 ? SK : S_;
   const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
   if (c >= I) return;
   const int64_t m = blockIdx.y;
   const float* row = Cs + m * 2 * I + c;
   f32x4 g0 = f32x4{0.f, 0.f, 0.f, 0.f}, g1 = g0, u0 = g0, u1 = g0;
+#pragma unroll
   for (int z = 0; z < S; ++z) {
     const float* src = row + z * slice_stride;
     g0 += *reinterpret_cast<const f32x4*>(src);
@@ -430,28 +434,49 @@ void launch_dense_gemm_splitk(int dtype, int bm, float* Cs, const void* A, const
 #undef DG_LAUNCH
 }
 
+template <typename T>
+static void splitk_reduce_t(T* out, const float* Cs, int S, int64_t n8, int64_t ss,
+                            hipStream_t s) {
+  const dim3 grid((unsigned)((n8 + 255) / 256));
+#define SKR(K) splitk_reduce_kernel<T, K><<<grid, 256, 0, s>>>(out, Cs, S, n8, ss)
+  switch (S) {
+    case 2: SKR(2); break;
+    case 4: SKR(4); break;
+    case 8: SKR(8); break;
+    default: SKR(0); break;
+  }
+#undef SKR
+}
+
 void launch_splitk_reduce(int dtype, void* out, const float* Cs, int S, int64_t numel,
                           int64_t slice_stride, hipStream_t s) {
   const int64_t n8 = numel / 8;
-  const dim3 grid((unsigned)((n8 + 255) / 256));
-  if (dtype == DT_BF16)
-    splitk_reduce_kernel<bf16><<<grid, 256, 0, s>>>((bf16*)out, Cs, S, n8, slice_stride);
-  else
-    splitk_reduce_kernel<f16><<<grid, 256, 0, s>>>((f16*)out, Cs, S, n8, slice_stride);
+  if (dtype == DT_BF16) splitk_reduce_t<bf16>((bf16*)out, Cs, S, n8, slice_stride, s);
+  else splitk_reduce_t<f16>((f16*)out, Cs, S, n8, slice_stride, s);
+}
+
+template <typename T>
+static void splitk_reduce_silu_t(T* out, const float* Cs, int S, int n, int I, int64_t ss,
+                                 hipStream_t s) {
+  const dim3 grid((unsigned)((I / 8 + 255) / 256), (unsigned)n);
+#define SKS(K) splitk_reduce_silu_kernel<T, K><<<grid, 256, 0, s>>>(out, Cs, S, I, ss)
+  switch (S) {
+    case 2: SKS(2); break;
+    case 4: SKS(4); break;
+    default: SKS(0); break;
+  }
+#undef SKS
 }
 
 void launch_splitk_reduce_silu(int dtype, void* out, const float* Cs, int S, int M, int I,
                                int64_t slice_stride, hipStream_t s) {
   for (int m0 = 0; m0 < M; m0 += 65535) {   // gridDim.y <= 65535
     const int n = std::min(M - m0, 65535);
-    const dim3 grid((unsigned)((I / 8 + 255) / 256), (unsigned)n);
     const float* c = Cs + (int64_t)m0 * 2 * I;
     if (dtype == DT_BF16)
-      splitk_reduce_silu_kernel<bf16><<<grid, 256, 0, s>>>((bf16*)out + (int64_t)m0 * I, c, S, I,
-                                                          slice_stride);
+      splitk_reduce_silu_t<bf16>((bf16*)out + (int64_t)m0 * I, c, S, n, I, slice_stride, s);
     else
-      splitk_reduce_silu_kernel<f16><<<grid, 256, 0, s>>>((f16*)out + (int64_t)m0 * I, c, S, I,
-                                                         slice_stride);
+      splitk_reduce_silu_t<f16>((f16*)out + (int64_t)m0 * I, c, S, n, I, slice_stride, s);
   }
 }
 

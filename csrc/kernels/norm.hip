@@ -64,10 +64,13 @@ __global__ __launch_bounds__(NORM_NT) void rms_norm_kernel(
 //   h = sum_z Cs[z, row, :] (rounded to T, as the unfused reduce stores it)
 //   residual += h;  out = rms_norm(residual) * w
 // The [M, H] projection output is never written and one launch per projection goes.
-template <typename T>
+template <typename T, int SK>
 __global__ __launch_bounds__(NORM_NT) void splitk_add_rms_norm_kernel(
     T* __restrict__ out, const float* __restrict__ Cs, T* __restrict__ residual,
-    const T* __restrict__ w, int H, int S, int64_t slice_stride, float eps) {
+    const T* __restrict__ w, int H, int S_, int64_t slice_stride, float eps) {
+  // SK > 0: the slice count is a compile-time constant, so every slice load of a thread
+  // is issued before the first add (one memory round trip instead of S)
+  const int S = SK > 0 ? SK : S_;
   __shared__ float scratch[NORM_NT / 64];
   const int row = blockIdx.x;
   const int nv = H >> 3;
@@ -85,7 +88,13 @@ __global__ __launch_bounds__(NORM_NT) void splitk_add_rms_norm_kernel(
     const int idx = threadIdx.x + i * NORM_NT;
     if (idx < nv) {
       f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f}, b = a;
-      for (int z = 0; z < S; ++z) {
+#pragma unroll
+      for (int z = 0; z < (SK > 0 ? SK : 1); ++z) {
+        const float* src = cr + z * slice_stride + idx * 8;
+        a += *reinterpret_cast<const f32x4*>(src);
+        b += *reinterpret_cast<const f32x4*>(src + 4);
+      }
+      for (int z = SK > 0 ? SK : 1; z < S; ++z) {
         const float* src = cr + z * slice_stride + idx * 8;
         a += *reinterpret_cast<const f32x4*>(src);
         b += *reinterpret_cast<const f32x4*>(src + 4);
@@ -187,16 +196,31 @@ void launch_rms_norm(int dtype, void* out, const void* x, void* residual, const 
   else rms_dispatch<f16>(out, x, residual, w, rows, H, x_stride, eps, s);
 }
 
+template <typename T>
+static void splitk_add_rms_dispatch(T* out, const float* Cs, T* residual, const T* w, int rows,
+                                    int H, int S, int64_t ss, float eps, hipStream_t s) {
+#define SKN(K) splitk_add_rms_norm_kernel<T, K><<<rows, NORM_NT, 0, s>>>(out, Cs, residual, w, \
+                                                                         H, S, ss, eps)
+  switch (S) {
+    case 2: SKN(2); break;
+    case 3: SKN(3); break;
+    case 4: SKN(4); break;
+    case 8: SKN(8); break;
+    default: SKN(0); break;
+  }
+#undef SKN
+}
+
 void launch_splitk_add_rms_norm(int dtype, void* out, const float* Cs, void* residual,
                                 const void* w, int rows, int H, int S, int64_t slice_stride,
                                 float eps, hipStream_t s) {
   if (rows == 0) return;
   if (dtype == DT_BF16)
-    splitk_add_rms_norm_kernel<bf16><<<rows, NORM_NT, 0, s>>>(
-        (bf16*)out, Cs, (bf16*)residual, (const bf16*)w, H, S, slice_stride, eps);
+    splitk_add_rms_dispatch<bf16>((bf16*)out, Cs, (bf16*)residual, (const bf16*)w, rows, H, S,
+                                  slice_stride, eps, s);
   else
-    splitk_add_rms_norm_kernel<f16><<<rows, NORM_NT, 0, s>>>(
-        (f16*)out, Cs, (f16*)residual, (const f16*)w, H, S, slice_stride, eps);
+    splitk_add_rms_dispatch<f16>((f16*)out, Cs, (f16*)residual, (const f16*)w, rows, H, S,
+                                 slice_stride, eps, s);
 }
 
 void launch_layer_norm(int dtype, void* out, const void* x, const void* w, const void* b,

@@ -4,6 +4,9 @@
 // of 16-byte chunks (c, c + d/2) of one head so the rotation needs no exchange;
 // the head's TPH = d/16 threads are an aligned lane group for the q/k-norm sum.
 //
+// SL: the QKV projection arrives as S fp32 split-K slices [S, T, N] of the K9m decode
+// GEMM (gemm_decode.hip) and is summed here (rounded to T as the unfused GEMM output
+// would be), so the slice reduction costs no kernel of its own.
 // Cache layouts (see ops/reference.py):
 //   k_cache [nb, nkv, bs, d]    v_cache [nb, nkv, bs/8, d, 8]  (V^T in 8-key groups)
 // KV8: the cache holds fp8 e4m3 of (value / scale) (--kv-cache-dtype fp8); the value
@@ -15,9 +18,33 @@ namespace kgc {
 
 constexpr int ROPE_NT = 128;
 
-template <typename T, bool NORM, bool ROPE, bool KV8>
+// 8 consecutive elements of the QKV row: T storage, or the sum of S fp32 slices
+template <typename T, bool SL>
+__device__ __forceinline__ u32x4 qkv8(const void* qkv, int64_t row_elem, int col, int S,
+                                      int64_t slice_stride) {
+  if constexpr (!SL) {
+    return *reinterpret_cast<const u32x4*>(reinterpret_cast<const T*>(qkv) + row_elem + col);
+  } else {
+    const float* p = reinterpret_cast<const float*>(qkv) + row_elem + col;
+    f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+    for (int z = 1; z < S; ++z) {
+      a += *reinterpret_cast<const f32x4*>(p + z * slice_stride);
+      b += *reinterpret_cast<const f32x4*>(p + z * slice_stride + 4);
+    }
+    Pack8<T> o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      o.h[q] = from_f<T>(a[q]);
+      o.h[4 + q] = from_f<T>(b[q]);
+    }
+    return o.u;
+  }
+}
+
+template <typename T, bool NORM, bool ROPE, bool KV8, bool SL>
 __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
-    const T* __restrict__ qkv, int64_t qkv_stride, const int64_t* __restrict__ positions,
+    const void* __restrict__ qkv, int64_t qkv_stride, int S, int64_t slice_stride,
+    const int64_t* __restrict__ positions,
     const float* __restrict__ cos_sin, T* __restrict__ q_out, void* __restrict__ k_cache,
     void* __restrict__ v_cache, const int64_t* __restrict__ slot_mapping,
     const T* __restrict__ qn_w, const T* __restrict__ kn_w, int nq, int nkv, int d, int bs,
@@ -31,17 +58,16 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
   const int n_qk_pad = (n_qk + 63) & ~63;
   const int it = blockIdx.y * ROPE_NT + threadIdx.x;
   const int64_t slot = slot_mapping[t];
-  const T* row = qkv + (int64_t)t * qkv_stride;
+  const int64_t row = (int64_t)t * qkv_stride;   // element offset of this token's row
   const int64_t blk = slot >= 0 ? slot / bs : 0;
   const int off = slot >= 0 ? (int)(slot % bs) : 0;
   if (it < n_qk_pad) {                  // whole waves take this branch together
     const bool active = it < n_qk;
     const int head = active ? it / tph : 0;     // 0..nq-1 = q, nq.. = k
     const int c = it % tph;                     // chunk index within the first half
-    const T* src = row + head * d;
     Pack8<T> a, b;
-    a.u = *reinterpret_cast<const u32x4*>(src + c * 8);
-    b.u = *reinterpret_cast<const u32x4*>(src + half + c * 8);
+    a.u = qkv8<T, SL>(qkv, row + head * d, c * 8, S, slice_stride);
+    b.u = qkv8<T, SL>(qkv, row + head * d, half + c * 8, S, slice_stride);
     float4 c0, c1, s0, s1;
     if (ROPE) {
       const float* cs = cos_sin + positions[t] * d;
@@ -116,7 +142,7 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
   if (slot < 0 || iv >= nkv * (d >> 3)) return;
   const int h = iv / (d >> 3), c = iv % (d >> 3);
   Pack8<T> v;
-  v.u = *reinterpret_cast<const u32x4*>(row + (nq + nkv) * d + h * d + c * 8);
+  v.u = qkv8<T, SL>(qkv, row + (nq + nkv) * d + h * d, c * 8, S, slice_stride);
   const int64_t e = (blk * nkv + h) * (int64_t)bs * d + ((int64_t)(off >> 3) * d + c * 8) * 8 +
                     (off & 7);
   if constexpr (KV8) {
@@ -137,8 +163,9 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
   }
 }
 
-template <typename T, bool KV8>
-static void rope_dispatch(const void* qkv, int64_t qkv_stride, const int64_t* pos,
+template <typename T, bool KV8, bool SL>
+static void rope_dispatch(const void* qkv, int64_t qkv_stride, int S, int64_t ss,
+                          const int64_t* pos,
                           const float* cs, void* q_out, void* kc, void* vc,
                           const int64_t* slots, const void* qn, const void* kn, int T_,
                           int nq, int nkv, int d, int bs, float eps, bool rope, float k_inv,
@@ -147,8 +174,8 @@ static void rope_dispatch(const void* qkv, int64_t qkv_stride, const int64_t* po
   const int n_items = (((nq + nkv) * (d >> 4) + 63) & ~63) + nkv * (d >> 3);
   const dim3 grid(T_, (n_items + ROPE_NT - 1) / ROPE_NT);
 #define KGC_ROPE_LAUNCH(N, R)                                                               \
-  rope_kv_kernel<T, N, R, KV8><<<grid, ROPE_NT, 0, s>>>(                                    \
-      (const T*)qkv, qkv_stride, pos, cs, (T*)q_out, kc, vc, slots, (const T*)qn,           \
+  rope_kv_kernel<T, N, R, KV8, SL><<<grid, ROPE_NT, 0, s>>>(                                \
+      qkv, qkv_stride, S, ss, pos, cs, (T*)q_out, kc, vc, slots, (const T*)qn,               \
       (const T*)kn, nq, nkv, d, bs, eps, k_inv, v_inv)
   const bool norm = qn != nullptr;
   if (norm && rope) KGC_ROPE_LAUNCH(true, true);
@@ -158,22 +185,47 @@ static void rope_dispatch(const void* qkv, int64_t qkv_stride, const int64_t* po
 #undef KGC_ROPE_LAUNCH
 }
 
-void launch_rope_kv_write(int dtype, const void* qkv, int64_t qkv_stride,
-                          const int64_t* positions, const float* cos_sin, void* q_out,
-                          void* k_cache, void* v_cache, const int64_t* slot_mapping,
-                          const void* q_norm_w, const void* k_norm_w, int T, int nq, int nkv,
-                          int d, int bs, float eps, bool use_rope, bool kv_fp8, float k_scale,
-                          float v_scale, hipStream_t s) {
-#define KGC_ROPE_TYPES(TT, K8)                                                               \
-  rope_dispatch<TT, K8>(qkv, qkv_stride, positions, cos_sin, q_out, k_cache, v_cache,       \
-                        slot_mapping, q_norm_w, k_norm_w, T, nq, nkv, d, bs, eps, use_rope, \
-                        1.f / k_scale, 1.f / v_scale, s)
+template <typename T, bool KV8>
+static void rope_dispatch_sl(const void* qkv, int64_t qkv_stride, int S, int64_t ss,
+                             const int64_t* pos, const float* cs, void* q_out, void* kc, void* vc,
+                             const int64_t* slots, const void* qn, const void* kn, int T_,
+                             int nq, int nkv, int d, int bs, float eps, bool rope, float k_inv,
+                             float v_inv, hipStream_t s) {
+  if (S > 0)
+    rope_dispatch<T, KV8, true>(qkv, qkv_stride, S, ss, pos, cs, q_out, kc, vc, slots, qn, kn,
+                                T_, nq, nkv, d, bs, eps, rope, k_inv, v_inv, s);
+  else
+    rope_dispatch<T, KV8, false>(qkv, qkv_stride, 0, 0, pos, cs, q_out, kc, vc, slots, qn, kn,
+                                 T_, nq, nkv, d, bs, eps, rope, k_inv, v_inv, s);
+}
+
+void launch_rope_kv_write(int dtype, const void* qkv, int64_t qkv_stride, int S,
+                          int64_t slice_stride, const int64_t* positions, const float* cos_sin,
+                          void* q_out, void* k_cache, void* v_cache,
+                          const int64_t* slot_mapping, const void* q_norm_w,
+                          const void* k_norm_w, int T, int nq, int nkv, int d, int bs,
+                          float eps, bool use_rope, bool kv_fp8, float k_scale, float v_scale,
+                          hipStream_t s) {
+  const float ki = 1.f / k_scale, vi = 1.f / v_scale;
   if (dtype == DT_BF16) {
-    if (kv_fp8) KGC_ROPE_TYPES(bf16, true); else KGC_ROPE_TYPES(bf16, false);
+    if (kv_fp8)
+      rope_dispatch_sl<bf16, true>(qkv, qkv_stride, S, slice_stride, positions, cos_sin, q_out,
+                                   k_cache, v_cache, slot_mapping, q_norm_w, k_norm_w, T, nq,
+                                   nkv, d, bs, eps, use_rope, ki, vi, s);
+    else
+      rope_dispatch_sl<bf16, false>(qkv, qkv_stride, S, slice_stride, positions, cos_sin, q_out,
+                                    k_cache, v_cache, slot_mapping, q_norm_w, k_norm_w, T, nq,
+                                    nkv, d, bs, eps, use_rope, ki, vi, s);
   } else {
-    if (kv_fp8) KGC_ROPE_TYPES(f16, true); else KGC_ROPE_TYPES(f16, false);
+    if (kv_fp8)
+      rope_dispatch_sl<f16, true>(qkv, qkv_stride, S, slice_stride, positions, cos_sin, q_out,
+                                  k_cache, v_cache, slot_mapping, q_norm_w, k_norm_w, T, nq,
+                                  nkv, d, bs, eps, use_rope, ki, vi, s);
+    else
+      rope_dispatch_sl<f16, false>(qkv, qkv_stride, S, slice_stride, positions, cos_sin, q_out,
+                                   k_cache, v_cache, slot_mapping, q_norm_w, k_norm_w, T, nq,
+                                   nkv, d, bs, eps, use_rope, ki, vi, s);
   }
-#undef KGC_ROPE_TYPES
 }
 
 }  // namespace kgc

@@ -459,7 +459,8 @@ class ModelRunner:
             gemm.tune_skinny([p for p in self.model.parameters() if p.dim() == 2],
                              self.buckets, norm_shapes=ns,
                              silu_shapes=getattr(self.model, "silu_shapes", lambda: set())(),
-                             tail_shapes=getattr(self.model, "tail_shapes", lambda: set())())
+                             tail_shapes=getattr(self.model, "tail_shapes", lambda: set())(),
+                             qkv_dims=getattr(self.model, "qkv_dims", lambda: {})())
         if (not self.use_graphs or not (self.model.first and self.model.last)
                 or not getattr(self.model, "graph_safe", True)):
             self.use_graphs = False

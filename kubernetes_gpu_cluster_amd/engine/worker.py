@@ -69,6 +69,16 @@ class Worker:
         torch.manual_seed(cfg.seed)
         self.mcfg, self.model = load_model(cfg.model, self.dtype, dev, cfg.random_init,
                                            seed=cfg.seed)
+        if dev.type == "cuda" and not cfg.enforce_eager:
+            # packed copies of the decode-GEMM weights for the K9m tiles, made before the
+            # KV cache is sized so the pool accounts for them (ops/gemm.py)
+            from ..ops import gemm
+            silu = list(getattr(self.model, "silu_weights", lambda: [])())
+            skip = {id(x) for x in silu}
+            tied = getattr(self.mcfg, "tie_embeddings", False)
+            ws = [p for n, p in self.model.named_parameters() if p.dim() == 2
+                  and id(p) not in skip and (tied or "embed" not in n)]
+            gemm.pack_decode_weights(ws, silu)
         if self.ps.tp_size > 1 and dev.type == "cuda" and not cfg.disable_custom_all_reduce:
             from ..parallel.custom_allreduce import maybe_init_custom_allreduce
             comm.set_custom_allreduce(maybe_init_custom_allreduce(self.ps, dev))

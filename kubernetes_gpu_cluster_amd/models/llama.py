@@ -69,7 +69,15 @@ class LlamaAttention(nn.Module):
         self.attn = PagedAttention(self.nq, self.nkv, cfg.head_dim, layer_idx)
 
     def forward(self, positions, x, ctx: ForwardContext):
-        return self.o_proj(self.attend(positions, self.qkv_proj(x), ctx))
+        return self.o_proj(self.attend(positions, self.project_qkv(x), ctx))
+
+    def project_qkv(self, x):
+        """The QKV projection; where the decode plan runs it as K9m split-K, the fp32
+        K-slices themselves (the RoPE / KV-write kernel sums them, ops/gemm.py linear_qkv)."""
+        p = self.qkv_proj
+        if p.bias is None and x.is_cuda:
+            return gemm.linear_qkv(x, p.weight)
+        return p(x)
 
     def attend(self, positions, qkv, ctx: ForwardContext):
         """RoPE + KV-cache write + paged attention on a QKV projection -> [T, nq*d]."""
@@ -78,7 +86,8 @@ class LlamaAttention(nn.Module):
                               self.nq, self.nkv, self.cfg.head_dim,
                               None if self.q_norm is None else self.q_norm.weight,
                               None if self.k_norm is None else self.k_norm.weight,
-                              self.cfg.rms_eps, k_scale=ctx.k_scale, v_scale=ctx.v_scale)
+                              self.cfg.rms_eps, k_scale=ctx.k_scale, v_scale=ctx.v_scale,
+                              dtype=self.qkv_proj.weight.dtype)
         return self.attn(q, ctx)
 
 
@@ -170,10 +179,10 @@ class LlamaForCausalLM(nn.Module):
 
     # ------------------------------------------------------------------ fused projection tails
     def _tail_fusable(self, x) -> bool:
-        """One GPU, whole model, dense bias-free MLP / o_proj, and a split-K plan at this M:
+        """One GPU, whole model, dense bias-free MLP / o_proj, and a K9m plan at this M:
         the o / down projections then run with their reduction fused into the next norm."""
         if not (x.is_cuda and self.first and self.last and self.layers and not self.cfg.is_moe
-                and get_state().tp_size == 1 and gemm.splitk_plan_has_m(x.shape[0])
+                and get_state().tp_size == 1 and gemm.dgemm_plan_has_m(x.shape[0], "tail")
                 and _tail_fusion_enabled):
             return False
         l0 = self.layers[0]
@@ -194,7 +203,7 @@ class LlamaForCausalLM(nn.Module):
                 x, residual = gemm.linear_add_rms(h, prev.mlp.down_proj.weight, residual,
                                                   ln1.weight, ln1.eps)
             at, ln2 = layer.self_attn, layer.post_attention_layernorm
-            a = at.attend(positions, at.qkv_proj(x), ctx)
+            a = at.attend(positions, at.project_qkv(x), ctx)
             x, residual = gemm.linear_add_rms(a, at.o_proj.weight, residual, ln2.weight, ln2.eps)
             h = gemm.linear_silu(x, layer.mlp.gate_up_proj.weight)
             prev = layer
@@ -223,6 +232,21 @@ class LlamaForCausalLM(nn.Module):
         l0 = self.layers[0]
         return ((l0.self_attn.qkv_proj.weight, l0.mlp.gate_up_proj.weight),
                 (l0.self_attn.o_proj.weight, l0.mlp.down_proj.weight))
+
+    def qkv_dims(self) -> dict:
+        """(N, K) of the QKV weight -> (nq, nkv, head_dim) of its RoPE / KV-write consumer
+        (ops/gemm.py tunes the K9m QKV GEMM with that kernel summing its K-slices)."""
+        if not self.layers or not hasattr(self.layers[0], "self_attn"):
+            return {}
+        at = self.layers[0].self_attn
+        if at.qkv_proj.bias is not None:
+            return {}
+        return {tuple(at.qkv_proj.weight.shape): (at.nq, at.nkv, self.cfg.head_dim)}
+
+    def silu_weights(self) -> list:
+        """The merged gate_up weights (decode: silu_mul fused into their K9m GEMM)."""
+        return [l.mlp.gate_up_proj.weight for l in self.layers
+                if isinstance(getattr(l, "mlp", None), LlamaMLP)]
 
     def silu_shapes(self) -> set:
         """(N, K) of the merged gate_up weights (their split-K reduction carries silu_mul)."""

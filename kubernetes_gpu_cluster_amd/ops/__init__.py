@@ -109,15 +109,19 @@ def rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Ten
                   q_norm_w: Optional[torch.Tensor] = None,
                   k_norm_w: Optional[torch.Tensor] = None, eps: float = 1e-6,
                   use_rope: bool = True, k_scale: float = 1.0,
-                  v_scale: float = 1.0) -> torch.Tensor:
+                  v_scale: float = 1.0, dtype: Optional[torch.dtype] = None) -> torch.Tensor:
     """k_cache / v_cache may be fp8 (torch.float8_e4m3fn): values are stored as
-    fp8(x / scale)."""
+    fp8(x / scale).  On the GPU ``qkv`` may also be the K9m split-K slices of the QKV
+    projection (fp32 [S, T, N], ops/gemm.py linear_qkv): the kernel sums them, and
+    ``dtype`` names the activation dtype of q."""
     if not _gpu(qkv):
         return ref.rope_qk_kv_write(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping,
                                     num_heads, num_kv_heads, head_dim, q_norm_w, k_norm_w, eps,
                                     use_rope, k_scale, v_scale)
-    T = qkv.shape[0]
-    q = torch.empty(T, num_heads, head_dim, dtype=qkv.dtype, device=qkv.device)
+    sl = qkv.dim() == 3
+    T = qkv.shape[1] if sl else qkv.shape[0]
+    q = torch.empty(T, num_heads, head_dim, dtype=(dtype or qkv.dtype) if sl else qkv.dtype,
+                    device=qkv.device)
     _k().rope_kv_write(qkv, positions, cos_sin, q, k_cache, v_cache, slot_mapping, q_norm_w,
                        k_norm_w, num_heads, num_kv_heads, head_dim, eps, use_rope, k_scale,
                        v_scale)

@@ -1,9 +1,9 @@
 """Linear layers on the GPU: hipBLASLt (``F.linear``), the hand-written K9 skinny
-GEMM (``csrc/kernels/gemm_skinny.hip``) for small-batch decode, or the dense split-K
-MFMA GEMM (``dense_gemm_splitk`` in ``csrc/kernels/moe.hip``: the K14 tiles with one
-K-slice per XCD, fp32 slices summed by ``splitk_reduce``) for mid-size decode batches,
-where hipBLASLt's few output tiles leave the long-K projections (the MLP down
-projection, K = 14336) at ~1.8 TB/s.
+GEMM (``csrc/kernels/gemm_skinny.hip``) for small-batch decode (M <= 64), or the K9m
+mid-batch decode GEMM (``csrc/kernels/gemm_decode.hip``: LDS-DMA ring, packed weight
+tiles, XCD-mapped split-K with the K-slice reduction fused into the consumer) for
+M = 65..512, where hipBLASLt leaves the long-K projections (the MLP down projection,
+K = 14336) at ~1.8 TB/s.
 
 Which one runs is a per-(M, N, K) decision made once at engine start by timing
 both on the model's own weights (``tune_skinny``), never guessed: at M <= 64 the GEMM
@@ -36,84 +36,140 @@ _chosen_us: dict[tuple[int, int, int], float] = {}
 _rms_us: dict[tuple[int, int], float] = {}
 _enabled = os.environ.get("KGC_SKINNY_GEMM", "1") != "0"
 
-# dense split-K: (M, N, K) -> (bm, S) where it measured faster than hipBLASLt
-SPLITK_MAX_M = 512
-_SK_CONFIGS = [(bm, S) for bm in (64, 128) for S in (2, 4, 8)]
-_plan_sk: dict[tuple[int, int, int], tuple[int, int]] = {}
-_sk_enabled = os.environ.get("KGC_SPLITK_GEMM", "1") != "0"
+# K9m mid-batch decode GEMM (csrc/kernels/gemm_decode.hip), M in (SKINNY_MAX_M, DG_MAX_M]:
+# (M, N, K, kind) -> (cfg, S) where it measured faster than hipBLASLt (+ the same consumer).
+# kind: "plain" (qkv / lm_head / any linear), "silu" (merged gate_up -> silu_mul),
+# "tail" (o / down -> residual add + RMSNorm).  S > 1: fp32 K-slices summed by the consumer.
+DG_MAX_M = 512
+_plan_dg: dict[tuple[int, int, int, str], tuple[int, int]] = {}
+_dg_enabled = os.environ.get("KGC_DGEMM", "1") != "0"
+# packed weight copies for the packed K9m tiles: (data_ptr, silu) -> [N/128, K/64, 8192]
+_packed: dict[tuple[int, bool], torch.Tensor] = {}
+_PACK_FRACTION = float(os.environ.get("KGC_DGEMM_PACK_FRACTION", "0.25"))
 
 
-def splitk_ok(M: int, N: int, K: int, cfg) -> bool:
-    bm, S = cfg
-    return 1 <= M <= SPLITK_MAX_M and N % 128 == 0 and K % 64 == 0 and K // 64 >= S
-
-
-def splitk_gemm(x: torch.Tensor, w: torch.Tensor, cfg,
-                out: Optional[torch.Tensor] = None,
-                ws: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """x W^T as S fp32 K-slices (one per XCD group) plus a reduction to x's dtype."""
+def _dg_info(cfg: int):
     from . import _k
-    bm, S = cfg
+    bm, bn, pk = _k().dgemm_cfg_info(cfg)
+    return bm, bn, bool(pk)
+
+
+def dgemm_ok(M: int, N: int, K: int) -> bool:
+    return SKINNY_MAX_M < M <= DG_MAX_M and N % 128 == 0 and K % 64 == 0
+
+
+def pack_decode_weights(plain: Iterable[torch.Tensor], silu: Iterable[torch.Tensor]) -> int:
+    """Packed copies ([N/128][K/64][128 x 64] tiles, swizzle baked in: one contiguous 16 KB
+    block per K-step of a column tile) of the decode-GEMM weights, made once at load time so
+    the K9m weight stream reads HBM in whole blocks (~5.8 vs ~4.4 TB/s for the row-major
+    tile walk, tools/dma_probe.hip).  ``silu``: merged gate_up weights, packed with gate and
+    up 16-row groups interleaved for the fused SiLU epilogue.  Skipped (row-major K9m tiles
+    only) when the copies would exceed KGC_DGEMM_PACK_FRACTION of device memory, e.g. a
+    70B model on one GPU.  Call BEFORE the KV cache is sized.  Returns bytes packed."""
+    if not _dg_enabled:
+        return 0
+    from . import _k
+    todo = []
+    for w, sl in [(w, False) for w in plain] + [(w, True) for w in silu]:
+        if (w.is_cuda and w.dim() == 2 and w.dtype in (torch.bfloat16, torch.float16)
+                and w.is_contiguous() and w.shape[0] % 128 == 0 and w.shape[1] % 64 == 0
+                and (w.data_ptr(), sl) not in _packed):
+            todo.append((w, sl))
+    need = sum(w.numel() * w.element_size() for w, _ in todo)
+    if not todo:
+        return 0
+    free, total = torch.cuda.mem_get_info(todo[0][0].device)
+    if need > _PACK_FRACTION * total or need > free - (8 << 30):
+        log.info("K9m: %.1f GB of packed weights exceeds the budget; row-major tiles only",
+                 need / 1e9)
+        return 0
+    for w, sl in todo:
+        N, K = w.shape
+        p = torch.empty(N // 128, K // 64, 8192, dtype=w.dtype, device=w.device)
+        _k().dgemm_pack(p, w, sl)
+        _packed[(w.data_ptr(), sl)] = p
+    log.info("K9m: packed %d decode weights (%.1f GB)", len(todo), need / 1e9)
+    return need
+
+
+def packed_weight(w: torch.Tensor, silu: bool = False) -> Optional[torch.Tensor]:
+    return _packed.get((w.data_ptr(), silu))
+
+
+def _dg_weight(w: torch.Tensor, cfg: int, silu: bool) -> Optional[torch.Tensor]:
+    return packed_weight(w, silu) if _dg_info(cfg)[2] else w
+
+
+def dgemm(x: torch.Tensor, w: torch.Tensor, cfg: int, S: int, epi: int = 1,
+          out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """K9m: S == 1 -> x W^T in x's dtype (epi 1) or silu-paired [M, N/2] (epi 2);
+    S > 1 -> the [S, M, N] fp32 K-slices (the caller's consumer sums them)."""
+    from . import _k
     M, N = x.shape[0], w.shape[0]
-    if ws is None:
-        ws = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
-    if out is None:
-        out = torch.empty(M, N, dtype=x.dtype, device=x.device)
-    k = _k()
-    k.dense_gemm_splitk(ws, x, w, bm)
-    k.splitk_reduce(out, ws)
+    wk = _dg_weight(w, cfg, epi == 2)
+    if wk is None:
+        raise RuntimeError("K9m plan names a packed tile but the weight was not packed")
+    if S > 1:
+        out = torch.empty(S, M, N, dtype=torch.float32, device=x.device) if out is None else out
+        _k().dgemm(out, x, wk, cfg, 0)
+    else:
+        if out is None:
+            out = torch.empty(M, N // 2 if epi == 2 else N, dtype=x.dtype, device=x.device)
+        _k().dgemm(out, x, wk, cfg, epi)
     return out
 
 
-def splitk_gemm_silu(x: torch.Tensor, w: torch.Tensor, cfg,
-                     out: Optional[torch.Tensor] = None,
-                     ws: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """silu(x Wg^T) * (x Wu^T) for a merged [gate; up] weight: the split-K slices are
-    summed and activated in one pass (``splitk_reduce_silu``), so the [M, 2I] gate_up
-    output is never materialised and no separate silu_mul runs."""
-    from . import _k
-    bm, S = cfg
-    M, N = x.shape[0], w.shape[0]
-    if ws is None:
-        ws = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
-    if out is None:
-        out = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
-    k = _k()
-    k.dense_gemm_splitk(ws, x, w, bm)
-    k.splitk_reduce_silu(out, ws)
-    return out
+def _dg_plan(x: torch.Tensor, w: torch.Tensor, kind: str):
+    if not _plan_dg or not x.is_cuda or x.dim() != 2 or x.stride(1) != 1 or x.stride(0) % 8:
+        return None
+    return _plan_dg.get((x.shape[0], w.shape[0], w.shape[1], kind))
 
 
 def linear_silu(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """silu_mul(linear(x, w, bias)) over a merged gate_up weight, with the activation
-    folded into the split-K reduction where the plan runs split-K at this (M, N, K)."""
-    from . import silu_mul
-    if (_plan_sk and bias is None and x.is_cuda and x.dim() == 2 and x.stride(1) == 1
-            and x.stride(0) % 8 == 0 and w.shape[0] % 16 == 0):
-        cfg = _plan_sk.get((x.shape[0], w.shape[0], w.shape[1]))
-        if cfg is not None:
-            return splitk_gemm_silu(x, w, cfg)
+    """silu_mul(linear(x, w, bias)) over a merged gate_up weight: where the plan runs K9m
+    at this (M, N, K) the activation is the GEMM's epilogue (S = 1) or rides the split-K
+    reduction (``splitk_reduce_silu``), so the [M, 2I] gate_up output never exists."""
+    from . import _k, silu_mul
+    if bias is None:
+        p = _dg_plan(x, w, "silu")
+        if p is not None:
+            cfg, S = p
+            if S == 1:
+                return dgemm(x, w, cfg, 1, epi=2)
+            ws = dgemm(x, w, cfg, S)
+            out = torch.empty(x.shape[0], w.shape[0] // 2, dtype=x.dtype, device=x.device)
+            _k().splitk_reduce_silu(out, ws)
+            return out
     return silu_mul(linear(x, w, bias))
+
+
+def linear_qkv(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """The QKV projection for the fused RoPE / KV-write kernel: x W^T, or -- where the plan
+    runs K9m split-K at this (M, N, K) -- its fp32 K-slices [S, M, N], which that kernel
+    sums (``ops.rope_kv_write``), so the reduction needs no launch of its own."""
+    p = _dg_plan(x, w, "qkv")
+    if p is not None:
+        cfg, S = p
+        return dgemm(x, w, cfg, S)
+    return linear(x, w)
 
 
 def linear_add_rms(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor,
                    gamma: torch.Tensor, eps: float) -> tuple[torch.Tensor, torch.Tensor]:
     """residual += x W^T; returns (rms_norm(residual) * gamma, residual) -- a row-parallel
     projection (o / down, TP = 1) and the fused add + RMSNorm that consumes it.  Where the
-    plan runs split-K at this (M, N, K), the slice reduction, residual add and norm are one
-    kernel (``splitk_add_rms_norm``); otherwise the GEMM and ``fused_add_rms_norm`` run."""
+    plan runs K9m split-K at this (M, N, K), the slice reduction, residual add and norm are
+    one kernel (``splitk_add_rms_norm``); otherwise the GEMM and ``fused_add_rms_norm``."""
     from . import _k, fused_add_rms_norm
-    if (_plan_sk and x.is_cuda and x.dim() == 2 and x.stride(1) == 1 and x.stride(0) % 8 == 0
-            and w.shape[0] <= 8192 and residual.is_contiguous()):
-        cfg = _plan_sk.get((x.shape[0], w.shape[0], w.shape[1]))
-        if cfg is not None:
-            bm, S = cfg
-            ws = torch.empty(S, x.shape[0], w.shape[0], dtype=torch.float32, device=x.device)
+    p = _dg_plan(x, w, "tail")
+    if p is not None and w.shape[0] <= 8192 and residual.is_contiguous():
+        cfg, S = p
+        if S > 1:
+            ws = dgemm(x, w, cfg, S)
             out = torch.empty_like(residual)
-            k = _k()
-            k.dense_gemm_splitk(ws, x, w, bm)
-            k.splitk_add_rms_norm(out, ws, residual, gamma, eps)
+            _k().splitk_add_rms_norm(out, ws, residual, gamma, eps)
             return out, residual
+        return fused_add_rms_norm(dgemm(x, w, cfg, 1), residual, gamma, eps)
     return fused_add_rms_norm(linear(x, w), residual, gamma, eps)
 
 
@@ -137,11 +193,17 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         cfg = _plan.get((x.shape[0], w.shape[0], w.shape[1]))
         if cfg is not None and x.stride(1) == 1:
             return skinny_gemm(x, w, bias, cfg)
-    if (_plan_sk and bias is None and x.is_cuda and x.dim() == 2 and x.stride(1) == 1
-            and x.stride(0) % 8 == 0):
-        cfg = _plan_sk.get((x.shape[0], w.shape[0], w.shape[1]))
-        if cfg is not None:
-            return splitk_gemm(x, w, cfg)
+    if bias is None:
+        p = _dg_plan(x, w, "plain")
+        if p is not None:
+            cfg, S = p
+            if S == 1:
+                return dgemm(x, w, cfg, 1)
+            from . import _k
+            ws = dgemm(x, w, cfg, S)
+            out = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
+            _k().splitk_reduce(out, ws)
+            return out
     return F.linear(x, w, bias)
 
 
@@ -184,7 +246,7 @@ def fused_norm_plan(M: int, norm_shapes, acc_shapes):
 
 
 def clear_plan() -> None:
-    _plan_sk.clear()
+    _plan_dg.clear()
     _plan_norm.clear()
     _chosen_us.clear()
     _rms_us.clear()
@@ -195,12 +257,12 @@ def plan() -> dict:
     return dict(_plan)
 
 
-def splitk_plan() -> dict:
-    return dict(_plan_sk)
+def dgemm_plan() -> dict:
+    return dict(_plan_dg)
 
 
-def splitk_plan_has_m(M: int) -> bool:
-    return _sk_enabled and any(k[0] == M for k in _plan_sk)
+def dgemm_plan_has_m(M: int, kind: str) -> bool:
+    return _dg_enabled and any(k[0] == M and k[3] == kind for k in _plan_dg)
 
 
 def _time(fn, reps: int) -> float:
@@ -218,7 +280,7 @@ def _time(fn, reps: int) -> float:
 @torch.inference_mode()
 def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: float = 0.97,
                 reps: int = 3, norm_shapes=(), norm_max_m: int = 16, silu_shapes=(),
-                tail_shapes=()) -> dict:
+                tail_shapes=(), qkv_dims=None) -> dict:
     """Time hipBLASLt against every skinny configuration for each weight shape and
     batch size M (decode buckets <= SKINNY_MAX_M) and record the skinny kernel where it
     is faster by more than ``1 - margin``.  Each timing sweeps ALL weights of the shape
@@ -268,63 +330,110 @@ def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: floa
                 _tune_norm(ws, x, out, M, N, K, reps)
             log.info("gemm M=%d N=%d K=%d: hipBLASLt %.1f us, skinny %s %.1f us -> %s", M, N, K,
                      lib_t * 1e3 / n, sk_cfg, sk_t * 1e3 / n, "skinny" if best else "hipBLASLt")
-        if _sk_enabled:
-            _tune_splitk(ws, N, K, [m for m in ms if SKINNY_MAX_M < m <= SPLITK_MAX_M], margin,
-                         reps, res, silu=(N, K) in silu_shapes, tail=(N, K) in tail_shapes)
+        if _dg_enabled:
+            qd = (qkv_dims or {}).get((N, K))
+            kind = ("silu" if (N, K) in silu_shapes else
+                    "tail" if (N, K) in tail_shapes else "qkv" if qd else "plain")
+            _tune_dgemm(ws, N, K, [m for m in ms if SKINNY_MAX_M < m <= DG_MAX_M], margin,
+                        reps, res, kind, qd)
     log.info("GEMM tuning: %d shapes in %.1f s", len(res), time.time() - t0)
     return res
 
 
-def _tune_splitk(ws, N: int, K: int, ms, margin: float, reps: int, res: dict,
-                 silu: bool = False, tail: bool = False) -> None:
-    """hipBLASLt vs every dense split-K configuration at each M in ``ms``, over all
-    weights of the shape (HBM-resident, as in a decode step).  ``silu``: both sides
-    include the SiLU-and-mul that follows a gate_up projection; ``tail``: both sides
-    include the residual add + RMSNorm that consumes an o / down projection."""
-    from . import _k, fused_add_rms_norm, silu_mul
-    for M in sorted(set(ms)):
-        if not splitk_ok(M, N, K, (64, 1)):
+# K9m candidates per M range: (cfg ids, split factors).  Packed tiles only when the weight
+# was packed; 4 loader waves (6, 7) and split loaders (8, 9) per tools/dgemm_bench.py.
+def _dg_candidates(M: int, N: int, K: int, kind: str, packed: bool):
+    from . import _k
+    cfgs = [5, 7, 2] if M <= 128 else [6, 8, 4, 0]
+    out = []
+    for c in range(_k().dgemm_num_cfgs()):
+        if c not in cfgs:
             continue
-        x = torch.randn(M, K, dtype=ws[0].dtype, device=ws[0].device)
-        out = torch.empty(M, N // 2 if silu else N, dtype=x.dtype, device=x.device)
-        act = torch.empty(M, N // 2, dtype=x.dtype, device=x.device) if silu else None
-        tail = tail and not silu and N <= 8192
-        res_t = torch.zeros(M, N, dtype=x.dtype, device=x.device) if tail else None
-        gamma = torch.ones(N, dtype=x.dtype, device=x.device) if tail else None
+        bm, bn, pk = _dg_info(c)
+        if (pk and not packed) or N % bn:
+            continue
+        splits = (1,) if kind == "silu" else (1, 2, 4, 8)
+        for S in splits:
+            if S <= K // 64:
+                out.append((c, S))
+    return out
+
+
+def _tune_dgemm(ws, N: int, K: int, ms, margin: float, reps: int, res: dict,
+                kind: str, qkv_dims=None) -> None:
+    """hipBLASLt vs the K9m candidates at each M in ``ms``, over all weights of the shape
+    (HBM-resident, as in a decode step), each side timed WITH its consumer: "silu" the
+    SiLU-and-mul, "tail" the residual add + RMSNorm, "qkv" the RoPE / KV-write kernel
+    (which sums the K-slices itself), "plain" the split-K reduction."""
+    from . import _k, fused_add_rms_norm, rope_kv_write, silu_mul
+    packed = all(packed_weight(w, kind == "silu") is not None for w in ws)
+    for M in sorted(set(ms)):
+        if not dgemm_ok(M, N, K) or (kind == "tail" and N > 8192):
+            continue
+        dev, dt = ws[0].device, ws[0].dtype
+        x = torch.randn(M, K, dtype=dt, device=dev)
+        res_t = torch.zeros(M, N, dtype=dt, device=dev) if kind == "tail" else None
+        gamma = torch.ones(N, dtype=dt, device=dev) if kind == "tail" else None
+        act = torch.empty(M, N // 2, dtype=dt, device=dev) if kind == "silu" else None
+        if kind == "qkv":
+            # the RoPE / KV-write consumer on a scratch cache (every token to block 1)
+            nq, nkv, hd = qkv_dims
+            pos = torch.zeros(M, dtype=torch.int64, device=dev)
+            slots = torch.arange(M, dtype=torch.int64, device=dev) % 32 + 32
+            cs = torch.zeros(1, hd, dtype=torch.float32, device=dev)
+            kc = torch.zeros(2, nkv, 32, hd, dtype=dt, device=dev)
+            vc = torch.zeros(2, nkv, 4, hd, 8, dtype=dt, device=dev)
+
+            def consume(y):
+                rope_kv_write(y, pos, cs, kc, vc, slots, nq, nkv, hd, dtype=dt)
 
         def lib():
             for w in ws:
                 y = F.linear(x, w)
-                if silu:
+                if kind == "silu":
                     silu_mul(y, act)
-                elif tail:
+                elif kind == "tail":
                     fused_add_rms_norm(y, res_t, gamma, 1e-6)
+                elif kind == "qkv":
+                    consume(y)
         lib_t = _time(lib, reps)
         best_t, best_cfg = float("inf"), None
+        for cfg, S in _dg_candidates(M, N, K, kind, packed):
+            wl = [_dg_weight(w, cfg, kind == "silu") for w in ws]
+            buf = (torch.empty(S, M, N, dtype=torch.float32, device=x.device) if S > 1 else
+                   torch.empty(M, N // 2 if kind == "silu" else N, dtype=x.dtype,
+                               device=x.device))
+            red = torch.empty(M, N // 2 if kind == "silu" else N, dtype=x.dtype, device=x.device)
 
-        def sk_tail(x, w, cfg, out, buf):
-            _k().dense_gemm_splitk(buf, x, w, cfg[0])
-            _k().splitk_add_rms_norm(out, buf, res_t, gamma, 1e-6)
-        sk_fn = splitk_gemm_silu if silu else (sk_tail if tail else splitk_gemm)
-        for cfg in _SK_CONFIGS:
-            if not splitk_ok(M, N, K, cfg) or (cfg[0] == 128 and M <= 64):
-                continue
-            buf = torch.empty(cfg[1], M, N, dtype=torch.float32, device=x.device)
-
-            def sk(cfg=cfg, buf=buf):
-                for w in ws:
-                    sk_fn(x, w, cfg, out, buf)
-            t = _time(sk, reps)
+            def run(cfg=cfg, S=S, wl=wl, buf=buf, red=red):
+                for w in wl:
+                    if S == 1:
+                        _k().dgemm(buf, x, w, cfg, 2 if kind == "silu" else 1)
+                        if kind == "tail":
+                            fused_add_rms_norm(buf, res_t, gamma, 1e-6)
+                        elif kind == "qkv":
+                            consume(buf)
+                    else:
+                        _k().dgemm(buf, x, w, cfg, 0)
+                        if kind == "qkv":
+                            consume(buf)
+                        elif kind == "silu":
+                            _k().splitk_reduce_silu(red, buf)
+                        elif kind == "tail":
+                            _k().splitk_add_rms_norm(red, buf, res_t, gamma, 1e-6)
+                        else:
+                            _k().splitk_reduce(red, buf)
+            t = _time(run, reps)
             if t < best_t:
-                best_t, best_cfg = t, cfg
+                best_t, best_cfg = t, (cfg, S)
         n = len(ws)
         chosen = best_cfg if best_t < lib_t * margin else None
         if chosen is not None:
-            _plan_sk[(M, N, K)] = chosen
-        res[(M, N, K)] = (chosen, lib_t * 1e3 / n, best_t * 1e3 / n, best_cfg)
-        log.info("gemm M=%d N=%d K=%d%s: hipBLASLt %.1f us, split-K %s %.1f us -> %s", M, N, K,
-                 " +silu" if silu else (" +add_rms" if tail else ""), lib_t * 1e3 / n,
-                 best_cfg, best_t * 1e3 / n, "split-K" if chosen else "hipBLASLt")
+            _plan_dg[(M, N, K, kind)] = chosen
+        res[(M, N, K, kind)] = (chosen, lib_t * 1e3 / n, best_t * 1e3 / n, best_cfg)
+        log.info("gemm M=%d N=%d K=%d %s: hipBLASLt %.1f us, K9m %s %.1f us -> %s", M, N, K,
+                 kind, lib_t * 1e3 / n, best_cfg, best_t * 1e3 / n,
+                 "K9m" if chosen else "hipBLASLt")
 
 
 def _tune_norm(ws, x, out, M: int, N: int, K: int, reps: int) -> None:

@@ -36,7 +36,7 @@ def test_tail_fusion_not_taken_on_cpu():
     from kubernetes_gpu_cluster_amd.models.llama import LlamaForCausalLM
     cfg = configs.PRESETS["tiny-llama"]
     m = LlamaForCausalLM(cfg, torch.float32, torch.device("cpu"))
-    gemm._plan_sk[(4, 1, 1)] = (64, 2)
+    gemm._plan_dg[(4, 1, 1, "tail")] = (2, 2)
     try:
         assert not m._tail_fusable(torch.zeros(4, cfg.hidden_size))
     finally:

@@ -81,6 +81,35 @@ def test_rope_kv_write(gpu, dt, qk_norm, d):
     torch.testing.assert_close(vc.cpu().float(), vc2.float(), atol=0, rtol=0)
 
 
+@pytest.mark.parametrize("S", [1, 2, 4])
+@pytest.mark.parametrize("qk_norm", [False, True])
+def test_rope_kv_write_from_splitk_slices(gpu, S, qk_norm):
+    """The K9m QKV slices (fp32 [S, T, N]) summed inside rope_kv_write == rope_kv_write on
+    the bf16-rounded sum (what a separate reduction kernel would hand it), bit for bit."""
+    torch.manual_seed(7 + S)
+    T, nq, nkv, d, bs, nb = 40, 8, 2, 128, 16, 12
+    N = (nq + 2 * nkv) * d
+    sl = torch.randn(S, T, N, dtype=torch.float32, device=gpu)
+    pos = torch.randint(0, 1000, (T,), device=gpu)
+    slots = torch.randperm(nb * bs, device=gpu)[:T]
+    cs = ref.rope_cos_sin_cache(d, 2048, 5e5).to(gpu)
+    qn = torch.randn(d, dtype=torch.bfloat16, device=gpu) if qk_norm else None
+    kn = torch.randn(d, dtype=torch.bfloat16, device=gpu) if qk_norm else None
+    kc, vc = _cache(nb, nkv, bs, d, torch.bfloat16, gpu)
+    kc2, vc2 = kc.clone(), vc.clone()
+    q = ops.rope_kv_write(sl, pos, cs, kc, vc, slots, nq, nkv, d, qn, kn, 1e-6,
+                          dtype=torch.bfloat16)
+    summed = sl[0].clone()
+    for z in range(1, S):
+        summed += sl[z]
+    q2 = ops.rope_kv_write(summed.to(torch.bfloat16), pos, cs, kc2, vc2, slots, nq, nkv, d, qn,
+                           kn, 1e-6)
+    assert q.dtype == torch.bfloat16
+    torch.testing.assert_close(q, q2, atol=0, rtol=0)
+    torch.testing.assert_close(kc, kc2, atol=0, rtol=0)
+    torch.testing.assert_close(vc, vc2, atol=0, rtol=0)
+
+
 def _fill_random_cache(B, ctx_lens, nkv, bs, d, dt, dev, nb_extra=7):
     max_blocks = max(math.ceil(c / bs) for c in ctx_lens) + 1
     nb = sum(math.ceil(c / bs) for c in ctx_lens) + nb_extra
@@ -423,34 +452,71 @@ def test_skinny_gemm_norm_and_accumulate(gpu, M, nw):
     torch.testing.assert_close(c.float().cpu(), exp, atol=6e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("M,N,K,bm,S", [(256, 1024, 4096, 128, 8), (80, 768, 2048, 64, 4),
-                                        (144, 512, 1024, 128, 2), (33, 256, 8192, 64, 8)])
-def test_dense_gemm_splitk_matches_fp32(gpu, M, N, K, bm, S):
-    """Dense split-K decode GEMM (XCD-mapped K-slices) + reduction vs an fp32 matmul,
-    including M not a multiple of the row block (clamped loads, masked stores)."""
+@pytest.mark.parametrize("cfg", list(range(10)))
+@pytest.mark.parametrize("M,N,K", [(256, 1024, 4096), (200, 768, 1024), (77, 512, 2048)])
+def test_dgemm_matches_fp32(gpu, cfg, M, N, K):
+    """K9m decode GEMM (every tile config, packed and row-major weights) vs an fp32 matmul:
+    bf16 output (S = 1), fp32 split-K slices (S = 2, 4) and the fused SiLU epilogue, with M
+    not a multiple of the row block (clamped loads, masked stores)."""
     from kubernetes_gpu_cluster_amd.ops import gemm
-    torch.manual_seed(M + N)
+    k = torch.ops.kgc
+    bm, bn, pk = k.dgemm_cfg_info(cfg)
+    if N % bn:
+        pytest.skip("N not a multiple of BN")
+    torch.manual_seed(M + N + cfg)
     x = torch.randn(M, K, dtype=torch.bfloat16, device=gpu)
     w = torch.randn(N, K, dtype=torch.bfloat16, device=gpu) * 0.02
     ref = x.float().cpu() @ w.float().cpu().t()
-    ws = torch.full((S, M, N), float("nan"), dtype=torch.float32, device=gpu)
-    got = gemm.splitk_gemm(x, w, (bm, S), ws=ws)
-    torch.testing.assert_close(got.float().cpu(), ref, atol=3e-2, rtol=2e-2)
-    # every slice row was written (no NaN left from the fill), and slices sum to the result
-    torch.testing.assert_close(ws.sum(0).cpu(), ref, atol=2e-3, rtol=2e-3)
+
+    def weight(silu):
+        if not pk:
+            return w
+        p = torch.empty(N // 128, K // 64, 8192, dtype=w.dtype, device=gpu)
+        k.dgemm_pack(p, w, silu)
+        return p
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
+    k.dgemm(out, x, weight(False), cfg, 1)
+    torch.testing.assert_close(out.float().cpu(), ref, atol=3e-2, rtol=2e-2)
+    for S in (2, 4):
+        ws = torch.full((S, M, N), float("nan"), dtype=torch.float32, device=gpu)
+        k.dgemm(ws, x, weight(False), cfg, 0)
+        # every slice row was written (no NaN left) and the slices sum to the product
+        torch.testing.assert_close(ws.sum(0).cpu(), ref, atol=2e-3, rtol=2e-3)
+    act = torch.empty(M, N // 2, dtype=torch.bfloat16, device=gpu)
+    k.dgemm(act, x, weight(True), cfg, 2)
+    exp = torch.nn.functional.silu(ref[:, : N // 2]) * ref[:, N // 2:]
+    torch.testing.assert_close(act.float().cpu(), exp, atol=3e-2, rtol=2e-2)
 
 
-def test_linear_uses_splitk_plan(gpu):
+def test_dgemm_pack_layout(gpu):
+    """The packed tile [nb][kb][r][pos] holds W[nb*128 + r][kb*64 + (pos ^ r%8)*8 ..]."""
+    k = torch.ops.kgc
+    N, K = 256, 128
+    w = torch.arange(N * K, dtype=torch.float32).reshape(N, K).to(torch.float16).to(gpu)
+    p = torch.empty(N // 128, K // 64, 8192, dtype=w.dtype, device=gpu)
+    k.dgemm_pack(p, w, False)
+    pc = p.cpu().view(N // 128, K // 64, 128, 8, 8)
+    wc = w.cpu()
+    for nb, kb, r, pos in [(0, 0, 0, 0), (1, 1, 5, 3), (0, 1, 127, 7), (1, 0, 64, 2)]:
+        src = wc[nb * 128 + r, kb * 64 + (pos ^ (r % 8)) * 8: kb * 64 + (pos ^ (r % 8)) * 8 + 8]
+        assert torch.equal(pc[nb, kb, r, pos], src)
+
+
+def test_linear_uses_dgemm_plan(gpu):
     from kubernetes_gpu_cluster_amd.ops import gemm
     torch.manual_seed(5)
     w = torch.randn(1024, 4096, dtype=torch.bfloat16, device=gpu) * 0.02
     x = torch.randn(96, 4096, dtype=torch.bfloat16, device=gpu)
-    gemm._plan_sk[(96, 1024, 4096)] = (64, 4)
+    assert gemm.pack_decode_weights([w], []) > 0
     try:
-        got = gemm.linear(x, w)
+        for plan in [(5, 4), (2, 1), (6, 2)]:
+            gemm._plan_dg[(96, 1024, 4096, "plain")] = plan
+            got = gemm.linear(x, w)
+            torch.testing.assert_close(got.float(), (x.float() @ w.float().t()), atol=3e-2,
+                                       rtol=2e-2)
     finally:
         gemm.clear_plan()
-    torch.testing.assert_close(got.float(), (x.float() @ w.float().t()), atol=3e-2, rtol=2e-2)
+        gemm._packed.clear()
 
 
 def test_linear_uses_tuned_plan(gpu):
@@ -466,34 +532,32 @@ def test_linear_uses_tuned_plan(gpu):
 
 
 
-@pytest.mark.parametrize("M,N,K,bm,S", [(256, 2048, 4096, 128, 4), (80, 1536, 2048, 64, 8),
-                                        (33, 512, 1024, 64, 2)])
-def test_splitk_gemm_silu_matches_fp32(gpu, M, N, K, bm, S):
-    """gate_up split-K GEMM with SiLU-and-mul folded into the slice reduction vs an fp32
-    silu(g) * u reference (N = 2I, merged [gate; up] weight)."""
+@pytest.mark.parametrize("M,N,K,plan", [(256, 2048, 4096, (8, 1)), (80, 1536, 2048, (5, 1)),
+                                         (144, 1024, 1024, (0, 2)), (96, 2048, 2048, (2, 1))])
+def test_linear_silu_dgemm_matches_fp32(gpu, M, N, K, plan):
+    """gate_up through the K9m plan -- fused SiLU epilogue (S = 1, packed silu weights) or
+    split-K slices summed by splitk_reduce_silu -- vs an fp32 silu(g) * u reference."""
     from kubernetes_gpu_cluster_amd.ops import gemm
     torch.manual_seed(M + N + 1)
     x = torch.randn(M, K, dtype=torch.bfloat16, device=gpu)
     w = torch.randn(N, K, dtype=torch.bfloat16, device=gpu) * 0.03
     y = x.float().cpu() @ w.float().cpu().t()
-    g, u = y[:, : N // 2], y[:, N // 2:]
-    ref = torch.nn.functional.silu(g) * u
-    got = gemm.splitk_gemm_silu(x, w, (bm, S))
-    assert got.shape == (M, N // 2)
-    torch.testing.assert_close(got.float().cpu(), ref, atol=3e-2, rtol=2e-2)
-    # through the dispatcher: linear_silu takes the plan's split-K path
-    gemm._plan_sk[(M, N, K)] = (bm, S)
+    ref = torch.nn.functional.silu(y[:, : N // 2]) * y[:, N // 2:]
+    gemm.pack_decode_weights([w], [w])
+    gemm._plan_dg[(M, N, K, "silu")] = plan
     try:
-        got2 = gemm.linear_silu(x, w)
+        got = gemm.linear_silu(x, w)
     finally:
         gemm.clear_plan()
-    torch.testing.assert_close(got2, got)
+        gemm._packed.clear()
+    assert got.shape == (M, N // 2)
+    torch.testing.assert_close(got.float().cpu(), ref, atol=3e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("M,N,K,bm,S", [(256, 4096, 4096, 64, 4), (96, 4096, 14336, 64, 8),
-                                        (40, 1024, 2048, 128, 2)])
-def test_linear_add_rms_splitk_matches_fp32(gpu, M, N, K, bm, S):
-    """Split-K reduction fused into residual add + RMSNorm vs an fp32 reference of
+@pytest.mark.parametrize("M,N,K,plan", [(256, 4096, 4096, (6, 4)), (96, 4096, 14336, (5, 8)),
+                                         (130, 1024, 2048, (4, 1))])
+def test_linear_add_rms_dgemm_matches_fp32(gpu, M, N, K, plan):
+    """K9m split-K reduction fused into residual add + RMSNorm vs an fp32 reference of
     residual += x W^T; out = rms_norm(residual) * gamma."""
     from kubernetes_gpu_cluster_amd.ops import gemm
     torch.manual_seed(M + K)
@@ -503,18 +567,20 @@ def test_linear_add_rms_splitk_matches_fp32(gpu, M, N, K, bm, S):
     gamma = torch.rand(N, dtype=torch.bfloat16, device=gpu) + 0.5
     r32 = res.float().cpu() + (x.float().cpu() @ w.float().cpu().t())
     exp = r32 * torch.rsqrt(r32.pow(2).mean(-1, keepdim=True) + 1e-5) * gamma.float().cpu()
-    gemm._plan_sk[(M, N, K)] = (bm, S)
+    gemm.pack_decode_weights([w], [])
+    gemm._plan_dg[(M, N, K, "tail")] = plan
     try:
         out, r = gemm.linear_add_rms(x, w, res, gamma, 1e-5)
     finally:
         gemm.clear_plan()
+        gemm._packed.clear()
     assert r.data_ptr() == res.data_ptr()   # residual updated in place
     torch.testing.assert_close(r.float().cpu(), r32, atol=5e-2, rtol=2e-2)
     torch.testing.assert_close(out.float().cpu(), exp, atol=5e-2, rtol=2e-2)
 
 
 def test_tail_fused_model_matches_regular_path(gpu):
-    """Whole-model forward with o/down reductions fused into the norms (forced split-K
+    """Whole-model forward with o/down reductions fused into the norms (forced K9m split-K
     plan) vs the regular layer loop on the same weights."""
     from kubernetes_gpu_cluster_amd.models import configs
     from kubernetes_gpu_cluster_amd.models.llama import LlamaForCausalLM
@@ -541,7 +607,7 @@ def test_tail_fused_model_matches_regular_path(gpu):
         ref_out = model(ids, None, _Ctx())
         for l in model.layers:
             for w in (l.self_attn.o_proj.weight, l.mlp.down_proj.weight):
-                gemm._plan_sk[(M, w.shape[0], w.shape[1])] = (64, 4)
+                gemm._plan_dg[(M, w.shape[0], w.shape[1], "tail")] = (2, 4)
         llama_mod._tail_fusion_enabled = True
         assert model._tail_fusable(x)
         got = model(ids, None, _Ctx())
