@@ -508,6 +508,14 @@ int64_t ar_open_handle(Tensor h) {
 }
 void ar_close_handle(int64_t p) { kgc::ar_close_handle((void*)(intptr_t)p); }
 int64_t ar_read_err(int64_t sig) { return (int64_t)kgc::ar_read_err((void*)(intptr_t)sig); }
+// host_out: pinned int32 [1]; valid once the current stream has passed this point
+void ar_err_copy_async(int64_t sig, Tensor host_out) {
+  TORCH_CHECK(host_out.device().is_cpu() && host_out.is_pinned() &&
+              host_out.scalar_type() == at::kInt && host_out.numel() >= 1,
+              "host_out: pinned int32 [1]");
+  kgc::ar_err_copy_async((void*)(intptr_t)sig, reinterpret_cast<uint32_t*>(host_out.data_ptr()),
+                         stream());
+}
 
 void xgmi_allreduce(Tensor inout, std::vector<int64_t> data, std::vector<int64_t> sig, int64_t rank,
                     int64_t cap_bytes, bool two_shot) {
@@ -622,6 +630,7 @@ TORCH_LIBRARY(kgc, m) {
   m.def("ar_open_handle(Tensor handle) -> int", &ar_open_handle);
   m.def("ar_close_handle(int ptr) -> ()", &ar_close_handle);
   m.def("ar_read_err(int sig) -> int", &ar_read_err);
+  m.def("ar_err_copy_async(int sig, Tensor(a!) host_out) -> ()", &ar_err_copy_async);
   m.def("xgmi_allreduce(Tensor(a!) inout, int[] data, int[] sig, int rank, int cap_bytes, "
         "bool two_shot) -> ()");
   m.def("prefill_block_m() -> int", &prefill_block_m);

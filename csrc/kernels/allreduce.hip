@@ -199,6 +199,13 @@ void* ar_open_handle(const uint8_t* in64) {
 
 void ar_close_handle(void* p) { ar_check(hipIpcCloseMemHandle(p), "hipIpcCloseMemHandle"); }
 
+// stream-ordered copy of the sticky error word (read on the host once the step is done)
+void ar_err_copy_async(void* sig, uint32_t* host_dst, hipStream_t s) {
+  ar_check(hipMemcpyAsync(host_dst, &reinterpret_cast<ArSignal*>(sig)->err, 4,
+                          hipMemcpyDeviceToHost, s),
+           "xgmi allreduce: error word copy");
+}
+
 uint32_t ar_read_err(void* sig) {
   uint32_t e = 0;
   ar_check(hipMemcpy(&e, &reinterpret_cast<ArSignal*>(sig)->err, 4, hipMemcpyDeviceToHost),

@@ -101,5 +101,6 @@ void ar_get_handle(void* p, uint8_t* out64);
 void* ar_open_handle(const uint8_t* in64);
 void ar_close_handle(void* p);
 uint32_t ar_read_err(void* sig);
+void ar_err_copy_async(void* sig, uint32_t* host_dst, hipStream_t s);
 
 }  // namespace kgc

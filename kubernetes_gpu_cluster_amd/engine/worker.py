@@ -31,6 +31,7 @@ from .. import ops
 from ..models import load_model, resolve_model
 from ..models.moe import set_moe_mode
 from ..parallel import comm
+from .health import RankWatchdog, watch_parent
 from ..parallel.state import destroy_parallel, get_state, init_parallel
 from .config import EngineConfig
 from .model_runner import ModelRunner, StepPlan
@@ -201,16 +202,22 @@ class LocalExecutor:
 class TokenFuture:
     """Sampled ids of a launched step; result() blocks until the D2H copy landed.
     ``logprobs()`` -> {sampled row: (logprob of the sampled token, [(id, logprob)] top-k)}
-    for the rows whose requests asked for logprobs."""
+    for the rows whose requests asked for logprobs.  ``on_done`` runs once the step has
+    completed on the device (failure checks: engine/health.py)."""
 
-    def __init__(self, buf: torch.Tensor, ev=None, values: Optional[list[int]] = None, lp=None):
+    def __init__(self, buf: torch.Tensor, ev=None, values: Optional[list[int]] = None, lp=None,
+                 on_done=None):
         self.buf, self.ev, self.values, self._lp = buf, ev, values, lp
+        self._on_done = on_done
 
     def result(self) -> list[int]:
         if self.values is None:
             if self.ev is not None:
                 self.ev.synchronize()
             self.values = self.buf.tolist()
+            if self._on_done is not None:
+                done, self._on_done = self._on_done, None
+                done()
         return self.values
 
     def logprobs(self) -> dict:
@@ -225,6 +232,23 @@ class TokenFuture:
 class _DistExecutorBase:
     """Rank 0 side of the command protocol (shared by spawned / torchrun ranks)."""
     worker: Worker
+    watchdog: Optional[RankWatchdog] = None
+
+    def _step_launched(self):
+        """Book-keeping after a step's kernels are enqueued: progress for the watchdog, and
+        an async copy of the xGMI all-reduce error word checked when the step completes."""
+        if self.watchdog is not None:
+            self.watchdog.step_begin()
+        car = comm.get_custom_allreduce()
+        if car is not None:
+            car.enqueue_err_read()
+
+        def done():
+            if self.watchdog is not None:
+                self.watchdog.step_end()
+            if car is not None:
+                car.raise_if_failed()
+        return done
 
     @property
     def runner(self) -> ModelRunner:
@@ -248,24 +272,39 @@ class _DistExecutorBase:
         return get_state().pp_size == 1
 
     def execute_async(self, plan: StepPlan) -> TokenFuture:
+        if self.watchdog is not None:
+            self.watchdog.step_begin()
         _bcast_cmd(CMD_STEP, 0, plan.header())
         _bcast_plan_blobs(self.worker.runner, plan.header())
         out = self.worker.run(plan)
-        return TokenFuture(*self.runner.tokens_to_host(out), lp=self.runner.take_logprobs())
+        if self.watchdog is not None:
+            self.watchdog.step_end()
+        return TokenFuture(*self.runner.tokens_to_host(out), lp=self.runner.take_logprobs(),
+                           on_done=self._step_launched())
 
     def execute(self, plan: StepPlan) -> list[int]:
+        if self.watchdog is not None:
+            self.watchdog.step_begin()
         _bcast_cmd(CMD_STEP, 0, plan.header())
         _bcast_plan_blobs(self.worker.runner, plan.header())
         out = self.worker.run(plan)
+        done = self._step_launched()
         s = get_state()
         if s.pp_size > 1:
             t = torch.empty(plan.S, dtype=torch.int64)
             src = getattr(s, "global_base", 0) + (s.pp_size - 1) * s.tp_size
             dist.recv(t, src=src, group=s.cpu_group)
-            return t.tolist()
-        return out.tolist()
+            res = t.tolist()
+        else:
+            res = out.tolist()
+        done()
+        if self.watchdog is not None:
+            self.watchdog.step_end()
+        return res
 
     def shutdown(self) -> None:
+        if self.watchdog is not None:
+            self.watchdog.stop()          # the ranks are about to exit on purpose
         try:
             _bcast_cmd(CMD_EXIT)
         except Exception:  # noqa: BLE001
@@ -291,6 +330,7 @@ def _spawn_entry(rank: int, cfg: EngineConfig, env: dict, local: Optional[int] =
     os.environ.update(env)
     os.environ["RANK"] = str(rank)
     os.environ["LOCAL_RANK"] = str(local)
+    watch_parent()            # never outlive the driver (engine/health.py)
     try:
         w = Worker(cfg, rank=rank, local_device=local)
         worker_loop(w)
@@ -330,6 +370,8 @@ class MultiprocExecutor(_DistExecutorBase):
             if k in os.environ:
                 env[k] = os.environ[k]
         self.procs = spawn_local_ranks(cfg, env, 1, cfg.ranks_per_node)
+        # a dead rank or a step stuck in a collective ends this process (engine/health.py)
+        self.watchdog = RankWatchdog(self.procs).start()
         os.environ.update(env)
         os.environ["RANK"] = "0"
         os.environ["LOCAL_RANK"] = "0"

@@ -472,17 +472,30 @@ def _serve(ns, cfg: EngineConfig, connect=None, core_proc=None, sock=None) -> No
     app = build_app(eng, tok, name, eng.engine.max_model_len)
     server = uvicorn.Server(uvicorn.Config(app, host=ns.host, port=ns.port,
                                            log_level=ns.uvicorn_log_level))
-    if connect is not None:
-        def watchdog():
-            while not server.should_exit:
-                time.sleep(1.0)
-                if not eng.is_alive:
-                    server.should_exit = True
-        threading.Thread(target=watchdog, name="kgc-api-watchdog", daemon=True).start()
+    dead = threading.Event()
+
+    def watchdog():
+        # the engine (core process, its TP/PP ranks, or the in-process loop) died: stop
+        # serving and exit non-zero so the pod restarts (engine/health.py); /health
+        # answers 503 meanwhile
+        while not server.should_exit:
+            time.sleep(0.5)
+            if not eng.is_alive:
+                logging.getLogger("kgc.api").critical("engine is dead; shutting down")
+                dead.set()
+                server.should_exit = True
+    threading.Thread(target=watchdog, name="kgc-api-watchdog", daemon=True).start()
     try:
         server.run(sockets=[sock] if sock is not None else None)
     finally:
-        eng.shutdown()
+        if dead.is_set():
+            t = threading.Thread(target=eng.shutdown, daemon=True)
+            t.start()
+            t.join(10)
+        else:
+            eng.shutdown()
+    if dead.is_set():
+        raise SystemExit(3)
 
 
 def _serve_worker(ns, cfg: EngineConfig, connect) -> None:
@@ -523,6 +536,8 @@ def main(argv=None) -> None:
             if w.is_alive():
                 w.terminate()
         shutil.rmtree(tmp, ignore_errors=True)
+    if core.exitcode not in (0, None):
+        raise SystemExit(3)
 
 
 if __name__ == "__main__":

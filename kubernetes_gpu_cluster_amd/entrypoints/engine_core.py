@@ -145,8 +145,13 @@ def _core_main(cfg: EngineConfig, conn, listen: Optional[tuple] = None) -> None:
                 c.send(("dead", tb))
             except OSError:
                 pass
-    finally:
-        eng.shutdown()
+        # never recover in place (engine/health.py): give the shutdown a bounded chance
+        # (it may block on a collective with a dead rank), then exit non-zero
+        t = threading.Thread(target=eng.shutdown, daemon=True)
+        t.start()
+        t.join(10)
+        os._exit(1)
+    eng.shutdown()
 
 
 def start_core(cfg: EngineConfig, address: str, authkey: bytes, n_frontends: int):

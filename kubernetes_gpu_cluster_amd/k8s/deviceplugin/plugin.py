@@ -129,8 +129,13 @@ class AMDGPUPlugin:
                 paths = ["/dev/kfd"]
                 for g in gpus:
                     paths.append(f"/dev/dri/renderD{g['render_minor']}")
-                    if self.with_card and g["card"] >= 0:
-                        paths.append(f"/dev/dri/card{g['card']}")
+                    # the card node is optional for compute: only hand the kubelet device
+                    # specs whose host node exists (a missing one fails container creation;
+                    # seen on a real MI355X whose container exposes render nodes only)
+                    card = f"/dev/dri/card{g['card']}"
+                    if (self.with_card and g["card"] >= 0 and
+                            os.path.exists(os.path.join(self.root, card.lstrip("/")))):
+                        paths.append(card)
                 for p in paths:
                     cr.devices.add(container_path=p, host_path=p, permissions="rw")
             if self.strategy == "cdi":

@@ -25,6 +25,8 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
+from ..engine.health import AllReduceFailed
+
 log = logging.getLogger("kgc.allreduce")
 
 SUPPORTED_WORLD = (2, 4, 8)
@@ -51,6 +53,7 @@ class CustomAllReduce:
         self.one_shot_max = one_shot_max if one_shot_max is not None else (
             512 << 10 if world <= 2 else 256 << 10)
         self._own, self._opened = 0, []
+        self._err_host: Optional[torch.Tensor] = None
         handle, err = None, None
         try:
             from .. import ops
@@ -101,7 +104,21 @@ class CustomAllReduce:
         """Raise if any barrier timed out waiting for a peer (see allreduce.hip)."""
         err = int(torch.ops.kgc.ar_read_err(self.sig[self.rank]))
         if err:
-            raise RuntimeError(f"xGMI all-reduce: peers {bin(err)} never arrived")
+            raise AllReduceFailed(f"xGMI all-reduce: peers {bin(err)} never arrived")
+
+    def enqueue_err_read(self) -> None:
+        """Queue an async copy of the sticky error word behind the current step (no sync)."""
+        if self._err_host is None:
+            self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        torch.ops.kgc.ar_err_copy_async(self.sig[self.rank], self._err_host)
+
+    def raise_if_failed(self) -> None:
+        """After the step that queued ``enqueue_err_read`` completed: raise on a timed-out
+        barrier -- the step summed stale peer data, so its tokens must not be served."""
+        if self._err_host is not None and int(self._err_host[0]):
+            raise AllReduceFailed(
+                f"xGMI all-reduce: peers {bin(int(self._err_host[0]))} never arrived "
+                f"(a TP rank is dead or wedged); the engine stops")
 
     def close(self) -> None:
         if self._own or self._opened:

@@ -132,7 +132,12 @@ std::vector<DevNode> device_nodes(const std::vector<int>& gpus, const amdgpu_top
       d.minor = it->second.second;
     } else {
       struct stat st;
-      if (::stat((r + p).c_str(), &st) != 0) throw std::runtime_error("device node missing: " + r + p);
+      if (::stat((r + p).c_str(), &st) != 0) {
+        // the DRM card node is optional for compute (ROCm needs /dev/kfd + renderD): a
+        // host or container that exposes only render nodes must still get its GPUs
+        if (p.rfind("/dev/dri/card", 0) == 0) continue;
+        throw std::runtime_error("device node missing: " + r + p);
+      }
       if (!S_ISCHR(st.st_mode)) throw std::runtime_error("not a character device: " + r + p);
       d.major = major(st.st_rdev);
       d.minor = minor(st.st_rdev);

@@ -85,3 +85,41 @@ def _worker(rank, world, port, cap):
 def test_xgmi_allreduce_matches_sum(world, gpu):
     mp.start_processes(_worker, args=(world, _port(), 4 << 20), nprocs=world, join=True,
                        start_method="spawn")
+
+
+def _timeout_worker(rank, world, port):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from kubernetes_gpu_cluster_amd.engine.health import AllReduceFailed
+    from kubernetes_gpu_cluster_amd.parallel.custom_allreduce import CustomAllReduce
+    dev = torch.device("cuda", 0)
+    car = CustomAllReduce(dist.group.WORLD, rank, world, dev, cap_bytes=1 << 20)
+    try:
+        x = torch.ones(4096, dtype=torch.bfloat16, device=dev)
+        car.all_reduce(x)                       # both ranks: a healthy call
+        car.enqueue_err_read()
+        torch.cuda.synchronize()
+        car.raise_if_failed()
+        dist.barrier()
+        if rank == 0:
+            # rank 1 "dies": rank 0's barrier gives up after its bounded spin and the
+            # engine-side check raises instead of serving the stale sum
+            car.all_reduce(x)
+            car.enqueue_err_read()
+            torch.cuda.synchronize()
+            with pytest.raises(AllReduceFailed, match="never arrived"):
+                car.raise_if_failed()
+        dist.barrier()
+    finally:
+        car.close()
+        dist.destroy_process_group()
+
+
+def test_xgmi_allreduce_peer_timeout_raises(gpu):
+    """A missing TP peer: the barrier's bounded spin sets the sticky error word, the async
+    copy behind the step brings it to the host, and raise_if_failed (called when the
+    step's tokens are read, engine/worker.py) raises AllReduceFailed."""
+    mp.start_processes(_timeout_worker, args=(2, _port()), nprocs=2, join=True,
+                       start_method="spawn")
