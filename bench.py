@@ -1,19 +1,33 @@
 #!/usr/bin/env python3
-"""Headline benchmark: output tokens/s + p50 TTFT of the Llama-3-8B serving engine
-(BASELINE.json metric) on N MI355X GPUs of one node.
+"""Headline benchmark: output tokens/s + p50 TTFT of the Llama-3-8B *service*
+(BASELINE.json metric: "Llama-3-8B K8s service") on N MI355X GPUs of one node.
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 the
 driver launches one rank per GPU with torch.distributed.run.  One *step* is one
 serving wave: ``--num-prompts`` requests (synthetic random token prompts of
 ``--input-len`` tokens, ``--output-len`` generated tokens each, ignore_eos, temperature
-1.0 sampling) arrive at once and the continuous-batching engine runs until every
-request has finished -- the vLLM ``benchmark_serving`` request-rate=inf shape.
-TTFT is arrival -> first token of each request.
+1.0 sampling) arrive at once and are served until every request has finished -- the
+vLLM ``benchmark_serving`` request-rate=inf shape.
+
+``--mode service`` (default) measures what a client of ``svc/vllm-router-service``
+gets (/root/reference/old_README.md:1175,1473-1476): every replica-leading rank starts
+the OpenAI API server (engine core + API processes) and a router in front of it as
+fresh child processes (this process never touches the GPU, so nothing GPU-initialised
+is ever forked or exec'd), then streams the waves over HTTP/SSE through the router.
+TTFT is client send -> first SSE event.  The timed region is bracketed by a barrier
+over all ranks on both sides; it ends when the last stream of the last wave has been
+read, i.e. after the engine's final step has finished on the GPU and its tokens have
+reached the client (the service-level equivalent of synchronize()).  The engine-level
+figures of the same requests (arrival at the engine core -> first token / finish,
+from ``GET /kgc/engine_stats``) are reported next to them as ``engine_*`` keys.
+
+``--mode engine`` drives ``LLMEngine.step()`` in-process instead (no HTTP): the
+engine-only ceiling of the same waves.
 
 Parallelism: ``dpN`` (default) runs one engine replica per GPU, like the reference's
 ``replicaCount`` DP deployment behind the router (values-01-minimal-example2.yaml:10);
 per-GPU work is fixed, so scaling is weak.  ``--tp N`` runs one tensor-parallel
-engine over the N ranks (RCCL/xGMI all-reduce) instead.
+engine over N GPUs (RCCL/xGMI all-reduce) per replica instead.
 Weights are random-init bf16 of the real architecture (no checkpoints offline).
 """
 from __future__ import annotations
@@ -56,6 +70,12 @@ def parse():
                     help="automatic prefix caching (engine default: on; random prompts never hit)")
     ap.add_argument("--log-level", default="WARNING",
                     help="python logging level on stderr (INFO shows the GEMM tuner's choices)")
+    ap.add_argument("--mode", default="service", choices=["service", "engine"],
+                    help="service: HTTP/SSE through API server + router (headline); "
+                         "engine: LLMEngine.step() in-process")
+    ap.add_argument("--api-server-count", type=int, default=0,
+                    help="service mode: API processes per engine (0: server default)")
+    ap.add_argument("--startup-timeout", type=float, default=1800)
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: run the same harness on the fp32 CPU path (gloo) -- a test "
                          "harness for the multi-rank logic, not a measurement")
@@ -95,8 +115,7 @@ def run_wave(engine, args, wave: int, rank: int):
     return out_toks, t1 - t0, ttfts, tpots, steps
 
 
-def main():
-    args = parse()
+def main_engine(args):
     import logging
     logging.basicConfig(level=getattr(logging, args.log_level.upper(), logging.WARNING),
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
@@ -166,7 +185,7 @@ def main():
     if tp == 1:
         barrier()
     elapsed = time.monotonic() - t0
-    if is_driver and tp > 1:
+    if is_driver:
         engine.shutdown()
     # aggregate over replicas (drivers) -- every rank participates in the collectives
     if world > 1:
@@ -211,6 +230,193 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def _note(msg: str) -> None:
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _server_devices(local_rank: int, tp: int, cpu: bool):
+    """HIP_VISIBLE_DEVICES of one replica: GPUs local_rank .. local_rank+tp-1 of what
+    this process may see (None on the CPU path)."""
+    if cpu:
+        return None
+    vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")
+    ids = vis.split(",") if vis else [str(i) for i in range(local_rank + tp)]
+    return ",".join(ids[local_rank:local_rank + tp])
+
+
+def _engine_args(args, cpu: bool) -> list:
+    ea = ["--load-format", "dummy", "--dtype", args.dtype, "--seed", "0",
+          "--tensor-parallel-size", str(args.tp),
+          "--max-model-len", str(args.max_model_len), "--max-num-seqs", str(args.max_num_seqs),
+          "--max-num-batched-tokens", str(args.max_num_batched_tokens),
+          "--gpu-memory-utilization", str(args.gpu_memory_utilization),
+          "--disable-log-requests"]
+    if not args.prefix_caching:
+        ea.append("--no-enable-prefix-caching")
+    if args.enforce_eager:
+        ea.append("--enforce-eager")
+    if args.api_server_count:
+        ea += ["--api-server-count", str(args.api_server_count)]
+    if cpu:
+        ea += ["--device", "cpu"]
+    return ea
+
+
+def main_service(args):
+    """One replica per ``tp`` ranks: the leading rank launches API server + router and
+    drives its own client; every rank joins the barriers and the aggregation (gloo,
+    CPU only -- this process never initialises the GPU)."""
+    import asyncio
+    import urllib.request
+    from kubernetes_gpu_cluster_amd.benchmarks import serving_client as sc
+    from kubernetes_gpu_cluster_amd.models.configs import resolve_model
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = args.device == "cpu"
+    if cpu:
+        args.dtype = "float32"
+    tp = args.tp
+    assert world % tp == 0, f"WORLD_SIZE {world} is not a multiple of --tp {tp}"
+    replicas = world // tp
+    leader = rank % tp == 0
+    if world > 1:
+        import datetime
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=args.startup_timeout + 600))
+    vocab = resolve_model(args.model)[0].vocab_size
+    procs, logs = [], []
+    api_url = url = None
+    res_all, windows, eng = [], [], {}
+    elapsed = 0.0
+    try:
+        if leader:
+            api_port, router_port = _free_port(), _free_port()
+            api_url = f"http://127.0.0.1:{api_port}"
+            url = f"http://127.0.0.1:{router_port}"
+            procs.append(sc.start_api_server(args.model, api_port,
+                                             _server_devices(local_rank, tp, cpu),
+                                             _engine_args(args, cpu)))
+            procs.append(sc.start_router(router_port, [api_url]))
+            _note(f"rank {rank}: API server {api_url} (tp {tp}), router {url}; waiting for health")
+            asyncio.run(sc.wait_healthy([api_url, url], args.startup_timeout, procs, _note))
+            _note(f"rank {rank}: service is up")
+
+        async def waves(n: int, base_seed: int, timed: bool):
+            out = []
+            async with sc.new_session() as s:      # one client; connections are reused
+                for w in range(n):
+                    prompts = sc.random_prompts(args.num_prompts, args.input_len, vocab,
+                                                seed=base_seed + 1000 * w + rank)
+                    r, lo, hi = await sc.run_wave(s, url, args.model, prompts, args.output_len,
+                                                  temperature=args.temperature)
+                    out.append((r, lo, hi))
+            return out
+
+        if leader and args.warmup:
+            for r, _, _ in asyncio.run(waves(args.warmup, 7_000_000, False)):
+                bad = [x for x in r if not x.ok]
+                if bad:
+                    raise RuntimeError(f"warmup: {len(bad)} requests failed (status {bad[0].status})")
+        if world > 1:
+            dist.barrier()
+        t0 = time.monotonic()
+        if leader:
+            for r, lo, hi in asyncio.run(waves(args.steps, 0, True)):
+                res_all += r
+                windows.append((lo, hi))
+        if world > 1:
+            dist.barrier()
+        elapsed = time.monotonic() - t0
+        if leader:
+            with urllib.request.urlopen(f"{api_url}/kgc/engine_stats?since={t0 - 1.0}", timeout=30) as f:
+                st = json.loads(f.read())
+            eng = sc.engine_figures(st["requests"], windows)
+            eng["steps"] = st["steps"]
+    finally:
+        codes = sc.stop(procs)
+        if leader and procs:
+            _note(f"rank {rank}: service stopped (exit codes {codes})")
+    ok = [r for r in res_all if r.ok]
+    mine = {"toks": sum(r.tokens for r in ok), "failed": len(res_all) - len(ok),
+            "ttft": [r.ttft for r in ok], "tpot": [(r.e2e - r.ttft) / max(1, r.tokens - 1) for r in ok],
+            "itl": [x for r in ok for x in r.itl], "elapsed": elapsed if leader else 0.0,
+            "eng": eng}
+    parts = [mine]
+    if world > 1:
+        parts = [None] * world
+        dist.all_gather_object(parts, mine)
+    if rank == 0:
+        elapsed = max(p["elapsed"] for p in parts)
+        toks = sum(p["toks"] for p in parts)
+        failed = sum(p["failed"] for p in parts)
+        ttft = [x for p in parts for x in p["ttft"]]
+        tpot = [x for p in parts for x in p["tpot"]]
+        itl = [x for p in parts for x in p["itl"]]
+        engs = [p["eng"] for p in parts if p["eng"]]
+        e_tok = sum(e["engine_tokens"] for e in engs)
+        e_span = max((e["engine_span_s"] for e in engs), default=0.0)
+        e_ttft = [x for e in engs for x in e["engine_ttft"]]
+        e_tpot = [x for e in engs for x in e["engine_tpot"]]
+        value = toks / elapsed if elapsed > 0 else 0.0
+        e_value = e_tok / e_span if e_span > 0 else None
+        med = lambda xs: round(statistics.median(xs) * 1e3, 3) if xs else None  # noqa: E731
+        out = {
+            "metric": BASELINE_METRIC, "value": round(value, 2), "unit": "output_tokens/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": {"bfloat16": "bf16", "float16": "fp16", "float32": "fp32"}.get(args.dtype, args.dtype),
+            "data": "synthetic random-token prompts, random-init weights",
+            "mode": "service (client -> router -> OpenAI API server -> engine core, HTTP/SSE)",
+            "p50_ttft_ms": med(ttft),
+            "p99_ttft_ms": round(sorted(ttft)[int(0.99 * (len(ttft) - 1))] * 1e3, 2) if ttft else None,
+            "p50_tpot_ms": med(tpot), "p50_itl_ms": med(itl),
+            "completed": len(ttft), "failed": failed,
+            "engine_tok_s": round(e_value, 2) if e_value else None,
+            "engine_p50_ttft_ms": med(e_ttft), "engine_p50_tpot_ms": med(e_tpot),
+            "engine_output_tokens": e_tok,
+            "engine_steps": sum(e.get("steps", 0) for e in engs),
+            "service_vs_engine": round(value / e_value, 4) if e_value else None,
+            "config": {"model": args.model, "global_batch": args.num_prompts * replicas,
+                       "seq_len": args.input_len + args.output_len, "input_len": args.input_len,
+                       "output_len": args.output_len,
+                       "parallelism": f"dp{replicas}" if tp == 1 else f"tp{tp}" + (f"xdp{replicas}" if replicas > 1 else ""),
+                       "max_num_seqs": args.max_num_seqs,
+                       "max_num_batched_tokens": args.max_num_batched_tokens,
+                       "cuda_graphs": not args.enforce_eager,
+                       "endpoint": "router -> /v1/completions (stream)"},
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if failed_any(parts if rank == 0 else [mine]):
+        sys.exit(1)
+
+
+def failed_any(parts) -> bool:
+    return any(p["failed"] for p in parts)
+
+
+def main():
+    args = parse()
+    if args.mode == "engine":
+        main_engine(args)
+    else:
+        main_service(args)
 
 
 if __name__ == "__main__":

@@ -7,8 +7,11 @@ once (``--request-rate inf``) or as a Poisson process.
 
 Against a running service:
     python bench/serve_bench.py --base-url http://vllm-router-service:80
-Self-contained on one node (one engine per GPU + the router, like the dpN deployment):
+Self-contained on one node (one engine per GPU + one router over all of them, like
+the dpN deployment):
     python bench/serve_bench.py --launch --gpus 1 --model llama-3-8b
+(``bench.py`` is the driver's headline harness: one router per replica, timed waves
+between barriers, engine-side figures alongside.)
 """
 from __future__ import annotations
 
@@ -16,111 +19,41 @@ import argparse
 import asyncio
 import json
 import os
-import random
-import signal
-import statistics
-import subprocess
 import sys
-import time
-
-import aiohttp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from kubernetes_gpu_cluster_amd.benchmarks import serving_client as sc  # noqa: E402
 
 
-def pct(xs, q):
-    xs = sorted(xs)
-    return xs[min(len(xs) - 1, int(q * len(xs)))] if xs else float("nan")
+async def run_client(a, prompts_seed: int) -> dict:
+    prompts = sc.random_prompts(a.num_prompts, a.input_len, a.vocab, prompts_seed)
+    async with sc.new_session() as s:
+        res, t0, t1 = await sc.run_wave(s, a.base_url, a.model, prompts, a.output_len,
+                                        a.request_rate, seed=a.seed)
+    out = {"metric": "service output tokens/sec + p50 TTFT", "unit": "output_tokens/s"}
+    out.update(sc.summarize(res, t1 - t0))
+    out["config"] = {"model": a.model, "num_prompts": a.num_prompts, "input_len": a.input_len,
+                     "output_len": a.output_len, "request_rate": a.request_rate}
+    return out
 
 
-async def one_request(session, url, model, prompt, out_len, res):
-    body = {"model": model, "prompt": prompt, "max_tokens": out_len, "ignore_eos": True,
-            "stream": True, "temperature": 1.0}
-    t0 = time.perf_counter()
-    ttft, last, chunks, itl = None, t0, 0, []
-    async with session.post(url + "/v1/completions", json=body) as r:
-        if r.status != 200:
-            res.append({"ok": False, "status": r.status})
-            return
-        async for raw in r.content:
-            line = raw.decode().strip()
-            if not line.startswith("data:") or line == "data: [DONE]":
-                continue
-            now = time.perf_counter()
-            if ttft is None:
-                ttft = now - t0
-            else:
-                itl.append(now - last)
-            last = now
-            chunks += 1
-    res.append({"ok": True, "ttft": ttft, "e2e": last - t0, "tokens": out_len, "itl": itl})
-
-
-async def run_client(a) -> dict:
-    rng = random.Random(a.seed)
-    prompts = [[rng.randrange(100, a.vocab) for _ in range(a.input_len)]
-               for _ in range(a.num_prompts)]
-    res: list = []
-    conn = aiohttp.TCPConnector(limit=0)
-    timeout = aiohttp.ClientTimeout(total=None, sock_read=600)
-    async with aiohttp.ClientSession(connector=conn, timeout=timeout) as s:
-        tasks = []
-        t0 = time.perf_counter()
-        for p in prompts:
-            tasks.append(asyncio.create_task(one_request(s, a.base_url, a.model, p, a.output_len, res)))
-            if a.request_rate != float("inf"):
-                await asyncio.sleep(rng.expovariate(a.request_rate))
-        await asyncio.gather(*tasks)
-        dur = time.perf_counter() - t0
-    ok = [r for r in res if r["ok"]]
-    toks = sum(r["tokens"] for r in ok)
-    tpot = [(r["e2e"] - r["ttft"]) / max(1, r["tokens"] - 1) for r in ok]
-    return {"metric": "service output tokens/sec + p50 TTFT", "value": round(toks / dur, 2),
-            "unit": "output_tokens/s", "completed": len(ok), "failed": len(res) - len(ok),
-            "duration_s": round(dur, 3), "p50_ttft_ms": round(1e3 * pct([r["ttft"] for r in ok], 0.5), 2),
-            "p99_ttft_ms": round(1e3 * pct([r["ttft"] for r in ok], 0.99), 2),
-            "p50_tpot_ms": round(1e3 * pct(tpot, 0.5), 3),
-            "p50_itl_ms": round(1e3 * statistics.median([x for r in ok for x in r["itl"]] or [0]), 3),
-            "config": {"model": a.model, "num_prompts": a.num_prompts, "input_len": a.input_len,
-                       "output_len": a.output_len, "request_rate": a.request_rate}}
-
-
-async def wait_healthy(urls, timeout_s):
-    deadline = time.time() + timeout_s
-    async with aiohttp.ClientSession() as s:
-        for u in urls:
-            while True:
-                try:
-                    async with s.get(u + "/health") as r:
-                        if r.status == 200:
-                            break
-                except aiohttp.ClientError:
-                    pass
-                if time.time() > deadline:
-                    raise TimeoutError(f"{u} not healthy after {timeout_s}s")
-                await asyncio.sleep(2)
-
-
-def launch(a) -> list[subprocess.Popen]:
+def launch(a) -> list:
     procs, backends = [], []
-    env0 = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
     for g in range(a.gpus):
         port = a.engine_port + g
-        env = dict(env0, HIP_VISIBLE_DEVICES=str(g))
-        cmd = [sys.executable, "-m", "kubernetes_gpu_cluster_amd.entrypoints.api_server", a.model,
-               "--port", str(port), "--host", "127.0.0.1", "--load-format", "dummy",
-               "--max-num-seqs", str(a.max_num_seqs), "--max-model-len", str(a.max_model_len),
-               "--uvicorn-log-level", "warning"] + a.engine_args
-        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
+        procs.append(sc.start_api_server(
+            a.model, port, str(g), ["--load-format", "dummy", "--max-num-seqs", str(a.max_num_seqs),
+                                    "--max-model-len", str(a.max_model_len)] + a.engine_args))
         backends.append(f"http://127.0.0.1:{port}")
     if a.no_router:
-        asyncio.run(wait_healthy(backends, a.startup_timeout))
+        asyncio.run(sc.wait_healthy(backends, a.startup_timeout, procs))
         a.base_url = backends[0]
         return procs
-    cmd = [sys.executable, "-m", "kubernetes_gpu_cluster_amd.router.router", "--host", "127.0.0.1",
-           "--port", str(a.router_port), "--backends", ",".join(backends)]
-    procs.append(subprocess.Popen(cmd, env=env0, start_new_session=True))
-    asyncio.run(wait_healthy(backends + [f"http://127.0.0.1:{a.router_port}"], a.startup_timeout))
+    procs.append(sc.start_router(a.router_port, backends))
+    asyncio.run(sc.wait_healthy(backends + [f"http://127.0.0.1:{a.router_port}"],
+                                a.startup_timeout, procs))
     a.base_url = f"http://127.0.0.1:{a.router_port}"
     return procs
 
@@ -153,8 +86,8 @@ def main():
         if a.warmup_prompts:
             w = argparse.Namespace(**vars(a))
             w.num_prompts, w.output_len = a.warmup_prompts, 16
-            asyncio.run(run_client(w))
-        out = asyncio.run(run_client(a))
+            asyncio.run(run_client(w, a.seed + 1))
+        out = asyncio.run(run_client(a, a.seed))
         out["n_engines"] = a.gpus if a.launch else None
         line = json.dumps(out)
         print(line, flush=True)
@@ -162,16 +95,7 @@ def main():
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
     finally:
-        for p in procs:
-            try:
-                os.killpg(p.pid, signal.SIGTERM)
-            except ProcessLookupError:
-                pass
-        for p in procs:
-            try:
-                p.wait(timeout=30)
-            except subprocess.TimeoutExpired:
-                os.killpg(p.pid, signal.SIGKILL)
+        sc.stop(procs, grace=30)
 
 
 if __name__ == "__main__":

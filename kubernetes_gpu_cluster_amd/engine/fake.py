@@ -52,6 +52,7 @@ class FakeOutput:
     finish_time: Optional[float]
     num_preemptions: int = 0
     logprobs: Optional[list] = None
+    num_output_tokens: int = 0
 
 
 def timing_from_env(spec: str) -> tuple[float, float, float]:
@@ -119,7 +120,8 @@ class FakeEngine:
                 r.first_token_time = now
             done = len(r.out) >= r.max_tokens
             outs.append(FakeOutput(r.rid, [tok], done, "length" if done else None, r.arrival,
-                                   r.first_token_time, now if done else None))
+                                   r.first_token_time, now if done else None,
+                                   num_output_tokens=len(r.out)))
             if done:
                 self.running.remove(r)
         return outs

@@ -273,6 +273,9 @@ class LLMEngine:
         return None
 
     def shutdown(self) -> None:
+        path = self.metrics.dump_trace()      # KGC_TRACE=path: per-step spans (Chrome trace)
+        if path:
+            log.info("engine step trace: %s", path)
         self.executor.shutdown()
 
 

@@ -331,6 +331,11 @@ def _spawn_entry(rank: int, cfg: EngineConfig, env: dict, local: Optional[int] =
     os.environ["RANK"] = str(rank)
     os.environ["LOCAL_RANK"] = str(local)
     watch_parent()            # never outlive the driver (engine/health.py)
+    # a SIGTERM / Ctrl-C to the process group is the API server's to handle; the driver
+    # then shuts the ranks down in order (a rank that died first would read as a fault)
+    import signal
+    signal.signal(signal.SIGTERM, signal.SIG_IGN)
+    signal.signal(signal.SIGINT, signal.SIG_IGN)
     try:
         w = Worker(cfg, rank=rank, local_device=local)
         worker_loop(w)

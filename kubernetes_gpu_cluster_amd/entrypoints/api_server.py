@@ -190,12 +190,14 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
         subs = [dataclasses.replace(sp, n=1, seed=None if sp.seed is None else sp.seed + i)
                 for i in range(n)]
         rids = [rid if n == 1 else f"{rid}-{i}" for i in range(n)]
+        # submit every choice before the response starts (EngineDeadError -> 503 here)
+        gens = [engine.generate(ids, subs[i], rids[i]) for i in range(n)]
         if stream and n == 1:
             # one coroutine per stream: engine output -> detok -> SSE bytes, no task or
             # queue hop (the per-token path dominates the API process at 256 streams)
             async def sse1():
                 detok = _Detok(tokenizer, sp.stop)
-                gen = engine.generate(ids, subs[0], rid)
+                gen = gens[0]
                 try:
                     async for out in gen:
                         delta = detok.update(out.output_token_ids)
@@ -219,7 +221,7 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
 
             async def pump(i):
                 detok = _Detok(tokenizer, subs[i].stop)
-                gen = engine.generate(ids, subs[i], rids[i])
+                gen = gens[i]
                 try:
                     async for out in gen:
                         delta = detok.update(out.output_token_ids)
@@ -259,7 +261,7 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
 
         async def one(i):
             detok = _Detok(tokenizer, subs[i].stop)
-            gen = engine.generate(ids, subs[i], rids[i])
+            gen = gens[i]
             last, lps = None, []
             async for out in gen:
                 last = out
@@ -418,6 +420,12 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
         if not engine.is_alive:
             return PlainTextResponse("engine dead", status_code=503)
         return PlainTextResponse("ok")
+
+    @app.get("/kgc/engine_stats")
+    async def engine_stats(since: float = 0.0):
+        """Engine-side timings of requests that arrived at or after ``since`` (host
+        ``time.monotonic()``) and have finished: (arrival, first token, finish, tokens)."""
+        return JSONResponse(await engine.engine_stats(since))
 
     @app.get("/metrics")
     async def metrics():

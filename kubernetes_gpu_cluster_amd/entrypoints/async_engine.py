@@ -8,6 +8,7 @@ engine release the GIL, so the HTTP event loop keeps serving while a step runs.
 from __future__ import annotations
 
 import asyncio
+import collections
 import logging
 import queue
 import threading
@@ -33,6 +34,30 @@ def _merge(prev, nxt) -> None:
         nxt.logprobs = (prev.logprobs or []) + (nxt.logprobs or [])
 
 
+class DoneLog:
+    """Engine-side timing of finished requests -- (arrival, first token, finish, output
+    tokens), all ``time.monotonic()`` of the serving host -- for ``GET
+    /kgc/engine_stats``: the engine-level counterpart of what an HTTP client measures
+    (bench.py reports both)."""
+
+    def __init__(self, maxlen: int = 1 << 17):
+        self.log: collections.deque = collections.deque(maxlen=maxlen)
+        self.steps = 0
+        self.step_s = 0.0
+
+    def on_step(self, outs, dt: float) -> None:
+        self.steps += 1
+        self.step_s += dt
+        for o in outs:
+            if o.finished:
+                self.log.append((o.arrival_time, o.first_token_time, o.finish_time,
+                                 o.num_output_tokens))
+
+    def snapshot(self, since: float = 0.0) -> dict:
+        return {"now": time.monotonic(), "steps": self.steps, "step_busy_s": self.step_s,
+                "requests": [r for r in list(self.log) if r[0] >= since]}
+
+
 def _deliver(items) -> None:
     for q, o in items:
         q.put_nowait(o)
@@ -49,6 +74,7 @@ class AsyncLLMEngine:
         self._stop = False
         self.error: Optional[BaseException] = None
         self.last_step_time = time.monotonic()
+        self.done_log = DoneLog()
         self._thread = threading.Thread(target=self._loop, name="kgc-engine", daemon=True)
         self._thread.start()
 
@@ -64,7 +90,8 @@ class AsyncLLMEngine:
         wake-up per request: at batch 256 that is 256 self-pipe writes per step)."""
         by_loop: dict = {}
         for o in outs:
-            ent = self._streams.get(o.request_id)
+            ent = (self._streams.pop(o.request_id, None) if o.finished
+                   else self._streams.get(o.request_id))
             if ent is not None:
                 by_loop.setdefault(ent[0], []).append((ent[1], o))
         for loop, items in by_loop.items():
@@ -90,8 +117,11 @@ class AsyncLLMEngine:
                         break
                     eng.abort(rid)
                 if eng.has_unfinished():
-                    self._push_step(eng.step())
+                    t0 = time.monotonic()
+                    outs = eng.step()
+                    self._push_step(outs)
                     self.last_step_time = time.monotonic()
+                    self.done_log.on_step(outs, self.last_step_time - t0)
                 else:
                     self._wake.wait(0.05)
                     self._wake.clear()
@@ -106,8 +136,9 @@ class AsyncLLMEngine:
     def is_alive(self) -> bool:
         return self._thread.is_alive() and self.error is None
 
-    async def generate(self, prompt_ids: list[int], params: SamplingParams,
-                       request_id: str) -> AsyncIterator[RequestOutput]:
+    def generate(self, prompt_ids: list[int], params: SamplingParams,
+                 request_id: str) -> AsyncIterator[RequestOutput]:
+        """Submit now (from the request handler) and return the output stream."""
         if not self.is_alive:
             raise EngineDeadError(str(self.error))
         loop = asyncio.get_running_loop()
@@ -115,6 +146,9 @@ class AsyncLLMEngine:
         self._streams[request_id] = (loop, q)
         self._new.put((request_id, prompt_ids, params, time.monotonic()))
         self._wake.set()
+        return self._stream(request_id, q)
+
+    async def _stream(self, request_id: str, q: asyncio.Queue) -> AsyncIterator[RequestOutput]:
         finished = False
         try:
             while True:
@@ -145,6 +179,9 @@ class AsyncLLMEngine:
     async def metrics_text(self) -> str:
         from prometheus_client import generate_latest
         return generate_latest(self.engine.metrics.registry).decode()
+
+    async def engine_stats(self, since: float = 0.0) -> dict:
+        return self.done_log.snapshot(since)
 
     def shutdown(self) -> None:
         self._stop = True

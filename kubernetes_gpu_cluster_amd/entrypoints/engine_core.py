@@ -26,6 +26,7 @@ accepts either.  ``--engine-in-process`` selects the thread-backed engine instea
 from __future__ import annotations
 
 import asyncio
+import collections
 import itertools
 import logging
 import multiprocessing as mp
@@ -38,7 +39,7 @@ from typing import AsyncIterator, Optional
 
 from ..engine.config import EngineConfig
 from ..engine.sequence import RequestOutput, SamplingParams
-from .async_engine import EngineDeadError, _deliver, _merge
+from .async_engine import DoneLog, EngineDeadError, _deliver, _merge
 
 log = logging.getLogger("kgc.engine_core")
 
@@ -59,6 +60,12 @@ def _core_main(cfg: EngineConfig, conn, listen: Optional[tuple] = None) -> None:
     n)``, accept ``n`` frontend connections (``--api-server-count``) and route every
     request's outputs back to the frontend that submitted it."""
     logging.basicConfig(level=logging.INFO)
+    # the API process owns termination: a SIGTERM / Ctrl-C to the process group (pod stop)
+    # reaches it, it stops serving and tells the core to shut down; the core also ends
+    # when every frontend connection is gone (EOF), so it never outlives the server
+    import signal
+    signal.signal(signal.SIGTERM, signal.SIG_IGN)
+    signal.signal(signal.SIGINT, signal.SIG_IGN)
     conns = [conn] if conn is not None else []
     listener = None
     if listen is not None:
@@ -86,10 +93,19 @@ def _core_main(cfg: EngineConfig, conn, listen: Optional[tuple] = None) -> None:
     else:
         conn.send(ready_msg)
     owner: dict = {}          # request id -> connection of the frontend that submitted it
+    # host-time accounting of the core loop, logged at exit: where a step's host time goes
+    # besides the engine step itself (inbox handling, output fan-out to the frontends)
+    st = {"iters": 0, "steps": 0, "step_s": 0.0, "send_s": 0.0, "inbox_s": 0.0}
+    # (core receive time, frontend stamp) of the latest requests (bounded: a server runs
+    # for weeks)
+    adds: collections.deque = collections.deque(maxlen=1 << 16)
+    done = DoneLog()
     try:
         running = True
         while running and conns:
             idle = not eng.has_unfinished()
+            st["iters"] += 1
+            ti = time.perf_counter()
             # drain every inbox; block briefly only when there is nothing to run
             ready = mp_wait(conns, 0.05 if idle else 0)
             while ready and running:
@@ -105,6 +121,7 @@ def _core_main(cfg: EngineConfig, conn, listen: Optional[tuple] = None) -> None:
                     kind = msg[0]
                     if kind == "add":
                         _, rid, ids, params, arrival = msg
+                        adds.append((time.monotonic(), arrival))
                         try:
                             eng.add_request(ids, params, request_id=rid, arrival_time=arrival)
                             owner[rid] = c
@@ -116,13 +133,23 @@ def _core_main(cfg: EngineConfig, conn, listen: Optional[tuple] = None) -> None:
                     elif kind == "metrics":
                         from prometheus_client import generate_latest
                         c.send(("metrics", msg[1], generate_latest(eng.metrics.registry).decode()))
+                    elif kind == "stats":
+                        c.send(("stats", msg[1], done.snapshot(msg[2])))
                     elif kind == "shutdown":
                         running = False
                         break
                 ready = mp_wait(conns, 0) if running and conns else []
+            if not idle:
+                st["inbox_s"] += time.perf_counter() - ti
             if running and eng.has_unfinished():
                 by_conn: dict = {}
-                for o in eng.step():
+                t1 = time.perf_counter()
+                outs = eng.step()
+                t2 = time.perf_counter()
+                st["steps"] += 1
+                st["step_s"] += t2 - t1
+                done.on_step(outs, t2 - t1)
+                for o in outs:
                     c = owner.get(o.request_id)
                     if c is None:
                         continue
@@ -137,6 +164,7 @@ def _core_main(cfg: EngineConfig, conn, listen: Optional[tuple] = None) -> None:
                         c.send(("out", items))
                     except OSError:
                         pass
+                st["send_s"] += time.perf_counter() - t2
     except BaseException:  # noqa: BLE001
         tb = traceback.format_exc()
         log.error("engine core died: %s", tb)
@@ -151,6 +179,14 @@ def _core_main(cfg: EngineConfig, conn, listen: Optional[tuple] = None) -> None:
         t.start()
         t.join(10)
         os._exit(1)
+    log.info("core loop: %d iterations, %d engine steps; host time: step %.2f s, output "
+             "fan-out %.2f s, inbox %.2f s", st["iters"], st["steps"], st["step_s"],
+             st["send_s"], st["inbox_s"])
+    if adds:
+        lat = sorted(r - a for r, a in adds)
+        log.info("core intake (last %d requests): %.3f s first -> last receive; frontend -> core "
+                 "latency p50 %.2f ms, max %.2f ms", len(adds), adds[-1][0] - adds[0][0],
+                 1e3 * lat[len(lat) // 2], 1e3 * lat[-1])
     eng.shutdown()
 
 
@@ -234,7 +270,7 @@ class EngineCoreClient:
                 if kind == "out":
                     by_loop: dict = {}
                     for rid, new, fin, reason, arr, ftt, ft, npre, lps in msg[1]:
-                        st = self._streams.get(rid)
+                        st = self._streams.get(rid) if not fin else self._streams.pop(rid, None)
                         if st is None:
                             continue
                         st.ids.extend(new)
@@ -247,7 +283,7 @@ class EngineCoreClient:
                     st = self._streams.get(msg[1])
                     if st is not None:
                         st.loop.call_soon_threadsafe(st.q.put_nowait, ValueError(msg[2]))
-                elif kind == "metrics":
+                elif kind in ("metrics", "stats"):
                     w = self._metrics_waiters.pop(msg[1], None)
                     if w is not None:
                         loop, fut = w
@@ -266,14 +302,20 @@ class EngineCoreClient:
     def is_alive(self) -> bool:
         return self.error is None and (self._proc is None or self._proc.is_alive())
 
-    async def generate(self, prompt_ids: list[int], params: SamplingParams,
-                       request_id: str) -> AsyncIterator[RequestOutput]:
+    def generate(self, prompt_ids: list[int], params: SamplingParams,
+                 request_id: str) -> AsyncIterator[RequestOutput]:
+        """Submit NOW (from the request handler, before the response starts streaming: a
+        burst of arrivals reaches the core while the frontend is still parsing the rest)
+        and return the request's output stream."""
         if not self.is_alive:
             raise EngineDeadError(str(self.error))
         loop = asyncio.get_running_loop()
         q: asyncio.Queue = asyncio.Queue()
         self._streams[request_id] = _Stream(loop, q, list(prompt_ids))
         self._send(("add", request_id, list(prompt_ids), params, time.monotonic()))
+        return self._stream(request_id, q)
+
+    async def _stream(self, request_id: str, q: asyncio.Queue) -> AsyncIterator[RequestOutput]:
         finished = False
         try:
             while True:
@@ -306,6 +348,14 @@ class EngineCoreClient:
         tok = next(self._tokens)
         self._metrics_waiters[tok] = (loop, fut)
         self._send(("metrics", tok))
+        return await asyncio.wait_for(fut, 10)
+
+    async def engine_stats(self, since: float = 0.0) -> dict:
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        tok = next(self._tokens)
+        self._metrics_waiters[tok] = (loop, fut)
+        self._send(("stats", tok, since))
         return await asyncio.wait_for(fut, 10)
 
     def shutdown(self) -> None:

@@ -1,5 +1,6 @@
 """bench.py's driver contract on the CPU path: one JSON line from rank 0, whole-job
-aggregates, 1 rank and 2 ranks (torch.distributed.run, gloo) for dp and tp."""
+aggregates, 1 rank and 2 ranks (torch.distributed.run, gloo) for dp and tp; the default
+service mode launches API server + router per replica and streams over HTTP."""
 import json
 import os
 import socket
@@ -35,6 +36,18 @@ def test_bench_single_rank():
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in j
     assert j["n_gpus"] == 1 and j["value"] > 0 and j["config"]["parallelism"] == "dp1"
+    # service mode (default): HTTP/SSE numbers plus the engine-side view of the same requests
+    assert j["mode"].startswith("service") and j["failed"] == 0 and j["completed"] == 4
+    assert j["engine_output_tokens"] == 4 * 4 and j["engine_tok_s"] > 0
+    assert j["p50_ttft_ms"] >= j["engine_p50_ttft_ms"] > 0
+
+
+def test_bench_engine_mode():
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--mode", "engine"] + SMALL,
+                       cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    j = _json_lines(r.stdout)[0]
+    assert j["value"] > 0 and j["engine_steps"] > 0 and "mode" not in j
 
 
 @pytest.mark.parametrize("tp", [1, 2])

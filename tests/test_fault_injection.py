@@ -92,7 +92,11 @@ def test_tp_rank_death_exits_api_server(tmp_path):
         rc = p.wait(timeout=30)
         assert rc != 0, f"server exited 0 after a rank died\n{(tmp_path / 'server.log').read_text()}"
         assert time.time() - killed < 30
-        assert "exited with code" in (tmp_path / "server.log").read_text()
+        # either the rank watchdog saw the exit code first, or the collective with the
+        # dead peer failed first and the core died on that step -- both end the server
+        text = (tmp_path / "server.log").read_text()
+        assert ("exited with code" in text or "engine core died" in text
+                or "engine is dead" in text), text[-3000:]
     finally:
         if p.poll() is None:
             p.kill()
