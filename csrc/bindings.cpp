@@ -241,6 +241,34 @@ void sample(Tensor out, Tensor logits, Tensor temperature, Tensor top_k, Tensor 
                      stream());
 }
 
+void sample_vp(Tensor packed, Tensor logits, int64_t V, Tensor temperature, Tensor seeds,
+               int64_t vocab_off) {
+  check_gpu(logits, "logits");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits [B, Vshard] with dense rows");
+  const int64_t B = logits.size(0);
+  TORCH_CHECK(V >= 1 && V <= logits.size(1), "V (valid shard columns) out of range");
+  TORCH_CHECK(packed.scalar_type() == at::kLong && packed.numel() >= B, "packed int64 [B]");
+  TORCH_CHECK(temperature.scalar_type() == at::kFloat && temperature.numel() >= B, "temperature fp32");
+  TORCH_CHECK(seeds.scalar_type() == at::kLong && seeds.numel() >= B, "seeds int64");
+  TORCH_CHECK(B <= 65535 * 256 && vocab_off >= 0 && vocab_off + V < INT32_MAX, "kgc.sample_vp: shape");
+  if (B == 0) return;
+  Tensor partial = at::empty({B * kgc::sample_splits((int)B)}, logits.options().dtype(at::kLong));
+  kgc::launch_sample_vp(dt_code(logits), packed.data_ptr<int64_t>(),
+                        reinterpret_cast<uint64_t*>(partial.data_ptr<int64_t>()), logits.data_ptr(),
+                        logits.stride(0), (int)B, (int)V, temperature.data_ptr<float>(),
+                        seeds.data_ptr<int64_t>(), (int)vocab_off, stream());
+}
+
+void sample_vp_unpack(Tensor out, Tensor packed) {
+  check_gpu(packed, "packed");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(packed.device());
+  TORCH_CHECK(packed.scalar_type() == at::kLong && out.scalar_type() == at::kLong &&
+              out.numel() >= packed.numel() && packed.is_contiguous(), "int64 [B]");
+  kgc::launch_sample_vp_unpack(out.data_ptr<int64_t>(), packed.data_ptr<int64_t>(),
+                               (int)packed.numel(), stream());
+}
+
 // ---- K13/K14 MoE
 void moe_route(Tensor topk_w, Tensor topk_ids, Tensor logits, bool renorm) {
   check_gpu(logits, "logits");
@@ -607,6 +635,9 @@ TORCH_LIBRARY(kgc, m) {
         "Tensor work_mblk, float scale, float k_scale=1.0, float v_scale=1.0) -> ()");
   m.def("sample(Tensor(a!) out, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, "
         "Tensor seeds) -> ()");
+  m.def("sample_vp(Tensor(a!) packed, Tensor logits, int V, Tensor temperature, Tensor seeds, "
+        "int vocab_off) -> ()");
+  m.def("sample_vp_unpack(Tensor(a!) out, Tensor packed) -> ()");
   m.def("decode_partition_size() -> int", &decode_partition_size);
   m.def("moe_route(Tensor(a!) topk_w, Tensor(b!) topk_ids, Tensor logits, bool renorm) -> ()");
   m.def("moe_align(Tensor(a!) sorted_ids, Tensor(b!) block_expert, Tensor(c!) meta, "
@@ -646,6 +677,8 @@ TORCH_LIBRARY_IMPL(kgc, CUDA, m) {
   m.impl("paged_decode", &paged_decode);
   m.impl("prefill_attention", &prefill_attention);
   m.impl("sample", &sample);
+  m.impl("sample_vp", &sample_vp);
+  m.impl("sample_vp_unpack", &sample_vp_unpack);
   m.impl("xgmi_allreduce", &xgmi_allreduce);
   m.impl("moe_route", &moe_route);
   m.impl("moe_align", &moe_align);

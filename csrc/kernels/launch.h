@@ -38,6 +38,12 @@ int sample_splits(int B);   // vocabulary splits per row; partial holds B * spli
 void launch_sample(int dtype, int64_t* out, uint64_t* partial, const void* logits,
                    int64_t row_stride, int B, int V, const float* temperature, const int* top_k,
                    const float* top_p, const int64_t* seeds, hipStream_t s);
+// vocab-parallel: per-row packed (value, global index) of this rank's shard (biased for
+// a signed MAX all-reduce), and the unpack after that all-reduce
+void launch_sample_vp(int dtype, int64_t* packed, uint64_t* partial, const void* logits,
+                      int64_t row_stride, int B, int V, const float* temperature,
+                      const int64_t* seeds, int vocab_off, hipStream_t s);
+void launch_sample_vp_unpack(int64_t* out, const int64_t* packed, int B, hipStream_t s);
 
 // K9 skinny (small-M decode) GEMM: C[M, N] = X[M, K] . W[N, K]^T (+ bias), M <= 16*mt.
 // epi: 0 plain, 1 RMS-normalise X rows on the fly (gamma [K], eps), 2 accumulate into C

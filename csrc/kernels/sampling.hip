@@ -7,6 +7,12 @@
 //                                 support) -> Gumbel-max over the kept support.
 // The Gumbel noise is a counter-based hash of (seed, column), bit-identical to
 // ops/reference.uniform_noise, so sampled ids are reproducible per request seed.
+//
+// Vocab-parallel mode (TP > 1, rows without top-k / top-p): each rank runs the
+// (Gumbel-)argmax over its own vocabulary shard with the noise of the GLOBAL column
+// (vocab_off + i), and emits one packed (value, index) int64 per row; a MAX all-reduce
+// of those 8 bytes per row over the TP group picks the token the unsharded sampler
+// would have picked -- instead of all-gathering B x V logits to every rank.
 #include "common.h"
 #include "launch.h"
 #include <algorithm>
@@ -94,7 +100,7 @@ template <typename T>
 __global__ __launch_bounds__(SMP_NT) void sample_kernel(
     uint64_t* __restrict__ partial, const T* __restrict__ logits, int64_t row_stride, int V,
     const float* __restrict__ temperature, const int* __restrict__ top_k,
-    const float* __restrict__ top_p, const int64_t* __restrict__ seeds) {
+    const float* __restrict__ top_p, const int64_t* __restrict__ seeds, int vocab_off) {
   __shared__ float red_v[SMP_NT / 64];
   __shared__ int red_i[SMP_NT / 64];
   __shared__ float hist_f[256];
@@ -106,8 +112,8 @@ __global__ __launch_bounds__(SMP_NT) void sample_kernel(
   const T* row = logits + (int64_t)b * row_stride;
   const float temp = temperature[b];
   const bool greedy = temp <= 1e-5f;
-  const int k = greedy ? 0 : top_k[b];
-  const float p = greedy ? 1.f : top_p[b];
+  const int k = (greedy || top_k == nullptr) ? 0 : top_k[b];          // null: vocab-parallel
+  const float p = (greedy || top_p == nullptr) ? 1.f : top_p[b];
   const bool use_k = k > 0 && k < V;
   const bool use_p = p < 1.f;
   const int S = gridDim.y, y = blockIdx.y;
@@ -231,14 +237,15 @@ __global__ __launch_bounds__(SMP_NT) void sample_kernel(
   float best = -INFINITY;
   int besti = 0x7fffffff;
   visit_row(row, i_lo, i_hi, tid, [&](int i, float r) {
+    const int gi = i + vocab_off;                 // global column (vocab-parallel shard)
     float x = xv(r);
     if (!greedy) {
       if (r < thr) return;
-      const uint32_t h = mix32(mix32(key ^ (uint32_t)(i * 0x9E3779B9u)) + hi);
+      const uint32_t h = mix32(mix32(key ^ (uint32_t)(gi * 0x9E3779B9u)) + hi);
       const float u = ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
       x += -logf(-logf(u));
     }
-    argmax_merge(best, besti, x, i);
+    argmax_merge(best, besti, x, gi);
   });
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -268,9 +275,49 @@ __global__ __launch_bounds__(256) void sample_merge_kernel(int64_t* __restrict__
   out[b] = (best == 0 || idx >= 0x7fffffffu) ? 0 : (int64_t)idx;
 }
 
+// Vocab-parallel: the row's packed candidate, biased (top bit flipped) so that a SIGNED
+// int64 max -- what RCCL / gloo reduce -- orders it like the unsigned packing.
+constexpr uint64_t VP_BIAS = 0x8000000000000000ull;
+
+__global__ __launch_bounds__(256) void sample_vp_merge_kernel(int64_t* __restrict__ packed,
+                                                              const uint64_t* __restrict__ partial,
+                                                              int B, int S) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  uint64_t best = 0;
+  for (int y = 0; y < S; ++y) best = max(best, partial[(int64_t)b * S + y]);
+  packed[b] = (int64_t)(best ^ VP_BIAS);
+}
+
+// after the MAX all-reduce over the TP group: packed candidate -> token id
+__global__ __launch_bounds__(256) void sample_vp_unpack_kernel(int64_t* __restrict__ out,
+                                                               const int64_t* __restrict__ packed,
+                                                               int B) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= B) return;
+  const uint64_t best = (uint64_t)packed[b] ^ VP_BIAS;
+  const uint32_t idx = ~(uint32_t)(best & 0xffffffffu);
+  out[b] = (best == 0 || idx >= 0x7fffffffu) ? 0 : (int64_t)idx;
+}
+
 int sample_splits(int B) {
   // enough 1024-thread blocks to cover the chip at small batch; 1 block/row at large
   return B >= 512 ? 1 : std::min(32, (512 + B - 1) / B);
+}
+
+static void sample_blocks(int dtype, uint64_t* partial, const void* logits, int64_t row_stride,
+                          int B, int V, const float* temperature, const int* top_k,
+                          const float* top_p, const int64_t* seeds, int vocab_off, dim3 grid,
+                          hipStream_t s) {
+  if (dtype == DT_BF16)
+    sample_kernel<bf16><<<grid, SMP_NT, 0, s>>>(partial, (const bf16*)logits, row_stride, V,
+                                                temperature, top_k, top_p, seeds, vocab_off);
+  else if (dtype == DT_F16)
+    sample_kernel<f16><<<grid, SMP_NT, 0, s>>>(partial, (const f16*)logits, row_stride, V,
+                                               temperature, top_k, top_p, seeds, vocab_off);
+  else
+    sample_kernel<float><<<grid, SMP_NT, 0, s>>>(partial, (const float*)logits, row_stride, V,
+                                                 temperature, top_k, top_p, seeds, vocab_off);
 }
 
 void launch_sample(int dtype, int64_t* out, uint64_t* partial, const void* logits,
@@ -278,16 +325,24 @@ void launch_sample(int dtype, int64_t* out, uint64_t* partial, const void* logit
                    const float* top_p, const int64_t* seeds, hipStream_t s) {
   if (B == 0) return;
   const dim3 grid(B, sample_splits(B));
-  if (dtype == DT_BF16)
-    sample_kernel<bf16><<<grid, SMP_NT, 0, s>>>(partial, (const bf16*)logits, row_stride, V,
-                                                temperature, top_k, top_p, seeds);
-  else if (dtype == DT_F16)
-    sample_kernel<f16><<<grid, SMP_NT, 0, s>>>(partial, (const f16*)logits, row_stride, V,
-                                               temperature, top_k, top_p, seeds);
-  else
-    sample_kernel<float><<<grid, SMP_NT, 0, s>>>(partial, (const float*)logits, row_stride, V,
-                                                 temperature, top_k, top_p, seeds);
+  sample_blocks(dtype, partial, logits, row_stride, B, V, temperature, top_k, top_p, seeds, 0,
+                grid, s);
   sample_merge_kernel<<<(B + 255) / 256, 256, 0, s>>>(out, partial, B, grid.y);
+}
+
+void launch_sample_vp(int dtype, int64_t* packed, uint64_t* partial, const void* logits,
+                      int64_t row_stride, int B, int V, const float* temperature,
+                      const int64_t* seeds, int vocab_off, hipStream_t s) {
+  if (B == 0) return;
+  const dim3 grid(B, sample_splits(B));
+  sample_blocks(dtype, partial, logits, row_stride, B, V, temperature, nullptr, nullptr, seeds,
+                vocab_off, grid, s);
+  sample_vp_merge_kernel<<<(B + 255) / 256, 256, 0, s>>>(packed, partial, B, grid.y);
+}
+
+void launch_sample_vp_unpack(int64_t* out, const int64_t* packed, int B, hipStream_t s) {
+  if (B == 0) return;
+  sample_vp_unpack_kernel<<<(B + 255) / 256, 256, 0, s>>>(out, packed, B);
 }
 
 }  // namespace kgc

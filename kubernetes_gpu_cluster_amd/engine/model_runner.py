@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 import time
 from typing import Optional
 
@@ -51,6 +52,7 @@ class StepPlan:
     max_ctx: int           # longest decode context
     dev_tok: int           # 1: decode input tokens come from the device-side last_tok table
     tok_bcast: int         # 1: TP ranks take the driver's sampled ids (driver-side logits processing)
+    vp: int                # 1: vocab-parallel sampling (TP > 1: no logits gather this step)
     i64: np.ndarray
     i32: np.ndarray
     f32: np.ndarray
@@ -60,7 +62,7 @@ class StepPlan:
 
     def header(self) -> list[int]:
         return [self.T, self.Tp, self.P, self.D, self.S, self.W, self.B, self.max_ctx,
-                self.dev_tok, self.tok_bcast]
+                self.dev_tok, self.tok_bcast, self.vp]
 
 
 class Layout:
@@ -137,7 +139,18 @@ class ModelRunner:
         self.tok_host = [torch.zeros(max_num_seqs, dtype=torch.int64, pin_memory=self.is_gpu)
                          for _ in range(2)]
         self._tok_flip = 0
-        self.stats = {"graph_steps": 0, "eager_steps": 0}
+        self.stats = {"graph_steps": 0, "eager_steps": 0, "vp_steps": 0,
+                      "tp_allreduce_bytes": 0, "tp_logits_bytes": 0}
+        # vocab-parallel sampling (TP > 1): every rank keeps its logits shard; rows
+        # without top-k / top-p / processors / logprobs are sampled by an 8-byte-per-row
+        # MAX all-reduce instead of an all-gather of B x V logits (ops.sample_vp_partial)
+        head = getattr(model, "lm_head", None)
+        self.vp = (self.ps.tp_size > 1 and getattr(model, "last", True) and head is not None
+                   and hasattr(head, "start") and os.environ.get("KGC_VP_SAMPLING", "1") != "0")
+        if self.vp:
+            self.vp_off = head.start
+            self.vp_cols = max(0, min(head.per, head.vocab - head.start))
+            self.vp_packed = torch.zeros(max_num_seqs, dtype=torch.int64, device=device)
 
     # ------------------------------------------------------------------ KV cache
     def kv_bytes_per_block(self) -> int:
@@ -222,7 +235,7 @@ class ModelRunner:
         i64[L.lidx:L.lidx + P] = qsl[1:] - 1
         self.hf.numpy()[: 2 * self.L.Smax] = 1.0
         i64[L.sslots:L.sslots + P] = 0
-        plan = StepPlan(T, T, P, 0, P, len(ws), 0, 0, 0, 0, i64, i32, self.hf.numpy())
+        plan = StepPlan(T, T, P, 0, P, len(ws), 0, 0, 0, 0, int(self.vp), i64, i32, self.hf.numpy())
         self.run(plan)
 
     # ------------------------------------------------------------------ packing (driver)
@@ -316,7 +329,11 @@ class ModelRunner:
                 if needs_counts(s.params):
                     s.proc_slot = s.slot
         bcast = int(proc is not None and self.ps.tp_size > 1)
-        return StepPlan(T, Tp, P, D, S, W, B, max_ctx, int(device_tokens and D > 0), bcast,
+        V = self.mcfg.vocab_size
+        vp = int(self.vp and lp is None and proc is None
+                 and all((s.params.top_k <= 0 or s.params.top_k >= V) and s.params.top_p >= 1.0
+                         for s in samplers))
+        return StepPlan(T, Tp, P, D, S, W, B, max_ctx, int(device_tokens and D > 0), bcast, vp,
                         i64, i32, f32, lp, proc, proc_init), samplers
 
     # ------------------------------------------------------------------ execution (all ranks)
@@ -378,6 +395,7 @@ class ModelRunner:
             g.replay()
             logits = logits[: plan.S]
             self.stats["graph_steps"] += 1
+            T = plan.B
         else:
             T = plan.T if not plan.B else plan.B
             D = plan.D if not plan.B else plan.B
@@ -388,7 +406,16 @@ class ModelRunner:
                 comm.pp_send(list(out))
                 return None
             idx = self.d64[L.lidx:L.lidx + plan.S]
-            logits = self.model.compute_logits(out.index_select(0, idx))
+            logits = self.model.compute_logits(out.index_select(0, idx), gather=not self.vp)
+        if ps.tp_size > 1:
+            self._count_tp_bytes(plan, T)
+        if self.vp:                 # logits are this rank's vocabulary shard
+            if plan.vp:
+                res = self._sample_vp(logits, plan)
+                self.last_tok.index_copy_(0, self.d64[L.sslots:L.sslots + plan.S], res)
+                self._last_lp = None
+                return res
+            logits = comm.tp_all_gather(logits, -1)[:, : self.mcfg.vocab_size]
         pre_lp = None
         if plan.proc and self.model.last:
             if plan.lp:       # logprobs report the raw distribution, before processing
@@ -411,6 +438,34 @@ class ModelRunner:
         else:
             self._last_lp = None
         return res
+
+    def _sample_vp(self, local: torch.Tensor, plan: StepPlan) -> torch.Tensor:
+        S, L = plan.S, self.L
+        packed = self.vp_packed[:S]
+        if self.vp_cols:
+            r = ops.sample_vp_partial(local, self.vp_cols, self.df[L.temp:L.temp + S],
+                                      self.d64[L.seeds:L.seeds + S], self.vp_off,
+                                      out=packed if self.is_gpu else None)
+            if r is not packed:
+                packed.copy_(r)
+        else:                       # a shard of vocabulary padding only
+            packed.fill_(torch.iinfo(torch.int64).min)
+        comm.tp_all_reduce_max(packed)
+        self.stats["vp_steps"] += 1
+        return ops.sample_vp_finish(packed, out=self.sample_out[:S] if self.is_gpu else None)
+
+    def _count_tp_bytes(self, plan: StepPlan, T: int) -> None:
+        """Bytes each rank contributes to TP collectives this step (the row-parallel
+        all-reduces of every layer, and the logits exchange)."""
+        tp = self.ps.tp_size
+        el = torch.finfo(self.dtype).bits // 8
+        n_ar = 2 * self.mcfg.num_layers + 1          # o + down per layer, embedding
+        self.stats["tp_allreduce_bytes"] += n_ar * T * self.mcfg.hidden_size * el
+        if self.vp and plan.vp:
+            self.stats["tp_logits_bytes"] += plan.S * 8
+        else:
+            per = self.model.lm_head.per
+            self.stats["tp_logits_bytes"] += plan.S * per * (tp - 1) * el
 
     def _logprobs_pre(self, lp: list, logits: torch.Tensor):
         """log-softmax of the raw logits for the rows that asked for logprobs and their
@@ -485,12 +540,12 @@ class ModelRunner:
             idx = self.d64[L.lidx:L.lidx + B]
             for _ in range(2):   # warm up (allocator, library handles) outside capture
                 h = self._forward(B, meta)
-                self.model.compute_logits(h.index_select(0, idx))
+                self.model.compute_logits(h.index_select(0, idx), gather=not self.vp)
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self.graph_pool):
                 h = self._forward(B, meta)
-                logits = self.model.compute_logits(h.index_select(0, idx))
+                logits = self.model.compute_logits(h.index_select(0, idx), gather=not self.vp)
             self.graphs[B] = (g, logits)
         torch.cuda.synchronize()
         return time.time() - t0

@@ -37,6 +37,7 @@ from .config import EngineConfig
 from .model_runner import ModelRunner, StepPlan
 
 CMD_STEP, CMD_PROFILE, CMD_INIT_CACHE, CMD_CAPTURE, CMD_EXIT = 1, 2, 3, 4, 5
+N_HDR = 11                  # StepPlan.header() fields
 
 
 def default_max_model_len(cfg: EngineConfig) -> int:
@@ -109,7 +110,7 @@ class Worker:
 # ---------------------------------------------------------------------- plan transport
 def _bcast_cmd(cmd: int, arg: int = 0, header: Optional[list[int]] = None) -> list[int]:
     s = get_state()
-    h = torch.zeros(12, dtype=torch.int64)
+    h = torch.zeros(16, dtype=torch.int64)
     if s.rank == 0:
         h[0], h[1] = cmd, arg
         if header:
@@ -157,7 +158,7 @@ def worker_loop(worker: Worker) -> None:
         elif cmd == CMD_CAPTURE:
             worker.capture()
         elif cmd == CMD_STEP:
-            hdr = h[2:12]
+            hdr = h[2:2 + N_HDR]
             _bcast_plan_blobs(worker.runner, hdr)
             r = worker.runner
             plan = StepPlan(*hdr, r.h64.numpy(), r.h32.numpy(), r.hf.numpy())

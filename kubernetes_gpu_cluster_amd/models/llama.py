@@ -295,8 +295,9 @@ class LlamaForCausalLM(nn.Module):
                               c_dn)
         return self.norm(res)
 
-    def compute_logits(self, hidden: torch.Tensor) -> torch.Tensor:
-        return self.lm_head(hidden)
+    def compute_logits(self, hidden: torch.Tensor, gather: bool = True) -> torch.Tensor:
+        """gather=False: this TP rank's vocabulary shard (vocab-parallel sampling)."""
+        return self.lm_head(hidden, gather)
 
     # ------------------------------------------------------------------ weights
     def _hf_map(self, name: str):

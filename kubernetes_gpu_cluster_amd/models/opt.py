@@ -88,8 +88,8 @@ class OPTForCausalLM(nn.Module):
             x = layer(positions, x, ctx)
         return self.final_layer_norm(x)
 
-    def compute_logits(self, hidden):
-        return self.lm_head(hidden)
+    def compute_logits(self, hidden, gather: bool = True):
+        return self.lm_head(hidden, gather)
 
     def load_weights(self, weights: Iterable[tuple[str, torch.Tensor]]) -> int:
         n = 0

@@ -226,8 +226,34 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
     return out
 
 
+def sample_vp_partial(logits: torch.Tensor, V: int, temperature: torch.Tensor,
+                      seeds: torch.Tensor, vocab_off: int,
+                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Vocab-parallel K10 (rows without top-k / top-p): this rank's packed (value,
+    global index) candidate per row over its shard ``logits[:, :V]`` (columns
+    ``vocab_off ..``), as int64 ordered for a MAX all-reduce over the TP group; then
+    ``sample_vp_finish``.  The result equals ``sample`` on the unsharded logits."""
+    B = logits.shape[0]
+    if not _gpu(logits):
+        return ref.sample_vp_partial(logits[:, :V], temperature[:B], seeds[:B], vocab_off)
+    if out is None:
+        out = torch.empty(B, dtype=torch.int64, device=logits.device)
+    _k().sample_vp(out, logits, V, temperature, seeds, vocab_off)
+    return out
+
+
+def sample_vp_finish(packed: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Token ids from the all-reduced packed candidates."""
+    if not _gpu(packed):
+        return ref.sample_vp_unpack(packed)
+    if out is None:
+        out = torch.empty_like(packed)
+    _k().sample_vp_unpack(out, packed)
+    return out
+
+
 __all__ = ["load_extension", "rms_norm", "fused_add_rms_norm", "layer_norm", "silu_mul",
-           "rope_kv_write", "paged_attention_decode", "prefill_attention", "sample",
+           "rope_kv_write", "paged_attention_decode", "prefill_attention", "sample", "sample_vp_partial", "sample_vp_finish",
            "decode_partials", "decode_grid_z", "prefill_work_list", "ref"]
 
 

@@ -15,6 +15,7 @@ loads, see csrc/kernels/attention_decode.hip):
 from __future__ import annotations
 
 import math
+import struct
 from typing import Optional
 
 import torch
@@ -226,6 +227,51 @@ def uniform_noise(seeds: torch.Tensor, vocab: int) -> torch.Tensor:
     h = _mix32(key ^ ((col[None, :] * 0x9E3779B9) & _M32))
     h = _mix32(h + ((seeds.long()[:, None] >> 32) & _M32))
     return ((h >> 8).double() + 0.5).float() * (1.0 / 16777216.0)
+
+
+def uniform_noise_cols(seeds: torch.Tensor, col0: int, n: int) -> torch.Tensor:
+    """``uniform_noise`` restricted to the global columns col0 .. col0 + n - 1."""
+    col = torch.arange(col0, col0 + n, dtype=torch.int64)
+    key = _mix32(seeds.long()[:, None] & _M32)
+    h = _mix32(key ^ ((col[None, :] * 0x9E3779B9) & _M32))
+    h = _mix32(h + ((seeds.long()[:, None] >> 32) & _M32))
+    return ((h >> 8).double() + 0.5).float() * (1.0 / 16777216.0)
+
+
+_VP_BIAS = 1 << 63
+
+
+def _ord_key(v: float) -> int:
+    b = struct.unpack("<I", struct.pack("<f", v))[0]
+    return (~b & 0xFFFFFFFF) if b & 0x80000000 else (b | 0x80000000)
+
+
+def sample_vp_partial(logits: torch.Tensor, temperature: torch.Tensor, seeds: torch.Tensor,
+                      vocab_off: int) -> torch.Tensor:
+    """Vocab-parallel sampler, one shard: per row the packed (ord(value) << 32 | ~global
+    index) of the shard's (Gumbel-)argmax, biased to a signed int64 so that a MAX
+    all-reduce over the shards yields the unsharded sampler's pick (ties -> lower
+    index).  Rows must not use top-k / top-p."""
+    B, V = logits.shape
+    x = logits.float().cpu()
+    u = uniform_noise_cols(seeds.cpu(), vocab_off, V)
+    out = torch.empty(B, dtype=torch.int64)
+    for b in range(B):
+        t = float(temperature[b])
+        row = x[b] if t <= 1e-5 else x[b] / t - torch.log(-torch.log(u[b]))
+        i = int(torch.argmax(row))                       # first index on ties
+        packed = (_ord_key(float(row[i])) << 32) | (~(i + vocab_off) & 0xFFFFFFFF)
+        out[b] = packed - _VP_BIAS                       # == (packed ^ bias) as int64
+    return out.to(logits.device)
+
+
+def sample_vp_unpack(packed: torch.Tensor) -> torch.Tensor:
+    out = torch.empty_like(packed)
+    for b, v in enumerate(packed.tolist()):
+        u64 = v + _VP_BIAS
+        idx = ~u64 & 0xFFFFFFFF
+        out[b] = 0 if (u64 == 0 or idx >= 0x7FFFFFFF) else idx
+    return out
 
 
 def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,

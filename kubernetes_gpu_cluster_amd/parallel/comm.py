@@ -39,6 +39,14 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
+def tp_all_reduce_max(x: torch.Tensor) -> torch.Tensor:
+    """In-place MAX over the TP group (vocab-parallel sampling: 8 bytes per row)."""
+    s = get_state()
+    if s.tp_size > 1:
+        dist.all_reduce(x, op=dist.ReduceOp.MAX, group=s.tp_group)
+    return x
+
+
 def tp_all_gather(x: torch.Tensor, dim: int = -1) -> torch.Tensor:
     s = get_state()
     if s.tp_size == 1:

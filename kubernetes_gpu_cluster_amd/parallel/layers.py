@@ -218,9 +218,13 @@ class ParallelLMHead(nn.Module):
     def get_weight(self):
         return self.emb.weight if self.emb is not None else self.weight
 
-    def forward(self, h: torch.Tensor) -> torch.Tensor:
+    def forward(self, h: torch.Tensor, gather: bool = True) -> torch.Tensor:
+        """gather=False keeps this rank's shard [T, per] (padding columns included:
+        the vocab-parallel sampler reads only the valid ones)."""
         logits = linear(h, self.get_weight())
         tp, _ = _tp()
+        if not gather:
+            return logits
         if tp > 1:
             logits = comm.tp_all_gather(logits, -1)
         return logits[:, : self.vocab]

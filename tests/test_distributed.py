@@ -192,3 +192,53 @@ def test_engine_tp2_logits_processing_matches_tp1(tmp_path):
         outs[tp] = [o.output_token_ids for o in llm.generate(prompts, sp)]
         llm.shutdown()
     assert outs[2] == outs[1]
+
+
+def test_vocab_parallel_sampling_matches_gathered(tmp_path, monkeypatch):
+    """TP=2 vocab-parallel sampling (each rank's shard -> packed (value, index) -> MAX
+    all-reduce of 8 bytes per row) picks exactly the tokens the gathered-logits sampler
+    picks, for greedy and seeded temperature rows; top-p rows fall back to the gather.
+    Per-step logits traffic drops from S x V/tp x (tp-1) elements to S x 8 bytes."""
+    from kubernetes_gpu_cluster_amd.engine.llm_engine import LLM
+    from kubernetes_gpu_cluster_amd.engine.sequence import SamplingParams
+    d = str(tmp_path / "m")
+    _write_hf_dir(d, "tiny-llama")
+    prompts = [list(range(3, 30)), [5, 6, 7] * 7, [9, 10]]
+    sp_vp = [SamplingParams(temperature=0.8, seed=1, max_tokens=10, ignore_eos=True),
+             SamplingParams(temperature=0, max_tokens=10, ignore_eos=True),
+             SamplingParams(temperature=1.0, seed=7, max_tokens=10, ignore_eos=True)]
+    sp_topp = [SamplingParams(temperature=0.9, seed=3, top_p=0.8, max_tokens=6, ignore_eos=True)] * 3
+    outs, stats = {}, {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("KGC_VP_SAMPLING", mode)
+        llm = LLM(d, device="cpu", dtype="float32", tensor_parallel_size=2, max_model_len=256,
+                  max_num_seqs=4, max_num_batched_tokens=64, num_gpu_blocks_override=64)
+        outs[mode] = ([o.output_token_ids for o in llm.generate(prompts, sp_vp)],
+                      [o.output_token_ids for o in llm.generate(prompts, sp_topp)])
+        stats[mode] = dict(llm.engine.executor.runner.stats)
+        llm.shutdown()
+    assert outs["1"] == outs["0"]
+    assert stats["1"]["vp_steps"] > 0 and stats["0"]["vp_steps"] == 0
+    assert stats["1"]["tp_logits_bytes"] < stats["0"]["tp_logits_bytes"]
+
+
+def test_tp_logits_bytes_llama3_8b_tp8():
+    """The per-step logits exchange at B = 256, TP = 8 (Llama-3-8B vocabulary): ~57 MB
+    per rank gathered vs 2 KB vocab-parallel."""
+    import types
+    from kubernetes_gpu_cluster_amd.engine.model_runner import ModelRunner
+    from kubernetes_gpu_cluster_amd.models.configs import PRESETS
+    from kubernetes_gpu_cluster_amd.parallel.layers import _pad_vocab
+    mcfg = PRESETS["llama-3-8b"]
+    per = _pad_vocab(mcfg.vocab_size, 8) // 8
+    got = {}
+    for vp in (True, False):
+        r = types.SimpleNamespace(ps=types.SimpleNamespace(tp_size=8), dtype=torch.bfloat16,
+                                  mcfg=mcfg, vp=vp, model=types.SimpleNamespace(
+                                      lm_head=types.SimpleNamespace(per=per)),
+                                  stats={"tp_allreduce_bytes": 0, "tp_logits_bytes": 0})
+        plan = types.SimpleNamespace(S=256, vp=int(vp))
+        ModelRunner._count_tp_bytes(r, plan, 256)
+        got[vp] = r.stats["tp_logits_bytes"]
+    assert got[True] == 256 * 8
+    assert got[False] > 50e6

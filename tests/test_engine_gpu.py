@@ -139,12 +139,15 @@ def test_engine_preemption_recompute(gpu):
     assert eng.bm.num_free == eng.bm.num_blocks - 1
 
 
-def test_tp2_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch):
+@pytest.mark.parametrize("eager", [True, False])
+def test_tp2_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch, eager):
     """The tensor-parallel engine on the GPU: two ranks share cuda:0 (gloo process group,
     since RCCL refuses two ranks on one device), sharded QKV/MLP/vocab layers, the xGMI
     all-reduce kernel over IPC buffers for the row-parallel sums, multiprocess workers.
-    Greedy continuations match TP=1 (bf16; sharded sums round differently, so a couple
-    of late near-tie flips are tolerated)."""
+    eager=False is the production decode path: hipGraph-captured decode buckets with
+    the xGMI all-reduce INSIDE the graphs, and vocab-parallel sampling after the replay
+    (no logits all-gather).  Greedy continuations match TP=1 (bf16; sharded sums round
+    differently, so a couple of late near-tie flips are tolerated)."""
     import json
     import os
     from safetensors.torch import save_file
@@ -166,7 +169,7 @@ def test_tp2_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch):
     outs = {}
     monkeypatch.setenv("KGC_DIST_BACKEND", "gloo")
     for tp in (1, 2):
-        llm = LLM(d, device="cuda", dtype="bfloat16", tensor_parallel_size=tp, enforce_eager=True,
+        llm = LLM(d, device="cuda", dtype="bfloat16", tensor_parallel_size=tp, enforce_eager=eager,
                   max_model_len=256, max_num_seqs=4, max_num_batched_tokens=128,
                   num_gpu_blocks_override=64)
         if tp == 2:
@@ -176,6 +179,10 @@ def test_tp2_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch):
         outs[tp] = [o.output_token_ids for o in llm.generate(prompts, sp)]
         if tp == 2:
             car.check()
+            st = llm.engine.executor.runner.stats
+            assert st["vp_steps"] > 0, st
+            if not eager:
+                assert st["graph_steps"] > 0, st
         llm.shutdown()
     same = sum(a == b for x, y in zip(outs[1], outs[2]) for a, b in zip(x, y))
     assert all(x[0] == y[0] for x, y in zip(outs[1], outs[2])), outs
@@ -222,3 +229,51 @@ def test_fp8_kv_engine_graphs(gpu):
         top_a = a.logprobs[0][2]
         assert tok_b in [t for t, _ in top_a], (a.output_token_ids, b.output_token_ids)
         assert abs(top_a[0][1] - b.logprobs[0][2][0][1]) < 0.15
+
+
+def _rccl_capture_worker(port):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        x = torch.zeros(1 << 16, dtype=torch.bfloat16, device=dev)
+        y = torch.empty(1 << 16, dtype=torch.bfloat16, device=dev)
+        dist.all_reduce(x)                       # communicator + warm up outside capture
+        dist.all_gather_into_tensor(y, x)
+        torch.cuda.synchronize()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            x.mul_(2)
+            dist.all_reduce(x)
+            dist.all_gather_into_tensor(y, x)
+        for it in range(3):
+            src = torch.randint(-50, 50, (1 << 16,), device=dev).to(torch.bfloat16)
+            x.copy_(src)
+            g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(x, src * 2) and torch.equal(y, src * 2), it
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_collectives_capture_in_hipgraph(gpu):
+    """A single-rank RCCL process group: all_reduce and all_gather captured into a
+    hipGraph and replayed (the decode graphs' collectives at TP > 1 when the xGMI
+    kernel is off or a tensor exceeds its buffer)."""
+    import socket
+    import torch.multiprocessing as tmp
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = tmp.get_context("spawn")
+    p = ctx.Process(target=_rccl_capture_worker, args=(port,))
+    p.start()
+    p.join(300)
+    if p.is_alive():
+        p.kill()
+    assert p.exitcode == 0

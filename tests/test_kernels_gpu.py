@@ -239,6 +239,35 @@ def test_sample_distribution(gpu):
     assert (freq - exp).abs().max() < 0.015
 
 
+@pytest.mark.parametrize("tp", [2, 8])
+def test_sample_vocab_parallel_equals_unsharded(gpu, tp):
+    """K10 vocab-parallel: per-shard packed candidates (global-column noise) + MAX over
+    the shards + unpack == the unsharded sampler, bit for bit (greedy and temperature
+    rows; padded shard columns excluded); and == the CPU reference."""
+    torch.manual_seed(7)
+    B, V = 64, 128256
+    per = (V + 64 * tp - 1) // (64 * tp) * 64            # ParallelLMHead padding
+    logits = (torch.randn(B, per * tp, device=gpu) * 3).to(torch.bfloat16)
+    logits[5, 1000] = logits[5, V - 3] = 40.0             # greedy tie across shards
+    temp = torch.tensor([0.0, 1.0, 0.7, 1.3] * (B // 4), device=gpu)
+    seeds = torch.arange(B, dtype=torch.int64, device=gpu) * 104729 + (3 << 32)
+    ones = torch.ones(B, device=gpu)
+    full = ops.sample(logits[:, :V].contiguous(), temp, torch.full((B,), -1, dtype=torch.int32,
+                      device=gpu), ones, seeds).cpu()
+    parts = []
+    for r in range(tp):
+        shard = logits[:, r * per:(r + 1) * per].contiguous()
+        cols = max(0, min(per, V - r * per))
+        parts.append(ops.sample_vp_partial(shard, cols, temp, seeds, r * per))
+    packed = torch.stack(parts).max(0).values
+    got = ops.sample_vp_finish(packed).cpu()
+    assert got.tolist() == full.tolist()
+    assert got[5].item() == 1000
+    # CPU reference of one shard's candidate (index; the fp32 value may differ in ulps)
+    r0 = ref.sample_vp_partial(logits[:8, :per].cpu(), temp[:8].cpu(), seeds[:8].cpu(), 0)
+    assert ref.sample_vp_unpack(r0).tolist() == ops.sample_vp_finish(parts[0][:8]).cpu().tolist()
+
+
 # ------------------------------------------------------------------ MoE (K13 / K14)
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("E,k", [(8, 2), (4, 2), (64, 6)])
