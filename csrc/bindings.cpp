@@ -140,7 +140,7 @@ void rope_kv_write(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor q_out, T
                             q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
                             slot_mapping.data_ptr<int64_t>(), qn, kn, (int)T, (int)nq, (int)nkv,
                             (int)d, (int)k_cache.size(2), (float)eps, use_rope, kv8,
-                            (float)k_scale, (float)v_scale, stream());
+                            (float)k_scale, (float)v_scale, (int)k_cache.size(0), stream());
 }
 
 void check_kv(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, int64_t nq) {
@@ -187,7 +187,7 @@ void paged_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor b
                            tmp_out.data_ptr<float>(), (int)B, (int)nq, (int)k_cache.size(1),
                            (int)d, log2_exact(k_cache.size(2), "block_size"), (int)Zmax, (int)Z,
                            (float)scale, k_cache.scalar_type() == at::kFloat8_e4m3fn,
-                           (float)k_scale, (float)v_scale, stream());
+                           (float)k_scale, (float)v_scale, (int)k_cache.size(0), stream());
 }
 
 void prefill_attention(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables,
@@ -216,7 +216,7 @@ void prefill_attention(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Ten
                                 (int)k_cache.size(1), (int)d,
                                 log2_exact(k_cache.size(2), "block_size"), (float)scale,
                                 k_cache.scalar_type() == at::kFloat8_e4m3fn, (float)k_scale,
-                                (float)v_scale, stream());
+                                (float)v_scale, (int)k_cache.size(0), stream());
 }
 
 void sample(Tensor out, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds) {
@@ -567,6 +567,53 @@ void xgmi_allreduce(Tensor inout, std::vector<int64_t> data, std::vector<int64_t
                         cap_bytes / 16, two_shot, stream());
 }
 
+// debug builds: OR of the K1/K2/K3 bounds-check error words (read and cleared)
+int64_t debug_errors() {
+  return (int64_t)(kgc::dbg_err_attention_decode() | (kgc::dbg_err_attention_prefill() << 1) |
+                   (kgc::dbg_err_rope_cache() << 2));
+}
+
+bool debug_build() {
+#ifdef KGC_DEBUG
+  return true;
+#else
+  return false;
+#endif
+}
+
+int64_t allreduce_rms_max_hidden_op() { return kgc::allreduce_rms_max_hidden(); }
+
+void xgmi_allreduce_rms(Tensor out, Tensor in, Tensor residual, Tensor w, double eps,
+                        std::vector<int64_t> data, std::vector<int64_t> sig, int64_t rank,
+                        int64_t cap_bytes) {
+  check_gpu(in, "in");
+  check_same_dev(in, out, "out");
+  check_same_dev(in, residual, "residual");
+  check_same_dev(in, w, "w");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(in.device());
+  const int64_t nr = (int64_t)data.size();
+  TORCH_CHECK(nr == 2 || nr == 4 || nr == 8, "xgmi all-reduce: 2, 4 or 8 ranks");
+  TORCH_CHECK((int64_t)sig.size() == nr && rank >= 0 && rank < nr, "bad rank / pointer lists");
+  TORCH_CHECK(in.dim() == 2 && in.is_contiguous() && out.is_contiguous() &&
+              residual.is_contiguous() && w.is_contiguous(), "contiguous [M, H] rows");
+  TORCH_CHECK(out.sizes() == in.sizes() && residual.sizes() == in.sizes() &&
+              w.numel() == in.size(1), "out / residual [M, H], w [H]");
+  TORCH_CHECK(in.scalar_type() == out.scalar_type() && in.scalar_type() == residual.scalar_type() &&
+              in.scalar_type() == w.scalar_type() &&
+              (in.scalar_type() == at::kBFloat16 || in.scalar_type() == at::kHalf), "bf16 / fp16 only");
+  const int64_t M = in.size(0), H = in.size(1);
+  TORCH_CHECK(H % 8 == 0 && H <= kgc::allreduce_rms_max_hidden(), "hidden size unsupported");
+  TORCH_CHECK(M * H * in.element_size() <= cap_bytes, "rows larger than the IPC buffer");
+  kgc::ArPtrs P{};
+  for (int64_t r = 0; r < nr; ++r) {
+    P.data[r] = (void*)(intptr_t)data[r];
+    P.sig[r] = (void*)(intptr_t)sig[r];
+  }
+  kgc::launch_allreduce_rms(dt_code(in), P, (int)nr, (int)rank, in.data_ptr(), out.data_ptr(),
+                            residual.data_ptr(), w.data_ptr(), (int)M, (int)H, (float)eps,
+                            cap_bytes / 16, stream());
+}
+
 void skinny_gemm(Tensor C, Tensor X, Tensor W, std::optional<Tensor> bias, int64_t mt,
                  int64_t nt, int64_t nw, bool ntl, int64_t epi, std::optional<Tensor> gamma,
                  double eps) {
@@ -664,6 +711,11 @@ TORCH_LIBRARY(kgc, m) {
   m.def("ar_err_copy_async(int sig, Tensor(a!) host_out) -> ()", &ar_err_copy_async);
   m.def("xgmi_allreduce(Tensor(a!) inout, int[] data, int[] sig, int rank, int cap_bytes, "
         "bool two_shot) -> ()");
+  m.def("xgmi_allreduce_rms(Tensor(a!) out, Tensor inp, Tensor(b!) residual, Tensor w, float eps, "
+        "int[] data, int[] sig, int rank, int cap_bytes) -> ()");
+  m.def("allreduce_rms_max_hidden() -> int", &allreduce_rms_max_hidden_op);
+  m.def("debug_errors() -> int", &debug_errors);
+  m.def("debug_build() -> bool", &debug_build);
   m.def("prefill_block_m() -> int", &prefill_block_m);
   m.def("skinny_gemm(Tensor(a!) C, Tensor X, Tensor W, Tensor? bias, int mt, int nt, int nw, "
         "bool ntl, int epi=0, Tensor? gamma=None, float eps=1e-6) -> ()");
@@ -680,6 +732,7 @@ TORCH_LIBRARY_IMPL(kgc, CUDA, m) {
   m.impl("sample_vp", &sample_vp);
   m.impl("sample_vp_unpack", &sample_vp_unpack);
   m.impl("xgmi_allreduce", &xgmi_allreduce);
+  m.impl("xgmi_allreduce_rms", &xgmi_allreduce_rms);
   m.impl("moe_route", &moe_route);
   m.impl("moe_align", &moe_align);
   m.impl("moe_gemm", &moe_gemm);

@@ -4,6 +4,13 @@ Drives ``hipcc`` directly (no hipify, no torch JIT cache) so the exact same
 ``.so`` travels with the repo snapshot to the GPU box:
 
     python csrc/build.py [--force] [-j N] [--arch gfx950]
+    KGC_HIP_DEBUG=1 python csrc/build.py      # or --debug
+
+The debug build (``_kgc_ops_debug.so``, its own object directory) defines
+``KGC_DEBUG``: the attention / KV-write kernels (K1, K2, K3) range-check every block
+table entry, slot and context length they read, clamp a bad one, and report it
+through ``kgc.debug_errors()``.  ``KGC_HIP_DEBUG=1`` at run time makes
+``ops.load_extension`` load that library and raise after every step that tripped a check.
 
 Kernel translation units (``csrc/kernels/*.hip``) never include torch headers;
 only ``csrc/bindings.cpp`` does.  Objects are rebuilt when their source or any
@@ -21,8 +28,16 @@ import sysconfig
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "csrc")
-OUT = os.path.join(ROOT, "kubernetes_gpu_cluster_amd", "_kgc_ops.so")
-BUILD = os.path.join(ROOT, "build", "kgc_ops")
+DEBUG = os.environ.get("KGC_HIP_DEBUG", "0") not in ("", "0")
+
+
+def _paths(debug: bool) -> tuple[str, str]:
+    name = "_kgc_ops_debug.so" if debug else "_kgc_ops.so"
+    return (os.path.join(ROOT, "kubernetes_gpu_cluster_amd", name),
+            os.path.join(ROOT, "build", "kgc_ops_debug" if debug else "kgc_ops"))
+
+
+OUT, BUILD = _paths(DEBUG)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
@@ -46,12 +61,16 @@ def _run(cmd):
     return r.stderr
 
 
-def build(force: bool = False, jobs: int = 8, arch: str = "gfx950", verbose: bool = False) -> str:
+def build(force: bool = False, jobs: int = 8, arch: str = "gfx950", verbose: bool = False,
+          debug: bool = DEBUG) -> str:
     inc, api_inc, lib, abi = _torch_paths()
+    OUT, BUILD = _paths(debug)
     os.makedirs(BUILD, exist_ok=True)
     hdr_t = _newest_header()
     common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={arch}", "-I", CSRC,
               "-D__HIP_PLATFORM_AMD__=1", "-Wno-unused-result", "-ffp-contract=fast"]
+    if debug:
+        common.append("-DKGC_DEBUG=1")
     kern = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     jobs_list = []
     for src in kern:
@@ -64,7 +83,7 @@ def build(force: bool = False, jobs: int = 8, arch: str = "gfx950", verbose: boo
               "-isystem", sysconfig.get_paths()["include"],
               f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1",
               "-DTORCH_API_INCLUDE_EXTENSION_H", "-Wno-deprecated-declarations",
-              "-Wno-unused-parameter"]
+              "-Wno-unused-parameter"] + (["-DKGC_DEBUG=1"] if debug else [])
     jobs_list.append((bind, bobj, bflags))
 
     def stale(src, obj):
@@ -97,8 +116,9 @@ def main():
     ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 8))
     ap.add_argument("--arch", default="gfx950")
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--debug", action="store_true", help="the KGC_DEBUG bounds-checking build")
     a = ap.parse_args()
-    print(build(a.force, a.jobs, a.arch, a.verbose))
+    print(build(a.force, a.jobs, a.arch, a.verbose, debug=a.debug or DEBUG))
 
 
 if __name__ == "__main__":

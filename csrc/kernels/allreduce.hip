@@ -2,7 +2,8 @@
 // the reference only toggles it: values-01-minimal-example8.yaml:32
 // `--disable-custom-all-reduce`).
 //
-// Every TP rank owns one uncached IPC buffer: [ArSignal][data parity 0][data parity 1].
+// Every TP rank owns one uncached IPC buffer: [ArSignal][data parity 0][data parity 1]
+// [fused parity 0][fused parity 1] (the last two for allreduce_rms_kernel).
 // The peers' buffers are mapped into each process (hipIpcOpenMemHandle), so a kernel
 // reads the other GPUs' HBM directly over the point-to-point xGMI links -- all 7 links
 // of an MI355X in parallel, instead of RCCL's ring that is bound by one link per step.
@@ -132,6 +133,113 @@ __global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArPtrs P, int ran
     }
   }
   if (threadIdx.x == 0) self->counter[blockIdx.x] = epoch;
+}
+
+// ---- fused one-shot all-reduce + residual add + RMSNorm (row-parallel o / down
+// projections at TP > 1):  h = sum_r in_r (rounded to T, as the all-reduce stores it);
+// residual += h (rounded);  out = rms_norm(residual) * w  -- the same rounding points
+// as xgmi_allreduce followed by fused_add_rms_norm (norm.hip), in one launch and one
+// pass over the peers' rows.
+// Rows map to blocks (row % AR_MAX_BLOCKS) in the copy-in and in the reduce, so block
+// b's barrier covers exactly the rows block b reads.  This kernel has its own IPC data
+// regions (P.data points past the plain all-reduce's two), so a peer block still in an
+// earlier call of the OTHER kernel -- whose element -> block mapping differs -- never
+// reads memory this one overwrites.
+constexpr int ARN_MAXV = 4;   // 512 threads x 4 x 8 = 16384 = widest hidden supported
+
+template <typename T, int NR>
+__global__ __launch_bounds__(AR_THREADS) void allreduce_rms_kernel(
+    ArPtrs P, int rank, const T* __restrict__ in, T* __restrict__ out, T* __restrict__ residual,
+    const T* __restrict__ w, int M, int H, float eps, int64_t cap_vec) {
+  __shared__ float scratch[AR_THREADS / 64];
+  ArSignal* self = reinterpret_cast<ArSignal*>(P.sig[rank]);
+  __shared__ uint32_t s_epoch;
+  if (threadIdx.x == 0) s_epoch = self->counter[blockIdx.x] + 1;
+  __syncthreads();
+  const uint32_t epoch = s_epoch;
+  const int64_t par_off = (int64_t)(epoch & 1) * cap_vec;
+  const int nv = H >> 3;                             // 16-byte vectors per row
+  const u32x4* src = reinterpret_cast<const u32x4*>(in);
+  u32x4* mine = reinterpret_cast<u32x4*>(P.data[rank]) + par_off;
+
+  for (int row = blockIdx.x; row < M; row += AR_MAX_BLOCKS)
+    for (int v = threadIdx.x; v < nv; v += AR_THREADS)
+      mine[(int64_t)row * nv + v] = src[(int64_t)row * nv + v];
+  ar_barrier<NR>(P, rank, 0, epoch);
+
+  Pack8<T> wv[ARN_MAXV];
+#pragma unroll
+  for (int i = 0; i < ARN_MAXV; ++i) {
+    const int v = threadIdx.x + i * AR_THREADS;
+    if (v < nv) wv[i].u = reinterpret_cast<const u32x4*>(w)[v];
+  }
+  for (int row = blockIdx.x; row < M; row += AR_MAX_BLOCKS) {   // uniform per block
+    Pack8<T> h[ARN_MAXV];
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < ARN_MAXV; ++i) {
+      const int v = threadIdx.x + i * AR_THREADS;
+      if (v >= nv) continue;
+      const int64_t e = (int64_t)row * nv + v;
+      Pack8<T> pk[NR];
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+        pk[r].u = ld_peer(reinterpret_cast<const u32x4*>(P.data[r]) + par_off + e);
+      Pack8<T> res;
+      res.u = reinterpret_cast<const u32x4*>(residual)[e];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float acc = 0.f;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) acc += to_f<T>(pk[r].h[j]);
+        const float sum = to_f<T>(from_f<T>(acc));             // the all-reduce output
+        h[i].h[j] = from_f<T>(sum + to_f<T>(res.h[j]));          // residual += h
+        const float f = to_f<T>(h[i].h[j]);
+        ss += f * f;
+      }
+      reinterpret_cast<u32x4*>(residual)[e] = h[i].u;
+    }
+    ss = block_sum<AR_THREADS>(ss, scratch);
+    const float inv = rsqrtf(ss / (float)H + eps);
+#pragma unroll
+    for (int i = 0; i < ARN_MAXV; ++i) {
+      const int v = threadIdx.x + i * AR_THREADS;
+      if (v >= nv) continue;
+      Pack8<T> o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o.h[j] = from_f<T>(to_f<T>(h[i].h[j]) * inv * to_f<T>(wv[i].h[j]));
+      reinterpret_cast<u32x4*>(out)[(int64_t)row * nv + v] = o.u;
+    }
+  }
+  if (threadIdx.x == 0) self->counter[blockIdx.x] = epoch;
+}
+
+template <typename T>
+static void arn_by_ranks(int nranks, const ArPtrs& P, int rank, const void* in, void* out,
+                         void* residual, const void* w, int M, int H, float eps, int64_t cap_vec,
+                         hipStream_t s) {
+  const dim3 g(AR_MAX_BLOCKS), b(AR_THREADS);
+#define KGC_ARN(NR_)                                                                          \
+  allreduce_rms_kernel<T, NR_><<<g, b, 0, s>>>(P, rank, (const T*)in, (T*)out, (T*)residual, \
+                                               (const T*)w, M, H, eps, cap_vec)
+  switch (nranks) {
+    case 2: KGC_ARN(2); break;
+    case 4: KGC_ARN(4); break;
+    case 8: KGC_ARN(8); break;
+    default: break;
+  }
+#undef KGC_ARN
+}
+
+int allreduce_rms_max_hidden() { return AR_THREADS * ARN_MAXV * 8; }
+
+void launch_allreduce_rms(int dtype, const ArPtrs& P, int nranks, int rank, const void* in,
+                          void* out, void* residual, const void* w, int M, int H, float eps,
+                          int64_t cap_vec, hipStream_t s) {
+  if (dtype == DT_BF16)
+    arn_by_ranks<bf16>(nranks, P, rank, in, out, residual, w, M, H, eps, cap_vec, s);
+  else
+    arn_by_ranks<f16>(nranks, P, rank, in, out, residual, w, M, H, eps, cap_vec, s);
 }
 
 template <typename T, int NR>

@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
     const void* __restrict__ vc_, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ ctx_lens, float* __restrict__ max_logits,
     float* __restrict__ exp_sums, float* __restrict__ tmp_out, int nq, int nkv, int bs_log2,
-    int Zmax, float scale_log2, float v_scale) {
+    int Zmax, float scale_log2, float v_scale, int num_blocks) {
   typedef typename Vec8<T>::type V8;
   typedef std::conditional_t<KV8, uint8_t, T> C;   // cache element
   const C* __restrict__ kc = reinterpret_cast<const C*>(kc_);
@@ -74,7 +74,9 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
   const int r16 = lane & 15, qd = lane >> 4;
   const int G = nq / nkv;
   // clamp to the block-table capacity: a bad length gives wrong output, never a fault
-  const int ctx = min(ctx_lens[b], bt_stride << bs_log2);
+  int ctx_in = ctx_lens[b];
+  KGC_DCHECK_RANGE(ctx_in, 0, (bt_stride << bs_log2) + 1, "decode ctx_len");
+  const int ctx = min(ctx_in, bt_stride << bs_log2);
   const int* bt = block_tables + (int64_t)b * bt_stride;
   const int bsm = (1 << bs_log2) - 1;
   const int64_t head_stride = (int64_t)D << bs_log2;   // elements per (block, kv-head)
@@ -119,11 +121,11 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
     for (int c = 0; c < NCH; ++c) {
       const int ta = min(base + c * 32 + keyA, end - 1);
       const int tb = min(base + c * 32 + keyA + 4, end - 1);
-      kaddr[c][0] = kbase + bt[ta >> bs_log2] * blk_stride + (int64_t)(ta & bsm) * D + 8 * qd;
-      kaddr[c][1] = kbase + bt[tb >> bs_log2] * blk_stride + (int64_t)(tb & bsm) * D + 8 * qd;
+      kaddr[c][0] = kbase + kgc_bt(bt, ta >> bs_log2, bt_stride, num_blocks) * blk_stride + (int64_t)(ta & bsm) * D + 8 * qd;
+      kaddr[c][1] = kbase + kgc_bt(bt, tb >> bs_log2, bt_stride, num_blocks) * blk_stride + (int64_t)(tb & bsm) * D + 8 * qd;
       // V^T 8-key group of keys t0..t0+7: [(t0 & bsm) / 8][d][8]; 16 lanes = 256 B
       const int t0 = min(base + c * 32 + 8 * qd, end - 1) & ~7;
-      vaddr[c] = vbase + bt[t0 >> bs_log2] * blk_stride + ((t0 & bsm) >> 3) * (D * 8) + r16 * 8;
+      vaddr[c] = vbase + kgc_bt(bt, t0 >> bs_log2, bt_stride, num_blocks) * blk_stride + ((t0 & bsm) >> 3) * (D * 8) + r16 * 8;
     }
     Pack8<T> kf[NCH][2][KS];
     Pack8<T> vf[PREF ? NCH : 1][DT];
@@ -293,11 +295,11 @@ template <typename T, int D, bool KV8>
 static void decode_dispatch(void* out, const void* q, const void* kc, const void* vc,
                             const int* bt, int bt_stride, const int* ctx, float* ml, float* es,
                             float* tmp, int B, int nq, int nkv, int bs_log2, int Zmax, int Z,
-                            float scale_log2, float v_scale, hipStream_t s) {
+                            float scale_log2, float v_scale, int num_blocks, hipStream_t s) {
   auto kern = paged_decode_kernel<T, D, true, KV8, 4, 1>;
   kern<<<dim3(B, nkv, Z), 256, 0, s>>>(
       (T*)out, (const T*)q, kc, vc, bt, bt_stride, ctx, ml, es, tmp, nq,
-      nkv, bs_log2, Zmax, scale_log2, v_scale);
+      nkv, bs_log2, Zmax, scale_log2, v_scale, num_blocks);
   if (Z > 1)
     paged_decode_reduce_kernel<T, D><<<dim3(B, nq), 64, 0, s>>>((T*)out, ml, es, tmp, ctx, nq,
                                                                 Z, Zmax);
@@ -308,13 +310,13 @@ void launch_paged_decode(int dtype, void* out, const void* q, const void* k_cach
                          const int* ctx_lens, float* max_logits, float* exp_sums,
                          float* tmp_out, int B, int nq, int nkv, int D, int bs_log2,
                          int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
-                         float v_scale, hipStream_t s) {
+                         float v_scale, int num_blocks, hipStream_t s) {
   if (B == 0) return;
   const float sl2 = scale * k_scale * 1.4426950408889634f;
 #define KGC_DEC(TT, DD, K8)                                                               \
   decode_dispatch<TT, DD, K8>(out, q, k_cache, v_cache, block_tables, bt_stride, ctx_lens, \
                               max_logits, exp_sums, tmp_out, B, nq, nkv, bs_log2, Zmax, Z, \
-                              sl2, v_scale, s)
+                              sl2, v_scale, num_blocks, s)
 #define KGC_DEC_D(TT, K8) \
   if (D == 128) KGC_DEC(TT, 128, K8); else KGC_DEC(TT, 64, K8)
   if (dtype == DT_BF16) {
@@ -327,5 +329,7 @@ void launch_paged_decode(int dtype, void* out, const void* q, const void* k_cach
 }
 
 int paged_decode_partition_size() { return DEC_PART; }
+
+KGC_DEBUG_TU(attention_decode)
 
 }  // namespace kgc

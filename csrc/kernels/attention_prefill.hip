@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
     const void* __restrict__ vc_, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ qsl, const int* __restrict__ seq_lens,
     const int* __restrict__ work_seq, const int* __restrict__ work_mblk, int nq, int nkv,
-    int bs_log2, float scale_log2, float v_scale) {
+    int bs_log2, float scale_log2, float v_scale, int num_blocks) {
   typedef typename Vec8<T>::type V8;
   typedef std::conditional_t<KV8, uint8_t, T> C;   // cache element
   typedef std::conditional_t<KV8, u32x2, u32x4> R; // staged raw fragment (8 elements)
@@ -63,7 +63,9 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
   const int h = hq / (nq / nkv);
   const int q0 = qsl[seq];
   const int qlen = qsl[seq + 1] - q0;
-  const int L = min(seq_lens[seq], bt_stride << bs_log2);  // never index past the table
+  int L_in = seq_lens[seq];
+  KGC_DCHECK_RANGE(L_in, 0, (bt_stride << bs_log2) + 1, "prefill seq_len");
+  const int L = min(L_in, bt_stride << bs_log2);  // never index past the table
   const int ctx0 = L - qlen;
   if (qlen <= 0 || ctx0 < 0) return;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -97,7 +99,7 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
       const int ci = threadIdx.x + 256 * u;
       const int key = ci / NCH, c = ci % NCH;
       const int ka = min(kt * PF_BN + key, L - 1);
-      const C* src = kc + (int64_t)bt[ka >> bs_log2] * nkv * hs + h * hs +
+      const C* src = kc + (int64_t)kgc_bt(bt, ka >> bs_log2, bt_stride, num_blocks) * nkv * hs + h * hs +
                      (int64_t)(ka & bsm) * D + c * 8;
       kreg[u] = *reinterpret_cast<const R*>(src);
     }
@@ -106,7 +108,7 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
       const int ci = threadIdx.x + 256 * u;
       const int c = ci / D, d = ci % D;
       const int ka = min(kt * PF_BN + 8 * c, L - 1) & ~7;
-      const C* src = vc + (int64_t)bt[ka >> bs_log2] * nkv * hs + h * hs +
+      const C* src = vc + (int64_t)kgc_bt(bt, ka >> bs_log2, bt_stride, num_blocks) * nkv * hs + h * hs +
                      ((ka & bsm) >> 3) * (D * 8) + d * 8;
       vreg[u] = *reinterpret_cast<const R*>(src);
     }
@@ -240,11 +242,12 @@ template <typename T, int D, bool KV8>
 static void prefill_dispatch(const void* q, void* out, const void* kc, const void* vc,
                              const int* bt, int bt_stride, const int* qsl, const int* sl,
                              const int* ws, const int* wm, int n_work, int nq, int nkv,
-                             int bs_log2, float scale_log2, float v_scale, hipStream_t s) {
+                             int bs_log2, float scale_log2, float v_scale, int num_blocks,
+                             hipStream_t s) {
   const size_t lds = 2 * 2 * PF_BN * D * sizeof(T);
   prefill_attn_kernel<T, D, KV8><<<dim3(n_work, nq), 256, lds, s>>>(
       (const T*)q, (T*)out, kc, vc, bt, bt_stride, qsl, sl, ws, wm, nq,
-      nkv, bs_log2, scale_log2, v_scale);
+      nkv, bs_log2, scale_log2, v_scale, num_blocks);
 }
 
 void launch_prefill_attention(int dtype, const void* q, void* out, const void* k_cache,
@@ -252,13 +255,13 @@ void launch_prefill_attention(int dtype, const void* q, void* out, const void* k
                               const int* query_start_loc, const int* seq_lens,
                               const int* work_seq, const int* work_mblk, int n_work, int nq,
                               int nkv, int D, int bs_log2, float scale, bool kv_fp8,
-                              float k_scale, float v_scale, hipStream_t s) {
+                              float k_scale, float v_scale, int num_blocks, hipStream_t s) {
   if (n_work == 0) return;
   const float sl2 = scale * k_scale * 1.4426950408889634f;
 #define KGC_PF(TT, DD, K8)                                                                 \
   prefill_dispatch<TT, DD, K8>(q, out, k_cache, v_cache, block_tables, bt_stride,          \
                                query_start_loc, seq_lens, work_seq, work_mblk, n_work, nq, \
-                               nkv, bs_log2, sl2, v_scale, s)
+                               nkv, bs_log2, sl2, v_scale, num_blocks, s)
 #define KGC_PF_D(TT, K8) \
   if (D == 128) KGC_PF(TT, 128, K8); else KGC_PF(TT, 64, K8)
   if (dtype == DT_BF16) {
@@ -271,5 +274,7 @@ void launch_prefill_attention(int dtype, const void* q, void* out, const void* k
 }
 
 int prefill_block_m() { return PF_BM; }
+
+KGC_DEBUG_TU(attention_prefill)
 
 }  // namespace kgc

@@ -139,4 +139,48 @@ __device__ __forceinline__ u32x4 ld_frag8(const void* base, int64_t elem) {
     return *reinterpret_cast<const u32x4*>(reinterpret_cast<const T*>(base) + elem);
 }
 
+
+// ---- debug build (KGC_HIP_DEBUG=1 python csrc/build.py -> _kgc_ops_debug.so): device-side
+// bounds checks of the indices the attention / KV-write kernels take from the host
+// (block tables, slot mapping, context lengths).  A failed check prints once, sets the
+// translation unit's sticky error word (read by kgc.debug_errors(), which raises on the
+// host) and CLAMPS the index to a valid value -- never a trap, never an out-of-bounds
+// access.  In release builds the checks compile to nothing.
+#ifdef KGC_DEBUG
+static __device__ unsigned int kgc_dbg_err;
+#define KGC_DEBUG_TU(name)                                                   \
+  uint32_t dbg_err_##name() {                                                \
+    unsigned int v = 0, z = 0;                                               \
+    (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(kgc_dbg_err), sizeof(v));       \
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(kgc_dbg_err), &z, sizeof(z));         \
+    return v;                                                                \
+  }
+#define KGC_DCHECK_RANGE(v, lo, hi, what)                                                     \
+  do {                                                                                        \
+    if ((long long)(v) < (long long)(lo) || (long long)(v) >= (long long)(hi)) {              \
+      if (atomicOr(&kgc_dbg_err, 1u) == 0u)                                                   \
+        printf("kgc debug check: %s = %lld not in [%lld, %lld) at %s:%d (wg %d,%d,%d t %d)\n", \
+               what, (long long)(v), (long long)(lo), (long long)(hi), __FILE__, __LINE__,   \
+               (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z, (int)threadIdx.x);         \
+      (v) = (lo);                                                                             \
+    }                                                                                         \
+  } while (0)
+#else
+#define KGC_DEBUG_TU(name) \
+  uint32_t dbg_err_##name() { return 0; }
+#define KGC_DCHECK_RANGE(v, lo, hi, what) \
+  do {                                    \
+  } while (0)
+#endif
+
+// block-table entry i of a sequence's row (debug: column and block id range-checked)
+__device__ __forceinline__ int kgc_bt(const int* bt, int i, int bt_stride, int num_blocks) {
+  KGC_DCHECK_RANGE(i, 0, bt_stride, "block-table column");
+  int v = bt[i];
+  KGC_DCHECK_RANGE(v, 0, num_blocks, "block id");
+  (void)bt_stride;
+  (void)num_blocks;
+  return v;
+}
+
 }  // namespace kgc

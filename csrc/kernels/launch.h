@@ -19,20 +19,25 @@ void launch_rope_kv_write(int dtype, const void* qkv, int64_t qkv_stride, int S,
                           void* k_cache, void* v_cache, const int64_t* slot_mapping,
                           const void* q_norm_w, const void* k_norm_w, int T, int nq, int nkv,
                           int d, int bs, float eps, bool use_rope, bool kv_fp8, float k_scale,
-                          float v_scale, hipStream_t s);
+                          float v_scale, int num_blocks, hipStream_t s);
 void launch_paged_decode(int dtype, void* out, const void* q, const void* k_cache,
                          const void* v_cache, const int* block_tables, int bt_stride,
                          const int* ctx_lens, float* max_logits, float* exp_sums,
                          float* tmp_out, int B, int nq, int nkv, int D, int bs_log2,
                          int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
-                         float v_scale, hipStream_t s);
+                         float v_scale, int num_blocks, hipStream_t s);
 int paged_decode_partition_size();
 void launch_prefill_attention(int dtype, const void* q, void* out, const void* k_cache,
                               const void* v_cache, const int* block_tables, int bt_stride,
                               const int* query_start_loc, const int* seq_lens,
                               const int* work_seq, const int* work_mblk, int n_work, int nq,
                               int nkv, int D, int bs_log2, float scale, bool kv_fp8,
-                              float k_scale, float v_scale, hipStream_t s);
+                              float k_scale, float v_scale, int num_blocks, hipStream_t s);
+// debug builds: sticky bounds-check error words of the K1 / K2 / K3 translation units
+// (read and cleared; always 0 in release builds)
+uint32_t dbg_err_attention_decode();
+uint32_t dbg_err_attention_prefill();
+uint32_t dbg_err_rope_cache();
 int prefill_block_m();
 int sample_splits(int B);   // vocabulary splits per row; partial holds B * splits words
 void launch_sample(int dtype, int64_t* out, uint64_t* partial, const void* logits,
@@ -101,6 +106,12 @@ size_t allreduce_signal_bytes();
 int allreduce_max_blocks();
 void launch_allreduce(int dtype, const ArPtrs& P, int nranks, int rank, void* inout,
                       int64_t nvec, int64_t cap_vec, bool two_shot, hipStream_t s);
+// fused one-shot all-reduce + residual add + RMSNorm over [M, H] rows (P.data: the
+// fused regions); H % 8 == 0 and H <= allreduce_rms_max_hidden()
+int allreduce_rms_max_hidden();
+void launch_allreduce_rms(int dtype, const ArPtrs& P, int nranks, int rank, const void* in,
+                          void* out, void* residual, const void* w, int M, int H, float eps,
+                          int64_t cap_vec, hipStream_t s);
 void* ar_alloc(int64_t bytes);
 void ar_free(void* p);
 void ar_get_handle(void* p, uint8_t* out64);

@@ -48,7 +48,7 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
     const float* __restrict__ cos_sin, T* __restrict__ q_out, void* __restrict__ k_cache,
     void* __restrict__ v_cache, const int64_t* __restrict__ slot_mapping,
     const T* __restrict__ qn_w, const T* __restrict__ kn_w, int nq, int nkv, int d, int bs,
-    float eps, float k_inv, float v_inv) {
+    float eps, float k_inv, float v_inv, int num_blocks) {
   // item space of one token: [q/k rotation items, padded to a wave] [v scatter items];
   // gridDim.y workgroups of ROPE_NT items share a token (fills the CUs at decode).
   const int t = blockIdx.x;
@@ -57,7 +57,8 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
   const int n_qk = (nq + nkv) * tph;
   const int n_qk_pad = (n_qk + 63) & ~63;
   const int it = blockIdx.y * ROPE_NT + threadIdx.x;
-  const int64_t slot = slot_mapping[t];
+  int64_t slot = slot_mapping[t];
+  KGC_DCHECK_RANGE(slot, -1, (int64_t)num_blocks * bs, "KV slot");   // -1: no KV write
   const int64_t row = (int64_t)t * qkv_stride;   // element offset of this token's row
   const int64_t blk = slot >= 0 ? slot / bs : 0;
   const int off = slot >= 0 ? (int)(slot % bs) : 0;
@@ -169,14 +170,14 @@ static void rope_dispatch(const void* qkv, int64_t qkv_stride, int S, int64_t ss
                           const float* cs, void* q_out, void* kc, void* vc,
                           const int64_t* slots, const void* qn, const void* kn, int T_,
                           int nq, int nkv, int d, int bs, float eps, bool rope, float k_inv,
-                          float v_inv, hipStream_t s) {
+                          float v_inv, int num_blocks, hipStream_t s) {
   if (T_ == 0) return;
   const int n_items = (((nq + nkv) * (d >> 4) + 63) & ~63) + nkv * (d >> 3);
   const dim3 grid(T_, (n_items + ROPE_NT - 1) / ROPE_NT);
 #define KGC_ROPE_LAUNCH(N, R)                                                               \
   rope_kv_kernel<T, N, R, KV8, SL><<<grid, ROPE_NT, 0, s>>>(                                \
       qkv, qkv_stride, S, ss, pos, cs, (T*)q_out, kc, vc, slots, (const T*)qn,               \
-      (const T*)kn, nq, nkv, d, bs, eps, k_inv, v_inv)
+      (const T*)kn, nq, nkv, d, bs, eps, k_inv, v_inv, num_blocks)
   const bool norm = qn != nullptr;
   if (norm && rope) KGC_ROPE_LAUNCH(true, true);
   else if (norm) KGC_ROPE_LAUNCH(true, false);
@@ -190,13 +191,13 @@ static void rope_dispatch_sl(const void* qkv, int64_t qkv_stride, int S, int64_t
                              const int64_t* pos, const float* cs, void* q_out, void* kc, void* vc,
                              const int64_t* slots, const void* qn, const void* kn, int T_,
                              int nq, int nkv, int d, int bs, float eps, bool rope, float k_inv,
-                             float v_inv, hipStream_t s) {
+                             float v_inv, int num_blocks, hipStream_t s) {
   if (S > 0)
     rope_dispatch<T, KV8, true>(qkv, qkv_stride, S, ss, pos, cs, q_out, kc, vc, slots, qn, kn,
-                                T_, nq, nkv, d, bs, eps, rope, k_inv, v_inv, s);
+                                T_, nq, nkv, d, bs, eps, rope, k_inv, v_inv, num_blocks, s);
   else
     rope_dispatch<T, KV8, false>(qkv, qkv_stride, 0, 0, pos, cs, q_out, kc, vc, slots, qn, kn,
-                                 T_, nq, nkv, d, bs, eps, rope, k_inv, v_inv, s);
+                                 T_, nq, nkv, d, bs, eps, rope, k_inv, v_inv, num_blocks, s);
 }
 
 void launch_rope_kv_write(int dtype, const void* qkv, int64_t qkv_stride, int S,
@@ -205,27 +206,29 @@ void launch_rope_kv_write(int dtype, const void* qkv, int64_t qkv_stride, int S,
                           const int64_t* slot_mapping, const void* q_norm_w,
                           const void* k_norm_w, int T, int nq, int nkv, int d, int bs,
                           float eps, bool use_rope, bool kv_fp8, float k_scale, float v_scale,
-                          hipStream_t s) {
+                          int num_blocks, hipStream_t s) {
   const float ki = 1.f / k_scale, vi = 1.f / v_scale;
   if (dtype == DT_BF16) {
     if (kv_fp8)
       rope_dispatch_sl<bf16, true>(qkv, qkv_stride, S, slice_stride, positions, cos_sin, q_out,
                                    k_cache, v_cache, slot_mapping, q_norm_w, k_norm_w, T, nq,
-                                   nkv, d, bs, eps, use_rope, ki, vi, s);
+                                   nkv, d, bs, eps, use_rope, ki, vi, num_blocks, s);
     else
       rope_dispatch_sl<bf16, false>(qkv, qkv_stride, S, slice_stride, positions, cos_sin, q_out,
                                     k_cache, v_cache, slot_mapping, q_norm_w, k_norm_w, T, nq,
-                                    nkv, d, bs, eps, use_rope, ki, vi, s);
+                                    nkv, d, bs, eps, use_rope, ki, vi, num_blocks, s);
   } else {
     if (kv_fp8)
       rope_dispatch_sl<f16, true>(qkv, qkv_stride, S, slice_stride, positions, cos_sin, q_out,
                                   k_cache, v_cache, slot_mapping, q_norm_w, k_norm_w, T, nq,
-                                  nkv, d, bs, eps, use_rope, ki, vi, s);
+                                  nkv, d, bs, eps, use_rope, ki, vi, num_blocks, s);
     else
       rope_dispatch_sl<f16, false>(qkv, qkv_stride, S, slice_stride, positions, cos_sin, q_out,
                                    k_cache, v_cache, slot_mapping, q_norm_w, k_norm_w, T, nq,
-                                   nkv, d, bs, eps, use_rope, ki, vi, s);
+                                   nkv, d, bs, eps, use_rope, ki, vi, num_blocks, s);
   }
 }
+
+KGC_DEBUG_TU(rope_cache)
 
 }  // namespace kgc

@@ -379,6 +379,8 @@ class ModelRunner:
     @torch.inference_mode()
     def run(self, plan: StepPlan) -> Optional[torch.Tensor]:
         """Execute one step on this rank.  Returns sampled ids [S] (last PP stage)."""
+        if ops.DEBUG and self.is_gpu:
+            ops.debug_check()           # the previous step's kernels (bounds-checking build)
         self._upload(plan)
         L = self.L
         ps = self.ps

@@ -37,6 +37,8 @@ def pp_layer_range(num_layers: int, pp_size: int, pp_rank: int) -> tuple[int, in
 
 
 _tail_fusion_enabled = os.environ.get("KGC_TAIL_FUSION", "1") != "0"
+# TP > 1: all-reduce fused with the residual add + RMSNorm after o / down (KGC_TP_AR_NORM=0: off)
+_tp_ar_norm_enabled = os.environ.get("KGC_TP_AR_NORM", "1") != "0"
 
 
 class RMSNorm(nn.Module):
@@ -168,6 +170,8 @@ class LlamaForCausalLM(nn.Module):
         x = self.embed_tokens(input_ids) if self.first else hidden
         if self._tail_fusable(x):
             return self._forward_tail_fused(positions, x, ctx)
+        if self._tp_tail_fusable():
+            return self._forward_tp_fused(positions, x, ctx)
         for layer in self.layers:
             x, residual = layer(positions, x, residual, ctx)
         if not self.last:
@@ -209,6 +213,39 @@ class LlamaForCausalLM(nn.Module):
             prev = layer
         x, _ = gemm.linear_add_rms(h, prev.mlp.down_proj.weight, residual, self.norm.weight,
                                    self.norm.eps)
+        return x
+
+    def _tp_tail_fusable(self) -> bool:
+        """TP > 1, whole model, dense bias-free o / down projections: each row-parallel
+        projection's all-reduce runs fused with the residual add + RMSNorm that consumes
+        it (``comm.tp_all_reduce_add_rms``: the xGMI kernel at decode sizes)."""
+        if not (get_state().tp_size > 1 and self.first and self.last and self.layers
+                and not self.cfg.is_moe and _tp_ar_norm_enabled):
+            return False
+        l0 = self.layers[0]
+        return l0.self_attn.o_proj.bias is None and l0.mlp.down_proj.bias is None
+
+    def _forward_tp_fused(self, positions, x, ctx):
+        """``LlamaDecoderLayer.forward`` at TP > 1 with the o / down all-reduces handed to
+        the norms that consume them: o_proj -> post-attention norm, down_proj -> the next
+        layer's input norm (the last one -> the final norm).  Same math and rounding."""
+        residual, h, prev = x, None, None
+        for layer in self.layers:
+            ln1 = layer.input_layernorm
+            if prev is None:
+                x = ln1(x)
+            else:
+                x, residual = comm.tp_all_reduce_add_rms(
+                    gemm.linear(h, prev.mlp.down_proj.weight), residual, ln1.weight, ln1.eps)
+            at, ln2 = layer.self_attn, layer.post_attention_layernorm
+            a = at.attend(positions, at.project_qkv(x), ctx)
+            x, residual = comm.tp_all_reduce_add_rms(gemm.linear(a, at.o_proj.weight), residual,
+                                                     ln2.weight, ln2.eps)
+            gu = layer.mlp.gate_up_proj
+            h = gemm.linear_silu(x, gu.weight, gu.bias)
+            prev = layer
+        x, _ = comm.tp_all_reduce_add_rms(gemm.linear(h, prev.mlp.down_proj.weight), residual,
+                                          self.norm.weight, self.norm.eps)
         return x
 
     # ------------------------------------------------------------------ fused small-M decode

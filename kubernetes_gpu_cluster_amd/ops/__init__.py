@@ -15,7 +15,10 @@ import torch
 
 from . import reference as ref
 
-_SO = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_kgc_ops.so")
+# KGC_HIP_DEBUG=1: the bounds-checking build (``KGC_HIP_DEBUG=1 python csrc/build.py``)
+DEBUG = os.environ.get("KGC_HIP_DEBUG", "0") not in ("", "0")
+_SO = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                   "_kgc_ops_debug.so" if DEBUG else "_kgc_ops.so")
 _loaded: Optional[bool] = None
 _load_err: Optional[str] = None
 
@@ -38,6 +41,24 @@ def load_extension(strict: bool = False) -> bool:
 
 def extension_path() -> str:
     return _SO
+
+
+class KernelDebugCheckFailed(RuntimeError):
+    """A debug-build kernel read an out-of-range block-table entry, slot or length."""
+
+
+def debug_check() -> None:
+    """Debug build: raise if any K1/K2/K3 bounds check tripped since the last call (the
+    kernel printed the offending value and clamped it).  No-op in release builds."""
+    if not DEBUG or not load_extension():
+        return
+    torch.cuda.synchronize()
+    err = int(torch.ops.kgc.debug_errors())
+    if err:
+        which = [n for b, n in ((1, "paged decode (K1)"), (2, "prefill attention (K2)"),
+                                (4, "rope / KV write (K3)")) if err & b]
+        raise KernelDebugCheckFailed(f"device bounds check failed in {', '.join(which)}; "
+                                     f"see the kernel's printf above")
 
 
 def _k():

@@ -39,6 +39,18 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
+def tp_all_reduce_add_rms(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
+                          eps: float) -> tuple[torch.Tensor, torch.Tensor]:
+    """Row-parallel projection output -> (rms_norm(residual + sum_ranks x) * w, residual),
+    residual updated in place: the fused xGMI kernel when the rows fit its one-shot
+    size, else all-reduce + fused_add_rms_norm (identical rounding either way)."""
+    from .. import ops
+    car = _custom_ar
+    if car is not None and get_state().tp_size > 1 and car.can_fuse(x):
+        return car.all_reduce_add_rms(x, residual, w, eps)
+    return ops.fused_add_rms_norm(tp_all_reduce(x), residual, w, eps)
+
+
 def tp_all_reduce_max(x: torch.Tensor) -> torch.Tensor:
     """In-place MAX over the TP group (vocab-parallel sampling: 8 bytes per row)."""
     s = get_state()

@@ -61,7 +61,8 @@ class CustomAllReduce:
             k = torch.ops.kgc
             with torch.cuda.device(device):
                 sig_bytes = int(k.ar_signal_bytes())
-                self._own = int(k.ar_alloc(sig_bytes + 2 * self.cap))
+                # [signal | all-reduce parity 0 | parity 1 | fused parity 0 | parity 1]
+                self._own = int(k.ar_alloc(sig_bytes + 4 * self.cap))
                 handle = k.ar_get_handle(self._own).tolist()
         except Exception as e:  # noqa: BLE001
             err = e
@@ -87,6 +88,12 @@ class CustomAllReduce:
             raise RuntimeError(f"xGMI all-reduce peer mapping failed: {err}")
         self.sig = bases
         self.data = [b + sig_bytes for b in bases]
+        self.fdata = [b + sig_bytes + 2 * self.cap for b in bases]
+        # fused all-reduce + add + RMSNorm: one-shot, so the sizes where the plain
+        # all-reduce would be one-shot too (larger rows: two-shot + fused_add_rms_norm)
+        self.fused_max = int(os.environ.get("KGC_AR_RMS_MAX", self.one_shot_max))
+        self.max_hidden = int(k.allreduce_rms_max_hidden())
+        self.fused_calls = 0        # host-side launches (a graph capture counts once)
 
     def should_use(self, x: torch.Tensor) -> bool:
         if not x.is_cuda or x.dtype not in (torch.bfloat16, torch.float16):
@@ -99,6 +106,25 @@ class CustomAllReduce:
         torch.ops.kgc.xgmi_allreduce(x, self.data, self.sig, self.rank, self.cap,
                                      nb > self.one_shot_max)
         return x
+
+    def can_fuse(self, x: torch.Tensor) -> bool:
+        if not x.is_cuda or x.dtype not in (torch.bfloat16, torch.float16) or x.dim() != 2:
+            return False
+        H = x.shape[1]
+        nb = x.numel() * x.element_size()
+        return (x.is_contiguous() and 0 < nb <= min(self.fused_max, self.cap) and H % 8 == 0
+                and H <= self.max_hidden)
+
+    def all_reduce_add_rms(self, x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
+                           eps: float, out: torch.Tensor = None):
+        """One launch: h = sum over ranks of x; residual += h; out = rms_norm(residual) * w
+        (same rounding as all_reduce + fused_add_rms_norm).  Returns (out, residual)."""
+        if out is None:
+            out = torch.empty_like(x)
+        self.fused_calls += 1
+        torch.ops.kgc.xgmi_allreduce_rms(out, x, residual, w, eps, self.fdata, self.sig,
+                                         self.rank, self.cap)
+        return out, residual
 
     def check(self) -> None:
         """Raise if any barrier timed out waiting for a peer (see allreduce.hip)."""

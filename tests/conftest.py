@@ -23,3 +23,13 @@ def gpu():
     from kubernetes_gpu_cluster_amd import ops
     ops.load_extension(strict=True)   # GPU tests must exercise the native path
     return torch.device("cuda:0")
+
+
+@pytest.fixture(autouse=True)
+def _kernel_debug_check(request):
+    """Under KGC_HIP_DEBUG=1 (the bounds-checking build), fail any GPU test after which
+    a K1/K2/K3 device check tripped."""
+    yield
+    if os.environ.get("KGC_HIP_DEBUG", "0") not in ("", "0") and "gpu" in request.fixturenames:
+        from kubernetes_gpu_cluster_amd import ops
+        ops.debug_check()

@@ -123,3 +123,77 @@ def test_xgmi_allreduce_peer_timeout_raises(gpu):
     step's tokens are read, engine/worker.py) raises AllReduceFailed."""
     mp.start_processes(_timeout_worker, args=(2, _port()), nprocs=2, join=True,
                        start_method="spawn")
+
+
+def _rms_worker(rank, world, port):
+    """Fused all-reduce + residual add + RMSNorm == xgmi all-reduce then fused_add_rms_norm,
+    interleaved with plain all-reduces (separate IPC regions), eager and graph-captured."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from kubernetes_gpu_cluster_amd import ops
+    from kubernetes_gpu_cluster_amd.parallel.custom_allreduce import CustomAllReduce
+    dev = torch.device("cuda", 0)
+    car = CustomAllReduce(dist.group.WORLD, rank, world, dev, cap_bytes=4 << 20,
+                          one_shot_max=4 << 20)
+    try:
+        for dtype in (torch.bfloat16, torch.float16):
+            for M, H in ((1, 4096), (7, 8192), (130, 4096), (64, 16384), (3, 1024)):
+                g = torch.Generator().manual_seed(M * 31 + H + rank)
+                x = (torch.randn(M, H, generator=g) * 0.5).to(dtype).to(dev)
+                gres = torch.Generator().manual_seed(M * 7 + H)         # same on every rank
+                res = torch.randn(M, H, generator=gres).to(dtype).to(dev)
+                w = (torch.rand(H, generator=gres) + 0.5).to(dtype).to(dev)
+                assert car.can_fuse(x), (M, H)
+                r_got = res.clone()
+                o_got, _ = car.all_reduce_add_rms(x, r_got, w, 1e-5)
+                if H <= 8192:    # unfused reference on the same GPU (rms_norm: H <= 8192)
+                    y = x.clone()
+                    car.all_reduce(y)
+                    r_ref = res.clone()
+                    o_ref, _ = ops.fused_add_rms_norm(y, r_ref, w, 1e-5)
+                    assert torch.equal(r_got, r_ref), (M, H, dtype)
+                    torch.testing.assert_close(o_got.float(), o_ref.float(), atol=1e-2, rtol=1e-2)
+                # an fp32 oracle of the whole op
+                xs = [(torch.randn(M, H, generator=torch.Generator().manual_seed(M * 31 + H + r))
+                       * 0.5).to(dtype).float() for r in range(world)]
+                h = sum(xs).to(dtype).float()
+                rr = (h + res.cpu().float()).to(dtype).float()
+                oo = rr * torch.rsqrt(rr.pow(2).mean(-1, keepdim=True) + 1e-5) * w.cpu().float()
+                torch.testing.assert_close(o_got.cpu().float(), oo, atol=3e-2, rtol=3e-2)
+        # graph capture: fused + plain all-reduce in one graph, replays with fresh inputs
+        M, H = 16, 4096
+        xin = torch.zeros(M, H, dtype=torch.bfloat16, device=dev)
+        res = torch.zeros(M, H, dtype=torch.bfloat16, device=dev)
+        w = torch.ones(H, dtype=torch.bfloat16, device=dev)
+        plain = torch.zeros(8192, dtype=torch.bfloat16, device=dev)
+        car.all_reduce_add_rms(xin, res, w, 1e-5)
+        car.all_reduce(plain)
+        torch.cuda.synchronize()
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            out, _ = car.all_reduce_add_rms(xin, res, w, 1e-5)
+            car.all_reduce(plain)
+        for it in range(3):
+            xin.copy_(torch.full((M, H), float(rank + it + 1), dtype=torch.bfloat16))
+            res.zero_()
+            plain.fill_(float(rank + 1))
+            gr.replay()
+            torch.cuda.synchronize()
+            tot = sum(r + it + 1 for r in range(world))
+            assert torch.equal(res.cpu(), torch.full((M, H), float(tot), dtype=torch.bfloat16)), it
+            torch.testing.assert_close(out.float().cpu(), torch.ones(M, H), atol=1e-2, rtol=0)
+            assert torch.equal(plain.cpu(), torch.full((8192,), float(sum(range(1, world + 1))),
+                                                       dtype=torch.bfloat16))
+        car.check()
+        dist.barrier()
+    finally:
+        car.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_allreduce_add_rmsnorm_fused(world, gpu):
+    mp.start_processes(_rms_worker, args=(world, _port()), nprocs=world, join=True,
+                       start_method="spawn")

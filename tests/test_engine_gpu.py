@@ -179,6 +179,7 @@ def test_tp2_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch, eager):
         outs[tp] = [o.output_token_ids for o in llm.generate(prompts, sp)]
         if tp == 2:
             car.check()
+            assert car.fused_calls > 0, "fused all-reduce + add + RMSNorm never ran"
             st = llm.engine.executor.runner.stats
             assert st["vp_steps"] > 0, st
             if not eager:
