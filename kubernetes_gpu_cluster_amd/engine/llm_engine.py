@@ -19,7 +19,7 @@ from ..models import resolve_model
 from ..utils.metrics import EngineMetrics
 from .block_manager import BlockManager
 from .config import EngineConfig
-from .scheduler import Scheduler
+from .scheduler import Scheduler, VirtualSchedulers
 from .sequence import RequestOutput, SamplingParams, SeqStatus, Sequence
 from .worker import TokenFuture, LocalExecutor, MultiprocExecutor, default_max_model_len
 
@@ -86,8 +86,17 @@ class LLMEngine:
         runner = executor.runner
         self.bm = BlockManager(nb, cfg.block_size, cfg.max_num_seqs, runner.max_blocks,
                                enable_prefix_caching=cfg.enable_prefix_caching)
-        self.scheduler = Scheduler(self.bm, cfg.max_num_seqs, cfg.token_budget(),
-                                   self.max_model_len, cfg.enable_chunked_prefill)
+        # PP > 1: one micro-batch per stage in flight (engine/scheduler.VirtualSchedulers)
+        self.pp_depth = int(getattr(executor, "pipeline_depth", 1))
+        if self.pp_depth > 1:
+            self.scheduler = VirtualSchedulers(self.pp_depth, self.bm, cfg.max_num_seqs,
+                                               cfg.token_budget(), self.max_model_len,
+                                               cfg.enable_chunked_prefill)
+        else:
+            self.scheduler = Scheduler(self.bm, cfg.max_num_seqs, cfg.token_budget(),
+                                       self.max_model_len, cfg.enable_chunked_prefill)
+        self._pp_inflight: list = [None] * self.pp_depth
+        self._vnext = 0
         self.seqs: dict[str, Sequence] = {}
         self._ids = itertools.count()
         self.metrics = EngineMetrics()
@@ -125,7 +134,8 @@ class LLMEngine:
             self.metrics.on_finish(s)
 
     def has_unfinished(self) -> bool:
-        return self.scheduler.has_work() or self._inflight is not None
+        return (self.scheduler.has_work() or self._inflight is not None
+                or any(x is not None for x in self._pp_inflight))
 
     # ------------------------------------------------------------------ step
     def step(self) -> list[RequestOutput]:
@@ -139,6 +149,8 @@ class LLMEngine:
             self.bm.check_invariants(list(self.scheduler.running))
         if self._prof is not None:
             self._prof.tick()
+        if self.pp_depth > 1:
+            return self._step_pipelined()
         if not self.async_mode:
             return self._step_sync()
         launched = None
@@ -148,26 +160,49 @@ class LLMEngine:
             plan, samplers = self.executor.runner.build_plan(batch.prefills, batch.decodes,
                                                              self.bm.table, device_tokens=True)
             fut = self.executor.execute_async(plan)
-            for seq, n in batch.prefills:
-                seq.num_computed += n
-            for seq in batch.decodes:
-                seq.num_computed += 1
-            for seq in samplers:
-                seq.output_token_ids.append(_PENDING)
-                seq.num_pending += 1
-            if self.bm.prefix_caching:      # publish blocks whose token ids are all known
-                for seq, _ in batch.prefills:
-                    self.bm.register_full_blocks(seq, seq.num_tokens - seq.num_pending)
-            for seq in samplers:
-                if len(seq.output_token_ids) >= seq.max_tokens or seq.num_tokens >= self.max_model_len:
-                    # finished by length: release now (stream order protects the KV
-                    # blocks still being written by the in-flight step)
-                    self.scheduler.finish(seq, "length")
-                    self.seqs.pop(seq.request_id, None)
-            launched = (fut, samplers, plan, t0, len(batch.preempted))
+            launched = self._launched(batch, plan, samplers, fut, t0)
         outs = self._process(self._inflight) if self._inflight is not None else []
         self._inflight = launched
         return outs
+
+    def _step_pipelined(self) -> list[RequestOutput]:
+        """PP > 1: micro-batch v = this step's turn.  Its previous step's tokens are read
+        first (they left the last stage while the other micro-batches ran), then its next
+        step is scheduled and handed to stage 0, and the call returns without waiting."""
+        v = self._vnext
+        self._vnext = (v + 1) % self.pp_depth
+        outs: list[RequestOutput] = []
+        if self._pp_inflight[v] is not None:
+            outs = self._process(self._pp_inflight[v])
+            self._pp_inflight[v] = None
+        batch = self.scheduler.schedule_v(v)
+        if not batch.is_empty:
+            t0 = time.monotonic()
+            plan, samplers = self.executor.runner.build_plan(batch.prefills, batch.decodes,
+                                                             self.bm.table)
+            fut = self.executor.execute_pipelined(plan)
+            self._pp_inflight[v] = self._launched(batch, plan, samplers, fut, t0)
+        return outs
+
+    def _launched(self, batch, plan, samplers, fut, t0):
+        """Host bookkeeping of a step handed to the device before its tokens are known."""
+        for seq, n in batch.prefills:
+            seq.num_computed += n
+        for seq in batch.decodes:
+            seq.num_computed += 1
+        for seq in samplers:
+            seq.output_token_ids.append(_PENDING)
+            seq.num_pending += 1
+        if self.bm.prefix_caching:      # publish blocks whose token ids are all known
+            for seq, _ in batch.prefills:
+                self.bm.register_full_blocks(seq, seq.num_tokens - seq.num_pending)
+        for seq in samplers:
+            if len(seq.output_token_ids) >= seq.max_tokens or seq.num_tokens >= self.max_model_len:
+                # finished by length: release now (stream order protects the KV
+                # blocks still being written by the in-flight step)
+                self.scheduler.finish(seq, "length")
+                self.seqs.pop(seq.request_id, None)
+        return (fut, samplers, plan, t0, len(batch.preempted))
 
     def _process(self, inflight) -> list[RequestOutput]:
         fut, samplers, plan, t0, npre = inflight

@@ -141,6 +141,10 @@ class ModelRunner:
         self._tok_flip = 0
         self.stats = {"graph_steps": 0, "eager_steps": 0, "vp_steps": 0,
                       "tp_allreduce_bytes": 0, "tp_logits_bytes": 0}
+        # KGC_FAKE_STAGE_MS: every step of this rank is a sleep of that many ms with the
+        # real pipeline-stage traffic around it (PP scheduling / utilisation tests)
+        self._fake_ms = float(os.environ.get("KGC_FAKE_STAGE_MS", "0") or 0)
+        self.stage_stats = {"busy_s": 0.0, "t_first": None, "t_last": None, "steps": 0}
         # vocab-parallel sampling (TP > 1): every rank keeps its logits shard; rows
         # without top-k / top-p / processors / logprobs are sampled by an 8-byte-per-row
         # MAX all-reduce instead of an all-gather of B x V logits (ops.sample_vp_partial)
@@ -381,6 +385,8 @@ class ModelRunner:
         """Execute one step on this rank.  Returns sampled ids [S] (last PP stage)."""
         if ops.DEBUG and self.is_gpu:
             ops.debug_check()           # the previous step's kernels (bounds-checking build)
+        if self._fake_ms:
+            return self._run_fake(plan)
         self._upload(plan)
         L = self.L
         ps = self.ps
@@ -440,6 +446,33 @@ class ModelRunner:
         else:
             self._last_lp = None
         return res
+
+    def _run_fake(self, plan: StepPlan) -> Optional[torch.Tensor]:
+        shp = (plan.B or plan.T, self.mcfg.hidden_size)
+        if not self.model.first:
+            comm.pp_recv([shp, shp], self.dtype, self.device)
+        t0 = time.monotonic()
+        time.sleep(self._fake_ms * 1e-3)
+        t1 = time.monotonic()
+        st = self.stage_stats
+        st["busy_s"] += t1 - t0
+        st["t_first"] = t0 if st["t_first"] is None else st["t_first"]
+        st["t_last"] = t1
+        st["steps"] += 1
+        if not self.model.last:
+            z = torch.zeros(shp, dtype=self.dtype, device=self.device)
+            comm.pp_send([z, z])
+            return None
+        return torch.full((plan.S,), 7, dtype=torch.int64, device=self.device)
+
+    def write_stage_stats(self) -> None:
+        """KGC_STAGE_STATS_DIR: this rank's fake-stage busy time and span (JSON)."""
+        d = os.environ.get("KGC_STAGE_STATS_DIR")
+        if not d or not self.stage_stats["steps"]:
+            return
+        import json
+        with open(os.path.join(d, f"rank{torch.distributed.get_rank()}.json"), "w") as f:
+            json.dump(dict(self.stage_stats, pp_rank=self.ps.pp_rank), f)
 
     def _sample_vp(self, local: torch.Tensor, plan: StepPlan) -> torch.Tensor:
         S, L = plan.S, self.L

@@ -140,3 +140,56 @@ class Scheduler:
             self.running.remove(seq)
         except ValueError:
             pass
+
+
+class VirtualSchedulers:
+    """Pipeline parallelism: one scheduler per micro-batch ("virtual engine") over the
+    shared KV pool.  The engine launches micro-batch v's step, then v+1's, ... and only
+    returns to v once v's tokens are back from the last stage, so with ``pp_size``
+    micro-batches every stage has work (vLLM's virtual-engine scheme).  A sequence stays
+    in the micro-batch it was admitted to (``seq.vengine``); new requests go to the one
+    with the fewest sequences.  Each holds at most ``max_num_seqs // n`` sequences, and
+    each step still has the full token budget."""
+
+    def __init__(self, n: int, block_manager: BlockManager, max_num_seqs: int, token_budget: int,
+                 max_model_len: int, chunked_prefill: bool = True):
+        per = max(1, max_num_seqs // n)
+        self.scheds = [Scheduler(block_manager, per, token_budget, max_model_len, chunked_prefill)
+                       for _ in range(n)]
+
+    def __len__(self) -> int:
+        return len(self.scheds)
+
+    def add(self, seq: Sequence) -> None:
+        v = min(range(len(self.scheds)),
+                key=lambda i: len(self.scheds[i].running) + len(self.scheds[i].waiting))
+        seq.vengine = v
+        self.scheds[v].add(seq)
+
+    def abort(self, request_id: str) -> Optional[Sequence]:
+        for sc in self.scheds:
+            s = sc.abort(request_id)
+            if s is not None:
+                return s
+        return None
+
+    def has_work(self) -> bool:
+        return any(sc.has_work() for sc in self.scheds)
+
+    def schedule_v(self, v: int) -> ScheduledBatch:
+        return self.scheds[v].schedule()
+
+    def finish(self, seq: Sequence, reason: str) -> None:
+        self.scheds[getattr(seq, "vengine", 0)].finish(seq, reason)
+
+    @property
+    def running(self) -> list[Sequence]:
+        return [s for sc in self.scheds for s in sc.running]
+
+    @property
+    def waiting(self) -> list[Sequence]:
+        return [s for sc in self.scheds for s in sc.waiting]
+
+    @property
+    def num_preemptions(self) -> int:
+        return sum(sc.num_preemptions for sc in self.scheds)

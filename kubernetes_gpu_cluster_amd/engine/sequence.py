@@ -69,7 +69,7 @@ class Sequence:
                  "status", "block_ids", "num_computed", "arrival_time", "first_token_time",
                  "finish_time", "finish_reason", "seed", "num_preemptions", "max_tokens",
                  "slot", "last_token_time", "token_times", "prompt_text", "stream",
-                 "num_pending", "proc_slot", "block_keys", "num_registered")
+                 "num_pending", "proc_slot", "block_keys", "num_registered", "vengine")
 
     def __init__(self, request_id: str, prompt_token_ids: list[int], params: SamplingParams,
                  arrival_time: Optional[float] = None, max_model_len: int = 1 << 30):
@@ -98,6 +98,7 @@ class Sequence:
         self.proc_slot = -1                   # slot whose penalty statistics are built
         self.block_keys: list[bytes] = []       # prefix-cache keys of its full blocks
         self.num_registered = 0               # leading blocks published to the prefix cache
+        self.vengine = 0                      # PP micro-batch (engine/scheduler.VirtualSchedulers)
 
     @property
     def num_tokens(self) -> int:

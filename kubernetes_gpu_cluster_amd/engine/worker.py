@@ -108,6 +108,32 @@ class Worker:
 
 
 # ---------------------------------------------------------------------- plan transport
+# TP only: commands and plans are broadcast over the gloo group (every rank takes part
+# in every step at the same time anyway).  PP > 1: the driver SENDS them to every rank
+# (non-blocking isend, FIFO per pair), so it can hand stage 0 the next micro-batch while
+# the later stages are still busy with earlier ones -- a broadcast would make the driver
+# wait for the slowest stage to join and serialise the pipeline.
+_pending_sends: list = []     # (work, tensor): tensors kept alive until their isend completes
+
+
+def _p2p_plans(s) -> bool:
+    return s.pp_size > 1
+
+
+def _send_to_ranks(s, tensors: list) -> None:
+    base = getattr(s, "global_base", 0)
+    for r in range(1, s.tp_size * s.pp_size):
+        for t in tensors:
+            _pending_sends.append((dist.isend(t, dst=base + r, group=s.cpu_group), t))
+    _pending_sends[:] = [(w, t) for w, t in _pending_sends if not w.is_completed()]
+
+
+def _drain_sends() -> None:
+    for w, _ in _pending_sends:
+        w.wait()
+    _pending_sends.clear()
+
+
 def _bcast_cmd(cmd: int, arg: int = 0, header: Optional[list[int]] = None) -> list[int]:
     s = get_state()
     h = torch.zeros(16, dtype=torch.int64)
@@ -115,15 +141,28 @@ def _bcast_cmd(cmd: int, arg: int = 0, header: Optional[list[int]] = None) -> li
         h[0], h[1] = cmd, arg
         if header:
             h[2:2 + len(header)] = torch.tensor(header)
-    dist.broadcast(h, src=getattr(s, "global_base", 0), group=s.cpu_group)
+    if _p2p_plans(s):
+        if s.rank == 0:
+            _send_to_ranks(s, [h])
+        else:
+            dist.recv(h, src=getattr(s, "global_base", 0), group=s.cpu_group)
+    else:
+        dist.broadcast(h, src=getattr(s, "global_base", 0), group=s.cpu_group)
     return h.tolist()
 
 
 def _bcast_plan_blobs(runner: ModelRunner, plan_hdr: list[int]) -> None:
-    """Ship only the used prefixes of the blobs (the layout is fixed)."""
     s = get_state()
     src = getattr(s, "global_base", 0)
-    for t in (runner.h64, runner.h32, runner.hf):
+    blobs = (runner.h64, runner.h32, runner.hf)
+    if _p2p_plans(s):
+        if s.rank == 0:      # the driver rewrites its blobs for the next micro-batch
+            _send_to_ranks(s, [t.clone() for t in blobs])
+        else:
+            for t in blobs:
+                dist.recv(t, src=src, group=s.cpu_group)
+        return
+    for t in blobs:
         dist.broadcast(t, src=src, group=s.cpu_group)
 
 
@@ -147,6 +186,7 @@ def worker_loop(worker: Worker) -> None:
         h = _bcast_cmd(0)
         cmd, arg = h[0], h[1]
         if cmd == CMD_EXIT:
+            worker.runner.write_stage_stats()
             _release_custom_allreduce()
             worker.release()
             break
@@ -230,6 +270,25 @@ class TokenFuture:
                 for i, (r, k) in enumerate(rows)}
 
 
+class PipelinedTokenFuture:
+    """Sampled ids of a micro-batch in the pipeline (PP > 1): arrive from the last stage."""
+
+    def __init__(self, work, buf: torch.Tensor, on_done):
+        self.work, self.buf, self._on_done = work, buf, on_done
+        self.values: Optional[list[int]] = None
+
+    def result(self) -> list[int]:
+        if self.values is None:
+            self.work.wait()
+            self.values = self.buf.tolist()
+            done, self._on_done = self._on_done, None
+            done()
+        return self.values
+
+    def logprobs(self) -> dict:
+        return {}
+
+
 class _DistExecutorBase:
     """Rank 0 side of the command protocol (shared by spawned / torchrun ranks)."""
     worker: Worker
@@ -272,6 +331,24 @@ class _DistExecutorBase:
     def supports_async(self) -> bool:
         return get_state().pp_size == 1
 
+    @property
+    def pipeline_depth(self) -> int:
+        """Micro-batches the engine keeps in flight (one per pipeline stage)."""
+        return get_state().pp_size
+
+    def execute_pipelined(self, plan: StepPlan) -> "PipelinedTokenFuture":
+        """PP > 1: send the plan to every rank, run stage 0 of it here (its activations
+        go to stage 1 by point-to-point), and return at once; the last stage's TP leader
+        sends the sampled ids back, received by a posted irecv."""
+        done = self._step_launched()
+        _bcast_cmd(CMD_STEP, 0, plan.header())
+        _bcast_plan_blobs(self.worker.runner, plan.header())
+        self.worker.run(plan)
+        s = get_state()
+        t = torch.empty(plan.S, dtype=torch.int64)
+        src = getattr(s, "global_base", 0) + (s.pp_size - 1) * s.tp_size
+        return PipelinedTokenFuture(dist.irecv(t, src=src, group=s.cpu_group), t, done)
+
     def execute_async(self, plan: StepPlan) -> TokenFuture:
         if self.watchdog is not None:
             self.watchdog.step_begin()
@@ -306,8 +383,10 @@ class _DistExecutorBase:
     def shutdown(self) -> None:
         if self.watchdog is not None:
             self.watchdog.stop()          # the ranks are about to exit on purpose
+        self.worker.runner.write_stage_stats()
         try:
             _bcast_cmd(CMD_EXIT)
+            _drain_sends()
         except Exception:  # noqa: BLE001
             pass
         _release_custom_allreduce()
@@ -332,11 +411,6 @@ def _spawn_entry(rank: int, cfg: EngineConfig, env: dict, local: Optional[int] =
     os.environ["RANK"] = str(rank)
     os.environ["LOCAL_RANK"] = str(local)
     watch_parent()            # never outlive the driver (engine/health.py)
-    # a SIGTERM / Ctrl-C to the process group is the API server's to handle; the driver
-    # then shuts the ranks down in order (a rank that died first would read as a fault)
-    import signal
-    signal.signal(signal.SIGTERM, signal.SIG_IGN)
-    signal.signal(signal.SIGINT, signal.SIG_IGN)
     try:
         w = Worker(cfg, rank=rank, local_device=local)
         worker_loop(w)
