@@ -19,9 +19,12 @@ def family(name: str) -> str:
         return "skinny_gemm(K9)"
     if "moe_gemm" in n:
         return "moe_gemm(K14)"
+    if "dgemm" in n:
+        return "dgemm(K9m)"
     if "Cijk" in n or "gemm" in n.lower():
         return "gemm(hipblaslt)"
-    for k in ("decode_gemm", "paged_decode_reduce", "paged_decode", "prefill_attn", "rms_norm",
+    for k in ("splitk_add_rms_norm", "splitk_reduce_silu", "splitk_reduce", "decode_gemm",
+              "paged_decode_reduce", "paged_decode", "prefill_attn", "rms_norm",
               "silu_mul", "rope_kv", "sample_kernel", "layer_norm", "allreduce", "nccl", "rccl"):
         if k in n:
             return k
@@ -71,7 +74,7 @@ def main():
         agg = collections.Counter()
         for s in dec:
             agg.update(s[3])
-        for k, v in agg.most_common(12):
+        for k, v in agg.most_common(16):
             print(f"   {k:38} {v / len(dec) / 1e3:9.1f} us/step")
 
 
