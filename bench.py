@@ -310,32 +310,40 @@ def main_service(args):
             asyncio.run(sc.wait_healthy([api_url, url], args.startup_timeout, procs, _note))
             _note(f"rank {rank}: service is up")
 
-        async def waves(n: int, base_seed: int, timed: bool):
-            out = []
-            async with sc.new_session() as s:      # one client; connections are reused
-                for w in range(n):
-                    prompts = sc.random_prompts(args.num_prompts, args.input_len, vocab,
-                                                seed=base_seed + 1000 * w + rank)
-                    r, lo, hi = await sc.run_wave(s, url, args.model, prompts, args.output_len,
-                                                  temperature=args.temperature)
-                    out.append((r, lo, hi))
-            return out
+        def make_prompts(n: int, base_seed: int):
+            # generated before any timer starts (~0.1 s of Python per 256 x 512 wave)
+            return [sc.random_prompts(args.num_prompts, args.input_len, vocab,
+                                      seed=base_seed + 1000 * w + rank) for w in range(n)]
 
-        if leader and args.warmup:
-            for r, _, _ in asyncio.run(waves(args.warmup, 7_000_000, False)):
-                bad = [x for x in r if not x.ok]
-                if bad:
-                    raise RuntimeError(f"warmup: {len(bad)} requests failed (status {bad[0].status})")
-        if world > 1:
-            dist.barrier()
-        t0 = time.monotonic()
-        if leader:
-            for r, lo, hi in asyncio.run(waves(args.steps, 0, True)):
-                res_all += r
-                windows.append((lo, hi))
-        if world > 1:
-            dist.barrier()
-        elapsed = time.monotonic() - t0
+        async def run_all():
+            """Warmup and timed waves on ONE client session (its keep-alive connections
+            are reused, as a long-lived client's are); the barriers block the loop on
+            purpose -- nothing else runs on it between waves."""
+            warm = make_prompts(args.warmup, 7_000_000) if leader else []
+            timed = make_prompts(args.steps, 0) if leader else []
+            out = []
+            async with sc.new_session() as s:
+                for prompts in warm:
+                    r, _, _ = await sc.run_wave(s, url, args.model, prompts, args.output_len,
+                                                temperature=args.temperature)
+                    bad = [x for x in r if not x.ok]
+                    if bad:
+                        raise RuntimeError(f"warmup: {len(bad)} requests failed "
+                                           f"(status {bad[0].status})")
+                if world > 1:
+                    dist.barrier()
+                t0 = time.monotonic()
+                for prompts in timed:
+                    out.append(await sc.run_wave(s, url, args.model, prompts, args.output_len,
+                                                 temperature=args.temperature))
+                if world > 1:
+                    dist.barrier()
+                return out, t0, time.monotonic() - t0
+
+        waves_out, t0, elapsed = asyncio.run(run_all())
+        for r, lo, hi in waves_out:
+            res_all += r
+            windows.append((lo, hi))
         if leader:
             with urllib.request.urlopen(f"{api_url}/kgc/engine_stats?since={t0 - 1.0}", timeout=30) as f:
                 st = json.loads(f.read())
