@@ -567,6 +567,82 @@ void xgmi_allreduce(Tensor inout, std::vector<int64_t> data, std::vector<int64_t
                         cap_bytes / 16, two_shot, stream());
 }
 
+// ---- C7 expert-parallel all-to-all over IPC peer memory
+static kgc::EpPtrs ep_ptrs(const std::vector<int64_t>& data, const std::vector<int64_t>& sig,
+                           int64_t rank) {
+  const int64_t nr = (int64_t)data.size();
+  TORCH_CHECK(nr == 2 || nr == 4 || nr == 8, "EP all-to-all: 2, 4 or 8 ranks");
+  TORCH_CHECK((int64_t)sig.size() == nr && rank >= 0 && rank < nr, "bad rank / pointer lists");
+  kgc::EpPtrs P{};
+  for (int64_t r = 0; r < nr; ++r) {
+    P.data[r] = (void*)(intptr_t)data[r];
+    P.sig[r] = (void*)(intptr_t)sig[r];
+  }
+  return P;
+}
+
+static void ep_check_rows(const Tensor& t, const char* what) {
+  check_gpu(t, what);
+  TORCH_CHECK(t.dim() == 2 && t.is_contiguous() && t.size(1) % 8 == 0 &&
+              (t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kHalf),
+              what, ": contiguous bf16/fp16 [rows, H], H % 8 == 0");
+}
+
+int64_t ep_signal_bytes_op() { return (int64_t)kgc::ep_signal_bytes(); }
+int64_t ep_region_bytes_op(int64_t nr, int64_t C, int64_t H, int64_t esz) {
+  return kgc::ep_region_bytes((int)nr, (int)C, (int)H, (int)esz);
+}
+int64_t ep_max_pairs_op() { return kgc::ep_max_pairs(); }
+
+void ep_dispatch(Tensor x, Tensor topk_ids, std::vector<int64_t> data, std::vector<int64_t> sig,
+                 int64_t rank, int64_t E_local, int64_t C) {
+  ep_check_rows(x, "x");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  TORCH_CHECK(topk_ids.scalar_type() == at::kInt && topk_ids.dim() == 2 && topk_ids.is_contiguous() &&
+              topk_ids.size(0) == x.size(0), "topk_ids int32 [T, k]");
+  const int64_t npairs = topk_ids.numel();
+  TORCH_CHECK(npairs <= C && npairs <= kgc::ep_max_pairs(), "more (token, expert) pairs than the EP buffers hold");
+  kgc::launch_ep_dispatch(dt_code(x), ep_ptrs(data, sig, rank), (int)data.size(), (int)rank,
+                          x.data_ptr(), topk_ids.data_ptr<int>(), (int)npairs,
+                          (int)topk_ids.size(1), (int)x.size(1), (int)E_local, (int)C, stream());
+}
+
+void ep_receive(Tensor x_local, Tensor ids, Tensor route, std::vector<int64_t> data,
+                std::vector<int64_t> sig, int64_t rank, int64_t E_local, int64_t C) {
+  ep_check_rows(x_local, "x_local");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x_local.device());
+  const int64_t slots = (int64_t)data.size() * C;
+  TORCH_CHECK(x_local.size(0) == slots && ids.numel() == slots && route.numel() == slots &&
+              ids.scalar_type() == at::kInt && route.scalar_type() == at::kInt,
+              "x_local [NR * C, H], ids / route int32 [NR * C]");
+  kgc::launch_ep_receive(dt_code(x_local), ep_ptrs(data, sig, rank), (int)data.size(), (int)rank,
+                         x_local.data_ptr(), ids.data_ptr<int>(), route.data_ptr<int>(),
+                         (int)x_local.size(1), (int)E_local, (int)C, stream());
+}
+
+void ep_return(Tensor y, Tensor route, std::vector<int64_t> data, std::vector<int64_t> sig,
+               int64_t rank, int64_t C) {
+  ep_check_rows(y, "y");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(y.device());
+  TORCH_CHECK(y.size(0) == (int64_t)data.size() * C && route.numel() == y.size(0) &&
+              route.scalar_type() == at::kInt, "y [NR * C, H], route int32 [NR * C]");
+  kgc::launch_ep_return(dt_code(y), ep_ptrs(data, sig, rank), (int)data.size(), (int)rank,
+                        y.data_ptr(), route.data_ptr<int>(), (int)y.size(1), (int)C, stream());
+}
+
+void ep_combine(Tensor out, Tensor topk_w, std::vector<int64_t> data, std::vector<int64_t> sig,
+                int64_t rank, int64_t C) {
+  ep_check_rows(out, "out");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(out.device());
+  TORCH_CHECK(topk_w.scalar_type() == at::kFloat && topk_w.dim() == 2 && topk_w.is_contiguous() &&
+              topk_w.size(0) == out.size(0) && topk_w.numel() <= C, "topk_w fp32 [T, k]");
+  kgc::launch_ep_combine(dt_code(out), ep_ptrs(data, sig, rank), (int)data.size(), (int)rank,
+                         out.data_ptr(), topk_w.data_ptr<float>(), (int)out.size(0),
+                         (int)topk_w.size(1), (int)out.size(1), (int)C, stream());
+}
+
+int64_t ep_read_err_op(int64_t sig) { return kgc::ep_read_err((void*)(intptr_t)sig); }
+
 // debug builds: OR of the K1/K2/K3 bounds-check error words (read and cleared)
 int64_t debug_errors() {
   return (int64_t)(kgc::dbg_err_attention_decode() | (kgc::dbg_err_attention_prefill() << 1) |
@@ -715,6 +791,16 @@ TORCH_LIBRARY(kgc, m) {
         "int[] data, int[] sig, int rank, int cap_bytes) -> ()");
   m.def("allreduce_rms_max_hidden() -> int", &allreduce_rms_max_hidden_op);
   m.def("debug_errors() -> int", &debug_errors);
+  m.def("ep_signal_bytes() -> int", &ep_signal_bytes_op);
+  m.def("ep_region_bytes(int nr, int C, int H, int esz) -> int", &ep_region_bytes_op);
+  m.def("ep_max_pairs() -> int", &ep_max_pairs_op);
+  m.def("ep_read_err(int sig) -> int", &ep_read_err_op);
+  m.def("ep_dispatch(Tensor x, Tensor topk_ids, int[] data, int[] sig, int rank, int E_local, "
+        "int C) -> ()");
+  m.def("ep_receive(Tensor(a!) x_local, Tensor(b!) ids, Tensor(c!) route, int[] data, int[] sig, "
+        "int rank, int E_local, int C) -> ()");
+  m.def("ep_return(Tensor y, Tensor route, int[] data, int[] sig, int rank, int C) -> ()");
+  m.def("ep_combine(Tensor(a!) out, Tensor topk_w, int[] data, int[] sig, int rank, int C) -> ()");
   m.def("debug_build() -> bool", &debug_build);
   m.def("prefill_block_m() -> int", &prefill_block_m);
   m.def("skinny_gemm(Tensor(a!) C, Tensor X, Tensor W, Tensor? bias, int mt, int nt, int nw, "
@@ -733,6 +819,10 @@ TORCH_LIBRARY_IMPL(kgc, CUDA, m) {
   m.impl("sample_vp_unpack", &sample_vp_unpack);
   m.impl("xgmi_allreduce", &xgmi_allreduce);
   m.impl("xgmi_allreduce_rms", &xgmi_allreduce_rms);
+  m.impl("ep_dispatch", &ep_dispatch);
+  m.impl("ep_receive", &ep_receive);
+  m.impl("ep_return", &ep_return);
+  m.impl("ep_combine", &ep_combine);
   m.impl("moe_route", &moe_route);
   m.impl("moe_align", &moe_align);
   m.impl("moe_gemm", &moe_gemm);

@@ -112,6 +112,21 @@ int allreduce_rms_max_hidden();
 void launch_allreduce_rms(int dtype, const ArPtrs& P, int nranks, int rank, const void* in,
                           void* out, void* residual, const void* w, int M, int H, float eps,
                           int64_t cap_vec, hipStream_t s);
+// C7 expert-parallel dispatch / combine over the same kind of IPC buffers (ep_a2a.hip)
+using EpPtrs = ArPtrs;
+size_t ep_signal_bytes();
+int64_t ep_region_bytes(int nr, int C, int H, int esz);
+int ep_max_pairs();
+void launch_ep_dispatch(int dtype, const EpPtrs& P, int nr, int rank, const void* x,
+                        const int* topk_ids, int npairs, int k, int H, int E_local, int C,
+                        hipStream_t s);
+void launch_ep_receive(int dtype, const EpPtrs& P, int nr, int rank, void* x_local, int* ids,
+                       int* route, int H, int E_local, int C, hipStream_t s);
+void launch_ep_return(int dtype, const EpPtrs& P, int nr, int rank, const void* y,
+                      const int* route, int H, int C, hipStream_t s);
+void launch_ep_combine(int dtype, const EpPtrs& P, int nr, int rank, void* out,
+                       const float* topk_w, int ntok, int k, int H, int C, hipStream_t s);
+uint32_t ep_read_err(void* sig);
 void* ar_alloc(int64_t bytes);
 void ar_free(void* p);
 void ar_get_handle(void* p, uint8_t* out64);

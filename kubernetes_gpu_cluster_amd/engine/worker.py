@@ -84,6 +84,17 @@ class Worker:
         if self.ps.tp_size > 1 and dev.type == "cuda" and not cfg.disable_custom_all_reduce:
             from ..parallel.custom_allreduce import maybe_init_custom_allreduce
             comm.set_custom_allreduce(maybe_init_custom_allreduce(self.ps, dev))
+        self.ep_a2a = None
+        if self.ps.tp_size > 1 and dev.type == "cuda" and cfg.moe_parallel == "ep":
+            from ..models.moe import MoEBlock
+            from ..parallel.expert_a2a import maybe_init_expert_a2a
+            blocks = [m for m in self.model.modules() if isinstance(m, MoEBlock) and m.mode == "ep"]
+            if blocks:
+                self.ep_a2a = maybe_init_expert_a2a(
+                    self.ps, dev, min(cfg.cuda_graph_max_bs, cfg.max_num_seqs), blocks[0].k,
+                    self.mcfg.hidden_size, self.dtype)
+                for b in blocks:
+                    b.ep_a2a = self.ep_a2a
         self.runner = ModelRunner(self.model, self.mcfg, self.dtype, dev, cfg.block_size,
                                   self.max_model_len, cfg.max_num_seqs, cfg.token_budget(),
                                   cfg.enforce_eager, cfg.cuda_graph_max_bs,
@@ -104,6 +115,9 @@ class Worker:
         return self.runner.run(plan)
 
     def release(self) -> None:
+        if self.ep_a2a is not None:
+            self.ep_a2a.close()
+            self.ep_a2a = None
         self.runner.release()
 
 

@@ -13,8 +13,9 @@ it): router GEMM -> ``moe_route`` (K13) -> ``moe_align`` bucketing -> grouped MF
 GEMM (gate/up, rows gathered) -> silu_mul (K7) -> grouped GEMM (down, rows
 scattered back) -> weighted ``moe_combine`` (csrc/kernels/moe.hip).  The CPU path
 (and shapes the grouped-GEMM tiles do not cover) sorts the pairs by expert and runs
-one GEMM pair per non-empty expert; ``ep`` mode needs the per-rank counts on the
-host for the variable-size all-to-all, so it runs eagerly (no decode graphs).
+one GEMM pair per non-empty expert.  ``ep`` mode exchanges decode-size batches through
+the device-side all-to-all over xGMI peer memory (``parallel/expert_a2a.py``, captured
+in decode graphs); larger calls use an RCCL all_to_all with host-side counts.
 """
 from __future__ import annotations
 
@@ -92,8 +93,14 @@ class MoEBlock(nn.Module):
         if torch.device(device).type == "cuda" and not self.native:
             log.warning("MoE dims (2I=%d, H=%d) not covered by the grouped GEMM tiles; "
                         "using the per-expert path (no decode graphs)", 2 * self.I_local, H)
-        # decode hipGraphs need a block with no host synchronisation
-        self.graph_safe = self.native and self.mode == "tp"
+        # ep mode on one node: the device-side all-to-all over xGMI peer memory
+        # (parallel/expert_a2a.py), attached by the worker once the EP group exists
+        self.ep_a2a = None
+
+    @property
+    def graph_safe(self) -> bool:
+        """Decode hipGraphs need a block with no host synchronisation."""
+        return self.native and (self.mode == "tp" or self.ep_a2a is not None)
 
     def experts(self, x, topk_w, topk_ids, expert_offset: int = 0, all_local: bool = True):
         # the grouped kernel streams each expert's weights once per row block: best at
@@ -150,7 +157,15 @@ class MoEBlock(nn.Module):
 
     def _forward_ep(self, x, topk_w, topk_ids):
         """All-to-all dispatch/combine (C7).  Each (token, slot) pair goes to the rank
-        owning its expert; the owner computes and sends the weighted row back."""
+        owning its expert; the owner computes and sends the weighted row back.  Decode
+        sizes run the device-side exchange over xGMI peer memory (graph-capturable);
+        larger calls an RCCL all_to_all with host-side counts."""
+        a2a = self.ep_a2a
+        if a2a is not None and self.native and a2a.fits(x, topk_ids):
+            return a2a.forward(x, topk_w, topk_ids,
+                               lambda xs, w, ids, off: ops.fused_moe(xs, self.w13, self.w2, w,
+                                                                     ids, off),
+                               self.E_local)
         s = get_state()
         tp = s.tp_size
         T, H = x.shape
