@@ -643,6 +643,14 @@ void ep_combine(Tensor out, Tensor topk_w, std::vector<int64_t> data, std::vecto
 
 int64_t ep_read_err_op(int64_t sig) { return kgc::ep_read_err((void*)(intptr_t)sig); }
 
+void ep_err_copy_async(int64_t sig, Tensor host_out) {
+  TORCH_CHECK(host_out.device().is_cpu() && host_out.is_pinned() &&
+              host_out.scalar_type() == at::kInt && host_out.numel() >= 1,
+              "host_out: pinned int32 [1]");
+  kgc::ep_err_copy_async((void*)(intptr_t)sig, reinterpret_cast<uint32_t*>(host_out.data_ptr()),
+                         stream());
+}
+
 // debug builds: OR of the K1/K2/K3 bounds-check error words (read and cleared)
 int64_t debug_errors() {
   return (int64_t)(kgc::dbg_err_attention_decode() | (kgc::dbg_err_attention_prefill() << 1) |
@@ -795,6 +803,7 @@ TORCH_LIBRARY(kgc, m) {
   m.def("ep_region_bytes(int nr, int C, int H, int esz) -> int", &ep_region_bytes_op);
   m.def("ep_max_pairs() -> int", &ep_max_pairs_op);
   m.def("ep_read_err(int sig) -> int", &ep_read_err_op);
+  m.def("ep_err_copy_async(int sig, Tensor(a!) host_out) -> ()", &ep_err_copy_async);
   m.def("ep_dispatch(Tensor x, Tensor topk_ids, int[] data, int[] sig, int rank, int E_local, "
         "int C) -> ()");
   m.def("ep_receive(Tensor(a!) x_local, Tensor(b!) ids, Tensor(c!) route, int[] data, int[] sig, "

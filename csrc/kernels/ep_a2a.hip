@@ -341,6 +341,10 @@ void launch_ep_combine(int dtype, const EpPtrs& P, int nr, int rank, void* out,
 
 int ep_max_pairs() { return EP_MAX_PAIRS; }
 
+void ep_err_copy_async(void* sig, uint32_t* host_dst, hipStream_t s) {
+  (void)hipMemcpyAsync(host_dst, &reinterpret_cast<EpSignal*>(sig)->err, 4, hipMemcpyDeviceToHost, s);
+}
+
 uint32_t ep_read_err(void* sig) {
   uint32_t e = 0;
   (void)hipMemcpy(&e, &reinterpret_cast<EpSignal*>(sig)->err, 4, hipMemcpyDeviceToHost);

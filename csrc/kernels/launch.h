@@ -127,6 +127,7 @@ void launch_ep_return(int dtype, const EpPtrs& P, int nr, int rank, const void* 
 void launch_ep_combine(int dtype, const EpPtrs& P, int nr, int rank, void* out,
                        const float* topk_w, int ntok, int k, int H, int C, hipStream_t s);
 uint32_t ep_read_err(void* sig);
+void ep_err_copy_async(void* sig, uint32_t* host_dst, hipStream_t s);
 void* ar_alloc(int64_t bytes);
 void ar_free(void* p);
 void ar_get_handle(void* p, uint8_t* out64);

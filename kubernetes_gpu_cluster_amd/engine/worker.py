@@ -313,15 +313,17 @@ class _DistExecutorBase:
         an async copy of the xGMI all-reduce error word checked when the step completes."""
         if self.watchdog is not None:
             self.watchdog.step_begin()
-        car = comm.get_custom_allreduce()
-        if car is not None:
-            car.enqueue_err_read()
+        # sticky error words of the peer-memory collectives (xGMI all-reduce, EP exchange)
+        checks = [c for c in (comm.get_custom_allreduce(), getattr(self.worker, "ep_a2a", None))
+                  if c is not None]
+        for c in checks:
+            c.enqueue_err_read()
 
         def done():
             if self.watchdog is not None:
                 self.watchdog.step_end()
-            if car is not None:
-                car.raise_if_failed()
+            for c in checks:
+                c.raise_if_failed()
         return done
 
     @property

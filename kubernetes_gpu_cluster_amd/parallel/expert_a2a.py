@@ -42,6 +42,7 @@ class ExpertAllToAll:
         self.rank, self.world, self.device = rank, world, device
         self.C, self.H, self.dtype = int(max_pairs), int(hidden), dtype
         self._own, self._opened = 0, []
+        self._err_host: Optional[torch.Tensor] = None
         handle, err = None, None
         try:
             with torch.cuda.device(device):
@@ -103,6 +104,18 @@ class ExpertAllToAll:
         err = int(torch.ops.kgc.ep_read_err(self.sig[self.rank]))
         if err:
             raise AllReduceFailed(f"EP all-to-all: peers {bin(err)} never arrived")
+
+    def enqueue_err_read(self) -> None:
+        """Queue an async copy of the sticky error word behind the current step."""
+        if self._err_host is None:
+            self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        torch.ops.kgc.ep_err_copy_async(self.sig[self.rank], self._err_host)
+
+    def raise_if_failed(self) -> None:
+        h = self._err_host
+        if h is not None and int(h[0]):
+            raise AllReduceFailed(f"EP all-to-all: peers {bin(int(h[0]))} never arrived "
+                                  f"(an EP rank is dead or wedged); the engine stops")
 
     def close(self) -> None:
         if self._own or self._opened:
