@@ -651,6 +651,51 @@ void ep_err_copy_async(int64_t sig, Tensor host_out) {
                          stream());
 }
 
+// ---- C5 pipeline-stage handoff over IPC peer memory
+int64_t pp_signal_bytes_op() { return (int64_t)kgc::pp_signal_bytes(); }
+int64_t pp_read_err_op(int64_t sig) { return kgc::pp_read_err((void*)(intptr_t)sig); }
+
+static void pp_check_pair(const Tensor& h, const Tensor& r) {
+  check_gpu(h, "h");
+  check_same_dev(h, r, "r");
+  TORCH_CHECK(h.is_contiguous() && r.is_contiguous() && h.sizes() == r.sizes() &&
+              h.scalar_type() == r.scalar_type() && (h.numel() * h.element_size()) % 16 == 0,
+              "hidden / residual: contiguous, same shape and dtype, 16-byte multiple");
+}
+
+void pp_send(Tensor h, Tensor r, int64_t peer_data, int64_t peer_sig, int64_t own_sig,
+             int64_t slot_bytes, int64_t R) {
+  pp_check_pair(h, r);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(h.device());
+  const int64_t bytes = h.numel() * h.element_size();
+  TORCH_CHECK(bytes <= slot_bytes && R >= 1, "rows larger than a handoff slot");
+  kgc::launch_pp_send((void*)(intptr_t)peer_data, (void*)(intptr_t)peer_sig,
+                      (void*)(intptr_t)own_sig, h.data_ptr(), r.data_ptr(), bytes, slot_bytes,
+                      (int)R, stream());
+}
+
+void pp_recv(Tensor h, Tensor r, int64_t own_data, int64_t own_sig, int64_t peer_sig,
+             int64_t slot_bytes, int64_t R) {
+  pp_check_pair(h, r);
+  c10::hip::HIPGuardMasqueradingAsCUDA g(h.device());
+  const int64_t bytes = h.numel() * h.element_size();
+  TORCH_CHECK(bytes <= slot_bytes && R >= 1, "rows larger than a handoff slot");
+  kgc::launch_pp_recv((void*)(intptr_t)own_data, (void*)(intptr_t)own_sig,
+                      (void*)(intptr_t)peer_sig, h.data_ptr(), r.data_ptr(), bytes, slot_bytes,
+                      (int)R, stream());
+}
+
+// one device word (e.g. a peer-memory collective's sticky error) -> pinned host int32,
+// stream-ordered behind the step that may set it
+void u32_copy_async(int64_t addr, Tensor host_out, int64_t index) {
+  TORCH_CHECK(host_out.device().is_cpu() && host_out.is_pinned() &&
+              host_out.scalar_type() == at::kInt && index >= 0 && index < host_out.numel(),
+              "host_out: pinned int32, index in range");
+  TORCH_CHECK(hipMemcpyAsync(reinterpret_cast<int*>(host_out.data_ptr()) + index,
+                             (const void*)(intptr_t)addr, 4, hipMemcpyDeviceToHost,
+                             stream()) == hipSuccess, "u32_copy_async");
+}
+
 // debug builds: OR of the K1/K2/K3 bounds-check error words (read and cleared)
 int64_t debug_errors() {
   return (int64_t)(kgc::dbg_err_attention_decode() | (kgc::dbg_err_attention_prefill() << 1) |
@@ -800,6 +845,13 @@ TORCH_LIBRARY(kgc, m) {
   m.def("allreduce_rms_max_hidden() -> int", &allreduce_rms_max_hidden_op);
   m.def("debug_errors() -> int", &debug_errors);
   m.def("ep_signal_bytes() -> int", &ep_signal_bytes_op);
+  m.def("pp_signal_bytes() -> int", &pp_signal_bytes_op);
+  m.def("u32_copy_async(int addr, Tensor(a!) host_out, int index) -> ()", &u32_copy_async);
+  m.def("pp_read_err(int sig) -> int", &pp_read_err_op);
+  m.def("pp_send(Tensor h, Tensor r, int peer_data, int peer_sig, int own_sig, int slot_bytes, "
+        "int R) -> ()");
+  m.def("pp_recv(Tensor(a!) h, Tensor(b!) r, int own_data, int own_sig, int peer_sig, "
+        "int slot_bytes, int R) -> ()");
   m.def("ep_region_bytes(int nr, int C, int H, int esz) -> int", &ep_region_bytes_op);
   m.def("ep_max_pairs() -> int", &ep_max_pairs_op);
   m.def("ep_read_err(int sig) -> int", &ep_read_err_op);
@@ -829,6 +881,8 @@ TORCH_LIBRARY_IMPL(kgc, CUDA, m) {
   m.impl("xgmi_allreduce", &xgmi_allreduce);
   m.impl("xgmi_allreduce_rms", &xgmi_allreduce_rms);
   m.impl("ep_dispatch", &ep_dispatch);
+  m.impl("pp_send", &pp_send);
+  m.impl("pp_recv", &pp_recv);
   m.impl("ep_receive", &ep_receive);
   m.impl("ep_return", &ep_return);
   m.impl("ep_combine", &ep_combine);

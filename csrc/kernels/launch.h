@@ -128,6 +128,13 @@ void launch_ep_combine(int dtype, const EpPtrs& P, int nr, int rank, void* out,
                        const float* topk_w, int ntok, int k, int H, int C, hipStream_t s);
 uint32_t ep_read_err(void* sig);
 void ep_err_copy_async(void* sig, uint32_t* host_dst, hipStream_t s);
+// C5 pipeline-stage handoff over IPC peer memory (pp_handoff.hip)
+size_t pp_signal_bytes();
+void launch_pp_send(void* peer_data, void* peer_sig, void* own_sig, const void* h, const void* r,
+                    int64_t bytes, int64_t slot_bytes, int R, hipStream_t s);
+void launch_pp_recv(void* own_data, void* own_sig, void* peer_sig, void* h, void* r,
+                    int64_t bytes, int64_t slot_bytes, int R, hipStream_t s);
+uint32_t pp_read_err(void* sig);
 void* ar_alloc(int64_t bytes);
 void ar_free(void* p);
 void ar_get_handle(void* p, uint8_t* out64);

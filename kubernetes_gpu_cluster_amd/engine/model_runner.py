@@ -144,6 +144,7 @@ class ModelRunner:
         # KGC_FAKE_STAGE_MS: every step of this rank is a sleep of that many ms with the
         # real pipeline-stage traffic around it (PP scheduling / utilisation tests)
         self._fake_ms = float(os.environ.get("KGC_FAKE_STAGE_MS", "0") or 0)
+        self.pp_link = None         # parallel/pp_handoff.PipelineHandoff (PP decode graphs)
         self.stage_stats = {"busy_s": 0.0, "t_first": None, "t_last": None, "steps": 0}
         # vocab-parallel sampling (TP > 1): every rank keeps its logits shard; rows
         # without top-k / top-p / processors / logprobs are sampled by an 8-byte-per-row
@@ -391,18 +392,22 @@ class ModelRunner:
         L = self.L
         ps = self.ps
         hidden_in = None
+        graph = bool(plan.B) and plan.B in self.graphs
         if not self.model.first:
-            shp = (plan.B or plan.T, self.mcfg.hidden_size)
-            hidden_in = comm.pp_recv([shp, shp], self.dtype, self.device)
+            if not graph:           # a graph step receives inside its replay (pp_link)
+                shp = (plan.B or plan.T, self.mcfg.hidden_size)
+                hidden_in = comm.pp_recv([shp, shp], self.dtype, self.device)
         elif plan.dev_tok:
             n = max(plan.D, plan.B)
             torch.index_select(self.last_tok, 0, self.d64[L.dslots:L.dslots + n],
                                out=self.d64[L.ids + plan.Tp:L.ids + plan.Tp + n])
-        if plan.B and plan.B in self.graphs and self.model.first and self.model.last:
+        if graph:
             g, logits = self.graphs[plan.B]
             g.replay()
-            logits = logits[: plan.S]
             self.stats["graph_steps"] += 1
+            if not self.model.last:
+                return None
+            logits = logits[: plan.S]
             T = plan.B
         else:
             T = plan.T if not plan.B else plan.B
@@ -551,7 +556,8 @@ class ModelRunner:
                              silu_shapes=getattr(self.model, "silu_shapes", lambda: set())(),
                              tail_shapes=getattr(self.model, "tail_shapes", lambda: set())(),
                              qkv_dims=getattr(self.model, "qkv_dims", lambda: {})())
-        if (not self.use_graphs or not (self.model.first and self.model.last)
+        whole = self.model.first and self.model.last
+        if (not self.use_graphs or not (whole or self.pp_link is not None)
                 or not getattr(self.model, "graph_safe", True)):
             self.use_graphs = False
             return 0.0
@@ -573,14 +579,22 @@ class ModelRunner:
             z = ops.decode_grid_z(B, nkv, self.max_model_len)
             meta = self._meta(B, 0, 0, B, 0, self.max_model_len, z=z)
             idx = self.d64[L.lidx:L.lidx + B]
-            for _ in range(2):   # warm up (allocator, library handles) outside capture
-                h = self._forward(B, meta)
-                self.model.compute_logits(h.index_select(0, idx), gather=not self.vp)
+
+            def step_body(B=B, meta=meta, idx=idx):
+                # PP stages: receive from the previous stage / send to the next one as
+                # kernels over peer memory, so the whole stage step is one replay
+                hin = self.pp_link.recv(B) if not self.model.first else None
+                h = self._forward(B, meta, hin)
+                if not self.model.last:
+                    self.pp_link.send(*h)
+                    return None
+                return self.model.compute_logits(h.index_select(0, idx), gather=not self.vp)
+            for _ in range(2):   # warm up (allocator, library handles) outside capture;
+                step_body()      # PP: every stage runs the same warm-ups, in bucket order
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, pool=self.graph_pool):
-                h = self._forward(B, meta)
-                logits = self.model.compute_logits(h.index_select(0, idx), gather=not self.vp)
+                logits = step_body()
             self.graphs[B] = (g, logits)
         torch.cuda.synchronize()
         return time.time() - t0

@@ -99,6 +99,12 @@ class Worker:
                                   self.max_model_len, cfg.max_num_seqs, cfg.token_budget(),
                                   cfg.enforce_eager, cfg.cuda_graph_max_bs,
                                   kv_dtype=cfg.kv_torch_dtype(self.dtype))
+        if (self.ps.pp_size > 1 and dev.type == "cuda" and not cfg.enforce_eager
+                and cfg.nnodes == 1):
+            # per-stage decode graphs: the stage handoff as kernels over peer memory
+            from ..parallel.pp_handoff import maybe_init_pp_handoff
+            self.runner.pp_link = maybe_init_pp_handoff(self.ps, dev, self.runner.graph_max_bs,
+                                                        self.mcfg.hidden_size, self.dtype)
 
     def profile(self) -> int:
         if self.cfg.num_gpu_blocks_override:
@@ -115,6 +121,9 @@ class Worker:
         return self.runner.run(plan)
 
     def release(self) -> None:
+        if self.runner.pp_link is not None:
+            self.runner.pp_link.close()
+            self.runner.pp_link = None
         if self.ep_a2a is not None:
             self.ep_a2a.close()
             self.ep_a2a = None
@@ -314,8 +323,8 @@ class _DistExecutorBase:
         if self.watchdog is not None:
             self.watchdog.step_begin()
         # sticky error words of the peer-memory collectives (xGMI all-reduce, EP exchange)
-        checks = [c for c in (comm.get_custom_allreduce(), getattr(self.worker, "ep_a2a", None))
-                  if c is not None]
+        checks = [c for c in (comm.get_custom_allreduce(), getattr(self.worker, "ep_a2a", None),
+                              self.worker.runner.pp_link) if c is not None]
         for c in checks:
             c.enqueue_err_read()
 

@@ -90,12 +90,19 @@ def tp_broadcast(x: torch.Tensor, src_local: int = 0) -> torch.Tensor:
     return x
 
 
+def _host_staged() -> bool:
+    """gloo point-to-point moves host memory only: GPU tensors are staged through the
+    host (the KGC_DIST_BACKEND=gloo harness that puts several ranks on one GPU)."""
+    return dist.get_backend() == "gloo"
+
+
 def pp_send(tensors: list[torch.Tensor]) -> None:
     """C5: stage boundary, hidden + residual to the next stage."""
     s = get_state()
     dst = getattr(s, "global_base", 0) + s.rank + s.tp_size
     for t in tensors:
-        dist.send(t.contiguous(), dst=dst)
+        t = t.contiguous()
+        dist.send(t.cpu() if t.is_cuda and _host_staged() else t, dst=dst)
 
 
 def pp_recv(shapes: list[tuple], dtype: torch.dtype, device) -> list[torch.Tensor]:
@@ -104,7 +111,12 @@ def pp_recv(shapes: list[tuple], dtype: torch.dtype, device) -> list[torch.Tenso
     out = []
     for shp in shapes:
         t = torch.empty(shp, dtype=dtype, device=device)
-        dist.recv(t, src=src)
+        if t.is_cuda and _host_staged():
+            h = torch.empty(shp, dtype=dtype)
+            dist.recv(h, src=src)
+            t.copy_(h)
+        else:
+            dist.recv(t, src=src)
         out.append(t)
     return out
 

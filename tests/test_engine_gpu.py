@@ -322,3 +322,42 @@ def test_mixtral_ep2_graphs_on_one_gpu(gpu, tmp_path, monkeypatch):
     # computes eagerly; vs TP = 1 only rounding differs (near-tie expert flips late on)
     assert outs[(2, "1")] == outs[(2, "0")], outs
     assert all(x[:3] == y[:3] for x, y in zip(outs[(1, "1")], outs[(2, "1")])), outs
+
+
+def test_pp2_stage_graphs_on_one_gpu(gpu, tmp_path, monkeypatch):
+    """PP = 2 on the GPU, two stage ranks on cuda:0: each stage captures its decode step
+    (receive kernel -> its layers -> send kernel / LM head) as hipGraphs with the handoff
+    over peer memory, the engine keeps both micro-batches in flight, and greedy output
+    equals the single-GPU engine (the stage split does not change the arithmetic)."""
+    import json
+    import os
+    from safetensors.torch import save_file
+    from kubernetes_gpu_cluster_amd.engine.llm_engine import LLM
+    cfg = PRESETS["tiny-llama"]
+    d = str(tmp_path / "m")
+    os.makedirs(d)
+    save_file({k: v.contiguous() for k, v in full_state_dict_random(cfg, seed=5, std=0.15).items()},
+              os.path.join(d, "model.safetensors"))
+    json.dump({"model_type": "llama", "hidden_size": cfg.hidden_size,
+               "num_hidden_layers": cfg.num_layers, "num_attention_heads": cfg.num_heads,
+               "num_key_value_heads": cfg.num_kv_heads, "head_dim": cfg.head_dim,
+               "intermediate_size": cfg.intermediate_size, "vocab_size": cfg.vocab_size,
+               "max_position_embeddings": 512, "rope_theta": cfg.rope_theta,
+               "rms_norm_eps": cfg.rms_eps, "eos_token_id": 2, "bos_token_id": 1},
+              open(os.path.join(d, "config.json"), "w"))
+    prompts = [list(range(3, 40)), [5, 6, 7] * 20, [9, 10, 11], [4] * 9]
+    sp = [SamplingParams(temperature=0, max_tokens=12, ignore_eos=True)] * 4
+    monkeypatch.setenv("KGC_DIST_BACKEND", "gloo")
+    outs = {}
+    for pp in (1, 2):
+        llm = LLM(d, device="cuda", dtype="bfloat16", pipeline_parallel_size=pp,
+                  max_model_len=256, max_num_seqs=4, max_num_batched_tokens=128,
+                  num_gpu_blocks_override=64)
+        outs[pp] = [o.output_token_ids for o in llm.generate(prompts, sp)]
+        if pp == 2:
+            r = llm.engine.executor.runner
+            assert r.pp_link is not None, "PP peer-memory handoff not set up"
+            assert r.stats["graph_steps"] > 0, r.stats
+            r.pp_link.check()
+        llm.shutdown()
+    assert outs[2] == outs[1], outs
