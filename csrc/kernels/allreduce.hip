@@ -121,15 +121,19 @@ __global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArPtrs P, int ran
   if constexpr (!TWO) {
     for (int64_t v = first; v < nvec; v += stride) io[v] = reduce_at(v);
   } else {
+    // Every phase walks the SAME element -> block mapping as the copy-in (element v
+    // belongs to block (v / AR_THREADS) % AR_MAX_BLOCKS): block b's barrier then covers
+    // exactly the elements block b reads.  (Indexing the segment from its own start
+    // would hand block b elements another block copied in, whose peers it never waited
+    // for -- a race whenever the segment start is not a multiple of the grid stride.)
     const int64_t seg = nvec / NR;    // host guarantees nvec % NR == 0
-    const int64_t lo = (int64_t)rank * seg;
-    for (int64_t v = first; v < seg; v += stride) mine[lo + v] = reduce_at(lo + v);
+    const int64_t lo = (int64_t)rank * seg, hi = lo + seg;
+    for (int64_t v = first; v < nvec; v += stride)
+      if (v >= lo && v < hi) mine[v] = reduce_at(v);
     ar_barrier<NR>(P, rank, 1, epoch);
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      const u32x4* src = reinterpret_cast<const u32x4*>(P.data[r]) + par_off + (int64_t)r * seg;
-      u32x4* dst = io + (int64_t)r * seg;
-      for (int64_t v = first; v < seg; v += stride) dst[v] = ld_peer(src + v);
+    for (int64_t v = first; v < nvec; v += stride) {
+      const int r = (int)(v / seg);   // owner of the reduced segment holding v
+      io[v] = ld_peer(reinterpret_cast<const u32x4*>(P.data[r]) + par_off + v);
     }
   }
   if (threadIdx.x == 0) self->counter[blockIdx.x] = epoch;
