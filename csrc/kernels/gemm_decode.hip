@@ -256,12 +256,12 @@ __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
 //   waves 12-13 weight loaders: an NB-slot B ring (NB - 2 steps in flight: 32-48 KB of
 //               HBM reads per CU at all times);
 // each loader group waits only on its own vmcnt, and one s_barrier per step joins all 14.
-template <typename T, int BM, int BN, int EPI, int NB>
+template <typename T, int BM, int BN, int EPI, int NB, int NA = 3>
 __global__ __launch_bounds__(896, 1) void dgemm_sl_kernel(
     void* __restrict__ Cv, const T* __restrict__ X, const T* __restrict__ W, int M, int N,
     int K, int64_t ldx, int S, int MB, int64_t slice_stride) {
   constexpr int MT = BM / 4 / 16, NT = BN / 2 / 16;
-  constexpr int NA = 3;
+  static_assert(NA >= 2 && NB >= 2, "rings of at least two slots");
   constexpr int LA = BM / 8 / 4, LB = BN / 8 / 2;   // DMAs per A / B loader wave per step
   constexpr int A_SLOT = BM * DG_ROWB, B_SLOT = BN * DG_ROWB;
   static_assert(NA * A_SLOT + NB * B_SLOT <= 163840, "LDS rings exceed 160 KiB");
@@ -394,14 +394,14 @@ __global__ __launch_bounds__(896, 1) void dgemm_sl_kernel(
   }
 }
 
-template <typename T, int BM, int BN, int NB>
+template <typename T, int BM, int BN, int NB, int NA = 3>
 void dgemm_sl_cfg(int epi, void* C, const void* X, const void* W, int M, int N, int K,
                   int64_t ldx, int S, int64_t ss, hipStream_t s) {
   const int MB = (M + BM - 1) / BM;
   const dim3 grid((unsigned)(MB * (N / BN) * S));
 #define DG_SL(E)                                                                       \
-  dgemm_sl_kernel<T, BM, BN, E, NB><<<grid, 896, 0, s>>>(C, (const T*)X, (const T*)W, M, \
-                                                          N, K, ldx, S, MB, ss)
+  dgemm_sl_kernel<T, BM, BN, E, NB, NA><<<grid, 896, 0, s>>>(C, (const T*)X, (const T*)W, M, \
+                                                              N, K, ldx, S, MB, ss)
   if (epi == EPI_PARTIAL) DG_SL(EPI_PARTIAL);
   else if (epi == EPI_OUT) DG_SL(EPI_OUT);
   else DG_SL(EPI_SILU);
@@ -430,7 +430,8 @@ __global__ __launch_bounds__(256) void dgemm_pack_kernel(T* __restrict__ P,
 
 // Tile table: id -> (BM, BN, packed weights); ids 6, 7 = 4, 5 with 4 loader waves;
 // ids 8, 9 = split loaders (dgemm_sl_kernel) 256 x 128 with a 4- / 128 x 128 with a 6-slot
-// weight ring
+// weight ring.  (A 2-slot activation ring with the LDS given to a 6- / 8-slot weight ring
+// measured 5-10 % slower on every shape: profiles/k9m_dgemm_bench_r2_sweep.jsonl.)
 constexpr int kNumCfgs = 10;
 static const int kCfg[kNumCfgs][3] = {{256, 128, 0}, {256, 64, 0},  {128, 128, 0}, {128, 64, 0},
                                       {256, 128, 1}, {128, 128, 1}, {256, 128, 1}, {128, 128, 1},
