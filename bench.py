@@ -236,11 +236,19 @@ def _note(msg: str) -> None:
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def _free_port() -> int:
+def _free_port(local_rank: int, slot: int) -> int:
+    """A free port from this rank's own range (ranks of one node never race for the
+    same number): 18000 + 64 * local_rank + slot, stepping by 1024 when busy."""
     import socket
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    for step in range(16):
+        port = 18000 + 64 * local_rank + slot + 1024 * step
+        with socket.socket() as s:
+            try:
+                s.bind(("127.0.0.1", port))
+            except OSError:
+                continue
+            return port
+    raise RuntimeError(f"no free port for rank {local_rank}")
 
 
 def _server_devices(local_rank: int, tp: int, cpu: bool):
@@ -299,7 +307,7 @@ def main_service(args):
     elapsed = 0.0
     try:
         if leader:
-            api_port, router_port = _free_port(), _free_port()
+            api_port, router_port = _free_port(local_rank, 0), _free_port(local_rank, 1)
             api_url = f"http://127.0.0.1:{api_port}"
             url = f"http://127.0.0.1:{router_port}"
             procs.append(sc.start_api_server(args.model, api_port,
