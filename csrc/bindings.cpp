@@ -219,7 +219,8 @@ void prefill_attention(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Ten
                                 (float)v_scale, (int)k_cache.size(0), stream());
 }
 
-void sample(Tensor out, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds) {
+void sample(Tensor out, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds,
+            bool thresholds) {
   check_gpu(logits, "logits");
   c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits [B, V] with dense rows");
@@ -231,6 +232,25 @@ void sample(Tensor out, Tensor logits, Tensor temperature, Tensor top_k, Tensor 
   TORCH_CHECK(seeds.scalar_type() == at::kLong && seeds.numel() >= B, "seeds int64");
   TORCH_CHECK(B <= 65535 * 256 && logits.size(1) < INT32_MAX, "kgc.sample: shape");
   if (B == 0) return;
+  if (thresholds && kgc::sample_coop_splits((int)B) > 0) {
+    // rows with top-k / top-p: the cooperative kernel splits the threshold passes over
+    // the row's workgroups (per-row workspace from the caching allocator)
+    Tensor partial = at::empty({B * kgc::sample_coop_splits((int)B)}, logits.options().dtype(at::kLong));
+    // one persistent zeroed workspace per device (256 rows); every call leaves it zeroed
+    static std::vector<Tensor> wss(64);
+    const int dev = logits.device().index();
+    TORCH_CHECK(dev >= 0 && dev < 64, "device index");
+    if (!wss[dev].defined())
+      wss[dev] = at::zeros({256 * (int64_t)kgc::sample_coop_ws_bytes()},
+                           logits.options().dtype(at::kByte));
+    Tensor ws = wss[dev];
+    kgc::launch_sample_coop(dt_code(logits), out.data_ptr<int64_t>(),
+                            reinterpret_cast<uint64_t*>(partial.data_ptr<int64_t>()), ws.data_ptr(),
+                            logits.data_ptr(), logits.stride(0), (int)B, (int)logits.size(1),
+                            temperature.data_ptr<float>(), top_k.data_ptr<int>(),
+                            top_p.data_ptr<float>(), seeds.data_ptr<int64_t>(), stream());
+    return;
+  }
   // per-(row, vocab split) candidates; from the caching allocator, so graph capture
   // gives the workspace a fixed address like any other captured temporary
   Tensor partial = at::empty({B * kgc::sample_splits((int)B)}, logits.options().dtype(at::kLong));
@@ -810,7 +830,7 @@ TORCH_LIBRARY(kgc, m) {
         "Tensor block_tables, Tensor query_start_loc, Tensor seq_lens, Tensor work_seq, "
         "Tensor work_mblk, float scale, float k_scale=1.0, float v_scale=1.0) -> ()");
   m.def("sample(Tensor(a!) out, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, "
-        "Tensor seeds) -> ()");
+        "Tensor seeds, bool thresholds=True) -> ()");
   m.def("sample_vp(Tensor(a!) packed, Tensor logits, int V, Tensor temperature, Tensor seeds, "
         "int vocab_off) -> ()");
   m.def("sample_vp_unpack(Tensor(a!) out, Tensor packed) -> ()");

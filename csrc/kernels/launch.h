@@ -43,6 +43,15 @@ int sample_splits(int B);   // vocabulary splits per row; partial holds B * spli
 void launch_sample(int dtype, int64_t* out, uint64_t* partial, const void* logits,
                    int64_t row_stride, int B, int V, const float* temperature, const int* top_k,
                    const float* top_p, const int64_t* seeds, hipStream_t s);
+// cooperative sampler for rows with top-k / top-p (B <= 256): ws holds
+// B * sample_coop_ws_bytes() bytes, all-zero before the first call (the kernel leaves it
+// zeroed), partial B * coop splits words
+int sample_coop_ws_bytes();
+int sample_coop_splits(int B);
+void launch_sample_coop(int dtype, int64_t* out, uint64_t* partial, void* ws, const void* logits,
+                        int64_t row_stride, int B, int V, const float* temperature,
+                        const int* top_k, const float* top_p, const int64_t* seeds,
+                        hipStream_t s);
 // vocab-parallel: per-row packed (value, global index) of this rank's shard (biased for
 // a signed MAX all-reduce), and the unpack after that all-reduce
 void launch_sample_vp(int dtype, int64_t* packed, uint64_t* partial, const void* logits,

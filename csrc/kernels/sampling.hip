@@ -16,6 +16,7 @@
 #include "common.h"
 #include "launch.h"
 #include <algorithm>
+#include <cstdlib>
 
 namespace kgc {
 
@@ -273,6 +274,277 @@ __global__ __launch_bounds__(256) void sample_merge_kernel(int64_t* __restrict__
   for (int y = 0; y < S; ++y) best = max(best, partial[(int64_t)b * S + y]);
   const uint32_t idx = ~(uint32_t)(best & 0xffffffffu);
   out[b] = (best == 0 || idx >= 0x7fffffffu) ? 0 : (int64_t)idx;
+}
+
+// ---------------------------------------------------------------------------------------
+// Cooperative variant for rows with top-k / top-p: the S workgroups of a row split the
+// threshold passes too (each visits V / S logits per pass) and combine their partial
+// histograms in a per-row global workspace, with a workgroup barrier per pass (counters
+// in the zero-initialised workspace; B * S <= 256, so every workgroup of the grid is
+// co-resident and the barriers cannot deadlock; spins are bounded anyway).  The
+// single-workgroup kernel above computes every threshold over the whole row in each of
+// the S workgroups: ~230 us per top-p row at batch 1.
+struct CoopWs {
+  uint32_t bar[16];
+  uint32_t maxkey;
+  uint32_t err;
+  float z;
+  float pad;
+  float hist_k[SMP_NBIN];
+  float hist_p[SMP_NBIN];
+  float hist_r[8][256];
+};
+
+int sample_coop_ws_bytes() { return (int)sizeof(CoopWs); }
+
+template <typename T>
+__global__ __launch_bounds__(SMP_NT) void sample_coop_kernel(
+    uint64_t* __restrict__ partial, const T* __restrict__ logits, int64_t row_stride, int V,
+    const float* __restrict__ temperature, const int* __restrict__ top_k,
+    const float* __restrict__ top_p, const int64_t* __restrict__ seeds, CoopWs* __restrict__ wsa) {
+  __shared__ float red_v[SMP_NT / 64];
+  __shared__ int red_i[SMP_NT / 64];
+  __shared__ float hist_f[256];
+  __shared__ float hist_d[SMP_NBIN];
+  __shared__ float scan_w[SMP_NT / 64];
+  __shared__ uint32_t sel_bin;
+  __shared__ float sel_f;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const T* row = logits + (int64_t)b * row_stride;
+  CoopWs* ws = wsa + b;
+  const float temp = temperature[b];
+  const bool greedy = temp <= 1e-5f;
+  const int k = greedy ? 0 : top_k[b];
+  const float p = greedy ? 1.f : top_p[b];
+  const bool use_k = k > 0 && k < V;
+  const bool use_p = p < 1.f;
+  const int S = gridDim.y, y = blockIdx.y;
+  const int i_lo = (int)((int64_t)V * y / S);
+  const int i_hi = (int)((int64_t)V * (y + 1) / S);
+  int nbar = 0;
+  // all S workgroups of this row: arrive, wait for the others (bounded), acquire
+  auto row_barrier = [&]() {
+    __syncthreads();
+    if (tid == 0) {
+      __threadfence();
+      uint32_t* c = &ws->bar[nbar];
+      atomicAdd(c, 1u);
+      int it = 0;
+      while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)S) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++it > (1 << 24)) {
+          atomicOr(&ws->err, 1u);
+          break;
+        }
+      }
+      __threadfence();
+    }
+    __syncthreads();
+    ++nbar;
+  };
+  auto gload = [](const float* p_) { return __hip_atomic_load(p_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+
+  float thr = -INFINITY;
+  if (use_k || use_p) {
+    float mx = -INFINITY;
+    visit_row(row, i_lo, i_hi, tid, [&](int, float r) { mx = fmaxf(mx, r); });
+    mx = block_max<SMP_NT>(mx, red_v);
+    if (tid == 0) atomicMax(&ws->maxkey, ord_key(mx));
+    row_barrier();
+    mx = key_val(__hip_atomic_load(&ws->maxkey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const float it = 1.f / temp;
+    auto dbin = [&](float x) -> int {
+      const float d = (mx - x) * it * (float)SMP_DB;
+      return d < (float)(SMP_NBIN - 1) ? (int)d : SMP_NBIN - 1;
+    };
+    auto cross_dist = [&](float target) {
+      if (tid == 0) { sel_bin = SMP_NBIN - 1; sel_f = 0.f; }
+      const float h0 = hist_d[2 * tid], h1 = hist_d[2 * tid + 1];
+      const float incl = block_scan_incl(h0 + h1, scan_w);
+      const float excl = incl - h0 - h1;
+      if (excl < target && excl + h0 >= target) { sel_bin = 2 * tid; sel_f = excl; }
+      else if (excl + h0 < target && incl >= target) { sel_bin = 2 * tid + 1; sel_f = excl + h0; }
+      __syncthreads();
+    };
+    auto cross_radix = [&](const float* h, float start, float target, int lowest, int fallback) {
+      const int pos = tid, bin = 255 - pos;
+      const float v = (pos < 256 && bin >= lowest) ? h[bin] : 0.f;
+      const float incl = start + block_scan_incl(v, scan_w);
+      const float excl = incl - v;
+      if (tid == SMP_NT - 1) { sel_bin = fallback; sel_f = incl; }
+      __syncthreads();
+      if (pos < 256 && bin >= lowest && excl < target && incl >= target) {
+        sel_bin = bin;
+        sel_f = excl;
+      }
+      __syncthreads();
+    };
+    // this workgroup's LDS histogram -> the row's global one (non-zero bins only)
+    auto publish = [&](const float* h, float* g, int n) {
+      __syncthreads();
+      for (int j = tid; j < n; j += SMP_NT)
+        if (h[j] != 0.f) atomicAdd(&g[j], h[j]);
+    };
+    auto fetch = [&](float* h, const float* g, int n) {
+      for (int j = tid; j < n; j += SMP_NT) h[j] = gload(&g[j]);
+      __syncthreads();
+    };
+    if (use_k) {
+      for (int j = tid; j < SMP_NBIN; j += SMP_NT) hist_d[j] = 0.f;
+      __syncthreads();
+      visit_row(row, i_lo, i_hi, tid, [&](int, float r) { atomicAdd(&hist_d[dbin(r)], 1.f); });
+      publish(hist_d, ws->hist_k, SMP_NBIN);
+      row_barrier();
+      fetch(hist_d, ws->hist_k, SMP_NBIN);
+      cross_dist((float)k);
+      const int kbin = (int)sel_bin;
+      uint32_t prefix = 0, mask = 0;
+      float remaining = (float)k - sel_f;
+      for (int q = 0, shift = 24; shift >= 0; ++q, shift -= 8) {
+        if (tid < 256) hist_f[tid] = 0.f;
+        __syncthreads();
+        visit_row(row, i_lo, i_hi, tid, [&](int, float r) {
+          const uint32_t kk = ord_key(r);
+          if (dbin(r) == kbin && (kk & mask) == prefix) atomicAdd(&hist_f[(kk >> shift) & 255], 1.f);
+        });
+        publish(hist_f, ws->hist_r[q], 256);
+        row_barrier();
+        fetch(hist_f, ws->hist_r[q], 256);
+        cross_radix(hist_f, 0.f, remaining, 0, 0);
+        remaining -= sel_f;
+        prefix |= sel_bin << shift;
+        mask |= 255u << shift;
+      }
+      thr = key_val(prefix);
+    }
+    if (use_p) {
+      for (int j = tid; j < SMP_NBIN; j += SMP_NT) hist_d[j] = 0.f;
+      __syncthreads();
+      float z = 0.f;
+      visit_row(row, i_lo, i_hi, tid, [&](int, float r) {
+        if (r >= thr) {
+          const float e = __expf((r - mx) * it);
+          z += e;
+          atomicAdd(&hist_d[dbin(r)], e);
+        }
+      });
+      z = block_sum<SMP_NT>(z, red_v);
+      if (tid == 0) atomicAdd(&ws->z, z);
+      publish(hist_d, ws->hist_p, SMP_NBIN);
+      row_barrier();
+      z = gload(&ws->z);
+      fetch(hist_d, ws->hist_p, SMP_NBIN);
+      const float target = p * z;
+      cross_dist(target);
+      const int pbin = (int)sel_bin;
+      uint32_t prefix = 0, mask = 0;
+      float above = sel_f;
+      const uint32_t kthr = ord_key(thr);
+      for (int q = 4, shift = 24; shift >= 0; ++q, shift -= 8) {
+        if (tid < 256) hist_f[tid] = 0.f;
+        __syncthreads();
+        visit_row(row, i_lo, i_hi, tid, [&](int, float r) {
+          const uint32_t kk = ord_key(r);
+          if (kk >= kthr && dbin(r) == pbin && (kk & mask) == prefix)
+            atomicAdd(&hist_f[(kk >> shift) & 255], __expf((r - mx) * it));
+        });
+        publish(hist_f, ws->hist_r[q], 256);
+        row_barrier();
+        fetch(hist_f, ws->hist_r[q], 256);
+        cross_radix(hist_f, above, target, 1, 0);
+        above = sel_f;
+        prefix |= sel_bin << shift;
+        mask |= 255u << shift;
+      }
+      thr = fmaxf(thr, key_val(prefix));
+    }
+    // The workspace is persistent and must be all-zero for the next call: the last of
+    // the row's workgroups to finish reading it clears what this call used.
+    __shared__ int last;
+    __syncthreads();
+    if (tid == 0) {
+      __threadfence();
+      last = atomicAdd(&ws->bar[15], 1u) == (uint32_t)(S - 1);
+    }
+    __syncthreads();
+    if (last) {
+      if (use_k) {
+        for (int j = tid; j < SMP_NBIN; j += SMP_NT) ws->hist_k[j] = 0.f;
+        for (int j = tid; j < 4 * 256; j += SMP_NT) ws->hist_r[j / 256][j % 256] = 0.f;
+      }
+      if (use_p) {
+        for (int j = tid; j < SMP_NBIN; j += SMP_NT) ws->hist_p[j] = 0.f;
+        for (int j = tid; j < 4 * 256; j += SMP_NT) ws->hist_r[4 + j / 256][j % 256] = 0.f;
+      }
+      if (tid < 16) ws->bar[tid] = 0;
+      if (tid == 0) {
+        ws->maxkey = 0;
+        ws->z = 0.f;
+      }
+      __threadfence();
+    }
+  }
+
+  // ---------- (Gumbel-)argmax over this workgroup's slice of the support
+  const uint64_t seed = (uint64_t)seeds[b];
+  const uint32_t key = mix32((uint32_t)seed);
+  const uint32_t hi = (uint32_t)(seed >> 32);
+  float best = -INFINITY;
+  int besti = 0x7fffffff;
+  visit_row(row, i_lo, i_hi, tid, [&](int i, float r) {
+    float x = greedy ? r : r / temp;
+    if (!greedy) {
+      if (r < thr) return;
+      const uint32_t h = mix32(mix32(key ^ (uint32_t)(i * 0x9E3779B9u)) + hi);
+      const float u = ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
+      x += -logf(-logf(u));
+    }
+    argmax_merge(best, besti, x, i);
+  });
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float v2 = __shfl_xor(best, o, 64);
+    const int i2 = __shfl_xor(besti, o, 64);
+    argmax_merge(best, besti, v2, i2);
+  }
+  if (lane == 0) { red_v[w] = best; red_i[w] = besti; }
+  __syncthreads();
+  if (tid == 0) {
+    float bv = red_v[0];
+    int bi = red_i[0];
+    for (int j = 1; j < SMP_NT / 64; ++j) argmax_merge(bv, bi, red_v[j], red_i[j]);
+    partial[(int64_t)b * S + y] = ((uint64_t)ord_key(bv) << 32) | (uint32_t)(~(uint32_t)bi);
+  }
+}
+
+// workgroups per row of the cooperative sampler: the whole grid must be co-resident
+// (one 1024-thread workgroup per CU is always available): B * S <= 256
+// Workgroups per row (0: use the single-workgroup-threshold kernel).  Measured on
+// MI355X (profiles/sample_microbench.jsonl): 16 per row up to B = 16, then 256 / B; above
+// B = 128 one cooperative workgroup per row loses to the older kernel, which splits the
+// argmax over 2 workgroups per row (B * S must stay <= 256 for co-residency).
+int sample_coop_splits(int B) {
+  if (B > 128) return 0;
+  return std::max(1, std::min(16, 256 / B));
+}
+
+void launch_sample_coop(int dtype, int64_t* out, uint64_t* partial, void* ws, const void* logits,
+                        int64_t row_stride, int B, int V, const float* temperature,
+                        const int* top_k, const float* top_p, const int64_t* seeds,
+                        hipStream_t s) {
+  if (B == 0) return;
+  const dim3 grid(B, sample_coop_splits(B));
+  CoopWs* w = reinterpret_cast<CoopWs*>(ws);       // persistent, all-zero between calls
+  if (dtype == DT_BF16)
+    sample_coop_kernel<bf16><<<grid, SMP_NT, 0, s>>>(partial, (const bf16*)logits, row_stride, V,
+                                                     temperature, top_k, top_p, seeds, w);
+  else if (dtype == DT_F16)
+    sample_coop_kernel<f16><<<grid, SMP_NT, 0, s>>>(partial, (const f16*)logits, row_stride, V,
+                                                    temperature, top_k, top_p, seeds, w);
+  else
+    sample_coop_kernel<float><<<grid, SMP_NT, 0, s>>>(partial, (const float*)logits, row_stride,
+                                                      V, temperature, top_k, top_p, seeds, w);
+  sample_merge_kernel<<<(B + 255) / 256, 256, 0, s>>>(out, partial, B, grid.y);
 }
 
 // Vocab-parallel: the row's packed candidate, biased (top bit flipped) so that a SIGNED

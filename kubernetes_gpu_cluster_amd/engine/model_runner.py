@@ -333,7 +333,11 @@ class ModelRunner:
             for s in samplers:
                 if needs_counts(s.params):
                     s.proc_slot = s.slot
-        bcast = int(proc is not None and self.ps.tp_size > 1)
+        # TP > 1: ranks adopt the driver's ids when it processes logits, and for top-k /
+        # top-p rows (their float histograms are summed in a hardware-dependent order)
+        thr = any((0 < s.params.top_k < self.mcfg.vocab_size) or s.params.top_p < 1.0
+                  for s in samplers)
+        bcast = int((proc is not None or thr) and self.ps.tp_size > 1)
         V = self.mcfg.vocab_size
         vp = int(self.vp and lp is None and proc is None
                  and all((s.params.top_k <= 0 or s.params.top_k >= V) and s.params.top_p >= 1.0
@@ -440,7 +444,8 @@ class ModelRunner:
         out = self.sample_out[: plan.S]
         res = ops.sample(logits, self.df[L.temp:L.temp + plan.S], self.d32[L.topk:L.topk + plan.S],
                          self.df[L.topp:L.topp + plan.S], self.d64[L.seeds:L.seeds + plan.S],
-                         out=out if self.is_gpu else None)
+                         out=out if self.is_gpu else None,
+                         thresholds=self._plan_thresholds(plan))
         if plan.tok_bcast:
             comm.tp_broadcast(res, 0)          # every TP rank continues with the driver's ids
         if plan.proc and self.model.last:
@@ -451,6 +456,13 @@ class ModelRunner:
         else:
             self._last_lp = None
         return res
+
+    def _plan_thresholds(self, plan: StepPlan) -> bool:
+        """Does any sampled row of this step use top-k / top-p (host-side blobs)?"""
+        L, S, V = self.L, plan.S, self.mcfg.vocab_size
+        k = plan.i32[L.topk:L.topk + S]
+        p = plan.f32[L.topp:L.topp + S]
+        return bool(((k > 0) & (k < V)).any() or (p < 1.0).any())
 
     def _run_fake(self, plan: StepPlan) -> Optional[torch.Tensor]:
         shp = (plan.B or plan.T, self.mcfg.hidden_size)

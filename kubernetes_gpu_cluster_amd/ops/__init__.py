@@ -237,13 +237,16 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
 # ------------------------------------------------------------------ sampling
 def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
            top_p: torch.Tensor, seeds: torch.Tensor,
-           out: Optional[torch.Tensor] = None) -> torch.Tensor:
+           out: Optional[torch.Tensor] = None, thresholds: bool = True) -> torch.Tensor:
+    """K10.  ``thresholds=False`` promises that no row uses top-k / top-p (the caller
+    knows from the host-side plan): the single-pass kernel then runs; otherwise the
+    cooperative kernel splits each row's threshold passes over its workgroups."""
     if not _gpu(logits):
         return ref.sample(logits, temperature, top_k, top_p, seeds)
     B = logits.shape[0]
     if out is None:
         out = torch.empty(B, dtype=torch.int64, device=logits.device)
-    _k().sample(out, logits, temperature, top_k, top_p, seeds)
+    _k().sample(out, logits, temperature, top_k, top_p, seeds, thresholds)
     return out
 
 

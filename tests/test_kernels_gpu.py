@@ -210,13 +210,17 @@ def test_prefill_matches_dense(gpu):
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
-def test_sample(gpu, dt):
+@pytest.mark.parametrize("B", [16, 1, 4, 260])
+def test_sample(gpu, dt, B):
+    """B <= 256: the cooperative kernel (threshold passes split over each row's
+    workgroups, per-row barriers); B = 260: the single-workgroup-per-threshold kernel."""
     torch.manual_seed(6)
-    B, V = 16, 128256
+    V = 128256
     logits = (torch.randn(B, V, device=gpu) * 3).to(dt)
-    temp = torch.tensor([0.0, 1.0, 0.7, 1.3] * 4, device=gpu)
-    top_k = torch.tensor([-1, -1, 50, -1] * 4, dtype=torch.int32, device=gpu)
-    top_p = torch.tensor([1.0, 1.0, 1.0, 0.9] * 4, device=gpu)
+    reps = (B + 3) // 4
+    temp = torch.tensor([0.0, 1.0, 0.7, 1.3] * reps, device=gpu)[:B]
+    top_k = torch.tensor([-1, -1, 50, -1] * reps, dtype=torch.int32, device=gpu)[:B]
+    top_p = torch.tensor([1.0, 1.0, 1.0, 0.9] * reps, device=gpu)[:B]
     seeds = torch.arange(B, dtype=torch.int64, device=gpu) * 7919 + (5 << 32)
     got = ops.sample(logits, temp, top_k, top_p, seeds).cpu()
     exp = ref.sample(logits.cpu(), temp.cpu(), top_k.cpu(), top_p.cpu(), seeds.cpu())
@@ -225,6 +229,13 @@ def test_sample(gpu, dt):
     exact = [i for i in range(B) if i % 4 != 3]
     assert got[exact].tolist() == exp[exact].tolist()
     assert (got == exp).float().mean() >= 0.9
+    # rows without thresholds: the single-pass path picks the same ids
+    plain = [i for i in range(B) if i % 4 in (0, 1)]
+    if plain:
+        idx = torch.tensor(plain, device=gpu)
+        g2 = ops.sample(logits[idx].contiguous(), temp[idx], top_k[idx], top_p[idx], seeds[idx],
+                        thresholds=False).cpu()
+        assert g2.tolist() == got[plain].tolist()
 
 
 def test_sample_distribution(gpu):
