@@ -68,6 +68,10 @@ def parse():
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--prefix-caching", type=int, default=1, choices=[0, 1],
                     help="automatic prefix caching (engine default: on; random prompts never hit)")
+    ap.add_argument("--prefill-first", dest="prefill_first", action="store_true", default=True,
+                    help="engine scheduling (default, as in deploy/values/values-llama3-8b-"
+                         "tp1.yaml): decodes sit out while prompts wait for a slot")
+    ap.add_argument("--no-prefill-first", dest="prefill_first", action="store_false")
     ap.add_argument("--log-level", default="WARNING",
                     help="python logging level on stderr (INFO shows the GEMM tuner's choices)")
     ap.add_argument("--mode", default="service", choices=["service", "engine"],
@@ -148,7 +152,8 @@ def main_engine(args):
                        max_num_batched_tokens=args.max_num_batched_tokens,
                        gpu_memory_utilization=args.gpu_memory_utilization,
                        enforce_eager=args.enforce_eager, random_init=True, seed=0,
-                       device=args.device, enable_prefix_caching=bool(args.prefix_caching))
+                       device=args.device, enable_prefix_caching=bool(args.prefix_caching),
+                       prefill_first=args.prefill_first)
     engine = None
     if tp > 1:
         assert world % tp == 0
@@ -220,7 +225,8 @@ def main_engine(args):
                        "parallelism": f"dp{replicas}" if tp == 1 else f"tp{tp}" + (f"xdp{replicas}" if replicas > 1 else ""),
                        "max_num_seqs": args.max_num_seqs,
                        "max_num_batched_tokens": args.max_num_batched_tokens,
-                       "cuda_graphs": not args.enforce_eager},
+                       "cuda_graphs": not args.enforce_eager,
+                       "scheduling": "prefill-first" if args.prefill_first else "decode-first"},
         }
         line = json.dumps(out)
         print(line, flush=True)
@@ -272,6 +278,8 @@ def _engine_args(args, cpu: bool) -> list:
         ea.append("--no-enable-prefix-caching")
     if args.enforce_eager:
         ea.append("--enforce-eager")
+    if args.prefill_first:
+        ea.append("--prefill-first")
     if args.api_server_count:
         ea += ["--api-server-count", str(args.api_server_count)]
     if cpu:
@@ -409,6 +417,7 @@ def main_service(args):
                        "max_num_seqs": args.max_num_seqs,
                        "max_num_batched_tokens": args.max_num_batched_tokens,
                        "cuda_graphs": not args.enforce_eager,
+                       "scheduling": "prefill-first" if args.prefill_first else "decode-first",
                        "endpoint": "router -> /v1/completions (stream)"},
         }
         line = json.dumps(out)

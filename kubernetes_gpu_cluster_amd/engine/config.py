@@ -37,6 +37,7 @@ class EngineConfig:
     max_num_seqs: int = 256
     max_num_batched_tokens: Optional[int] = None
     enable_chunked_prefill: bool = True
+    prefill_first: bool = False           # decodes sit out while prompts wait (scheduler.py)
     enable_prefix_caching: bool = True    # vLLM V1 default: reuse cached KV of shared prefixes
     enforce_eager: bool = False
     disable_custom_all_reduce: bool = False
@@ -114,6 +115,9 @@ def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     a("--enable-chunked-prefill", dest="enable_chunked_prefill", action="store_true",
       default=True)
     a("--no-enable-chunked-prefill", dest="enable_chunked_prefill", action="store_false")
+    a("--prefill-first", action="store_true",
+      help="while prompts wait for a free sequence slot, running sequences skip decode steps "
+           "and the token budget goes to prefill (lower TTFT under bursts)")
     a("--enable-prefix-caching", dest="enable_prefix_caching", action="store_true", default=True)
     a("--no-enable-prefix-caching", dest="enable_prefix_caching", action="store_false")
     a("--enforce-eager", action="store_true")
@@ -149,6 +153,7 @@ def config_from_args(ns: argparse.Namespace) -> EngineConfig:
         gpu_memory_utilization=ns.gpu_memory_utilization, block_size=ns.block_size,
         max_num_seqs=ns.max_num_seqs, max_num_batched_tokens=ns.max_num_batched_tokens,
         enable_chunked_prefill=ns.enable_chunked_prefill, enforce_eager=ns.enforce_eager,
+        prefill_first=ns.prefill_first,
         enable_prefix_caching=ns.enable_prefix_caching,
         disable_custom_all_reduce=ns.disable_custom_all_reduce,
         trust_remote_code=ns.trust_remote_code, kv_cache_dtype=ns.kv_cache_dtype, seed=ns.seed,

@@ -91,10 +91,11 @@ class LLMEngine:
         if self.pp_depth > 1:
             self.scheduler = VirtualSchedulers(self.pp_depth, self.bm, cfg.max_num_seqs,
                                                cfg.token_budget(), self.max_model_len,
-                                               cfg.enable_chunked_prefill)
+                                               cfg.enable_chunked_prefill, cfg.prefill_first)
         else:
             self.scheduler = Scheduler(self.bm, cfg.max_num_seqs, cfg.token_budget(),
-                                       self.max_model_len, cfg.enable_chunked_prefill)
+                                       self.max_model_len, cfg.enable_chunked_prefill,
+                                       cfg.prefill_first)
         self._pp_inflight: list = [None] * self.pp_depth
         self._vnext = 0
         self.seqs: dict[str, Sequence] = {}

@@ -45,8 +45,12 @@ class ScheduledBatch:
 
 class Scheduler:
     def __init__(self, block_manager: BlockManager, max_num_seqs: int, token_budget: int,
-                 max_model_len: int, chunked_prefill: bool = True):
+                 max_model_len: int, chunked_prefill: bool = True, prefill_first: bool = False):
         self.bm = block_manager
+        # prefill-first: while prompts wait and a sequence slot is free, decoding sequences
+        # sit the step out and the whole token budget goes to prefill (lower TTFT under a
+        # burst, at the cost of the running sequences' TPOT)
+        self.prefill_first = prefill_first
         self.max_num_seqs = max_num_seqs
         self.token_budget = token_budget
         self.max_model_len = max_model_len
@@ -81,6 +85,15 @@ class Scheduler:
         self.waiting.appendleft(seq)
 
     def schedule(self) -> ScheduledBatch:
+        defer = (self.prefill_first and bool(self.waiting)
+                 and len(self.running) < self.max_num_seqs)
+        batch = self._schedule(defer)
+        if defer and batch.is_empty:
+            # nothing admissible (e.g. the KV pool is full): decode as usual
+            batch = self._schedule(False)
+        return batch
+
+    def _schedule(self, defer_decodes: bool) -> ScheduledBatch:
         budget = self.token_budget
         prefills: list[tuple[Sequence, int]] = []
         decodes: list[Sequence] = []
@@ -89,6 +102,9 @@ class Scheduler:
         while i < len(self.running) and budget > 0:
             seq = self.running[i]
             remaining = seq.num_tokens - seq.num_computed
+            if defer_decodes and remaining == 1:
+                i += 1
+                continue
             n = 1 if remaining == 1 else min(remaining, budget)
             scheduled = True
             while not self.bm.can_allocate(seq, seq.num_computed + n):
@@ -152,10 +168,10 @@ class VirtualSchedulers:
     each step still has the full token budget."""
 
     def __init__(self, n: int, block_manager: BlockManager, max_num_seqs: int, token_budget: int,
-                 max_model_len: int, chunked_prefill: bool = True):
+                 max_model_len: int, chunked_prefill: bool = True, prefill_first: bool = False):
         per = max(1, max_num_seqs // n)
-        self.scheds = [Scheduler(block_manager, per, token_budget, max_model_len, chunked_prefill)
-                       for _ in range(n)]
+        self.scheds = [Scheduler(block_manager, per, token_budget, max_model_len, chunked_prefill,
+                                 prefill_first) for _ in range(n)]
 
     def __len__(self) -> int:
         return len(self.scheds)

@@ -319,3 +319,34 @@ def test_engine_prefix_cache_with_preemption(monkeypatch):
     assert b.engine.scheduler.num_preemptions > 0
     b.shutdown()
     assert got == ref
+
+
+def test_prefill_first_policy():
+    """--prefill-first: while prompts wait for a slot, running sequences skip their decode
+    and the budget goes to prefill; with nothing admissible they decode as usual, and the
+    output is the same as the default policy (greedy)."""
+    from kubernetes_gpu_cluster_amd.engine.llm_engine import LLM
+    sp = SamplingParams(temperature=0, max_tokens=4, ignore_eos=True)
+    bm = BlockManager(64, 16, 8, 16, enable_prefix_caching=False)
+    sc = Scheduler(bm, 8, 32, 256, True, prefill_first=True)
+    a = Sequence("a", list(range(3, 19)), sp, None, 256)
+    sc.add(a)
+    b1 = sc.schedule()
+    assert [s.request_id for s, _ in b1.prefills] == ["a"]
+    a.num_computed += 16
+    a.output_token_ids.append(7)            # a now decodes
+    sc.add(Sequence("b", list(range(3, 35)), sp, None, 256))
+    b2 = sc.schedule()                       # b waits: a sits out, b takes the budget
+    assert not b2.decodes and [s.request_id for s, _ in b2.prefills] == ["b"]
+    b3 = sc.schedule()                       # nothing waiting: a decodes again
+    assert [s.request_id for s in b3.decodes] == ["a"]
+    prompts = [[5 + i, 6, 7, 8] * 3 for i in range(6)]
+    outs = []
+    for pf in (False, True):
+        llm = LLM("tiny-llama", random_init=True, device="cpu", dtype="float32",
+                  max_model_len=128, max_num_seqs=4, max_num_batched_tokens=16,
+                  prefill_first=pf)
+        outs.append([o.output_token_ids for o in llm.generate(prompts, SamplingParams(
+            temperature=0, max_tokens=6, ignore_eos=True))])
+        llm.shutdown()
+    assert outs[0] == outs[1]
