@@ -361,3 +361,68 @@ def test_pp2_stage_graphs_on_one_gpu(gpu, tmp_path, monkeypatch):
             r.pp_link.check()
         llm.shutdown()
     assert outs[2] == outs[1], outs
+
+
+def test_two_node_tp2_on_one_gpu(gpu, tmp_path):
+    """The multi-pod engine (leader/worker StatefulSet layout) on the GPU: node 0 (the
+    driver, this process) and entrypoints.worker_node (node 1, a separate process)
+    rendezvous over TCP and run one TP=2 engine; both ranks use cuda:0 with a gloo group.
+    Greedy output == the single-GPU engine."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    from safetensors.torch import save_file
+    from kubernetes_gpu_cluster_amd.engine.llm_engine import LLM
+    cfg = PRESETS["tiny-llama"]
+    d = str(tmp_path / "m")
+    os.makedirs(d)
+    save_file({k: v.contiguous() for k, v in full_state_dict_random(cfg, seed=5, std=0.15).items()},
+              os.path.join(d, "model.safetensors"))
+    json.dump({"model_type": "llama", "hidden_size": cfg.hidden_size,
+               "num_hidden_layers": cfg.num_layers, "num_attention_heads": cfg.num_heads,
+               "num_key_value_heads": cfg.num_kv_heads, "head_dim": cfg.head_dim,
+               "intermediate_size": cfg.intermediate_size, "vocab_size": cfg.vocab_size,
+               "max_position_embeddings": 512, "rope_theta": cfg.rope_theta,
+               "rms_norm_eps": cfg.rms_eps, "eos_token_id": 2, "bos_token_id": 1},
+              open(os.path.join(d, "config.json"), "w"))
+    prompts = [list(range(3, 40)), [5, 6, 7] * 20]
+    sp = [SamplingParams(temperature=0, max_tokens=8, ignore_eos=True)] * 2
+    common = dict(device="cuda", dtype="bfloat16", max_model_len=256, max_num_seqs=4,
+                  max_num_batched_tokens=128, num_gpu_blocks_override=64, enforce_eager=True)
+    ref_llm = LLM(d, **common)
+    ref = [o.output_token_ids for o in ref_llm.generate(prompts, sp)]
+    ref_llm.shutdown()
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root, KGC_DIST_BACKEND="gloo")
+    worker = subprocess.Popen(
+        [sys.executable, "-m", "kubernetes_gpu_cluster_amd.entrypoints.worker_node", d,
+         "--tensor-parallel-size", "2", "--nnodes", "2", "--node-rank", "1",
+         "--master-addr", "127.0.0.1", "--master-port", str(port), "--device", "cuda",
+         "--dtype", "bfloat16", "--max-model-len", "256", "--max-num-seqs", "4",
+         "--max-num-batched-tokens", "128", "--num-gpu-blocks-override", "64",
+         "--enforce-eager"],
+        cwd=root, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    old = os.environ.get("KGC_DIST_BACKEND")
+    os.environ["KGC_DIST_BACKEND"] = "gloo"
+    try:
+        llm = LLM(d, tensor_parallel_size=2, nnodes=2, node_rank=0, master_addr="127.0.0.1",
+                  master_port=port, **common)
+        got = [o.output_token_ids for o in llm.generate(prompts, sp)]
+        llm.shutdown()
+        rc = worker.wait(timeout=120)
+    finally:
+        if old is None:
+            os.environ.pop("KGC_DIST_BACKEND", None)
+        else:
+            os.environ["KGC_DIST_BACKEND"] = old
+        if worker.poll() is None:
+            worker.kill()
+    assert rc == 0, worker.stdout.read()[-3000:]
+    same = sum(a == b for x, y in zip(ref, got) for a, b in zip(x, y))
+    assert all(x[0] == y[0] for x, y in zip(ref, got)), (ref, got)
+    assert same >= 0.8 * sum(len(x) for x in ref), (ref, got)
