@@ -784,7 +784,14 @@ void skinny_gemm(Tensor C, Tensor X, Tensor W, std::optional<Tensor> bias, int64
   TORCH_CHECK(K % (32 * nw) == 0, "kgc.skinny_gemm: K % (32*nw) != 0");
   TORCH_CHECK(X.stride(1) == 1 && X.stride(0) % 8 == 0 && X.stride(0) >= K,
               "kgc.skinny_gemm: X rows dense, 16B aligned");
-  TORCH_CHECK(C.size(0) == M && C.size(1) == N && C.stride(1) == 1, "kgc.skinny_gemm: C [M, N]");
+  if (epi == 3) {   // SK_SILU: merged [gate; up] weight [2I, K] -> C [M, I]
+    TORCH_CHECK(nt == 2 && !bias.has_value() && N % 32 == 0,
+                "kgc.skinny_gemm: silu epilogue needs nt=2, no bias, N % 32 == 0");
+    TORCH_CHECK(C.size(0) == M && C.size(1) == N / 2 && C.stride(1) == 1,
+                "kgc.skinny_gemm: silu epilogue writes C [M, N/2]");
+  } else {
+    TORCH_CHECK(C.size(0) == M && C.size(1) == N && C.stride(1) == 1, "kgc.skinny_gemm: C [M, N]");
+  }
   TORCH_CHECK(N <= INT32_MAX && K <= INT32_MAX, "kgc.skinny_gemm: dims overflow");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(X.data_ptr()) % 16 == 0 &&
               reinterpret_cast<uintptr_t>(W.data_ptr()) % 16 == 0, "kgc.skinny_gemm: alignment");
@@ -795,7 +802,8 @@ void skinny_gemm(Tensor C, Tensor X, Tensor W, std::optional<Tensor> bias, int64
     check_same_dev(X, *bias, "bias");
     bp = bias->data_ptr();
   }
-  TORCH_CHECK(epi >= 0 && epi <= 2, "kgc.skinny_gemm: epi in {0 plain, 1 norm, 2 accumulate}");
+  TORCH_CHECK(epi >= 0 && epi <= 3,
+              "kgc.skinny_gemm: epi in {0 plain, 1 norm, 2 accumulate, 3 silu(gate) * up}");
   const void* gp = nullptr;
   if (epi == 1) {
     TORCH_CHECK(gamma.has_value() && gamma->is_contiguous() && gamma->numel() == K &&

@@ -29,19 +29,25 @@
 //            row (one factor per row, so it commutes with the K-sum).  ~15 VALU cycles
 //            per X element: only the one-m-tile (M <= 16) form is used by the model.
 //   SK_ACC:  C += X W^T (+ bias) -- the residual add of o_proj / down_proj.
+//   SK_SILU: W is the merged [gate; up] weight [2I, K] (row-major, as loaded); n-tile 0 of
+//            a workgroup streams gate rows g0..g0+15 and n-tile 1 the matching up rows
+//            I+g0.., so the merged sums of one lane pair give C[m, g0+n] = silu(g) * u with
+//            C [M, I]: the [M, 2I] gate_up output and the silu_mul launch never exist.
+//            NT = 2 only, no bias.
 #include "common.h"
 #include "launch.h"
 
 namespace kgc {
 
-enum { SK_PLAIN = 0, SK_NORM = 1, SK_ACC = 2 };
+enum { SK_PLAIN = 0, SK_NORM = 1, SK_ACC = 2, SK_SILU = 3 };
 
 template <typename T, int MT, int NT, int NW, bool NTL, int EPI>
 __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
     T* __restrict__ C, const T* __restrict__ X, const T* __restrict__ W,
     const T* __restrict__ bias, const T* __restrict__ gamma, float eps, int M, int K,
     int64_t ldx, int64_t ldc) {
-  constexpr bool NORM = EPI == SK_NORM, ACC = EPI == SK_ACC;
+  constexpr bool NORM = EPI == SK_NORM, ACC = EPI == SK_ACC, SILU = EPI == SK_SILU;
+  static_assert(!SILU || NT == 2, "SK_SILU pairs n-tile 0 (gate) with n-tile 1 (up)");
   // k-steps of loads in flight per batch (SK_NORM: gamma fragments ride along, so the
   // batch is halved to keep the register sets -- and the waves per SIMD -- as they were)
   constexpr int U = (!NORM && (MT + NT) <= 2) ? 8 : 4;
@@ -50,13 +56,16 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
   __shared__ float inv_s[16 * MT];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r16 = lane & 15, q4 = lane >> 4;
-  const int64_t n0 = (int64_t)blockIdx.x * (16 * NT);
+  // SK_SILU: gridDim.x = I / 16 workgroups over the I = 16 * gridDim.x output columns
+  const int64_t n0 = (int64_t)blockIdx.x * (SILU ? 16 : 16 * NT);
+  const int64_t n_half = SILU ? (int64_t)gridDim.x * 16 : 0;
   const int kw = K / NW;
   const int kbeg = wave * kw, kend = kbeg + kw;
 
   const T* wrow[NT];
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) wrow[nt] = W + (n0 + 16 * nt + r16) * (int64_t)K + 8 * q4;
+  for (int nt = 0; nt < NT; ++nt)
+    wrow[nt] = W + (n0 + (SILU ? nt * n_half : 16 * nt) + r16) * (int64_t)K + 8 * q4;
   const T* xrow[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) xrow[mt] = X + (int64_t)min(16 * mt + r16, M - 1) * ldx + 8 * q4;
@@ -153,7 +162,7 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
     if constexpr (NORM) ssr[wave][mt][lane] = ss[mt];
   }
   __syncthreads();
-  constexpr int TN = 16 * NT;
+  constexpr int TN = SILU ? 16 : 16 * NT;
   const int rows = min(M, 16 * MT);
   if constexpr (NORM) {
     // row m's sum of squares: its 4 lanes (q4) in each of the NW waves
@@ -174,6 +183,13 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
     float s = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) s += red[w][mt][nt][l][i];
+    if constexpr (SILU) {
+      float u = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) u += red[w][mt][1][l][i];
+      C[(int64_t)m * ldc + n0 + n] = from_f<T>(s / (1.f + __expf(-s)) * u);
+      continue;
+    }
     if constexpr (NORM) s *= inv_s[m];
     if (bias != nullptr) s += to_f<T>(bias[n0 + n]);
     T* c = C + (int64_t)m * ldc + n0 + n;
@@ -191,7 +207,10 @@ static void sk_launch(int epi, dim3 grid, hipStream_t s, void* C, const void* X,
       (T*)C, (const T*)X, (const T*)W, (const T*)bias, (const T*)gamma, eps, M, K, ldx, ldc)
   if (epi == SK_NORM) SK_GO(SK_NORM);
   else if (epi == SK_ACC) SK_GO(SK_ACC);
-  else SK_GO(SK_PLAIN);
+  else if constexpr (NT == 2) {
+    if (epi == SK_SILU) SK_GO(SK_SILU);
+    else SK_GO(SK_PLAIN);
+  } else SK_GO(SK_PLAIN);
 #undef SK_GO
 }
 
@@ -199,7 +218,7 @@ template <typename T, int MT, int NT>
 static void skinny_nw(int nw, bool ntl, int epi, void* C, const void* X, const void* W,
                       const void* bias, const void* gamma, float eps, int M, int N, int K,
                       int64_t ldx, int64_t ldc, hipStream_t s) {
-  const dim3 grid(N / (16 * NT));
+  const dim3 grid(epi == SK_SILU ? N / 32 : N / (16 * NT));   // SK_SILU: N = 2I
 #define SK_NW(NW_)                                                                            \
   if (ntl) sk_launch<T, MT, NT, NW_, true>(epi, grid, s, C, X, W, bias, gamma, eps, M, K, ldx, ldc); \
   else sk_launch<T, MT, NT, NW_, false>(epi, grid, s, C, X, W, bias, gamma, eps, M, K, ldx, ldc)

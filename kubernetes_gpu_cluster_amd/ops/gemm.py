@@ -34,6 +34,9 @@ _plan: dict[tuple[int, int, int], tuple[int, int, int, bool]] = {}
 _plan_norm: dict[tuple[int, int, int], tuple[tuple, float]] = {}
 _chosen_us: dict[tuple[int, int, int], float] = {}
 _rms_us: dict[tuple[int, int], float] = {}
+# merged gate_up (M, 2I, K) -> cfg of the SK_SILU skinny variant, where it measured faster
+# than the plain plan + a silu_mul launch
+_plan_silu: dict[tuple[int, int, int], tuple[int, int, int, bool]] = {}
 _enabled = os.environ.get("KGC_SKINNY_GEMM", "1") != "0"
 
 # K9m mid-batch decode GEMM (csrc/kernels/gemm_decode.hip), M in (SKINNY_MAX_M, DG_MAX_M]:
@@ -130,6 +133,10 @@ def linear_silu(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] =
     at this (M, N, K) the activation is the GEMM's epilogue (S = 1) or rides the split-K
     reduction (``splitk_reduce_silu``), so the [M, 2I] gate_up output never exists."""
     from . import _k, silu_mul
+    if bias is None and x.is_cuda and x.dim() == 2 and x.stride(1) == 1 and _plan_silu:
+        cfg = _plan_silu.get((x.shape[0], w.shape[0], w.shape[1]))
+        if cfg is not None:
+            return skinny_silu(x, w, cfg)
     if bias is None:
         p = _dg_plan(x, w, "silu")
         if p is not None:
@@ -221,6 +228,17 @@ def skinny_norm(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor],
     return out
 
 
+def skinny_silu(x: torch.Tensor, w: torch.Tensor, cfg,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """silu(x Wg^T) * (x Wu^T) over the merged [gate; up] weight in one launch (K9
+    SK_SILU epilogue): out [M, I]."""
+    from . import _k
+    if out is None:
+        out = torch.empty(x.shape[0], w.shape[0] // 2, dtype=x.dtype, device=x.device)
+    _k().skinny_gemm(out, x, w, None, *cfg, 3, None, 1e-6)
+    return out
+
+
 def skinny_accum(out: torch.Tensor, x: torch.Tensor, w: torch.Tensor,
                  bias: Optional[torch.Tensor], cfg) -> torch.Tensor:
     """out += x W^T (+ bias) in one launch (K9 SK_ACC epilogue: the residual add)."""
@@ -246,6 +264,7 @@ def fused_norm_plan(M: int, norm_shapes, acc_shapes):
 
 
 def clear_plan() -> None:
+    _plan_silu.clear()
     _plan_dg.clear()
     _plan_norm.clear()
     _chosen_us.clear()
@@ -255,6 +274,10 @@ def clear_plan() -> None:
 
 def plan() -> dict:
     return dict(_plan)
+
+
+def silu_plan() -> dict:
+    return dict(_plan_silu)
 
 
 def dgemm_plan() -> dict:
@@ -328,6 +351,8 @@ def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: floa
                 _plan[(M, N, K)] = best
             if (N, K) in norm_shapes and M <= norm_max_m:
                 _tune_norm(ws, x, out, M, N, K, reps)
+            if (N, K) in silu_shapes:
+                _tune_silu(ws, x, M, N, K, reps, margin)
             log.info("gemm M=%d N=%d K=%d: hipBLASLt %.1f us, skinny %s %.1f us -> %s", M, N, K,
                      lib_t * 1e3 / n, sk_cfg, sk_t * 1e3 / n, "skinny" if best else "hipBLASLt")
         if _dg_enabled:
@@ -434,6 +459,35 @@ def _tune_dgemm(ws, N: int, K: int, ms, margin: float, reps: int, res: dict,
         log.info("gemm M=%d N=%d K=%d %s: hipBLASLt %.1f us, K9m %s %.1f us -> %s", M, N, K,
                  kind, lib_t * 1e3 / n, best_cfg, best_t * 1e3 / n,
                  "K9m" if chosen else "hipBLASLt")
+
+
+def _tune_silu(ws, x, M: int, N: int, K: int, reps: int, margin: float) -> None:
+    """Time the SK_SILU variants against the plain plan (skinny or hipBLASLt, as just
+    chosen) followed by silu_mul, over every layer's gate_up weight."""
+    from . import silu_mul
+    act = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
+
+    def sep():
+        for w in ws:
+            silu_mul(linear(x, w), act)
+    sep_t = _time(sep, reps)
+    best_t, best_cfg = float("inf"), None
+    for cfg in _CONFIGS:
+        if cfg[1] != 2 or not skinny_ok(M, N, K, cfg) or (cfg[0] > 1 and M <= 16 * (cfg[0] // 2)):
+            continue
+
+        def fn(cfg=cfg):
+            for w in ws:
+                skinny_silu(x, w, cfg, act)
+        t = _time(fn, reps)
+        if t < best_t:
+            best_t, best_cfg = t, cfg
+    n = len(ws)
+    if best_cfg is not None and best_t < sep_t * margin:
+        _plan_silu[(M, N, K)] = best_cfg
+    log.info("gemm M=%d N=%d K=%d silu: plan + silu_mul %.1f us, SK_SILU %s %.1f us -> %s",
+             M, N, K, sep_t * 1e3 / n, best_cfg, best_t * 1e3 / n,
+             "SK_SILU" if (M, N, K) in _plan_silu else "separate")
 
 
 def _tune_norm(ws, x, out, M: int, N: int, K: int, reps: int) -> None:

@@ -246,7 +246,7 @@ def test_tp_logits_bytes_llama3_8b_tp8():
 
 def test_pipelined_pp2_keeps_both_stages_busy(tmp_path, monkeypatch):
     """PP = 2 with one micro-batch per stage in flight: on a steady decode load with a
-    fixed per-step stage time (KGC_FAKE_STAGE_MS: each rank's step is a 30 ms sleep with
+    fixed per-step stage time (KGC_FAKE_STAGE_MS: each rank's step is a 60 ms sleep with
     the real plan / activation / token traffic around it), both stages are busy > 80 %
     of the time -- a serial pipeline would keep each below 50 %."""
     import json
@@ -254,7 +254,7 @@ def test_pipelined_pp2_keeps_both_stages_busy(tmp_path, monkeypatch):
     from kubernetes_gpu_cluster_amd.engine.sequence import SamplingParams
     stats = tmp_path / "stats"
     stats.mkdir()
-    monkeypatch.setenv("KGC_FAKE_STAGE_MS", "30")
+    monkeypatch.setenv("KGC_FAKE_STAGE_MS", "60")
     monkeypatch.setenv("KGC_STAGE_STATS_DIR", str(stats))
     llm = LLM("tiny-llama", random_init=True, device="cpu", dtype="float32",
               pipeline_parallel_size=2, max_model_len=256, max_num_seqs=8,

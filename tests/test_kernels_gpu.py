@@ -492,6 +492,50 @@ def test_skinny_gemm_norm_and_accumulate(gpu, M, nw):
     torch.testing.assert_close(c.float().cpu(), exp, atol=6e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("M,N,K", [(1, 28672, 4096), (5, 1024, 2048), (16, 2048, 1024),
+                                   (40, 512, 4096), (64, 1024, 512)])
+def test_skinny_silu_matches_fp32(gpu, dt, M, N, K):
+    """K9 SK_SILU: silu(x Wg^T) * (x Wu^T) over a merged [gate; up] weight [2I, K] in one
+    launch, every (mt, nw, ntl) holding M, vs fp32; and linear_silu takes the plan."""
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, dtype=dt, device=gpu)
+    w = torch.randn(N, K, dtype=dt, device=gpu) * K ** -0.5
+    ref = x.float().cpu() @ w.float().cpu().t()
+    exp = torch.nn.functional.silu(ref[:, : N // 2]) * ref[:, N // 2:]
+    ran = 0
+    for cfg in gemm._CONFIGS:
+        if cfg[1] != 2 or not gemm.skinny_ok(M, N, K, cfg):
+            continue
+        out = torch.full((M, N // 2), float("nan"), dtype=dt, device=gpu)
+        gemm.skinny_silu(x, w, cfg, out)
+        torch.testing.assert_close(out.float().cpu(), exp, atol=3e-2, rtol=2e-2)
+        ran += 1
+    assert ran > 0
+    try:
+        gemm._plan_silu[(M, N, K)] = (1 if M <= 16 else (2 if M <= 32 else 4), 2, 4, True)
+        torch.testing.assert_close(gemm.linear_silu(x, w).float().cpu(), exp, atol=3e-2,
+                                   rtol=2e-2)
+    finally:
+        gemm.clear_plan()
+
+
+def test_tune_skinny_silu_records_plan(gpu):
+    """The tuner times SK_SILU against the plain plan + silu_mul for merged gate_up shapes."""
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    torch.manual_seed(9)
+    ws = [torch.randn(4096, 2048, dtype=torch.bfloat16, device=gpu) * 0.02 for _ in range(4)]
+    try:
+        gemm.tune_skinny(ws, [1, 8], silu_shapes={(4096, 2048)})
+        x = torch.randn(8, 2048, dtype=torch.bfloat16, device=gpu)
+        ref = x.float() @ ws[0].float().t()
+        exp = torch.nn.functional.silu(ref[:, :2048]) * ref[:, 2048:]
+        torch.testing.assert_close(gemm.linear_silu(x, ws[0]).float(), exp, atol=3e-2, rtol=2e-2)
+    finally:
+        gemm.clear_plan()
+
+
 @pytest.mark.parametrize("cfg", list(range(10)))
 @pytest.mark.parametrize("M,N,K", [(256, 1024, 4096), (200, 768, 1024), (77, 512, 2048)])
 def test_dgemm_matches_fp32(gpu, cfg, M, N, K):

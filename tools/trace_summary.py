@@ -76,6 +76,18 @@ def main():
             agg.update(s[3])
         for k, v in agg.most_common(16):
             print(f"   {k:38} {v / len(dec) / 1e3:9.1f} us/step")
+        # prefill (chunked) steps: the ones that run the prefill attention kernel
+        pre = [s for s in steps if s[3].get("prefill_attn", 0) > 0]
+        if pre:
+            print(f"\nprefill steps: {len(pre)}")
+            print(f"median span {statistics.median([s[0] for s in pre]) / 1e6:.3f} ms, "
+                  f"busy {statistics.median([s[1] for s in pre]) / 1e6:.3f} ms, "
+                  f"total span {sum(s[0] for s in pre) / 1e6:.1f} ms")
+            agg = collections.Counter()
+            for s in pre:
+                agg.update(s[3])
+            for k, v in agg.most_common(16):
+                print(f"   {k:38} {v / len(pre) / 1e3:9.1f} us/step")
 
 
 if __name__ == "__main__":
