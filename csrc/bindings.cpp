@@ -765,7 +765,7 @@ void xgmi_allreduce_rms(Tensor out, Tensor in, Tensor residual, Tensor w, double
 
 void skinny_gemm(Tensor C, Tensor X, Tensor W, std::optional<Tensor> bias, int64_t mt,
                  int64_t nt, int64_t nw, bool ntl, int64_t epi, std::optional<Tensor> gamma,
-                 double eps) {
+                 double eps, std::optional<Tensor> norm_out, std::optional<Tensor> ticket) {
   check_gpu(X, "X");
   check_same_dev(X, W, "W");
   check_same_dev(X, C, "C");
@@ -802,20 +802,45 @@ void skinny_gemm(Tensor C, Tensor X, Tensor W, std::optional<Tensor> bias, int64
     check_same_dev(X, *bias, "bias");
     bp = bias->data_ptr();
   }
-  TORCH_CHECK(epi >= 0 && epi <= 3,
-              "kgc.skinny_gemm: epi in {0 plain, 1 norm, 2 accumulate, 3 silu(gate) * up}");
+  TORCH_CHECK(epi >= 0 && epi <= 4, "kgc.skinny_gemm: epi in {0 plain, 1 norm, 2 accumulate, "
+              "3 silu(gate) * up, 4 accumulate + rms_norm}");
   const void* gp = nullptr;
-  if (epi == 1) {
-    TORCH_CHECK(gamma.has_value() && gamma->is_contiguous() && gamma->numel() == K &&
-                gamma->scalar_type() == X.scalar_type(), "kgc.skinny_gemm: norm needs gamma [K]");
+  if (epi == 1 || epi == 4) {
+    const int64_t gn = epi == 1 ? K : N;
+    TORCH_CHECK(gamma.has_value() && gamma->is_contiguous() && gamma->numel() == gn &&
+                gamma->scalar_type() == X.scalar_type(),
+                "kgc.skinny_gemm: norm needs gamma [K] (epi 1) / [N] (epi 4)");
     check_same_dev(X, *gamma, "gamma");
     gp = gamma->data_ptr();
   }
-  if (epi == 2)   // C is read and rewritten in place: it must not overlap the input rows
+  if (epi == 2 || epi == 4)   // C is read and rewritten in place: it must not overlap the inputs
     TORCH_CHECK(C.data_ptr() != X.data_ptr(), "kgc.skinny_gemm: accumulate target aliases X");
+  void* np = nullptr;
+  uint32_t* tp = nullptr;
+  if (epi == 4) {
+    TORCH_CHECK(N % 512 == 0 && N <= 8192,
+                "kgc.skinny_gemm: accumulate + rms_norm needs N % 512 == 0, N <= 8192");
+    TORCH_CHECK(norm_out.has_value() && norm_out->is_contiguous() && norm_out->size(0) == M &&
+                norm_out->size(1) == N && norm_out->scalar_type() == X.scalar_type() &&
+                norm_out->data_ptr() != C.data_ptr(), "kgc.skinny_gemm: norm_out [M, N]");
+    TORCH_CHECK(ticket.has_value() && ticket->numel() >= 1 &&
+                ticket->scalar_type() == at::kInt, "kgc.skinny_gemm: ticket int32 [>= 1]");
+    check_same_dev(X, *norm_out, "norm_out");
+    check_same_dev(X, *ticket, "ticket");
+    np = norm_out->data_ptr();
+    tp = reinterpret_cast<uint32_t*>(ticket->data_ptr());
+  }
   kgc::launch_skinny_gemm(dt_code(X), (int)mt, (int)nt, (int)nw, ntl, (int)epi, C.data_ptr(),
                           X.data_ptr(), W.data_ptr(), bp, gp, (float)eps, (int)M, (int)N, (int)K,
-                          X.stride(0), C.stride(0), stream());
+                          X.stride(0), C.stride(0), np, tp, stream());
+}
+
+void sample_stamps_enable(bool on) { kgc::sample_stamps_enable(on); }
+
+std::vector<int64_t> sample_stamps() {
+  uint64_t st[16] = {};
+  kgc::sample_stamps_read(st);
+  return std::vector<int64_t>(st, st + 16);
 }
 
 int64_t decode_partition_size() { return kgc::paged_decode_partition_size(); }
@@ -891,9 +916,12 @@ TORCH_LIBRARY(kgc, m) {
   m.def("ep_return(Tensor y, Tensor route, int[] data, int[] sig, int rank, int C) -> ()");
   m.def("ep_combine(Tensor(a!) out, Tensor topk_w, int[] data, int[] sig, int rank, int C) -> ()");
   m.def("debug_build() -> bool", &debug_build);
+  m.def("sample_stamps_enable(bool on) -> ()", &sample_stamps_enable);
+  m.def("sample_stamps() -> int[]", &sample_stamps);
   m.def("prefill_block_m() -> int", &prefill_block_m);
   m.def("skinny_gemm(Tensor(a!) C, Tensor X, Tensor W, Tensor? bias, int mt, int nt, int nw, "
-        "bool ntl, int epi=0, Tensor? gamma=None, float eps=1e-6) -> ()");
+        "bool ntl, int epi=0, Tensor? gamma=None, float eps=1e-6, Tensor(b!)? norm_out=None, "
+        "Tensor(c!)? ticket=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(kgc, CUDA, m) {

@@ -34,19 +34,28 @@
 //            I+g0.., so the merged sums of one lane pair give C[m, g0+n] = silu(g) * u with
 //            C [M, I]: the [M, 2I] gate_up output and the silu_mul launch never exist.
 //            NT = 2 only, no bias.
+//   SK_ACC_NORM: SK_ACC, then the residual add + RMSNorm that consumes C inside the same
+//            launch: every workgroup publishes its tile of C (write-through stores,
+//            drained, no release fence) and draws a ticket; the last of the grid acquires and
+//            writes NO[m, :] = C[m, :] * rsqrt(mean(C[m, :]^2) + eps) * gamma (one wave
+//            per row, the rounding of fused_add_rms_norm), then re-arms the ticket.  The
+//            separate norm launch and its kernel boundary disappear (o_proj -> post-
+//            attention norm, down_proj -> next input norm at small M).  The ticket is
+//            zeroed at allocation and by every last arriver; one ticket per stream.
 #include "common.h"
 #include "launch.h"
 
 namespace kgc {
 
-enum { SK_PLAIN = 0, SK_NORM = 1, SK_ACC = 2, SK_SILU = 3 };
+enum { SK_PLAIN = 0, SK_NORM = 1, SK_ACC = 2, SK_SILU = 3, SK_ACC_NORM = 4 };
 
 template <typename T, int MT, int NT, int NW, bool NTL, int EPI>
 __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
     T* __restrict__ C, const T* __restrict__ X, const T* __restrict__ W,
     const T* __restrict__ bias, const T* __restrict__ gamma, float eps, int M, int K,
-    int64_t ldx, int64_t ldc) {
-  constexpr bool NORM = EPI == SK_NORM, ACC = EPI == SK_ACC, SILU = EPI == SK_SILU;
+    int64_t ldx, int64_t ldc, T* __restrict__ NO, uint32_t* __restrict__ ticket) {
+  constexpr bool NORM = EPI == SK_NORM, SILU = EPI == SK_SILU, ACCN = EPI == SK_ACC_NORM;
+  constexpr bool ACC = EPI == SK_ACC || ACCN;
   static_assert(!SILU || NT == 2, "SK_SILU pairs n-tile 0 (gate) with n-tile 1 (up)");
   // k-steps of loads in flight per batch (SK_NORM: gamma fragments ride along, so the
   // batch is halved to keep the register sets -- and the waves per SIMD -- as they were)
@@ -194,19 +203,75 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
     if (bias != nullptr) s += to_f<T>(bias[n0 + n]);
     T* c = C + (int64_t)m * ldc + n0 + n;
     if constexpr (ACC) s += to_f<T>(*c);
-    *c = from_f<T>(s);
+    if constexpr (ACCN) {
+      // write-through (sc1) store: the last workgroup reads it from another CU with no
+      // release fence on this side
+      const T v = from_f<T>(s);
+      __hip_atomic_store(reinterpret_cast<uint16_t*>(c), __builtin_bit_cast(uint16_t, v),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      *c = from_f<T>(s);
+    }
+  }
+  if constexpr (ACCN) {
+    __shared__ uint32_t last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's C stores landed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+      last = t == gridDim.x - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    __syncthreads();
+    if (!last) return;
+    // one wave per row; a lane holds its <= 16 chunks of 8 in registers, so a row costs ONE
+    // load round trip (these lines were written by other CUs: L2 / HBM latency)
+    const int N = gridDim.x * TN;                        // whole rows (host: 512 | N <= 8192)
+    constexpr int CH = 16;
+    for (int m = wave; m < M; m += NW) {
+      const T* c = C + (int64_t)m * ldc;
+      Pack8<T> v[CH];
+#pragma unroll
+      for (int j = 0; j < CH; ++j)
+        if (j * 512 < N) v[j].u = *reinterpret_cast<const u32x4*>(c + j * 512 + lane * 8);
+      float ss = 0.f;
+#pragma unroll
+      for (int j = 0; j < CH; ++j)
+        if (j * 512 < N) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ss += to_f<T>(v[j].h[e]) * to_f<T>(v[j].h[e]);
+        }
+      const float inv = rsqrtf(wave_sum(ss) / (float)N + eps);
+      T* o = NO + (int64_t)m * N;
+#pragma unroll
+      for (int j = 0; j < CH; ++j)
+        if (j * 512 < N) {
+          Pack8<T> g, r;
+          g.u = *reinterpret_cast<const u32x4*>(gamma + j * 512 + lane * 8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) r.h[e] = from_f<T>(to_f<T>(v[j].h[e]) * inv * to_f<T>(g.h[e]));
+          *reinterpret_cast<u32x4*>(o + j * 512 + lane * 8) = r.u;
+        }
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
 template <typename T, int MT, int NT, int NW, bool NTL>
 static void sk_launch(int epi, dim3 grid, hipStream_t s, void* C, const void* X, const void* W,
                       const void* bias, const void* gamma, float eps, int M, int K,
-                      int64_t ldx, int64_t ldc) {
+                      int64_t ldx, int64_t ldc, void* NO, uint32_t* ticket) {
 #define SK_GO(E)                                                                              \
   skinny_gemm_kernel<T, MT, NT, NW, NTL, E><<<grid, NW * 64, 0, s>>>(                        \
-      (T*)C, (const T*)X, (const T*)W, (const T*)bias, (const T*)gamma, eps, M, K, ldx, ldc)
+      (T*)C, (const T*)X, (const T*)W, (const T*)bias, (const T*)gamma, eps, M, K, ldx, ldc, \
+      (T*)NO, ticket)
   if (epi == SK_NORM) SK_GO(SK_NORM);
   else if (epi == SK_ACC) SK_GO(SK_ACC);
+  else if (epi == SK_ACC_NORM) SK_GO(SK_ACC_NORM);
   else if constexpr (NT == 2) {
     if (epi == SK_SILU) SK_GO(SK_SILU);
     else SK_GO(SK_PLAIN);
@@ -217,11 +282,13 @@ static void sk_launch(int epi, dim3 grid, hipStream_t s, void* C, const void* X,
 template <typename T, int MT, int NT>
 static void skinny_nw(int nw, bool ntl, int epi, void* C, const void* X, const void* W,
                       const void* bias, const void* gamma, float eps, int M, int N, int K,
-                      int64_t ldx, int64_t ldc, hipStream_t s) {
+                      int64_t ldx, int64_t ldc, void* NO, uint32_t* ticket, hipStream_t s) {
   const dim3 grid(epi == SK_SILU ? N / 32 : N / (16 * NT));   // SK_SILU: N = 2I
 #define SK_NW(NW_)                                                                            \
-  if (ntl) sk_launch<T, MT, NT, NW_, true>(epi, grid, s, C, X, W, bias, gamma, eps, M, K, ldx, ldc); \
-  else sk_launch<T, MT, NT, NW_, false>(epi, grid, s, C, X, W, bias, gamma, eps, M, K, ldx, ldc)
+  if (ntl) sk_launch<T, MT, NT, NW_, true>(epi, grid, s, C, X, W, bias, gamma, eps, M, K, ldx, ldc, \
+                                           NO, ticket);                                      \
+  else sk_launch<T, MT, NT, NW_, false>(epi, grid, s, C, X, W, bias, gamma, eps, M, K, ldx, ldc, \
+                                        NO, ticket)
   if (nw == 16) { SK_NW(16); }
   else if (nw == 8) { SK_NW(8); }
   else { SK_NW(4); }
@@ -231,10 +298,12 @@ static void skinny_nw(int nw, bool ntl, int epi, void* C, const void* X, const v
 template <typename T>
 static void skinny_t(int mt, int nt, int nw, bool ntl, int epi, void* C, const void* X,
                      const void* W, const void* bias, const void* gamma, float eps, int M, int N,
-                     int K, int64_t ldx, int64_t ldc, hipStream_t s) {
+                     int K, int64_t ldx, int64_t ldc, void* NO, uint32_t* ticket, hipStream_t s) {
 #define SK_MT(MT_)                                                                            \
-  if (nt == 2) skinny_nw<T, MT_, 2>(nw, ntl, epi, C, X, W, bias, gamma, eps, M, N, K, ldx, ldc, s); \
-  else skinny_nw<T, MT_, 1>(nw, ntl, epi, C, X, W, bias, gamma, eps, M, N, K, ldx, ldc, s)
+  if (nt == 2) skinny_nw<T, MT_, 2>(nw, ntl, epi, C, X, W, bias, gamma, eps, M, N, K, ldx, ldc, \
+                                    NO, ticket, s);                                           \
+  else skinny_nw<T, MT_, 1>(nw, ntl, epi, C, X, W, bias, gamma, eps, M, N, K, ldx, ldc, NO,    \
+                            ticket, s)
   if (mt == 1) { SK_MT(1); }
   else if (mt == 2) { SK_MT(2); }
   else { SK_MT(4); }
@@ -243,12 +312,15 @@ static void skinny_t(int mt, int nt, int nw, bool ntl, int epi, void* C, const v
 
 void launch_skinny_gemm(int dtype, int mt, int nt, int nw, bool ntl, int epi, void* C,
                         const void* X, const void* W, const void* bias, const void* gamma,
-                        float eps, int M, int N, int K, int64_t ldx, int64_t ldc, hipStream_t s) {
+                        float eps, int M, int N, int K, int64_t ldx, int64_t ldc, void* NO,
+                        uint32_t* ticket, hipStream_t s) {
   if (M == 0 || N == 0) return;
   if (dtype == DT_BF16)
-    skinny_t<bf16>(mt, nt, nw, ntl, epi, C, X, W, bias, gamma, eps, M, N, K, ldx, ldc, s);
+    skinny_t<bf16>(mt, nt, nw, ntl, epi, C, X, W, bias, gamma, eps, M, N, K, ldx, ldc, NO, ticket,
+                   s);
   else
-    skinny_t<f16>(mt, nt, nw, ntl, epi, C, X, W, bias, gamma, eps, M, N, K, ldx, ldc, s);
+    skinny_t<f16>(mt, nt, nw, ntl, epi, C, X, W, bias, gamma, eps, M, N, K, ldx, ldc, NO, ticket,
+                  s);
 }
 
 }  // namespace kgc

@@ -60,10 +60,17 @@ void launch_sample_vp(int dtype, int64_t* packed, uint64_t* partial, const void*
 void launch_sample_vp_unpack(int64_t* out, const int64_t* packed, int B, hipStream_t s);
 
 // K9 skinny (small-M decode) GEMM: C[M, N] = X[M, K] . W[N, K]^T (+ bias), M <= 16*mt.
-// epi: 0 plain, 1 RMS-normalise X rows on the fly (gamma [K], eps), 2 accumulate into C
+// epi: 0 plain, 1 RMS-normalise X rows on the fly (gamma [K], eps), 2 accumulate into C,
+// 3 silu(gate) * up over a merged weight (C [M, N/2]), 4 accumulate into C then
+// NO = rms_norm(C) * gamma [N] in the same launch (ticket: a zeroed u32, one per stream)
+// cooperative sampler phase stamps (profiling): enable, then read 16 wall-clock stamps
+void sample_stamps_enable(bool on);
+void sample_stamps_read(uint64_t* out16);
+
 void launch_skinny_gemm(int dtype, int mt, int nt, int nw, bool ntl, int epi, void* C,
                         const void* X, const void* W, const void* bias, const void* gamma,
-                        float eps, int M, int N, int K, int64_t ldx, int64_t ldc, hipStream_t s);
+                        float eps, int M, int N, int K, int64_t ldx, int64_t ldc, void* NO,
+                        uint32_t* ticket, hipStream_t s);
 
 // K13/K14 MoE: routing, expert bucketing, grouped MFMA GEMM, weighted combine.
 int moe_block_n();

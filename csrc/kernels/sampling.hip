@@ -284,15 +284,34 @@ __global__ __launch_bounds__(256) void sample_merge_kernel(int64_t* __restrict__
 // co-resident and the barriers cannot deadlock; spins are bounded anyway).  The
 // single-workgroup kernel above computes every threshold over the whole row in each of
 // the S workgroups: ~230 us per top-p row at batch 1.
+// Candidates of the crossing distance bin: when a row has at most SMP_CAP of them, each
+// workgroup finishes the threshold with the 4 radix passes over that list in its own LDS
+// (fixed-point masses: integer sums, so every workgroup of the row lands on the same key)
+// instead of 4 global passes over the row with a row barrier each.
+constexpr int SMP_CAP = 2048;
+
+// Phase stamps of the cooperative kernel (profiling only, off by default): workgroup
+// (0, 0) records wall_clock64() (100 MHz) at each phase boundary when enabled.
+__device__ int g_smp_stamp_on;
+__device__ uint64_t g_smp_stamps[16];
+#define SMP_STAMP(i)                                                                         \
+  do {                                                                                       \
+    if (g_smp_stamp_on && b == 0 && y == 0 && tid == 0) g_smp_stamps[i] = wall_clock64();   \
+  } while (0)
+
 struct CoopWs {
   uint32_t bar[16];
   uint32_t maxkey;
   uint32_t err;
   float z;
   float pad;
+  uint32_t ncand[2];
+  uint32_t pad2[2];
   float hist_k[SMP_NBIN];
   float hist_p[SMP_NBIN];
   float hist_r[8][256];
+  uint32_t cand_key[2][SMP_CAP];
+  float cand_w[2][SMP_CAP];
 };
 
 int sample_coop_ws_bytes() { return (int)sizeof(CoopWs); }
@@ -309,6 +328,10 @@ __global__ __launch_bounds__(SMP_NT) void sample_coop_kernel(
   __shared__ float scan_w[SMP_NT / 64];
   __shared__ uint32_t sel_bin;
   __shared__ float sel_f;
+  __shared__ uint32_t cand_k[SMP_CAP];
+  __shared__ uint64_t cand_m[SMP_CAP];
+  __shared__ uint64_t hist_u[256];
+  __shared__ uint64_t sel_u;
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const T* row = logits + (int64_t)b * row_stride;
   CoopWs* ws = wsa + b;
@@ -322,13 +345,18 @@ __global__ __launch_bounds__(SMP_NT) void sample_coop_kernel(
   const int i_lo = (int)((int64_t)V * y / S);
   const int i_hi = (int)((int64_t)V * (y + 1) / S);
   int nbar = 0;
-  // all S workgroups of this row: arrive, wait for the others (bounded), acquire
+  SMP_STAMP(0);
+  // all S workgroups of this row: arrive, wait for the others (bounded).  Everything a
+  // workgroup hands to the others goes through agent-scope atomics or write-through
+  // stores, and every read of it is an agent-scope (sc1) atomic load, so the barrier needs
+  // no release / acquire fence: the __syncthreads() before the arrive drains every wave's
+  // stores and atomics (vmcnt(0)), and the counter is an atomic (cdna_hip_programming.md
+  // §6 Guideline 16, the write-through form).  Plain loads here only read the logits.
   auto row_barrier = [&]() {
     __syncthreads();
     if (tid == 0) {
-      __threadfence();
       uint32_t* c = &ws->bar[nbar];
-      atomicAdd(c, 1u);
+      __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       int it = 0;
       while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)S) {
         __builtin_amdgcn_s_sleep(1);
@@ -337,7 +365,6 @@ __global__ __launch_bounds__(SMP_NT) void sample_coop_kernel(
           break;
         }
       }
-      __threadfence();
     }
     __syncthreads();
     ++nbar;
@@ -350,7 +377,9 @@ __global__ __launch_bounds__(SMP_NT) void sample_coop_kernel(
     visit_row(row, i_lo, i_hi, tid, [&](int, float r) { mx = fmaxf(mx, r); });
     mx = block_max<SMP_NT>(mx, red_v);
     if (tid == 0) atomicMax(&ws->maxkey, ord_key(mx));
+    SMP_STAMP(1);
     row_barrier();
+    SMP_STAMP(2);
     mx = key_val(__hip_atomic_load(&ws->maxkey, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     const float it = 1.f / temp;
     auto dbin = [&](float x) -> int {
@@ -389,18 +418,108 @@ __global__ __launch_bounds__(SMP_NT) void sample_coop_kernel(
       for (int j = tid; j < n; j += SMP_NT) h[j] = gload(&g[j]);
       __syncthreads();
     };
+    // append this workgroup's candidates (weight >= 0) to the row's list t; write-through
+    // stores, published by the row barrier that follows
+    auto collect = [&](int t, auto&& weight) {
+      // staged in LDS (cand_k / cand_m are free until local_select), then ONE global
+      // atomic per workgroup reserves its range of the row's list.  sel_bin doubles as the
+      // LDS counter: every wave has read the previous selection (kbin / pbin) first
+      __syncthreads();
+      if (tid == 0) sel_bin = 0;
+      __syncthreads();
+      visit_row(row, i_lo, i_hi, tid, [&](int, float r) {
+        const float wt = weight(r);
+        if (wt >= 0.f) {
+          const uint32_t slot = atomicAdd(&sel_bin, 1u);
+          if (slot < (uint32_t)SMP_CAP) {
+            cand_k[slot] = ord_key(r);
+            cand_m[slot] = __float_as_uint(wt);
+          }
+        }
+      });
+      __syncthreads();
+      const uint32_t n = sel_bin;
+      if (tid == 0)   // an overflowing workgroup pushes the row's count past SMP_CAP
+        sel_u = __hip_atomic_fetch_add(&ws->ncand[t], n > (uint32_t)SMP_CAP ? (uint32_t)SMP_CAP + 1 : n,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const uint32_t base = (uint32_t)sel_u;
+      for (uint32_t j = tid; j < n && j < (uint32_t)SMP_CAP && base + j < (uint32_t)SMP_CAP; j += SMP_NT) {
+        __hip_atomic_store(&ws->cand_key[t][base + j], cand_k[j], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ws->cand_w[t][base + j], __uint_as_float((uint32_t)cand_m[j]),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    };
+    // the 4 radix passes of a threshold over the n <= SMP_CAP candidates of list t, in LDS:
+    // the key of the candidate at which the running mass (keys descending) first reaches
+    // `need` (fixed point: mass * scale); bins below `lowest` never cross (fallback bin 0)
+    auto local_select = [&](int t, int n, float scale, float need, int lowest) -> uint32_t {
+      for (int j = tid; j < n; j += SMP_NT) {
+        cand_k[j] = __hip_atomic_load(&ws->cand_key[t][j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cand_m[j] = (uint64_t)(gload(&ws->cand_w[t][j]) * scale);
+      }
+      uint64_t rem = need > 0.f ? (uint64_t)(need * scale) : 0;
+      uint32_t prefix = 0, mask = 0;
+      for (int shift = 24; shift >= 0; shift -= 8) {
+        if (tid < 256) hist_u[tid] = 0;
+        __syncthreads();
+        for (int j = tid; j < n; j += SMP_NT)
+          if ((cand_k[j] & mask) == prefix) atomicAdd(&hist_u[(cand_k[j] >> shift) & 255], cand_m[j]);
+        __syncthreads();
+        if (w == 0) {   // one wave scans the 256 bins, 4 per lane, from bin 255 down
+          uint64_t v[4], sum = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int bn = 255 - 4 * lane - i;
+            v[i] = bn >= lowest ? hist_u[bn] : 0;
+            sum += v[i];
+          }
+          uint64_t incl = sum;
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t u = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += u;
+          }
+          if (lane == 63) { sel_bin = 0; sel_u = incl; }    // no crossing: keep the whole bin
+          uint64_t run = incl - sum;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int bn = 255 - 4 * lane - i;
+            if (bn >= lowest && run < rem && run + v[i] >= rem) { sel_bin = bn; sel_u = run; }
+            run += v[i];
+          }
+        }
+        __syncthreads();
+        rem -= sel_u;
+        prefix |= sel_bin << shift;
+        mask |= 255u << shift;
+      }
+      return prefix;
+    };
     if (use_k) {
       for (int j = tid; j < SMP_NBIN; j += SMP_NT) hist_d[j] = 0.f;
       __syncthreads();
       visit_row(row, i_lo, i_hi, tid, [&](int, float r) { atomicAdd(&hist_d[dbin(r)], 1.f); });
+      SMP_STAMP(3);
       publish(hist_d, ws->hist_k, SMP_NBIN);
       row_barrier();
       fetch(hist_d, ws->hist_k, SMP_NBIN);
       cross_dist((float)k);
+      SMP_STAMP(4);
       const int kbin = (int)sel_bin;
       uint32_t prefix = 0, mask = 0;
       float remaining = (float)k - sel_f;
-      for (int q = 0, shift = 24; shift >= 0; ++q, shift -= 8) {
+      collect(0, [&](float r) { return dbin(r) == kbin ? 1.f : -1.f; });
+      row_barrier();
+      const int nk = (int)__hip_atomic_load(&ws->ncand[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      SMP_STAMP(5);
+      if (nk <= SMP_CAP) {
+        prefix = local_select(0, nk, 1.f, remaining, 0);
+        mask = 0xffffffffu;   // skip the global passes below
+      }
+      SMP_STAMP(6);
+      for (int q = 0, shift = 24; shift >= 0 && mask != 0xffffffffu; ++q, shift -= 8) {
         if (tid < 256) hist_f[tid] = 0.f;
         __syncthreads();
         visit_row(row, i_lo, i_hi, tid, [&](int, float r) {
@@ -430,17 +549,31 @@ __global__ __launch_bounds__(SMP_NT) void sample_coop_kernel(
       });
       z = block_sum<SMP_NT>(z, red_v);
       if (tid == 0) atomicAdd(&ws->z, z);
+      SMP_STAMP(7);
       publish(hist_d, ws->hist_p, SMP_NBIN);
       row_barrier();
       z = gload(&ws->z);
       fetch(hist_d, ws->hist_p, SMP_NBIN);
       const float target = p * z;
       cross_dist(target);
+      SMP_STAMP(8);
       const int pbin = (int)sel_bin;
       uint32_t prefix = 0, mask = 0;
       float above = sel_f;
       const uint32_t kthr = ord_key(thr);
-      for (int q = 4, shift = 24; shift >= 0; ++q, shift -= 8) {
+      collect(1, [&](float r) {
+        return (ord_key(r) >= kthr && dbin(r) == pbin) ? __expf((r - mx) * it) : -1.f;
+      });
+      row_barrier();
+      const int np = (int)__hip_atomic_load(&ws->ncand[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      SMP_STAMP(9);
+      if (np <= SMP_CAP) {
+        // masses <= 1 each, <= 2^11 of them: 2^40 fixed point stays far below 2^64
+        prefix = local_select(1, np, 1099511627776.f, target - above, 1);
+        mask = 0xffffffffu;
+      }
+      SMP_STAMP(10);
+      for (int q = 4, shift = 24; shift >= 0 && mask != 0xffffffffu; ++q, shift -= 8) {
         if (tid < 256) hist_f[tid] = 0.f;
         __syncthreads();
         visit_row(row, i_lo, i_hi, tid, [&](int, float r) {
@@ -458,33 +591,8 @@ __global__ __launch_bounds__(SMP_NT) void sample_coop_kernel(
       }
       thr = fmaxf(thr, key_val(prefix));
     }
-    // The workspace is persistent and must be all-zero for the next call: the last of
-    // the row's workgroups to finish reading it clears what this call used.
-    __shared__ int last;
-    __syncthreads();
-    if (tid == 0) {
-      __threadfence();
-      last = atomicAdd(&ws->bar[15], 1u) == (uint32_t)(S - 1);
-    }
-    __syncthreads();
-    if (last) {
-      if (use_k) {
-        for (int j = tid; j < SMP_NBIN; j += SMP_NT) ws->hist_k[j] = 0.f;
-        for (int j = tid; j < 4 * 256; j += SMP_NT) ws->hist_r[j / 256][j % 256] = 0.f;
-      }
-      if (use_p) {
-        for (int j = tid; j < SMP_NBIN; j += SMP_NT) ws->hist_p[j] = 0.f;
-        for (int j = tid; j < 4 * 256; j += SMP_NT) ws->hist_r[4 + j / 256][j % 256] = 0.f;
-      }
-      if (tid < 16) ws->bar[tid] = 0;
-      if (tid == 0) {
-        ws->maxkey = 0;
-        ws->z = 0.f;
-      }
-      __threadfence();
-    }
   }
-
+  SMP_STAMP(11);
   // ---------- (Gumbel-)argmax over this workgroup's slice of the support
   const uint64_t seed = (uint64_t)seeds[b];
   const uint32_t key = mix32((uint32_t)seed);
@@ -515,6 +623,45 @@ __global__ __launch_bounds__(SMP_NT) void sample_coop_kernel(
     for (int j = 1; j < SMP_NT / 64; ++j) argmax_merge(bv, bi, red_v[j], red_i[j]);
     partial[(int64_t)b * S + y] = ((uint64_t)ord_key(bv) << 32) | (uint32_t)(~(uint32_t)bi);
   }
+  // The workspace is persistent and must be all-zero for the next call: the last of the
+  // row's workgroups to finish (every read of the workspace is behind it: __syncthreads()
+  // drains this workgroup's loads) clears what this call used.  After the argmax pass, so
+  // the clearing stays off the row's critical path; the next launch sees the plain stores.
+  if (use_k || use_p) {
+    __shared__ int last;
+    __syncthreads();
+    if (tid == 0)
+      last = __hip_atomic_fetch_add(&ws->bar[15], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             (uint32_t)(S - 1);
+    __syncthreads();
+    if (last) {
+      if (use_k) {
+        for (int j = tid; j < SMP_NBIN; j += SMP_NT) ws->hist_k[j] = 0.f;
+        for (int j = tid; j < 4 * 256; j += SMP_NT) ws->hist_r[j / 256][j % 256] = 0.f;
+      }
+      if (use_p) {
+        for (int j = tid; j < SMP_NBIN; j += SMP_NT) ws->hist_p[j] = 0.f;
+        for (int j = tid; j < 4 * 256; j += SMP_NT) ws->hist_r[4 + j / 256][j % 256] = 0.f;
+      }
+      if (tid < 16) ws->bar[tid] = 0;
+      if (tid == 0) {
+        ws->maxkey = 0;
+        ws->z = 0.f;
+        ws->ncand[0] = 0;
+        ws->ncand[1] = 0;
+      }
+    }
+  }
+  SMP_STAMP(12);
+}
+
+void sample_stamps_enable(bool on) {
+  const int v = on ? 1 : 0;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_smp_stamp_on), &v, sizeof(v));
+}
+
+void sample_stamps_read(uint64_t* out16) {
+  (void)hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_smp_stamps), 16 * sizeof(uint64_t));
 }
 
 // workgroups per row of the cooperative sampler: the whole grid must be co-resident

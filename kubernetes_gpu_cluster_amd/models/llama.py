@@ -183,10 +183,11 @@ class LlamaForCausalLM(nn.Module):
 
     # ------------------------------------------------------------------ fused projection tails
     def _tail_fusable(self, x) -> bool:
-        """One GPU, whole model, dense bias-free MLP / o_proj, and a K9m plan at this M:
-        the o / down projections then run with their reduction fused into the next norm."""
+        """One GPU, whole model, dense bias-free MLP / o_proj, and a fused-tail plan at this
+        M (K9m split-K, or K9 SK_ACC_NORM at small M): the o / down projections then run
+        with their reduction / residual add fused into the next norm."""
         if not (x.is_cuda and self.first and self.last and self.layers and not self.cfg.is_moe
-                and get_state().tp_size == 1 and gemm.dgemm_plan_has_m(x.shape[0], "tail")
+                and get_state().tp_size == 1 and gemm.tail_plan_has_m(x.shape[0])
                 and _tail_fusion_enabled):
             return False
         l0 = self.layers[0]

@@ -37,6 +37,11 @@ _rms_us: dict[tuple[int, int], float] = {}
 # merged gate_up (M, 2I, K) -> cfg of the SK_SILU skinny variant, where it measured faster
 # than the plain plan + a silu_mul launch
 _plan_silu: dict[tuple[int, int, int], tuple[int, int, int, bool]] = {}
+# row-parallel (o / down) (M, N, K) -> cfg of the SK_ACC_NORM skinny variant (residual add
+# and the consuming RMSNorm inside the GEMM launch), where it measured faster than the
+# plain plan + fused_add_rms_norm; and the per-device tickets that variant draws
+_plan_accnorm: dict[tuple[int, int, int], tuple[int, int, int, bool]] = {}
+_tickets: dict[torch.device, torch.Tensor] = {}
 _enabled = os.environ.get("KGC_SKINNY_GEMM", "1") != "0"
 
 # K9m mid-batch decode GEMM (csrc/kernels/gemm_decode.hip), M in (SKINNY_MAX_M, DG_MAX_M]:
@@ -168,6 +173,12 @@ def linear_add_rms(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor,
     plan runs K9m split-K at this (M, N, K), the slice reduction, residual add and norm are
     one kernel (``splitk_add_rms_norm``); otherwise the GEMM and ``fused_add_rms_norm``."""
     from . import _k, fused_add_rms_norm
+    if _plan_accnorm and x.is_cuda and x.dim() == 2 and x.stride(1) == 1:
+        cfg = _plan_accnorm.get((x.shape[0], w.shape[0], w.shape[1]))
+        if cfg is not None and residual.is_contiguous():
+            out = torch.empty_like(residual)
+            skinny_acc_norm(residual, x, w, gamma, eps, cfg, out)
+            return out, residual
     p = _dg_plan(x, w, "tail")
     if p is not None and w.shape[0] <= 8192 and residual.is_contiguous():
         cfg, S = p
@@ -239,6 +250,22 @@ def skinny_silu(x: torch.Tensor, w: torch.Tensor, cfg,
     return out
 
 
+def _ticket(device: torch.device) -> torch.Tensor:
+    t = _tickets.get(device)
+    if t is None:
+        t = _tickets[device] = torch.zeros(16, dtype=torch.int32, device=device)
+    return t
+
+
+def skinny_acc_norm(residual: torch.Tensor, x: torch.Tensor, w: torch.Tensor,
+                    gamma: torch.Tensor, eps: float, cfg, out: torch.Tensor) -> torch.Tensor:
+    """residual += x W^T; out = rms_norm(residual) * gamma -- one launch (K9 SK_ACC_NORM:
+    the last workgroup of the grid normalises the finished rows)."""
+    from . import _k
+    _k().skinny_gemm(residual, x, w, None, *cfg, 4, gamma, eps, out, _ticket(x.device))
+    return out
+
+
 def skinny_accum(out: torch.Tensor, x: torch.Tensor, w: torch.Tensor,
                  bias: Optional[torch.Tensor], cfg) -> torch.Tensor:
     """out += x W^T (+ bias) in one launch (K9 SK_ACC epilogue: the residual add)."""
@@ -264,6 +291,7 @@ def fused_norm_plan(M: int, norm_shapes, acc_shapes):
 
 
 def clear_plan() -> None:
+    _plan_accnorm.clear()
     _plan_silu.clear()
     _plan_dg.clear()
     _plan_norm.clear()
@@ -286,6 +314,15 @@ def dgemm_plan() -> dict:
 
 def dgemm_plan_has_m(M: int, kind: str) -> bool:
     return _dg_enabled and any(k[0] == M and k[3] == kind for k in _plan_dg)
+
+
+def tail_plan_has_m(M: int) -> bool:
+    """A fused projection-tail plan at this M: K9m split-K (M > 64) or SK_ACC_NORM."""
+    return dgemm_plan_has_m(M, "tail") or any(k[0] == M for k in _plan_accnorm)
+
+
+def accnorm_plan() -> dict:
+    return dict(_plan_accnorm)
 
 
 def _time(fn, reps: int) -> float:
@@ -353,6 +390,8 @@ def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: floa
                 _tune_norm(ws, x, out, M, N, K, reps)
             if (N, K) in silu_shapes:
                 _tune_silu(ws, x, M, N, K, reps, margin)
+            if (N, K) in tail_shapes and N % 512 == 0 and N <= 8192:
+                _tune_accnorm(ws, x, M, N, K, reps, margin)
             log.info("gemm M=%d N=%d K=%d: hipBLASLt %.1f us, skinny %s %.1f us -> %s", M, N, K,
                      lib_t * 1e3 / n, sk_cfg, sk_t * 1e3 / n, "skinny" if best else "hipBLASLt")
         if _dg_enabled:
@@ -465,6 +504,8 @@ def _tune_silu(ws, x, M: int, N: int, K: int, reps: int, margin: float) -> None:
     """Time the SK_SILU variants against the plain plan (skinny or hipBLASLt, as just
     chosen) followed by silu_mul, over every layer's gate_up weight."""
     from . import silu_mul
+    if os.environ.get("KGC_SKINNY_SILU", "1") == "0":
+        return
     act = torch.empty(M, N // 2, dtype=x.dtype, device=x.device)
 
     def sep():
@@ -488,6 +529,48 @@ def _tune_silu(ws, x, M: int, N: int, K: int, reps: int, margin: float) -> None:
     log.info("gemm M=%d N=%d K=%d silu: plan + silu_mul %.1f us, SK_SILU %s %.1f us -> %s",
              M, N, K, sep_t * 1e3 / n, best_cfg, best_t * 1e3 / n,
              "SK_SILU" if (M, N, K) in _plan_silu else "separate")
+
+
+def _tune_accnorm(ws, x, M: int, N: int, K: int, reps: int, margin: float) -> None:
+    """Time SK_ACC_NORM against the plain plan + fused_add_rms_norm, both captured in a
+    graph (the separate side is two launches per layer: eager timing would measure the
+    host's launch rate)."""
+    from . import fused_add_rms_norm
+    if os.environ.get("KGC_SKINNY_ACC_NORM", "1") == "0":
+        return
+    gamma = torch.ones(N, dtype=x.dtype, device=x.device)
+    res = torch.zeros(M, N, dtype=x.dtype, device=x.device)
+    out = torch.empty_like(res)
+
+    def graphed(body):
+        body()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            body()
+        return _time(g.replay, reps)
+
+    def sep():
+        for w in ws:
+            fused_add_rms_norm(linear(x, w), res, gamma, 1e-6)
+    sep_t = graphed(sep)
+    best_t, best_cfg = float("inf"), None
+    for cfg in _CONFIGS:
+        if not skinny_ok(M, N, K, cfg) or (cfg[0] > 1 and M <= 16 * (cfg[0] // 2)):
+            continue
+
+        def fn(cfg=cfg):
+            for w in ws:
+                skinny_acc_norm(res, x, w, gamma, 1e-6, cfg, out)
+        t = graphed(fn)
+        if t < best_t:
+            best_t, best_cfg = t, cfg
+    n = len(ws)
+    if best_cfg is not None and best_t < sep_t * margin:
+        _plan_accnorm[(M, N, K)] = best_cfg
+    log.info("gemm M=%d N=%d K=%d tail: plan + add_rms_norm %.1f us, SK_ACC_NORM %s %.1f us "
+             "-> %s", M, N, K, sep_t * 1e3 / n, best_cfg, best_t * 1e3 / n,
+             "SK_ACC_NORM" if (M, N, K) in _plan_accnorm else "separate")
 
 
 def _tune_norm(ws, x, out, M: int, N: int, K: int, reps: int) -> None:

@@ -238,6 +238,30 @@ def test_sample(gpu, dt, B):
         assert g2.tolist() == got[plain].tolist()
 
 
+@pytest.mark.parametrize("B", [2, 8])
+def test_sample_threshold_ties_overflow_candidates(gpu, B):
+    """Integer-valued logits put ~10K tokens in every distance bin: the crossing bin holds
+    more than the candidate list (2048), so the cooperative kernel takes the global radix
+    passes; a tied top-k boundary keeps the whole tie group, as the reference does."""
+    torch.manual_seed(11)
+    V = 128256
+    logits = (torch.randn(B, V, device=gpu) * 3).round().to(torch.bfloat16)
+    temp = torch.ones(B, device=gpu)
+    top_k = torch.tensor([50, -1] * (B // 2), dtype=torch.int32, device=gpu)
+    top_p = torch.tensor([1.0, 0.9] * (B // 2), device=gpu)
+    seeds = torch.arange(B, dtype=torch.int64, device=gpu) * 31 + (9 << 32)
+    got = ops.sample(logits, temp, top_k, top_p, seeds).cpu()
+    exp = ref.sample(logits.cpu(), temp.cpu(), top_k.cpu(), top_p.cpu(), seeds.cpu())
+    assert got[0::2].tolist() == exp[0::2].tolist()
+    # top-p rows: the sampled token lies in the reference nucleus (whole tie groups)
+    for b in range(1, B, 2):
+        row = logits[b].float().cpu()
+        probs = torch.softmax(row, -1)
+        sp, _ = torch.sort(probs, descending=True)
+        keep = (torch.cumsum(sp, 0) - sp) < 0.9
+        assert probs[got[b]] >= sp[keep][-1]
+
+
 def test_sample_distribution(gpu):
     """Gumbel-max frequencies follow softmax(logits / T)."""
     V, N = 8, 20000
@@ -692,6 +716,87 @@ def test_tail_fused_model_matches_regular_path(gpu):
         for l in model.layers:
             for w in (l.self_attn.o_proj.weight, l.mlp.down_proj.weight):
                 gemm._plan_dg[(M, w.shape[0], w.shape[1], "tail")] = (2, 4)
+        llama_mod._tail_fusion_enabled = True
+        assert model._tail_fusable(x)
+        got = model(ids, None, _Ctx())
+    finally:
+        gemm.clear_plan()
+        llama_mod._tail_fusion_enabled = True
+    torch.testing.assert_close(got.float(), ref_out.float(), atol=6e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("M,N,K,cfg", [(1, 4096, 4096, (1, 1, 4, True)),
+                                       (5, 4096, 14336, (1, 2, 8, False)),
+                                       (16, 1024, 2048, (1, 1, 16, True)),
+                                       (40, 512, 1024, (4, 2, 4, False))])
+def test_skinny_acc_norm_matches_fp32(gpu, M, N, K, cfg):
+    """K9 SK_ACC_NORM: residual += x W^T, then out = rms_norm(residual) * gamma by the last
+    workgroup of the same launch, vs fp32; repeated eager calls and graph replays re-arm
+    the ticket (every call normalises, none is skipped)."""
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, dtype=torch.bfloat16, device=gpu)
+    w = torch.randn(N, K, dtype=torch.bfloat16, device=gpu) * K ** -0.5
+    res0 = torch.randn(M, N, dtype=torch.bfloat16, device=gpu)
+    gamma = torch.rand(N, dtype=torch.bfloat16, device=gpu) + 0.5
+
+    def expect(r_before):
+        r32 = r_before.float().cpu() + x.float().cpu() @ w.float().cpu().t()
+        return r32, r32 * torch.rsqrt(r32.pow(2).mean(-1, keepdim=True) + 1e-5) * gamma.float().cpu()
+    res = res0.clone()
+    out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=gpu)
+    for _ in range(3):
+        before = res.clone()
+        gemm.skinny_acc_norm(res, x, w, gamma, 1e-5, cfg, out)
+        r32, exp = expect(before)
+        torch.testing.assert_close(res.float().cpu(), r32, atol=5e-2, rtol=2e-2)
+        # normalised from the bf16 residual as stored: compare against that exactly-rounded row
+        rb = res.float().cpu()
+        exact = (rb * torch.rsqrt(rb.pow(2).mean(-1, keepdim=True) + 1e-5) * gamma.float().cpu())
+        torch.testing.assert_close(out.float().cpu(), exact, atol=2e-2, rtol=1e-2)
+        torch.testing.assert_close(out.float().cpu(), exp, atol=6e-2, rtol=3e-2)
+    assert int(gemm._ticket(x.device)[0]) == 0
+    g = torch.cuda.CUDAGraph()
+    res.copy_(res0)
+    with torch.cuda.graph(g):
+        gemm.skinny_acc_norm(res, x, w, gamma, 1e-5, cfg, out)
+    for _ in range(2):
+        res.copy_(res0)
+        out.fill_(float("nan"))
+        g.replay()
+        torch.cuda.synchronize()
+        _, exp = expect(res0)
+        torch.testing.assert_close(out.float().cpu(), exp, atol=6e-2, rtol=3e-2)
+    assert int(gemm._ticket(x.device)[0]) == 0
+
+
+def test_tail_fused_model_small_m_acc_norm(gpu):
+    """Whole-model forward at M = 4 with o/down + the consuming norms as SK_ACC_NORM
+    launches (forced plan) vs the regular layer loop on the same weights."""
+    from kubernetes_gpu_cluster_amd.models import configs
+    from kubernetes_gpu_cluster_amd.models.llama import LlamaForCausalLM
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    from kubernetes_gpu_cluster_amd.models import llama as llama_mod
+    cfg = configs.PRESETS["llama-3-8b"].shrink(name="tail-fuse-s", num_layers=2)
+    torch.manual_seed(1)
+    model = LlamaForCausalLM(cfg, torch.bfloat16, gpu)
+    for p in model.parameters():
+        p.data.normal_(0, 0.02) if p.dim() == 2 else p.data.fill_(1.0)
+    M = 4
+    ids = torch.randint(0, cfg.vocab_size, (M,), device=gpu)
+    x = model.embed_tokens(ids)
+
+    class _Ctx:
+        pass
+    for l in model.layers:
+        l.self_attn.attend = (lambda positions, qkv, ctx, nq=l.self_attn.nq * cfg.head_dim:
+                              qkv[:, :nq].contiguous())
+    try:
+        llama_mod._tail_fusion_enabled = False
+        ref_out = model(ids, None, _Ctx())
+        for l in model.layers:
+            for w in (l.self_attn.o_proj.weight, l.mlp.down_proj.weight):
+                gemm._plan_accnorm[(M, w.shape[0], w.shape[1])] = (1, 1, 8, True)
         llama_mod._tail_fusion_enabled = True
         assert model._tail_fusable(x)
         got = model(ids, None, _Ctx())
