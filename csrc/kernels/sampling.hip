@@ -664,15 +664,25 @@ void sample_stamps_read(uint64_t* out16) {
   (void)hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_smp_stamps), 16 * sizeof(uint64_t));
 }
 
-// workgroups per row of the cooperative sampler: the whole grid must be co-resident
-// (one 1024-thread workgroup per CU is always available): B * S <= 256
-// Workgroups per row (0: use the single-workgroup-threshold kernel).  Measured on
-// MI355X (profiles/sample_microbench.jsonl): 16 per row up to B = 16, then 256 / B; above
-// B = 128 one cooperative workgroup per row loses to the older kernel, which splits the
-// argmax over 2 workgroups per row (B * S must stay <= 256 for co-residency).
+// Workgroups per row of the cooperative sampler (0: use the single-workgroup-threshold
+// kernel).  The whole grid must be co-resident (one 1024-thread workgroup per CU is always
+// available), so B * S <= the device's CU count (256 on a whole MI355X, fewer in a
+// partitioned mode); with S = 1 a row's barriers wait for nobody.  Measured on MI355X
+// (profiles/sample_microbench.jsonl): 16 per row up to B = 16, then CUs / B; at B = 256
+// one workgroup per row (top-p 549 -> 268 us against the older kernel).
 int sample_coop_splits(int B) {
-  if (B > 128) return 0;
-  return std::max(1, std::min(16, 256 / B));
+  static int cus[64] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) return 0;
+  if (cus[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 1;   // unknown: never co-resident enough for more than one row -> older kernel
+    cus[dev] = n;
+  }
+  if (B > cus[dev]) return 0;
+  return std::max(1, std::min(16, cus[dev] / B));
 }
 
 void launch_sample_coop(int dtype, int64_t* out, uint64_t* partial, void* ws, const void* logits,

@@ -210,7 +210,7 @@ def test_prefill_matches_dense(gpu):
 
 
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("B", [16, 1, 4, 260])
+@pytest.mark.parametrize("B", [16, 1, 4, 256, 260])
 def test_sample(gpu, dt, B):
     """B <= 256: the cooperative kernel (threshold passes split over each row's
     workgroups, per-row barriers); B = 260: the single-workgroup-per-threshold kernel."""
