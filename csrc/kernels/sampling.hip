@@ -327,7 +327,7 @@ __global__ __launch_bounds__(SMP_NT) void sample_coop_kernel(
   __shared__ float hist_d[SMP_NBIN];
   __shared__ float scan_w[SMP_NT / 64];
   __shared__ uint32_t sel_bin;
-  __shared__ float sel_f;
+  __shared__ float sel_f, sel_t;
   __shared__ uint32_t cand_k[SMP_CAP];
   __shared__ uint64_t cand_m[SMP_CAP];
   __shared__ uint64_t hist_u[256];
@@ -497,17 +497,95 @@ __global__ __launch_bounds__(SMP_NT) void sample_coop_kernel(
       }
       return prefix;
     };
-    if (use_k) {
-      for (int j = tid; j < SMP_NBIN; j += SMP_NT) hist_d[j] = 0.f;
+    // wave 0: over h[0..n) (n <= 128, ascending distance = descending logit), the first
+    // bin whose running total (from `start`) reaches `target` -> sel_bin, the total before
+    // it -> sel_f; no crossing: the last bin.  Lane l scans bins 2l, 2l + 1.
+    auto wave_cross = [&](const float* h, int n, float start, float target) {
+      if (w == 0) {
+        const float v0 = 2 * lane < n ? h[2 * lane] : 0.f;
+        const float v1 = 2 * lane + 1 < n ? h[2 * lane + 1] : 0.f;
+        float incl = v0 + v1;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const float u = __shfl_up(incl, o, 64);
+          if (lane >= o) incl += u;
+        }
+        incl += start;
+        const float e0 = incl - v0 - v1, e1 = e0 + v0;
+        if (2 * lane == n - 1) { sel_bin = n - 1; sel_f = e0; }
+        if (2 * lane + 1 == n - 1) { sel_bin = n - 1; sel_f = e1; }
+        if (2 * lane < n && e0 < target && e1 >= target) { sel_bin = 2 * lane; sel_f = e0; }
+        else if (2 * lane + 1 < n && e1 < target && incl >= target) { sel_bin = 2 * lane + 1; sel_f = e1; }
+      }
       __syncthreads();
-      visit_row(row, i_lo, i_hi, tid, [&](int, float r) { atomicAdd(&hist_d[dbin(r)], 1.f); });
-      SMP_STAMP(3);
-      publish(hist_d, ws->hist_k, SMP_NBIN);
+    };
+    // The crossing distance bin of a threshold, two-level: per-thread register counters over
+    // NCB coarse bins (2 nats = 128 distance bins each) -- no LDS atomic per logit -- summed
+    // over the row, then LDS-atomic distance bins only for the logits of the crossing
+    // coarse bin.  wt(r) = the logit's weight (< 0: not counted); g = the row's global
+    // histogram (NCB coarse + 128 fine bins); target_of(row total) = the weight to reach.
+    // Returns the distance bin; sel_f = the weight above it, sel_t = the target.
+    constexpr int NCB = SMP_NBIN / 128;
+    auto dist_cross = [&](auto&& wt, float* g, auto&& target_of) -> int {
+      float acc[NCB];
+#pragma unroll
+      for (int j = 0; j < NCB; ++j) acc[j] = 0.f;
+      visit_row(row, i_lo, i_hi, tid, [&](int, float r) {
+        const float x = wt(r);
+        if (x < 0.f) return;
+        const int cb = dbin(r) >> 7;
+#pragma unroll
+        for (int j = 0; j < NCB; ++j) acc[j] += cb == j ? x : 0.f;
+      });
+      if (tid < 128) hist_d[tid] = 0.f;
+      __syncthreads();
+      // reduce-scatter of the NCB = 16 counters over the wave by recursive halving: 8 + 4 +
+      // 2 + 1 shuffles (not 16 x 6), then 2 to finish; lanes 4c..4c+3 hold coarse bin c
+#pragma unroll
+      for (int half = NCB / 2, off = 32; half >= 1; half >>= 1, off >>= 1) {
+        const bool hi = (lane & off) != 0;
+#pragma unroll
+        for (int j = 0; j < half; ++j) {
+          const float mine = hi ? acc[half + j] : acc[j];
+          const float other = hi ? acc[j] : acc[half + j];
+          acc[j] = mine + __shfl_xor(other, off, 64);
+        }
+      }
+      acc[0] += __shfl_xor(acc[0], 2, 64);
+      acc[0] += __shfl_xor(acc[0], 1, 64);
+      if ((lane & 3) == 0 && acc[0] != 0.f) atomicAdd(&hist_d[lane >> 2], acc[0]);
+      publish(hist_d, g, NCB);
       row_barrier();
-      fetch(hist_d, ws->hist_k, SMP_NBIN);
-      cross_dist((float)k);
+      fetch(hist_d, g, NCB);
+      // the row's total weight, summed in the same order in every workgroup
+      float total = 0.f;
+      for (int j = 0; j < NCB; ++j) total += hist_d[j];
+      const float target = target_of(total);
+      if (tid == 0) sel_t = target;
+      wave_cross(hist_d, NCB, 0.f, target);
+      const int cbin = (int)sel_bin;
+      const float above = sel_f;
+      __syncthreads();
+      if (tid < 128) hist_d[tid] = 0.f;
+      __syncthreads();
+      visit_row(row, i_lo, i_hi, tid, [&](int, float r) {
+        const int d = dbin(r);
+        if ((d >> 7) != cbin) return;
+        const float x = wt(r);
+        if (x >= 0.f) atomicAdd(&hist_d[d & 127], x);
+      });
+      publish(hist_d, g + NCB, 128);
+      row_barrier();
+      fetch(hist_d, g + NCB, 128);
+      wave_cross(hist_d, 128, above, target);
+      return cbin * 128 + (int)sel_bin;
+    };
+    if (use_k) {
+      SMP_STAMP(3);
+      const int kbin_ = dist_cross([&](float) { return 1.f; }, ws->hist_k,
+                                   [&](float) { return (float)k; });
       SMP_STAMP(4);
-      const int kbin = (int)sel_bin;
+      const int kbin = kbin_;
       uint32_t prefix = 0, mask = 0;
       float remaining = (float)k - sel_f;
       collect(0, [&](float r) { return dbin(r) == kbin ? 1.f : -1.f; });
@@ -537,27 +615,14 @@ __global__ __launch_bounds__(SMP_NT) void sample_coop_kernel(
       thr = key_val(prefix);
     }
     if (use_p) {
-      for (int j = tid; j < SMP_NBIN; j += SMP_NT) hist_d[j] = 0.f;
-      __syncthreads();
-      float z = 0.f;
-      visit_row(row, i_lo, i_hi, tid, [&](int, float r) {
-        if (r >= thr) {
-          const float e = __expf((r - mx) * it);
-          z += e;
-          atomicAdd(&hist_d[dbin(r)], e);
-        }
-      });
-      z = block_sum<SMP_NT>(z, red_v);
-      if (tid == 0) atomicAdd(&ws->z, z);
       SMP_STAMP(7);
-      publish(hist_d, ws->hist_p, SMP_NBIN);
-      row_barrier();
-      z = gload(&ws->z);
-      fetch(hist_d, ws->hist_p, SMP_NBIN);
-      const float target = p * z;
-      cross_dist(target);
+      // the mass target p * z, z = the row's softmax mass over the top-k support (the
+      // coarse histogram's total)
+      const int pbin_ = dist_cross([&](float r) { return r >= thr ? __expf((r - mx) * it) : -1.f; },
+                                   ws->hist_p, [&](float zt) { return p * zt; });
+      const float target = sel_t;
       SMP_STAMP(8);
-      const int pbin = (int)sel_bin;
+      const int pbin = pbin_;
       uint32_t prefix = 0, mask = 0;
       float above = sel_f;
       const uint32_t kthr = ord_key(thr);
