@@ -76,8 +76,10 @@ def main():
             agg.update(s[3])
         for k, v in agg.most_common(16):
             print(f"   {k:38} {v / len(dec) / 1e3:9.1f} us/step")
-        # prefill (chunked) steps: the ones that run the prefill attention kernel
-        pre = [s for s in steps if s[3].get("prefill_attn", 0) > 0]
+        # prefill (chunked) steps: the ones that run the prefill attention kernel and no
+        # decode-sized GEMM (start-up tuning runs those between sampler calls too)
+        pre = [s for s in steps if s[3].get("prefill_attn", 0) > 0
+               and not s[3].get("skinny_gemm(K9)") and not s[3].get("dgemm(K9m)")]
         if pre:
             print(f"\nprefill steps: {len(pre)}")
             print(f"median span {statistics.median([s[0] for s in pre]) / 1e6:.3f} ms, "
