@@ -95,7 +95,7 @@ __device__ __forceinline__ int64_t weight_row(int nb, int r, int N) {
 template <typename T, int BM, int BN, int EPI, bool PK, int ABL = ABL_NONE, int LDW = 0>
 __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
     void* __restrict__ Cv, const T* __restrict__ X, const T* __restrict__ W, int M, int N,
-    int K, int64_t ldx, int S, int MB, int64_t slice_stride) {
+    int K, int64_t ldx, int S, int MB, int64_t slice_stride, int xmap) {
   constexpr int MT = BM / 4 / 16;                 // 16-row MFMA tiles per wave
   constexpr int NT = BN / 2 / 16;                 // 16-col MFMA tiles per wave
   constexpr int NIW = LDW > 0 ? LDW : 8;          // waves issuing DMAs
@@ -113,9 +113,23 @@ __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
   const bool consumer = LDW == 0 || wave < 8;
   const int iw = LDW > 0 ? wave - 8 : wave;       // index among the issuing waves
   const int wm = (wave >> 1) & 3, wn = wave & 1;
-  const int z = blockIdx.x % S;
-  const int j = blockIdx.x / S;
-  const int mb = j % MB, nb = j / MB;
+  int z, j, mb, nb;
+  if (xmap) {
+    // XCD-paired row blocks (host: S | 8, (N / BN) % (8 / S) == 0): workgroups L and L + 8
+    // -- one XCD under round-robin placement (speed only, never correctness) -- take the
+    // row blocks of the SAME weight columns and K-slice, so the second read of each weight
+    // tile is an L2 hit instead of an HBM (or Infinity Cache) read
+    const int r8 = blockIdx.x & 7, q = blockIdx.x >> 3, cpg = 8 / S;
+    z = r8 % S;
+    mb = q % MB;
+    nb = (q / MB) * cpg + r8 / S;
+    j = nb * MB + mb;
+  } else {
+    z = blockIdx.x % S;
+    j = blockIdx.x / S;
+    mb = j % MB;
+    nb = j / MB;
+  }
   const int m0 = mb * BM;
 
   // ---- DMA sources: lane l of instruction i fills LDS row 8i + l/8, 16-B slot l%8 with
@@ -432,19 +446,25 @@ __global__ __launch_bounds__(256) void dgemm_pack_kernel(T* __restrict__ P,
 // ids 8, 9 = split loaders (dgemm_sl_kernel) 256 x 128 with a 4- / 128 x 128 with a 6-slot
 // weight ring.  (A 2-slot activation ring with the LDS given to a 6- / 8-slot weight ring
 // measured 5-10 % slower on every shape: profiles/k9m_dgemm_bench_r2_sweep.jsonl.)
-constexpr int kNumCfgs = 10;
+// id 10 = 5 with XCD-paired row blocks (the two 128-row blocks of a column tile on one XCD:
+// o_proj at M = 256, S = 4 17.4 vs 18.9 us).  128 x 256 tiles (weights packed 256 wide,
+// 3-slot ring of 48 KB) measured 20-30 % slower than the split loaders on gate_up and
+// down, with or without the pairing (profiles/k9m_dgemm_bench_r2_sweep.jsonl).
+constexpr int kNumCfgs = 11;
 static const int kCfg[kNumCfgs][3] = {{256, 128, 0}, {256, 64, 0},  {128, 128, 0}, {128, 64, 0},
                                       {256, 128, 1}, {128, 128, 1}, {256, 128, 1}, {128, 128, 1},
-                                      {256, 128, 1}, {128, 128, 1}};
+                                      {256, 128, 1}, {128, 128, 1}, {128, 128, 1}};
 
 template <typename T, int BM, int BN, bool PK, int LDW = 0>
 void dgemm_cfg(int epi, void* C, const void* X, const void* W, int M, int N, int K, int64_t ldx,
-               int S, int64_t ss, hipStream_t s) {
+               int S, int64_t ss, hipStream_t s, int xmap = 0) {
   const int MB = (M + BM - 1) / BM;
   const dim3 grid((unsigned)(MB * (N / BN) * S));
+  // the XCD pairing needs S | 8 and whole groups of 8 / S column tiles
+  const int xm = (xmap && MB > 1 && 8 % S == 0 && (N / BN) % (8 / S) == 0) ? 1 : 0;
 #define DG_LAUNCH(E)                                                             \
   dgemm_kernel<T, BM, BN, E, PK, ABL_NONE, LDW><<<grid, DG_THREADS + LDW * 64, 0, s>>>( \
-      C, (const T*)X, (const T*)W, M, N, K, ldx, S, MB, ss)
+      C, (const T*)X, (const T*)W, M, N, K, ldx, S, MB, ss, xm)
   if (epi == EPI_PARTIAL) DG_LAUNCH(EPI_PARTIAL);
   else if (epi == EPI_OUT) DG_LAUNCH(EPI_OUT);
   else DG_LAUNCH(EPI_SILU);
@@ -464,7 +484,8 @@ void dgemm_t(int cfg, int epi, void* C, const void* X, const void* W, int M, int
     case 6: dgemm_cfg<T, 256, 128, true, 4>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
     case 7: dgemm_cfg<T, 128, 128, true, 4>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
     case 8: dgemm_sl_cfg<T, 256, 128, 4>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
-    default: dgemm_sl_cfg<T, 128, 128, 6>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
+    case 9: dgemm_sl_cfg<T, 128, 128, 6>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
+    default: dgemm_cfg<T, 128, 128, true>(epi, C, X, W, M, N, K, ldx, S, ss, s, 1); break;
   }
 }
 
@@ -491,11 +512,11 @@ void launch_dgemm_pack(int dtype, bool silu, void* P, const void* W, int N, int 
 #define PACK(T, E) \
   dgemm_pack_kernel<T, 128, E><<<grid, 256, 0, s>>>((T*)P, (const T*)W, N, K)
   if (dtype == DT_BF16) {
-    if (silu) PACK(bf16, EPI_SILU);
-    else PACK(bf16, EPI_OUT);
+    if (silu) { PACK(bf16, EPI_SILU); }
+    else { PACK(bf16, EPI_OUT); }
   } else {
-    if (silu) PACK(f16, EPI_SILU);
-    else PACK(f16, EPI_OUT);
+    if (silu) { PACK(f16, EPI_SILU); }
+    else { PACK(f16, EPI_OUT); }
   }
 #undef PACK
 }
@@ -507,7 +528,7 @@ void launch_dgemm_ablate(int mode, float* C, const void* X, const void* W, int M
   const dim3 grid((unsigned)(MB * (N / 128) * S));
 #define AB(MODE)                                                                     \
   dgemm_kernel<bf16, 256, 128, EPI_PARTIAL, true, MODE><<<grid, DG_THREADS, 0, s>>>( \
-      C, (const bf16*)X, (const bf16*)W, M, N, K, ldx, S, MB, ss)
+      C, (const bf16*)X, (const bf16*)W, M, N, K, ldx, S, MB, ss, 0)
   switch (mode) {
     case ABL_NO_MFMA: AB(ABL_NO_MFMA); break;
     case ABL_NO_DMA: AB(ABL_NO_DMA); break;

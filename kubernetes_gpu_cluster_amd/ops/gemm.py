@@ -405,10 +405,11 @@ def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: floa
 
 
 # K9m candidates per M range: (cfg ids, split factors).  Packed tiles only when the weight
-# was packed; 4 loader waves (6, 7) and split loaders (8, 9) per tools/dgemm_bench.py.
+# was packed; 4 loader waves (6, 7), split loaders (8, 9) and XCD-paired 128-row blocks (10)
+# per tools/dgemm_bench.py.
 def _dg_candidates(M: int, N: int, K: int, kind: str, packed: bool):
     from . import _k
-    cfgs = [5, 7, 2] if M <= 128 else [6, 8, 4, 0]
+    cfgs = [5, 7, 2] if M <= 128 else [6, 8, 4, 0, 10]
     out = []
     for c in range(_k().dgemm_num_cfgs()):
         if c not in cfgs:

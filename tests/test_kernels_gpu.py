@@ -560,7 +560,7 @@ def test_tune_skinny_silu_records_plan(gpu):
         gemm.clear_plan()
 
 
-@pytest.mark.parametrize("cfg", list(range(10)))
+@pytest.mark.parametrize("cfg", list(range(11)))
 @pytest.mark.parametrize("M,N,K", [(256, 1024, 4096), (200, 768, 1024), (77, 512, 2048)])
 def test_dgemm_matches_fp32(gpu, cfg, M, N, K):
     """K9m decode GEMM (every tile config, packed and row-major weights) vs an fp32 matmul:

@@ -60,6 +60,7 @@ def main():
     ap.add_argument("--only", default=None,
                     help="cfg:S:epi -- time just this configuration (profiling runs)")
     ap.add_argument("--no-lib", action="store_true", help="skip the hipBLASLt baseline")
+    ap.add_argument("--cfgs", default=None, help="comma list: only these tile configs")
     ap.add_argument("--ablate", default=None,
                     help="S value: time the packed 256 x 128 tile with modes full / no-MFMA / "
                          "no-DMA / no-A-DMA / no-B-DMA at this split")
@@ -87,6 +88,7 @@ def main():
                 k.dgemm_pack(p, w, silu)
                 out.append(p)
             return out
+        want_cfgs = None if not a.cfgs else {int(c) for c in a.cfgs.split(",")}
         wps = {False: packed(False)}
         if name == "gate_up":
             wps[True] = packed(True)
@@ -118,7 +120,7 @@ def main():
             cfgs = []
             for cid in range(k.dgemm_num_cfgs()):
                 bm, bn, pk = k.dgemm_cfg_info(cid)
-                if (bm == 256 and M <= 128) or N % bn:
+                if (bm == 256 and M <= 128) or N % bn or (want_cfgs is not None and cid not in want_cfgs):
                     continue
                 for S in [int(s) for s in a.splits.split(",")]:
                     if K // 64 < S:
