@@ -190,6 +190,82 @@ void paged_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor b
                            (float)k_scale, (float)v_scale, (int)k_cache.size(0), stream());
 }
 
+// paged_decode with rope_kv_write folded in (decode-only steps): qkv is the projection
+// [B, >= (nq+2nkv)*d] in the activation dtype, or its K9m fp32 split-K slices [S, B, N].
+void paged_decode_rope(Tensor out, Tensor qkv, Tensor positions, Tensor cos_sin, Tensor k_cache,
+                       Tensor v_cache, Tensor slot_mapping, std::optional<Tensor> q_norm_w,
+                       std::optional<Tensor> k_norm_w, Tensor block_tables, Tensor ctx_lens,
+                       Tensor max_logits, Tensor exp_sums, Tensor tmp_out, int64_t nq,
+                       int64_t Z, double scale, double eps, bool use_rope, double k_scale,
+                       double v_scale) {
+  check_gpu(qkv, "qkv");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
+  TORCH_CHECK(out.dim() == 3 && out.is_contiguous() && out.size(1) == nq,
+              "kgc.paged_decode_rope: out [B, nq, d] contiguous");
+  const int64_t B = out.size(0), d = out.size(2), nkv = k_cache.size(1);
+  check_kv(out, k_cache, v_cache, nq);
+  TORCH_CHECK(k_cache.size(3) == d, "head_dim mismatch");
+  kgc::DecodeRope rp{};
+  const int64_t N = (nq + 2 * nkv) * d;
+  if (qkv.dim() == 3) {
+    TORCH_CHECK(qkv.scalar_type() == at::kFloat && qkv.is_contiguous() && qkv.size(1) == B &&
+                qkv.size(2) >= N && qkv.size(2) % 8 == 0 && qkv.size(0) >= 1,
+                "kgc.paged_decode_rope: slices fp32 [S, B, (nq+2nkv)*d] contiguous");
+    rp.S = (int)qkv.size(0);
+    rp.slice_stride = qkv.stride(0);
+    rp.qkv_stride = qkv.stride(1);
+  } else {
+    TORCH_CHECK(qkv.dim() == 2 && qkv.size(0) == B && qkv.stride(1) == 1 && qkv.size(1) >= N &&
+                qkv.stride(0) % 8 == 0 && qkv.scalar_type() == out.scalar_type(),
+                "kgc.paged_decode_rope: qkv [B, (nq+2nkv)*d] in the output dtype");
+    rp.S = 0;
+    rp.qkv_stride = qkv.stride(0);
+  }
+  TORCH_CHECK(positions.scalar_type() == at::kLong && positions.numel() == B, "positions int64 [B]");
+  TORCH_CHECK(slot_mapping.scalar_type() == at::kLong && slot_mapping.numel() == B,
+              "slot_mapping int64 [B]");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() && cos_sin.size(1) == d,
+              "cos_sin fp32 [max_pos, d]");
+  TORCH_CHECK(block_tables.scalar_type() == at::kInt && block_tables.dim() == 2 &&
+              block_tables.size(0) >= B && block_tables.is_contiguous(),
+              "block_tables int32 [B, max_blocks] contiguous");
+  TORCH_CHECK(ctx_lens.scalar_type() == at::kInt && ctx_lens.numel() >= B, "ctx_lens int32 [B]");
+  TORCH_CHECK(max_logits.scalar_type() == at::kFloat && exp_sums.scalar_type() == at::kFloat &&
+              tmp_out.scalar_type() == at::kFloat, "partials fp32");
+  const int64_t Zmax = max_logits.size(-1);
+  TORCH_CHECK(max_logits.is_contiguous() && exp_sums.is_contiguous() && tmp_out.is_contiguous() &&
+              max_logits.numel() >= B * nq * Zmax && exp_sums.numel() >= B * nq * Zmax &&
+              tmp_out.numel() >= B * nq * Zmax * d, "partials too small");
+  TORCH_CHECK(Z >= 1 && Z <= Zmax && Z <= 1024,
+              "kgc.paged_decode_rope: need 1 <= Z <= min(partial slots, 1024)");
+  TORCH_CHECK(k_scale > 0 && v_scale > 0, "kv scales must be > 0");
+  for (const Tensor* t : {&qkv, &positions, &cos_sin, &slot_mapping, &block_tables, &ctx_lens})
+    check_same_dev(out, *t, "paged_decode_rope operand");
+  if (q_norm_w.has_value()) {
+    TORCH_CHECK(k_norm_w.has_value() && q_norm_w->numel() == d && k_norm_w->numel() == d &&
+                q_norm_w->scalar_type() == out.scalar_type() &&
+                k_norm_w->scalar_type() == out.scalar_type(), "qk norm weights [d]");
+    rp.q_norm_w = q_norm_w->data_ptr();
+    rp.k_norm_w = k_norm_w->data_ptr();
+  }
+  rp.qkv = qkv.data_ptr();
+  rp.use_rope = use_rope ? 1 : 0;
+  rp.positions = positions.data_ptr<int64_t>();
+  rp.cos_sin = cos_sin.data_ptr<float>();
+  rp.slots = slot_mapping.data_ptr<int64_t>();
+  rp.eps = (float)eps;
+  rp.k_inv = (float)(1.0 / k_scale);
+  rp.v_inv = (float)(1.0 / v_scale);
+  kgc::launch_paged_decode_rope(dt_code(out), rp, out.data_ptr(), k_cache.data_ptr(),
+                                v_cache.data_ptr(), block_tables.data_ptr<int>(),
+                                (int)block_tables.stride(0), ctx_lens.data_ptr<int>(),
+                                max_logits.data_ptr<float>(), exp_sums.data_ptr<float>(),
+                                tmp_out.data_ptr<float>(), (int)B, (int)nq, (int)nkv, (int)d,
+                                log2_exact(k_cache.size(2), "block_size"), (int)Zmax, (int)Z,
+                                (float)scale, k_cache.scalar_type() == at::kFloat8_e4m3fn,
+                                (float)k_scale, (float)v_scale, (int)k_cache.size(0), stream());
+}
+
 void prefill_attention(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables,
                        Tensor query_start_loc, Tensor seq_lens, Tensor work_seq,
                        Tensor work_mblk, double scale, double k_scale, double v_scale) {
@@ -859,6 +935,11 @@ TORCH_LIBRARY(kgc, m) {
   m.def("paged_decode(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
         "Tensor block_tables, Tensor ctx_lens, Tensor(b!) max_logits, Tensor(c!) exp_sums, "
         "Tensor(d!) tmp_out, int Z, float scale, float k_scale=1.0, float v_scale=1.0) -> ()");
+  m.def("paged_decode_rope(Tensor(a!) out, Tensor qkv, Tensor positions, Tensor cos_sin, "
+        "Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor slot_mapping, Tensor? q_norm_w, "
+        "Tensor? k_norm_w, Tensor block_tables, Tensor ctx_lens, Tensor(d!) max_logits, "
+        "Tensor(e!) exp_sums, Tensor(f!) tmp_out, int nq, int Z, float scale, float eps, "
+        "bool use_rope, float k_scale=1.0, float v_scale=1.0) -> ()");
   m.def("prefill_attention(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
         "Tensor block_tables, Tensor query_start_loc, Tensor seq_lens, Tensor work_seq, "
         "Tensor work_mblk, float scale, float k_scale=1.0, float v_scale=1.0) -> ()");
@@ -930,6 +1011,7 @@ TORCH_LIBRARY_IMPL(kgc, CUDA, m) {
   m.impl("silu_mul", &silu_mul);
   m.impl("rope_kv_write", &rope_kv_write);
   m.impl("paged_decode", &paged_decode);
+  m.impl("paged_decode_rope", &paged_decode_rope);
   m.impl("prefill_attention", &prefill_attention);
   m.impl("sample", &sample);
   m.impl("sample_vp", &sample_vp);

@@ -22,6 +22,15 @@
 // The head of every accumulator element is lane&15, so the softmax statistics and
 // the O rescale are lane-local up to a 4-lane (xor 16/32) reduction.
 // Scores are kept in the log2 domain (scale * log2(e) folded in), exp2.
+//
+// FUSE (decode-only steps, launch_paged_decode_rope): the RoPE / q-k-norm / KV-write
+// kernel (rope_cache.hip) runs as this kernel's prologue: one thread per NeoX chunk
+// pair of the GQA group's heads builds q (split-K slice sum, q-norm, RoPE) into LDS,
+// where every wave picks up its MFMA B fragments, while wave 3 of the z-slice whose
+// last wave owns the final context token writes that token's k / v (workgroup fence +
+// barrier, then the normal loads see it through the CU's own L1).  Measured first
+// with every wave building its own q in registers (4 dependent slice round trips
+// each): 149 vs 137 us for rope_kv + decode at B = 256, S = 4.
 #include "common.h"
 #include "launch.h"
 #include <type_traits>
@@ -36,6 +45,137 @@ __device__ __forceinline__ u32x4 ld16(const void* p) {
   return *reinterpret_cast<const u32x4*>(p);
 }
 
+// ---- FUSE prologue helpers (rope_cache.hip computes the same values for the general
+// case; the roundings to T match it: summed slices, normed values and rotated outputs)
+template <typename T>
+__device__ __forceinline__ void qkv_row8(const DecodeRope& rp, int64_t e, float* x) {
+  if (rp.S == 0) {
+    Pack8<T> p;
+    p.u = ld16(reinterpret_cast<const T*>(rp.qkv) + e);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = to_f(p.h[j]);
+    return;
+  }
+  // SB = 4 slices' loads in flight per round trip (clamped duplicates are not added);
+  // summed z = 0, 1, ... from 0 as rope_cache.hip does: bit-identical
+  const float* src = reinterpret_cast<const float*>(rp.qkv) + e;
+  f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = a;
+  constexpr int SB = 4;
+  for (int z0 = 0; z0 < rp.S; z0 += SB) {
+    f32x4 ta[SB], tb[SB];
+#pragma unroll
+    for (int j = 0; j < SB; ++j) {
+      const int64_t z = min(z0 + j, rp.S - 1);
+      ta[j] = *reinterpret_cast<const f32x4*>(src + z * rp.slice_stride);
+      tb[j] = *reinterpret_cast<const f32x4*>(src + z * rp.slice_stride + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < SB; ++j)
+      if (z0 + j < rp.S) { a += ta[j]; b += tb[j]; }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    x[q] = to_f(from_f<T>(a[q]));
+    x[4 + q] = to_f(from_f<T>(b[q]));
+  }
+}
+
+// x * inv * w[col..col+7], rounded through T
+template <typename T>
+__device__ __forceinline__ void norm8(float* x, float inv, const void* w, int col) {
+  Pack8<T> wv;
+  wv.u = ld16(reinterpret_cast<const T*>(w) + col);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = to_f(from_f<T>(x[j] * inv * to_f(wv.h[j])));
+}
+
+// NeoX rotation of the chunk pair (a at col, b at col + D/2); cs = cos_sin row
+__device__ __forceinline__ void rope8(float* a, float* b, const float* cs, int col, int half) {
+  const float4 c0 = *reinterpret_cast<const float4*>(cs + col);
+  const float4 c1 = *reinterpret_cast<const float4*>(cs + col + 4);
+  const float4 s0 = *reinterpret_cast<const float4*>(cs + half + col);
+  const float4 s1 = *reinterpret_cast<const float4*>(cs + half + col + 4);
+  const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float xa = a[j], xb = b[j];
+    a[j] = xa * cc[j] - xb * sn[j];
+    b[j] = xb * cc[j] + xa * sn[j];
+  }
+}
+
+// The new token's k (rotated) and v of kv-head h into the paged cache: lanes
+// 0 .. D/16-1 own a k chunk pair (their D/16 lanes reduce the k-norm sum), lanes
+// 16 .. 16+D/8-1 one v chunk (8 two-byte stores into the V^T 8-key group).
+template <typename T, int D, bool KV8>
+__device__ __forceinline__ void decode_kv_write(const DecodeRope& rp, int b, int h, int nq,
+                                                int nkv, int bs_log2, int num_blocks,
+                                                void* kc_, void* vc_, int lane) {
+  int64_t slot = rp.slots[b];
+  KGC_DCHECK_RANGE(slot, -1, (int64_t)num_blocks << bs_log2, "decode KV slot");
+  if (slot < 0) return;
+  constexpr int TPH = D / 16, half = D / 2;
+  const int64_t blk = slot >> bs_log2;
+  const int off = (int)(slot & ((1 << bs_log2) - 1));
+  const int64_t row = (int64_t)b * rp.qkv_stride;
+  if (lane < TPH) {
+    const int c = lane;
+    float xa[8], xb[8];
+    qkv_row8<T>(rp, row + (int64_t)(nq + h) * D + c * 8, xa);
+    qkv_row8<T>(rp, row + (int64_t)(nq + h) * D + half + c * 8, xb);
+    if (rp.k_norm_w) {
+      float ss = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += xa[j] * xa[j] + xb[j] * xb[j];
+#pragma unroll
+      for (int o = 1; o < TPH; o <<= 1) ss += __shfl_xor(ss, o, 64);
+      const float inv = rsqrtf(ss / (float)D + rp.eps);
+      norm8<T>(xa, inv, rp.k_norm_w, c * 8);
+      norm8<T>(xb, inv, rp.k_norm_w, half + c * 8);
+    }
+    if (rp.use_rope) rope8(xa, xb, rp.cos_sin + rp.positions[b] * D, c * 8, half);
+    Pack8<T> oa, ob;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { oa.h[j] = from_f<T>(xa[j]); ob.h[j] = from_f<T>(xb[j]); }
+    const int64_t e = ((blk * nkv + h) << bs_log2 | off) * D;
+    if constexpr (KV8) {
+      uint8_t* dst = reinterpret_cast<uint8_t*>(kc_) + e;
+      float fa[8], fb[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { fa[j] = to_f(oa.h[j]) * rp.k_inv; fb[j] = to_f(ob.h[j]) * rp.k_inv; }
+      *reinterpret_cast<u32x2*>(dst + c * 8) =
+          u32x2{fp8x4(fa[0], fa[1], fa[2], fa[3]), fp8x4(fa[4], fa[5], fa[6], fa[7])};
+      *reinterpret_cast<u32x2*>(dst + half + c * 8) =
+          u32x2{fp8x4(fb[0], fb[1], fb[2], fb[3]), fp8x4(fb[4], fb[5], fb[6], fb[7])};
+    } else {
+      T* dst = reinterpret_cast<T*>(kc_) + e;
+      *reinterpret_cast<u32x4*>(dst + c * 8) = oa.u;
+      *reinterpret_cast<u32x4*>(dst + half + c * 8) = ob.u;
+    }
+  } else if (lane >= 16 && lane < 16 + D / 8) {
+    const int c = lane - 16;
+    float xv[8];
+    qkv_row8<T>(rp, row + (int64_t)(nq + nkv + h) * D + c * 8, xv);
+    const int64_t e = ((blk * nkv + h) << bs_log2) * D + ((int64_t)(off >> 3) * D + c * 8) * 8 +
+                      (off & 7);
+    if constexpr (KV8) {
+      uint8_t* dst = reinterpret_cast<uint8_t*>(vc_) + e;
+      const uint32_t w0 = fp8x4(xv[0] * rp.v_inv, xv[1] * rp.v_inv, xv[2] * rp.v_inv, xv[3] * rp.v_inv);
+      const uint32_t w1 = fp8x4(xv[4] * rp.v_inv, xv[5] * rp.v_inv, xv[6] * rp.v_inv, xv[7] * rp.v_inv);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        dst[j * 8] = (uint8_t)(w0 >> (8 * j));
+        dst[(j + 4) * 8] = (uint8_t)(w1 >> (8 * j));
+      }
+    } else {
+      T* dst = reinterpret_cast<T*>(vc_) + e;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dst[j * 8] = from_f<T>(xv[j]);
+    }
+  }
+}
+
 // PREF: true = issue all K and V loads of a wave-iteration before its first MFMA;
 // false = load each fragment right before its MFMA.  NCH = 32-token chunks per
 // wave-iteration, OCC = waves per SIMD.  Shipped: PREF, NCH = 1, OCC = 4 (<= 128 VGPR).
@@ -48,13 +188,16 @@ __device__ __forceinline__ u32x4 ld16(const void* p) {
 // +3 %, neither kept.
 // KV8: fp8 e4m3 cache (8-byte fragment loads widened in registers); the K scale is
 // folded into scale_log2 by the launcher, the V scale (v_scale) into the output.
-template <typename T, int D, bool PREF, bool KV8, int OCC = 3, int NCH = DEC_CHUNKS>
+// FUSE: q comes from the QKV projection row through the rope prologue (rp) and the
+// workgroup holding the last context token writes that token's k / v first.
+template <typename T, int D, bool PREF, bool KV8, int OCC = 3, int NCH = DEC_CHUNKS,
+          bool FUSE = false>
 __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
     T* __restrict__ out, const T* __restrict__ q, const void* __restrict__ kc_,
     const void* __restrict__ vc_, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ ctx_lens, float* __restrict__ max_logits,
     float* __restrict__ exp_sums, float* __restrict__ tmp_out, int nq, int nkv, int bs_log2,
-    int Zmax, float scale_log2, float v_scale, int num_blocks) {
+    int Zmax, float scale_log2, float v_scale, int num_blocks, DecodeRope rp) {
   typedef typename Vec8<T>::type V8;
   typedef std::conditional_t<KV8, uint8_t, T> C;   // cache element
   const C* __restrict__ kc = reinterpret_cast<const C*>(kc_);
@@ -69,6 +212,7 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
   // bank groups, 4 lanes each (the b128 minimum), instead of 16 heads on one group
   __shared__ __attribute__((aligned(16))) float lds_o[4][16][D + 4];
   __shared__ float lds_m[4][16], lds_l[4][16];
+  __shared__ __attribute__((aligned(16))) T lds_q[FUSE ? 16 : 1][FUSE ? D : 8];
   const int b = blockIdx.x, h = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r16 = lane & 15, qd = lane >> 4;
@@ -84,18 +228,6 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
   const C* vbase = vc + h * head_stride;
   const int64_t blk_stride = (int64_t)nkv * head_stride;
 
-  V8 qf[KS];
-  {
-    const bool valid = r16 < G;
-    const T* qrow = q + ((int64_t)b * nq + h * G + (valid ? r16 : 0)) * D;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      Pack8<T> t;
-      t.u = *reinterpret_cast<const u32x4*>(qrow + 32 * s + 8 * qd);
-      if (!valid) t.u = u32x4{0, 0, 0, 0};
-      qf[s] = t.v;
-    }
-  }
   const int keyA = 8 * (r16 >> 2) + (r16 & 3);
   float m_run = -INFINITY, l_run = 0.f;
   f32x4 o[DT];
@@ -113,37 +245,102 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
   const int c0 = (int)(((int64_t)nchunk * wk) / nwk);
   const int c1 = (int)(((int64_t)nchunk * (wk + 1)) / nwk);
   const int end = min(ctx, c1 << 5);       // this wave's token range is [c0*32, end)
-  for (int ci = c0; ci < c1; ci += NCH) {
+  Pack8<T> kf[NCH][2][KS];
+  Pack8<T> vf[NCH][DT];
+  static_assert(PREF, "the per-fragment-load form (measured 3-8 % slower) was removed");
+  // K / V fragments of the wave-iteration starting at chunk ci (PREF: all up front)
+  auto load_k = [&](int ci) {
     const int base = ci << 5;
-    const C* kaddr[NCH][2];
-    const C* vaddr[NCH];
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int ta = min(base + c * 32 + keyA, end - 1);
       const int tb = min(base + c * 32 + keyA + 4, end - 1);
-      kaddr[c][0] = kbase + kgc_bt(bt, ta >> bs_log2, bt_stride, num_blocks) * blk_stride + (int64_t)(ta & bsm) * D + 8 * qd;
-      kaddr[c][1] = kbase + kgc_bt(bt, tb >> bs_log2, bt_stride, num_blocks) * blk_stride + (int64_t)(tb & bsm) * D + 8 * qd;
+      const C* ka = kbase + kgc_bt(bt, ta >> bs_log2, bt_stride, num_blocks) * blk_stride + (int64_t)(ta & bsm) * D + 8 * qd;
+      const C* kb = kbase + kgc_bt(bt, tb >> bs_log2, bt_stride, num_blocks) * blk_stride + (int64_t)(tb & bsm) * D + 8 * qd;
+#pragma unroll
+      for (int s2 = 0; s2 < KS; ++s2) {
+        kf[c][0][s2].u = ldf(ka + 32 * s2);
+        kf[c][1][s2].u = ldf(kb + 32 * s2);
+      }
+    }
+  };
+  auto load_v = [&](int ci) {
+    const int base = ci << 5;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
       // V^T 8-key group of keys t0..t0+7: [(t0 & bsm) / 8][d][8]; 16 lanes = 256 B
       const int t0 = min(base + c * 32 + 8 * qd, end - 1) & ~7;
-      vaddr[c] = vbase + kgc_bt(bt, t0 >> bs_log2, bt_stride, num_blocks) * blk_stride + ((t0 & bsm) >> 3) * (D * 8) + r16 * 8;
+      const C* va = vbase + kgc_bt(bt, t0 >> bs_log2, bt_stride, num_blocks) * blk_stride + ((t0 & bsm) >> 3) * (D * 8) + r16 * 8;
+#pragma unroll
+      for (int t = 0; t < DT; ++t) vf[c][t].u = ldf(va + 16 * t * 8);
     }
-    Pack8<T> kf[NCH][2][KS];
-    Pack8<T> vf[PREF ? NCH : 1][DT];
-    if constexpr (PREF) {
+  };
+  // FUSE: the first iteration's K loads go out before the q prologue (whose slice
+  // reads and barrier they then overlap), unless that iteration holds the new token
+  // this workgroup is about to write.  (K and V both in flight spilled at 128 VGPRs.)
+  const bool prefetched = FUSE && c0 < c1 && c0 != nchunk - 1;
+  if (prefetched) load_k(c0);
+  V8 qf[KS];
+  if constexpr (FUSE) {
+    // q of the GQA group staged through LDS: thread i < G * D/16 owns the NeoX chunk
+    // pair (c, c + D/2) of head i / (D/16) (its head's D/16 threads are an aligned lane
+    // group for the q-norm sum); wave 3 of the z-slice holding the last context token
+    // writes that token's k / v meanwhile.  One barrier publishes both.
+    constexpr int TPH = D / 16;
+    const int tid = threadIdx.x;
+    if (tid < G * TPH) {
+      const int g = tid / TPH, c = tid % TPH;
+      const int64_t qe = (int64_t)b * rp.qkv_stride + (int64_t)(h * G + g) * D;
+      float xa[8], xb[8];
+      qkv_row8<T>(rp, qe + c * 8, xa);
+      qkv_row8<T>(rp, qe + D / 2 + c * 8, xb);
+      if (rp.q_norm_w) {
+        float ss = 0.f;
 #pragma unroll
-      for (int c = 0; c < NCH; ++c)
+        for (int j = 0; j < 8; ++j) ss += xa[j] * xa[j] + xb[j] * xb[j];
 #pragma unroll
-        for (int s2 = 0; s2 < KS; ++s2) {
-          kf[c][0][s2].u = ldf(kaddr[c][0] + 32 * s2);
-          kf[c][1][s2].u = ldf(kaddr[c][1] + 32 * s2);
-        }
+        for (int o = 1; o < TPH; o <<= 1) ss += __shfl_xor(ss, o, 64);
+        const float inv = rsqrtf(ss / (float)D + rp.eps);
+        norm8<T>(xa, inv, rp.q_norm_w, c * 8);
+        norm8<T>(xb, inv, rp.q_norm_w, D / 2 + c * 8);
+      }
+      if (rp.use_rope) rope8(xa, xb, rp.cos_sin + rp.positions[b] * D, c * 8, D / 2);
+      Pack8<T> oa, ob;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { oa.h[j] = from_f<T>(xa[j]); ob.h[j] = from_f<T>(xb[j]); }
+      *reinterpret_cast<u32x4*>(&lds_q[g][c * 8]) = oa.u;
+      *reinterpret_cast<u32x4*>(&lds_q[g][D / 2 + c * 8]) = ob.u;
     }
-    if constexpr (PREF) {
+    if (wave == 3 && blockIdx.z == gridDim.z - 1 && ctx > 0)
+      decode_kv_write<T, D, KV8>(rp, b, h, nq, nkv, bs_log2, num_blocks,
+                                 const_cast<void*>(kc_), const_cast<void*>(vc_), lane);
+    // release the k / v stores to the workgroup (same CU, same L1) and the LDS q
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const bool valid = r16 < G;
 #pragma unroll
-      for (int c = 0; c < NCH; ++c)
-#pragma unroll
-        for (int t = 0; t < DT; ++t) vf[PREF ? c : 0][t].u = ldf(vaddr[c] + 16 * t * 8);
+    for (int s = 0; s < KS; ++s) {
+      Pack8<T> t;
+      t.u = *reinterpret_cast<const u32x4*>(&lds_q[valid ? r16 : 0][32 * s + 8 * qd]);
+      if (!valid) t.u = u32x4{0, 0, 0, 0};
+      qf[s] = t.v;
     }
+  } else {
+    const bool valid = r16 < G;
+    const T* qrow = q + ((int64_t)b * nq + h * G + (valid ? r16 : 0)) * D;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      Pack8<T> t;
+      t.u = *reinterpret_cast<const u32x4*>(qrow + 32 * s + 8 * qd);
+      if (!valid) t.u = u32x4{0, 0, 0, 0};
+      qf[s] = t.v;
+    }
+  }
+  for (int ci = c0; ci < c1; ci += NCH) {
+    const int base = ci << 5;
+    if (!(prefetched && ci == c0)) load_k(ci);
+    load_v(ci);
     f32x4 sa[NCH], sb[NCH];
     // ---- S^T = K . Q^T
 #pragma unroll
@@ -151,10 +348,6 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
       f32x4 accA = {0.f, 0.f, 0.f, 0.f}, accB = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s2 = 0; s2 < KS; ++s2) {
-        if constexpr (!PREF) {
-          kf[c][0][s2].u = ldf(kaddr[c][0] + 32 * s2);
-          kf[c][1][s2].u = ldf(kaddr[c][1] + 32 * s2);
-        }
         accA = mfma16x16x32(kf[c][0][s2].v, qf[s2], accA);
         accB = mfma16x16x32(kf[c][1][s2].v, qf[s2], accB);
       }
@@ -193,10 +386,7 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
       }
 #pragma unroll
       for (int t = 0; t < DT; ++t) {
-        Pack8<T> v;
-        if constexpr (PREF) v = vf[PREF ? c : 0][t];
-        else v.u = ldf(vaddr[c] + 16 * t * 8);
-        o[t] = mfma16x16x32(v.v, pf.v, o[t]);
+        o[t] = mfma16x16x32(vf[c][t].v, pf.v, o[t]);
       }
     }
   }
@@ -291,32 +481,34 @@ __global__ __launch_bounds__(64) void paged_decode_reduce_kernel(
   for (int e = 0; e < EPT; ++e) orow[tid * EPT + e] = from_f<T>(acc[e] * inv);
 }
 
-template <typename T, int D, bool KV8>
+template <typename T, int D, bool KV8, bool FUSE>
 static void decode_dispatch(void* out, const void* q, const void* kc, const void* vc,
                             const int* bt, int bt_stride, const int* ctx, float* ml, float* es,
                             float* tmp, int B, int nq, int nkv, int bs_log2, int Zmax, int Z,
-                            float scale_log2, float v_scale, int num_blocks, hipStream_t s) {
-  auto kern = paged_decode_kernel<T, D, true, KV8, 4, 1>;
+                            float scale_log2, float v_scale, int num_blocks,
+                            const DecodeRope& rp, hipStream_t s) {
+  auto kern = paged_decode_kernel<T, D, true, KV8, 4, 1, FUSE>;
   kern<<<dim3(B, nkv, Z), 256, 0, s>>>(
       (T*)out, (const T*)q, kc, vc, bt, bt_stride, ctx, ml, es, tmp, nq,
-      nkv, bs_log2, Zmax, scale_log2, v_scale, num_blocks);
+      nkv, bs_log2, Zmax, scale_log2, v_scale, num_blocks, rp);
   if (Z > 1)
     paged_decode_reduce_kernel<T, D><<<dim3(B, nq), 64, 0, s>>>((T*)out, ml, es, tmp, ctx, nq,
                                                                 Z, Zmax);
 }
 
-void launch_paged_decode(int dtype, void* out, const void* q, const void* k_cache,
-                         const void* v_cache, const int* block_tables, int bt_stride,
-                         const int* ctx_lens, float* max_logits, float* exp_sums,
-                         float* tmp_out, int B, int nq, int nkv, int D, int bs_log2,
-                         int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
-                         float v_scale, int num_blocks, hipStream_t s) {
+template <bool FUSE>
+static void decode_launch(int dtype, void* out, const void* q, const void* k_cache,
+                          const void* v_cache, const int* block_tables, int bt_stride,
+                          const int* ctx_lens, float* max_logits, float* exp_sums,
+                          float* tmp_out, int B, int nq, int nkv, int D, int bs_log2,
+                          int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
+                          float v_scale, int num_blocks, const DecodeRope& rp, hipStream_t s) {
   if (B == 0) return;
   const float sl2 = scale * k_scale * 1.4426950408889634f;
-#define KGC_DEC(TT, DD, K8)                                                               \
-  decode_dispatch<TT, DD, K8>(out, q, k_cache, v_cache, block_tables, bt_stride, ctx_lens, \
-                              max_logits, exp_sums, tmp_out, B, nq, nkv, bs_log2, Zmax, Z, \
-                              sl2, v_scale, num_blocks, s)
+#define KGC_DEC(TT, DD, K8)                                                                 \
+  decode_dispatch<TT, DD, K8, FUSE>(out, q, k_cache, v_cache, block_tables, bt_stride,       \
+                                    ctx_lens, max_logits, exp_sums, tmp_out, B, nq, nkv,     \
+                                    bs_log2, Zmax, Z, sl2, v_scale, num_blocks, rp, s)
 #define KGC_DEC_D(TT, K8) \
   if (D == 128) KGC_DEC(TT, 128, K8); else KGC_DEC(TT, 64, K8)
   if (dtype == DT_BF16) {
@@ -326,6 +518,29 @@ void launch_paged_decode(int dtype, void* out, const void* q, const void* k_cach
   }
 #undef KGC_DEC_D
 #undef KGC_DEC
+}
+
+void launch_paged_decode(int dtype, void* out, const void* q, const void* k_cache,
+                         const void* v_cache, const int* block_tables, int bt_stride,
+                         const int* ctx_lens, float* max_logits, float* exp_sums,
+                         float* tmp_out, int B, int nq, int nkv, int D, int bs_log2,
+                         int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
+                         float v_scale, int num_blocks, hipStream_t s) {
+  const DecodeRope none{};
+  decode_launch<false>(dtype, out, q, k_cache, v_cache, block_tables, bt_stride, ctx_lens,
+                       max_logits, exp_sums, tmp_out, B, nq, nkv, D, bs_log2, Zmax, Z, scale,
+                       kv_fp8, k_scale, v_scale, num_blocks, none, s);
+}
+
+void launch_paged_decode_rope(int dtype, const DecodeRope& rp, void* out, void* k_cache,
+                              void* v_cache, const int* block_tables, int bt_stride,
+                              const int* ctx_lens, float* max_logits, float* exp_sums,
+                              float* tmp_out, int B, int nq, int nkv, int D, int bs_log2,
+                              int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
+                              float v_scale, int num_blocks, hipStream_t s) {
+  decode_launch<true>(dtype, out, nullptr, k_cache, v_cache, block_tables, bt_stride, ctx_lens,
+                      max_logits, exp_sums, tmp_out, B, nq, nkv, D, bs_log2, Zmax, Z, scale,
+                      kv_fp8, k_scale, v_scale, num_blocks, rp, s);
 }
 
 int paged_decode_partition_size() { return DEC_PART; }

@@ -36,6 +36,7 @@
 // deploys, /root/reference/values-01-minimal-example2.yaml:6-7).
 #include "common.h"
 #include "launch.h"
+#include <cstdlib>
 
 namespace kgc {
 
@@ -90,12 +91,30 @@ __device__ __forceinline__ int64_t weight_row(int nb, int r, int N) {
   }
 }
 
+// Split-K partials are stored write-through (sc1, a relaxed agent-scope atomic store):
+// no dirty L2 lines are left for the kernel boundary to write back (the boundary costs
+// + B / 6 TB/s behind B dirty bytes: ~5.6 us behind the 33.5 MB of down_proj slices at
+// M = 256, S = 8), the bytes leave during the GEMM instead.  wt = 0: plain stores
+// (KGC_PARTIAL_WT=0, for A/B).
+__device__ __forceinline__ void store_partial(float* p, float v, int wt) {
+  if (wt) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
+static int partial_wt() {
+  static const int v = [] {
+    const char* e = getenv("KGC_PARTIAL_WT");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 // LDW = 4: four extra loader waves issue every DMA and the 8 MFMA waves never stall on
 // DMA issue (one s_barrier per step for all 12 waves); LDW = 0: the MFMA waves issue too.
 template <typename T, int BM, int BN, int EPI, bool PK, int ABL = ABL_NONE, int LDW = 0>
 __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
     void* __restrict__ Cv, const T* __restrict__ X, const T* __restrict__ W, int M, int N,
-    int K, int64_t ldx, int S, int MB, int64_t slice_stride, int xmap) {
+    int K, int64_t ldx, int S, int MB, int64_t slice_stride, int xmap, int wt) {
   constexpr int MT = BM / 4 / 16;                 // 16-row MFMA tiles per wave
   constexpr int NT = BN / 2 / 16;                 // 16-col MFMA tiles per wave
   constexpr int NIW = LDW > 0 ? LDW : 8;          // waves issuing DMAs
@@ -245,7 +264,7 @@ __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
         float* cp = reinterpret_cast<float*>(Cv) + z * slice_stride + (int64_t)row * N +
                     nb * BN + wn * (BN / 2) + fr;
 #pragma unroll
-        for (int n = 0; n < NT; ++n) cp[n * 16] = acc[i][n][e];
+        for (int n = 0; n < NT; ++n) store_partial(cp + n * 16, acc[i][n][e], wt);
       } else if constexpr (EPI == EPI_OUT) {
         T* cp = reinterpret_cast<T*>(Cv) + (int64_t)row * N + nb * BN + wn * (BN / 2) + fr;
 #pragma unroll
@@ -273,7 +292,7 @@ __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
 template <typename T, int BM, int BN, int EPI, int NB, int NA = 3>
 __global__ __launch_bounds__(896, 1) void dgemm_sl_kernel(
     void* __restrict__ Cv, const T* __restrict__ X, const T* __restrict__ W, int M, int N,
-    int K, int64_t ldx, int S, int MB, int64_t slice_stride) {
+    int K, int64_t ldx, int S, int MB, int64_t slice_stride, int wt) {
   constexpr int MT = BM / 4 / 16, NT = BN / 2 / 16;
   static_assert(NA >= 2 && NB >= 2, "rings of at least two slots");
   constexpr int LA = BM / 8 / 4, LB = BN / 8 / 2;   // DMAs per A / B loader wave per step
@@ -392,7 +411,7 @@ __global__ __launch_bounds__(896, 1) void dgemm_sl_kernel(
         float* cp = reinterpret_cast<float*>(Cv) + z * slice_stride + (int64_t)row * N +
                     nb * BN + wn * (BN / 2) + fr;
 #pragma unroll
-        for (int n = 0; n < NT; ++n) cp[n * 16] = acc[i][n][e];
+        for (int n = 0; n < NT; ++n) store_partial(cp + n * 16, acc[i][n][e], wt);
       } else if constexpr (EPI == EPI_OUT) {
         T* cp = reinterpret_cast<T*>(Cv) + (int64_t)row * N + nb * BN + wn * (BN / 2) + fr;
 #pragma unroll
@@ -415,7 +434,8 @@ void dgemm_sl_cfg(int epi, void* C, const void* X, const void* W, int M, int N, 
   const dim3 grid((unsigned)(MB * (N / BN) * S));
 #define DG_SL(E)                                                                       \
   dgemm_sl_kernel<T, BM, BN, E, NB, NA><<<grid, 896, 0, s>>>(C, (const T*)X, (const T*)W, M, \
-                                                              N, K, ldx, S, MB, ss)
+                                                              N, K, ldx, S, MB, ss, \
+                                                              partial_wt())
   if (epi == EPI_PARTIAL) DG_SL(EPI_PARTIAL);
   else if (epi == EPI_OUT) DG_SL(EPI_OUT);
   else DG_SL(EPI_SILU);
@@ -464,7 +484,7 @@ void dgemm_cfg(int epi, void* C, const void* X, const void* W, int M, int N, int
   const int xm = (xmap && MB > 1 && 8 % S == 0 && (N / BN) % (8 / S) == 0) ? 1 : 0;
 #define DG_LAUNCH(E)                                                             \
   dgemm_kernel<T, BM, BN, E, PK, ABL_NONE, LDW><<<grid, DG_THREADS + LDW * 64, 0, s>>>( \
-      C, (const T*)X, (const T*)W, M, N, K, ldx, S, MB, ss, xm)
+      C, (const T*)X, (const T*)W, M, N, K, ldx, S, MB, ss, xm, partial_wt())
   if (epi == EPI_PARTIAL) DG_LAUNCH(EPI_PARTIAL);
   else if (epi == EPI_OUT) DG_LAUNCH(EPI_OUT);
   else DG_LAUNCH(EPI_SILU);
@@ -528,7 +548,7 @@ void launch_dgemm_ablate(int mode, float* C, const void* X, const void* W, int M
   const dim3 grid((unsigned)(MB * (N / 128) * S));
 #define AB(MODE)                                                                     \
   dgemm_kernel<bf16, 256, 128, EPI_PARTIAL, true, MODE><<<grid, DG_THREADS, 0, s>>>( \
-      C, (const bf16*)X, (const bf16*)W, M, N, K, ldx, S, MB, ss, 0)
+      C, (const bf16*)X, (const bf16*)W, M, N, K, ldx, S, MB, ss, 0, partial_wt())
   switch (mode) {
     case ABL_NO_MFMA: AB(ABL_NO_MFMA); break;
     case ABL_NO_DMA: AB(ABL_NO_DMA); break;

@@ -27,6 +27,30 @@ void launch_paged_decode(int dtype, void* out, const void* q, const void* k_cach
                          int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
                          float v_scale, int num_blocks, hipStream_t s);
 int paged_decode_partition_size();
+// K1 + K3/K5/K6 fused for decode-only steps: the decode kernel takes the QKV projection
+// row itself (T [B, qkv_stride], or S > 0 fp32 split-K slices [S, B, qkv_stride]),
+// builds q (optional per-head RMSNorm, NeoX RoPE) in the MFMA operand registers, and
+// the workgroup that owns a sequence's last token writes its rotated k and its v into
+// the paged cache before reading it back -- no rope_kv launch, no q round trip.
+struct DecodeRope {
+  const void* qkv;
+  int64_t qkv_stride;        // elements between token rows (of one slice when S > 0)
+  int64_t slice_stride;      // elements between slices
+  int S;                     // 0: qkv holds T values
+  int use_rope;
+  const int64_t* positions;  // [B]
+  const float* cos_sin;      // [max_pos, d]: cos(half) | sin(half)
+  const int64_t* slots;      // [B]; < 0: no cache write
+  const void* q_norm_w;      // nullptr: no q/k RMSNorm
+  const void* k_norm_w;
+  float eps, k_inv, v_inv;
+};
+void launch_paged_decode_rope(int dtype, const DecodeRope& rp, void* out, void* k_cache,
+                              void* v_cache, const int* block_tables, int bt_stride,
+                              const int* ctx_lens, float* max_logits, float* exp_sums,
+                              float* tmp_out, int B, int nq, int nkv, int D, int bs_log2,
+                              int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
+                              float v_scale, int num_blocks, hipStream_t s);
 void launch_prefill_attention(int dtype, const void* q, void* out, const void* k_cache,
                               const void* v_cache, const int* block_tables, int bt_stride,
                               const int* query_start_loc, const int* seq_lens,

@@ -39,6 +39,8 @@ def pp_layer_range(num_layers: int, pp_size: int, pp_rank: int) -> tuple[int, in
 _tail_fusion_enabled = os.environ.get("KGC_TAIL_FUSION", "1") != "0"
 # TP > 1: all-reduce fused with the residual add + RMSNorm after o / down (KGC_TP_AR_NORM=0: off)
 _tp_ar_norm_enabled = os.environ.get("KGC_TP_AR_NORM", "1") != "0"
+# decode-only steps: RoPE + KV write folded into the paged-decode kernel (KGC_DECODE_ROPE_FUSED=0: off)
+_decode_rope_fused = os.environ.get("KGC_DECODE_ROPE_FUSED", "1") != "0"
 
 
 class RMSNorm(nn.Module):
@@ -84,6 +86,18 @@ class LlamaAttention(nn.Module):
     def attend(self, positions, qkv, ctx: ForwardContext):
         """RoPE + KV-cache write + paged attention on a QKV projection -> [T, nq*d]."""
         kc, vc = ctx.kv_caches[self.attn.layer_idx]
+        m = ctx.attn
+        if (_decode_rope_fused and qkv.is_cuda and not m.num_prefill_tokens and m.num_decodes
+                and m.num_decodes == (qkv.shape[1] if qkv.dim() == 3 else qkv.shape[0])):
+            # decode-only step: RoPE / q-k norm / KV write run inside the decode kernel
+            o = ops.paged_attention_decode_rope(
+                qkv, positions, ctx.cos_sin, kc, vc, m.slot_mapping, self.nq, self.nkv,
+                self.cfg.head_dim, m.decode_block_tables, m.decode_ctx_lens, self.attn.scale,
+                None if self.q_norm is None else self.q_norm.weight,
+                None if self.k_norm is None else self.k_norm.weight, self.cfg.rms_eps,
+                workspace=m.decode_workspace, grid_z=m.decode_grid_z, k_scale=ctx.k_scale,
+                v_scale=ctx.v_scale, dtype=self.qkv_proj.weight.dtype)
+            return o.view(o.shape[0], self.nq * self.cfg.head_dim)
         q = ops.rope_kv_write(qkv, positions, ctx.cos_sin, kc, vc, ctx.attn.slot_mapping,
                               self.nq, self.nkv, self.cfg.head_dim,
                               None if self.q_norm is None else self.q_norm.weight,

@@ -200,6 +200,41 @@ def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torc
     return out
 
 
+def paged_attention_decode_rope(qkv: torch.Tensor, positions: torch.Tensor,
+                                cos_sin: torch.Tensor, k_cache: torch.Tensor,
+                                v_cache: torch.Tensor, slot_mapping: torch.Tensor,
+                                num_heads: int, num_kv_heads: int, head_dim: int,
+                                block_tables: torch.Tensor, context_lens: torch.Tensor,
+                                scale: float, q_norm_w: Optional[torch.Tensor] = None,
+                                k_norm_w: Optional[torch.Tensor] = None, eps: float = 1e-6,
+                                use_rope: bool = True, workspace=None, grid_z: int = 1,
+                                k_scale: float = 1.0, v_scale: float = 1.0,
+                                dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    """``rope_kv_write`` + ``paged_attention_decode`` of a decode-only batch in ONE
+    launch (K1 with K3/K5/K6 as its prologue): q is built in registers from the QKV
+    projection (or its K9m fp32 split-K slices [S, B, N]), the new token's k / v are
+    written to the cache by the workgroup that reads them back.  -> [B, nq, d]."""
+    if not _gpu(qkv):
+        q = ref.rope_qk_kv_write(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping,
+                                 num_heads, num_kv_heads, head_dim, q_norm_w, k_norm_w, eps,
+                                 use_rope, k_scale, v_scale)
+        return ref.paged_attention_decode(q, k_cache, v_cache, block_tables, context_lens, scale,
+                                          k_scale, v_scale)
+    sl = qkv.dim() == 3
+    B = qkv.shape[1] if sl else qkv.shape[0]
+    out = torch.empty(B, num_heads, head_dim, dtype=(dtype or qkv.dtype) if sl else qkv.dtype,
+                      device=qkv.device)
+    if workspace is None:
+        workspace = decode_partials(B, num_heads, head_dim, block_tables.shape[1],
+                                    k_cache.shape[2], qkv.device)
+    ml, es, tmp = workspace
+    grid_z = min(grid_z, ml.shape[-1])
+    _k().paged_decode_rope(out, qkv, positions, cos_sin, k_cache, v_cache, slot_mapping,
+                           q_norm_w, k_norm_w, block_tables, context_lens, ml, es, tmp,
+                           num_heads, grid_z, scale, eps, use_rope, k_scale, v_scale)
+    return out
+
+
 def prefill_work_list(query_lens: list[int], seq_lens: list[int]) -> tuple[list[int], list[int]]:
     """(seq, 128-row block) work items, heaviest (most keys) first."""
     items = []
@@ -277,7 +312,7 @@ def sample_vp_finish(packed: torch.Tensor, out: Optional[torch.Tensor] = None) -
 
 
 __all__ = ["load_extension", "rms_norm", "fused_add_rms_norm", "layer_norm", "silu_mul",
-           "rope_kv_write", "paged_attention_decode", "prefill_attention", "sample", "sample_vp_partial", "sample_vp_finish",
+           "rope_kv_write", "paged_attention_decode", "paged_attention_decode_rope", "prefill_attention", "sample", "sample_vp_partial", "sample_vp_finish",
            "decode_partials", "decode_grid_z", "prefill_work_list", "ref"]
 
 

@@ -126,6 +126,29 @@ def test_graph_equals_eager_and_async_equals_sync(gpu):
             assert a[:4] == b[:4], (k, a, b)
 
 
+def test_decode_rope_fused_equals_unfused(gpu, monkeypatch):
+    """Decode steps with RoPE + KV write inside the paged-decode kernel give the same
+    greedy tokens as rope_kv_write + paged_decode, eager and replayed from hipGraphs."""
+    from kubernetes_gpu_cluster_amd.models import llama
+    g = torch.Generator().manual_seed(5)
+    prompts = [torch.randint(100, 128000, (n,), generator=g).tolist() for n in (9, 150, 33)]
+    params = [SamplingParams(temperature=0.0, max_tokens=16, ignore_eos=True)
+              for _ in prompts]
+    outs = {}
+    for fused in (False, True):
+        monkeypatch.setattr(llama, "_decode_rope_fused", fused)
+        for eager in (True, False):
+            eng = _tiny_engine(enforce_eager=eager)
+            outs[(fused, eager)] = _run(eng, prompts, params)
+            del eng
+            torch.cuda.empty_cache()
+    base = outs[(False, True)]
+    for k, v in outs.items():
+        for a, b in zip(v, base):
+            assert len(a) == 16
+            assert a[:4] == b[:4], (k, a, b)
+
+
 def test_engine_preemption_recompute(gpu):
     """A KV pool too small for the batch forces recompute preemption; every request
     still completes with the requested length."""

@@ -10,7 +10,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "kubernetes_gpu_cluster_amd")
 
-OPS = ["rms_norm", "rope_kv_write", "paged_decode", "prefill_attention", "sample", "sample_vp",
+OPS = ["rms_norm", "rope_kv_write", "paged_decode", "paged_decode_rope", "prefill_attention", "sample", "sample_vp",
        "sample_vp_unpack", "dgemm", "dgemm_pack", "xgmi_allreduce", "xgmi_allreduce_rms",
        "moe_route", "debug_errors", "debug_build"]
 

@@ -47,6 +47,19 @@ try:
 except ops.KernelDebugCheckFailed as e:
     assert "K3" in str(e), e
 ops.debug_check()                                   # cleared after the raise
+# K1 with K3 folded in (decode-only steps): the new token's slot is range-checked too
+qkv2 = torch.randn(2, (nq + 2 * nkv) * d, dtype=torch.bfloat16, device=dev)
+pos2 = (cl - 1).long()
+ok_slots = torch.tensor([2 * bs + 3, 3 * bs + 4], dtype=torch.int64, device=dev)
+ops.paged_attention_decode_rope(qkv2, pos2, cs, kc, vc, ok_slots, nq, nkv, d, good, cl, d ** -0.5)
+ops.debug_check()
+bad_slots = torch.tensor([2 * bs + 3, nb * bs + 1], dtype=torch.int64, device=dev)
+ops.paged_attention_decode_rope(qkv2, pos2, cs, kc, vc, bad_slots, nq, nkv, d, good, cl, d ** -0.5)
+try:
+    ops.debug_check()
+    raise SystemExit("decode+rope: bad slot not reported")
+except ops.KernelDebugCheckFailed as e:
+    assert "K1" in str(e), e
 print("DEBUG-BUILD-OK")
 '''
 

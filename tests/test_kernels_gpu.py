@@ -143,6 +143,69 @@ def test_paged_decode(gpu, dt, d, nq, nkv, bs):
         torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(dt))
 
 
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("d,nq,nkv", [(128, 32, 8), (64, 8, 2), (128, 16, 16)])
+@pytest.mark.parametrize("qk_norm", [False, True])
+@pytest.mark.parametrize("S", [0, 3])
+@pytest.mark.parametrize("fp8", [False, True])
+def test_paged_decode_rope(gpu, dt, d, nq, nkv, qk_norm, S, fp8):
+    """The decode kernel with rope_kv_write folded in == rope_kv_write + paged_decode on
+    the same inputs (q / k / v and the cache update), and == the fp32 reference.  One row
+    is graph padding (ctx 0, slot -1): nothing of it reaches the cache."""
+    torch.manual_seed(17 + d + S)
+    bs = 16
+    ctx = [1, 17, 300, 1000, 0, 64, 129]
+    B = len(ctx)
+    kc, vc, bt = _fill_random_cache(B, [max(c, 1) for c in ctx], nkv, bs, d, dt, gpu)
+    ks = vs = 1.0
+    if fp8:
+        ks, vs = 0.05, 0.07
+        kc = (kc.float() / ks).to(torch.float8_e4m3fn)
+        vc = (vc.float() / vs).to(torch.float8_e4m3fn)
+    N = (nq + 2 * nkv) * d
+    if S:
+        qkv = torch.randn(S, B, N, dtype=torch.float32, device=gpu)
+        summed = qkv[0].clone()           # summed in the kernel's order (z = 0, 1, ...)
+        for z in range(1, S):
+            summed += qkv[z]
+        summed = summed.to(dt)
+    else:
+        qkv = torch.randn(B, N, dtype=dt, device=gpu)
+        summed = qkv
+    pos = torch.tensor([max(c - 1, 0) for c in ctx], device=gpu)
+    slots = torch.tensor([int(bt[b, (c - 1) // bs]) * bs + (c - 1) % bs if c else -1
+                          for b, c in enumerate(ctx)], device=gpu)
+    cs = ref.rope_cos_sin_cache(d, 4096, 5e5).to(gpu)
+    qn = torch.randn(d, dtype=dt, device=gpu) if qk_norm else None
+    kn = torch.randn(d, dtype=dt, device=gpu) if qk_norm else None
+    cl = torch.tensor(ctx, dtype=torch.int32, device=gpu)
+    scale = d ** -0.5
+    tol = _tol(dt) if not fp8 else dict(atol=6e-2, rtol=6e-2)
+    kc0, vc0 = kc.clone(), vc.clone()
+    for z in (1, 3):
+        kc1, vc1 = kc0.clone(), vc0.clone()
+        out = ops.paged_attention_decode_rope(qkv, pos, cs, kc1, vc1, slots, nq, nkv, d, bt, cl,
+                                              scale, qn, kn, 1e-6, grid_z=z, k_scale=ks,
+                                              v_scale=vs, dtype=dt)
+        kc2, vc2 = kc0.clone(), vc0.clone()
+        q2 = ops.rope_kv_write(summed, pos, cs, kc2, vc2, slots, nq, nkv, d, qn, kn, 1e-6,
+                               k_scale=ks, v_scale=vs)
+        out2 = ops.paged_attention_decode(q2, kc2, vc2, bt, cl, scale, grid_z=z, k_scale=ks,
+                                          v_scale=vs)
+        # v is moved, not computed: bit for bit.  k / q may differ in the last bit (the
+        # q/k-norm sum order, FMA contraction of the rotation).
+        torch.testing.assert_close(vc1.view(torch.uint8), vc2.view(torch.uint8), atol=0, rtol=0)
+        torch.testing.assert_close(kc1.float(), kc2.float(), **tol)
+        torch.testing.assert_close(out.float(), out2.float(), **tol)
+        # fp32 reference of the whole fused op (CPU)
+        kc3, vc3 = kc0.cpu().clone(), vc0.cpu().clone()
+        qr = ref.rope_qk_kv_write(summed.cpu(), pos.cpu(), cs.cpu(), kc3, vc3, slots.cpu(), nq,
+                                  nkv, d, None if qn is None else qn.cpu(),
+                                  None if kn is None else kn.cpu(), 1e-6, True, ks, vs)
+        exp = ref.paged_attention_decode(qr, kc3, vc3, bt.cpu(), cl.cpu(), scale, ks, vs)
+        torch.testing.assert_close(out.cpu().float(), exp.float(), **tol)
+
+
 def test_paged_decode_workspace_reuse(gpu):
     """One static partials workspace serves launches of any Z (incl. an empty context),
     eager or replayed from a graph."""

@@ -1,6 +1,6 @@
 """Decode / prefill attention microbenchmark on realistic serving shapes.
 
-    python tools/attn_bench.py [--batch 256] [--ctx 640] [--nq 32 --nkv 8]
+    python tools/attn_bench.py [--batch 256] [--ctx 640] [--nq 32 --nkv 8] [--rope S]
 
 Reports time per call and the KV bytes streamed per second (the decode kernel is
 HBM-bound: every cached K/V byte of every sequence is read once per step).
@@ -44,6 +44,9 @@ def main():
     ap.add_argument("--ragged", type=float, default=0.25,
                     help="context lengths uniform in [ctx*(1-r), ctx] (0: all equal, as in bench.py)")
     ap.add_argument("--z", type=int, default=0, help="force the z-split (0: engine heuristic)")
+    ap.add_argument("--rope", type=int, default=-1,
+                    help=">= 0: also time rope_kv_write + decode vs the fused decode kernel "
+                         "(0: bf16 QKV, S > 0: S fp32 split-K slices)")
     a = ap.parse_args()
     from kubernetes_gpu_cluster_amd import ops
     dev = torch.device("cuda")
@@ -71,6 +74,33 @@ def main():
     print(json.dumps({"kernel": "paged_decode", "batch": B, "ctx_mean": float(ctx.float().mean()),
                       "z": z, "max_err": round(err, 4), "us": round(t * 1e6, 2), "kv_TBps": round(kv_bytes / t / 1e12, 3),
                       "variant": os.environ.get("KGC_DEC_VARIANT", "0")}))
+    if a.rope >= 0:
+        # rope_kv_write + paged_decode vs the fused decode kernel, the QKV projection
+        # handed over as bf16 (--rope 0) or as S K9m split-K slices (--rope S)
+        N = (a.nq + 2 * a.nkv) * d
+        S = a.rope
+        qkv = (torch.randn(S, B, N, device=dev) if S else
+               torch.randn(B, N, device=dev, dtype=torch.bfloat16))
+        pos = (ctx - 1).long()
+        slots = (bt.gather(1, ((ctx - 1) // bs).long().unsqueeze(1)).squeeze(1).long() * bs
+                 + ((ctx - 1) % bs).long())
+        cs = R.rope_cos_sin_cache(d, a.max_len, 5e5).to(dev)
+        nq, nkv = a.nq, a.nkv
+
+        def unfused():
+            qq = ops.rope_kv_write(qkv, pos, cs, kc, vc, slots, nq, nkv, d, dtype=torch.bfloat16)
+            return ops.paged_attention_decode(qq, kc, vc, bt, ctx, d ** -0.5, ws, z)
+
+        def fused():
+            return ops.paged_attention_decode_rope(qkv, pos, cs, kc, vc, slots, nq, nkv, d, bt,
+                                                   ctx, d ** -0.5, workspace=ws, grid_z=z,
+                                                   dtype=torch.bfloat16)
+        e = (unfused().float() - fused().float()).abs().max().item()
+        tu, tf = timeit(unfused), timeit(fused)
+        print(json.dumps({"kernel": "rope_kv + paged_decode vs paged_decode_rope", "batch": B,
+                          "ctx_mean": float(ctx.float().mean()), "z": z, "S": S,
+                          "unfused_us": round(tu * 1e6, 2), "fused_us": round(tf * 1e6, 2),
+                          "max_diff": round(e, 5)}))
 
 
 if __name__ == "__main__":
