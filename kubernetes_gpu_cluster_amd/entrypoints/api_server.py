@@ -43,6 +43,18 @@ class _Lenient(BaseModel):
     model_config = ConfigDict(extra="allow")
 
 
+class TokenizeRequest(_Lenient):
+    model: Optional[str] = None
+    prompt: Optional[str] = None
+    messages: Optional[list[dict]] = None
+    add_generation_prompt: bool = True
+
+
+class DetokenizeRequest(_Lenient):
+    model: Optional[str] = None
+    tokens: list[int]
+
+
 class CompletionRequest(_Lenient):
     model: Optional[str] = None
     prompt: Union[str, list[str], list[int], list[list[int]]]
@@ -408,6 +420,28 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
             return _err(503, f"engine unavailable: {e}", "server_error")
         except ValueError as e:
             return _err(400, str(e))
+
+    @app.post("/tokenize")
+    async def tokenize(req: TokenizeRequest):
+        """vLLM's /tokenize: a prompt, or chat messages rendered with the chat template."""
+        if req.messages is not None:
+            msgs = [{"role": m.get("role", "user"), "content": m.get("content") or ""}
+                    for m in req.messages]
+            text = tokenizer.apply_chat_template(msgs,
+                                                 add_generation_prompt=req.add_generation_prompt)
+        elif req.prompt is not None:
+            text = req.prompt
+        else:
+            return _err(400, "tokenize needs 'prompt' or 'messages'")
+        ids = tokenizer.encode(text)
+        return {"count": len(ids), "max_model_len": max_model_len, "tokens": ids}
+
+    @app.post("/detokenize")
+    async def detokenize(req: DetokenizeRequest):
+        vocab = getattr(tokenizer, "vocab_size", None)
+        if vocab and any(not 0 <= t < vocab for t in req.tokens):
+            return _err(400, f"token ids must be in [0, {vocab})")
+        return {"prompt": tokenizer.decode(list(req.tokens))}
 
     @app.get("/v1/models")
     async def models():

@@ -60,6 +60,10 @@ class HFTokenizer:
         self.chat_template = cfg.get("chat_template")
         self._hf = None
 
+    @property
+    def vocab_size(self) -> int:
+        return self.tok.get_vocab_size(with_added_tokens=True)
+
     def encode(self, text: str, add_special_tokens: bool = True) -> list[int]:
         return self.tok.encode(text, add_special_tokens=add_special_tokens).ids
 

@@ -201,3 +201,17 @@ def test_shared_core_serves_two_frontends(tmp_path):
     a.shutdown()
     core.join(30)
     assert not core.is_alive()
+
+
+def test_tokenize_detokenize(client):
+    """vLLM's /tokenize (prompt or chat messages) and /detokenize round trip."""
+    r = client.post("/tokenize", json={"prompt": "hello world"})
+    j = r.json()
+    assert r.status_code == 200, j
+    assert j["count"] == len(j["tokens"]) > 0 and j["max_model_len"] == 256
+    d = client.post("/detokenize", json={"tokens": j["tokens"]})
+    assert d.status_code == 200 and "hello world" in d.json()["prompt"]
+    c = client.post("/tokenize", json={"messages": [{"role": "user", "content": "hi"}]})
+    assert c.status_code == 200 and c.json()["count"] > 0
+    assert client.post("/tokenize", json={}).status_code == 400
+    assert client.post("/detokenize", json={"tokens": [10 ** 9]}).status_code == 400
