@@ -261,6 +261,8 @@ class Router:
         a.router.add_get("/health", self.health)
         a.router.add_get("/metrics", self.metrics)
         a.router.add_route("*", "/v1/{tail:.*}", self.proxy)
+        a.router.add_post("/tokenize", self.proxy)       # vLLM's (de)tokenizer endpoints
+        a.router.add_post("/detokenize", self.proxy)
         a.on_startup.append(self.start)
         a.on_cleanup.append(self.stop)
         return a

@@ -36,6 +36,11 @@ def fake_engine(name: str, model: str = "m", fail: bool = False):
     app.router.add_get("/health", health)
     app.router.add_get("/v1/models", models)
     app.router.add_post("/v1/completions", comp)
+
+    async def tokenize(r):
+        body = await r.json()
+        return web.json_response({"backend": name, "count": len(body.get("prompt", ""))})
+    app.router.add_post("/tokenize", tokenize)
     return app
 
 
@@ -64,6 +69,9 @@ async def _scenario():
             seen.add((await resp.json())["backend"])
         assert seen == {"a", "b"}
         assert r.m_retry._value.get() > 0
+        # /tokenize is routed by model like the /v1 endpoints
+        j = await (await client.post("/tokenize", json={"model": "m2", "prompt": "abc"})).json()
+        assert j["backend"] == "c" and j["count"] == 3
         # SSE relay
         resp = await client.post("/v1/completions", json={"model": "m1", "stream": True})
         text = await resp.text()
