@@ -337,6 +337,18 @@ def _time(fn, reps: int) -> float:
     return e0.elapsed_time(e1) / reps
 
 
+def _time_graphed(body, reps: int) -> float:
+    """``_time`` of ``body`` captured in one hipGraph: candidates that differ in launch
+    count are compared as a decode graph replays them (eager timing would add the host's
+    launch rate to the side with more launches, or hide the in-graph kernel boundaries)."""
+    body()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        body()
+    return _time(g.replay, reps)
+
+
 @torch.inference_mode()
 def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: float = 0.97,
                 reps: int = 3, norm_shapes=(), norm_max_m: int = 16, silu_shapes=(),
@@ -503,7 +515,9 @@ def _tune_dgemm(ws, N: int, K: int, ms, margin: float, reps: int, res: dict,
 
 def _tune_silu(ws, x, M: int, N: int, K: int, reps: int, margin: float) -> None:
     """Time the SK_SILU variants against the plain plan (skinny or hipBLASLt, as just
-    chosen) followed by silu_mul, over every layer's gate_up weight."""
+    chosen) followed by silu_mul, over every layer's gate_up weight, both in a graph
+    (eager timing called M = 1-4 a tie; in the decode graph the separate silu_mul launch
+    costs ~4.7 us per layer)."""
     from . import silu_mul
     if os.environ.get("KGC_SKINNY_SILU", "1") == "0":
         return
@@ -512,7 +526,7 @@ def _tune_silu(ws, x, M: int, N: int, K: int, reps: int, margin: float) -> None:
     def sep():
         for w in ws:
             silu_mul(linear(x, w), act)
-    sep_t = _time(sep, reps)
+    sep_t = _time_graphed(sep, reps)
     best_t, best_cfg = float("inf"), None
     for cfg in _CONFIGS:
         if cfg[1] != 2 or not skinny_ok(M, N, K, cfg) or (cfg[0] > 1 and M <= 16 * (cfg[0] // 2)):
@@ -521,7 +535,7 @@ def _tune_silu(ws, x, M: int, N: int, K: int, reps: int, margin: float) -> None:
         def fn(cfg=cfg):
             for w in ws:
                 skinny_silu(x, w, cfg, act)
-        t = _time(fn, reps)
+        t = _time_graphed(fn, reps)
         if t < best_t:
             best_t, best_cfg = t, cfg
     n = len(ws)
@@ -543,18 +557,10 @@ def _tune_accnorm(ws, x, M: int, N: int, K: int, reps: int, margin: float) -> No
     res = torch.zeros(M, N, dtype=x.dtype, device=x.device)
     out = torch.empty_like(res)
 
-    def graphed(body):
-        body()
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            body()
-        return _time(g.replay, reps)
-
     def sep():
         for w in ws:
             fused_add_rms_norm(linear(x, w), res, gamma, 1e-6)
-    sep_t = graphed(sep)
+    sep_t = _time_graphed(sep, reps)
     best_t, best_cfg = float("inf"), None
     for cfg in _CONFIGS:
         if not skinny_ok(M, N, K, cfg) or (cfg[0] > 1 and M <= 16 * (cfg[0] // 2)):
@@ -563,7 +569,7 @@ def _tune_accnorm(ws, x, M: int, N: int, K: int, reps: int, margin: float) -> No
         def fn(cfg=cfg):
             for w in ws:
                 skinny_acc_norm(res, x, w, gamma, 1e-6, cfg, out)
-        t = graphed(fn)
+        t = _time_graphed(fn, reps)
         if t < best_t:
             best_t, best_cfg = t, cfg
     n = len(ws)
