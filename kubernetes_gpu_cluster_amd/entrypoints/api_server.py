@@ -170,9 +170,24 @@ class _Detok:
         return out
 
 
-def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len: int) -> FastAPI:
+def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len: int,
+              api_key: Optional[str] = None) -> FastAPI:
     app = FastAPI(title="kgc OpenAI-compatible server", version=__version__)
     created = int(time.time())
+
+    if api_key:
+        # vLLM's --api-key: every /v1 route wants "Authorization: Bearer <key>"; /health,
+        # /metrics, /version and (de)tokenize stay open for probes and scrapers
+        import hmac
+        want = f"Bearer {api_key}".encode()
+
+        @app.middleware("http")
+        async def check_api_key(request, call_next):
+            if request.method != "OPTIONS" and request.url.path.startswith("/v1"):
+                got = request.headers.get("authorization", "").encode()
+                if not hmac.compare_digest(got, want):
+                    return JSONResponse({"error": "Unauthorized"}, status_code=401)
+            return await call_next(request)
 
     def params_from(req, max_tokens: Optional[int], logprobs: Optional[int] = None) -> SamplingParams:
         stops = req.stop if isinstance(req.stop, list) else ([req.stop] if req.stop else [])
@@ -479,6 +494,8 @@ def make_parser() -> argparse.ArgumentParser:
     p.add_argument("--host", default="0.0.0.0")
     p.add_argument("--port", type=int, default=8000)
     p.add_argument("--uvicorn-log-level", default="info")
+    p.add_argument("--api-key", default=os.environ.get("VLLM_API_KEY"),
+                   help="require 'Authorization: Bearer <key>' on /v1 routes (env VLLM_API_KEY)")
     p.add_argument("--engine-in-process", action="store_true",
                    help="run the engine loop on a thread of this process instead of a "
                         "separate engine-core process")
@@ -511,7 +528,7 @@ def _serve(ns, cfg: EngineConfig, connect=None, core_proc=None, sock=None) -> No
     tok = get_tokenizer(cfg.model, eng.engine.mcfg, cfg.tokenizer,
                         allow_synthetic=cfg.random_init)
     name = cfg.served_model_name or cfg.model
-    app = build_app(eng, tok, name, eng.engine.max_model_len)
+    app = build_app(eng, tok, name, eng.engine.max_model_len, ns.api_key)
     server = uvicorn.Server(uvicorn.Config(app, host=ns.host, port=ns.port,
                                            log_level=ns.uvicorn_log_level))
     dead = threading.Event()

@@ -55,7 +55,11 @@ class Router:
                  health_interval: float = 5.0, fail_threshold: int = 2,
                  k8s_selector: Optional[str] = None, k8s_namespace: Optional[str] = None,
                  k8s_port: int = 8000, dns_service: Optional[str] = None, max_retries: int = 2,
-                 request_timeout: float = 3600.0):
+                 request_timeout: float = 3600.0, backend_api_key: Optional[str] = None):
+        # engines started with --api-key: the router's own /v1/models polls carry the key
+        # (client requests are proxied with their own Authorization header)
+        self._poll_headers = ({"Authorization": f"Bearer {backend_api_key}"}
+                              if backend_api_key else {})
         self.backends: dict[str, Backend] = {u.rstrip("/"): Backend(u) for u in backends}
         self.policy = policy
         self.health_interval = health_interval
@@ -143,7 +147,7 @@ class Router:
             async with self.session.get(b.url + "/health", timeout=aiohttp.ClientTimeout(total=3)) as r:
                 ok = r.status == 200
             if ok and not b.models:
-                async with self.session.get(b.url + "/v1/models",
+                async with self.session.get(b.url + "/v1/models", headers=self._poll_headers,
                                             timeout=aiohttp.ClientTimeout(total=3)) as r:
                     if r.status == 200:
                         b.models = {m["id"] for m in (await r.json()).get("data", [])}
@@ -307,13 +311,17 @@ def main(argv=None):
                    choices=["least-outstanding", "round-robin", "session"])
     p.add_argument("--health-interval", type=float, default=5.0)
     p.add_argument("--access-log", action="store_true", help="log every proxied request")
+    p.add_argument("--backend-api-key", default=os.environ.get("VLLM_API_KEY"),
+                   help="bearer key for the router's own /v1/models polls of engines that "
+                        "run with --api-key (env VLLM_API_KEY)")
     a = p.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
     if not a.access_log:
         logging.getLogger("aiohttp.access").setLevel(logging.WARNING)
     r = Router([u for u in a.backends.split(",") if u], a.policy, a.health_interval,
                k8s_selector=a.k8s_label_selector, k8s_namespace=a.k8s_namespace,
-               k8s_port=a.k8s_port, dns_service=a.dns_service)
+               k8s_port=a.k8s_port, dns_service=a.dns_service,
+               backend_api_key=a.backend_api_key)
     web.run_app(r.app(), host=a.host, port=a.port)
 
 

@@ -215,3 +215,24 @@ def test_tokenize_detokenize(client):
     assert c.status_code == 200 and c.json()["count"] > 0
     assert client.post("/tokenize", json={}).status_code == 400
     assert client.post("/detokenize", json={"tokens": [10 ** 9]}).status_code == 400
+
+
+def test_api_key_guards_v1_routes():
+    """--api-key (vLLM semantics): /v1 routes need the bearer token, probes stay open."""
+    cfg = _cfg()
+    eng = AsyncLLMEngine(cfg)
+    try:
+        tok = get_tokenizer(cfg.model, eng.engine.mcfg)
+        app = build_app(eng, tok, "tiny-llama", eng.engine.max_model_len, api_key="s3cret")
+        with TestClient(app) as c:
+            assert c.get("/v1/models").status_code == 401
+            assert c.get("/v1/models", headers={"Authorization": "Bearer nope"}).status_code == 401
+            ok = c.get("/v1/models", headers={"Authorization": "Bearer s3cret"})
+            assert ok.status_code == 200 and ok.json()["data"][0]["id"] == "tiny-llama"
+            r = c.post("/v1/completions", json={"prompt": "hi", "max_tokens": 2},
+                       headers={"Authorization": "Bearer s3cret"})
+            assert r.status_code == 200
+            assert c.get("/health").status_code == 200
+            assert c.get("/metrics").status_code == 200
+    finally:
+        eng.shutdown()
