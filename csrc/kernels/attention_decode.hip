@@ -212,7 +212,9 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
   // bank groups, 4 lanes each (the b128 minimum), instead of 16 heads on one group
   __shared__ __attribute__((aligned(16))) float lds_o[4][16][D + 4];
   __shared__ float lds_m[4][16], lds_l[4][16];
-  __shared__ __attribute__((aligned(16))) T lds_q[FUSE ? 16 : 1][FUSE ? D : 8];
+  // q rows padded by 8 elements: unpadded, the 256-B rows put the 16 heads a b128 read
+  // gathers on the same 4 banks (393K bank-conflict cycles per dispatch at B = 256)
+  __shared__ __attribute__((aligned(16))) T lds_q[FUSE ? 16 : 1][FUSE ? D + 8 : 8];
   const int b = blockIdx.x, h = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r16 = lane & 15, qd = lane >> 4;
