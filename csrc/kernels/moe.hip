@@ -441,7 +441,10 @@ static void splitk_reduce_t(T* out, const float* Cs, int S, int64_t n8, int64_t 
 #define SKR(K) splitk_reduce_kernel<T, K><<<grid, 256, 0, s>>>(out, Cs, S, n8, ss)
   switch (S) {
     case 2: SKR(2); break;
+    case 3: SKR(3); break;
     case 4: SKR(4); break;
+    case 5: SKR(5); break;
+    case 6: SKR(6); break;
     case 8: SKR(8); break;
     default: SKR(0); break;
   }

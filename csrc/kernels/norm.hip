@@ -205,6 +205,8 @@ static void splitk_add_rms_dispatch(T* out, const float* Cs, T* residual, const 
     case 2: SKN(2); break;
     case 3: SKN(3); break;
     case 4: SKN(4); break;
+    case 5: SKN(5); break;
+    case 6: SKN(6); break;
     case 8: SKN(8); break;
     default: SKN(0); break;
   }

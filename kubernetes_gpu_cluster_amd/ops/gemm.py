@@ -419,6 +419,10 @@ def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: floa
 # K9m candidates per M range: (cfg ids, split factors).  Packed tiles only when the weight
 # was packed; 4 loader waves (6, 7), split loaders (8, 9) and XCD-paired 128-row blocks (10)
 # per tools/dgemm_bench.py.
+_DG_SPLITS = tuple(int(v) for v in
+                   os.environ.get("KGC_DGEMM_SPLITS", "1,2,3,4,5,6,8").split(","))
+
+
 def _dg_candidates(M: int, N: int, K: int, kind: str, packed: bool):
     from . import _k
     cfgs = [5, 7, 2] if M <= 128 else [6, 8, 4, 0, 10]
@@ -429,7 +433,9 @@ def _dg_candidates(M: int, N: int, K: int, kind: str, packed: bool):
         bm, bn, pk = _dg_info(c)
         if (pk and not packed) or N % bn:
             continue
-        splits = (1,) if kind == "silu" else (1, 2, 4, 8)
+        # S = 3, 5, 6 fill the CUs where powers of two do not (qkv at M = 256: 48
+        # column tiles x 5 = 240 workgroups vs 192 at S = 4); no XCD pairing for them
+        splits = (1,) if kind == "silu" else _DG_SPLITS
         for S in splits:
             if S <= K // 64:
                 out.append((c, S))

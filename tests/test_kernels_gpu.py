@@ -146,7 +146,7 @@ def test_paged_decode(gpu, dt, d, nq, nkv, bs):
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("d,nq,nkv", [(128, 32, 8), (64, 8, 2), (128, 16, 16)])
 @pytest.mark.parametrize("qk_norm", [False, True])
-@pytest.mark.parametrize("S", [0, 3])
+@pytest.mark.parametrize("S", [0, 3, 5])
 @pytest.mark.parametrize("fp8", [False, True])
 def test_paged_decode_rope(gpu, dt, d, nq, nkv, qk_norm, S, fp8):
     """The decode kernel with rope_kv_write folded in == rope_kv_write + paged_decode on
@@ -195,7 +195,10 @@ def test_paged_decode_rope(gpu, dt, d, nq, nkv, qk_norm, S, fp8):
         # v is moved, not computed: bit for bit.  k / q may differ in the last bit (the
         # q/k-norm sum order, FMA contraction of the rotation).
         torch.testing.assert_close(vc1.view(torch.uint8), vc2.view(torch.uint8), atol=0, rtol=0)
-        torch.testing.assert_close(kc1.float(), kc2.float(), **tol)
+        # fp8: a last-bit difference before quantisation can move a value across an e4m3
+        # rounding boundary: one e4m3 step (2^-3 relative) on the rare element
+        torch.testing.assert_close(kc1.float(), kc2.float(),
+                                   **(dict(atol=1e-3, rtol=0.13) if fp8 else tol))
         torch.testing.assert_close(out.float(), out2.float(), **tol)
         # fp32 reference of the whole fused op (CPU)
         kc3, vc3 = kc0.cpu().clone(), vc0.cpu().clone()
@@ -627,7 +630,8 @@ def test_tune_skinny_silu_records_plan(gpu):
 @pytest.mark.parametrize("M,N,K", [(256, 1024, 4096), (200, 768, 1024), (77, 512, 2048)])
 def test_dgemm_matches_fp32(gpu, cfg, M, N, K):
     """K9m decode GEMM (every tile config, packed and row-major weights) vs an fp32 matmul:
-    bf16 output (S = 1), fp32 split-K slices (S = 2, 4) and the fused SiLU epilogue, with M
+    bf16 output (S = 1), fp32 split-K slices (S = 2, 3, 4, 5: uneven K ranges at 3 and 5)
+    and the fused SiLU epilogue, with M
     not a multiple of the row block (clamped loads, masked stores)."""
     from kubernetes_gpu_cluster_amd.ops import gemm
     k = torch.ops.kgc
@@ -648,7 +652,7 @@ def test_dgemm_matches_fp32(gpu, cfg, M, N, K):
     out = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
     k.dgemm(out, x, weight(False), cfg, 1)
     torch.testing.assert_close(out.float().cpu(), ref, atol=3e-2, rtol=2e-2)
-    for S in (2, 4):
+    for S in (2, 3, 4, 5):
         ws = torch.full((S, M, N), float("nan"), dtype=torch.float32, device=gpu)
         k.dgemm(ws, x, weight(False), cfg, 0)
         # every slice row was written (no NaN left) and the slices sum to the product
