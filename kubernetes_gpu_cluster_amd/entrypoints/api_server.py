@@ -342,14 +342,107 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
     def prompt_ids(p) -> list[int]:
         return tokenizer.encode(p) if isinstance(p, str) else [int(x) for x in p]
 
+    async def completions_batch(req: CompletionRequest, prompts: list):
+        """A list of prompts in one /v1/completions request (as vLLM / OpenAI accept it):
+        choice index = prompt * n + choice; streamed chunks interleave, tagged by index."""
+        all_ids = [prompt_ids(p) for p in prompts]
+        for ids in all_ids:
+            if len(ids) >= max_model_len:
+                raise ValueError(f"prompt has {len(ids)} tokens; max_model_len is {max_model_len}")
+        sp = params_from(req, req.max_tokens, req.logprobs)
+        n, rid = sp.n, f"cmpl-{uuid.uuid4().hex}"
+        want_lp = req.logprobs is not None
+        prefixes = [((p if isinstance(p, str) else tokenizer.decode(ids)) if req.echo else "")
+                    for p, ids in zip(prompts, all_ids)]
+        subs, gens = [], []
+        for pi, ids in enumerate(all_ids):
+            for i in range(n):
+                sub = dataclasses.replace(sp, n=1, seed=None if sp.seed is None else sp.seed + i)
+                subs.append(sub)
+                gens.append(engine.generate(ids, sub, f"{rid}-{pi}-{i}"))
+
+        async def drain(k, q=None):
+            detok = _Detok(tokenizer, subs[k].stop)
+            gen, last, lps = gens[k], None, []
+            try:
+                async for out in gen:
+                    last = out
+                    delta = detok.update(out.output_token_ids)
+                    reason = out.finish_reason if out.finished else None
+                    if detok.stopped:
+                        reason = "stop"
+                    elif reason:
+                        delta += detok.flush()
+                    if out.logprobs:
+                        lps.extend(out.logprobs)
+                    if q is not None and (delta or reason or out.logprobs):
+                        await q.put((k, delta, reason, out.logprobs))
+                    if detok.stopped:
+                        await gen.aclose()
+                        break
+            except EngineDeadError as e:
+                if q is None:
+                    raise
+                await q.put((k, None, None, e))
+            finally:
+                if q is not None:
+                    await q.put((k, None, "__done__", None))
+            reason = "stop" if detok.stopped else (last.finish_reason if last else None)
+            return detok.text, reason, (len(last.output_token_ids) if last else 0), lps
+
+        if req.stream:
+            q: asyncio.Queue = asyncio.Queue()
+            head = f'data: {{"id": "{rid}", "object": "text_completion", "created": '
+            model_js = json.dumps(served_name)
+
+            async def sse():
+                tasks = [asyncio.create_task(drain(k, q)) for k in range(len(gens))]
+                done = 0
+                try:
+                    while done < len(gens):
+                        k, delta, reason, lps = await q.get()
+                        if reason == "__done__":
+                            done += 1
+                            continue
+                        if isinstance(lps, BaseException):
+                            yield f"data: {json.dumps({'error': str(lps)})}\n\n"
+                            continue
+                        lp = json.dumps(completion_logprobs(lps or [])) if want_lp else "null"
+                        yield (f'{head}{int(time.time())}, "model": {model_js}, "choices": '
+                               f'[{{"index": {k}, "text": {json.dumps(delta)}, "logprobs": '
+                               f'{lp}, "finish_reason": {json.dumps(reason)}}}]}}\n\n')
+                    yield "data: [DONE]\n\n"
+                finally:
+                    for t in tasks:
+                        t.cancel()
+            return StreamingResponse(sse(), media_type="text/event-stream")
+        res = await asyncio.gather(*[drain(k) for k in range(len(gens))])
+        choices = []
+        for k, (text, reason, _, lps) in enumerate(res):
+            pre = prefixes[k // n]
+            choices.append({"index": k, "text": pre + text,
+                            "logprobs": completion_logprobs(lps, len(pre)) if want_lp else None,
+                            "finish_reason": reason})
+        np_ = sum(len(ids) for ids in all_ids)
+        nc = sum(r[2] for r in res)
+        return JSONResponse({"id": rid, "object": "text_completion", "created": int(time.time()),
+                             "model": served_name, "choices": choices,
+                             "usage": {"prompt_tokens": np_, "completion_tokens": nc,
+                                       "total_tokens": np_ + nc}})
+
     @app.post("/v1/completions")
     async def completions(req: CompletionRequest):
         if not 1 <= req.n <= 16:
             return _err(400, "n must be in [1, 16]")
         prompts = req.prompt
         if isinstance(prompts, list) and prompts and isinstance(prompts[0], (str, list)):
-            if len(prompts) != 1:
-                return _err(400, "batched prompts: send one request per prompt")
+            if len(prompts) > 1:
+                try:
+                    return await completions_batch(req, prompts)
+                except EngineDeadError as e:
+                    return _err(503, f"engine unavailable: {e}", "server_error")
+                except ValueError as e:
+                    return _err(400, str(e))
             prompts = prompts[0]
         ids = prompt_ids(prompts)
         if len(ids) >= max_model_len:

@@ -236,3 +236,27 @@ def test_api_key_guards_v1_routes():
             assert c.get("/metrics").status_code == 200
     finally:
         eng.shutdown()
+
+
+def test_batched_prompts(client):
+    """A list of prompts in one completions request: choice index = prompt * n + choice,
+    echo per prompt, usage summed; streamed chunks carry every index and end in [DONE]."""
+    body = {"prompt": ["hello", "world peace"], "max_tokens": 3, "n": 2, "ignore_eos": True,
+            "temperature": 0, "echo": True}
+    r = client.post("/v1/completions", json=body)
+    j = r.json()
+    assert r.status_code == 200, j
+    assert [c["index"] for c in j["choices"]] == [0, 1, 2, 3]
+    assert j["choices"][0]["text"].startswith("hello")
+    assert j["choices"][0]["text"] == j["choices"][1]["text"]       # greedy: same per prompt
+    assert j["usage"]["completion_tokens"] == 12
+    single = client.post("/v1/completions", json=dict(body, prompt="hello", n=1)).json()
+    assert single["choices"][0]["text"] == j["choices"][0]["text"]
+    r = client.post("/v1/completions", json=dict(body, stream=True, echo=False))
+    events = [l[6:] for l in r.text.splitlines() if l.startswith("data: ")]
+    assert events[-1] == "[DONE]"
+    seen = {json.loads(e)["choices"][0]["index"] for e in events[:-1]}
+    assert seen == {0, 1, 2, 3}
+    # token-id prompts batch the same way
+    r = client.post("/v1/completions", json={"prompt": [[5, 6, 7], [8, 9]], "max_tokens": 2})
+    assert r.status_code == 200 and [c["index"] for c in r.json()["choices"]] == [0, 1]
