@@ -64,6 +64,7 @@ class CompletionRequest(_Lenient):
     top_k: Optional[int] = -1
     n: int = 1
     stream: bool = False
+    stream_options: Optional[dict] = None
     stop: Optional[Union[str, list[str]]] = None
     stop_token_ids: Optional[list[int]] = None
     seed: Optional[int] = None
@@ -94,6 +95,7 @@ class ChatCompletionRequest(_Lenient):
     top_k: Optional[int] = -1
     n: int = 1
     stream: bool = False
+    stream_options: Optional[dict] = None
     stop: Optional[Union[str, list[str]]] = None
     stop_token_ids: Optional[list[int]] = None
     seed: Optional[int] = None
@@ -210,7 +212,16 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
     def tok_str(t: int) -> str:
         return tokenizer.decode([t])
 
-    async def run(ids: list[int], sp: SamplingParams, rid: str, stream_fn, final_fn, stream: bool):
+    def usage_chunk(final_fn, np_: int, nc: int) -> str:
+        """stream_options.include_usage: the last event before [DONE], no choices."""
+        body = final_fn("", None, np_, nc)
+        body["choices"] = []
+        if body["object"] == "chat.completion":
+            body["object"] = "chat.completion.chunk"
+        return "data: " + json.dumps(body) + "\n\n"
+
+    async def run(ids: list[int], sp: SamplingParams, rid: str, stream_fn, final_fn, stream: bool,
+                  include_usage: bool = False):
         """One engine request per choice (n > 1 fans out with seeds seed+i); choices stream
         interleaved, each chunk tagged with its choice index."""
         n = sp.n
@@ -225,8 +236,10 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
             async def sse1():
                 detok = _Detok(tokenizer, sp.stop)
                 gen = gens[0]
+                nc = 0
                 try:
                     async for out in gen:
+                        nc = len(out.output_token_ids)
                         delta = detok.update(out.output_token_ids)
                         reason = out.finish_reason if out.finished else None
                         if detok.stopped:
@@ -241,16 +254,21 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
                     yield f"data: {json.dumps({'error': str(e)})}\n\n"
                 finally:
                     await gen.aclose()
+                if include_usage:
+                    yield usage_chunk(final_fn, len(ids), nc)
                 yield "data: [DONE]\n\n"
             return StreamingResponse(sse1(), media_type="text/event-stream")
         if stream:
             q: asyncio.Queue = asyncio.Queue()
+
+            ncs = [0] * n
 
             async def pump(i):
                 detok = _Detok(tokenizer, subs[i].stop)
                 gen = gens[i]
                 try:
                     async for out in gen:
+                        ncs[i] = len(out.output_token_ids)
                         delta = detok.update(out.output_token_ids)
                         reason = out.finish_reason if out.finished else None
                         if detok.stopped:
@@ -280,6 +298,8 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
                             yield f"data: {json.dumps({'error': str(lps)})}\n\n"
                             continue
                         yield stream_fn(delta, reason, lps, i)
+                    if include_usage:
+                        yield usage_chunk(final_fn, len(ids), sum(ncs))
                     yield "data: [DONE]\n\n"
                 finally:
                     for t in tasks:
@@ -474,7 +494,8 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
                     "usage": {"prompt_tokens": np_, "completion_tokens": nc,
                               "total_tokens": np_ + nc}}
         try:
-            return await run(ids, sp, rid, chunk, final, req.stream)
+            return await run(ids, sp, rid, chunk, final, req.stream,
+                             bool((req.stream_options or {}).get("include_usage")))
         except EngineDeadError as e:
             return _err(503, f"engine unavailable: {e}", "server_error")
         except ValueError as e:
@@ -523,7 +544,8 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
                     "usage": {"prompt_tokens": np_, "completion_tokens": nc,
                               "total_tokens": np_ + nc}}
         try:
-            return await run(ids, sp, rid, chunk, final, req.stream)
+            return await run(ids, sp, rid, chunk, final, req.stream,
+                             bool((req.stream_options or {}).get("include_usage")))
         except EngineDeadError as e:
             return _err(503, f"engine unavailable: {e}", "server_error")
         except ValueError as e:

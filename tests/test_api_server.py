@@ -260,3 +260,17 @@ def test_batched_prompts(client):
     # token-id prompts batch the same way
     r = client.post("/v1/completions", json={"prompt": [[5, 6, 7], [8, 9]], "max_tokens": 2})
     assert r.status_code == 200 and [c["index"] for c in r.json()["choices"]] == [0, 1]
+
+
+def test_stream_include_usage(client):
+    """stream_options.include_usage: one usage event (no choices) right before [DONE]."""
+    for path, body in (("/v1/completions", {"prompt": [5, 6, 7]}),
+                       ("/v1/chat/completions", {"messages": [{"role": "user", "content": "hi"}]})):
+        for n in (1, 2):
+            r = client.post(path, json=dict(body, max_tokens=3, n=n, ignore_eos=True, stream=True,
+                                            stream_options={"include_usage": True}))
+            events = [l[6:] for l in r.text.splitlines() if l.startswith("data: ")]
+            assert events[-1] == "[DONE]"
+            u = json.loads(events[-2])
+            assert u["choices"] == [] and u["usage"]["completion_tokens"] == 3 * n
+            assert all("usage" not in json.loads(e) for e in events[:-2])
