@@ -189,7 +189,9 @@ __device__ __forceinline__ void decode_kv_write(const DecodeRope& rp, int b, int
 // KV8: fp8 e4m3 cache (8-byte fragment loads widened in registers); the K scale is
 // folded into scale_log2 by the launcher, the V scale (v_scale) into the output.
 // FUSE: q comes from the QKV projection row through the rope prologue (rp) and the
-// workgroup holding the last context token writes that token's k / v first.
+// workgroup holding the last context token writes that token's k / v first -- through
+// kc_ / vc_ themselves (const_cast), so every store and load of the cache is based on
+// the same __restrict__ pointer and the workgroup fence orders them.
 template <typename T, int D, bool PREF, bool KV8, int OCC = 3, int NCH = DEC_CHUNKS,
           bool FUSE = false>
 __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
