@@ -35,7 +35,7 @@ import argparse
 import copy
 import re
 import sys
-from typing import Any
+from typing import Any, Optional
 
 import yaml
 
@@ -291,8 +291,21 @@ def _render_multinode(ms, name, release, namespace, nnodes, degree, labels, sel,
     return out
 
 
+def _api_key_env(v) -> Optional[dict]:
+    """servingEngineSpec.vllmApiKey (as the vllm-stack chart takes it): a literal key or
+    {secretName, secretKey} -> the VLLM_API_KEY env entry of every engine and the router."""
+    if not v:
+        return None
+    if isinstance(v, str):
+        return {"name": "VLLM_API_KEY", "value": v}
+    if isinstance(v, dict) and v.get("secretName") and v.get("secretKey"):
+        return {"name": "VLLM_API_KEY", "valueFrom": {"secretKeyRef": {
+            "name": v["secretName"], "key": v["secretKey"]}}}
+    raise ValuesError("servingEngineSpec.vllmApiKey: a string or {secretName, secretKey}")
+
+
 def render_router(release: str, namespace: str, engine_image: str, engine_tag: str,
-                  router: dict) -> list[dict]:
+                  router: dict, key_env: Optional[dict] = None) -> list[dict]:
     labels = {"app.kubernetes.io/name": LABEL_NAME, "app.kubernetes.io/component": "router",
               "app.kubernetes.io/instance": release}
     sa = f"{release}-router-sa"
@@ -324,6 +337,7 @@ def render_router(release: str, namespace: str, engine_image: str, engine_tag: s
                                    "command": ["python3", "-m",
                                                "kubernetes_gpu_cluster_amd.router.router"],
                                    "args": args,
+                                   **({"env": [key_env]} if key_env else {}),
                                    "ports": [{"name": "http", "containerPort": ROUTER_PORT}],
                                    "resources": {"requests": {"cpu": str(router.get("requestCPU", 1)),
                                                               "memory": str(router.get("requestMemory", "1Gi"))}},
@@ -351,15 +365,18 @@ def render(values: dict, release: str = "vllm", namespace: str = "default",
     if len(set(names)) != len(names):
         raise ValuesError(f"duplicate modelSpec names {names}")
     rc = ses.get("runtimeClassName", "") or ""
+    key_env = _api_key_env(ses.get("vllmApiKey"))
     out = []
     for ms in specs:
         ms = dict(ms)
+        if key_env:
+            ms["env"] = list(ms.get("env") or []) + [key_env]
         ms.setdefault("runtimeClassName", rc)
         rcn = ms.pop("runtimeClassName")
         out += render_engine(ms, release, namespace, engine_image, engine_tag, rcn)
     if (values.get("routerSpec") or {}).get("enableRouter", True):
         out += render_router(release, namespace, engine_image, engine_tag,
-                             values.get("routerSpec") or {})
+                             values.get("routerSpec") or {}, key_env)
     return out
 
 

@@ -146,9 +146,13 @@ def test_chart_parity():
                 "gpuMemoryUtilization", "maxModelLen", "extraArgs", "shmSize", "nodeSelector",
                 "affinity", "topologySpreadConstraints", "tolerations", "runtimeClassName",
                 "extraVolumes", "extraVolumeMounts", "-deployment-vllm", "serving-engine",
-                "PYTORCH_HIP_ALLOC_CONF", "/health"):
+                "PYTORCH_HIP_ALLOC_CONF", "/health", "vllmApiKey", "VLLM_API_KEY"):
         assert key in tpl, key
     assert "vllm-router-service" in rt and "port: 80" in rt and "pods" in rt
+    assert "vllmApiKey" in rt and "VLLM_API_KEY" in rt
+    for t in (tpl, rt):
+        opens = len(re.findall(r"{{-?\s*(if|range|with|define)\b", t))
+        assert opens == len(re.findall(r"{{-?\s*end\s*-?}}", t))
     mn = open(os.path.join(ROOT, "deploy/chart/kgc-stack/templates/engine-multinode.yaml")).read()
     for key in ("StatefulSet", "worker_node", "--nnodes", "--master-addr", "--node-rank-offset",
                 "apps.kubernetes.io/pod-index", "clusterIP: None", "engine-worker"):
@@ -195,3 +199,21 @@ def test_multinode_leader_worker_statefulsets():
     bad["servingEngineSpec"]["modelSpec"][0]["vllmConfig"]["nnodes"] = 3
     with pytest.raises(ValuesError):
         render(bad)
+
+
+def test_vllm_api_key_reaches_engines_and_router():
+    """servingEngineSpec.vllmApiKey (vllm-stack chart key): VLLM_API_KEY on every engine
+    container and on the router (its /v1/models polls), literal or from a Secret."""
+    v = _load(os.path.join(ROOT, "deploy/values/values-llama3-8b-tp1.yaml"))
+    for key, want in (("k1", {"name": "VLLM_API_KEY", "value": "k1"}),
+                      ({"secretName": "s", "secretKey": "api"},
+                       {"name": "VLLM_API_KEY", "valueFrom": {"secretKeyRef": {"name": "s", "key": "api"}}})):
+        v2 = dict(v, servingEngineSpec=dict(v["servingEngineSpec"], vllmApiKey=key))
+        objs = render(v2)
+        deps = _by_kind(objs, "Deployment")
+        assert deps and all(want in d["spec"]["template"]["spec"]["containers"][0]["env"]
+                            for d in deps), deps
+    objs = render(v)
+    assert all(not any(e.get("name") == "VLLM_API_KEY"
+                       for e in d["spec"]["template"]["spec"]["containers"][0].get("env", []))
+               for d in _by_kind(objs, "Deployment"))
