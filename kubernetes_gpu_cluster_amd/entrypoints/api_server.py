@@ -577,6 +577,7 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
     async def models():
         return {"object": "list", "data": [{"id": served_name, "object": "model",
                                             "created": created, "owned_by": "kgc",
+                                            "root": served_name, "parent": None,
                                             "max_model_len": max_model_len}]}
 
     @app.get("/health")
@@ -584,6 +585,11 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
         if not engine.is_alive:
             return PlainTextResponse("engine dead", status_code=503)
         return PlainTextResponse("ok")
+
+    @app.api_route("/ping", methods=["GET", "POST"])
+    async def ping():
+        """vLLM's /ping (SageMaker-style liveness): same answer as /health."""
+        return await health()
 
     @app.get("/kgc/engine_stats")
     async def engine_stats(since: float = 0.0):

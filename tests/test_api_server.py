@@ -35,6 +35,8 @@ def test_models_health_metrics(client):
     r = client.get("/v1/models")
     assert r.status_code == 200 and r.json()["data"][0]["id"] == "tiny-llama"
     assert client.get("/health").text == "ok"
+    assert client.get("/ping").status_code == 200 and client.post("/ping").status_code == 200
+    assert r.json()["data"][0]["root"] == "tiny-llama"
     client.post("/v1/completions", json={"prompt": "hi", "max_tokens": 2})
     m = client.get("/metrics").text
     assert "vllm:generation_tokens_total" in m and "vllm:time_to_first_token_seconds" in m
