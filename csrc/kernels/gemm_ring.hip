@@ -1,0 +1,350 @@
+// K9r: full-K "ring" decode GEMM for gfx950, M = 32..512 rows (the batch-256 decode step).
+//
+//   C[M, N] = X[M, K] . W[N, K]^T      bf16 in, fp32 MFMA accumulation
+//
+// Why a second mid-batch kernel beside K9m (gemm_decode.hip).  K9m fills the chip on the
+// narrow projections (o: N = 4096, qkv: 6144) by splitting K, and the fp32 K-slices it
+// writes (o at S = 4: 16.8 MB, qkv at S = 5: 31.5 MB, down at S = 8: 33.5 MB per layer)
+// cost as much HBM traffic as the weights, plus a read-back in the consumer.  K9r instead
+// sizes the OUTPUT tile so that ~256 tiles cover the whole [M, N] output (o at M = 256:
+// 64 x 64, qkv: 64 x 96, gate_up + SiLU: 128 x 224) and walks the whole K in one
+// workgroup: no partials, the epilogue writes bf16 straight to the consumer.
+//
+// A workgroup's intake is then (BM + BN) x K x 2 bytes (1 MB for o), which the per-CU
+// L1/LDS-DMA path (~64 B/clk) can only sustain with many bytes in flight: every K-step
+// (BK = 64) is one ring slot of (BM + BN) x 128 B in LDS, and the ring is as deep as LDS
+// allows (NS slots, NS - 1 K-steps in flight: 8 x 16 KB for 64 x 64, 7 x 20 KB for
+// 64 x 96), retired with counted `s_waitcnt vmcnt` and ONE raw s_barrier per step.
+//   * both operands by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave instruction) into
+//     128-B rows with the 16-B chunk XOR swizzle (chunk ^ row % 8) applied on the SOURCE
+//     address, conflict-free ds_read_b128 fragment reads (same image as K9m);
+//   * weights pre-packed once at load time as [N/G][K/64][G x 64] (G-row groups, swizzle
+//     baked in; G = BN makes every K-step of a column tile one contiguous block);
+//   * XCD-aware tile order: workgroups b, b+8, b+16, ... share an XCD (round-robin
+//     dispatch; speed only, never correctness), so the BM-row blocks of one weight column
+//     tile run side by side on one XCD and the weight tile is fetched from HBM once and
+//     served from that XCD's L2 to the others; with split-K the K-slice is fixed per XCD;
+//   * optional loader waves (LW): the MFMA waves never issue a DMA or wait on vmcnt;
+//   * epilogues: OUT (bf16 tile), SILU (merged [gate; up] weight packed with 8-row
+//     gate / up interleave inside every 16-row group: lane fr < 8 holds gate, its xor-8
+//     partner the matching up column, one DPP-free shuffle per element; any BN % 16 == 0
+//     works, e.g. 224 = 112 gate + 112 up columns, 256 tiles for Llama-3-8B's 14336),
+//     PARTIAL (fp32 K-slices, write-through, for the long-K down projection where a
+//     2-4 way split still pays).
+// Reference parity: SURVEY.md §2.5 K9 (decode GEMMs of the vLLM engine image the
+// reference deploys, /root/reference/values-01-minimal-example2.yaml:6-7).
+#include "common.h"
+#include "launch.h"
+#include <cstdlib>
+
+namespace kgc {
+
+namespace {
+
+constexpr int RG_BK = 64, RG_ROWB = 128;     // K-step, LDS row bytes (BK bf16)
+enum { RG_PARTIAL = 0, RG_OUT = 1, RG_SILU = 2 };
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
+
+template <int AUX>
+__device__ __forceinline__ void rg_glds16(const void* src, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)lds_wave_base, 16, 0, AUX);
+}
+
+template <int N>
+__device__ __forceinline__ void rg_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait until at most min(Y, younger) K-steps of L DMAs each are still in flight
+template <int L, int Y>
+__device__ __forceinline__ void rg_wait(int younger) {
+  if constexpr (Y == 0) {
+    rg_vmcnt<0>();
+  } else {
+    if (younger >= Y) { rg_vmcnt<L * Y>(); return; }
+    rg_wait<L, Y - 1>(younger);
+  }
+}
+
+__device__ __forceinline__ float rg_silu(float g) { return g / (1.f + __expf(-g)); }
+__device__ __forceinline__ int rg_swz(int row, int chunk) { return chunk ^ (row & 7); }
+
+// packed row p of a merged [gate; up] weight (I = N / 2 outputs): in every 16-row group,
+// rows 0-7 are gate columns 8g..8g+7, rows 8-15 the up columns of the same outputs
+__device__ __forceinline__ int64_t rg_silu_row(int64_t p, int I) {
+  const int64_t g = p >> 4;
+  const int i = (int)(p & 15);
+  return i < 8 ? g * 8 + i : I + g * 8 + (i - 8);
+}
+
+// CW = WM * WN MFMA waves, LW loader waves (0: the MFMA waves issue the DMAs themselves)
+template <int BM, int BN, int WM, int WN, int LW, int NS, int WAUX, int EPI>
+__global__ __launch_bounds__((WM * WN + LW) * 64, 1) void ring_gemm_kernel(
+    void* __restrict__ Cv, const bf16* __restrict__ X, const bf16* __restrict__ Wp, int M,
+    int N, int K, int64_t ldx, int S, int G, int MB, int64_t slice_stride, int xmap, int wt) {
+  constexpr int CW = WM * WN;
+  constexpr int NI = LW > 0 ? LW : CW;            // waves issuing DMAs
+  constexpr int D = NS - 1;                       // K-steps in flight
+  constexpr int PA = BM / 8, PB = BN / 8, P = PA + PB;   // 1-KiB DMA pieces per K-step
+  constexpr int LHI = (P + NI - 1) / NI, LLO = P / NI, REM = P % NI;
+  constexpr int SLOT = (BM + BN) * RG_ROWB;
+  constexpr int MT = BM / WM / 16, NT = BN / WN / 16;
+  static_assert(MT * WM * 16 == BM && NT * WN * 16 == BN, "wave tiling");
+  static_assert(NS >= 2 && NS * SLOT <= 163840, "LDS ring exceeds 160 KiB");
+  static_assert(D * LHI <= 63, "vmcnt range");
+  // ONE shared array (a second __shared__ object can make hipcc emit vmcnt(0) before the
+  // first ds_read of every step)
+  __shared__ __attribute__((aligned(16))) char lds[NS * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool issuer = LW > 0 ? wave >= CW : true;
+  const bool consumer = wave < CW;
+  const int iw = LW > 0 ? wave - CW : wave;       // index among the issuing waves
+
+  // ---- tile coordinates (XCD-aware when the host says the grid divides evenly)
+  const int nbt = N / BN;
+  int z, mb, nb;
+  if (xmap) {
+    const int r8 = blockIdx.x & 7, q = blockIdx.x >> 3, cpg = 8 / S;
+    z = r8 % S;
+    mb = q % MB;
+    nb = (q / MB) * cpg + r8 / S;
+  } else {
+    z = blockIdx.x % S;
+    const int j = blockIdx.x / S;
+    mb = j % MB;
+    nb = j / MB;
+  }
+  (void)nbt;
+  const int m0 = mb * BM;
+  const int nk_all = K / RG_BK;
+  const int kb0 = (int)((int64_t)nk_all * z / S);
+  const int nk = (int)((int64_t)nk_all * (z + 1) / S) - kb0;
+  // the row blocks of one column tile walk K in the same order (they share the weight
+  // lines through L2); column tiles start at different steps (spread the X line fetches)
+  const int rot = nk >= 4 ? (int)(((int64_t)nb * 37) % nk) : 0;
+
+  // ---- per-piece DMA sources (pieces p = iw, iw + NI, ...): A rows first, then B rows
+  const int drow = lane >> 3, dchunk = (lane & 7) ^ drow;
+  const int nl = iw < REM ? LHI : LLO;
+  const bf16* src[LHI];
+  int64_t sstep[LHI];
+  int ldso[LHI];
+  bool isb[LHI];
+#pragma unroll
+  for (int t = 0; t < LHI; ++t) {
+    const int p = iw + t * NI;
+    ldso[t] = p * 1024;
+    isb[t] = p >= PA;
+    if (p < PA) {
+      int r = m0 + p * 8 + drow;
+      r = r < M ? r : M - 1;                      // padded rows re-read the last row
+      src[t] = X + (int64_t)r * ldx + dchunk * 8;
+      sstep[t] = RG_BK;
+    } else {
+      const int q = p - PA;                       // B piece: tile rows 8q .. 8q + 7
+      const int64_t prow = (int64_t)nb * BN + q * 8;
+      const int64_t grp = prow / G;
+      const int r0 = (int)(prow - grp * G);
+      src[t] = Wp + grp * nk_all * ((int64_t)G * RG_BK) + r0 * RG_BK + lane * 8;
+      sstep[t] = (int64_t)G * RG_BK;
+    }
+  }
+
+  auto issue = [&](int step) {
+    char* base = lds + (step % NS) * SLOT;
+    int st = step + rot;
+    st = st >= nk ? st - nk : st;
+    const int kb = kb0 + st;
+#pragma unroll
+    for (int t = 0; t < LHI; ++t) {
+      if (t < nl) {
+        // weights: WAUX = 2 (nt) streams them past L2 (each weight byte is read by ONE
+        // workgroup when BM covers all rows); activations keep the default policy
+        if (isb[t]) rg_glds16<WAUX>(src[t] + kb * sstep[t], base + ldso[t]);
+        else rg_glds16<0>(src[t] + kb * sstep[t], base + ldso[t]);
+      }
+    }
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int wm = consumer ? wave / WN : 0, wn = consumer ? wave % WN : 0;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int a_row0 = wm * (BM / WM) + fr;
+  const int b_row0 = wn * (BN / WN) + fr;
+
+  if (issuer) {
+#pragma unroll
+    for (int p = 0; p < D; ++p)
+      if (p < nk) issue(p);
+  }
+  for (int it = 0; it < nk; ++it) {
+    // step `it` must have landed; up to D - 1 younger steps may stay in flight
+    if (issuer) {
+      const int younger = nk - 1 - it;
+      if (nl == LHI) rg_wait<LHI, D - 1>(younger);
+      else rg_wait<LLO, D - 1>(younger);
+    }
+    __builtin_amdgcn_s_barrier();
+    // every wave is past the reads of step it - 1, whose slot step it + D reuses
+    if (issuer && it + D < nk) issue(it + D);
+    if (!consumer) continue;
+    const char* sa = lds + (it % NS) * SLOT;
+    const char* sb = sa + BM * RG_ROWB;
+#pragma unroll
+    for (int ks = 0; ks < RG_BK / 32; ++ks) {
+      const int c = ks * 4 + fq;
+      Pack8<bf16> af[MT], bfr[NT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int r = a_row0 + i * 16;
+        af[i].u = *reinterpret_cast<const u32x4*>(sa + r * RG_ROWB + (rg_swz(r, c) << 4));
+      }
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const int r = b_row0 + n * 16;
+        bfr[n].u = *reinterpret_cast<const u32x4*>(sb + r * RG_ROWB + (rg_swz(r, c) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) acc[i][n] = mfma16x16x32(af[i].v, bfr[n].v, acc[i][n]);
+    }
+  }
+
+  // ---- epilogue: lane holds C[4*fq + e][fr] of every 16x16 tile
+  if (!consumer) return;
+  const int64_t col0 = (int64_t)nb * BN + wn * (BN / WN) + fr;
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int row = m0 + wm * (BM / WM) + i * 16 + fq * 4 + e;
+      if constexpr (EPI == RG_SILU) {
+        // the up half of each 16-column group sits in lanes fr + 8 (all lanes shuffle)
+        const int I = N >> 1;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          const float g = acc[i][n][e];
+          const float u = __shfl_xor(g, 8, 64);
+          if (row < M && fr < 8) {
+            const int64_t oc = ((col0 + n * 16) >> 4) * 8 + fr;
+            reinterpret_cast<bf16*>(Cv)[(int64_t)row * I + oc] = (bf16)(rg_silu(g) * u);
+          }
+        }
+      } else {
+        if (row >= M) continue;
+        if constexpr (EPI == RG_PARTIAL) {
+          float* cp = reinterpret_cast<float*>(Cv) + z * slice_stride + (int64_t)row * N + col0;
+#pragma unroll
+          for (int n = 0; n < NT; ++n) {
+            if (wt) __hip_atomic_store(cp + n * 16, acc[i][n][e], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            else cp[n * 16] = acc[i][n][e];
+          }
+        } else {
+          bf16* cp = reinterpret_cast<bf16*>(Cv) + (int64_t)row * N + col0;
+#pragma unroll
+          for (int n = 0; n < NT; ++n) cp[n * 16] = (bf16)acc[i][n][e];
+        }
+      }
+    }
+  }
+}
+
+// P[grp][kb][r][pos] (16-B chunks) = W[row(grp * G + r)][kb * 64 + (pos ^ r % 8) * 8 ..]
+__global__ __launch_bounds__(256) void ring_pack_kernel(bf16* __restrict__ P,
+                                                        const bf16* __restrict__ W, int N,
+                                                        int K, int G, int silu) {
+  const int nk_all = K / RG_BK;
+  const int64_t chunk = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)N * K / 8;
+  if (chunk >= total) return;
+  const int pos = (int)(chunk & 7);
+  const int64_t rowi = chunk >> 3;                 // (grp, kb, r) flattened
+  const int r = (int)(rowi % G);
+  const int64_t t = rowi / G;
+  const int kb = (int)(t % nk_all);
+  const int64_t grp = t / nk_all;
+  const int64_t p = grp * G + r;
+  const int64_t wrow = silu ? rg_silu_row(p, N >> 1) : p;
+  const int64_t s = wrow * K + kb * RG_BK + rg_swz(r, pos) * 8;
+  reinterpret_cast<u32x4*>(P)[chunk] = *reinterpret_cast<const u32x4*>(W + s);
+}
+
+struct RingCfg { int bm, bn, wm, wn, lw, ns, waux; };
+// id -> tile.  One workgroup per CU, ~256 workgroups at the target M.  BM = 256 (all rows
+// of a batch-256 step) reads every weight byte from HBM exactly once: measured, row
+// blocks of one column tile dispatched side by side on an XCD do NOT share the weight
+// lines through L2 (64 x 64 full-K o_proj: 25.5 us = 4 x 33.5 MB at the chip's rate).
+// The narrow projections then split K (o: 256 x 64, S = 4; qkv: 256 x 96, S = 4);
+// gate_up + SiLU: 256 x 112 (7 gate / up groups of 16), 256 tiles at S = 1.
+// All with 4 loader waves (the MFMA waves never issue a DMA: 1.3-1.6x faster measured).
+constexpr int kRingCfgs = 16;
+constexpr RingCfg kRing[kRingCfgs] = {
+    {256, 64, 4, 2, 4, 4, 0},  {256, 64, 4, 2, 4, 4, 2},  {256, 96, 4, 2, 4, 3, 0},
+    {256, 96, 4, 2, 4, 3, 2},  {256, 112, 4, 1, 4, 3, 0}, {256, 112, 4, 1, 4, 3, 2},
+    {256, 128, 4, 2, 4, 3, 0}, {256, 128, 4, 2, 4, 3, 2}, {256, 32, 4, 2, 4, 4, 0},
+    {128, 128, 2, 2, 4, 5, 0}, {128, 224, 2, 2, 4, 3, 0}, {128, 64, 2, 2, 4, 6, 0},
+    {128, 96, 2, 2, 4, 5, 0},  {128, 112, 4, 1, 4, 5, 0}, {64, 64, 2, 2, 4, 9, 0},
+    {256, 32, 4, 2, 4, 4, 2}};
+
+template <int C>
+void ring_launch(int epi, void* Cp, const void* X, const void* W, int M, int N, int K,
+                 int64_t ldx, int S, int G, int64_t ss, hipStream_t s) {
+  constexpr RingCfg c = kRing[C];
+  const int MB = (M + c.bm - 1) / c.bm;
+  const dim3 grid((unsigned)(MB * (N / c.bn) * S));
+  const int nbt = N / c.bn;
+  const int xm = (8 % S == 0 && nbt % (8 / S) == 0) ? 1 : 0;
+  static const int wt = [] {
+    const char* e = getenv("KGC_PARTIAL_WT");
+    return e ? atoi(e) : 1;
+  }();
+#define RG_LAUNCH(E)                                                                        \
+  ring_gemm_kernel<c.bm, c.bn, c.wm, c.wn, c.lw, c.ns, c.waux, E>                           \
+      <<<grid, (c.wm * c.wn + c.lw) * 64, 0, s>>>(Cp, (const bf16*)X, (const bf16*)W, M, N, \
+                                                  K, ldx, S, G, MB, ss, xm, wt)
+  if (epi == RG_PARTIAL) RG_LAUNCH(RG_PARTIAL);
+  else if (epi == RG_OUT) RG_LAUNCH(RG_OUT);
+  else RG_LAUNCH(RG_SILU);
+#undef RG_LAUNCH
+}
+
+template <int... Is>
+void ring_dispatch(int cfg, int epi, void* C, const void* X, const void* W, int M, int N, int K,
+                   int64_t ldx, int S, int G, int64_t ss, hipStream_t s,
+                   std::integer_sequence<int, Is...>) {
+  ((cfg == Is ? (ring_launch<Is>(epi, C, X, W, M, N, K, ldx, S, G, ss, s), 0) : 0), ...);
+}
+
+}  // namespace
+
+int ring_num_cfgs() { return kRingCfgs; }
+void ring_cfg_info(int cfg, int* bm, int* bn, int* threads, int* slots) {
+  *bm = kRing[cfg].bm;
+  *bn = kRing[cfg].bn;
+  *threads = (kRing[cfg].wm * kRing[cfg].wn + kRing[cfg].lw) * 64;
+  *slots = kRing[cfg].ns;
+}
+
+void launch_ring_gemm(int cfg, int epi, void* C, const void* X, const void* Wp, int M, int N,
+                      int K, int64_t ldx, int S, int G, int64_t slice_stride, hipStream_t s) {
+  ring_dispatch(cfg, epi, C, X, Wp, M, N, K, ldx, S, G, slice_stride, s,
+                std::make_integer_sequence<int, kRingCfgs>{});
+}
+
+void launch_ring_pack(bool silu, void* P, const void* W, int N, int K, int G, hipStream_t s) {
+  const int64_t chunks = (int64_t)N * K / 8;
+  const dim3 grid((unsigned)((chunks + 255) / 256));
+  ring_pack_kernel<<<grid, 256, 0, s>>>((bf16*)P, (const bf16*)W, N, K, G, silu ? 1 : 0);
+}
+
+}  // namespace kgc

@@ -38,6 +38,8 @@ class EngineConfig:
     max_num_batched_tokens: Optional[int] = None
     enable_chunked_prefill: bool = True
     prefill_first: bool = False           # decodes sit out while prompts wait (scheduler.py)
+    prefill_first_max_defer: int = 8      # ... for at most this many consecutive steps
+    prefill_first_max_gap_ms: float = 0.0  # ... or until a running stream waited this long
     enable_prefix_caching: bool = True    # vLLM V1 default: reuse cached KV of shared prefixes
     enforce_eager: bool = False
     disable_custom_all_reduce: bool = False
@@ -118,6 +120,12 @@ def add_engine_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     a("--prefill-first", action="store_true",
       help="while prompts wait for a free sequence slot, running sequences skip decode steps "
            "and the token budget goes to prefill (lower TTFT under bursts)")
+    a("--prefill-first-max-defer", type=int, default=8,
+      help="with --prefill-first: decodes run at least every N+1 steps (bounds TPOT under "
+           "continuous arrivals; 8 keeps a 256 x 512-token burst prefill-only)")
+    a("--prefill-first-max-gap-ms", type=float, default=0.0,
+      help="with --prefill-first: never defer decodes once a running stream has waited this "
+           "long for its next token (0 = off)")
     a("--enable-prefix-caching", dest="enable_prefix_caching", action="store_true", default=True)
     a("--no-enable-prefix-caching", dest="enable_prefix_caching", action="store_false")
     a("--enforce-eager", action="store_true")
@@ -153,7 +161,8 @@ def config_from_args(ns: argparse.Namespace) -> EngineConfig:
         gpu_memory_utilization=ns.gpu_memory_utilization, block_size=ns.block_size,
         max_num_seqs=ns.max_num_seqs, max_num_batched_tokens=ns.max_num_batched_tokens,
         enable_chunked_prefill=ns.enable_chunked_prefill, enforce_eager=ns.enforce_eager,
-        prefill_first=ns.prefill_first,
+        prefill_first=ns.prefill_first, prefill_first_max_defer=ns.prefill_first_max_defer,
+        prefill_first_max_gap_ms=ns.prefill_first_max_gap_ms,
         enable_prefix_caching=ns.enable_prefix_caching,
         disable_custom_all_reduce=ns.disable_custom_all_reduce,
         trust_remote_code=ns.trust_remote_code, kv_cache_dtype=ns.kv_cache_dtype, seed=ns.seed,

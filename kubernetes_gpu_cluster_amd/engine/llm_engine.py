@@ -91,11 +91,14 @@ class LLMEngine:
         if self.pp_depth > 1:
             self.scheduler = VirtualSchedulers(self.pp_depth, self.bm, cfg.max_num_seqs,
                                                cfg.token_budget(), self.max_model_len,
-                                               cfg.enable_chunked_prefill, cfg.prefill_first)
+                                               cfg.enable_chunked_prefill, cfg.prefill_first,
+                                               cfg.prefill_first_max_defer,
+                                               cfg.prefill_first_max_gap_ms)
         else:
             self.scheduler = Scheduler(self.bm, cfg.max_num_seqs, cfg.token_budget(),
                                        self.max_model_len, cfg.enable_chunked_prefill,
-                                       cfg.prefill_first)
+                                       cfg.prefill_first, cfg.prefill_first_max_defer,
+                                       cfg.prefill_first_max_gap_ms)
         self._pp_inflight: list = [None] * self.pp_depth
         self._vnext = 0
         self.seqs: dict[str, Sequence] = {}

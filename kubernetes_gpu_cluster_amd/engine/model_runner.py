@@ -117,9 +117,17 @@ class ModelRunner:
         max_tokens = max(token_budget, max_num_seqs)
         self.L = Layout(max_tokens, max_num_seqs, self.max_blocks, ops.PREFILL_BLOCK_M)
         pin = self.is_gpu
-        self.h64 = torch.zeros(self.L.n64, dtype=torch.int64, pin_memory=pin)
-        self.h32 = torch.zeros(self.L.n32, dtype=torch.int32, pin_memory=pin)
-        self.hf = torch.zeros(self.L.nf, dtype=torch.float32, pin_memory=pin)
+        # Pinned step blobs, a ring of sets: a plan is packed into one set while the
+        # non-blocking H2D copies of earlier plans (async mode: the previous step; PP: up
+        # to pp_size micro-batches in flight) may still read theirs.  A set is reused only
+        # after the event recorded behind its upload has completed (next_host_bufs).
+        self._hsets = [(torch.zeros(self.L.n64, dtype=torch.int64, pin_memory=pin),
+                        torch.zeros(self.L.n32, dtype=torch.int32, pin_memory=pin),
+                        torch.zeros(self.L.nf, dtype=torch.float32, pin_memory=pin))
+                       for _ in range(self.ps.pp_size + 2)]
+        self._hev: list = [None] * len(self._hsets)
+        self._hcur = 0
+        self.h64, self.h32, self.hf = self._hsets[0]
         self.d64 = torch.zeros(self.L.n64, dtype=torch.int64, device=device)
         self.d32 = torch.zeros(self.L.n32, dtype=torch.int32, device=device)
         self.df = torch.zeros(self.L.nf, dtype=torch.float32, device=device)
@@ -220,8 +228,21 @@ class ModelRunner:
             self.workspace = ops.decode_partials(self.max_num_seqs, nq, d, self.max_blocks, self.bs,
                                                  self.device)
 
+    def next_host_bufs(self) -> None:
+        """Switch h64 / h32 / hf to the next pinned set of the ring, waiting until the
+        upload that last read it has finished (normally long done: a set comes round
+        again only after pp_size + 1 further plans).  Call before packing a plan into
+        the blobs (driver: build_plan; other ranks: before receiving one)."""
+        self._hcur = (self._hcur + 1) % len(self._hsets)
+        ev = self._hev[self._hcur]
+        if ev is not None:
+            ev.synchronize()
+            self._hev[self._hcur] = None
+        self.h64, self.h32, self.hf = self._hsets[self._hcur]
+
     def _dummy_prefill(self, qlens: list[int]) -> None:
         """A prefill forward with slot -1 (no KV writes) over dummy block tables."""
+        self.next_host_bufs()
         T = sum(qlens)
         P = len(qlens)
         L = self.L
@@ -250,6 +271,7 @@ class ModelRunner:
         (in sampled-row order).  device_tokens: decode inputs are gathered on the GPU
         from last_tok (async mode), so the host needs no sampled token values."""
         L, bs, mb = self.L, self.bs, self.max_blocks
+        self.next_host_bufs()
         i64, i32, f32 = self.h64.numpy(), self.h32.numpy(), self.hf.numpy()
         P, D = len(prefills), len(decodes)
         samplers: list[Sequence] = []
@@ -351,6 +373,9 @@ class ModelRunner:
             self.d64.copy_(self.h64, non_blocking=True)
             self.d32.copy_(self.h32, non_blocking=True)
             self.df.copy_(self.hf, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._hev[self._hcur] = ev
         else:
             self.d64.copy_(torch.from_numpy(plan.i64))
             self.d32.copy_(torch.from_numpy(plan.i32))
@@ -579,6 +604,7 @@ class ModelRunner:
         L, mb = self.L, self.max_blocks
         nkv = self.model.local_kv_heads()
         # a valid idle decode state: ctx_len 0 rows (write zeros), slot -1
+        self.next_host_bufs()
         self.h64.zero_()
         self.h32.zero_()
         self.h64[L.slots:L.slots + self.graph_max_bs] = -1

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import collections
 import dataclasses
+import time
 from typing import Optional
 
 from .block_manager import BlockManager
@@ -45,12 +46,21 @@ class ScheduledBatch:
 
 class Scheduler:
     def __init__(self, block_manager: BlockManager, max_num_seqs: int, token_budget: int,
-                 max_model_len: int, chunked_prefill: bool = True, prefill_first: bool = False):
+                 max_model_len: int, chunked_prefill: bool = True, prefill_first: bool = False,
+                 max_defer_steps: int = 8, max_decode_gap_ms: float = 0.0):
         self.bm = block_manager
         # prefill-first: while prompts wait and a sequence slot is free, decoding sequences
         # sit the step out and the whole token budget goes to prefill (lower TTFT under a
-        # burst, at the cost of the running sequences' TPOT)
+        # burst, at the cost of the running sequences' TPOT).  Bounded: after
+        # max_defer_steps consecutive steps that skipped decodes (or once a running
+        # sequence has waited max_decode_gap_ms for a token), the next step decodes every
+        # running sequence and prefill takes what is left of the budget -- under continuous
+        # arrivals the running streams never starve.
         self.prefill_first = prefill_first
+        self.max_defer_steps = max(0, max_defer_steps)
+        self.max_decode_gap_s = max(0.0, max_decode_gap_ms) / 1e3
+        self._deferred = 0              # consecutive steps whose decodes sat out
+        self._skipped = 0
         self.max_num_seqs = max_num_seqs
         self.token_budget = token_budget
         self.max_model_len = max_model_len
@@ -84,13 +94,24 @@ class Scheduler:
         self.num_preemptions += 1
         self.waiting.appendleft(seq)
 
+    def _decode_overdue(self) -> bool:
+        if self.max_decode_gap_s <= 0:
+            return False
+        now = time.monotonic()
+        return any(s.last_token_time is not None and now - s.last_token_time > self.max_decode_gap_s
+                   for s in self.running)
+
     def schedule(self) -> ScheduledBatch:
         defer = (self.prefill_first and bool(self.waiting)
-                 and len(self.running) < self.max_num_seqs)
+                 and len(self.running) < self.max_num_seqs
+                 and self._deferred < self.max_defer_steps and not self._decode_overdue())
+        self._skipped = 0
         batch = self._schedule(defer)
         if defer and batch.is_empty:
             # nothing admissible (e.g. the KV pool is full): decode as usual
+            self._skipped = 0
             batch = self._schedule(False)
+        self._deferred = self._deferred + 1 if self._skipped else 0
         return batch
 
     def _schedule(self, defer_decodes: bool) -> ScheduledBatch:
@@ -103,6 +124,7 @@ class Scheduler:
             seq = self.running[i]
             remaining = seq.num_tokens - seq.num_computed
             if defer_decodes and remaining == 1:
+                self._skipped += 1
                 i += 1
                 continue
             n = 1 if remaining == 1 else min(remaining, budget)
@@ -168,10 +190,12 @@ class VirtualSchedulers:
     each step still has the full token budget."""
 
     def __init__(self, n: int, block_manager: BlockManager, max_num_seqs: int, token_budget: int,
-                 max_model_len: int, chunked_prefill: bool = True, prefill_first: bool = False):
+                 max_model_len: int, chunked_prefill: bool = True, prefill_first: bool = False,
+                 max_defer_steps: int = 8, max_decode_gap_ms: float = 0.0):
         per = max(1, max_num_seqs // n)
         self.scheds = [Scheduler(block_manager, per, token_budget, max_model_len, chunked_prefill,
-                                 prefill_first) for _ in range(n)]
+                                 prefill_first, max_defer_steps, max_decode_gap_ms)
+                       for _ in range(n)]
 
     def __len__(self) -> int:
         return len(self.scheds)

@@ -222,6 +222,7 @@ def worker_loop(worker: Worker) -> None:
             worker.capture()
         elif cmd == CMD_STEP:
             hdr = h[2:2 + N_HDR]
+            worker.runner.next_host_bufs()
             _bcast_plan_blobs(worker.runner, hdr)
             r = worker.runner
             plan = StepPlan(*hdr, r.h64.numpy(), r.h32.numpy(), r.hf.numpy())
@@ -317,18 +318,26 @@ class _DistExecutorBase:
     worker: Worker
     watchdog: Optional[RankWatchdog] = None
 
-    def _step_launched(self):
+    def _step_launched(self, begin: bool = True):
         """Book-keeping after a step's kernels are enqueued: progress for the watchdog, and
         an async copy of the xGMI all-reduce error word checked when the step completes."""
-        if self.watchdog is not None:
+        if begin and self.watchdog is not None:
             self.watchdog.step_begin()
         # sticky error words of the peer-memory collectives (xGMI all-reduce, EP exchange)
         checks = [c for c in (comm.get_custom_allreduce(), getattr(self.worker, "ep_a2a", None),
                               self.worker.runner.pp_link) if c is not None]
         for c in checks:
             c.enqueue_err_read()
+        # the error words land in pinned host memory behind this event: done() reads them
+        # only after it, so a failure of this step is reported with this step's tokens
+        ev = None
+        if checks and self.worker.runner.is_gpu:
+            ev = torch.cuda.Event()
+            ev.record()
 
         def done():
+            if ev is not None:
+                ev.synchronize()
             if self.watchdog is not None:
                 self.watchdog.step_end()
             for c in checks:
@@ -365,10 +374,13 @@ class _DistExecutorBase:
         """PP > 1: send the plan to every rank, run stage 0 of it here (its activations
         go to stage 1 by point-to-point), and return at once; the last stage's TP leader
         sends the sampled ids back, received by a posted irecv."""
-        done = self._step_launched()
+        if self.watchdog is not None:
+            self.watchdog.step_begin()
         _bcast_cmd(CMD_STEP, 0, plan.header())
         _bcast_plan_blobs(self.worker.runner, plan.header())
         self.worker.run(plan)
+        # the error-word copies go behind this micro-batch's kernels, not ahead of them
+        done = self._step_launched(begin=False)
         s = get_state()
         t = torch.empty(plan.S, dtype=torch.int64)
         src = getattr(s, "global_base", 0) + (s.pp_size - 1) * s.tp_size

@@ -29,6 +29,7 @@ from typing import Any, Optional, Union
 from fastapi import FastAPI, Request
 from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
 from pydantic import BaseModel, ConfigDict, Field
+from starlette.background import BackgroundTask
 
 from .. import __version__
 from ..engine.config import EngineConfig, add_engine_args, config_from_args
@@ -209,6 +210,11 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
                               logit_bias={int(k): float(v) for k, v in (req.logit_bias or {}).items()}
                               or None)
 
+    def close_all(gens) -> None:
+        """Abort every submitted choice that has not finished (no-op for finished ones)."""
+        for g in gens:
+            g.close()
+
     def tok_str(t: int) -> str:
         return tokenizer.decode([t])
 
@@ -257,7 +263,8 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
                 if include_usage:
                     yield usage_chunk(final_fn, len(ids), nc)
                 yield "data: [DONE]\n\n"
-            return StreamingResponse(sse1(), media_type="text/event-stream")
+            return StreamingResponse(sse1(), media_type="text/event-stream",
+                                     background=BackgroundTask(close_all, gens))
         if stream:
             q: asyncio.Queue = asyncio.Queue()
 
@@ -304,7 +311,8 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
                 finally:
                     for t in tasks:
                         t.cancel()
-            return StreamingResponse(sse(), media_type="text/event-stream")
+            return StreamingResponse(sse(), media_type="text/event-stream",
+                                     background=BackgroundTask(close_all, gens))
 
         async def one(i):
             detok = _Detok(tokenizer, subs[i].stop)
@@ -320,7 +328,10 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
                     break
             reason = "stop" if detok.stopped else (last.finish_reason if last else None)
             return detok.text, reason, (len(last.output_token_ids) if last else 0), lps
-        res = await asyncio.gather(*[one(i) for i in range(n)])
+        try:
+            res = await asyncio.gather(*[one(i) for i in range(n)])
+        finally:
+            close_all(gens)      # a failed or cancelled sibling leaves the others unread
         text, reason, nc, lps = res[0]
         body = final_fn(text, reason, len(ids), sum(r[2] for r in res),
                         lps if sp.logprobs is not None else None)
@@ -435,8 +446,12 @@ def build_app(engine: AsyncLLMEngine, tokenizer, served_name: str, max_model_len
                 finally:
                     for t in tasks:
                         t.cancel()
-            return StreamingResponse(sse(), media_type="text/event-stream")
-        res = await asyncio.gather(*[drain(k) for k in range(len(gens))])
+            return StreamingResponse(sse(), media_type="text/event-stream",
+                                     background=BackgroundTask(close_all, gens))
+        try:
+            res = await asyncio.gather(*[drain(k) for k in range(len(gens))])
+        finally:
+            close_all(gens)
         choices = []
         for k, (text, reason, _, lps) in enumerate(res):
             pre = prefixes[k // n]

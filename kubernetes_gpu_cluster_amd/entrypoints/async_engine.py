@@ -58,6 +58,64 @@ class DoneLog:
                 "requests": [r for r in list(self.log) if r[0] >= since]}
 
 
+class RequestStream:
+    """The output stream of one submitted request (``generate``).  Every exit that leaves
+    the request unfinished aborts it in the engine: ``aclose()`` / ``close()``, a
+    cancelled or failed consumer, and a stream that is dropped without ever being
+    iterated (a client that disconnects before the response starts, a sibling choice
+    whose task raised) -- the request was submitted eagerly, so without this it would
+    keep decoding to max_tokens in a batch slot nobody reads."""
+
+    def __init__(self, request_id: str, q: asyncio.Queue, on_close):
+        self.request_id = request_id
+        self._q = q
+        self._on_close = on_close           # on_close(request_id, abort: bool)
+        self._closed = False
+
+    def __aiter__(self):
+        return self
+
+    async def __anext__(self) -> RequestOutput:
+        if self._closed:
+            raise StopAsyncIteration
+        try:
+            item = await self._q.get()
+        except BaseException:
+            self.close()
+            raise
+        # coalesce: if the consumer fell behind, merge the queued steps into one output
+        # (token lists are cumulative), so a slow HTTP stream costs one event per wake-up
+        q = self._q
+        while not isinstance(item, BaseException) and not item.finished and not q.empty():
+            nxt = q.get_nowait()
+            if not isinstance(nxt, BaseException):
+                _merge(item, nxt)
+            item = nxt
+        if isinstance(item, BaseException):
+            self._end(abort=False)          # rejected, or the engine is gone
+            raise item
+        if item.finished:
+            self._end(abort=False)
+        return item
+
+    def _end(self, abort: bool) -> None:
+        if not self._closed:
+            self._closed = True
+            self._on_close(self.request_id, abort)
+
+    def close(self) -> None:
+        self._end(abort=True)
+
+    async def aclose(self) -> None:
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+
 def _deliver(items) -> None:
     for q, o in items:
         q.put_nowait(o)
@@ -146,31 +204,12 @@ class AsyncLLMEngine:
         self._streams[request_id] = (loop, q)
         self._new.put((request_id, prompt_ids, params, time.monotonic()))
         self._wake.set()
-        return self._stream(request_id, q)
+        return RequestStream(request_id, q, self._close_stream)
 
-    async def _stream(self, request_id: str, q: asyncio.Queue) -> AsyncIterator[RequestOutput]:
-        finished = False
-        try:
-            while True:
-                item = await q.get()
-                # coalesce: if the consumer fell behind, merge the queued steps into
-                # one output (token lists are cumulative), so a slow HTTP stream costs
-                # one event per wake-up instead of one per token
-                while not isinstance(item, BaseException) and not item.finished and not q.empty():
-                    nxt = q.get_nowait()
-                    if not isinstance(nxt, BaseException):
-                        _merge(item, nxt)
-                    item = nxt
-                if isinstance(item, BaseException):
-                    raise item
-                yield item
-                if item.finished:
-                    finished = True
-                    return
-        finally:
-            self._streams.pop(request_id, None)
-            if not finished:
-                self.abort(request_id)
+    def _close_stream(self, request_id: str, abort: bool) -> None:
+        self._streams.pop(request_id, None)
+        if abort:
+            self.abort(request_id)
 
     def abort(self, request_id: str) -> None:
         self._aborts.put(request_id)

@@ -39,7 +39,7 @@ from typing import AsyncIterator, Optional
 
 from ..engine.config import EngineConfig
 from ..engine.sequence import RequestOutput, SamplingParams
-from .async_engine import DoneLog, EngineDeadError, _deliver, _merge
+from .async_engine import DoneLog, EngineDeadError, RequestStream, _deliver
 
 log = logging.getLogger("kgc.engine_core")
 
@@ -313,28 +313,12 @@ class EngineCoreClient:
         q: asyncio.Queue = asyncio.Queue()
         self._streams[request_id] = _Stream(loop, q, list(prompt_ids))
         self._send(("add", request_id, list(prompt_ids), params, time.monotonic()))
-        return self._stream(request_id, q)
+        return RequestStream(request_id, q, self._close_stream)
 
-    async def _stream(self, request_id: str, q: asyncio.Queue) -> AsyncIterator[RequestOutput]:
-        finished = False
-        try:
-            while True:
-                item = await q.get()
-                while not isinstance(item, BaseException) and not item.finished and not q.empty():
-                    nxt = q.get_nowait()          # coalesce when the stream lags
-                    if not isinstance(nxt, BaseException):
-                        _merge(item, nxt)
-                    item = nxt
-                if isinstance(item, BaseException):
-                    raise item
-                yield item
-                if item.finished:
-                    finished = True
-                    return
-        finally:
-            self._streams.pop(request_id, None)
-            if not finished and self.is_alive:
-                self.abort(request_id)
+    def _close_stream(self, request_id: str, abort: bool) -> None:
+        self._streams.pop(request_id, None)
+        if abort and self.is_alive:
+            self.abort(request_id)
 
     def abort(self, request_id: str) -> None:
         try:

@@ -276,3 +276,49 @@ def test_stream_include_usage(client):
             u = json.loads(events[-2])
             assert u["choices"] == [] and u["usage"]["completion_tokens"] == 3 * n
             assert all("usage" not in json.loads(e) for e in events[:-2])
+
+
+@pytest.mark.parametrize("kind", ["thread", "core-process"])
+def test_unstarted_stream_aborts_request(kind):
+    """A request submitted eagerly whose output stream is dropped before the first chunk
+    is read (client gone before the response starts) is aborted in the engine instead of
+    decoding to max_tokens in a batch slot nobody reads."""
+    import asyncio
+    import gc
+    import time
+    from kubernetes_gpu_cluster_amd.engine.sequence import SamplingParams
+    cfg = _cfg()
+    if kind == "thread":
+        eng = AsyncLLMEngine(cfg)
+    else:
+        from kubernetes_gpu_cluster_amd.entrypoints.engine_core import EngineCoreClient
+        eng = EngineCoreClient(cfg)
+
+    async def submit_and_drop():
+        g = eng.generate([5, 6, 7], SamplingParams(max_tokens=200, ignore_eos=True), "drop-1")
+        del g
+        gc.collect()
+        # a finished request's stream closes without an abort
+        g2 = eng.generate([5, 6], SamplingParams(max_tokens=2, ignore_eos=True), "keep-1")
+        outs = [o async for o in g2]
+        assert outs[-1].finished and len(outs[-1].output_token_ids) == 2
+
+    try:
+        asyncio.run(submit_and_drop())
+        # wait until the engine goes idle (step count stable), then: the dropped request
+        # never finished (an unaborted one would have run to its 200 tokens)
+        last, stable = -1, 0
+        for _ in range(200):
+            st = asyncio.run(eng.engine_stats())
+            stable = stable + 1 if st["steps"] == last else 0
+            last = st["steps"]
+            if stable >= 5:
+                break
+            time.sleep(0.05)
+        assert stable >= 5, "engine never went idle"
+        assert all(r[3] != 200 for r in st["requests"]), st["requests"]
+        assert any(r[3] == 2 for r in st["requests"])
+        if kind == "thread":
+            assert "drop-1" not in eng.engine.seqs
+    finally:
+        eng.shutdown()

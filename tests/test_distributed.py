@@ -85,6 +85,29 @@ def test_tp2_matches_tp1(name):
     torch.testing.assert_close(got[1], ref, atol=1e-4, rtol=1e-4)   # identical on all ranks
 
 
+@pytest.mark.parametrize("name,tp", [("tiny-llama", 4), ("tiny-llama-gqa8", 4),
+                                     ("tiny-llama-gqa8", 8), ("tiny-llama-70b-shape", 8)])
+def test_tp4_tp8_match_tp1(name, tp):
+    """TP = 4 / 8 (BASELINE config 3 runs Llama-3-70B at TP = 8): logits == TP = 1 on
+    every rank, including kv heads replicated across ranks when num_kv_heads < tp
+    (tiny-llama at TP 4: 2 kv heads on 4 ranks; tiny-llama-gqa8 at TP 8: each of its 2 kv
+    heads on 4 ranks) and the 70B head layout (64 q / 8 kv: one kv head per rank)."""
+    ref = spawn(_logits, 1, name, 1, 1)[0]
+    got = spawn(_logits, tp, name, tp, 1)
+    assert sorted(got) == list(range(tp))
+    for r in range(tp):
+        torch.testing.assert_close(got[r], ref, atol=2e-4, rtol=2e-4)
+
+
+def test_moe_ep4_matches_tp1():
+    """Mixtral expert parallelism at EP = 4 (one expert per rank, attention at TP = 4
+    with replicated kv heads): logits == one process."""
+    ref = spawn(_logits, 1, "tiny-mixtral", 1, 1)[0]
+    got = spawn(_logits, 4, "tiny-mixtral", 4, 1, "ep")
+    for r in range(4):
+        torch.testing.assert_close(got[r], ref, atol=2e-4, rtol=2e-4)
+
+
 def test_pp2_matches_pp1():
     ref = spawn(_logits, 1, "tiny-llama", 1, 1)[0]
     got = spawn(_logits, 2, "tiny-llama", 1, 2)

@@ -350,3 +350,55 @@ def test_prefill_first_policy():
             temperature=0, max_tokens=6, ignore_eos=True))])
         llm.shutdown()
     assert outs[0] == outs[1]
+
+
+@pytest.mark.parametrize("k", [1, 3, 8])
+def test_prefill_first_bounded_deferral(k):
+    """--prefill-first under continuous arrivals (one new prompt every step, a free slot
+    always available): every running sequence still decodes at least once every k + 1
+    steps (--prefill-first-max-defer k), so TPOT stays bounded."""
+    sp = SamplingParams(temperature=0, max_tokens=1000, ignore_eos=True)
+    bm = BlockManager(4096, 16, 64, 64, enable_prefix_caching=False)
+    sc = Scheduler(bm, 64, 64, 1024, True, prefill_first=True, max_defer_steps=k)
+    last_decode: dict[str, int] = {}
+    worst = 0
+    for step in range(40):
+        sc.add(Sequence(f"r{step}", list(range(3, 19)), sp, None, 1024))
+        b = sc.schedule()
+        for s, n in b.prefills:
+            s.num_computed += n
+            if s.num_computed == s.num_tokens:
+                s.output_token_ids.append(7)
+                last_decode[s.request_id] = step
+        for s in b.decodes:
+            s.num_computed += 1
+            s.output_token_ids.append(7)
+            last_decode[s.request_id] = step
+        for s in sc.running:
+            if s.request_id in last_decode:
+                worst = max(worst, step - last_decode[s.request_id])
+    assert worst <= k + 1, worst
+    assert len(sc.running) > 10
+
+
+def test_prefill_first_gap_bound(monkeypatch):
+    """--prefill-first-max-gap-ms: a running stream that has waited longer than the gap
+    is decoded in the next step even while prompts keep arriving."""
+    from kubernetes_gpu_cluster_amd.engine import scheduler as sched_mod
+    sp = SamplingParams(temperature=0, max_tokens=100, ignore_eos=True)
+    bm = BlockManager(256, 16, 8, 16, enable_prefix_caching=False)
+    sc = Scheduler(bm, 8, 32, 256, True, prefill_first=True, max_defer_steps=100,
+                   max_decode_gap_ms=50)
+    clock = [1000.0]
+    monkeypatch.setattr(sched_mod.time, "monotonic", lambda: clock[0])
+    a = Sequence("a", list(range(3, 19)), sp, None, 256)
+    sc.add(a)
+    sc.schedule()
+    a.num_computed += 16
+    a.output_token_ids.append(7)
+    a.last_token_time = clock[0]
+    sc.add(Sequence("b", list(range(3, 19)), sp, None, 256))
+    assert not sc.schedule().decodes            # within the gap: a sits out
+    clock[0] += 0.2
+    sc.add(Sequence("c", list(range(3, 19)), sp, None, 256))
+    assert [s.request_id for s in sc.schedule().decodes] == ["a"]
