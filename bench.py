@@ -46,6 +46,16 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 BASELINE_METRIC = "output tokens/sec + p50 TTFT, Llama-3-8B K8s service at 1/2/4/8 MI355X"
+_METRIC_NAMES = {"llama-3-8b": "Llama-3-8B", "llama-3-70b": "Llama-3-70B",
+                 "mixtral-8x7b": "Mixtral-8x7B"}
+
+
+def metric_name(model: str) -> str:
+    """BASELINE.json's metric string for its model; the same shape, naming the model that
+    actually ran, for every other one (a 70B run is never labelled Llama-3-8B)."""
+    if model == "llama-3-8b":
+        return BASELINE_METRIC
+    return BASELINE_METRIC.replace("Llama-3-8B", _METRIC_NAMES.get(model, model))
 
 
 def parse():
@@ -80,6 +90,9 @@ def parse():
     ap.add_argument("--api-server-count", type=int, default=0,
                     help="service mode: API processes per engine (0: server default)")
     ap.add_argument("--startup-timeout", type=float, default=1800)
+    ap.add_argument("--router-workers", type=int, default=0,
+                    help="service mode: router processes in front of all replicas "
+                         "(0: one per replica, at most 16)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: run the same harness on the fp32 CPU path (gloo) -- a test "
                          "harness for the multi-rank logic, not a measurement")
@@ -208,7 +221,7 @@ def main_engine(args):
         value = toks / elapsed
         p50_ttft = statistics.median(ttfts) * 1e3 if ttfts else None
         out = {
-            "metric": BASELINE_METRIC, "value": round(value, 2), "unit": "output_tokens/s",
+            "metric": metric_name(args.model), "value": round(value, 2), "unit": "output_tokens/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
@@ -313,18 +326,41 @@ def main_service(args):
     api_url = url = None
     res_all, windows, eng = [], [], {}
     elapsed = 0.0
+    router = None
+    cpu0 = 0.0
     try:
         if leader:
-            api_port, router_port = _free_port(local_rank, 0), _free_port(local_rank, 1)
+            api_port = _free_port(local_rank, 0)
             api_url = f"http://127.0.0.1:{api_port}"
-            url = f"http://127.0.0.1:{router_port}"
             procs.append(sc.start_api_server(args.model, api_port,
                                              _server_devices(local_rank, tp, cpu),
                                              _engine_args(args, cpu)))
-            procs.append(sc.start_router(router_port, [api_url]))
-            _note(f"rank {rank}: API server {api_url} (tp {tp}), router {url}; waiting for health")
-            asyncio.run(sc.wait_healthy([api_url, url], args.startup_timeout, procs, _note))
-            _note(f"rank {rank}: service is up")
+            _note(f"rank {rank}: API server {api_url} (tp {tp}); waiting for health")
+            asyncio.run(sc.wait_healthy([api_url], args.startup_timeout, procs, _note))
+        # ONE service endpoint for the whole job, as the reference deploys DP:
+        # replicaCount engine pods behind one vllm-router-service
+        # (/root/reference/values-01-minimal-example2.yaml:10,23-49).  Rank 0 runs the
+        # router over every replica's API server; every replica's client load goes
+        # through it.
+        backends = [api_url]
+        if world > 1:
+            allu = [None] * world
+            dist.all_gather_object(allu, api_url)
+            backends = [u for u in allu if u]
+        if rank == 0:
+            workers = args.router_workers or max(1, min(16, len(backends)))
+            router_port = _free_port(local_rank, 1)
+            url = f"http://127.0.0.1:{router_port}"
+            router = sc.start_router(router_port, backends, workers=workers)
+            procs.append(router)
+            _note(f"router {url}: {workers} worker process(es) over {len(backends)} "
+                  f"replica(s); waiting for health")
+            asyncio.run(sc.wait_healthy([url], args.startup_timeout, procs, _note))
+            _note("service is up")
+        if world > 1:
+            box = [url]
+            dist.broadcast_object_list(box, src=0)
+            url = box[0]
 
         def make_prompts(n: int, base_seed: int):
             # generated before any timer starts (~0.1 s of Python per 256 x 512 wave)
@@ -349,17 +385,22 @@ def main_service(args):
                 if world > 1:
                     dist.barrier()
                 t0 = time.monotonic()
+                c0 = sc.cpu_seconds(router.pid) if router is not None else 0.0
                 for prompts in timed:
                     out.append(await sc.run_wave(s, url, args.model, prompts, args.output_len,
                                                  temperature=args.temperature))
                 if world > 1:
                     dist.barrier()
-                return out, t0, time.monotonic() - t0
+                t1 = time.monotonic()
+                c1 = sc.cpu_seconds(router.pid) if router is not None else 0.0
+                return out, t0, t1 - t0, c1 - c0
 
-        waves_out, t0, elapsed = asyncio.run(run_all())
+        waves_out, t0, elapsed, router_cpu = asyncio.run(run_all())
         for r, lo, hi in waves_out:
             res_all += r
-            windows.append((lo, hi))
+        # one window over all timed waves: behind the shared router a replica also serves
+        # other ranks' requests, whose waves need not line up with this rank's
+        windows.append((t0, t0 + elapsed))
         if leader:
             with urllib.request.urlopen(f"{api_url}/kgc/engine_stats?since={t0 - 1.0}", timeout=30) as f:
                 st = json.loads(f.read())
@@ -394,7 +435,7 @@ def main_service(args):
         e_value = e_tok / e_span if e_span > 0 else None
         med = lambda xs: round(statistics.median(xs) * 1e3, 3) if xs else None  # noqa: E731
         out = {
-            "metric": BASELINE_METRIC, "value": round(value, 2), "unit": "output_tokens/s",
+            "metric": metric_name(args.model), "value": round(value, 2), "unit": "output_tokens/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
@@ -410,6 +451,9 @@ def main_service(args):
             "engine_output_tokens": e_tok,
             "engine_steps": sum(e.get("steps", 0) for e in engs),
             "service_vs_engine": round(value / e_value, 4) if e_value else None,
+            # router CPU-seconds per wall second over the timed waves (all its workers)
+            "router_cpu_util": round(router_cpu / elapsed, 3) if elapsed > 0 else None,
+            "router_workers": args.router_workers or max(1, min(16, replicas)),
             "config": {"model": args.model, "global_batch": args.num_prompts * replicas,
                        "seq_len": args.input_len + args.output_len, "input_len": args.input_len,
                        "output_len": args.output_len,
@@ -418,7 +462,8 @@ def main_service(args):
                        "max_num_batched_tokens": args.max_num_batched_tokens,
                        "cuda_graphs": not args.enforce_eager,
                        "scheduling": "prefill-first" if args.prefill_first else "decode-first",
-                       "endpoint": "router -> /v1/completions (stream)"},
+                       "endpoint": f"one router ({replicas} replica(s)) -> /v1/completions "
+                                   f"(stream)"},
         }
         line = json.dumps(out)
         print(line, flush=True)

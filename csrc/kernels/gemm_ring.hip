@@ -83,7 +83,8 @@ __device__ __forceinline__ int64_t rg_silu_row(int64_t p, int I) {
 template <int BM, int BN, int WM, int WN, int LW, int NS, int WAUX, int EPI>
 __global__ __launch_bounds__((WM * WN + LW) * 64, 1) void ring_gemm_kernel(
     void* __restrict__ Cv, const bf16* __restrict__ X, const bf16* __restrict__ Wp, int M,
-    int N, int K, int64_t ldx, int S, int G, int MB, int64_t slice_stride, int xmap, int wt) {
+    int N, int K, int64_t ldx, int S, int G, int MB, int64_t slice_stride, int xmap, int wt,
+    int abl) {
   constexpr int CW = WM * WN;
   constexpr int NI = LW > 0 ? LW : CW;            // waves issuing DMAs
   constexpr int D = NS - 1;                       // K-steps in flight
@@ -160,7 +161,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, 1) void ring_gemm_kernel(
     const int kb = kb0 + st;
 #pragma unroll
     for (int t = 0; t < LHI; ++t) {
-      if (t < nl) {
+      if (t < nl && !(abl & (isb[t] ? 4 : 2))) {
         // weights: WAUX = 2 (nt) streams them past L2 (each weight byte is read by ONE
         // workgroup when BM covers all rows); activations keep the default policy
         if (isb[t]) rg_glds16<WAUX>(src[t] + kb * sstep[t], base + ldso[t]);
@@ -195,7 +196,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, 1) void ring_gemm_kernel(
     __builtin_amdgcn_s_barrier();
     // every wave is past the reads of step it - 1, whose slot step it + D reuses
     if (issuer && it + D < nk) issue(it + D);
-    if (!consumer) continue;
+    if (!consumer || (abl & 1)) continue;
     const char* sa = lds + (it % NS) * SLOT;
     const char* sb = sa + BM * RG_ROWB;
 #pragma unroll
@@ -219,42 +220,61 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, 1) void ring_gemm_kernel(
     }
   }
 
-  // ---- epilogue: lane holds C[4*fq + e][fr] of every 16x16 tile
-  if (!consumer) return;
-  const int64_t col0 = (int64_t)nb * BN + wn * (BN / WN) + fr;
+  // ---- epilogue.  Lane (fq, fr) holds C[4*fq + e][fr] of every 16x16 tile: stored
+  // straight from there a wave instruction writes four 32-64 B row pieces, and the
+  // per-launch cost of those scattered 2 / 4-byte stores measured 7-20 us (the loop
+  // without DMAs or MFMAs, KGC_RING_ABLATE=7: o 9.2 us, gate_up 24 us).  The tile goes
+  // through LDS instead (the ring is free now) and every wave, loaders included,
+  // writes whole rows with 16-B stores (write-through for the fp32 K-slices).
+  constexpr int OCOLS = EPI == RG_SILU ? BN / 2 : BN;          // output columns of the tile
+  constexpr int EB = EPI == RG_PARTIAL ? 4 : 2;                  // output element bytes
+  constexpr int ROWB = OCOLS * EB + 16;                          // padded staging row
+  constexpr int CPR = OCOLS * EB / 16;                           // 16-B chunks per row
+  static_assert(OCOLS * EB % 16 == 0, "16-B rows");
+  static_assert(BM * ROWB <= NS * SLOT, "staging tile fits in the ring");
+  __builtin_amdgcn_s_barrier();                 // every wave is done reading the ring
+  if (consumer) {
 #pragma unroll
-  for (int i = 0; i < MT; ++i) {
+    for (int i = 0; i < MT; ++i) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int row = m0 + wm * (BM / WM) + i * 16 + fq * 4 + e;
-      if constexpr (EPI == RG_SILU) {
-        // the up half of each 16-column group sits in lanes fr + 8 (all lanes shuffle)
-        const int I = N >> 1;
+      for (int e = 0; e < 4; ++e) {
+        const int rt = wm * (BM / WM) + i * 16 + fq * 4 + e;
+        char* srow = lds + rt * ROWB;
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
-          const float g = acc[i][n][e];
-          const float u = __shfl_xor(g, 8, 64);
-          if (row < M && fr < 8) {
-            const int64_t oc = ((col0 + n * 16) >> 4) * 8 + fr;
-            reinterpret_cast<bf16*>(Cv)[(int64_t)row * I + oc] = (bf16)(rg_silu(g) * u);
+          const int ct = wn * (BN / WN) + n * 16 + fr;
+          if constexpr (EPI == RG_PARTIAL) {
+            *reinterpret_cast<float*>(srow + ct * 4) = acc[i][n][e];
+          } else if constexpr (EPI == RG_OUT) {
+            *reinterpret_cast<bf16*>(srow + ct * 2) = (bf16)acc[i][n][e];
+          } else {
+            // the up half of each 16-column group sits in lanes fr + 8 (all lanes shuffle)
+            const float g = acc[i][n][e];
+            const float u = __shfl_xor(g, 8, 64);
+            if (fr < 8)
+              *reinterpret_cast<bf16*>(srow + (((ct >> 4) << 3) + fr) * 2) =
+                  (bf16)(rg_silu(g) * u);
           }
-        }
-      } else {
-        if (row >= M) continue;
-        if constexpr (EPI == RG_PARTIAL) {
-          float* cp = reinterpret_cast<float*>(Cv) + z * slice_stride + (int64_t)row * N + col0;
-#pragma unroll
-          for (int n = 0; n < NT; ++n) {
-            if (wt) __hip_atomic_store(cp + n * 16, acc[i][n][e], __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            else cp[n * 16] = acc[i][n][e];
-          }
-        } else {
-          bf16* cp = reinterpret_cast<bf16*>(Cv) + (int64_t)row * N + col0;
-#pragma unroll
-          for (int n = 0; n < NT; ++n) cp[n * 16] = (bf16)acc[i][n][e];
         }
       }
+    }
+  }
+  __syncthreads();
+  constexpr int NTH = (CW + LW) * 64;
+  const int ldc = EPI == RG_SILU ? N / 2 : N;
+  for (int c = tid; c < BM * CPR; c += NTH) {
+    const int r = c / CPR, j = c - (c / CPR) * CPR;
+    const int grow = m0 + r;
+    if (grow >= M) continue;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(lds + r * ROWB + j * 16);
+    if constexpr (EPI == RG_PARTIAL) {
+      float* gp = reinterpret_cast<float*>(Cv) + z * slice_stride + (int64_t)grow * N +
+                  (int64_t)nb * BN + j * 4;
+      if (wt) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(gp), "v"(v) : "memory");
+      else *reinterpret_cast<u32x4*>(gp) = v;
+    } else {
+      bf16* gp = reinterpret_cast<bf16*>(Cv) + (int64_t)grow * ldc + (int64_t)nb * OCOLS + j * 8;
+      *reinterpret_cast<u32x4*>(gp) = v;
     }
   }
 }
@@ -308,10 +328,16 @@ void ring_launch(int epi, void* Cp, const void* X, const void* W, int M, int N, 
     const char* e = getenv("KGC_PARTIAL_WT");
     return e ? atoi(e) : 1;
   }();
+  // profiling only (tools/ring_bench.py --ablate): bit 0 drops the MFMAs, bit 1 the
+  // activation DMAs, bit 2 the weight DMAs (waits unchanged: a lower bound)
+  static const int abl = [] {
+    const char* e = getenv("KGC_RING_ABLATE");
+    return e ? atoi(e) : 0;
+  }();
 #define RG_LAUNCH(E)                                                                        \
   ring_gemm_kernel<c.bm, c.bn, c.wm, c.wn, c.lw, c.ns, c.waux, E>                           \
       <<<grid, (c.wm * c.wn + c.lw) * 64, 0, s>>>(Cp, (const bf16*)X, (const bf16*)W, M, N, \
-                                                  K, ldx, S, G, MB, ss, xm, wt)
+                                                  K, ldx, S, G, MB, ss, xm, wt, abl)
   if (epi == RG_PARTIAL) RG_LAUNCH(RG_PARTIAL);
   else if (epi == RG_OUT) RG_LAUNCH(RG_OUT);
   else RG_LAUNCH(RG_SILU);

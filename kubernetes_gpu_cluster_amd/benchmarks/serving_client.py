@@ -14,6 +14,7 @@ touches the GPU.
 from __future__ import annotations
 
 import asyncio
+import json
 import os
 import random
 import signal
@@ -51,16 +52,31 @@ class Result:
 
 async def one_request(session: aiohttp.ClientSession, url: str, model: str, prompt,
                       out_len: int, temperature: float = 1.0) -> Result:
+    """One streamed completion.  Tokens are counted from what arrived: the
+    ``stream_options.include_usage`` event (completion_tokens) that the server sends
+    before ``[DONE]``.  A stream cut short (no usage event or no [DONE]) is a failed
+    request that credits no tokens -- never ``max_tokens`` on faith."""
     body = {"model": model, "prompt": prompt, "max_tokens": out_len, "ignore_eos": True,
-            "stream": True, "temperature": temperature}
+            "stream": True, "temperature": temperature,
+            "stream_options": {"include_usage": True}}
     t0 = time.monotonic()
     ttft, last, itl = None, t0, []
+    ntok, done = None, False
     async with session.post(url + "/v1/completions", json=body) as r:
         if r.status != 200:
             await r.read()
             return Result(False, r.status)
         async for raw in r.content:
-            if not raw.startswith(b"data:") or raw.startswith(b"data: [DONE]"):
+            if not raw.startswith(b"data:"):
+                continue
+            if raw.startswith(b"data: [DONE]"):
+                done = True
+                continue
+            if b'"usage"' in raw and b'"choices": []' in raw:
+                try:
+                    ntok = int(json.loads(raw[5:])["usage"]["completion_tokens"])
+                except (ValueError, KeyError, TypeError):
+                    pass
                 continue
             now = time.monotonic()
             if ttft is None:
@@ -68,7 +84,8 @@ async def one_request(session: aiohttp.ClientSession, url: str, model: str, prom
             else:
                 itl.append(now - last)
             last = now
-    return Result(ttft is not None, 200, ttft, last - t0, out_len, itl)
+    ok = ttft is not None and done and ntok is not None
+    return Result(ok, 200, ttft, last - t0, ntok if ok else 0, itl)
 
 
 async def run_wave(session, url: str, model: str, prompts, out_len: int,
@@ -146,9 +163,9 @@ def start_api_server(model: str, port: int, devices: Optional[str], engine_args:
                             stderr=subprocess.STDOUT if log is not None else None)
 
 
-def start_router(port: int, backends: list[str], log=None) -> subprocess.Popen:
+def start_router(port: int, backends: list[str], log=None, workers: int = 1) -> subprocess.Popen:
     cmd = [sys.executable, "-m", "kubernetes_gpu_cluster_amd.router.router", "--host", "127.0.0.1",
-           "--port", str(port), "--backends", ",".join(backends)]
+           "--port", str(port), "--backends", ",".join(backends), "--workers", str(workers)]
     return subprocess.Popen(cmd, env=_env({}), start_new_session=True, stdout=log,
                             stderr=subprocess.STDOUT if log is not None else None)
 
@@ -176,6 +193,23 @@ async def wait_healthy(urls: list[str], timeout_s: float, procs=(), progress=Non
                     progress(f"waiting for {u}/health ({time.monotonic() - deadline + timeout_s:.0f}s)")
                     last_note = time.monotonic()
                 await asyncio.sleep(1.0)
+
+
+def cpu_seconds(pid: int) -> float:
+    """user + system CPU time of a process and all its descendants (router workers)."""
+    import psutil
+    try:
+        root = psutil.Process(pid)
+        tot = 0.0
+        for p in [root] + root.children(recursive=True):
+            try:
+                t = p.cpu_times()
+                tot += t.user + t.system
+            except psutil.NoSuchProcess:
+                pass
+        return tot
+    except psutil.NoSuchProcess:
+        return 0.0
 
 
 def stop(procs: list[subprocess.Popen], grace: float = 60.0) -> list[Optional[int]]:

@@ -45,6 +45,34 @@ log = logging.getLogger("kgc.engine_core")
 
 
 # ---------------------------------------------------------------------------- core process
+class _Intake(threading.Thread):
+    """Receives the frontends' messages while the engine steps: a burst of requests is
+    unpickled and queued during the GPU step, not after it, so the core loop admits
+    everything that arrived at the next step boundary with no receive work of its own
+    (the loop only drains this queue).  Connections are only READ here; every send
+    stays on the core loop's thread."""
+
+    def __init__(self, conns: list):
+        super().__init__(name="kgc-core-intake", daemon=True)
+        self.conns = list(conns)
+        self.q: collections.deque = collections.deque()
+        self.wake = threading.Event()
+        self.stop = False
+
+    def run(self) -> None:
+        while self.conns and not self.stop:
+            for c in mp_wait(self.conns, 0.1):
+                try:
+                    msg = c.recv()
+                except (EOFError, OSError):
+                    self.conns.remove(c)
+                    msg = None              # the frontend went away
+                self.q.append((c, msg, time.monotonic()))
+                self.wake.set()
+        self.q.append((None, None, time.monotonic()))   # no frontend left
+        self.wake.set()
+
+
 def _make_engine(cfg: EngineConfig):
     if os.environ.get("KGC_FAKE_ENGINE"):
         # GPU-free timing model of the engine (engine/fake.py): load-tests the
@@ -100,45 +128,50 @@ def _core_main(cfg: EngineConfig, conn, listen: Optional[tuple] = None) -> None:
     # for weeks)
     adds: collections.deque = collections.deque(maxlen=1 << 16)
     done = DoneLog()
+    intake = _Intake(conns)
+    intake.start()
     try:
         running = True
         while running and conns:
             idle = not eng.has_unfinished()
             st["iters"] += 1
             ti = time.perf_counter()
-            # drain every inbox; block briefly only when there is nothing to run
-            ready = mp_wait(conns, 0.05 if idle else 0)
-            while ready and running:
-                for c in ready:
-                    try:
-                        msg = c.recv()
-                    except (EOFError, OSError):
+            # drain what the intake thread queued; block briefly only when idle
+            if idle and not intake.q:
+                intake.wake.wait(0.05)
+            intake.wake.clear()
+            while intake.q and running:
+                c, msg, t_recv = intake.q.popleft()
+                if c is None:
+                    conns.clear()
+                    break
+                if msg is None:
+                    if c in conns:
                         conns.remove(c)        # a frontend went away: drop its requests
-                        for rid in [r for r, oc in owner.items() if oc is c]:
-                            owner.pop(rid)
-                            eng.abort(rid)
-                        continue
-                    kind = msg[0]
-                    if kind == "add":
-                        _, rid, ids, params, arrival = msg
-                        adds.append((time.monotonic(), arrival))
-                        try:
-                            eng.add_request(ids, params, request_id=rid, arrival_time=arrival)
-                            owner[rid] = c
-                        except Exception as e:  # noqa: BLE001 - reported to that request
-                            c.send(("reject", rid, f"{type(e).__name__}: {e}"))
-                    elif kind == "abort":
-                        owner.pop(msg[1], None)
-                        eng.abort(msg[1])
-                    elif kind == "metrics":
-                        from prometheus_client import generate_latest
-                        c.send(("metrics", msg[1], generate_latest(eng.metrics.registry).decode()))
-                    elif kind == "stats":
-                        c.send(("stats", msg[1], done.snapshot(msg[2])))
-                    elif kind == "shutdown":
-                        running = False
-                        break
-                ready = mp_wait(conns, 0) if running and conns else []
+                    for rid in [r for r, oc in owner.items() if oc is c]:
+                        owner.pop(rid)
+                        eng.abort(rid)
+                    continue
+                kind = msg[0]
+                if kind == "add":
+                    _, rid, ids, params, arrival = msg
+                    adds.append((t_recv, arrival))
+                    try:
+                        eng.add_request(ids, params, request_id=rid, arrival_time=arrival)
+                        owner[rid] = c
+                    except Exception as e:  # noqa: BLE001 - reported to that request
+                        c.send(("reject", rid, f"{type(e).__name__}: {e}"))
+                elif kind == "abort":
+                    owner.pop(msg[1], None)
+                    eng.abort(msg[1])
+                elif kind == "metrics":
+                    from prometheus_client import generate_latest
+                    c.send(("metrics", msg[1], generate_latest(eng.metrics.registry).decode()))
+                elif kind == "stats":
+                    c.send(("stats", msg[1], done.snapshot(msg[2])))
+                elif kind == "shutdown":
+                    running = False
+                    break
             if not idle:
                 st["inbox_s"] += time.perf_counter() - ti
             if running and eng.has_unfinished():
@@ -179,6 +212,7 @@ def _core_main(cfg: EngineConfig, conn, listen: Optional[tuple] = None) -> None:
         t.start()
         t.join(10)
         os._exit(1)
+    intake.stop = True
     log.info("core loop: %d iterations, %d engine steps; host time: step %.2f s, output "
              "fan-out %.2f s, inbox %.2f s", st["iters"], st["steps"], st["step_s"],
              st["send_s"], st["inbox_s"])

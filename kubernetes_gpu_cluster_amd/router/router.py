@@ -13,6 +13,11 @@ router behind ``svc/vllm-router-service`` port 80; ``old_README.md:1175,1473-147
   connection error or 5xx before any byte was relayed is retried on another
   backend (failover); SSE streams are relayed chunk by chunk.
 * ``/v1/models`` (union), ``/health``, ``/metrics`` (router Prometheus metrics).
+* ``--workers K``: K router processes accept on ONE port (SO_REUSEPORT) and share the
+  backends' in-flight counts through shared memory (each worker owns one row of a
+  [K x slots] table and least-outstanding reads the column sums), so the DP replicas
+  behind one service endpoint stay balanced while the SSE relaying -- one event per
+  token per stream -- is spread over K cores instead of saturating one.
 """
 from __future__ import annotations
 
@@ -50,12 +55,44 @@ class Backend:
         return f"Backend({self.url}, healthy={self.healthy}, out={self.outstanding})"
 
 
+class SharedOutstanding:
+    """In-flight requests per backend, shared by the worker processes of one router:
+    a RawArray of [workers x slots] int64, row w written only by worker w (no lock, no
+    lost updates); a backend's global count is its column sum.  Backends map to slots
+    by URL hash (a collision only merges two backends' counts)."""
+
+    SLOTS = 1024
+
+    def __init__(self, workers: int):
+        import multiprocessing as mp
+        self.workers = workers
+        self.arr = mp.RawArray("q", workers * self.SLOTS)
+        # pick + reserve is one critical section across the workers: a burst of
+        # simultaneous arrivals is spread exactly evenly (a DP replica that gets even a
+        # few requests over its max_num_seqs serves them as a second, serial wave)
+        self.lock = mp.Lock()
+        self.row = 0
+
+    @classmethod
+    def slot(cls, url: str) -> int:
+        return int.from_bytes(hashlib.blake2b(url.encode(), digest_size=4).digest(), "big") % cls.SLOTS
+
+    def add(self, url: str, d: int) -> None:
+        self.arr[self.row * self.SLOTS + self.slot(url)] += d
+
+    def total(self, url: str) -> int:
+        j = self.slot(url)
+        return sum(self.arr[w * self.SLOTS + j] for w in range(self.workers))
+
+
 class Router:
     def __init__(self, backends: list[str], policy: str = "least-outstanding",
                  health_interval: float = 5.0, fail_threshold: int = 2,
                  k8s_selector: Optional[str] = None, k8s_namespace: Optional[str] = None,
                  k8s_port: int = 8000, dns_service: Optional[str] = None, max_retries: int = 2,
-                 request_timeout: float = 3600.0, backend_api_key: Optional[str] = None):
+                 request_timeout: float = 3600.0, backend_api_key: Optional[str] = None,
+                 shared: Optional[SharedOutstanding] = None):
+        self.shared = shared
         # engines started with --api-key: the router's own /v1/models polls carry the key
         # (client requests are proxied with their own Authorization header)
         self._poll_headers = ({"Authorization": f"Bearer {backend_api_key}"}
@@ -175,15 +212,35 @@ class Router:
 
     def pick(self, model: Optional[str], session_key: Optional[str] = None,
              exclude: set = frozenset()) -> Optional[Backend]:
+        """Choose a backend and count the request against it (``release`` undoes it)."""
         cs = [b for b in self.candidates(model) if b.url not in exclude]
         if not cs:
             return None
+        if self.shared is None:
+            b = self._choose(cs, session_key, {b.url: b.outstanding for b in cs})
+        else:
+            with self.shared.lock:
+                b = self._choose(cs, session_key, None)
+                self.shared.add(b.url, 1)
+        b.outstanding += 1
+        self.m_out.labels(b.url).set(b.outstanding)
+        return b
+
+    def release(self, b: Backend) -> None:
+        b.outstanding -= 1
+        if self.shared is not None:
+            self.shared.add(b.url, -1)
+        self.m_out.labels(b.url).set(b.outstanding)
+
+    def _choose(self, cs: list[Backend], session_key: Optional[str], load) -> Backend:
         if self.policy == "round-robin":
             return cs[next(self._rr) % len(cs)]
         if self.policy == "session" and session_key:
             return consistent_pick(cs, session_key)
-        lo = min(b.outstanding for b in cs)
-        ties = [b for b in cs if b.outstanding == lo]
+        if load is None:
+            load = {b.url: self.shared.total(b.url) for b in cs}
+        lo = min(load.values())
+        ties = [b for b in cs if load[b.url] == lo]
         return ties[next(self._rr) % len(ties)]
 
     # ------------------------------------------------------------------ proxy
@@ -204,8 +261,6 @@ class Router:
                 return web.json_response({"error": "no healthy backend" + (f" for model {model}" if model else "")},
                                          status=503)
             tried.add(b.url)
-            b.outstanding += 1
-            self.m_out.labels(b.url).set(b.outstanding)
             resp: Optional[web.StreamResponse] = None
             try:
                 hdrs = {k: v for k, v in request.headers.items()
@@ -237,8 +292,7 @@ class Router:
                 self.m_retry.inc()
                 log.warning("backend %s failed (%s); failing over", b.url, e)
             finally:
-                b.outstanding -= 1
-                self.m_out.labels(b.url).set(b.outstanding)
+                self.release(b)
         return web.json_response({"error": "all backends failed"}, status=502)
 
     async def models(self, request: web.Request) -> web.Response:
@@ -314,15 +368,63 @@ def main(argv=None):
     p.add_argument("--backend-api-key", default=os.environ.get("VLLM_API_KEY"),
                    help="bearer key for the router's own /v1/models polls of engines that "
                         "run with --api-key (env VLLM_API_KEY)")
+    p.add_argument("--workers", type=int, default=1,
+                   help="router processes sharing the port (SO_REUSEPORT) and the backends' "
+                        "in-flight counts; 0 = one per 2 CPUs, at most 8")
     a = p.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
     if not a.access_log:
         logging.getLogger("aiohttp.access").setLevel(logging.WARNING)
-    r = Router([u for u in a.backends.split(",") if u], a.policy, a.health_interval,
-               k8s_selector=a.k8s_label_selector, k8s_namespace=a.k8s_namespace,
-               k8s_port=a.k8s_port, dns_service=a.dns_service,
-               backend_api_key=a.backend_api_key)
-    web.run_app(r.app(), host=a.host, port=a.port)
+    workers = a.workers if a.workers > 0 else max(1, min(8, (os.cpu_count() or 2) // 2))
+
+    def serve(shared: Optional[SharedOutstanding]):
+        r = Router([u for u in a.backends.split(",") if u], a.policy, a.health_interval,
+                   k8s_selector=a.k8s_label_selector, k8s_namespace=a.k8s_namespace,
+                   k8s_port=a.k8s_port, dns_service=a.dns_service,
+                   backend_api_key=a.backend_api_key, shared=shared)
+        web.run_app(r.app(), host=a.host, port=a.port, reuse_port=workers > 1,
+                    print=None if workers > 1 else print)
+
+    if workers == 1:
+        serve(None)
+        return
+    shared = SharedOutstanding(workers)
+    run_workers(workers, shared, serve)
+
+
+def run_workers(workers: int, shared: SharedOutstanding, serve) -> None:
+    """Fork ``workers`` processes that each run ``serve(shared)`` on the same port; the
+    parent waits, forwards SIGTERM / SIGINT, and exits non-zero if any worker dies."""
+    import signal
+    pids = []
+    for w in range(workers):
+        pid = os.fork()
+        if pid == 0:
+            shared.row = w
+            try:
+                serve(shared)
+            finally:
+                os._exit(0)
+        pids.append(pid)
+
+    def stop(signum, frame):
+        for pid in pids:
+            try:
+                os.kill(pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+    signal.signal(signal.SIGTERM, stop)
+    signal.signal(signal.SIGINT, stop)
+    rc = 0
+    for _ in pids:
+        try:
+            _, status = os.wait()
+        except ChildProcessError:
+            break
+        if os.waitstatus_to_exitcode(status) not in (0, -signal.SIGTERM):
+            rc = 1
+            stop(None, None)
+    raise SystemExit(rc)
 
 
 if __name__ == "__main__":

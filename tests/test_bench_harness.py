@@ -64,5 +64,60 @@ def test_bench_two_ranks(tp):
     if tp == 1:
         assert j["config"]["parallelism"] == "dp2" and j["config"]["global_batch"] == 8
         assert j["engine_steps"] > 0
+        # ONE service endpoint: rank 0's router (a worker per replica) over both replicas
+        assert j["config"]["endpoint"].startswith("one router (2 replica(s))")
+        assert j["router_workers"] == 2 and j["router_cpu_util"] is not None
+        assert j["engine_output_tokens"] == 8 * 4
     else:
         assert j["config"]["parallelism"] == "tp2" and j["config"]["global_batch"] == 4
+
+
+def test_client_counts_received_tokens_not_max_tokens():
+    """The load generator credits the tokens the server reports in the include_usage
+    event before [DONE]; a stream cut short is a failed request worth 0 tokens, so a
+    truncating server makes the measured value drop instead of being credited
+    max_tokens per request."""
+    import asyncio
+    import json as _json
+    from aiohttp import web
+    from aiohttp.test_utils import TestServer
+    from kubernetes_gpu_cluster_amd.benchmarks import serving_client as sc
+
+    def app(truncate_every: int):
+        state = {"n": 0}
+
+        async def comp(r):
+            body = await r.json()
+            assert body["stream_options"] == {"include_usage": True}
+            state["n"] += 1
+            cut = truncate_every and state["n"] % truncate_every == 0
+            resp = web.StreamResponse(headers={"content-type": "text/event-stream"})
+            await resp.prepare(r)
+            n = body["max_tokens"]
+            for i in range(n if not cut else 2):
+                await resp.write(f'data: {{"choices": [{{"text": "t{i}"}}]}}\n\n'.encode())
+            if not cut:
+                u = {"choices": [], "usage": {"prompt_tokens": 3, "completion_tokens": n}}
+                await resp.write(f"data: {_json.dumps(u)}\n\ndata: [DONE]\n\n".encode())
+            await resp.write_eof()
+            return resp
+        a = web.Application()
+        a.router.add_post("/v1/completions", comp)
+        return a
+
+    async def run(truncate_every):
+        srv = TestServer(app(truncate_every))
+        await srv.start_server()
+        try:
+            async with sc.new_session() as s:
+                res, t0, t1 = await sc.run_wave(s, str(srv.make_url("")).rstrip("/"), "m",
+                                                [[5, 6, 7]] * 8, 6)
+        finally:
+            await srv.close()
+        return res
+
+    full = asyncio.run(run(0))
+    assert all(r.ok and r.tokens == 6 for r in full)
+    cut = asyncio.run(run(2))
+    assert sum(r.ok for r in cut) == 4 and sum(r.tokens for r in cut) == 4 * 6
+    assert sc.summarize(cut, 1.0)["value"] < sc.summarize(full, 1.0)["value"]

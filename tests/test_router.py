@@ -162,3 +162,88 @@ async def _concurrency_scenario(n=300):
 
 def test_router_has_no_connection_cap():
     asyncio.run(_concurrency_scenario())
+
+
+async def _multiworker_scenario(nbe=4, per=64, workers=3):
+    """``--workers K``: K router processes on one port (SO_REUSEPORT) share the backends'
+    in-flight counts, so a burst of nbe * per simultaneous streams lands exactly ``per``
+    on every backend (a replica given more than its max_num_seqs would serve the surplus
+    as a second, serial wave)."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    import time
+    import aiohttp
+    import psutil
+    n = nbe * per
+    hits = [0] * nbe
+    gate = asyncio.Event()
+
+    def make(i):
+        app = web.Application()
+
+        async def health(r):
+            return web.Response(text="ok")
+
+        async def models(r):
+            return web.json_response({"data": [{"id": "m"}]})
+
+        async def comp(r):
+            hits[i] += 1
+            if sum(hits) >= n:
+                gate.set()
+            resp = web.StreamResponse(headers={"content-type": "text/event-stream"})
+            await resp.prepare(r)
+            await asyncio.wait_for(gate.wait(), 60)
+            await resp.write(f"data: {i}\n\ndata: [DONE]\n\n".encode())
+            await resp.write_eof()
+            return resp
+        app.router.add_get("/health", health)
+        app.router.add_get("/v1/models", models)
+        app.router.add_post("/v1/completions", comp)
+        return app
+
+    bes = [TestServer(make(i)) for i in range(nbe)]
+    for b in bes:
+        await b.start_server()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    proc = subprocess.Popen([sys.executable, "-m", "kubernetes_gpu_cluster_amd.router.router",
+                             "--host", "127.0.0.1", "--port", str(port), "--workers", str(workers),
+                             "--backends", ",".join(str(b.make_url("")) for b in bes)],
+                            cwd=root, env=dict(os.environ, PYTHONPATH=root))
+    url = f"http://127.0.0.1:{port}"
+    sess = aiohttp.ClientSession(connector=aiohttp.TCPConnector(limit=0, force_close=True))
+    try:
+        deadline = time.monotonic() + 60
+        while True:
+            try:
+                async with sess.get(url + "/health") as r:
+                    if r.status == 200:
+                        break
+            except aiohttp.ClientError:
+                pass
+            assert time.monotonic() < deadline and proc.poll() is None
+            await asyncio.sleep(0.2)
+        assert len(psutil.Process(proc.pid).children()) == workers
+
+        async def one():
+            async with sess.post(url + "/v1/completions", json={"model": "m", "stream": True}) as r:
+                return await r.text()
+        outs = await asyncio.gather(*[one() for _ in range(n)])
+        assert all(o.endswith("[DONE]\n\n") for o in outs)
+        assert hits == [per] * nbe, hits
+    finally:
+        await sess.close()
+        proc.terminate()
+        proc.wait(30)
+        for b in bes:
+            await b.close()
+    assert proc.returncode == 0, proc.returncode
+
+
+def test_router_workers_share_load_exactly():
+    asyncio.run(_multiworker_scenario())
