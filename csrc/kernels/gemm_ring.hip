@@ -99,7 +99,10 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, 1) void ring_gemm_kernel(
   // first ds_read of every step)
   __shared__ __attribute__((aligned(16))) char lds[NS * SLOT];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // the wave index as a scalar: role and piece selection become SALU branches instead of
+  // exec-masked VALU blocks around every DMA
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const bool issuer = LW > 0 ? wave >= CW : true;
   const bool consumer = wave < CW;
   const int iw = LW > 0 ? wave - CW : wave;       // index among the issuing waves
@@ -127,30 +130,34 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, 1) void ring_gemm_kernel(
   // lines through L2); column tiles start at different steps (spread the X line fetches)
   const int rot = nk >= 4 ? (int)(((int64_t)nb * 37) % nk) : 0;
 
-  // ---- per-piece DMA sources (pieces p = iw, iw + NI, ...): A rows first, then B rows
+  // ---- per-piece DMA sources (pieces p = iw, iw + NI, ...): A rows first, then B rows.
+  // Every address is a wave-uniform base (SGPRs: the operand, the piece's weight group,
+  // the K-step) plus a per-lane 32-bit byte offset fixed for the whole walk, so a K-step
+  // costs the issuing wave one scalar add and one m0 write per DMA -- the loader's
+  // per-step instruction count sits on the critical path between two barriers
+  // (~0.25 us per step measured when every address was rebuilt with 64-bit VALU math).
   const int drow = lane >> 3, dchunk = (lane & 7) ^ drow;
   const int nl = iw < REM ? LHI : LLO;
-  const bf16* src[LHI];
-  int64_t sstep[LHI];
-  int ldso[LHI];
-  bool isb[LHI];
+  uint32_t voff[LHI];                           // per-lane byte offset
+  int64_t gbase[LHI];                           // uniform byte offset of the piece's group
+  const char* const Xb = reinterpret_cast<const char*>(X);
+  const char* const Wb = reinterpret_cast<const char*>(Wp);
+  const int64_t wstep = (int64_t)G * RG_BK * 2;   // bytes per K-step of one weight group
 #pragma unroll
   for (int t = 0; t < LHI; ++t) {
     const int p = iw + t * NI;
-    ldso[t] = p * 1024;
-    isb[t] = p >= PA;
     if (p < PA) {
       int r = m0 + p * 8 + drow;
       r = r < M ? r : M - 1;                      // padded rows re-read the last row
-      src[t] = X + (int64_t)r * ldx + dchunk * 8;
-      sstep[t] = RG_BK;
+      voff[t] = (uint32_t)(((int64_t)r * ldx + dchunk * 8) * 2);
+      gbase[t] = 0;
     } else {
       const int q = p - PA;                       // B piece: tile rows 8q .. 8q + 7
       const int64_t prow = (int64_t)nb * BN + q * 8;
       const int64_t grp = prow / G;
       const int r0 = (int)(prow - grp * G);
-      src[t] = Wp + grp * nk_all * ((int64_t)G * RG_BK) + r0 * RG_BK + lane * 8;
-      sstep[t] = (int64_t)G * RG_BK;
+      voff[t] = (uint32_t)((r0 * RG_BK + lane * 8) * 2);
+      gbase[t] = grp * nk_all * wstep;
     }
   }
 
@@ -159,13 +166,18 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, 1) void ring_gemm_kernel(
     int st = step + rot;
     st = st >= nk ? st - nk : st;
     const int kb = kb0 + st;
+    const int64_t aoff = (int64_t)kb * (RG_BK * 2), boff = (int64_t)kb * wstep;
 #pragma unroll
     for (int t = 0; t < LHI; ++t) {
-      if (t < nl && !(abl & (isb[t] ? 4 : 2))) {
+      const int p = iw + t * NI;
+      if (t < nl) {
         // weights: WAUX = 2 (nt) streams them past L2 (each weight byte is read by ONE
         // workgroup when BM covers all rows); activations keep the default policy
-        if (isb[t]) rg_glds16<WAUX>(src[t] + kb * sstep[t], base + ldso[t]);
-        else rg_glds16<0>(src[t] + kb * sstep[t], base + ldso[t]);
+        if (p >= PA) {
+          if (!(abl & 4)) rg_glds16<WAUX>(Wb + (gbase[t] + boff) + voff[t], base + p * 1024);
+        } else {
+          if (!(abl & 2)) rg_glds16<0>(Xb + aoff + voff[t], base + p * 1024);
+        }
       }
     }
   };
@@ -188,14 +200,14 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, 1) void ring_gemm_kernel(
   }
   for (int it = 0; it < nk; ++it) {
     // step `it` must have landed; up to D - 1 younger steps may stay in flight
-    if (issuer) {
+    if (issuer && !(abl & 16)) {
       const int younger = nk - 1 - it;
       if (nl == LHI) rg_wait<LHI, D - 1>(younger);
       else rg_wait<LLO, D - 1>(younger);
     }
     __builtin_amdgcn_s_barrier();
     // every wave is past the reads of step it - 1, whose slot step it + D reuses
-    if (issuer && it + D < nk) issue(it + D);
+    if (issuer && it + D < nk && !(abl & 8)) issue(it + D);
     if (!consumer || (abl & 1)) continue;
     const char* sa = lds + (it % NS) * SLOT;
     const char* sb = sa + BM * RG_ROWB;

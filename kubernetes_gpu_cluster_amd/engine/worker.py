@@ -60,6 +60,16 @@ class Worker:
         set_moe_mode(cfg.moe_parallel)
         init_parallel(cfg.tensor_parallel_size, cfg.pipeline_parallel_size, device=dev)
         self.ps = get_state()
+        # non-driver ranks of a multi-rank engine heart-beat into the rendezvous store
+        # (engine/health.py): the driver notices a rank on another node dying, and this
+        # rank notices the driver's node dying
+        self.heartbeat = None
+        if self.ps.tp_size * self.ps.pp_size > 1 and dist.is_initialized() and \
+                dist.get_rank() != getattr(self.ps, "global_base", 0):
+            from .health import Heartbeat, rendezvous_store
+            store = rendezvous_store()
+            if store is not None:
+                self.heartbeat = Heartbeat(store, dist.get_rank()).start()
         mcfg, _ = resolve_model(cfg.model)
         self.dtype = cfg.torch_dtype(torch.bfloat16 if mcfg.arch != "opt" else torch.float16)
         if dev.type == "cpu" and self.dtype == torch.float16:
@@ -209,6 +219,8 @@ def worker_loop(worker: Worker) -> None:
         h = _bcast_cmd(0)
         cmd, arg = h[0], h[1]
         if cmd == CMD_EXIT:
+            if worker.heartbeat is not None:
+                worker.heartbeat.stop()
             worker.runner.write_stage_stats()
             _release_custom_allreduce()
             worker.release()
@@ -430,10 +442,30 @@ class _DistExecutorBase:
 
 
 class ExternalExecutor(_DistExecutorBase):
-    """All ranks launched externally (torchrun); call on rank 0 only."""
+    """All ranks launched externally (torchrun); call on rank 0 only.  The driver cannot
+    see the other ranks' exit codes, so its watchdog follows their heartbeats (and the
+    adaptive step timeout) instead."""
 
     def __init__(self, worker: Worker):
         self.worker = worker
+        self.watchdog = _remote_watchdog([])
+
+
+def _watch_heartbeats(wd: RankWatchdog) -> None:
+    """Follow the heartbeats of this engine's other ranks (every rank but the driver)."""
+    from .health import rendezvous_store
+    s = get_state()
+    store = rendezvous_store()
+    n = s.tp_size * s.pp_size
+    if store is not None and n > 1:
+        base = getattr(s, "global_base", 0)
+        wd.watch_heartbeats(store, range(base + 1, base + n))
+
+
+def _remote_watchdog(procs) -> RankWatchdog:
+    wd = RankWatchdog(procs)
+    _watch_heartbeats(wd)
+    return wd.start()
 
 
 def _free_port() -> int:
@@ -493,6 +525,7 @@ class MultiprocExecutor(_DistExecutorBase):
         os.environ["RANK"] = "0"
         os.environ["LOCAL_RANK"] = "0"
         self.worker = Worker(cfg, rank=0, local_device=0)
+        _watch_heartbeats(self.watchdog)
 
     def shutdown(self) -> None:
         super().shutdown()

@@ -140,3 +140,157 @@ def test_parent_watch_fires_when_parent_changes(monkeypatch):
     health.watch_parent(poll=0.01, on_fatal=lambda c, m: hits.append(c))
     time.sleep(0.2)
     assert hits == [health.EXIT_PARENT_DEAD]
+
+
+def test_adaptive_step_timeout():
+    """Without KGC_STEP_TIMEOUT the limit is the warm-up grace for the first steps, then
+    max(floor, 10 x the longest step seen) -- tens of seconds, not ten minutes."""
+    w = health.RankWatchdog([], poll=0.05, on_fatal=lambda c, m: None)
+    w.fixed_timeout = None
+    w.floor, w.warmup_timeout = 1.0, 5.0
+    assert w.step_timeout == 5.0
+    for _ in range(health.WARMUP_STEPS):
+        w.step_begin()
+        time.sleep(0.01)
+        w.step_end()
+    assert w.steps_done == health.WARMUP_STEPS
+    assert w.step_timeout == 1.0                       # floor: 10 x ~10 ms < 1 s
+    w.longest_step = 0.5
+    assert w.step_timeout == 5.0
+    w.step_begin()
+    w._last -= 6.0                                     # a step wedged for 6 s
+    code, msg = w.check_once()
+    assert code == health.EXIT_STEP_TIMEOUT and "longest 0.5 s" in msg
+
+
+class _Store:
+    def __init__(self):
+        self.d = {}
+        self.fail = False
+
+    def add(self, k, v):
+        if self.fail:
+            raise RuntimeError("connection reset by peer")
+        self.d[k] = self.d.get(k, 0) + v
+        return self.d[k]
+
+
+def test_heartbeats_both_directions():
+    """Driver side: a rank whose heartbeat counter stops moving is reported dead after
+    KGC_HEARTBEAT_TIMEOUT.  Rank side: when the store (the driver's process) fails, the
+    rank exits EXIT_PARENT_DEAD -- unless a clean shutdown stopped the heartbeat first."""
+    st = _Store()
+    hb = health.Heartbeat(st, 3, period=0.02, timeout=5, on_fatal=lambda c, m: hits.append(c))
+    hits = []
+    hb.start()
+    w = health.RankWatchdog([], step_timeout=0, poll=0.05, on_fatal=lambda c, m: None)
+    w.watch_heartbeats(st, [3])
+    w.hb_timeout = 0.3
+    for _ in range(10):
+        assert w.check_once() is None
+        time.sleep(0.05)
+    hb.stop()
+    time.sleep(0.05)
+    assert w.check_once() is None                      # sees the last bump
+    time.sleep(0.4)
+    code, msg = w.check_once()
+    assert code == health.EXIT_RANK_DEAD and "rank 3" in msg
+    assert not hits                                    # a stopped heartbeat never fires
+    hits2 = []
+    st2 = _Store()
+    hb2 = health.Heartbeat(st2, 5, period=0.02, timeout=5,
+                           on_fatal=lambda c, m: hits2.append(c)).start()
+    time.sleep(0.1)
+    st2.fail = True
+    time.sleep(2.5)                                    # the 2 s clean-shutdown grace
+    assert hits2 == [health.EXIT_PARENT_DEAD]
+    hb2.stop()
+
+
+def _two_node_server(tmp_path, port, mport):
+    env = dict(os.environ, PYTHONPATH=REPO, KGC_HEARTBEAT_TIMEOUT="10")
+    common = ["--load-format", "dummy", "--device", "cpu", "--dtype", "float32",
+              "--tensor-parallel-size", "2", "--nnodes", "2", "--master-addr", "127.0.0.1",
+              "--master-port", str(mport), "--max-model-len", "256", "--max-num-seqs", "4"]
+    slog = open(tmp_path / "server.log", "w")
+    wlog = open(tmp_path / "worker.log", "w")
+    server = subprocess.Popen([sys.executable, "-m", "kubernetes_gpu_cluster_amd.entrypoints.api_server",
+                               "tiny-llama", "--node-rank", "0", "--api-server-count", "1",
+                               "--host", "127.0.0.1", "--port", str(port)] + common,
+                              stdout=slog, stderr=subprocess.STDOUT, env=env, cwd=REPO,
+                              start_new_session=True)
+    worker = subprocess.Popen([sys.executable, "-m", "kubernetes_gpu_cluster_amd.entrypoints.worker_node",
+                               "tiny-llama", "--node-rank", "1"] + common,
+                              stdout=wlog, stderr=subprocess.STDOUT, env=env, cwd=REPO,
+                              start_new_session=True)
+    t0 = time.time()
+    while _get(f"http://127.0.0.1:{port}/health") != 200:
+        assert server.poll() is None, (tmp_path / "server.log").read_text()[-3000:]
+        assert worker.poll() is None, (tmp_path / "worker.log").read_text()[-3000:]
+        assert time.time() - t0 < 180, "two-node server never became healthy"
+        time.sleep(0.5)
+    return server, worker, (slog, wlog)
+
+
+def _start_stream(port):
+    def stream():
+        body = json.dumps({"prompt": [5, 6, 7], "max_tokens": 200, "stream": True,
+                           "ignore_eos": True}).encode()
+        req = urllib.request.Request(f"http://127.0.0.1:{port}/v1/completions", body,
+                                     {"content-type": "application/json"})
+        try:
+            with urllib.request.urlopen(req, timeout=120) as r:
+                for _ in r:
+                    pass
+        except OSError:
+            pass
+    th = threading.Thread(target=stream, daemon=True)
+    th.start()
+    time.sleep(1.0)
+
+
+def _kill_tree(*procs):
+    for p in procs:
+        if p.poll() is None:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+
+
+@pytest.mark.timeout(300)
+def test_remote_rank_death_ends_driver(tmp_path):
+    """Two-node TP=2 engine (API server = node 0, worker_node = node 1, CPU/gloo): SIGKILL
+    the rank on node 1 mid-stream -> the API server exits non-zero within 60 s, and so
+    does the worker node."""
+    server, worker, logs = _two_node_server(tmp_path, _port(), _port())
+    try:
+        ranks = [c for c in psutil.Process(worker.pid).children()
+                 if "spawn_main" in " ".join(c.cmdline()) and "resource_tracker" not in " ".join(c.cmdline())]
+        assert ranks, "node-1 rank not found"
+        _start_stream(int(server.args[server.args.index("--port") + 1]))
+        os.kill(ranks[0].pid, signal.SIGKILL)
+        killed = time.time()
+        rc = server.wait(timeout=90)
+        assert rc != 0 and time.time() - killed < 60, (tmp_path / "server.log").read_text()[-3000:]
+        assert worker.wait(timeout=30) != 0
+    finally:
+        _kill_tree(server, worker)
+        for f in logs:
+            f.close()
+
+
+@pytest.mark.timeout(300)
+def test_driver_death_ends_worker_node(tmp_path):
+    """The driver's pod dies (SIGKILL of the whole API-server process group): the rank on
+    node 1 loses its heartbeat store and exits, ending the worker node non-zero."""
+    server, worker, logs = _two_node_server(tmp_path, _port(), _port())
+    try:
+        os.killpg(server.pid, signal.SIGKILL)
+        killed = time.time()
+        rc = worker.wait(timeout=90)
+        assert rc != 0 and time.time() - killed < 60, (tmp_path / "worker.log").read_text()[-3000:]
+    finally:
+        _kill_tree(server, worker)
+        for f in logs:
+            f.close()
