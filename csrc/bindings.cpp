@@ -585,7 +585,7 @@ void ring_gemm(Tensor C, Tensor X, Tensor Wp, int64_t cfg, int64_t epi) {
   TORCH_CHECK(Wp.dim() == 3 && Wp.is_contiguous() && Wp.size(2) % 512 == 0,
               "packed W [N/G, K/64, G*64] contiguous");
   const int64_t G = Wp.size(2) / 64, N = Wp.size(0) * G, K = Wp.size(1) * 64;
-  TORCH_CHECK(bn % G == 0 && G % 8 == 0, "G must divide BN");
+  TORCH_CHECK(G == bn, "W must be packed with G = the config's BN (ring_pack)");
   TORCH_CHECK(X.dim() == 2 && X.size(1) == K && X.stride(1) == 1 && X.stride(0) % 8 == 0 &&
               reinterpret_cast<uintptr_t>(X.data_ptr()) % 16 == 0,
               "X [M, K] bf16, 16-B aligned rows");
@@ -609,7 +609,7 @@ void ring_gemm(Tensor C, Tensor X, Tensor Wp, int64_t cfg, int64_t epi) {
   TORCH_CHECK((M + bm - 1) / bm * (N / bn) * S < ((int64_t)1 << 31), "grid too large");
   if (M == 0) return;
   kgc::launch_ring_gemm((int)cfg, (int)epi, C.data_ptr(), X.data_ptr(), Wp.data_ptr(), (int)M,
-                        (int)N, (int)K, X.stride(0), (int)S, (int)G, ss, stream());
+                        (int)N, (int)K, X.stride(0), (int)S, ss, stream());
 }
 
 // P [N/G, K/64, G*64] <- W [N, K] (silu: merged [gate; up], 8-row gate / up interleave)
@@ -855,6 +855,15 @@ void u32_copy_async(int64_t addr, Tensor host_out, int64_t index) {
                              stream()) == hipSuccess, "u32_copy_async");
 }
 
+// the cooperative sampler's sticky barrier-timeout word: its device address (current device)
+int64_t sample_err_addr() { return (int64_t)(intptr_t)kgc::sample_err_addr(); }
+
+// zero one device word, stream-ordered (after its value was copied out)
+void u32_clear_async(int64_t addr) {
+  TORCH_CHECK(hipMemsetAsync((void*)(intptr_t)addr, 0, 4, stream()) == hipSuccess,
+              "u32_clear_async");
+}
+
 // debug builds: OR of the K1/K2/K3 bounds-check error words (read and cleared)
 int64_t debug_errors() {
   return (int64_t)(kgc::dbg_err_attention_decode() | (kgc::dbg_err_attention_prefill() << 1) |
@@ -1045,6 +1054,8 @@ TORCH_LIBRARY(kgc, m) {
         "int[] data, int[] sig, int rank, int cap_bytes) -> ()");
   m.def("allreduce_rms_max_hidden() -> int", &allreduce_rms_max_hidden_op);
   m.def("debug_errors() -> int", &debug_errors);
+  m.def("sample_err_addr() -> int", &sample_err_addr);
+  m.def("u32_clear_async(int addr) -> ()", &u32_clear_async);
   m.def("ep_signal_bytes() -> int", &ep_signal_bytes_op);
   m.def("pp_signal_bytes() -> int", &pp_signal_bytes_op);
   m.def("u32_copy_async(int addr, Tensor(a!) host_out, int index) -> ()", &u32_copy_async);

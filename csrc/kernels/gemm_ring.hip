@@ -79,36 +79,38 @@ __device__ __forceinline__ int64_t rg_silu_row(int64_t p, int I) {
   return i < 8 ? g * 8 + i : I + g * 8 + (i - 8);
 }
 
-// CW = WM * WN MFMA waves, LW loader waves (0: the MFMA waves issue the DMAs themselves)
+// CW = WM * WN MFMA waves and LW loader waves.  The weight operand is packed with
+// G = BN (ring_pack): every K-step of a column tile is one contiguous BN x 128 B block.
 template <int BM, int BN, int WM, int WN, int LW, int NS, int WAUX, int EPI>
 __global__ __launch_bounds__((WM * WN + LW) * 64, 1) void ring_gemm_kernel(
     void* __restrict__ Cv, const bf16* __restrict__ X, const bf16* __restrict__ Wp, int M,
-    int N, int K, int64_t ldx, int S, int G, int MB, int64_t slice_stride, int xmap, int wt,
-    int abl) {
+    int N, int K, int64_t ldx, int S, int MB, int64_t slice_stride, int xmap, int wt, int abl) {
   constexpr int CW = WM * WN;
-  constexpr int NI = LW > 0 ? LW : CW;            // waves issuing DMAs
+  static_assert(LW >= 1, "dedicated loader waves");
   constexpr int D = NS - 1;                       // K-steps in flight
-  constexpr int PA = BM / 8, PB = BN / 8, P = PA + PB;   // 1-KiB DMA pieces per K-step
-  constexpr int LHI = (P + NI - 1) / NI, LLO = P / NI, REM = P % NI;
+  constexpr int PA = BM / 8, PB = BN / 8;         // 1-KiB DMA pieces per K-step
+  static_assert(PA % LW == 0, "activation pieces split evenly over the loaders");
+  // loader w issues LA activation pieces and LB (+1 for w < RB) weight pieces per step:
+  // compile-time counts, so the per-step issue is a straight run of DMAs with no branch
+  constexpr int LA = PA / LW, LB = PB / LW, RB = PB % LW;
+  constexpr int LMAX = LA + LB + (RB ? 1 : 0);
   constexpr int SLOT = (BM + BN) * RG_ROWB;
   constexpr int MT = BM / WM / 16, NT = BN / WN / 16;
   static_assert(MT * WM * 16 == BM && NT * WN * 16 == BN, "wave tiling");
   static_assert(NS >= 2 && NS * SLOT <= 163840, "LDS ring exceeds 160 KiB");
-  static_assert(D * LHI <= 63, "vmcnt range");
+  static_assert(D * LMAX <= 63, "vmcnt range");
   // ONE shared array (a second __shared__ object can make hipcc emit vmcnt(0) before the
   // first ds_read of every step)
   __shared__ __attribute__((aligned(16))) char lds[NS * SLOT];
 
-  // the wave index as a scalar: role and piece selection become SALU branches instead of
-  // exec-masked VALU blocks around every DMA
+  // the wave index as a scalar: role selection is one SALU branch
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool issuer = LW > 0 ? wave >= CW : true;
+  const bool issuer = wave >= CW;
   const bool consumer = wave < CW;
-  const int iw = LW > 0 ? wave - CW : wave;       // index among the issuing waves
+  const int iw = wave - CW;                       // loader index (issuers only)
 
   // ---- tile coordinates (XCD-aware when the host says the grid divides evenly)
-  const int nbt = N / BN;
   int z, mb, nb;
   if (xmap) {
     const int r8 = blockIdx.x & 7, q = blockIdx.x >> 3, cpg = 8 / S;
@@ -121,43 +123,36 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, 1) void ring_gemm_kernel(
     mb = j % MB;
     nb = j / MB;
   }
-  (void)nbt;
   const int m0 = mb * BM;
   const int nk_all = K / RG_BK;
-  const int kb0 = (int)((int64_t)nk_all * z / S);
-  const int nk = (int)((int64_t)nk_all * (z + 1) / S) - kb0;
-  // the row blocks of one column tile walk K in the same order (they share the weight
-  // lines through L2); column tiles start at different steps (spread the X line fetches)
-  const int rot = nk >= 4 ? (int)(((int64_t)nb * 37) % nk) : 0;
+  const int kb0 = nk_all * z / S;
+  const int nk = nk_all * (z + 1) / S - kb0;
+  // the row blocks of one column tile walk K in the same order; column tiles start at
+  // different steps (spread the X line fetches)
+  const int rot = nk >= 4 ? (nb * 37) % nk : 0;
 
-  // ---- per-piece DMA sources (pieces p = iw, iw + NI, ...): A rows first, then B rows.
-  // Every address is a wave-uniform base (SGPRs: the operand, the piece's weight group,
-  // the K-step) plus a per-lane 32-bit byte offset fixed for the whole walk, so a K-step
-  // costs the issuing wave one scalar add and one m0 write per DMA -- the loader's
-  // per-step instruction count sits on the critical path between two barriers
-  // (~0.25 us per step measured when every address was rebuilt with 64-bit VALU math).
+  // ---- loader state.  Every DMA address is a wave-uniform base (the operand, the
+  // column tile, the K-step: SGPRs) plus a per-lane 32-bit byte offset fixed for the whole
+  // walk, so a K-step costs a loader one scalar add and one m0 write per DMA.  (Rebuilding
+  // each address with 64-bit VALU math, and choosing the piece kind at run time, made the
+  // loader's per-step issue ~650 cycles -- measured, it sits between two barriers.)
   const int drow = lane >> 3, dchunk = (lane & 7) ^ drow;
-  const int nl = iw < REM ? LHI : LLO;
-  uint32_t voff[LHI];                           // per-lane byte offset
-  int64_t gbase[LHI];                           // uniform byte offset of the piece's group
+  uint32_t voa[LA], vob[LB + 1];
   const char* const Xb = reinterpret_cast<const char*>(X);
-  const char* const Wb = reinterpret_cast<const char*>(Wp);
-  const int64_t wstep = (int64_t)G * RG_BK * 2;   // bytes per K-step of one weight group
+  const int64_t wstep = (int64_t)BN * RG_BK * 2;  // bytes per K-step of one column tile
+  const char* const Wb = reinterpret_cast<const char*>(Wp) + (int64_t)nb * nk_all * wstep;
+  const int extra_b = (RB && iw < RB) ? 1 : 0;
+  if (issuer) {
 #pragma unroll
-  for (int t = 0; t < LHI; ++t) {
-    const int p = iw + t * NI;
-    if (p < PA) {
-      int r = m0 + p * 8 + drow;
+    for (int t = 0; t < LA; ++t) {
+      int r = m0 + (iw * LA + t) * 8 + drow;
       r = r < M ? r : M - 1;                      // padded rows re-read the last row
-      voff[t] = (uint32_t)(((int64_t)r * ldx + dchunk * 8) * 2);
-      gbase[t] = 0;
-    } else {
-      const int q = p - PA;                       // B piece: tile rows 8q .. 8q + 7
-      const int64_t prow = (int64_t)nb * BN + q * 8;
-      const int64_t grp = prow / G;
-      const int r0 = (int)(prow - grp * G);
-      voff[t] = (uint32_t)((r0 * RG_BK + lane * 8) * 2);
-      gbase[t] = grp * nk_all * wstep;
+      voa[t] = (uint32_t)(((int64_t)r * ldx + dchunk * 8) * 2);
+    }
+#pragma unroll
+    for (int t = 0; t < LB + 1; ++t) {
+      const int q = t < LB ? iw * LB + t : LW * LB + iw;   // B piece: tile rows 8q .. 8q+7
+      vob[t] = (uint32_t)((q * 8 * RG_BK + lane * 8) * 2);
     }
   }
 
@@ -166,20 +161,16 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, 1) void ring_gemm_kernel(
     int st = step + rot;
     st = st >= nk ? st - nk : st;
     const int kb = kb0 + st;
-    const int64_t aoff = (int64_t)kb * (RG_BK * 2), boff = (int64_t)kb * wstep;
+    const char* xa = Xb + (int64_t)kb * (RG_BK * 2);
+    const char* wa = Wb + (int64_t)kb * wstep;
+    // weights: WAUX = 2 (nt) streams them past L2 (each weight byte is read by ONE
+    // workgroup when BM covers all rows); activations keep the default policy
 #pragma unroll
-    for (int t = 0; t < LHI; ++t) {
-      const int p = iw + t * NI;
-      if (t < nl) {
-        // weights: WAUX = 2 (nt) streams them past L2 (each weight byte is read by ONE
-        // workgroup when BM covers all rows); activations keep the default policy
-        if (p >= PA) {
-          if (!(abl & 4)) rg_glds16<WAUX>(Wb + (gbase[t] + boff) + voff[t], base + p * 1024);
-        } else {
-          if (!(abl & 2)) rg_glds16<0>(Xb + aoff + voff[t], base + p * 1024);
-        }
-      }
-    }
+    for (int t = 0; t < LB; ++t)
+      rg_glds16<WAUX>(wa + vob[t], base + (PA + iw * LB + t) * 1024);
+    if (RB && extra_b) rg_glds16<WAUX>(wa + vob[LB], base + (PA + LW * LB + iw) * 1024);
+#pragma unroll
+    for (int t = 0; t < LA; ++t) rg_glds16<0>(xa + voa[t], base + (iw * LA + t) * 1024);
   };
 
   f32x4 acc[MT][NT];
@@ -200,14 +191,14 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, 1) void ring_gemm_kernel(
   }
   for (int it = 0; it < nk; ++it) {
     // step `it` must have landed; up to D - 1 younger steps may stay in flight
-    if (issuer && !(abl & 16)) {
+    if (issuer) {
       const int younger = nk - 1 - it;
-      if (nl == LHI) rg_wait<LHI, D - 1>(younger);
-      else rg_wait<LLO, D - 1>(younger);
+      if (RB && extra_b) rg_wait<LA + LB + 1, D - 1>(younger);
+      else rg_wait<LA + LB, D - 1>(younger);
     }
     __builtin_amdgcn_s_barrier();
     // every wave is past the reads of step it - 1, whose slot step it + D reuses
-    if (issuer && it + D < nk && !(abl & 8)) issue(it + D);
+    if (issuer && it + D < nk) issue(it + D);
     if (!consumer || (abl & 1)) continue;
     const char* sa = lds + (it % NS) * SLOT;
     const char* sb = sa + BM * RG_ROWB;
@@ -317,20 +308,18 @@ struct RingCfg { int bm, bn, wm, wn, lw, ns, waux; };
 // blocks of one column tile dispatched side by side on an XCD do NOT share the weight
 // lines through L2 (64 x 64 full-K o_proj: 25.5 us = 4 x 33.5 MB at the chip's rate).
 // The narrow projections then split K (o: 256 x 64, S = 4; qkv: 256 x 96, S = 4);
-// gate_up + SiLU: 256 x 112 (7 gate / up groups of 16), 256 tiles at S = 1.
-// All with 4 loader waves (the MFMA waves never issue a DMA: 1.3-1.6x faster measured).
-constexpr int kRingCfgs = 16;
+// gate_up + SiLU: 256 x 112 (7 gate / up groups of 16: 256 tiles at S = 1) or 256 x 128.
+// Dedicated loader waves throughout (the MFMA waves never issue a DMA: 1.3-1.6x faster).
+constexpr int kRingCfgs = 12;
 constexpr RingCfg kRing[kRingCfgs] = {
-    {256, 64, 4, 2, 4, 4, 0},  {256, 64, 4, 2, 4, 4, 2},  {256, 96, 4, 2, 4, 3, 0},
-    {256, 96, 4, 2, 4, 3, 2},  {256, 112, 4, 1, 4, 3, 0}, {256, 112, 4, 1, 4, 3, 2},
-    {256, 128, 4, 2, 4, 3, 0}, {256, 128, 4, 2, 4, 3, 2}, {256, 32, 4, 2, 4, 4, 0},
-    {128, 128, 2, 2, 4, 5, 0}, {128, 224, 2, 2, 4, 3, 0}, {128, 64, 2, 2, 4, 6, 0},
-    {128, 96, 2, 2, 4, 5, 0},  {128, 112, 4, 1, 4, 5, 0}, {64, 64, 2, 2, 4, 9, 0},
-    {256, 32, 4, 2, 4, 4, 2}};
+    {256, 64, 4, 2, 4, 4, 2},  {256, 64, 4, 2, 8, 4, 2},  {256, 96, 4, 2, 4, 3, 2},
+    {256, 96, 4, 2, 8, 3, 2},  {256, 112, 4, 1, 4, 3, 2}, {256, 112, 4, 1, 8, 3, 2},
+    {256, 128, 4, 2, 4, 3, 2}, {256, 128, 4, 2, 8, 3, 2}, {128, 128, 2, 2, 4, 5, 0},
+    {128, 64, 2, 2, 4, 6, 0},  {128, 96, 2, 2, 4, 5, 0},  {128, 112, 4, 1, 4, 5, 0}};
 
 template <int C>
 void ring_launch(int epi, void* Cp, const void* X, const void* W, int M, int N, int K,
-                 int64_t ldx, int S, int G, int64_t ss, hipStream_t s) {
+                 int64_t ldx, int S, int64_t ss, hipStream_t s) {
   constexpr RingCfg c = kRing[C];
   const int MB = (M + c.bm - 1) / c.bm;
   const dim3 grid((unsigned)(MB * (N / c.bn) * S));
@@ -340,8 +329,7 @@ void ring_launch(int epi, void* Cp, const void* X, const void* W, int M, int N, 
     const char* e = getenv("KGC_PARTIAL_WT");
     return e ? atoi(e) : 1;
   }();
-  // profiling only (tools/ring_bench.py --ablate): bit 0 drops the MFMAs, bit 1 the
-  // activation DMAs, bit 2 the weight DMAs (waits unchanged: a lower bound)
+  // profiling only: bit 0 drops the MFMAs (KGC_RING_ABLATE=1)
   static const int abl = [] {
     const char* e = getenv("KGC_RING_ABLATE");
     return e ? atoi(e) : 0;
@@ -349,7 +337,7 @@ void ring_launch(int epi, void* Cp, const void* X, const void* W, int M, int N, 
 #define RG_LAUNCH(E)                                                                        \
   ring_gemm_kernel<c.bm, c.bn, c.wm, c.wn, c.lw, c.ns, c.waux, E>                           \
       <<<grid, (c.wm * c.wn + c.lw) * 64, 0, s>>>(Cp, (const bf16*)X, (const bf16*)W, M, N, \
-                                                  K, ldx, S, G, MB, ss, xm, wt, abl)
+                                                  K, ldx, S, MB, ss, xm, wt, abl)
   if (epi == RG_PARTIAL) RG_LAUNCH(RG_PARTIAL);
   else if (epi == RG_OUT) RG_LAUNCH(RG_OUT);
   else RG_LAUNCH(RG_SILU);
@@ -358,9 +346,9 @@ void ring_launch(int epi, void* Cp, const void* X, const void* W, int M, int N, 
 
 template <int... Is>
 void ring_dispatch(int cfg, int epi, void* C, const void* X, const void* W, int M, int N, int K,
-                   int64_t ldx, int S, int G, int64_t ss, hipStream_t s,
+                   int64_t ldx, int S, int64_t ss, hipStream_t s,
                    std::integer_sequence<int, Is...>) {
-  ((cfg == Is ? (ring_launch<Is>(epi, C, X, W, M, N, K, ldx, S, G, ss, s), 0) : 0), ...);
+  ((cfg == Is ? (ring_launch<Is>(epi, C, X, W, M, N, K, ldx, S, ss, s), 0) : 0), ...);
 }
 
 }  // namespace
@@ -374,8 +362,8 @@ void ring_cfg_info(int cfg, int* bm, int* bn, int* threads, int* slots) {
 }
 
 void launch_ring_gemm(int cfg, int epi, void* C, const void* X, const void* Wp, int M, int N,
-                      int K, int64_t ldx, int S, int G, int64_t slice_stride, hipStream_t s) {
-  ring_dispatch(cfg, epi, C, X, Wp, M, N, K, ldx, S, G, slice_stride, s,
+                      int K, int64_t ldx, int S, int64_t slice_stride, hipStream_t s) {
+  ring_dispatch(cfg, epi, C, X, Wp, M, N, K, ldx, S, slice_stride, s,
                 std::make_integer_sequence<int, kRingCfgs>{});
 }
 

@@ -71,6 +71,8 @@ void launch_sample(int dtype, int64_t* out, uint64_t* partial, const void* logit
 // B * sample_coop_ws_bytes() bytes, all-zero before the first call (the kernel leaves it
 // zeroed), partial B * coop splits words
 int sample_coop_ws_bytes();
+// device address of the sampler's sticky barrier-timeout word (this device)
+void* sample_err_addr();
 int sample_coop_splits(int B);
 void launch_sample_coop(int dtype, int64_t* out, uint64_t* partial, void* ws, const void* logits,
                         int64_t row_stride, int B, int V, const float* temperature,
@@ -125,15 +127,15 @@ void launch_dgemm_pack(int dtype, bool silu, void* P, const void* W, int N, int 
                        hipStream_t s);
 void launch_dgemm_ablate(int mode, float* C, const void* X, const void* W, int M, int N, int K,
                          int64_t ldx, int S, int64_t ss, hipStream_t s);
-// K9r full-K ring decode GEMM (gemm_ring.hip), bf16: X [M, K] . W^T with tile config `cfg`
+// K9r ring decode GEMM (gemm_ring.hip), bf16: X [M, K] . W^T with tile config `cfg`
 // (ring_cfg_info: BM, BN, threads, ring slots) over W packed by launch_ring_pack into
-// [N/G][K/64][G*64] (G-row groups, G | BN).  epi 0: fp32 split-K slice z of C [S, M, N];
+// [N/G][K/64][G*64] with G = the config's BN.  epi 0: fp32 split-K slice z of C [S, M, N];
 // 1: C [M, N] bf16 (S = 1); 2: silu(gate) * up of a merged [gate; up] W packed with
 // silu = true into C [M, N/2] (S = 1)
 int ring_num_cfgs();
 void ring_cfg_info(int cfg, int* bm, int* bn, int* threads, int* slots);
 void launch_ring_gemm(int cfg, int epi, void* C, const void* X, const void* Wp, int M, int N,
-                      int K, int64_t ldx, int S, int G, int64_t slice_stride, hipStream_t s);
+                      int K, int64_t ldx, int S, int64_t slice_stride, hipStream_t s);
 void launch_ring_pack(bool silu, void* P, const void* W, int N, int K, int G, hipStream_t s);
 // residual += sum_z Cs[z] (rounded to dtype); out = rms_norm(residual) * w, one WG per row
 void launch_splitk_add_rms_norm(int dtype, void* out, const float* Cs, void* residual,

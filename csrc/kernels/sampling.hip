@@ -299,6 +299,9 @@ __device__ uint64_t g_smp_stamps[16];
     if (g_smp_stamp_on && b == 0 && y == 0 && tid == 0) g_smp_stamps[i] = wall_clock64();   \
   } while (0)
 
+// sticky "a cooperative row barrier gave up" word, read and cleared by the host
+__device__ uint32_t g_smp_err;
+
 struct CoopWs {
   uint32_t bar[16];
   uint32_t maxkey;
@@ -361,7 +364,11 @@ __global__ __launch_bounds__(SMP_NT) void sample_coop_kernel(
       while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)S) {
         __builtin_amdgcn_s_sleep(1);
         if (++it > (1 << 24)) {
+          // a row's workgroups were not co-resident (another kernel held CUs): the
+          // thresholds below are wrong -- flag it in the sticky device word the host
+          // reads after every step (ops.SamplerHealth) so the step is never served
           atomicOr(&ws->err, 1u);
+          atomicOr(&g_smp_err, 1u);
           break;
         }
       }
@@ -839,4 +846,12 @@ void launch_sample_vp_unpack(int64_t* out, const int64_t* packed, int B, hipStre
   sample_vp_unpack_kernel<<<(B + 255) / 256, 256, 0, s>>>(out, packed, B);
 }
 
+}  // namespace kgc
+
+namespace kgc {
+void* sample_err_addr() {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_smp_err)) != hipSuccess) return nullptr;
+  return p;
+}
 }  // namespace kgc

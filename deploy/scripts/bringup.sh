@@ -9,6 +9,9 @@
 #      Calico, node labelled gpu=true
 #   3. native node tools                    native/build.sh (OCI shim, hook, amd-ctk, amdgpu-topo)
 #   4. GPU enablement                       gpu-crio-setup.sh (runtime handler, CDI, device plugin)
+#   4b. engine image in CRI-O's store       --image-tar: podman load; otherwise podman / buildah
+#                                           build of deploy/docker/Dockerfile when missing;
+#                                           always `crictl inspecti` before anything is applied
 #   5. wait until the node advertises amd.com/gpu
 #   6. values -> manifests | kubectl apply  python -m kubernetes_gpu_cluster_amd.k8s.render
 #   7. wait for the engine Deployments and the vllm-router-service endpoints
@@ -16,8 +19,8 @@
 #
 #   sudo bash deploy/scripts/bringup.sh --single-node \
 #        [--values=deploy/values/values-llama3-8b-tp1.yaml] [--proxy=URL] [--kube-version=v1.33.3]
-#        [--image-tar=kgc-engine.tar] [--port=30080] [--timeout=1800] [--skip-node-setup]
-#        [--dry-run]
+#        [--image-tar=kgc-engine.tar | --no-build] [--image=kgc/engine:TAG] [--port=30080]
+#        [--timeout=1800] [--skip-node-setup] [--dry-run]
 #
 # --dry-run prints the full ordered call log (the sub-scripts run in their own dry-run
 # mode) without changing the machine.  --skip-node-setup starts at step 5 on a node that
@@ -31,6 +34,8 @@ VALUES="$REPO/deploy/values/values-llama3-8b-tp1.yaml"
 PROXY="${PROXY:-}"
 KUBE_VERSION=""
 IMAGE_TAR=""
+IMAGE="${IMAGE:-}"
+BUILD=1
 PORT=30080
 TIMEOUT=1800
 SKIP_NODE=0
@@ -40,7 +45,7 @@ while [[ $# -gt 0 ]]; do
   arg="$1"; val=""
   case "$arg" in
     --*=*) val="${arg#*=}"; arg="${arg%%=*}" ;;
-    --values|--proxy|--kube-version|--image-tar|--port|--timeout)
+    --values|--proxy|--kube-version|--image-tar|--image|--port|--timeout)
       [[ $# -ge 2 ]] || die "$arg needs a value"; val="$2"; shift ;;
   esac
   case "$arg" in
@@ -49,17 +54,25 @@ while [[ $# -gt 0 ]]; do
     --proxy) PROXY="$val" ;;
     --kube-version) KUBE_VERSION="$val" ;;
     --image-tar) IMAGE_TAR="$val" ;;
+    --image) IMAGE="$val" ;;
+    --no-build) BUILD=0 ;;
     --port) PORT="$val" ;;
     --timeout) TIMEOUT="$val" ;;
     --skip-node-setup) SKIP_NODE=1 ;;
     --dry-run) DRY_RUN=1 ;;
     --yes|-y) ASSUME_YES=1 ;;
-    -h|--help) sed -n 2,26p "$0"; exit 0 ;;
+    -h|--help) sed -n 2,29p "$0"; exit 0 ;;
     *) die "unknown argument $1" ;;
   esac
   shift
 done
 [[ -f "$VALUES" ]] || die "values file not found: $VALUES"
+if [[ -z "$IMAGE" ]]; then             # the renderer's default engine image
+  IMAGE=$(cd "$REPO" && "$PYTHON" -c 'from kubernetes_gpu_cluster_amd.k8s.render import \
+DEFAULT_ENGINE_IMAGE as i, DEFAULT_ENGINE_TAG as t; print(f"{i}:{t}")') \
+    || die "cannot read the default engine image from the renderer"
+fi
+[[ "$IMAGE" == *:* ]] || die "--image must be REPOSITORY:TAG (got $IMAGE)"
 export DRY_RUN ASSUME_YES ROOT
 
 sub_flags=()
@@ -76,8 +89,39 @@ node_setup() {
   run bash "$REPO/native/build.sh"
   step 4 "GPU enablement"
   bash "$HERE/gpu-crio-setup.sh" --yes "${sub_flags[@]}"
-  if [[ -n "$IMAGE_TAR" ]]; then         # offline node: side-load the engine image into CRI-O
-    run podman load -i "$IMAGE_TAR" || die "loading $IMAGE_TAR failed"
+}
+
+image_present() { crictl inspecti "$IMAGE" >/dev/null 2>&1; }
+
+# The engine Deployments reference $IMAGE with imagePullPolicy IfNotPresent: an offline
+# node that lacks it would sit in ImagePullBackOff until step 7 times out.  Put it into
+# CRI-O's store here (podman / buildah as root share containers/storage with CRI-O) and
+# refuse to apply manifests for an image the node does not have.
+ensure_image() {
+  step 4b "engine image $IMAGE"
+  if [[ -n "$IMAGE_TAR" ]]; then          # offline node: side-load the saved image
+    [[ "$DRY_RUN" == "1" || -f "$IMAGE_TAR" ]] || die "--image-tar $IMAGE_TAR not found"
+    run podman load -i "$IMAGE_TAR" || die "loading $IMAGE_TAR into CRI-O's store failed"
+  elif [[ "$DRY_RUN" == "1" ]] || ! image_present; then
+    if [[ "$BUILD" != "1" ]]; then
+      [[ "$DRY_RUN" == "1" ]] || die "engine image $IMAGE is not on this node and --no-build was given"
+    elif [[ "$DRY_RUN" == "1" ]] || have_cmd podman; then
+      run podman build -f "$REPO/deploy/docker/Dockerfile" -t "$IMAGE" "$REPO" \
+        || die "podman build of $IMAGE failed"
+    elif have_cmd buildah; then
+      run buildah bud -f "$REPO/deploy/docker/Dockerfile" -t "$IMAGE" "$REPO" \
+        || die "buildah build of $IMAGE failed"
+    else
+      die "engine image $IMAGE is not in CRI-O's store and neither podman nor buildah is" \
+          "installed: build deploy/docker/Dockerfile elsewhere and pass --image-tar"
+    fi
+  fi
+  if [[ "$DRY_RUN" == "1" ]]; then
+    printf "DRY: crictl inspecti %s\n" "$IMAGE"
+  else
+    image_present || die "engine image $IMAGE is still not in CRI-O's store (crictl inspecti);" \
+                         "not applying manifests that would sit in ImagePullBackOff"
+    log "engine image $IMAGE is on the node"
   fi
 }
 
@@ -119,11 +163,13 @@ deploy_and_smoke() {
   wait_for "amd.com/gpu on the node" gpus_advertised
   step 6 "render $(basename "$VALUES") and apply"
   if [[ "$DRY_RUN" == "1" ]]; then
-    "$PYTHON" -m kubernetes_gpu_cluster_amd.k8s.render -f "$VALUES" >/dev/null
-    printf "DRY: %s -m kubernetes_gpu_cluster_amd.k8s.render -f %s | kubectl apply -f -\n" \
-      "$PYTHON" "$VALUES"
+    (cd "$REPO" && "$PYTHON" -m kubernetes_gpu_cluster_amd.k8s.render -f "$VALUES" \
+      --engine-image "${IMAGE%:*}" --engine-tag "${IMAGE##*:}" >/dev/null)
+    printf "DRY: %s -m kubernetes_gpu_cluster_amd.k8s.render -f %s --engine-image %s --engine-tag %s | kubectl apply -f -\n" \
+      "$PYTHON" "$VALUES" "${IMAGE%:*}" "${IMAGE##*:}"
   else
-    (cd "$REPO" && "$PYTHON" -m kubernetes_gpu_cluster_amd.k8s.render -f "$VALUES") \
+    (cd "$REPO" && "$PYTHON" -m kubernetes_gpu_cluster_amd.k8s.render -f "$VALUES" \
+      --engine-image "${IMAGE%:*}" --engine-tag "${IMAGE##*:}") \
       | kubectl apply -f - || die "kubectl apply failed"
   fi
   step 7 "engine pods and router service"
@@ -153,6 +199,7 @@ deploy_and_smoke() {
 
 require_root
 [[ "$SKIP_NODE" == "1" ]] || node_setup
+ensure_image
 # kubectl as root on the control plane (k8s_setup copies admin.conf to $SUDO_USER's home)
 if [[ -z "${KUBECONFIG:-}" && -f "${ROOT}/etc/kubernetes/admin.conf" ]]; then
   export KUBECONFIG="${ROOT}/etc/kubernetes/admin.conf"

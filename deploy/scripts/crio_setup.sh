@@ -32,13 +32,14 @@ write_file /etc/apt/sources.list.d/cri-o.list \
 mkdir -p "${ROOT}/etc/apt/keyrings"
 run curl -fsSL ${PROXY:+--proxy "$PROXY"} \
   "https://download.opensuse.org/repositories/isv:/cri-o:/stable:/$CRIO_VERSION/deb/Release.key" \
-  -o "${ROOT}${KEYRING}" || warn "could not fetch the CRI-O key"
+  -o "${ROOT}${KEYRING}" \
+  || die "could not fetch the CRI-O apt key from download.opensuse.org (network / --proxy?)"
 if [[ -n "$PROXY" ]]; then
   write_file /etc/apt/apt.conf.d/95kgc-proxy "Acquire::http::Proxy \"$PROXY\";
 Acquire::https::Proxy \"$PROXY\";
 "
 fi
-run apt-get update -y || warn "apt-get update failed"
+run apt-get update -y || die "apt-get update failed (the CRI-O repository is unusable)"
 run apt-get install -y cri-o || die "installing cri-o failed"
 run systemctl enable --now crio || true
 

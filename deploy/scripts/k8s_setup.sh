@@ -141,8 +141,9 @@ install_k8s_apt() {
 "
   mkdir -p "${ROOT}/etc/apt/keyrings"
   run curl -fsSL ${PROXY:+--proxy "$PROXY"} "https://pkgs.k8s.io/core:/stable:/${minor}/deb/Release.key" \
-    -o "${ROOT}${keyring}" || warn "could not fetch the k8s apt key"
-  run apt-get update -y || warn "apt-get update failed"
+    -o "${ROOT}${keyring}" \
+    || die "could not fetch the Kubernetes apt key from pkgs.k8s.io (network / --proxy?)"
+  run apt-get update -y || die "apt-get update failed (the pkgs.k8s.io repository is unusable)"
   run apt-get install -y kubelet kubeadm kubectl || die "installing kubeadm failed"
   run apt-mark hold kubelet kubeadm kubectl || true
   run systemctl enable --now kubelet || true

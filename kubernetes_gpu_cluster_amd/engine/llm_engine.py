@@ -125,6 +125,9 @@ class LLMEngine:
                              f"{self.max_model_len}")
         if max(prompt_token_ids) >= self.mcfg.vocab_size or min(prompt_token_ids) < 0:
             raise ValueError("prompt token id out of vocabulary range")
+        if self.pp_depth > 1 and params.logprobs is not None:
+            # the pipelined path returns only the sampled ids from the last stage
+            raise ValueError("logprobs are not supported with pipeline_parallel_size > 1")
         seq = Sequence(rid, prompt_token_ids, params, arrival_time, self.max_model_len)
         self.seqs[rid] = seq
         self.scheduler.add(seq)

@@ -94,6 +94,8 @@ class Worker:
         if self.ps.tp_size > 1 and dev.type == "cuda" and not cfg.disable_custom_all_reduce:
             from ..parallel.custom_allreduce import maybe_init_custom_allreduce
             comm.set_custom_allreduce(maybe_init_custom_allreduce(self.ps, dev))
+        # the cooperative sampler's error word (last PP stage samples)
+        self.sampler_health = ops.SamplerHealth(dev) if dev.type == "cuda" else None
         self.ep_a2a = None
         if self.ps.tp_size > 1 and dev.type == "cuda" and cfg.moe_parallel == "ep":
             from ..models.moe import MoEBlock
@@ -262,11 +264,21 @@ class LocalExecutor:
 
     def execute(self, plan: StepPlan) -> list[int]:
         out = self.worker.run(plan)
-        return out.tolist()
+        sh = self.worker.sampler_health
+        if sh is not None:
+            sh.enqueue_err_read()
+        res = out.tolist()              # synchronises: the error word has landed
+        if sh is not None:
+            sh.raise_if_failed()
+        return res
 
     def execute_async(self, plan: StepPlan) -> "TokenFuture":
         out = self.worker.run(plan)
-        return TokenFuture(*self.runner.tokens_to_host(out), lp=self.runner.take_logprobs())
+        sh = self.worker.sampler_health
+        if sh is not None:
+            sh.enqueue_err_read()       # ahead of the token copy: its event covers both
+        return TokenFuture(*self.runner.tokens_to_host(out), lp=self.runner.take_logprobs(),
+                           on_done=sh.raise_if_failed if sh is not None else None)
 
     @property
     def supports_async(self) -> bool:
@@ -337,7 +349,8 @@ class _DistExecutorBase:
             self.watchdog.step_begin()
         # sticky error words of the peer-memory collectives (xGMI all-reduce, EP exchange)
         checks = [c for c in (comm.get_custom_allreduce(), getattr(self.worker, "ep_a2a", None),
-                              self.worker.runner.pp_link) if c is not None]
+                              self.worker.runner.pp_link, self.worker.sampler_health)
+                  if c is not None]
         for c in checks:
             c.enqueue_err_read()
         # the error words land in pinned host memory behind this event: done() reads them

@@ -285,6 +285,33 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
     return out
 
 
+class SamplerFailed(RuntimeError):
+    """The cooperative top-k / top-p sampler's row barrier timed out: the step's
+    thresholds (and tokens) are invalid."""
+
+
+class SamplerHealth:
+    """The cooperative sampler's sticky error word (sampling.hip ``g_smp_err``), checked
+    like the peer-memory collectives' words: ``enqueue_err_read`` queues a copy into
+    pinned memory and a clear behind the step, ``raise_if_failed`` (after the step
+    completed) raises instead of letting its tokens be served."""
+
+    def __init__(self, device: torch.device):
+        with torch.cuda.device(device):
+            self.addr = int(_k().sample_err_addr())
+        self.host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+
+    def enqueue_err_read(self) -> None:
+        _k().u32_copy_async(self.addr, self.host, 0)
+        _k().u32_clear_async(self.addr)
+
+    def raise_if_failed(self) -> None:
+        if int(self.host[0]):
+            self.host[0] = 0
+            raise SamplerFailed("top-k / top-p sampler: a row's workgroups were not co-resident "
+                                "and its barrier timed out; the step's tokens are invalid")
+
+
 def sample_vp_partial(logits: torch.Tensor, V: int, temperature: torch.Tensor,
                       seeds: torch.Tensor, vocab_off: int,
                       out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -295,3 +295,21 @@ def test_pipelined_pp2_keeps_both_stages_busy(tmp_path, monkeypatch):
         util[st["pp_rank"]] = st["busy_s"] / (st["t_last"] - st["t_first"])
     assert set(util) == {0, 1}, util
     assert min(util.values()) > 0.8, util
+
+
+def test_pp2_rejects_logprobs():
+    """The pipelined path returns only sampled ids from the last stage: a logprobs
+    request is refused up front instead of silently getting none."""
+    from kubernetes_gpu_cluster_amd.engine.llm_engine import LLM
+    from kubernetes_gpu_cluster_amd.engine.sequence import SamplingParams
+    llm = LLM("tiny-llama", random_init=True, device="cpu", dtype="float32",
+              pipeline_parallel_size=2, max_model_len=128, max_num_seqs=4,
+              max_num_batched_tokens=64, num_gpu_blocks_override=32)
+    try:
+        with pytest.raises(ValueError, match="logprobs"):
+            llm.engine.add_request([5, 6, 7], SamplingParams(max_tokens=2, logprobs=2))
+        outs = llm.generate([[5, 6, 7]], SamplingParams(temperature=0, max_tokens=3,
+                                                         ignore_eos=True))
+        assert len(outs[0].output_token_ids) == 3
+    finally:
+        llm.shutdown()

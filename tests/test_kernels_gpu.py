@@ -677,6 +677,37 @@ def test_dgemm_pack_layout(gpu):
         assert torch.equal(pc[nb, kb, r, pos], src)
 
 
+@pytest.mark.parametrize("cfg", range(12))
+def test_ring_gemm_matches_fp32(gpu, cfg):
+    """K9r ring GEMM (gemm_ring.hip, every tile config) vs an fp32 matmul: bf16 output,
+    fp32 split-K slices (S = 2, 3: uneven K ranges, XCD-mapped) and the SiLU epilogue over
+    the 8-row gate / up interleave; M not a multiple of BM (clamped loads, masked rows)."""
+    k = torch.ops.kgc
+    bm, bn, thr, ns = k.ring_cfg_info(cfg)
+    N, K = bn * 16, 640
+    M = bm - 37 if bm > 64 else bm + 5
+    torch.manual_seed(cfg)
+    x = torch.randn(M, K, dtype=torch.bfloat16, device=gpu)
+    w = torch.randn(N, K, dtype=torch.bfloat16, device=gpu) * 0.02
+    ref = x.float().cpu() @ w.float().cpu().t()
+
+    def packed(silu):
+        p = torch.empty(N // bn, K // 64, bn * 64, dtype=w.dtype, device=gpu)
+        k.ring_pack(p, w, silu)
+        return p
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
+    k.ring_gemm(out, x, packed(False), cfg, 1)
+    torch.testing.assert_close(out.float().cpu(), ref, atol=3e-2, rtol=2e-2)
+    for S in (2, 3):
+        ws = torch.full((S, M, N), float("nan"), dtype=torch.float32, device=gpu)
+        k.ring_gemm(ws, x, packed(False), cfg, 0)
+        torch.testing.assert_close(ws.sum(0).cpu(), ref, atol=2e-3, rtol=2e-3)
+    act = torch.empty(M, N // 2, dtype=torch.bfloat16, device=gpu)
+    k.ring_gemm(act, x, packed(True), cfg, 2)
+    exp = torch.nn.functional.silu(ref[:, : N // 2]) * ref[:, N // 2:]
+    torch.testing.assert_close(act.float().cpu(), exp, atol=3e-2, rtol=2e-2)
+
+
 def test_linear_uses_dgemm_plan(gpu):
     from kubernetes_gpu_cluster_amd.ops import gemm
     torch.manual_seed(5)
@@ -871,3 +902,24 @@ def test_tail_fused_model_small_m_acc_norm(gpu):
         gemm.clear_plan()
         llama_mod._tail_fusion_enabled = True
     torch.testing.assert_close(got.float(), ref_out.float(), atol=6e-2, rtol=3e-2)
+
+
+def test_sampler_health_word(gpu):
+    """The cooperative sampler's sticky barrier-timeout word: zero after a normal top-k /
+    top-p step, copied and cleared behind the step, and a set word raises SamplerFailed."""
+    torch.manual_seed(0)
+    B, V = 8, 32000
+    logits = torch.randn(B, V, device=gpu)
+    sh = ops.SamplerHealth(gpu)
+    temp = torch.full((B,), 0.8, device=gpu)
+    topk = torch.full((B,), 40, dtype=torch.int32, device=gpu)
+    topp = torch.full((B,), 0.9, device=gpu)
+    seeds = torch.arange(B, dtype=torch.int64, device=gpu)
+    ops.sample(logits, temp, topk, topp, seeds)
+    sh.enqueue_err_read()
+    torch.cuda.synchronize()
+    sh.raise_if_failed()                          # healthy step: no error
+    sh.host[0] = 1
+    with pytest.raises(ops.SamplerFailed):
+        sh.raise_if_failed()
+    assert int(sh.host[0]) == 0

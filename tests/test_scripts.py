@@ -260,8 +260,11 @@ def test_bringup_dry_run_full_ordered_log(env):
              "step 2: Kubernetes", "kubeadm init", "taint nodes --all",
              "step 3: native", "native/build.sh",
              "step 4: GPU enablement", "amd-ctk runtime configure",
+             "step 4b: engine image kgc/engine:", "podman build -f", "deploy/docker/Dockerfile",
+             "crictl inspecti kgc/engine:",
              "step 5:", "wait for amd.com/gpu on the node",
-             "step 6:", "k8s.render -f", "| kubectl apply -f -",
+             "step 6:", "k8s.render -f", "--engine-image kgc/engine --engine-tag",
+             "| kubectl apply -f -",
              "step 7:", "wait for serving-engine Deployments", "wait for vllm-router-service",
              "step 8:", "port-forward svc/vllm-router-service 30080:80",
              "curl -sf http://127.0.0.1:30080/v1/models", "bring-up complete"]
@@ -302,3 +305,46 @@ exit 0
     c = calls(log)
     assert any("rollout status deployment" in x for x in c)
     assert any("/v1/completions" in x for x in c)
+
+
+def _stub(d, name, body):
+    d.mkdir(exist_ok=True)
+    (d / name).write_text("#!/bin/bash\n" + body)
+    (d / name).chmod(0o755)
+
+
+def test_bringup_missing_image_fails_before_apply(env, tmp_path):
+    """No engine image on the node, no podman / buildah, no --image-tar: bring-up stops
+    at step 4b with a clear message and applies nothing (instead of 30 min of
+    ImagePullBackOff at step 7)."""
+    e, root, log = env
+    d = tmp_path / "nobuild"
+    _stub(d, "crictl", f'echo "crictl $*" >> "{log}"; exit 1\n')
+    # hide the default podman / buildah stubs (and any real ones) behind failing lookups
+    _stub(d, "podman", "exit 127\n")
+    path = f"{d}:{e['PATH']}"
+    e2 = dict(e, PATH=path, PYTHON=sys.executable, WAIT_INTERVAL="0")
+    r = sh("bringup.sh", "--skip-node-setup", "--no-build", env=e2, check=False)
+    assert r.returncode != 0
+    assert "not on this node and --no-build" in r.stderr
+    assert not any(c.startswith("kubectl apply") for c in calls(log))
+    # with building allowed but the build (podman) failing: also stops before apply
+    r = sh("bringup.sh", "--skip-node-setup", env=e2, check=False)
+    assert r.returncode != 0 and "podman build of kgc/engine" in r.stderr
+    assert not any(c.startswith("kubectl apply") for c in calls(log))
+
+
+def test_bringup_side_loads_image_tar(env, tmp_path):
+    """--image-tar: podman load into CRI-O's store, then crictl inspecti, then render with
+    exactly that image."""
+    e, root, log = env
+    tar = tmp_path / "engine.tar"
+    tar.write_text("x")
+    r = sh("bringup.sh", "--single-node", "--dry-run", f"--image-tar={tar}",
+           "--image=registry.local/kgc/engine:test1", env=dict(e, PYTHON=sys.executable))
+    out = r.stdout
+    i = out.find(f"podman load -i {tar}")
+    j = out.find("crictl inspecti registry.local/kgc/engine:test1")
+    k = out.find("--engine-image registry.local/kgc/engine --engine-tag test1")
+    assert 0 <= i < j < k, out
+    assert "podman build" not in out

@@ -57,6 +57,8 @@ def main():
     ap.add_argument("--splits", default="1,2,4")
     ap.add_argument("--g", type=int, default=0, help="row-group size of the packing (0 = BN)")
     ap.add_argument("--no-lib", action="store_true")
+    ap.add_argument("--xpad", type=int, default=0,
+                    help="activation row stride K + xpad elements (L2 channel spread probe)")
     a = ap.parse_args()
     from kubernetes_gpu_cluster_amd import ops
     ops.load_extension(strict=True)
@@ -72,7 +74,7 @@ def main():
         ws = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02 for _ in range(copies)]
         wb = N * K * 2
         for M in [int(x) for x in a.ms.split(",")]:
-            x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+            x = torch.randn(M, K + a.xpad, device=dev, dtype=torch.bfloat16)[:, :K]
             ref = x.float() @ ws[0].float().t()
             out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
             if not a.no_lib:
@@ -128,6 +130,7 @@ def main():
                                 k.ring_gemm(C, x, p, cid, epi)
                         t = bench(run, max(1, 64 // copies)) / copies
                         print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "kernel": "k9r",
+                                          "xpad": a.xpad,
                                           "cfg": cid, "bm": bm, "bn": bn, "threads": thr,
                                           "slots": ns, "G": G, "S": S, "epi": epi,
                                           "us": round(t * 1e6, 2),
