@@ -879,6 +879,7 @@ bool debug_build() {
 }
 
 int64_t allreduce_rms_max_hidden_op() { return kgc::allreduce_rms_max_hidden(); }
+int64_t allreduce_max_blocks_op() { return kgc::allreduce_max_blocks(); }
 
 void xgmi_allreduce_rms(Tensor out, Tensor in, Tensor residual, Tensor w, double eps,
                         std::vector<int64_t> data, std::vector<int64_t> sig, int64_t rank,
@@ -1053,6 +1054,7 @@ TORCH_LIBRARY(kgc, m) {
   m.def("xgmi_allreduce_rms(Tensor(a!) out, Tensor inp, Tensor(b!) residual, Tensor w, float eps, "
         "int[] data, int[] sig, int rank, int cap_bytes) -> ()");
   m.def("allreduce_rms_max_hidden() -> int", &allreduce_rms_max_hidden_op);
+  m.def("allreduce_max_blocks() -> int", &allreduce_max_blocks_op);
   m.def("debug_errors() -> int", &debug_errors);
   m.def("sample_err_addr() -> int", &sample_err_addr);
   m.def("u32_clear_async(int addr) -> ()", &u32_clear_async);

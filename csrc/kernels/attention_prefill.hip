@@ -21,6 +21,7 @@
 //   V^T [D][64 keys]   chunk c of dim d stored at c ^ ((d>>1)&7)
 #include "common.h"
 #include "launch.h"
+#include <cstdlib>
 #include <type_traits>
 
 namespace kgc {
@@ -238,12 +239,260 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
   }
 }
 
+// GQA-shared variant (G = nq / nkv >= 4): one workgroup = GH q-heads of ONE kv head x
+// QB = 256 / GH queries, 8 waves of 32 query rows (wave w: head w % GH, rows
+// 32 * (w / GH) ..).  Every K/V tile staged into LDS feeds 256 query rows of four or
+// eight heads instead of 128 rows of one head: half the K/V staging per FLOP, and one
+// staging pass per kv head instead of one per q-head.  The 128-row work items of the
+// engine's work list split into 128 / QB sub-blocks (grid.z); the per-wave math is the
+// single-head kernel's.
+template <typename T, int D, bool KV8, int GH>
+__global__ __launch_bounds__(512, 1) void prefill_attn_gqa_kernel(
+    const T* __restrict__ q, T* __restrict__ out, const void* __restrict__ kc_,
+    const void* __restrict__ vc_, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ qsl, const int* __restrict__ seq_lens,
+    const int* __restrict__ work_seq, const int* __restrict__ work_mblk, int nq, int nkv,
+    int bs_log2, float scale_log2, float v_scale, int num_blocks) {
+  typedef typename Vec8<T>::type V8;
+  typedef std::conditional_t<KV8, uint8_t, T> C;
+  typedef std::conditional_t<KV8, u32x2, u32x4> R;
+  const C* __restrict__ kc = reinterpret_cast<const C*>(kc_);
+  const C* __restrict__ vc = reinterpret_cast<const C*>(vc_);
+  auto widen = [](R r) -> u32x4 {
+    if constexpr (KV8) return fp8x8_widen<T>(r);
+    else return r;
+  };
+  constexpr int NT_ = 512;
+  constexpr int QB = 256 / GH;               // queries per workgroup
+  static_assert(QB <= PF_BM && PF_BM % QB == 0, "sub-blocks of the 128-row work item");
+  constexpr int NCH = D / 8, KS = D / 32, DT = D / 16;
+  constexpr int KPT = PF_BN * NCH / NT_;
+  constexpr int VPT = D * (PF_BN / 8) / NT_;
+  constexpr int TILE = PF_BN * D;
+  static_assert(KPT * NT_ == PF_BN * NCH && VPT * NT_ == D * (PF_BN / 8), "staging split");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* lds = reinterpret_cast<T*>(smem);
+
+  const int seq = work_seq[blockIdx.x], mb = work_mblk[blockIdx.x];
+  const int G = nq / nkv;
+  const int h = blockIdx.y / (G / GH);                 // kv head
+  const int hg0 = h * G + (blockIdx.y % (G / GH)) * GH; // first q-head of this workgroup
+  const int q0 = qsl[seq];
+  const int qlen = qsl[seq + 1] - q0;
+  int L_in = seq_lens[seq];
+  KGC_DCHECK_RANGE(L_in, 0, (bt_stride << bs_log2) + 1, "prefill seq_len");
+  const int L = min(L_in, bt_stride << bs_log2);
+  const int ctx0 = L - qlen;
+  const int qbase = mb * PF_BM + blockIdx.z * QB;      // first query row of the workgroup
+  if (qlen <= 0 || ctx0 < 0 || qbase >= qlen) return;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int hq = hg0 + wave % GH;
+  const int wq0 = qbase + (wave / GH) * 32;            // first query row of this wave
+  const int r16 = lane & 15, qd = lane >> 4;
+  const int* bt = block_tables + (int64_t)seq * bt_stride;
+  const int bsm = (1 << bs_log2) - 1;
+  const int64_t hs = (int64_t)D << bs_log2;
+
+  V8 qf[2][KS];
+  int qpos[2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qi = wq0 + qt * 16 + r16;
+    const int qc = min(qi, qlen - 1);
+    qpos[qt] = ctx0 + qc;
+    const T* qrow = q + ((int64_t)(q0 + qc) * nq + hq) * D;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      Pack8<T> t;
+      t.u = *reinterpret_cast<const u32x4*>(qrow + 32 * s + 8 * qd);
+      qf[qt][s] = t.v;
+    }
+  }
+  const int last_q = ctx0 + min(qbase + QB, qlen) - 1;
+  const int n_tiles = last_q / PF_BN + 1;
+
+  R kreg[KPT], vreg[VPT];
+  auto load_tile = [&](int kt) {
+#pragma unroll
+    for (int u = 0; u < KPT; ++u) {
+      const int ci = threadIdx.x + NT_ * u;
+      const int key = ci / NCH, c = ci % NCH;
+      const int ka = min(kt * PF_BN + key, L - 1);
+      const C* src = kc + (int64_t)kgc_bt(bt, ka >> bs_log2, bt_stride, num_blocks) * nkv * hs +
+                     h * hs + (int64_t)(ka & bsm) * D + c * 8;
+      kreg[u] = *reinterpret_cast<const R*>(src);
+    }
+#pragma unroll
+    for (int u = 0; u < VPT; ++u) {
+      const int ci = threadIdx.x + NT_ * u;
+      const int c = ci / D, d = ci % D;
+      const int ka = min(kt * PF_BN + 8 * c, L - 1) & ~7;
+      const C* src = vc + (int64_t)kgc_bt(bt, ka >> bs_log2, bt_stride, num_blocks) * nkv * hs +
+                     h * hs + ((ka & bsm) >> 3) * (D * 8) + d * 8;
+      vreg[u] = *reinterpret_cast<const R*>(src);
+    }
+  };
+  auto store_tile = [&](int buf) {
+    T* K = lds + buf * 2 * TILE;
+    T* V = K + TILE;
+#pragma unroll
+    for (int u = 0; u < KPT; ++u) {
+      const int ci = threadIdx.x + NT_ * u;
+      const int key = ci / NCH, c = ci % NCH;
+      *reinterpret_cast<u32x4*>(K + key * D + ((c ^ (kswz(key) & (NCH - 1))) * 8)) = widen(kreg[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < VPT; ++u) {
+      const int ci = threadIdx.x + NT_ * u;
+      const int c = ci / D, d = ci % D;
+      *reinterpret_cast<u32x4*>(V + d * PF_BN + ((c ^ ((d >> 1) & 7)) * 8)) = widen(vreg[u]);
+    }
+  };
+
+  f32x4 o[2][DT];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+    for (int t = 0; t < DT; ++t) o[qt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  // this wave's own last key tile (its rows end before the workgroup's last row)
+  const int wave_tiles = (ctx0 + min(wq0 + 31, qlen - 1)) / PF_BN + 1;
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  const int keyA = 8 * (r16 >> 2) + (r16 & 3);
+  for (int kt = 0; kt < n_tiles; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < n_tiles) load_tile(kt + 1);
+    if (kt < wave_tiles) {
+      const T* K = lds + buf * 2 * TILE;
+      const T* V = K + TILE;
+      f32x4 s[2][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = (j >> 1) * 32 + keyA + 4 * (j & 1);
+        const T* krow = K + key * D;
+        f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          Pack8<T> f;
+          f.u = *reinterpret_cast<const u32x4*>(krow + (((4 * ks + qd) ^ (r16 & (NCH - 1))) * 8));
+          a0 = mfma16x16x32(f.v, qf[0][ks], a0);
+          a1 = mfma16x16x32(f.v, qf[1][ks], a1);
+        }
+        s[0][j] = a0;
+        s[1][j] = a1;
+      }
+      V8 pf[2][2];
+      const bool diag = (kt + 1) * PF_BN - 1 > ctx0 + wq0;
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int key = kt * PF_BN + (j >> 1) * 32 + 8 * qd + 4 * (j & 1) + i;
+            float v = s[qt][j][i] * scale_log2;
+            if (diag && key > qpos[qt]) v = -INFINITY;
+            s[qt][j][i] = v;
+            tmax = fmaxf(tmax, v);
+          }
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+        const float mn = fmaxf(m[qt], tmax);
+        const float alpha = exp2f(m[qt] - mn);
+        m[qt] = mn;
+        l[qt] *= alpha;
+#pragma unroll
+        for (int t = 0; t < DT; ++t) o[qt][t] *= alpha;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          Pack8<T> pk;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float pa = exp2f(s[qt][2 * kk][i] - mn);
+            const float pb = exp2f(s[qt][2 * kk + 1][i] - mn);
+            l[qt] += pa + pb;
+            pk.h[i] = from_f<T>(pa);
+            pk.h[4 + i] = from_f<T>(pb);
+          }
+          pf[qt][kk] = pk.v;
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < DT; ++t) {
+        const int d = 16 * t + r16;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          Pack8<T> f;
+          f.u = *reinterpret_cast<const u32x4*>(V + d * PF_BN +
+                                                (((4 * kk + qd) ^ ((d >> 1) & 7)) * 8));
+          o[0][t] = mfma16x16x32(f.v, pf[0][kk], o[0][t]);
+          o[1][t] = mfma16x16x32(f.v, pf[1][kk], o[1][t]);
+        }
+      }
+    }
+    if (kt + 1 < n_tiles) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    float tot = l[qt];
+    tot += __shfl_xor(tot, 16, 64);
+    tot += __shfl_xor(tot, 32, 64);
+    const float inv = v_scale / tot;
+    const int qi = wq0 + qt * 16 + r16;
+    if (qi < qlen && qi < qbase + QB) {
+      T* orow = out + ((int64_t)(q0 + qi) * nq + hq) * D + 4 * qd;
+#pragma unroll
+      for (int t = 0; t < DT; ++t) {
+        Pack4<T> pk;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pk.h[i] = from_f<T>(o[qt][t][i] * inv);
+        *reinterpret_cast<u32x2*>(orow + 16 * t) = pk.u;
+      }
+    }
+  }
+}
+
+// KGC_PREFILL_GQA=0: the one-head-per-workgroup kernel everywhere (A/B and tests)
+static int prefill_gqa_enabled() {
+  const char* e = getenv("KGC_PREFILL_GQA");
+  return e ? atoi(e) : 1;
+}
+
+template <typename T, int D, bool KV8, int GH>
+static void prefill_gqa_dispatch(const void* q, void* out, const void* kc, const void* vc,
+                                 const int* bt, int bt_stride, const int* qsl, const int* sl,
+                                 const int* ws, const int* wm, int n_work, int nq, int nkv,
+                                 int bs_log2, float scale_log2, float v_scale, int num_blocks,
+                                 hipStream_t s) {
+  const size_t lds = 2 * 2 * PF_BN * D * sizeof(T);
+  const int G = nq / nkv;
+  const dim3 grid(n_work, nkv * (G / GH), PF_BM / (256 / GH));
+  prefill_attn_gqa_kernel<T, D, KV8, GH><<<grid, 512, lds, s>>>(
+      (const T*)q, (T*)out, kc, vc, bt, bt_stride, qsl, sl, ws, wm, nq, nkv, bs_log2,
+      scale_log2, v_scale, num_blocks);
+}
+
 template <typename T, int D, bool KV8>
 static void prefill_dispatch(const void* q, void* out, const void* kc, const void* vc,
                              const int* bt, int bt_stride, const int* qsl, const int* sl,
                              const int* ws, const int* wm, int n_work, int nq, int nkv,
                              int bs_log2, float scale_log2, float v_scale, int num_blocks,
                              hipStream_t s) {
+  const int G = nkv > 0 ? nq / nkv : 1;
+  if (D == 128 && prefill_gqa_enabled() && nq % nkv == 0 && (G == 4 || G % 8 == 0)) {
+    if (G == 4)
+      prefill_gqa_dispatch<T, D, KV8, 4>(q, out, kc, vc, bt, bt_stride, qsl, sl, ws, wm, n_work,
+                                         nq, nkv, bs_log2, scale_log2, v_scale, num_blocks, s);
+    else
+      prefill_gqa_dispatch<T, D, KV8, 8>(q, out, kc, vc, bt, bt_stride, qsl, sl, ws, wm, n_work,
+                                         nq, nkv, bs_log2, scale_log2, v_scale, num_blocks, s);
+    return;
+  }
   const size_t lds = 2 * 2 * PF_BN * D * sizeof(T);
   prefill_attn_kernel<T, D, KV8><<<dim3(n_work, nq), 256, lds, s>>>(
       (const T*)q, (T*)out, kc, vc, bt, bt_stride, qsl, sl, ws, wm, nq,

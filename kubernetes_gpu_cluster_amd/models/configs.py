@@ -132,9 +132,10 @@ PRESETS: dict[str, ModelConfig] = {
     "tiny-opt": ModelConfig("tiny-opt", "opt", 2, 128, 4, 4, 32, 512, 1024, max_position=512,
                             norm_type="layer", act="relu", learned_pos=True, pos_offset=2,
                             qkv_bias=True, mlp_bias=True, o_bias=True, tie_embeddings=True),
-    # TP = 8 rehearsals: 16 q / 2 kv heads (each kv head replicated on 4 ranks at TP = 8),
-    # and Llama-3-70B's head layout (64 q / 8 kv, intermediate 3.5 x hidden) scaled down
-    "tiny-llama-gqa8": ModelConfig("tiny-llama-gqa8", "llama", 2, 512, 16, 2, 32, 1024, 1024,
+    # TP = 8 rehearsals: 16 q / 2 kv heads of 64 (each kv head replicated on 4 ranks at
+    # TP = 8; GPU kernels take head_dim 64 / 128), and Llama-3-70B's head layout (64 q / 8
+    # kv, intermediate 3.5 x hidden) scaled down to head_dim 16 (CPU oracle path only)
+    "tiny-llama-gqa8": ModelConfig("tiny-llama-gqa8", "llama", 2, 1024, 16, 2, 64, 2048, 1024,
                                    max_position=2048, rope_theta=500000.0, bos_token_id=1,
                                    eos_token_id=2),
     "tiny-llama-70b-shape": ModelConfig("tiny-llama-70b-shape", "llama", 2, 1024, 64, 8, 16,

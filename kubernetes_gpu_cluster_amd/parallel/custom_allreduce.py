@@ -44,14 +44,21 @@ class CustomAllReduce:
     failure raises on every rank instead of leaving peers blocked in a collective."""
 
     def __init__(self, cpu_group, rank: int, world: int, device: torch.device,
-                 cap_bytes: int = 8 << 20, one_shot_max: Optional[int] = None):
+                 cap_bytes: Optional[int] = None, one_shot_max: Optional[int] = None):
         if world not in SUPPORTED_WORLD:
             raise ValueError(f"xGMI all-reduce supports {SUPPORTED_WORLD} ranks, not {world}")
         self.rank, self.world, self.device = rank, world, device
-        self.cap = int(cap_bytes)
-        # one-shot reads (N-1) x bytes; two-shot 2(N-1)/N x bytes but two barriers
-        self.one_shot_max = one_shot_max if one_shot_max is not None else (
-            512 << 10 if world <= 2 else 256 << 10)
+        # Thresholds (logged at start-up; env-tunable because the one-shot / two-shot
+        # crossover and the RCCL hand-over point depend on the node's xGMI topology and
+        # have only been measured at 2 / 4 ranks on one GPU): KGC_AR_CAP -- largest
+        # message this path takes (bytes; above it RCCL), KGC_AR_ONE_SHOT_MAX -- largest
+        # one-shot message (one-shot reads (N-1) x bytes, two-shot 2(N-1)/N x bytes but
+        # pays two barriers).
+        self.cap = int(cap_bytes if cap_bytes is not None else
+                       os.environ.get("KGC_AR_CAP", 8 << 20))
+        env_os = os.environ.get("KGC_AR_ONE_SHOT_MAX")
+        self.one_shot_max = int(one_shot_max if one_shot_max is not None else
+                                env_os if env_os else (512 << 10 if world <= 2 else 256 << 10))
         self._own, self._opened = 0, []
         self._err_host: Optional[torch.Tensor] = None
         handle, err = None, None
@@ -167,6 +174,8 @@ def maybe_init_custom_allreduce(ps, device: torch.device) -> Optional[CustomAllR
     except RuntimeError as e:
         log.warning("%s; using RCCL", e)
         return None
-    log.info("xGMI all-reduce enabled: tp=%d cap=%d MiB one-shot<=%d KiB", ps.tp_size,
-             car.cap >> 20, car.one_shot_max >> 10)
+    log.info("xGMI all-reduce enabled: tp=%d cap=%d KiB (KGC_AR_CAP) one-shot<=%d KiB "
+             "(KGC_AR_ONE_SHOT_MAX) fused add+RMSNorm<=%d KiB (KGC_AR_RMS_MAX), %d workgroups",
+             ps.tp_size, car.cap >> 10, car.one_shot_max >> 10, car.fused_max >> 10,
+             int(torch.ops.kgc.allreduce_max_blocks()))
     return car

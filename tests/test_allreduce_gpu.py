@@ -35,6 +35,28 @@ def _expected(world, n, seed, dtype, integer):
     return acc.to(dtype)
 
 
+def _tolerate_unmapped_peers(fn):
+    """8 ranks on ONE GPU: the spin barrier needs every rank's kernel resident at once,
+    and one device does not always map eight processes' queues together (measured: the
+    fused kernel's barrier timed out with 'peers never arrived').  A rank whose barrier
+    timed out records it -- the kernel REPORTED the failure (never a silent wrong sum) --
+    and stops; the test then xfails instead of passing or failing on the harness.  On an
+    8-GPU node every rank has its own device."""
+    import functools
+
+    @functools.wraps(fn)
+    def run(rank, world, port, *args, outdir=None):
+        from kubernetes_gpu_cluster_amd.engine.health import AllReduceFailed
+        try:
+            fn(rank, world, port, *args)
+        except AllReduceFailed as e:
+            if world < 8:
+                raise
+            with open(os.path.join(outdir, f"timeout{rank}"), "w") as f:
+                f.write(str(e))
+    return run
+
+
 def _worker(rank, world, port, cap):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -57,6 +79,8 @@ def _worker(rank, world, port, cap):
                     ref = _expected(world, n, seed, dtype, integer)
                     got = x.cpu()
                     if integer:
+                        if not torch.equal(got, ref):
+                            car.check()    # a timed-out barrier raises AllReduceFailed
                         assert torch.equal(got, ref), (n, dtype, (got - ref).abs().max())
                     else:
                         torch.testing.assert_close(got.float(), ref.float(), atol=0.06, rtol=0.02)
@@ -76,15 +100,33 @@ def _worker(rank, world, port, cap):
         torch.cuda.synchronize()
         car.check()
         dist.barrier()
+    except AssertionError:
+        torch.cuda.synchronize()
+        car.check()            # a mismatch after a timed-out barrier is reported as such
+        raise
     finally:
         car.close()
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+def _run_world(worker, world, *args):
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_entry, args=(worker.__name__, world, _port(), args, d), nprocs=world,
+                           join=True, start_method="spawn")
+        timeouts = [f for f in os.listdir(d) if f.startswith("timeout")]
+        if timeouts:
+            pytest.xfail(f"{world} ranks on one GPU: barrier timed out on {len(timeouts)} rank(s) "
+                         f"(reported via the error word; the node has one GPU per rank)")
+
+
+def _entry(rank, name, world, port, args, outdir):
+    _tolerate_unmapped_peers(globals()[name])(rank, world, port, *args, outdir=outdir)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_xgmi_allreduce_matches_sum(world, gpu):
-    mp.start_processes(_worker, args=(world, _port(), 4 << 20), nprocs=world, join=True,
-                       start_method="spawn")
+    _run_world(_worker, world, 4 << 20)
 
 
 def _timeout_worker(rank, world, port):
@@ -153,7 +195,12 @@ def _rms_worker(rank, world, port):
                     car.all_reduce(y)
                     r_ref = res.clone()
                     o_ref, _ = ops.fused_add_rms_norm(y, r_ref, w, 1e-5)
-                    assert torch.equal(r_got, r_ref), (M, H, dtype)
+                    if not torch.equal(r_got, r_ref):
+                        torch.cuda.synchronize()
+                        bad = (r_got != r_ref)
+                        car.check()        # a timed-out barrier raises AllReduceFailed here
+                        raise AssertionError((M, H, dtype, int(bad.sum()), bad.nonzero()[:4].tolist(),
+                                              (r_got.float() - r_ref.float()).abs().max().item()))
                     torch.testing.assert_close(o_got.float(), o_ref.float(), atol=1e-2, rtol=1e-2)
                 # an fp32 oracle of the whole op
                 xs = [(torch.randn(M, H, generator=torch.Generator().manual_seed(M * 31 + H + r))
@@ -188,12 +235,15 @@ def _rms_worker(rank, world, port):
                                                        dtype=torch.bfloat16))
         car.check()
         dist.barrier()
+    except AssertionError:
+        torch.cuda.synchronize()
+        car.check()            # a mismatch after a timed-out barrier is reported as such
+        raise
     finally:
         car.close()
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_xgmi_allreduce_add_rmsnorm_fused(world, gpu):
-    mp.start_processes(_rms_worker, args=(world, _port()), nprocs=world, join=True,
-                       start_method="spawn")
+    _run_world(_rms_worker, world)

@@ -4,6 +4,7 @@ import pytest
 import torch
 
 from kubernetes_gpu_cluster_amd.engine.config import EngineConfig
+from kubernetes_gpu_cluster_amd.engine.health import AllReduceFailed
 from kubernetes_gpu_cluster_amd.engine.llm_engine import LLMEngine
 from kubernetes_gpu_cluster_amd.engine.sequence import SamplingParams
 from kubernetes_gpu_cluster_amd.models import PRESETS, build_model, full_state_dict_random
@@ -162,20 +163,24 @@ def test_engine_preemption_recompute(gpu):
     assert eng.bm.num_free == eng.bm.num_blocks - 1
 
 
-@pytest.mark.parametrize("eager", [True, False])
-def test_tp2_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch, eager):
-    """The tensor-parallel engine on the GPU: two ranks share cuda:0 (gloo process group,
+@pytest.mark.parametrize("tp,eager,name", [(2, True, "tiny-llama"), (2, False, "tiny-llama"),
+                                          (4, False, "tiny-llama"),
+                                          (8, False, "tiny-llama-gqa8")])
+def test_tp_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch, tp, eager, name):
+    """The tensor-parallel engine on the GPU: TP ranks share cuda:0 (gloo process group,
     since RCCL refuses two ranks on one device), sharded QKV/MLP/vocab layers, the xGMI
     all-reduce kernel over IPC buffers for the row-parallel sums, multiprocess workers.
     eager=False is the production decode path: hipGraph-captured decode buckets with
     the xGMI all-reduce INSIDE the graphs, and vocab-parallel sampling after the replay
-    (no logits all-gather).  Greedy continuations match TP=1 (bf16; sharded sums round
-    differently, so a couple of late near-tie flips are tolerated)."""
+    (no logits all-gather).  TP = 4 replicates tiny-llama's 2 kv heads over 4 ranks; TP = 8
+    (BASELINE config 3's degree) runs the 8-rank all-reduce instantiation with each of
+    tiny-llama-gqa8's 2 kv heads on 4 ranks.  Greedy continuations match TP=1 (bf16;
+    sharded sums round differently, so a couple of late near-tie flips are tolerated)."""
     import json
     import os
     from safetensors.torch import save_file
     from kubernetes_gpu_cluster_amd.engine.llm_engine import LLM
-    cfg = PRESETS["tiny-llama"]
+    cfg = PRESETS[name]
     d = str(tmp_path / "m")
     os.makedirs(d)
     save_file({k: v.contiguous() for k, v in full_state_dict_random(cfg, seed=5, std=0.15).items()},
@@ -191,16 +196,27 @@ def test_tp2_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch, eager):
     sp = [SamplingParams(temperature=0, max_tokens=8, ignore_eos=True)] * 3
     outs = {}
     monkeypatch.setenv("KGC_DIST_BACKEND", "gloo")
-    for tp in (1, 2):
+    tp_n = tp
+    for tp in (1, tp_n):
         llm = LLM(d, device="cuda", dtype="bfloat16", tensor_parallel_size=tp, enforce_eager=eager,
                   max_model_len=256, max_num_seqs=4, max_num_batched_tokens=128,
                   num_gpu_blocks_override=64)
-        if tp == 2:
+        if tp > 1:
             from kubernetes_gpu_cluster_amd.parallel import comm
             car = comm.get_custom_allreduce()
-            assert car is not None, "xGMI all-reduce was not set up for TP=2"
-        outs[tp] = [o.output_token_ids for o in llm.generate(prompts, sp)]
-        if tp == 2:
+            assert car is not None, f"xGMI all-reduce was not set up for TP={tp}"
+            assert car.world == tp
+        try:
+            outs[tp] = [o.output_token_ids for o in llm.generate(prompts, sp)]
+        except AllReduceFailed as e:
+            llm.shutdown()
+            if tp < 8:
+                raise
+            # eight ranks' spin barriers on ONE GPU need all eight processes' kernels
+            # resident at once, which one device does not always grant
+            # (test_allreduce_gpu.py); the engine reported it instead of serving garbage
+            pytest.xfail(f"TP=8 on one GPU: {e}")
+        if tp > 1:
             car.check()
             assert car.fused_calls > 0, "fused all-reduce + add + RMSNorm never ran"
             st = llm.engine.executor.runner.stats
@@ -208,8 +224,8 @@ def test_tp2_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch, eager):
             if not eager:
                 assert st["graph_steps"] > 0, st
         llm.shutdown()
-    same = sum(a == b for x, y in zip(outs[1], outs[2]) for a, b in zip(x, y))
-    assert all(x[0] == y[0] for x, y in zip(outs[1], outs[2])), outs
+    same = sum(a == b for x, y in zip(outs[1], outs[tp_n]) for a, b in zip(x, y))
+    assert all(x[0] == y[0] for x, y in zip(outs[1], outs[tp_n])), outs
     assert same >= 0.8 * sum(len(x) for x in outs[1]), outs
 
 
@@ -303,7 +319,8 @@ def test_rccl_collectives_capture_in_hipgraph(gpu):
     assert p.exitcode == 0
 
 
-def test_mixtral_ep2_graphs_on_one_gpu(gpu, tmp_path, monkeypatch):
+@pytest.mark.parametrize("ep", [2, 4])
+def test_mixtral_ep_graphs_on_one_gpu(gpu, tmp_path, monkeypatch, ep):
     """Mixtral with --moe-parallel ep at TP = 2 (two ranks on cuda:0, gloo group): decode
     steps replay hipGraphs with the device-side expert all-to-all inside.  Greedy output
     equals the eager EP engine that exchanges through all_to_all with host-side counts
@@ -329,13 +346,13 @@ def test_mixtral_ep2_graphs_on_one_gpu(gpu, tmp_path, monkeypatch):
     sp = [SamplingParams(temperature=0, max_tokens=8, ignore_eos=True)] * 3
     monkeypatch.setenv("KGC_DIST_BACKEND", "gloo")
     outs = {}
-    for tp, ipc in ((1, "1"), (2, "1"), (2, "0")):
+    for tp, ipc in ((1, "1"), (ep, "1"), (ep, "0")):
         monkeypatch.setenv("KGC_EP_IPC", ipc)
         llm = LLM(d, device="cuda", dtype="bfloat16", tensor_parallel_size=tp,
                   moe_parallel="ep", max_model_len=256, max_num_seqs=4, enforce_eager=ipc == "0",
                   max_num_batched_tokens=128, num_gpu_blocks_override=64)
         outs[(tp, ipc)] = [o.output_token_ids for o in llm.generate(prompts, sp)]
-        if tp == 2 and ipc == "1":
+        if tp == ep and ipc == "1":
             w = llm.engine.executor.worker
             assert w.ep_a2a is not None, "device-side EP all-to-all not set up"
             assert llm.engine.executor.runner.stats["graph_steps"] > 0
@@ -343,8 +360,8 @@ def test_mixtral_ep2_graphs_on_one_gpu(gpu, tmp_path, monkeypatch):
         llm.shutdown()
     # the device-side exchange (graphs) computes exactly what the host-count all-to-all
     # computes eagerly; vs TP = 1 only rounding differs (near-tie expert flips late on)
-    assert outs[(2, "1")] == outs[(2, "0")], outs
-    assert all(x[:3] == y[:3] for x, y in zip(outs[(1, "1")], outs[(2, "1")])), outs
+    assert outs[(ep, "1")] == outs[(ep, "0")], outs
+    assert all(x[:3] == y[:3] for x, y in zip(outs[(1, "1")], outs[(ep, "1")])), outs
 
 
 def test_pp2_stage_graphs_on_one_gpu(gpu, tmp_path, monkeypatch):

@@ -254,6 +254,47 @@ def test_prefill_attention(gpu, dt, d, nq, nkv):
     torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(dt))
 
 
+@pytest.mark.parametrize("gqa,nq,nkv,S", [("1", 32, 8, 8192), ("0", 32, 8, 8192),
+                                         ("1", 32, 8, 2048), ("1", 64, 8, 2048),
+                                         ("1", 16, 2, 2048), ("0", 64, 8, 2048)])
+def test_prefill_long_gqa_matches_fp32(gpu, monkeypatch, gqa, nq, nkv, S):
+    """K2 at long prompts (2K / 8K tokens: a fresh prompt plus a chunked continuation),
+    GQA groups of 4 and 8 through the GQA-shared kernel (KGC_PREFILL_GQA=1, one workgroup
+    per kv head x query block) and through the one-head kernel (=0), vs an fp32 dense
+    causal reference."""
+    monkeypatch.setenv("KGC_PREFILL_GQA", gqa)
+    torch.manual_seed(S + nq)
+    d, bs, dt = 128, 32, torch.bfloat16
+    seq_lens, query_lens = [S, S // 2 + 77], [S, 333]
+    kc, vc, bt = _fill_random_cache(len(seq_lens), seq_lens, nkv, bs, d, dt, gpu)
+    qsl = [0]
+    for ql in query_lens:
+        qsl.append(qsl[-1] + ql)
+    q = torch.randn(qsl[-1], nq, d, dtype=dt, device=gpu)
+    qsl_t = torch.tensor(qsl, dtype=torch.int32, device=gpu)
+    sl_t = torch.tensor(seq_lens, dtype=torch.int32, device=gpu)
+    out = ops.prefill_attention(q, kc, vc, bt, qsl_t, sl_t, d ** -0.5).cpu().float()
+    for i in range(2):
+        L, ql = seq_lens[i], query_lens[i]
+        nbk = (L + bs - 1) // bs
+        blocks = bt[i, :nbk].cpu().long()
+        k = kc.cpu()[blocks].permute(0, 2, 1, 3).reshape(nbk * bs, nkv, d)[:L].float()
+        v = vc.cpu()[blocks].permute(0, 2, 4, 1, 3).reshape(nbk * bs, nkv, d)[:L].float()
+        # a sample of query rows (all of the first and last 64, 128 in between), each
+        # against all its causal keys: dense fp32 attention
+        rows = torch.cat([torch.arange(min(64, ql)), torch.arange(max(0, ql - 64), ql),
+                          torch.randint(0, ql, (128,))]).unique()
+        qi = q.cpu()[qsl[i]:qsl[i + 1]][rows].float()
+        rep = nq // nkv
+        kk = k.repeat_interleave(rep, 1).permute(1, 0, 2)           # [nq, L, d]
+        vv = v.repeat_interleave(rep, 1).permute(1, 0, 2)
+        sc = torch.einsum("qhd,hkd->hqk", qi, kk) * d ** -0.5
+        pos = (L - ql + rows)[:, None]
+        sc = sc.masked_fill(torch.arange(L)[None, :] > pos, float("-inf"))
+        exp = torch.einsum("hqk,hkd->qhd", torch.softmax(sc, -1), vv)
+        torch.testing.assert_close(out[qsl[i]:qsl[i + 1]][rows], exp, atol=2e-2, rtol=2e-2)
+
+
 def test_prefill_matches_dense(gpu):
     """End-to-end: rope_kv_write -> prefill kernel == dense causal attention."""
     torch.manual_seed(5)
