@@ -81,27 +81,42 @@ __device__ __forceinline__ int64_t rg_silu_row(int64_t p, int I) {
 
 // CW = WM * WN MFMA waves and LW loader waves.  The weight operand is packed with
 // G = BN (ring_pack): every K-step of a column tile is one contiguous BN x 128 B block.
-template <int BM, int BN, int WM, int WN, int LW, int NS, int WAUX, int EPI>
+// NSB = 0: one ring of NS slots, each holding a K-step of both operands, every loader
+// issuing both.  NSB > 0 (split rings): the activation ring has NS slots and the weight
+// ring NSB slots of their own; loader waves [0, LW/2) move activations, [LW/2, LW)
+// weights, each group waiting only on its own DMAs -- the weight stream (HBM, long
+// latency, small slots) can run many more K-steps ahead than the activation stream (L2,
+// large slots) within the same 160 KiB.
+template <int BM, int BN, int WM, int WN, int LW, int NS, int WAUX, int EPI, int NSB = 0>
 __global__ __launch_bounds__((WM * WN + LW) * 64, 1) void ring_gemm_kernel(
     void* __restrict__ Cv, const bf16* __restrict__ X, const bf16* __restrict__ Wp, int M,
     int N, int K, int64_t ldx, int S, int MB, int64_t slice_stride, int xmap, int wt, int abl) {
   constexpr int CW = WM * WN;
-  static_assert(LW >= 1, "dedicated loader waves");
-  constexpr int D = NS - 1;                       // K-steps in flight
+  constexpr bool SPLIT = NSB > 0;
+  static_assert(LW >= 1 && (!SPLIT || LW % 2 == 0), "dedicated loader waves");
+  constexpr int LWA = SPLIT ? LW / 2 : LW, LWB = SPLIT ? LW / 2 : LW;
+  constexpr int D = NS - 1;                       // activation K-steps in flight
+  constexpr int DB = SPLIT ? NSB - 1 : D;         // weight K-steps in flight
   constexpr int PA = BM / 8, PB = BN / 8;         // 1-KiB DMA pieces per K-step
-  static_assert(PA % LW == 0, "activation pieces split evenly over the loaders");
+  static_assert(PA % LWA == 0, "activation pieces split evenly over the loaders");
   // loader w issues LA activation pieces and LB (+1 for w < RB) weight pieces per step:
   // compile-time counts, so the per-step issue is a straight run of DMAs with no branch
-  constexpr int LA = PA / LW, LB = PB / LW, RB = PB % LW;
-  constexpr int LMAX = LA + LB + (RB ? 1 : 0);
-  constexpr int SLOT = (BM + BN) * RG_ROWB;
+  constexpr int LA = PA / LWA, LB = PB / LWB, RB = PB % LWB;
+  constexpr int LMAX = SPLIT ? (LA > LB + (RB ? 1 : 0) ? LA : LB + (RB ? 1 : 0))
+                             : LA + LB + (RB ? 1 : 0);
+  constexpr int XSLOT = BM * RG_ROWB, WSLOT = BN * RG_ROWB;
+  constexpr int SLOT = SPLIT ? XSLOT : (BM + BN) * RG_ROWB;
+  constexpr int LDS_BYTES = SPLIT ? NS * XSLOT + NSB * WSLOT : NS * SLOT;
   constexpr int MT = BM / WM / 16, NT = BN / WN / 16;
   static_assert(MT * WM * 16 == BM && NT * WN * 16 == BN, "wave tiling");
-  static_assert(NS >= 2 && NS * SLOT <= 163840, "LDS ring exceeds 160 KiB");
-  static_assert(D * LMAX <= 63, "vmcnt range");
+  static_assert(NS >= 2 && (!SPLIT || NSB >= 2) && LDS_BYTES <= 163840,
+                "LDS rings exceed 160 KiB");
+  static_assert(SPLIT ? ((D - 1) * LA <= 63 && (DB - 1) * (LB + (RB ? 1 : 0)) <= 63)
+                       : (D - 1) * LMAX <= 63, "vmcnt range");
   // ONE shared array (a second __shared__ object can make hipcc emit vmcnt(0) before the
   // first ds_read of every step)
-  __shared__ __attribute__((aligned(16))) char lds[NS * SLOT];
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  char* const wring = lds + NS * XSLOT;           // SPLIT: the weight ring
 
   // the wave index as a scalar: role selection is one SALU branch
   const int tid = threadIdx.x, lane = tid & 63;
@@ -141,36 +156,47 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, 1) void ring_gemm_kernel(
   const char* const Xb = reinterpret_cast<const char*>(X);
   const int64_t wstep = (int64_t)BN * RG_BK * 2;  // bytes per K-step of one column tile
   const char* const Wb = reinterpret_cast<const char*>(Wp) + (int64_t)nb * nk_all * wstep;
-  const int extra_b = (RB && iw < RB) ? 1 : 0;
+  // SPLIT: loaders [0, LWA) are the activation group (ia), [LWA, LW) the weight group (ib)
+  const bool a_loader = issuer && (!SPLIT || iw < LWA);
+  const bool b_loader = issuer && (!SPLIT || iw >= LWA);
+  const int ia = iw, ib = SPLIT ? iw - LWA : iw;
+  const int extra_b = (RB && ib < RB) ? 1 : 0;
   if (issuer) {
 #pragma unroll
     for (int t = 0; t < LA; ++t) {
-      int r = m0 + (iw * LA + t) * 8 + drow;
+      int r = m0 + (ia * LA + t) * 8 + drow;
       r = r < M ? r : M - 1;                      // padded rows re-read the last row
       voa[t] = (uint32_t)(((int64_t)r * ldx + dchunk * 8) * 2);
     }
 #pragma unroll
     for (int t = 0; t < LB + 1; ++t) {
-      const int q = t < LB ? iw * LB + t : LW * LB + iw;   // B piece: tile rows 8q .. 8q+7
+      const int q = t < LB ? ib * LB + t : LWB * LB + ib;  // B piece: tile rows 8q .. 8q+7
       vob[t] = (uint32_t)((q * 8 * RG_BK + lane * 8) * 2);
     }
   }
 
-  auto issue = [&](int step) {
-    char* base = lds + (step % NS) * SLOT;
+  auto kstep = [&](int step) {
     int st = step + rot;
     st = st >= nk ? st - nk : st;
-    const int kb = kb0 + st;
-    const char* xa = Xb + (int64_t)kb * (RG_BK * 2);
-    const char* wa = Wb + (int64_t)kb * wstep;
-    // weights: WAUX = 2 (nt) streams them past L2 (each weight byte is read by ONE
-    // workgroup when BM covers all rows); activations keep the default policy
+    return kb0 + st;
+  };
+  // weights: WAUX = 2 (nt) streams them past L2 (each weight byte is read by ONE
+  // workgroup when BM covers all rows); activations keep the default policy
+  auto issue_b = [&](int step, char* base) {
+    const char* wa = Wb + (int64_t)kstep(step) * wstep;
 #pragma unroll
-    for (int t = 0; t < LB; ++t)
-      rg_glds16<WAUX>(wa + vob[t], base + (PA + iw * LB + t) * 1024);
-    if (RB && extra_b) rg_glds16<WAUX>(wa + vob[LB], base + (PA + LW * LB + iw) * 1024);
+    for (int t = 0; t < LB; ++t) rg_glds16<WAUX>(wa + vob[t], base + (ib * LB + t) * 1024);
+    if (RB && extra_b) rg_glds16<WAUX>(wa + vob[LB], base + (LWB * LB + ib) * 1024);
+  };
+  auto issue_a = [&](int step, char* base) {
+    const char* xa = Xb + (int64_t)kstep(step) * (RG_BK * 2);
 #pragma unroll
-    for (int t = 0; t < LA; ++t) rg_glds16<0>(xa + voa[t], base + (iw * LA + t) * 1024);
+    for (int t = 0; t < LA; ++t) rg_glds16<0>(xa + voa[t], base + (ia * LA + t) * 1024);
+  };
+  auto issue = [&](int step) {                    // unified ring: both operands, one slot
+    char* base = lds + (step % NS) * SLOT;
+    issue_b(step, base + PA * 1024);
+    issue_a(step, base);
   };
 
   f32x4 acc[MT][NT];
@@ -184,24 +210,49 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, 1) void ring_gemm_kernel(
   const int a_row0 = wm * (BM / WM) + fr;
   const int b_row0 = wn * (BN / WN) + fr;
 
-  if (issuer) {
+  if constexpr (!SPLIT) {
+    if (issuer) {
 #pragma unroll
-    for (int p = 0; p < D; ++p)
-      if (p < nk) issue(p);
+      for (int p = 0; p < D; ++p)
+        if (p < nk) issue(p);
+    }
+  } else {
+    if (a_loader) {
+#pragma unroll
+      for (int p = 0; p < D; ++p)
+        if (p < nk) issue_a(p, lds + p * XSLOT);
+    } else if (b_loader) {
+#pragma unroll
+      for (int p = 0; p < DB; ++p)
+        if (p < nk) issue_b(p, wring + p * WSLOT);
+    }
   }
   for (int it = 0; it < nk; ++it) {
-    // step `it` must have landed; up to D - 1 younger steps may stay in flight
-    if (issuer) {
-      const int younger = nk - 1 - it;
-      if (RB && extra_b) rg_wait<LA + LB + 1, D - 1>(younger);
-      else rg_wait<LA + LB, D - 1>(younger);
+    // step `it` must have landed; younger steps may stay in flight
+    const int younger = nk - 1 - it;
+    if constexpr (!SPLIT) {
+      if (issuer) {
+        if (RB && extra_b) rg_wait<LA + LB + 1, D - 1>(younger);
+        else rg_wait<LA + LB, D - 1>(younger);
+      }
+    } else {
+      if (a_loader) rg_wait<LA, D - 1>(younger);
+      else if (b_loader) {
+        if (RB && extra_b) rg_wait<LB + 1, DB - 1>(younger);
+        else rg_wait<LB, DB - 1>(younger);
+      }
     }
     __builtin_amdgcn_s_barrier();
-    // every wave is past the reads of step it - 1, whose slot step it + D reuses
-    if (issuer && it + D < nk) issue(it + D);
+    // every wave is past the reads of step it - 1, whose slots the next issues reuse
+    if constexpr (!SPLIT) {
+      if (issuer && it + D < nk) issue(it + D);
+    } else {
+      if (a_loader && it + D < nk) issue_a(it + D, lds + ((it + D) % NS) * XSLOT);
+      else if (b_loader && it + DB < nk) issue_b(it + DB, wring + ((it + DB) % NSB) * WSLOT);
+    }
     if (!consumer || (abl & 1)) continue;
-    const char* sa = lds + (it % NS) * SLOT;
-    const char* sb = sa + BM * RG_ROWB;
+    const char* sa = SPLIT ? lds + (it % NS) * XSLOT : lds + (it % NS) * SLOT;
+    const char* sb = SPLIT ? wring + (it % (SPLIT ? NSB : 1)) * WSLOT : sa + BM * RG_ROWB;
 #pragma unroll
     for (int ks = 0; ks < RG_BK / 32; ++ks) {
       const int c = ks * 4 + fq;
@@ -234,7 +285,7 @@ __global__ __launch_bounds__((WM * WN + LW) * 64, 1) void ring_gemm_kernel(
   constexpr int ROWB = OCOLS * EB + 16;                          // padded staging row
   constexpr int CPR = OCOLS * EB / 16;                           // 16-B chunks per row
   static_assert(OCOLS * EB % 16 == 0, "16-B rows");
-  static_assert(BM * ROWB <= NS * SLOT, "staging tile fits in the ring");
+  static_assert(BM * ROWB <= LDS_BYTES, "staging tile fits in the ring");
   __builtin_amdgcn_s_barrier();                 // every wave is done reading the ring
   if (consumer) {
 #pragma unroll
@@ -302,7 +353,7 @@ __global__ __launch_bounds__(256) void ring_pack_kernel(bf16* __restrict__ P,
   reinterpret_cast<u32x4*>(P)[chunk] = *reinterpret_cast<const u32x4*>(W + s);
 }
 
-struct RingCfg { int bm, bn, wm, wn, lw, ns, waux; };
+struct RingCfg { int bm, bn, wm, wn, lw, ns, waux, nsb; };
 // id -> tile.  One workgroup per CU, ~256 workgroups at the target M.  BM = 256 (all rows
 // of a batch-256 step) reads every weight byte from HBM exactly once: measured, row
 // blocks of one column tile dispatched side by side on an XCD do NOT share the weight
@@ -310,12 +361,15 @@ struct RingCfg { int bm, bn, wm, wn, lw, ns, waux; };
 // The narrow projections then split K (o: 256 x 64, S = 4; qkv: 256 x 96, S = 4);
 // gate_up + SiLU: 256 x 112 (7 gate / up groups of 16: 256 tiles at S = 1) or 256 x 128.
 // Dedicated loader waves throughout (the MFMA waves never issue a DMA: 1.3-1.6x faster).
-constexpr int kRingCfgs = 12;
+// ids 12-17: split rings (activation ring of `ns` slots, weight ring of `nsb`).
+constexpr int kRingCfgs = 18;
 constexpr RingCfg kRing[kRingCfgs] = {
-    {256, 64, 4, 2, 4, 4, 2},  {256, 64, 4, 2, 8, 4, 2},  {256, 96, 4, 2, 4, 3, 2},
-    {256, 96, 4, 2, 8, 3, 2},  {256, 112, 4, 1, 4, 3, 2}, {256, 112, 4, 1, 8, 3, 2},
-    {256, 128, 4, 2, 4, 3, 2}, {256, 128, 4, 2, 8, 3, 2}, {128, 128, 2, 2, 4, 5, 0},
-    {128, 64, 2, 2, 4, 6, 0},  {128, 96, 2, 2, 4, 5, 0},  {128, 112, 4, 1, 4, 5, 0}};
+    {256, 64, 4, 2, 4, 4, 2, 0},  {256, 64, 4, 2, 8, 4, 2, 0},  {256, 96, 4, 2, 4, 3, 2, 0},
+    {256, 96, 4, 2, 8, 3, 2, 0},  {256, 112, 4, 1, 4, 3, 2, 0}, {256, 112, 4, 1, 8, 3, 2, 0},
+    {256, 128, 4, 2, 4, 3, 2, 0}, {256, 128, 4, 2, 8, 3, 2, 0}, {128, 128, 2, 2, 4, 5, 0, 0},
+    {128, 64, 2, 2, 4, 6, 0, 0},  {128, 96, 2, 2, 4, 5, 0, 0},  {128, 112, 4, 1, 4, 5, 0, 0},
+    {256, 64, 4, 2, 8, 3, 2, 8},  {256, 96, 4, 2, 8, 3, 2, 5},  {256, 112, 4, 1, 4, 3, 2, 4},
+    {256, 128, 4, 2, 8, 3, 2, 4}, {256, 64, 4, 2, 8, 2, 2, 12}, {128, 128, 2, 2, 8, 3, 2, 6}};
 
 template <int C>
 void ring_launch(int epi, void* Cp, const void* X, const void* W, int M, int N, int K,
@@ -335,7 +389,7 @@ void ring_launch(int epi, void* Cp, const void* X, const void* W, int M, int N, 
     return e ? atoi(e) : 0;
   }();
 #define RG_LAUNCH(E)                                                                        \
-  ring_gemm_kernel<c.bm, c.bn, c.wm, c.wn, c.lw, c.ns, c.waux, E>                           \
+  ring_gemm_kernel<c.bm, c.bn, c.wm, c.wn, c.lw, c.ns, c.waux, E, c.nsb>                    \
       <<<grid, (c.wm * c.wn + c.lw) * 64, 0, s>>>(Cp, (const bf16*)X, (const bf16*)W, M, N, \
                                                   K, ldx, S, MB, ss, xm, wt, abl)
   if (epi == RG_PARTIAL) RG_LAUNCH(RG_PARTIAL);
@@ -358,7 +412,7 @@ void ring_cfg_info(int cfg, int* bm, int* bn, int* threads, int* slots) {
   *bm = kRing[cfg].bm;
   *bn = kRing[cfg].bn;
   *threads = (kRing[cfg].wm * kRing[cfg].wn + kRing[cfg].lw) * 64;
-  *slots = kRing[cfg].ns;
+  *slots = kRing[cfg].ns * 100 + kRing[cfg].nsb;
 }
 
 void launch_ring_gemm(int cfg, int epi, void* C, const void* X, const void* Wp, int M, int N,
