@@ -10,8 +10,9 @@ Against a running service:
 Self-contained on one node (one engine per GPU + one router over all of them, like
 the dpN deployment):
     python bench/serve_bench.py --launch --gpus 1 --model llama-3-8b
-(``bench.py`` is the driver's headline harness: one router per replica, timed waves
-between barriers, engine-side figures alongside.)
+(``bench.py`` is the driver's headline harness: one router over every replica, timed
+bursts between barriers, engine-side figures alongside.  This script adds the Poisson
+arrival shape, ``--request-rate R``, whose p99 TPOT / ITL show decode starvation.)
 """
 from __future__ import annotations
 

@@ -880,6 +880,9 @@ bool debug_build() {
 
 int64_t allreduce_rms_max_hidden_op() { return kgc::allreduce_rms_max_hidden(); }
 int64_t allreduce_max_blocks_op() { return kgc::allreduce_max_blocks(); }
+int64_t peer_spin_ms_op() { return kgc::peer_spin_ms(); }
+int64_t coop_spin_ms_op() { return kgc::coop_spin_ms(); }
+int64_t wall_clock_rate_khz_op() { return kgc::wall_clock_rate_khz(); }
 
 void xgmi_allreduce_rms(Tensor out, Tensor in, Tensor residual, Tensor w, double eps,
                         std::vector<int64_t> data, std::vector<int64_t> sig, int64_t rank,
@@ -1055,6 +1058,9 @@ TORCH_LIBRARY(kgc, m) {
         "int[] data, int[] sig, int rank, int cap_bytes) -> ()");
   m.def("allreduce_rms_max_hidden() -> int", &allreduce_rms_max_hidden_op);
   m.def("allreduce_max_blocks() -> int", &allreduce_max_blocks_op);
+  m.def("peer_spin_ms() -> int", &peer_spin_ms_op);
+  m.def("coop_spin_ms() -> int", &coop_spin_ms_op);
+  m.def("wall_clock_rate_khz() -> int", &wall_clock_rate_khz_op);
   m.def("debug_errors() -> int", &debug_errors);
   m.def("sample_err_addr() -> int", &sample_err_addr);
   m.def("u32_clear_async(int addr) -> ()", &u32_clear_async);

@@ -66,10 +66,10 @@ __device__ __forceinline__ void ar_barrier(const ArPtrs& P, int rank, int phase,
     ar_store_flag(&peer->flag[phase][blockIdx.x][rank], epoch);
     ArSignal* self = reinterpret_cast<ArSignal*>(P.sig[rank]);
     uint32_t* f = &self->flag[phase][blockIdx.x][threadIdx.x];
-    int it = 0;
+    const unsigned long long dl = spin_deadline(KGC_PEER_SPIN_MS);
     while ((int32_t)(ar_load_flag(f) - epoch) < 0) {
       __builtin_amdgcn_s_sleep(1);
-      if (++it > (1 << 25)) {        // ~seconds: a peer is gone; fail loudly on the host
+      if (spin_expired(dl)) {        // a peer is gone: fail loudly on the host
         atomicOr(&self->err, 1u << threadIdx.x);
         break;
       }
@@ -268,6 +268,8 @@ static void ar_by_ranks(int nranks, const ArPtrs& P, int rank, void* inout, int6
 }
 
 int allreduce_max_blocks() { return AR_MAX_BLOCKS; }
+int peer_spin_ms() { return KGC_PEER_SPIN_MS; }
+int coop_spin_ms() { return KGC_COOP_SPIN_MS; }
 
 void launch_allreduce(int dtype, const ArPtrs& P, int nranks, int rank, void* inout,
                       int64_t nvec, int64_t cap_vec, bool two_shot, hipStream_t s) {
@@ -280,6 +282,14 @@ void launch_allreduce(int dtype, const ArPtrs& P, int nranks, int rank, void* in
 // ---- IPC buffer management (host) ----------------------------------------------
 static void ar_check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int64_t wall_clock_rate_khz() {
+  int dev = 0, khz = 0;
+  ar_check(hipGetDevice(&dev), "hipGetDevice");
+  ar_check(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev),
+           "hipDeviceGetAttribute(WallClockRate)");
+  return khz;
 }
 
 void* ar_alloc(int64_t bytes) {

@@ -183,4 +183,28 @@ __device__ __forceinline__ int kgc_bt(const int* bt, int i, int bt_stride, int n
   return v;
 }
 
+// ---- bounded spin-waits -------------------------------------------------------------
+// Every cross-workgroup / cross-GPU flag wait (xGMI all-reduce barriers, PP hand-off,
+// EP all-to-all, the cooperative sampler's row barriers) gives up after a WALL-CLOCK
+// bound, not an iteration count: the time a spin iteration takes depends on the flag's
+// memory scope and on what the other waves do, so an iteration bound is not a duration.
+// The clock is the constant-rate steady counter (s_memrealtime, 100 MHz on gfx950 =
+// hipDeviceAttributeWallClockRate; tests/test_allreduce_gpu.py checks the rate and the
+// measured time-out).  On expiry the kernel sets its sticky error word; the host raises
+// (engine/health.py) -- a peer that is gone fails the step in seconds, never hangs it.
+#ifndef KGC_PEER_SPIN_MS
+#define KGC_PEER_SPIN_MS 10000   // xGMI AR / PP / EP: peers can lag by a host hiccup
+#endif
+#ifndef KGC_COOP_SPIN_MS
+#define KGC_COOP_SPIN_MS 2000    // same-kernel workgroups (sampler): microseconds when healthy
+#endif
+constexpr unsigned long long kWallClockHz = 100000000ull;
+
+__device__ __forceinline__ unsigned long long spin_deadline(unsigned ms) {
+  return (unsigned long long)wall_clock64() + (unsigned long long)ms * (kWallClockHz / 1000ull);
+}
+__device__ __forceinline__ bool spin_expired(unsigned long long deadline) {
+  return (unsigned long long)wall_clock64() > deadline;
+}
+
 }  // namespace kgc

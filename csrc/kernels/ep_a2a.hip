@@ -103,10 +103,10 @@ __device__ void ep_wait_all(const EpPtrs& P, int rank, int phase, uint32_t epoch
   if (threadIdx.x < NR) {
     EpSignal* self = reinterpret_cast<EpSignal*>(P.sig[rank]);
     uint32_t* f = &self->flag[phase][threadIdx.x];
-    int it = 0;
+    const unsigned long long dl = spin_deadline(KGC_PEER_SPIN_MS);
     while ((int32_t)(ep_load(f) - epoch) < 0) {
       __builtin_amdgcn_s_sleep(1);
-      if (++it > (1 << 25)) {
+      if (spin_expired(dl)) {
         atomicOr(&self->err, 1u << threadIdx.x);
         break;
       }

@@ -156,6 +156,11 @@ struct ArPtrs {
 };
 size_t allreduce_signal_bytes();
 int allreduce_max_blocks();
+// spin-wait bounds (common.h) in ms: {peer (AR/PP/EP), same-kernel (sampler)}, and the
+// device's steady-counter rate the bounds assume (kHz)
+int peer_spin_ms();
+int coop_spin_ms();
+int64_t wall_clock_rate_khz();
 void launch_allreduce(int dtype, const ArPtrs& P, int nranks, int rank, void* inout,
                       int64_t nvec, int64_t cap_vec, bool two_shot, hipStream_t s);
 // fused one-shot all-reduce + residual add + RMSNorm over [M, H] rows (P.data: the

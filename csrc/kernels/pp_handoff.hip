@@ -42,10 +42,10 @@ __device__ __forceinline__ void pp_store(uint32_t* p, uint32_t v) {
 // thread 0 of every workgroup waits for *f >= target (bounded; failure -> err)
 __device__ void pp_wait(PpSignal* own, uint32_t* f, uint32_t target) {
   if (threadIdx.x == 0) {
-    int it = 0;
+    const unsigned long long dl = spin_deadline(KGC_PEER_SPIN_MS);
     while ((int32_t)(pp_load(f) - target) < 0) {
       __builtin_amdgcn_s_sleep(1);
-      if (++it > (1 << 25)) {
+      if (spin_expired(dl)) {
         atomicOr(&own->err, 1u);
         break;
       }

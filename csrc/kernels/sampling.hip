@@ -360,10 +360,10 @@ __global__ __launch_bounds__(SMP_NT) void sample_coop_kernel(
     if (tid == 0) {
       uint32_t* c = &ws->bar[nbar];
       __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int it = 0;
+      const unsigned long long dl = spin_deadline(KGC_COOP_SPIN_MS);
       while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)S) {
         __builtin_amdgcn_s_sleep(1);
-        if (++it > (1 << 24)) {
+        if (spin_expired(dl)) {
           // a row's workgroups were not co-resident (another kernel held CUs): the
           // thresholds below are wrong -- flag it in the sticky device word the host
           // reads after every step (ops.SamplerHealth) so the step is never served

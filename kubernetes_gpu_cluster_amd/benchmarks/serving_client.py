@@ -117,7 +117,10 @@ def summarize(res: list[Result], duration: float) -> dict:
             "p50_ttft_ms": round(1e3 * pct([r.ttft for r in ok], 0.5), 2),
             "p99_ttft_ms": round(1e3 * pct([r.ttft for r in ok], 0.99), 2),
             "p50_tpot_ms": round(1e3 * pct(tpot, 0.5), 3),
-            "p50_itl_ms": round(1e3 * statistics.median([x for r in ok for x in r.itl] or [0]), 3)}
+            "p99_tpot_ms": round(1e3 * pct(tpot, 0.99), 3),
+            "p50_itl_ms": round(1e3 * statistics.median([x for r in ok for x in r.itl] or [0]), 3),
+            "p99_itl_ms": round(1e3 * pct([x for r in ok for x in r.itl], 0.99), 3),
+            "max_itl_ms": round(1e3 * max([x for r in ok for x in r.itl] or [0]), 3)}
 
 
 def engine_figures(reqs: list, windows: list[tuple[float, float]]) -> dict:

@@ -146,11 +146,20 @@ def _timeout_worker(rank, world, port):
         car.raise_if_failed()
         dist.barrier()
         if rank == 0:
-            # rank 1 "dies": rank 0's barrier gives up after its bounded spin and the
-            # engine-side check raises instead of serving the stale sum
+            # rank 1 "dies": rank 0's barrier gives up after its wall-clock bound
+            # (common.h KGC_PEER_SPIN_MS, steady counter) and the engine-side check raises
+            # instead of serving the stale sum
+            import time
+            k = torch.ops.kgc
+            assert int(k.wall_clock_rate_khz()) == 100000      # the rate the bound assumes
+            bound = int(k.peer_spin_ms()) / 1e3
+            t0 = time.monotonic()
             car.all_reduce(x)
             car.enqueue_err_read()
             torch.cuda.synchronize()
+            took = time.monotonic() - t0
+            print(f"xGMI all-reduce peer time-out: {took:.3f} s (bound {bound:.1f} s)", flush=True)
+            assert 0.9 * bound <= took <= bound + 3.0, (took, bound)
             with pytest.raises(AllReduceFailed, match="never arrived"):
                 car.raise_if_failed()
         dist.barrier()

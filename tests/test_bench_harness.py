@@ -121,3 +121,24 @@ def test_client_counts_received_tokens_not_max_tokens():
     cut = asyncio.run(run(2))
     assert sum(r.ok for r in cut) == 4 and sum(r.tokens for r in cut) == 4 * 6
     assert sc.summarize(cut, 1.0)["value"] < sc.summarize(full, 1.0)["value"]
+
+
+def test_fake_engine_dp4_one_router_keeps_up():
+    """Router fan-in at DP = 4: four replicas whose engine cores are the
+    GPU-free timing model (engine/fake.py, Llama-3-8B step times), all client load
+    through rank 0's single multi-worker router.  The service must deliver what the
+    engines produce: service tok/s / engine tok/s >= 0.95 with nothing failed.
+    The 8-replica, full-config run is recorded in profiles/router_fanin_fake_dp8.jsonl."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "4",
+           "--device", "cpu", "--model", "llama-3-8b", "--num-prompts", "128", "--input-len", "256",
+           "--output-len", "128", "--steps", "1", "--warmup", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, KGC_FAKE_ENGINE="1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    j = _json_lines(r.stdout)[0]
+    assert j["failed"] == 0 and j["completed"] == 4 * 128
+    assert j["engine_output_tokens"] == 4 * 128 * 128
+    assert j["config"]["endpoint"].startswith("one router (4 replica(s))")
+    assert j["router_workers"] == 4
+    assert j["service_vs_engine"] >= 0.95, j
