@@ -31,6 +31,102 @@ constexpr int PF_BN = 64;
 
 __device__ __forceinline__ int kswz(int k) { return (k & 3) | (((k >> 3) & 3) << 2); }
 
+// Lazy O rescale (log2 units): the running max m only moves when some row's tile max
+// exceeds it by more than this, so P = exp2(s - m) stays <= 2^8 and the O / l rescale
+// (DT*8 + 2 VALU per lane) runs on a few tiles per row instead of on every tile.  The
+// decision covers the tile BEFORE its P is exponentiated and after the previous tile's
+// P.V is complete, and O, l and m move together (no P at the old scale is pending).
+constexpr float PF_RESCALE_THR = 8.f;
+
+// One 64-key tile for a wave's 32 query rows (two 16-row q-tiles), shared by both
+// kernels.  K / V are the staged LDS images; key0 = the tile's first key.  Scores stay
+// raw through the max (scale_log2 > 0 commutes with max) and enter the exponent as
+// fma(s, scale_log2, -m): one VALU per score instead of a multiply and a subtract.
+// exp2 is the bare v_exp_f32 (inputs <= PF_RESCALE_THR, -inf -> 0; no denormal
+// range fix-up: exp2f() lowered to ~6 VALU per call).  MASK = the causal diagonal
+// crosses this tile for some row of the wave; off-diagonal tiles skip the per-element
+// key compare entirely.
+template <typename T, int D, bool MASK>
+__device__ __forceinline__ void pf_wave_tile(const T* __restrict__ K, const T* __restrict__ V,
+                                             const typename Vec8<T>::type (&qf)[2][D / 32],
+                                             f32x4 (&o)[2][D / 16], float (&m)[2], float (&l)[2],
+                                             const int (&qpos)[2], int key0, float c, int r16,
+                                             int qd) {
+  typedef typename Vec8<T>::type V8;
+  constexpr int NCH = D / 8, KS = D / 32, DT = D / 16;
+  const int keyA = 8 * (r16 >> 2) + (r16 & 3);
+  // ---- S^T tiles: [qt][a0, b0, a1, b1]
+  f32x4 s[2][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int key = (j >> 1) * 32 + keyA + 4 * (j & 1);
+    const T* krow = K + key * D;
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      Pack8<T> f;
+      f.u = *reinterpret_cast<const u32x4*>(krow + (((4 * ks + qd) ^ (r16 & (NCH - 1))) * 8));
+      a0 = mfma16x16x32(f.v, qf[0][ks], a0);
+      a1 = mfma16x16x32(f.v, qf[1][ks], a1);
+    }
+    s[0][j] = a0;
+    s[1][j] = a1;
+  }
+  // ---- causal mask + lazy online softmax (query = lane&15: lane-local stats)
+  V8 pf[2][2];
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    if constexpr (MASK) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (key0 + (j >> 1) * 32 + 8 * qd + 4 * (j & 1) + i > qpos[qt]) s[qt][j][i] = -INFINITY;
+    }
+    float tmax = fmaxf(fmaxf(s[qt][0][0], s[qt][0][1]), fmaxf(s[qt][0][2], s[qt][0][3]));
+#pragma unroll
+    for (int j = 1; j < 4; ++j)
+      tmax = fmaxf(tmax, fmaxf(fmaxf(s[qt][j][0], s[qt][j][1]), fmaxf(s[qt][j][2], s[qt][j][3])));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    tmax *= c;                              // -inf stays -inf (a fully masked row)
+    if (__any(tmax > m[qt] + PF_RESCALE_THR)) {
+      const float mn = fmaxf(m[qt], tmax);
+      const float alpha = __builtin_amdgcn_exp2f(m[qt] - mn);   // 0 on the first tile
+      m[qt] = mn;
+      l[qt] *= alpha;
+#pragma unroll
+      for (int t = 0; t < DT; ++t) o[qt][t] *= alpha;
+    }
+    const float nm = -m[qt];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      Pack8<T> pk;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float pa = __builtin_amdgcn_exp2f(__builtin_fmaf(s[qt][2 * kk][i], c, nm));
+        const float pb = __builtin_amdgcn_exp2f(__builtin_fmaf(s[qt][2 * kk + 1][i], c, nm));
+        l[qt] += pa + pb;
+        pk.h[i] = from_f<T>(pa);
+        pk.h[4 + i] = from_f<T>(pb);
+      }
+      pf[qt][kk] = pk.v;
+    }
+  }
+  // ---- O^T += V^T . P^T
+#pragma unroll
+  for (int t = 0; t < DT; ++t) {
+    const int d = 16 * t + r16;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      Pack8<T> f;
+      f.u = *reinterpret_cast<const u32x4*>(V + d * PF_BN + (((4 * kk + qd) ^ ((d >> 1) & 7)) * 8));
+      o[0][t] = mfma16x16x32(f.v, pf[0][kk], o[0][t]);
+      o[1][t] = mfma16x16x32(f.v, pf[1][kk], o[1][t]);
+    }
+  }
+}
+
 // KV8: fp8 e4m3 cache; staged as 8-byte loads, widened to T on the way into LDS (the
 // LDS image and everything after it is unchanged).  K scale folded into scale_log2,
 // V scale applied in the epilogue.
@@ -93,15 +189,30 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
   const int last_q = ctx0 + min((mb + 1) * PF_BM, qlen) - 1;
   const int n_tiles = last_q / PF_BN + 1;
 
+  // Block ids of a tile's chunks are fetched one tile AHEAD of its K/V loads: the
+  // dependent block-table load would otherwise stall every tile's load issue for an
+  // L2 round trip before the compute it is meant to overlap.
   R kreg[KPT], vreg[VPT];
+  int kblk[KPT], vblk[VPT];
+  auto fetch_bt = [&](int kt) {
+#pragma unroll
+    for (int u = 0; u < KPT; ++u) {
+      const int key = (threadIdx.x + 256 * u) / NCH;
+      kblk[u] = kgc_bt(bt, min(kt * PF_BN + key, L - 1) >> bs_log2, bt_stride, num_blocks);
+    }
+#pragma unroll
+    for (int u = 0; u < VPT; ++u) {
+      const int c = (threadIdx.x + 256 * u) / D;
+      vblk[u] = kgc_bt(bt, (min(kt * PF_BN + 8 * c, L - 1) & ~7) >> bs_log2, bt_stride, num_blocks);
+    }
+  };
   auto load_tile = [&](int kt) {
 #pragma unroll
     for (int u = 0; u < KPT; ++u) {
       const int ci = threadIdx.x + 256 * u;
       const int key = ci / NCH, c = ci % NCH;
       const int ka = min(kt * PF_BN + key, L - 1);
-      const C* src = kc + (int64_t)kgc_bt(bt, ka >> bs_log2, bt_stride, num_blocks) * nkv * hs + h * hs +
-                     (int64_t)(ka & bsm) * D + c * 8;
+      const C* src = kc + ((int64_t)kblk[u] * nkv + h) * hs + (int64_t)(ka & bsm) * D + c * 8;
       kreg[u] = *reinterpret_cast<const R*>(src);
     }
 #pragma unroll
@@ -109,8 +220,7 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
       const int ci = threadIdx.x + 256 * u;
       const int c = ci / D, d = ci % D;
       const int ka = min(kt * PF_BN + 8 * c, L - 1) & ~7;
-      const C* src = vc + (int64_t)kgc_bt(bt, ka >> bs_log2, bt_stride, num_blocks) * nkv * hs + h * hs +
-                     ((ka & bsm) >> 3) * (D * 8) + d * 8;
+      const C* src = vc + ((int64_t)vblk[u] * nkv + h) * hs + ((ka & bsm) >> 3) * (D * 8) + d * 8;
       vreg[u] = *reinterpret_cast<const R*>(src);
     }
   };
@@ -138,83 +248,23 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
     for (int t = 0; t < DT; ++t) o[qt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
 
+  fetch_bt(0);
   load_tile(0);
+  if (n_tiles > 1) fetch_bt(1);
   store_tile(0);
   __syncthreads();
-  const int keyA = 8 * (r16 >> 2) + (r16 & 3);
   for (int kt = 0; kt < n_tiles; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < n_tiles) load_tile(kt + 1);
+    if (kt + 1 < n_tiles) {
+      load_tile(kt + 1);
+      fetch_bt(min(kt + 2, n_tiles - 1));   // unconditional: static vmcnt below
+    }
     const T* K = lds + buf * 2 * TILE;
     const T* V = K + TILE;
-    // ---- S^T tiles: [qt][a0, b0, a1, b1]
-    f32x4 s[2][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int key = (j >> 1) * 32 + keyA + 4 * (j & 1);
-      const T* krow = K + key * D;
-      f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        Pack8<T> f;
-        f.u = *reinterpret_cast<const u32x4*>(krow + (((4 * ks + qd) ^ (r16 & (NCH - 1))) * 8));
-        a0 = mfma16x16x32(f.v, qf[0][ks], a0);
-        a1 = mfma16x16x32(f.v, qf[1][ks], a1);
-      }
-      s[0][j] = a0;
-      s[1][j] = a1;
-    }
-    // ---- causal mask + online softmax (query = lane&15: lane-local stats)
-    V8 pf[2][2];
-    const bool diag = (kt + 1) * PF_BN - 1 > ctx0 + mb * PF_BM + wave * 32;
-#pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      float tmax = -INFINITY;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int key = kt * PF_BN + (j >> 1) * 32 + 8 * qd + 4 * (j & 1) + i;
-          float v = s[qt][j][i] * scale_log2;
-          if (diag && key > qpos[qt]) v = -INFINITY;
-          s[qt][j][i] = v;
-          tmax = fmaxf(tmax, v);
-        }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-      const float mn = fmaxf(m[qt], tmax);
-      const float alpha = exp2f(m[qt] - mn);
-      m[qt] = mn;
-      l[qt] *= alpha;
-#pragma unroll
-      for (int t = 0; t < DT; ++t) o[qt][t] *= alpha;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        Pack8<T> pk;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float pa = exp2f(s[qt][2 * kk][i] - mn);
-          const float pb = exp2f(s[qt][2 * kk + 1][i] - mn);
-          l[qt] += pa + pb;
-          pk.h[i] = from_f<T>(pa);
-          pk.h[4 + i] = from_f<T>(pb);
-        }
-        pf[qt][kk] = pk.v;
-      }
-    }
-    // ---- O^T += V^T . P^T
-#pragma unroll
-    for (int t = 0; t < DT; ++t) {
-      const int d = 16 * t + r16;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        Pack8<T> f;
-        f.u = *reinterpret_cast<const u32x4*>(V + d * PF_BN +
-                                              (((4 * kk + qd) ^ ((d >> 1) & 7)) * 8));
-        o[0][t] = mfma16x16x32(f.v, pf[0][kk], o[0][t]);
-        o[1][t] = mfma16x16x32(f.v, pf[1][kk], o[1][t]);
-      }
-    }
+    if ((kt + 1) * PF_BN - 1 > ctx0 + mb * PF_BM + wave * 32)
+      pf_wave_tile<T, D, true>(K, V, qf, o, m, l, qpos, kt * PF_BN, scale_log2, r16, qd);
+    else
+      pf_wave_tile<T, D, false>(K, V, qf, o, m, l, qpos, kt * PF_BN, scale_log2, r16, qd);
     if (kt + 1 < n_tiles) store_tile(buf ^ 1);
     __syncthreads();
   }
@@ -311,24 +361,38 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_gqa_kernel(
   const int last_q = ctx0 + min(qbase + QB, qlen) - 1;
   const int n_tiles = last_q / PF_BN + 1;
 
+  // Block ids of a tile's chunks are fetched one tile AHEAD of its K/V loads: the
+  // dependent block-table load would otherwise stall every tile's load issue for an
+  // L2 round trip before the compute it is meant to overlap.
   R kreg[KPT], vreg[VPT];
+  int kblk[KPT], vblk[VPT];
+  auto fetch_bt = [&](int kt) {
+#pragma unroll
+    for (int u = 0; u < KPT; ++u) {
+      const int key = (threadIdx.x + NT_ * u) / NCH;
+      kblk[u] = kgc_bt(bt, min(kt * PF_BN + key, L - 1) >> bs_log2, bt_stride, num_blocks);
+    }
+#pragma unroll
+    for (int u = 0; u < VPT; ++u) {
+      const int c = (threadIdx.x + NT_ * u) / D;
+      vblk[u] = kgc_bt(bt, (min(kt * PF_BN + 8 * c, L - 1) & ~7) >> bs_log2, bt_stride, num_blocks);
+    }
+  };
   auto load_tile = [&](int kt) {
 #pragma unroll
     for (int u = 0; u < KPT; ++u) {
       const int ci = threadIdx.x + NT_ * u;
       const int key = ci / NCH, c = ci % NCH;
       const int ka = min(kt * PF_BN + key, L - 1);
-      const C* src = kc + (int64_t)kgc_bt(bt, ka >> bs_log2, bt_stride, num_blocks) * nkv * hs +
-                     h * hs + (int64_t)(ka & bsm) * D + c * 8;
+      const C* src = kc + ((int64_t)kblk[u] * nkv + h) * hs + (int64_t)(ka & bsm) * D + c * 8;
       kreg[u] = *reinterpret_cast<const R*>(src);
     }
 #pragma unroll
-    for (int u = 0; u < VPT; ++u) {
+    for (int u = 0; u < VPT; ++u) {       // 8-key group c of dim d: contiguous in d
       const int ci = threadIdx.x + NT_ * u;
       const int c = ci / D, d = ci % D;
       const int ka = min(kt * PF_BN + 8 * c, L - 1) & ~7;
-      const C* src = vc + (int64_t)kgc_bt(bt, ka >> bs_log2, bt_stride, num_blocks) * nkv * hs +
-                     h * hs + ((ka & bsm) >> 3) * (D * 8) + d * 8;
+      const C* src = vc + ((int64_t)vblk[u] * nkv + h) * hs + ((ka & bsm) >> 3) * (D * 8) + d * 8;
       vreg[u] = *reinterpret_cast<const R*>(src);
     }
   };
@@ -358,81 +422,24 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_gqa_kernel(
   // this wave's own last key tile (its rows end before the workgroup's last row)
   const int wave_tiles = (ctx0 + min(wq0 + 31, qlen - 1)) / PF_BN + 1;
 
+  fetch_bt(0);
   load_tile(0);
+  if (n_tiles > 1) fetch_bt(1);
   store_tile(0);
   __syncthreads();
-  const int keyA = 8 * (r16 >> 2) + (r16 & 3);
   for (int kt = 0; kt < n_tiles; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < n_tiles) load_tile(kt + 1);
+    if (kt + 1 < n_tiles) {
+      load_tile(kt + 1);
+      fetch_bt(min(kt + 2, n_tiles - 1));   // unconditional: static vmcnt below
+    }
     if (kt < wave_tiles) {
       const T* K = lds + buf * 2 * TILE;
       const T* V = K + TILE;
-      f32x4 s[2][4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int key = (j >> 1) * 32 + keyA + 4 * (j & 1);
-        const T* krow = K + key * D;
-        f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          Pack8<T> f;
-          f.u = *reinterpret_cast<const u32x4*>(krow + (((4 * ks + qd) ^ (r16 & (NCH - 1))) * 8));
-          a0 = mfma16x16x32(f.v, qf[0][ks], a0);
-          a1 = mfma16x16x32(f.v, qf[1][ks], a1);
-        }
-        s[0][j] = a0;
-        s[1][j] = a1;
-      }
-      V8 pf[2][2];
-      const bool diag = (kt + 1) * PF_BN - 1 > ctx0 + wq0;
-#pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        float tmax = -INFINITY;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int key = kt * PF_BN + (j >> 1) * 32 + 8 * qd + 4 * (j & 1) + i;
-            float v = s[qt][j][i] * scale_log2;
-            if (diag && key > qpos[qt]) v = -INFINITY;
-            s[qt][j][i] = v;
-            tmax = fmaxf(tmax, v);
-          }
-        tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
-        tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-        const float mn = fmaxf(m[qt], tmax);
-        const float alpha = exp2f(m[qt] - mn);
-        m[qt] = mn;
-        l[qt] *= alpha;
-#pragma unroll
-        for (int t = 0; t < DT; ++t) o[qt][t] *= alpha;
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          Pack8<T> pk;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float pa = exp2f(s[qt][2 * kk][i] - mn);
-            const float pb = exp2f(s[qt][2 * kk + 1][i] - mn);
-            l[qt] += pa + pb;
-            pk.h[i] = from_f<T>(pa);
-            pk.h[4 + i] = from_f<T>(pb);
-          }
-          pf[qt][kk] = pk.v;
-        }
-      }
-#pragma unroll
-      for (int t = 0; t < DT; ++t) {
-        const int d = 16 * t + r16;
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          Pack8<T> f;
-          f.u = *reinterpret_cast<const u32x4*>(V + d * PF_BN +
-                                                (((4 * kk + qd) ^ ((d >> 1) & 7)) * 8));
-          o[0][t] = mfma16x16x32(f.v, pf[0][kk], o[0][t]);
-          o[1][t] = mfma16x16x32(f.v, pf[1][kk], o[1][t]);
-        }
-      }
+      if ((kt + 1) * PF_BN - 1 > ctx0 + wq0)
+        pf_wave_tile<T, D, true>(K, V, qf, o, m, l, qpos, kt * PF_BN, scale_log2, r16, qd);
+      else
+        pf_wave_tile<T, D, false>(K, V, qf, o, m, l, qpos, kt * PF_BN, scale_log2, r16, qd);
     }
     if (kt + 1 < n_tiles) store_tile(buf ^ 1);
     __syncthreads();

@@ -398,7 +398,88 @@ class ModelRunner:
             m.decode_workspace = self.workspace
             nkv = self.model.local_kv_heads()
             m.decode_grid_z = z if z is not None else ops.decode_grid_z(D, nkv, max_ctx)
+        elif P and self._overlap_ok(Tp):
+            m.split = self._split_prefill(Tp, P)
         return m
+
+    # ------------------------------------------------------------------ TP prefill overlap
+    def _overlap_ok(self, Tp: int) -> bool:
+        """Large prefill-only steps at TP > 1 run as two token halves whose all-reduces
+        overlap the other half's GEMMs (``LlamaForCausalLM._forward_tp_overlap``).
+        KGC_TP_OVERLAP=0 turns it off; KGC_TP_OVERLAP_MIN_TOKENS (default 2048) is the
+        smallest step it applies to (below it the all-reduces take the xGMI kernel)."""
+        if self.ps.tp_size == 1 or os.environ.get("KGC_TP_OVERLAP", "1") == "0":
+            return False
+        fn = getattr(self.model, "_tp_tail_fusable", None)
+        return (fn is not None and fn()
+                and Tp >= int(os.environ.get("KGC_TP_OVERLAP_MIN_TOKENS", "2048")))
+
+    def _split_prefill(self, Tp: int, P: int):
+        """Split the step's prefill tokens at row a into two AttnMetadata.  A sequence
+        cut by the split becomes a chunked-prefill continuation in the second half (its
+        queries [a', qlen) over seq_len keys); the first half's part of it attends over
+        seq_len - (qlen - a') keys.  Within a layer the first half's attention (and its
+        K/V write) runs before the second half's, so the continuation sees those keys.
+        Built from this rank's host copy of the plan (identical on every TP rank)."""
+        L, mb = self.L, self.max_blocks
+        i32 = self.h32.numpy()
+        qsl = i32[L.qsl:L.qsl + P + 1].astype(np.int64)
+        sl = i32[L.sl:L.sl + P].astype(np.int64)
+        pbt = i32[L.pbt:L.pbt + P * mb].reshape(P, mb)
+        a = (Tp // 2) // 128 * 128 or Tp // 2
+        k = int(np.searchsorted(qsl, a, side="right")) - 1      # qsl[k] <= a < qsl[k+1]
+        qlens = np.diff(qsl)
+        cut = a > qsl[k]
+        qa = np.concatenate([qlens[:k], [a - qsl[k]] if cut else []]).astype(np.int64)
+        sa = np.concatenate([sl[:k], [sl[k] - (qsl[k + 1] - a)] if cut else []]).astype(np.int64)
+        qb = np.concatenate([[qsl[k + 1] - a], qlens[k + 1:]]).astype(np.int64)
+        sb = sl[k:].copy()
+        halves = []
+        blob = []
+        for q, sq, bt in ((qa, sa, pbt[:len(qa)]), (qb, sb, pbt[k:])):
+            ws, wm = ops.prefill_work_list(q.tolist(), sq.tolist())
+            parts = [np.concatenate([[0], np.cumsum(q)]), sq, bt.reshape(-1), ws, wm]
+            halves.append([len(x) for x in parts])
+            blob += parts
+        flat = np.concatenate([np.asarray(x, dtype=np.int32) for x in blob])
+        dev = self._split_upload(flat)
+        metas, off = [], 0
+        d64 = self.d64
+        for h, (n0, n1) in enumerate(((0, a), (a, Tp))):
+            v = []
+            for n in halves[h]:
+                v.append(dev[off:off + n])
+                off += n
+            np_ = halves[h][1]
+            mh = AttnMetadata(slot_mapping=d64[L.slots + n0:L.slots + n1], num_prefill_tokens=n1 - n0,
+                              num_prefills=np_, num_decodes=0)
+            mh.query_start_loc, mh.prefill_seq_lens = v[0], v[1]
+            mh.prefill_block_tables = v[2].view(np_, mb)
+            mh.work_seq, mh.work_mblk = v[3], v[4]
+            metas.append(mh)
+        return a, metas[0], metas[1]
+
+    def _split_upload(self, flat: np.ndarray) -> torch.Tensor:
+        """Device copy of the split metadata through a 2-entry pinned ring (a buffer is
+        refilled only after the copy that last read it has completed)."""
+        if not self.is_gpu:
+            return torch.from_numpy(flat.copy())
+        if not hasattr(self, "_sp_bufs"):
+            self._sp_bufs, self._sp_ev, self._sp_cur = [None, None], [None, None], 0
+        i = self._sp_cur = 1 - self._sp_cur
+        if self._sp_ev[i] is not None:
+            self._sp_ev[i].synchronize()
+        buf = self._sp_bufs[i]
+        if buf is None or buf[0].numel() < flat.size:
+            n = max(flat.size, 4096)
+            buf = self._sp_bufs[i] = (torch.empty(n, dtype=torch.int32, pin_memory=True),
+                                      torch.empty(n, dtype=torch.int32, device=self.device))
+        buf[0].numpy()[:flat.size] = flat
+        buf[1][:flat.size].copy_(buf[0][:flat.size], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._sp_ev[i] = ev
+        return buf[1][:flat.size]
 
     def _forward(self, T, meta: AttnMetadata, hidden_in=None):
         L = self.L

@@ -34,6 +34,9 @@ class AttnMetadata:
     decode_ctx_lens: Optional[torch.Tensor] = None        # [D] int32
     decode_grid_z: int = 1
     decode_workspace: Optional[tuple] = None
+    # prefill-only TP step split into two token halves for comm/compute overlap:
+    # (a, meta of tokens [0, a), meta of tokens [a, T)) -- engine/model_runner.py
+    split: Optional[tuple] = None
 
 
 @dataclasses.dataclass

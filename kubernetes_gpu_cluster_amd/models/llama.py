@@ -11,6 +11,7 @@ embedding, the last the final norm and the LM head.
 """
 from __future__ import annotations
 
+import dataclasses
 import os
 import re
 from typing import Iterable, Optional
@@ -185,6 +186,8 @@ class LlamaForCausalLM(nn.Module):
         if self._tail_fusable(x):
             return self._forward_tail_fused(positions, x, ctx)
         if self._tp_tail_fusable():
+            if ctx.attn.split is not None:
+                return self._forward_tp_overlap(positions, x, ctx)
             return self._forward_tp_fused(positions, x, ctx)
         for layer in self.layers:
             x, residual = layer(positions, x, residual, ctx)
@@ -262,6 +265,53 @@ class LlamaForCausalLM(nn.Module):
         x, _ = comm.tp_all_reduce_add_rms(gemm.linear(h, prev.mlp.down_proj.weight), residual,
                                           self.norm.weight, self.norm.eps)
         return x
+
+    def _forward_tp_overlap(self, positions, x, ctx):
+        """``_forward_tp_fused`` on a large prefill step split into two token halves
+        (engine/model_runner.py ``_split_prefill``) so that each row-parallel all-reduce
+        (RCCL at these sizes: 16K tokens x 8192 x 2 B = 256 MB per call for Llama-3-70B at
+        TP = 8) runs while the OTHER half computes.  Per layer:
+
+            attn(A)  AR_o(A) ->                 attn(B)  AR_o(B) ->
+            [wait AR_o(A)] norm+MLP(A)  AR_d(A) ->   [wait AR_o(B)] norm+MLP(B)  AR_d(B) ->
+
+        so AR_o(A) hides under attn(B), AR_o(B) under MLP(A), AR_d(A) under MLP(B) and
+        AR_d(B) under the next layer's attn(A).  The first half's attention writes its
+        K/V before the second half's attention reads them (one compute stream), which a
+        sequence cut by the split needs.  Same math as the unsplit step; GEMM shapes
+        differ (M halves), so results agree to rounding, not bit for bit."""
+        a, ma, mb = ctx.attn.split
+        ctxs = (dataclasses.replace(ctx, attn=ma), dataclasses.replace(ctx, attn=mb))
+        pos = (positions[:a], positions[a:])
+        xs = [x[:a], x[a:]]
+        res = [x[:a], x[a:]]          # residual = embedding output, updated in place
+        h = [None, None]
+        pend = [None, None]
+        prev = None
+        for layer in self.layers:
+            ln1, ln2 = layer.input_layernorm, layer.post_attention_layernorm
+            at, gu = layer.self_attn, layer.mlp.gate_up_proj
+            for i in (0, 1):
+                if prev is None:
+                    xi = ln1(xs[i])
+                else:
+                    pend[i].wait()
+                    xi, res[i] = ops.fused_add_rms_norm(h[i], res[i], ln1.weight, ln1.eps)
+                o = gemm.linear(at.attend(pos[i], at.project_qkv(xi), ctxs[i]), at.o_proj.weight)
+                h[i], pend[i] = o, comm.tp_all_reduce_async(o)
+            for i in (0, 1):
+                pend[i].wait()
+                xi, res[i] = ops.fused_add_rms_norm(h[i], res[i], ln2.weight, ln2.eps)
+                d = gemm.linear(gemm.linear_silu(xi, gu.weight, gu.bias),
+                                layer.mlp.down_proj.weight)
+                h[i], pend[i] = d, comm.tp_all_reduce_async(d)
+            prev = layer
+        outs = []
+        for i in (0, 1):
+            pend[i].wait()
+            xi, _ = ops.fused_add_rms_norm(h[i], res[i], self.norm.weight, self.norm.eps)
+            outs.append(xi)
+        return torch.cat(outs, 0)
 
     # ------------------------------------------------------------------ fused small-M decode
     def _fused_cfgs(self, M: int):

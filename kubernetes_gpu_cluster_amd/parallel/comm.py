@@ -39,6 +39,24 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
+class _Done:
+    def wait(self) -> None:
+        pass
+
+
+def tp_all_reduce_async(x: torch.Tensor):
+    """In-place TP sum launched WITHOUT ordering the caller's later work behind it:
+    returns a handle whose ``wait()`` orders the current stream after the collective
+    (RCCL: a stream wait on the communicator's stream, no host block; gloo: blocks).
+    Used by the two-half prefill overlap (models/llama.py ``_forward_tp_overlap``), where
+    one half's GEMMs run while the other half's all-reduce is on the links.  Always
+    RCCL/gloo: the xGMI kernel would run on the compute stream and overlap nothing."""
+    s = get_state()
+    if s.tp_size == 1:
+        return _Done()
+    return dist.all_reduce(x, group=s.tp_group, async_op=True)
+
+
 def tp_all_reduce_add_rms(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
                           eps: float) -> tuple[torch.Tensor, torch.Tensor]:
     """Row-parallel projection output -> (rms_norm(residual + sum_ranks x) * w, residual),

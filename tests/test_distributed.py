@@ -99,6 +99,80 @@ def test_tp4_tp8_match_tp1(name, tp):
         torch.testing.assert_close(got[r], ref, atol=2e-4, rtol=2e-4)
 
 
+def _multi_logits(rank, name, tp, overlap):
+    """One prefill step over three prompts (38 tokens; the two-half split at row 19 cuts
+    the second prompt into a first-half part and a second-half continuation), then one
+    decode step for all three: the logits of every sampled row."""
+    os.environ["KGC_TP_OVERLAP"] = "1" if overlap else "0"
+    os.environ["KGC_TP_OVERLAP_MIN_TOKENS"] = "8"
+    from kubernetes_gpu_cluster_amd.engine.block_manager import BlockManager
+    from kubernetes_gpu_cluster_amd.engine.model_runner import ModelRunner
+    from kubernetes_gpu_cluster_amd.engine.sequence import SamplingParams, Sequence
+    from kubernetes_gpu_cluster_amd.models import build_model
+    from kubernetes_gpu_cluster_amd.parallel.state import destroy_parallel, init_parallel
+    init_parallel(tp, 1, backend="gloo", device=torch.device("cpu"))
+    cfg = PRESETS[name]
+    model = build_model(cfg, torch.float32, torch.device("cpu"))
+    model.load_weights(full_state_dict_random(cfg, seed=3, std=0.05).items())
+    runner = ModelRunner(model, cfg, torch.float32, torch.device("cpu"), 16, 256, 4, 128, True)
+    runner.init_kv_cache(48)
+    g = torch.Generator().manual_seed(1)
+    bm = BlockManager(48, 16, 4, runner.max_blocks)
+    seqs = [Sequence(str(i), torch.randint(3, cfg.vocab_size, (n,), generator=g).tolist(),
+                     SamplingParams()) for i, n in enumerate((7, 20, 11))]
+    outs, splits = [], []
+
+    def run(prefills, decodes):
+        plan, _ = runner.build_plan(prefills, decodes, bm.table)
+        runner._upload(plan)
+        meta = runner._meta(plan.T, plan.Tp, plan.P, plan.D, plan.W, plan.max_ctx)
+        splits.append(None if meta.split is None else meta.split[0])
+        with torch.inference_mode():
+            h = runner._forward(plan.T, meta)
+            idx = runner.d64[runner.L.lidx:runner.L.lidx + plan.S]
+            return model.compute_logits(h.index_select(0, idx))
+    for sq in seqs:
+        bm.allocate(sq, len(sq.prompt_token_ids))
+    outs.append(run([(sq, len(sq.prompt_token_ids)) for sq in seqs], []))
+    for sq in seqs:
+        sq.num_computed = len(sq.prompt_token_ids)
+        sq.output_token_ids.append(5)
+        bm.allocate(sq, sq.num_computed + 1)
+    outs.append(run([], seqs))
+    destroy_parallel()
+    return torch.cat(outs, 0), splits
+
+
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-qwen3"])
+def test_tp2_prefill_overlap_matches_tp1(name):
+    """The two-half TP prefill (models/llama.py _forward_tp_overlap: each half's
+    row-parallel all-reduce in flight while the other half computes) == TP = 1 and ==
+    TP = 2 without the split, incl. a prompt cut by the split (a chunked-prefill
+    continuation in the second half) and the decode step that reads its KV."""
+    ref, _ = spawn(_multi_logits, 1, name, 1, True)[0]
+    plain = spawn(_multi_logits, 2, name, 2, False)
+    got = spawn(_multi_logits, 2, name, 2, True)
+    assert got[0][1] == [19, None] and plain[0][1] == [None, None]
+    for r in range(2):
+        torch.testing.assert_close(got[r][0], ref, atol=1e-4, rtol=1e-4)
+        torch.testing.assert_close(got[r][0], plain[r][0], atol=1e-4, rtol=1e-4)
+
+
+def test_tp2_overlap_chunked_prompt_matches_tp1():
+    """_engine_logits' chunked prompt (13 + 16 tokens, then decodes) with the split on:
+    both chunks are cut mid-sequence (the second one a continuation cut again)."""
+    def run(tp):
+        os.environ["KGC_TP_OVERLAP_MIN_TOKENS"] = "8"
+        try:
+            return spawn(_logits, tp, "tiny-llama", tp, 1)
+        finally:
+            os.environ.pop("KGC_TP_OVERLAP_MIN_TOKENS")
+    ref = run(1)[0]
+    got = run(2)
+    torch.testing.assert_close(got[0], ref, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(got[1], ref, atol=1e-4, rtol=1e-4)
+
+
 def test_moe_ep4_matches_tp1():
     """Mixtral expert parallelism at EP = 4 (one expert per rank, attention at TP = 4
     with replicated kv heads): logits == one process."""

@@ -163,16 +163,20 @@ def test_engine_preemption_recompute(gpu):
     assert eng.bm.num_free == eng.bm.num_blocks - 1
 
 
-@pytest.mark.parametrize("tp,eager,name", [(2, True, "tiny-llama"), (2, False, "tiny-llama"),
-                                          (4, False, "tiny-llama"),
-                                          (8, False, "tiny-llama-gqa8")])
-def test_tp_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch, tp, eager, name):
+@pytest.mark.parametrize("tp,eager,name,overlap", [(2, True, "tiny-llama", False),
+                                                  (2, False, "tiny-llama", False),
+                                                  (2, False, "tiny-llama", True),
+                                                  (4, False, "tiny-llama", False),
+                                                  (8, False, "tiny-llama-gqa8", False)])
+def test_tp_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch, tp, eager, name, overlap):
     """The tensor-parallel engine on the GPU: TP ranks share cuda:0 (gloo process group,
     since RCCL refuses two ranks on one device), sharded QKV/MLP/vocab layers, the xGMI
     all-reduce kernel over IPC buffers for the row-parallel sums, multiprocess workers.
     eager=False is the production decode path: hipGraph-captured decode buckets with
     the xGMI all-reduce INSIDE the graphs, and vocab-parallel sampling after the replay
-    (no logits all-gather).  TP = 4 replicates tiny-llama's 2 kv heads over 4 ranks; TP = 8
+    (no logits all-gather).  overlap: the 100-token first prefill step runs as two
+    halves whose all-reduces are in flight while the other half computes
+    (KGC_TP_OVERLAP_MIN_TOKENS lowered from 2048 to 16).  TP = 4 replicates tiny-llama's 2 kv heads over 4 ranks; TP = 8
     (BASELINE config 3's degree) runs the 8-rank all-reduce instantiation with each of
     tiny-llama-gqa8's 2 kv heads on 4 ranks.  Greedy continuations match TP=1 (bf16;
     sharded sums round differently, so a couple of late near-tie flips are tolerated)."""
@@ -196,6 +200,8 @@ def test_tp_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch, tp, eager, name):
     sp = [SamplingParams(temperature=0, max_tokens=8, ignore_eos=True)] * 3
     outs = {}
     monkeypatch.setenv("KGC_DIST_BACKEND", "gloo")
+    if overlap:
+        monkeypatch.setenv("KGC_TP_OVERLAP_MIN_TOKENS", "16")
     tp_n = tp
     for tp in (1, tp_n):
         llm = LLM(d, device="cuda", dtype="bfloat16", tensor_parallel_size=tp, enforce_eager=eager,

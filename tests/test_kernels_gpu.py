@@ -295,6 +295,58 @@ def test_prefill_long_gqa_matches_fp32(gpu, monkeypatch, gqa, nq, nkv, S):
         torch.testing.assert_close(out[qsl[i]:qsl[i + 1]][rows], exp, atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("gqa", ["1", "0"])
+@pytest.mark.parametrize("shape", ["ramp", "steps"])
+def test_prefill_lazy_rescale_growing_scores(gpu, monkeypatch, gqa, shape):
+    """K2's lazy O rescale (PF_RESCALE_THR) on scores whose row max keeps GROWING along
+    the keys -- the branch random data never takes: every row's running max moves by
+    small steps (skipped: P up to 2^8 at the stale max) and by jumps (rescale of O, l and
+    m together), on the diagonal tiles and off them.  fp32 dense causal reference."""
+    monkeypatch.setenv("KGC_PREFILL_GQA", gqa)
+    torch.manual_seed(7)
+    d, bs, dt, nq, nkv = 128, 32, torch.bfloat16, 32, 8
+    seq_lens, query_lens = [2048, 1500], [2048, 300]
+    kc, vc, bt = _fill_random_cache(len(seq_lens), seq_lens, nkv, bs, d, dt, gpu)
+    kc_cpu = kc.cpu().float()
+    for i, L in enumerate(seq_lens):
+        pos = torch.arange(L).float()
+        if shape == "ramp":        # ~2 log2 units per 64-key tile: rescale every few tiles
+            a = pos * (120.0 / 2048)
+        else:                      # flat stretches and jumps of ~12 log2 units
+            a = torch.floor(pos / 300) * 25.0
+        nbk = (L + bs - 1) // bs
+        for j in range(nbk):
+            b = int(bt[i, j])
+            n = min(bs, L - j * bs)
+            kc_cpu[b, :, :n, :] += (a[j * bs:j * bs + n] / d)[None, :, None]
+    kc = kc_cpu.to(dt).to(gpu)
+    qsl = [0]
+    for ql in query_lens:
+        qsl.append(qsl[-1] + ql)
+    q = (torch.randn(qsl[-1], nq, d) * 0.5 + 4.0).to(dt).to(gpu)
+    qsl_t = torch.tensor(qsl, dtype=torch.int32, device=gpu)
+    sl_t = torch.tensor(seq_lens, dtype=torch.int32, device=gpu)
+    out = ops.prefill_attention(q, kc, vc, bt, qsl_t, sl_t, d ** -0.5).cpu().float()
+    assert torch.isfinite(out).all()
+    for i in range(2):
+        L, ql = seq_lens[i], query_lens[i]
+        nbk = (L + bs - 1) // bs
+        blocks = bt[i, :nbk].cpu().long()
+        k = kc.cpu()[blocks].permute(0, 2, 1, 3).reshape(nbk * bs, nkv, d)[:L].float()
+        v = vc.cpu()[blocks].permute(0, 2, 4, 1, 3).reshape(nbk * bs, nkv, d)[:L].float()
+        rows = torch.cat([torch.arange(min(96, ql)), torch.arange(max(0, ql - 64), ql),
+                          torch.randint(0, ql, (128,))]).unique()
+        qi = q.cpu()[qsl[i]:qsl[i + 1]][rows].float()
+        rep = nq // nkv
+        kk = k.repeat_interleave(rep, 1).permute(1, 0, 2)
+        vv = v.repeat_interleave(rep, 1).permute(1, 0, 2)
+        sc = torch.einsum("qhd,hkd->hqk", qi, kk) * d ** -0.5
+        posq = (L - ql + rows)[:, None]
+        sc = sc.masked_fill(torch.arange(L)[None, :] > posq, float("-inf"))
+        exp = torch.einsum("hqk,hkd->qhd", torch.softmax(sc, -1), vv)
+        torch.testing.assert_close(out[qsl[i]:qsl[i + 1]][rows], exp, atol=3e-2, rtol=3e-2)
+
+
 def test_prefill_matches_dense(gpu):
     """End-to-end: rope_kv_write -> prefill kernel == dense causal attention."""
     torch.manual_seed(5)
