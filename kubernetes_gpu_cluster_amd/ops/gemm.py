@@ -16,6 +16,7 @@ from __future__ import annotations
 import logging
 import os
 import time
+import weakref
 from typing import Iterable, Optional
 
 import torch
@@ -52,7 +53,34 @@ DG_MAX_M = 512
 _plan_dg: dict[tuple[int, int, int, str], tuple[int, int]] = {}
 _dg_enabled = os.environ.get("KGC_DGEMM", "1") != "0"
 # packed weight copies for the packed K9m tiles: (data_ptr, silu) -> [N/128, K/64, 8192]
-_packed: dict[tuple[int, bool], torch.Tensor] = {}
+# (data_ptr, silu) -> (weakref to the source weight, packed copy).  The weakref drops the
+# entry when the weight dies: a later tensor allocated at the same address (the next
+# engine in the same process, a test) must never pick up this weight's packed copy.
+_packed: dict[tuple[int, bool], tuple] = {}
+
+
+def _packed_get(w: torch.Tensor, silu: bool) -> Optional[torch.Tensor]:
+    key = (w.data_ptr(), silu)
+    e = _packed.get(key)
+    if e is None:
+        return None
+    src = e[0]()
+    if src is None:
+        _packed.pop(key, None)
+        return None
+    if src.data_ptr() != w.data_ptr() or src.shape != w.shape:
+        return None
+    return e[1]
+
+
+def _packed_put(w: torch.Tensor, silu: bool, p: torch.Tensor) -> None:
+    key = (w.data_ptr(), silu)
+
+    def drop(ref, key=key):
+        e = _packed.get(key)
+        if e is not None and e[0] is ref:
+            del _packed[key]
+    _packed[key] = (weakref.ref(w, drop), p)
 _PACK_FRACTION = float(os.environ.get("KGC_DGEMM_PACK_FRACTION", "0.25"))
 
 
@@ -81,7 +109,7 @@ def pack_decode_weights(plain: Iterable[torch.Tensor], silu: Iterable[torch.Tens
     for w, sl in [(w, False) for w in plain] + [(w, True) for w in silu]:
         if (w.is_cuda and w.dim() == 2 and w.dtype in (torch.bfloat16, torch.float16)
                 and w.is_contiguous() and w.shape[0] % 128 == 0 and w.shape[1] % 64 == 0
-                and (w.data_ptr(), sl) not in _packed):
+                and _packed_get(w, sl) is None):
             todo.append((w, sl))
     need = sum(w.numel() * w.element_size() for w, _ in todo)
     if not todo:
@@ -95,13 +123,13 @@ def pack_decode_weights(plain: Iterable[torch.Tensor], silu: Iterable[torch.Tens
         N, K = w.shape
         p = torch.empty(N // 128, K // 64, 8192, dtype=w.dtype, device=w.device)
         _k().dgemm_pack(p, w, sl)
-        _packed[(w.data_ptr(), sl)] = p
+        _packed_put(w, sl, p)
     log.info("K9m: packed %d decode weights (%.1f GB)", len(todo), need / 1e9)
     return need
 
 
 def packed_weight(w: torch.Tensor, silu: bool = False) -> Optional[torch.Tensor]:
-    return _packed.get((w.data_ptr(), silu))
+    return _packed_get(w, silu)
 
 
 def _dg_weight(w: torch.Tensor, cfg: int, silu: bool) -> Optional[torch.Tensor]:

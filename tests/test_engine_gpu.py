@@ -127,27 +127,56 @@ def test_graph_equals_eager_and_async_equals_sync(gpu):
             assert a[:4] == b[:4], (k, a, b)
 
 
+def _run_lp(eng, prompts, params):
+    """Greedy runs with top-2 logprobs per generated token: {request: [(tok, lp, top2)]}."""
+    seqs = [eng.add_request(p, sp) for p, sp in zip(prompts, params)]
+    lps = {s.request_id: [] for s in seqs}
+    while eng.has_unfinished():
+        for o in eng.step():
+            if o.logprobs:
+                lps[o.request_id].extend(o.logprobs)
+    return [(s.output_token_ids, lps[s.request_id]) for s in seqs]
+
+
+def _assert_greedy_agrees(got, base, n_first, tie=0.05):
+    """Greedy continuations agree on the first n_first tokens -- except at a near-tie:
+    where they first differ, the base run's top-2 logprob gap must be < ``tie`` and the
+    other run's token must be the base run's runner-up (kernels with different rounding,
+    e.g. a graph bucket's GEMM choice or split-context factor, may break a tie either
+    way; after that the two continuations are different texts and are not compared)."""
+    (a, _), (b, lpb) = got, base
+    for i in range(min(n_first, len(a), len(b))):
+        if a[i] == b[i]:
+            continue
+        tok, lp, top = lpb[i]
+        alts = dict(top)
+        assert a[i] in alts, (i, a, b, top)
+        assert abs(lp - alts[a[i]]) < tie, (i, a, b, top)
+        return
+
+
 def test_decode_rope_fused_equals_unfused(gpu, monkeypatch):
     """Decode steps with RoPE + KV write inside the paged-decode kernel give the same
-    greedy tokens as rope_kv_write + paged_decode, eager and replayed from hipGraphs."""
+    greedy tokens as rope_kv_write + paged_decode, eager and replayed from hipGraphs
+    (up to a near-tie, see _assert_greedy_agrees)."""
     from kubernetes_gpu_cluster_amd.models import llama
     g = torch.Generator().manual_seed(5)
     prompts = [torch.randint(100, 128000, (n,), generator=g).tolist() for n in (9, 150, 33)]
-    params = [SamplingParams(temperature=0.0, max_tokens=16, ignore_eos=True)
+    params = [SamplingParams(temperature=0.0, max_tokens=16, ignore_eos=True, logprobs=2)
               for _ in prompts]
     outs = {}
     for fused in (False, True):
         monkeypatch.setattr(llama, "_decode_rope_fused", fused)
         for eager in (True, False):
             eng = _tiny_engine(enforce_eager=eager)
-            outs[(fused, eager)] = _run(eng, prompts, params)
+            outs[(fused, eager)] = _run_lp(eng, prompts, params)
             del eng
             torch.cuda.empty_cache()
     base = outs[(False, True)]
     for k, v in outs.items():
-        for a, b in zip(v, base):
-            assert len(a) == 16
-            assert a[:4] == b[:4], (k, a, b)
+        for got, ref in zip(v, base):
+            assert len(got[0]) == 16 and len(got[1]) == 16
+            _assert_greedy_agrees(got, ref, 8)
 
 
 def test_engine_preemption_recompute(gpu):

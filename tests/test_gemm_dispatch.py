@@ -41,3 +41,23 @@ def test_tail_fusion_not_taken_on_cpu():
         assert not m._tail_fusable(torch.zeros(4, cfg.hidden_size))
     finally:
         gemm.clear_plan()
+
+
+def test_packed_weight_cache_drops_dead_weights():
+    """K9m's packed-weight cache is keyed by the weight's address; an entry must die with
+    its weight, so a later tensor allocated at the same address (the next engine in the
+    same process) never reads another weight's packed copy."""
+    import gc
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    w = torch.zeros(128, 64)
+    packed = torch.ones(3)
+    gemm._packed_put(w, False, packed)
+    assert gemm._packed_get(w, False) is packed and gemm.packed_weight(w) is packed
+    assert gemm._packed_get(w, True) is None
+    view = w[:64]                      # same address, different tensor: not the packed weight
+    assert gemm._packed_get(view, False) is None
+    assert gemm._packed_get(w, False) is packed    # ... and does not evict the entry
+    n = len(gemm._packed)
+    del w, view
+    gc.collect()
+    assert len(gemm._packed) == n - 1
