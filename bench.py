@@ -90,6 +90,9 @@ def parse():
     ap.add_argument("--api-server-count", type=int, default=0,
                     help="service mode: API processes per engine (0: server default)")
     ap.add_argument("--startup-timeout", type=float, default=1800)
+    ap.add_argument("--no-comm-probe", dest="comm_probe", action="store_false", default=True,
+                    help="service mode, N > 1: skip the RCCL / xGMI all-reduce probe that runs "
+                         "after the timed waves (benchmarks/comm_probe.py)")
     ap.add_argument("--router-workers", type=int, default=0,
                     help="service mode: router processes in front of all replicas "
                          "(0: one per replica, at most 16)")
@@ -410,6 +413,9 @@ def main_service(args):
         codes = sc.stop(procs)
         if leader and procs:
             _note(f"rank {rank}: service stopped (exit codes {codes})")
+    probe = None
+    if world > 1 and not cpu and args.comm_probe:
+        probe = _comm_probe(rank, world, local_rank)
     ok = [r for r in res_all if r.ok]
     mine = {"toks": sum(r.tokens for r in ok), "failed": len(res_all) - len(ok),
             "ttft": [r.ttft for r in ok], "tpot": [(r.e2e - r.ttft) / max(1, r.tokens - 1) for r in ok],
@@ -454,6 +460,9 @@ def main_service(args):
             # router CPU-seconds per wall second over the timed waves (all its workers)
             "router_cpu_util": round(router_cpu / elapsed, 3) if elapsed > 0 else None,
             "router_workers": args.router_workers or max(1, min(16, replicas)),
+            # after the timed waves, outside the timed region: RCCL all-reduce bus
+            # bandwidth and the xGMI kernel vs RCCL on this node's GPUs (N > 1)
+            "comm_probe": probe,
             "config": {"model": args.model, "global_batch": args.num_prompts * replicas,
                        "seq_len": args.input_len + args.output_len, "input_len": args.input_len,
                        "output_len": args.output_len,
@@ -475,6 +484,43 @@ def main_service(args):
         dist.destroy_process_group()
     if failed_any(parts if rank == 0 else [mine]):
         sys.exit(1)
+
+
+def _comm_probe(rank: int, world: int, local_rank: int, timeout_s: float = 240.0):
+    """benchmarks/comm_probe.py on every rank's GPU (the API servers are stopped), as a
+    child process with a hard time limit so a collective that never completes cannot
+    hold up the benchmark's own result.  Returns rank 0's table (None elsewhere)."""
+    import signal
+    import subprocess
+    import tempfile
+    from kubernetes_gpu_cluster_amd.benchmarks import serving_client as sc
+    box = [_free_port(local_rank, 2) if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    out = os.path.join(tempfile.gettempdir(), f"kgc_comm_probe_{os.getpid()}.json")
+    cmd = [sys.executable, "-m", "kubernetes_gpu_cluster_amd.benchmarks.comm_probe",
+           "--rank", str(rank), "--world", str(world), "--port", str(box[0]),
+           "--device", str(local_rank)] + (["--out", out] if rank == 0 else [])
+    _note(f"rank {rank}: collective probe (RCCL + xGMI all-reduce, world {world})")
+    p = subprocess.Popen(cmd, env=sc._env({}), start_new_session=True,
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    try:
+        _, err = p.communicate(timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.communicate()
+        return {"error": f"timed out after {timeout_s:.0f} s"} if rank == 0 else None
+    if rank != 0:
+        return None
+    if p.returncode != 0:
+        return {"error": f"exit {p.returncode}: {(err or '')[-400:]}"}
+    try:
+        with open(out) as f:
+            return json.loads(f.read())
+    except (OSError, ValueError) as e:
+        return {"error": str(e)}
+    finally:
+        if os.path.exists(out):
+            os.remove(out)
 
 
 def failed_any(parts) -> bool:

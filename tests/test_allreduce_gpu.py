@@ -256,3 +256,26 @@ def _rms_worker(rank, world, port):
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_xgmi_allreduce_add_rmsnorm_fused(world, gpu):
     _run_world(_rms_worker, world)
+
+
+def test_comm_probe_two_ranks_on_one_gpu(gpu, tmp_path):
+    """benchmarks/comm_probe.py (run by bench.py at N > 1 on the real node): two ranks on
+    cuda:0 with gloo standing in for RCCL; the xGMI kernel rows must be correct and the
+    table complete (one-shot, two-shot, library time per size, crossover)."""
+    import json
+    import subprocess
+    import sys
+    port = _port()
+    out = tmp_path / "probe.json"
+    procs = [subprocess.Popen([sys.executable, "-m", "kubernetes_gpu_cluster_amd.benchmarks.comm_probe",
+                               "--rank", str(r), "--world", "2", "--port", str(port), "--device", "0",
+                               "--backend", "gloo", "--iters", "3"]
+                              + (["--out", str(out)] if r == 0 else []))
+             for r in range(2)]
+    for p in procs:
+        assert p.wait(timeout=110) == 0
+    res = json.loads(out.read_text())
+    assert res["world"] == 2 and res["rccl_correct"]
+    assert len(res["rccl"]) == 4 and all(r["us"] > 0 for r in res["rccl"])
+    assert len(res["xgmi"]) == 6 and all(r["correct"] for r in res["xgmi"])
+    assert len(res["crossover"]["best_per_size"]) == 6
