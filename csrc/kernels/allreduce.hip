@@ -67,10 +67,19 @@ __device__ __forceinline__ void ar_barrier(const ArPtrs& P, int rank, int phase,
     ArSignal* self = reinterpret_cast<ArSignal*>(P.sig[rank]);
     uint32_t* f = &self->flag[phase][blockIdx.x][threadIdx.x];
     const unsigned long long dl = spin_deadline(KGC_PEER_SPIN_MS);
-    while ((int32_t)(ar_load_flag(f) - epoch) < 0) {
+    // a group that already failed (sticky err) does not wait again: one time-out per
+    // dead peer, not one per collective (graph warm-ups run dozens back to back)
+    const bool failed = ar_load_flag(&self->err) != 0u;
+    while (!failed && (int32_t)(ar_load_flag(f) - epoch) < 0) {
       __builtin_amdgcn_s_sleep(1);
       if (spin_expired(dl)) {        // a peer is gone: fail loudly on the host
-        atomicOr(&self->err, 1u << threadIdx.x);
+        // ... on EVERY rank's host: the word is raised in each peer's signal too, so the
+        // driver rank sees a time-out that only a worker rank observed (that worker
+        // would otherwise carry on with a stale peer input, silently, unchecked)
+        for (int p = 0; p < NR; ++p)
+          __hip_atomic_fetch_or(&reinterpret_cast<ArSignal*>(P.sig[p])->err,
+                                1u << threadIdx.x, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
     }

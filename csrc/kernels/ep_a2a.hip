@@ -104,10 +104,14 @@ __device__ void ep_wait_all(const EpPtrs& P, int rank, int phase, uint32_t epoch
     EpSignal* self = reinterpret_cast<EpSignal*>(P.sig[rank]);
     uint32_t* f = &self->flag[phase][threadIdx.x];
     const unsigned long long dl = spin_deadline(KGC_PEER_SPIN_MS);
-    while ((int32_t)(ep_load(f) - epoch) < 0) {
+    const bool failed = ep_load(&self->err) != 0u;   // sticky: fail fast after the first
+    while (!failed && (int32_t)(ep_load(f) - epoch) < 0) {
       __builtin_amdgcn_s_sleep(1);
-      if (spin_expired(dl)) {
-        atomicOr(&self->err, 1u << threadIdx.x);
+      if (spin_expired(dl)) {      // raised on every rank, as the all-reduce does
+        for (int p = 0; p < NR; ++p)
+          __hip_atomic_fetch_or(&reinterpret_cast<EpSignal*>(P.sig[p])->err,
+                                1u << threadIdx.x, __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
     }

@@ -43,7 +43,8 @@ __device__ __forceinline__ void pp_store(uint32_t* p, uint32_t v) {
 __device__ void pp_wait(PpSignal* own, uint32_t* f, uint32_t target) {
   if (threadIdx.x == 0) {
     const unsigned long long dl = spin_deadline(KGC_PEER_SPIN_MS);
-    while ((int32_t)(pp_load(f) - target) < 0) {
+    const bool failed = pp_load(&own->err) != 0u;    // sticky: fail fast after the first
+    while (!failed && (int32_t)(pp_load(f) - target) < 0) {
       __builtin_amdgcn_s_sleep(1);
       if (spin_expired(dl)) {
         atomicOr(&own->err, 1u);
