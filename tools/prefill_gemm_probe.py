@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--tokens", type=int, default=16384)
     ap.add_argument("--layers", type=int, default=8)
+    ap.add_argument("--reps", type=int, default=5,
+                    help="timed calls per measurement (200+: sustained, power-managed clocks)")
+    ap.add_argument("--tables", default="default,tuned")
     a = ap.parse_args()
     from kubernetes_gpu_cluster_amd.models.configs import PRESETS
     from kubernetes_gpu_cluster_amd.utils.gemm_tuning import enable_tuned_gemms
@@ -53,19 +56,19 @@ def main():
         print(json.dumps({"kind": kind, "table": table, "M": M, "ms": round(ms, 3),
                           "PFps": round(fl / ms / 1e12, 3)}), flush=True)
 
-    for table in ("default", "tuned"):
+    for table in a.tables.split(","):
         if table == "tuned" and not enable_tuned_gemms(a.model, 1):
             print(json.dumps({"error": "tuned table not loaded"}))
             break
         for n in shapes:
             w, x = ws[n][0], xs[n]
-            report(n, table, timed(lambda: F.linear(x, w)), flops[n])
+            report(n, table, timed(lambda: F.linear(x, w), a.reps), flops[n])
 
         def layer_seq():
             for i in range(a.layers):
                 for n in shapes:
                     F.linear(xs[n], ws[n][i])
-        ms = timed(layer_seq, reps=3) / a.layers
+        ms = timed(layer_seq, reps=max(3, a.reps // 20)) / a.layers
         report("layer", table, ms, sum(flops.values()))
 
 
