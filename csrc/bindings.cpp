@@ -529,6 +529,9 @@ void dgemm(Tensor C, Tensor X, Tensor W, int64_t cfg, int64_t epi) {
                 "C [M, N] (epi 1) or [M, N/2] (epi 2), contiguous, W's dtype");
   }
   TORCH_CHECK((M + bm - 1) / bm * (N / bn) * S < ((int64_t)1 << 31), "grid too large");
+  // the K9v configs cover all rows with one 256-row tile (no row-block loop)
+  TORCH_CHECK(!kgc::dgemm_cfg_single_row_block((int)cfg) || M <= bm,
+              "K9v configs take M <= 256");
   if (M == 0) return;
   kgc::launch_dgemm(dt_code(W), (int)cfg, (int)epi, C.data_ptr(), X.data_ptr(), W.data_ptr(),
                     (int)M, (int)N, (int)K, X.stride(0), (int)S, ss, stream());
@@ -557,6 +560,7 @@ std::vector<int64_t> dgemm_cfg_info(int64_t cfg) {
   return {bm, bn, packed};
 }
 int64_t dgemm_num_cfgs() { return kgc::dgemm_num_cfgs(); }
+bool dgemm_cfg_single_row_block(int64_t cfg) { return kgc::dgemm_cfg_single_row_block((int)cfg); }
 
 // profiling only: the packed 256 x 128 tile with its MFMAs / DMAs / one operand's DMAs removed
 void dgemm_ablate(Tensor C, Tensor X, Tensor W, int64_t mode) {
@@ -1036,6 +1040,7 @@ TORCH_LIBRARY(kgc, m) {
   m.def("dgemm(Tensor(a!) C, Tensor X, Tensor W, int cfg, int epi) -> ()");
   m.def("dgemm_cfg_info(int cfg) -> int[]", &dgemm_cfg_info);
   m.def("dgemm_num_cfgs() -> int", &dgemm_num_cfgs);
+  m.def("dgemm_cfg_single_row_block(int cfg) -> bool", &dgemm_cfg_single_row_block);
   m.def("dgemm_ablate(Tensor(a!) C, Tensor X, Tensor W, int mode) -> ()");
   m.def("dgemm_pack(Tensor(a!) P, Tensor W, bool silu) -> ()");
   m.def("ring_gemm(Tensor(a!) C, Tensor X, Tensor Wp, int cfg, int epi) -> ()");

@@ -121,6 +121,7 @@ void launch_dense_gemm_splitk(int dtype, int bm, float* Cs, const void* A, const
 int dgemm_num_cfgs();
 void dgemm_cfg_info(int cfg, int* bm, int* bn, int* packed);
 int dgemm_block_k();
+bool dgemm_cfg_single_row_block(int cfg);   // K9v: one BM-row tile, M <= BM
 void launch_dgemm(int dtype, int cfg, int epi, void* C, const void* X, const void* W, int M,
                   int N, int K, int64_t ldx, int S, int64_t slice_stride, hipStream_t s);
 void launch_dgemm_pack(int dtype, bool silu, void* P, const void* W, int N, int K,
