@@ -121,7 +121,10 @@ void rope_kv_write(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor q_out, T
   TORCH_CHECK(slot_mapping.scalar_type() == at::kLong && slot_mapping.numel() == T, "slot_mapping int64 [T]");
   TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() && cos_sin.size(1) == d,
               "cos_sin fp32 [max_pos, d]");
-  TORCH_CHECK(q_out.is_contiguous() && q_out.numel() == T * nq * d, "q_out [T, nq, d]");
+  // an empty q_out: write k / v only (prefill_attention_rope rotates q as it loads it)
+  const bool kv_only = q_out.numel() == 0;
+  TORCH_CHECK(kv_only || (q_out.is_contiguous() && q_out.numel() == T * nq * d),
+              "q_out [T, nq, d] (or empty: k / v only)");
   TORCH_CHECK(k_cache.is_contiguous() && v_cache.is_contiguous() && k_cache.dim() == 4 &&
               v_cache.dim() == 5 && k_cache.size(1) == nkv && k_cache.size(3) == d &&
               v_cache.size(3) == d && v_cache.size(4) == 8 &&
@@ -137,8 +140,9 @@ void rope_kv_write(Tensor qkv, Tensor positions, Tensor cos_sin, Tensor q_out, T
   }
   kgc::launch_rope_kv_write(dt_code(q_out), qkv.data_ptr(), stride, (int)S, ss,
                             positions.data_ptr<int64_t>(), cos_sin.data_ptr<float>(),
-                            q_out.data_ptr(), k_cache.data_ptr(), v_cache.data_ptr(),
-                            slot_mapping.data_ptr<int64_t>(), qn, kn, (int)T, (int)nq, (int)nkv,
+                            kv_only ? nullptr : q_out.data_ptr(), k_cache.data_ptr(),
+                            v_cache.data_ptr(), slot_mapping.data_ptr<int64_t>(), qn, kn,
+                            (int)T, (int)nq, (int)nkv,
                             (int)d, (int)k_cache.size(2), (float)eps, use_rope, kv8,
                             (float)k_scale, (float)v_scale, (int)k_cache.size(0), stream());
 }
@@ -292,7 +296,49 @@ void prefill_attention(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Ten
                                 (int)k_cache.size(1), (int)d,
                                 log2_exact(k_cache.size(2), "block_size"), (float)scale,
                                 k_cache.scalar_type() == at::kFloat8_e4m3fn, (float)k_scale,
-                                (float)v_scale, (int)k_cache.size(0), stream());
+                                (float)v_scale, (int)k_cache.size(0), nq * d, nullptr, 0, stream());
+}
+
+// K2 on a prefill-only step with RoPE folded into the q load: qkv [T, >= (nq+2nkv)*d]
+// (the unrotated QKV projection; rope_kv_write wrote only k / v), positions implicit
+// (ctx0 + row, as the engine assigns them), out [T, nq, d]
+void prefill_attention_rope(Tensor out, Tensor qkv, Tensor cos_sin, Tensor k_cache,
+                            Tensor v_cache, Tensor block_tables, Tensor query_start_loc,
+                            Tensor seq_lens, Tensor work_seq, Tensor work_mblk, int64_t nq,
+                            double scale, double k_scale, double v_scale) {
+  check_gpu(qkv, "qkv");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
+  TORCH_CHECK(out.dim() == 3 && out.is_contiguous() && out.size(1) == nq &&
+              out.scalar_type() == qkv.scalar_type(), "out [T, nq, d] contiguous, qkv's dtype");
+  const int64_t d = out.size(2), T = out.size(0);
+  check_kv(out, k_cache, v_cache, nq);
+  const int64_t nkv = k_cache.size(1);
+  TORCH_CHECK(k_cache.size(3) == d, "head_dim mismatch");
+  TORCH_CHECK(qkv.dim() == 2 && qkv.size(0) == T && qkv.stride(1) == 1 &&
+              qkv.size(1) >= (nq + 2 * nkv) * d && qkv.stride(0) % 8 == 0 &&
+              reinterpret_cast<uintptr_t>(qkv.data_ptr()) % 16 == 0,
+              "qkv [T, >= (nq + 2 nkv) d], 16-B aligned rows");
+  TORCH_CHECK(cos_sin.scalar_type() == at::kFloat && cos_sin.is_contiguous() &&
+              cos_sin.dim() == 2 && cos_sin.size(1) == d, "cos_sin fp32 [max_pos, d]");
+  const int64_t P = seq_lens.numel();
+  TORCH_CHECK(block_tables.scalar_type() == at::kInt && block_tables.dim() == 2 &&
+              block_tables.size(0) >= P && block_tables.is_contiguous(), "block_tables contiguous");
+  TORCH_CHECK(query_start_loc.scalar_type() == at::kInt && query_start_loc.numel() == P + 1, "query_start_loc");
+  TORCH_CHECK(seq_lens.scalar_type() == at::kInt, "seq_lens int32");
+  TORCH_CHECK(work_seq.scalar_type() == at::kInt && work_mblk.scalar_type() == at::kInt &&
+              work_seq.numel() == work_mblk.numel(), "work list");
+  TORCH_CHECK(work_seq.numel() <= 2147483647 && nq <= 65535, "grid");
+  TORCH_CHECK(cos_sin.size(0) >= 1 && cos_sin.size(0) < ((int64_t)1 << 31), "cos_sin rows");
+  kgc::launch_prefill_attention(dt_code(out), qkv.data_ptr(), out.data_ptr(), k_cache.data_ptr(),
+                                v_cache.data_ptr(), block_tables.data_ptr<int>(),
+                                (int)block_tables.stride(0), query_start_loc.data_ptr<int>(),
+                                seq_lens.data_ptr<int>(), work_seq.data_ptr<int>(),
+                                work_mblk.data_ptr<int>(), (int)work_seq.numel(), (int)nq,
+                                (int)nkv, (int)d, log2_exact(k_cache.size(2), "block_size"),
+                                (float)scale, k_cache.scalar_type() == at::kFloat8_e4m3fn,
+                                (float)k_scale, (float)v_scale, (int)k_cache.size(0),
+                                qkv.stride(0), cos_sin.data_ptr<float>(), (int)cos_sin.size(0),
+                                stream());
 }
 
 void sample(Tensor out, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, Tensor seeds,
@@ -1023,6 +1069,10 @@ TORCH_LIBRARY(kgc, m) {
   m.def("prefill_attention(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
         "Tensor block_tables, Tensor query_start_loc, Tensor seq_lens, Tensor work_seq, "
         "Tensor work_mblk, float scale, float k_scale=1.0, float v_scale=1.0) -> ()");
+  m.def("prefill_attention_rope(Tensor(a!) out, Tensor qkv, Tensor cos_sin, Tensor k_cache, "
+        "Tensor v_cache, Tensor block_tables, Tensor query_start_loc, Tensor seq_lens, "
+        "Tensor work_seq, Tensor work_mblk, int nq, float scale, float k_scale=1.0, "
+        "float v_scale=1.0) -> ()");
   m.def("sample(Tensor(a!) out, Tensor logits, Tensor temperature, Tensor top_k, Tensor top_p, "
         "Tensor seeds, bool thresholds=True) -> ()");
   m.def("sample_vp(Tensor(a!) packed, Tensor logits, int V, Tensor temperature, Tensor seeds, "
@@ -1104,6 +1154,7 @@ TORCH_LIBRARY_IMPL(kgc, CUDA, m) {
   m.impl("paged_decode", &paged_decode);
   m.impl("paged_decode_rope", &paged_decode_rope);
   m.impl("prefill_attention", &prefill_attention);
+  m.impl("prefill_attention_rope", &prefill_attention_rope);
   m.impl("sample", &sample);
   m.impl("sample_vp", &sample_vp);
   m.impl("sample_vp_unpack", &sample_vp_unpack);

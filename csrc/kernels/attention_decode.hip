@@ -99,9 +99,7 @@ __device__ __forceinline__ void rope8(float* a, float* b, const float* cs, int c
   const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float xa = a[j], xb = b[j];
-    a[j] = xa * cc[j] - xb * sn[j];
-    b[j] = xb * cc[j] + xa * sn[j];
+    neox_rot(a[j], b[j], cc[j], sn[j], a[j], b[j]);
   }
 }
 

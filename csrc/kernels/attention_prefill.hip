@@ -31,6 +31,45 @@ constexpr int PF_BN = 64;
 
 __device__ __forceinline__ int kswz(int k) { return (k & 3) | (((k >> 3) & 3) << 2); }
 
+// q fragments of one 16-row q-tile: lane (r16, qd) holds dims 32 s + 8 qd .. + 7 of its
+// row.  cos_sin != nullptr: the row is the unrotated q of the fused QKV projection and
+// gets NeoX RoPE at position pos here -- dims i and i + D/2 sit in fragments s and
+// s + KS/2 of the same lane, so the rotation is lane-local -- rounded to T exactly as
+// rope_cache.hip rounds it.  (Prefill-only steps: rope_kv_write then writes only k / v,
+// and q is neither stored nor re-read.)
+template <typename T, int D>
+__device__ __forceinline__ void pf_load_q(const T* qrow, const float* __restrict__ cos_sin,
+                                          int cs_rows, int pos, int qd,
+                                          typename Vec8<T>::type (&qf)[D / 32]) {
+  constexpr int KS = D / 32;
+  Pack8<T> t[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) t[s].u = *reinterpret_cast<const u32x4*>(qrow + 32 * s + 8 * qd);
+  if (cos_sin != nullptr) {
+    // clamped: a bad sequence length gives wrong output, never a fault
+    const float* cs = cos_sin + (int64_t)min(pos, cs_rows - 1) * D;
+#pragma unroll
+    for (int s = 0; s < KS / 2; ++s) {
+      const int col = 32 * s + 8 * qd;
+      const float4 c0 = *reinterpret_cast<const float4*>(cs + col);
+      const float4 c1 = *reinterpret_cast<const float4*>(cs + col + 4);
+      const float4 s0 = *reinterpret_cast<const float4*>(cs + D / 2 + col);
+      const float4 s1 = *reinterpret_cast<const float4*>(cs + D / 2 + col + 4);
+      const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float ra, rb;
+        neox_rot(to_f(t[s].h[j]), to_f(t[s + KS / 2].h[j]), cc[j], sn[j], ra, rb);
+        t[s].h[j] = from_f<T>(ra);
+        t[s + KS / 2].h[j] = from_f<T>(rb);
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < KS; ++s) qf[s] = t[s].v;
+}
+
 // Lazy O rescale (log2 units): the running max m only moves when some row's tile max
 // exceeds it by more than this, so P = exp2(s - m) stays <= 2^8 and the O / l rescale
 // (DT*8 + 2 VALU per lane) runs on a few tiles per row instead of on every tile.  The
@@ -136,7 +175,8 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
     const void* __restrict__ vc_, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ qsl, const int* __restrict__ seq_lens,
     const int* __restrict__ work_seq, const int* __restrict__ work_mblk, int nq, int nkv,
-    int bs_log2, float scale_log2, float v_scale, int num_blocks) {
+    int bs_log2, float scale_log2, float v_scale, int num_blocks, int64_t q_stride,
+    const float* __restrict__ cos_sin, int cs_rows) {
   typedef typename Vec8<T>::type V8;
   typedef std::conditional_t<KV8, uint8_t, T> C;   // cache element
   typedef std::conditional_t<KV8, u32x2, u32x4> R; // staged raw fragment (8 elements)
@@ -178,13 +218,8 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
     const int qi = mb * PF_BM + wave * 32 + qt * 16 + r16;
     const int qc = min(qi, qlen - 1);
     qpos[qt] = ctx0 + qc;
-    const T* qrow = q + ((int64_t)(q0 + qc) * nq + hq) * D;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      Pack8<T> t;
-      t.u = *reinterpret_cast<const u32x4*>(qrow + 32 * s + 8 * qd);
-      qf[qt][s] = t.v;
-    }
+    pf_load_q<T, D>(q + (int64_t)(q0 + qc) * q_stride + (int64_t)hq * D, cos_sin, cs_rows,
+                    qpos[qt], qd, qf[qt]);
   }
   const int last_q = ctx0 + min((mb + 1) * PF_BM, qlen) - 1;
   const int n_tiles = last_q / PF_BN + 1;
@@ -302,7 +337,8 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_gqa_kernel(
     const void* __restrict__ vc_, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ qsl, const int* __restrict__ seq_lens,
     const int* __restrict__ work_seq, const int* __restrict__ work_mblk, int nq, int nkv,
-    int bs_log2, float scale_log2, float v_scale, int num_blocks) {
+    int bs_log2, float scale_log2, float v_scale, int num_blocks, int64_t q_stride,
+    const float* __restrict__ cos_sin, int cs_rows) {
   typedef typename Vec8<T>::type V8;
   typedef std::conditional_t<KV8, uint8_t, T> C;
   typedef std::conditional_t<KV8, u32x2, u32x4> R;
@@ -350,13 +386,8 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_gqa_kernel(
     const int qi = wq0 + qt * 16 + r16;
     const int qc = min(qi, qlen - 1);
     qpos[qt] = ctx0 + qc;
-    const T* qrow = q + ((int64_t)(q0 + qc) * nq + hq) * D;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      Pack8<T> t;
-      t.u = *reinterpret_cast<const u32x4*>(qrow + 32 * s + 8 * qd);
-      qf[qt][s] = t.v;
-    }
+    pf_load_q<T, D>(q + (int64_t)(q0 + qc) * q_stride + (int64_t)hq * D, cos_sin, cs_rows,
+                    qpos[qt], qd, qf[qt]);
   }
   const int last_q = ctx0 + min(qbase + QB, qlen) - 1;
   const int n_tiles = last_q / PF_BN + 1;
@@ -475,13 +506,13 @@ static void prefill_gqa_dispatch(const void* q, void* out, const void* kc, const
                                  const int* bt, int bt_stride, const int* qsl, const int* sl,
                                  const int* ws, const int* wm, int n_work, int nq, int nkv,
                                  int bs_log2, float scale_log2, float v_scale, int num_blocks,
-                                 hipStream_t s) {
+                                 int64_t q_stride, const float* cos_sin, int cs_rows, hipStream_t s) {
   const size_t lds = 2 * 2 * PF_BN * D * sizeof(T);
   const int G = nq / nkv;
   const dim3 grid(n_work, nkv * (G / GH), PF_BM / (256 / GH));
   prefill_attn_gqa_kernel<T, D, KV8, GH><<<grid, 512, lds, s>>>(
       (const T*)q, (T*)out, kc, vc, bt, bt_stride, qsl, sl, ws, wm, nq, nkv, bs_log2,
-      scale_log2, v_scale, num_blocks);
+      scale_log2, v_scale, num_blocks, q_stride, cos_sin, cs_rows);
 }
 
 template <typename T, int D, bool KV8>
@@ -489,21 +520,23 @@ static void prefill_dispatch(const void* q, void* out, const void* kc, const voi
                              const int* bt, int bt_stride, const int* qsl, const int* sl,
                              const int* ws, const int* wm, int n_work, int nq, int nkv,
                              int bs_log2, float scale_log2, float v_scale, int num_blocks,
-                             hipStream_t s) {
+                             int64_t q_stride, const float* cos_sin, int cs_rows, hipStream_t s) {
   const int G = nkv > 0 ? nq / nkv : 1;
   if (D == 128 && prefill_gqa_enabled() && nq % nkv == 0 && (G == 4 || G % 8 == 0)) {
     if (G == 4)
       prefill_gqa_dispatch<T, D, KV8, 4>(q, out, kc, vc, bt, bt_stride, qsl, sl, ws, wm, n_work,
-                                         nq, nkv, bs_log2, scale_log2, v_scale, num_blocks, s);
+                                         nq, nkv, bs_log2, scale_log2, v_scale, num_blocks,
+                                         q_stride, cos_sin, cs_rows, s);
     else
       prefill_gqa_dispatch<T, D, KV8, 8>(q, out, kc, vc, bt, bt_stride, qsl, sl, ws, wm, n_work,
-                                         nq, nkv, bs_log2, scale_log2, v_scale, num_blocks, s);
+                                         nq, nkv, bs_log2, scale_log2, v_scale, num_blocks,
+                                         q_stride, cos_sin, cs_rows, s);
     return;
   }
   const size_t lds = 2 * 2 * PF_BN * D * sizeof(T);
   prefill_attn_kernel<T, D, KV8><<<dim3(n_work, nq), 256, lds, s>>>(
       (const T*)q, (T*)out, kc, vc, bt, bt_stride, qsl, sl, ws, wm, nq,
-      nkv, bs_log2, scale_log2, v_scale, num_blocks);
+      nkv, bs_log2, scale_log2, v_scale, num_blocks, q_stride, cos_sin, cs_rows);
 }
 
 void launch_prefill_attention(int dtype, const void* q, void* out, const void* k_cache,
@@ -511,13 +544,14 @@ void launch_prefill_attention(int dtype, const void* q, void* out, const void* k
                               const int* query_start_loc, const int* seq_lens,
                               const int* work_seq, const int* work_mblk, int n_work, int nq,
                               int nkv, int D, int bs_log2, float scale, bool kv_fp8,
-                              float k_scale, float v_scale, int num_blocks, hipStream_t s) {
+                              float k_scale, float v_scale, int num_blocks, int64_t q_stride,
+                              const float* cos_sin, int cs_rows, hipStream_t s) {
   if (n_work == 0) return;
   const float sl2 = scale * k_scale * 1.4426950408889634f;
 #define KGC_PF(TT, DD, K8)                                                                 \
   prefill_dispatch<TT, DD, K8>(q, out, k_cache, v_cache, block_tables, bt_stride,          \
                                query_start_loc, seq_lens, work_seq, work_mblk, n_work, nq, \
-                               nkv, bs_log2, sl2, v_scale, num_blocks, s)
+                               nkv, bs_log2, sl2, v_scale, num_blocks, q_stride, cos_sin, cs_rows, s)
 #define KGC_PF_D(TT, K8) \
   if (D == 128) KGC_PF(TT, 128, K8); else KGC_PF(TT, 64, K8)
   if (dtype == DT_BF16) {

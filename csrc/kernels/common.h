@@ -91,6 +91,15 @@ __device__ __forceinline__ float block_max(float v, float* scratch) {
 
 __device__ __forceinline__ float fast_exp(float x) { return __expf(x); }
 
+// NeoX RoPE of the pair (a at dim i, b at dim i + d/2), with the two products and their
+// fused add spelled out so every kernel that rotates (rope_cache.hip, the decode
+// prologue, the prefill kernel's q load) rounds identically, whatever -ffp-contract does
+__device__ __forceinline__ void neox_rot(float a, float b, float c, float s, float& oa,
+                                         float& ob) {
+  oa = __builtin_fmaf(a, c, -(b * s));
+  ob = __builtin_fmaf(b, c, a * s);
+}
+
 // ---- fp8 (OCP e4m3, gfx950) KV cache ---------------------------------------------
 // Values are stored as fp8(x / scale) with the per-tensor scale folded into the
 // attention math by the kernels (K: softmax scale, V: output), so dequantisation is

@@ -56,7 +56,8 @@ void launch_prefill_attention(int dtype, const void* q, void* out, const void* k
                               const int* query_start_loc, const int* seq_lens,
                               const int* work_seq, const int* work_mblk, int n_work, int nq,
                               int nkv, int D, int bs_log2, float scale, bool kv_fp8,
-                              float k_scale, float v_scale, int num_blocks, hipStream_t s);
+                              float k_scale, float v_scale, int num_blocks, int64_t q_stride,
+                              const float* cos_sin, int cs_rows, hipStream_t s);
 // debug builds: sticky bounds-check error words of the K1 / K2 / K3 translation units
 // (read and cleared; always 0 in release builds)
 uint32_t dbg_err_attention_decode();

@@ -41,7 +41,9 @@ __device__ __forceinline__ u32x4 qkv8(const void* qkv, int64_t row_elem, int col
   }
 }
 
-template <typename T, bool NORM, bool ROPE, bool KV8, bool SL>
+// KVO: k / v only (q_out unused): the prefill attention kernel rotates q itself as it
+// loads it from the QKV row, so a prefill-only step never writes or re-reads q
+template <typename T, bool NORM, bool ROPE, bool KV8, bool SL, bool KVO>
 __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
     const void* __restrict__ qkv, int64_t qkv_stride, int S, int64_t slice_stride,
     const int64_t* __restrict__ positions,
@@ -54,7 +56,7 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
   const int t = blockIdx.x;
   const int tph = d >> 4;               // threads per head (pairs of 8-elem chunks)
   const int half = d >> 1;
-  const int n_qk = (nq + nkv) * tph;
+  const int n_qk = (KVO ? nkv : nq + nkv) * tph;
   const int n_qk_pad = (n_qk + 63) & ~63;
   const int it = blockIdx.y * ROPE_NT + threadIdx.x;
   int64_t slot = slot_mapping[t];
@@ -64,7 +66,7 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
   const int off = slot >= 0 ? (int)(slot % bs) : 0;
   if (it < n_qk_pad) {                  // whole waves take this branch together
     const bool active = it < n_qk;
-    const int head = active ? it / tph : 0;     // 0..nq-1 = q, nq.. = k
+    const int head = (active ? it / tph : 0) + (KVO ? nq : 0);   // 0..nq-1 = q, nq.. = k
     const int c = it % tph;                     // chunk index within the first half
     Pack8<T> a, b;
     a.u = qkv8<T, SL>(qkv, row + head * d, c * 8, S, slice_stride);
@@ -106,14 +108,16 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
       const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        oa.h[j] = from_f<T>(xa[j] * cc[j] - xb[j] * sn[j]);
-        ob.h[j] = from_f<T>(xb[j] * cc[j] + xa[j] * sn[j]);
+        float ra, rb;
+        neox_rot(xa[j], xb[j], cc[j], sn[j], ra, rb);
+        oa.h[j] = from_f<T>(ra);
+        ob.h[j] = from_f<T>(rb);
       }
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) { oa.h[j] = from_f<T>(xa[j]); ob.h[j] = from_f<T>(xb[j]); }
     }
-    if (head < nq) {
+    if (!KVO && head < nq) {
       T* dst = q_out + ((int64_t)t * nq + head) * d;
       *reinterpret_cast<u32x4*>(dst + c * 8) = oa.u;
       *reinterpret_cast<u32x4*>(dst + half + c * 8) = ob.u;
@@ -172,17 +176,22 @@ static void rope_dispatch(const void* qkv, int64_t qkv_stride, int S, int64_t ss
                           int nq, int nkv, int d, int bs, float eps, bool rope, float k_inv,
                           float v_inv, int num_blocks, hipStream_t s) {
   if (T_ == 0) return;
-  const int n_items = (((nq + nkv) * (d >> 4) + 63) & ~63) + nkv * (d >> 3);
+  const bool kvo = q_out == nullptr;
+  const int n_items = ((((kvo ? 0 : nq) + nkv) * (d >> 4) + 63) & ~63) + nkv * (d >> 3);
   const dim3 grid(T_, (n_items + ROPE_NT - 1) / ROPE_NT);
-#define KGC_ROPE_LAUNCH(N, R)                                                               \
-  rope_kv_kernel<T, N, R, KV8, SL><<<grid, ROPE_NT, 0, s>>>(                                \
+#define KGC_ROPE_LAUNCH(N, R, O)                                                            \
+  rope_kv_kernel<T, N, R, KV8, SL, O><<<grid, ROPE_NT, 0, s>>>(                             \
       qkv, qkv_stride, S, ss, pos, cs, (T*)q_out, kc, vc, slots, (const T*)qn,               \
       (const T*)kn, nq, nkv, d, bs, eps, k_inv, v_inv, num_blocks)
   const bool norm = qn != nullptr;
-  if (norm && rope) KGC_ROPE_LAUNCH(true, true);
-  else if (norm) KGC_ROPE_LAUNCH(true, false);
-  else if (rope) KGC_ROPE_LAUNCH(false, true);
-  else KGC_ROPE_LAUNCH(false, false);
+  if (kvo) {                    // prefill-only steps of RoPE models without q/k norm
+    if (rope && !norm) KGC_ROPE_LAUNCH(false, true, true);
+    else if (rope) KGC_ROPE_LAUNCH(true, true, true);
+    else KGC_ROPE_LAUNCH(false, false, true);
+  } else if (norm && rope) KGC_ROPE_LAUNCH(true, true, false);
+  else if (norm) KGC_ROPE_LAUNCH(true, false, false);
+  else if (rope) KGC_ROPE_LAUNCH(false, true, false);
+  else KGC_ROPE_LAUNCH(false, false, false);
 #undef KGC_ROPE_LAUNCH
 }
 

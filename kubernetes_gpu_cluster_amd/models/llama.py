@@ -42,6 +42,9 @@ _tail_fusion_enabled = os.environ.get("KGC_TAIL_FUSION", "1") != "0"
 _tp_ar_norm_enabled = os.environ.get("KGC_TP_AR_NORM", "1") != "0"
 # decode-only steps: RoPE + KV write folded into the paged-decode kernel (KGC_DECODE_ROPE_FUSED=0: off)
 _decode_rope_fused = os.environ.get("KGC_DECODE_ROPE_FUSED", "1") != "0"
+# prefill-only steps of RoPE models without q/k norm: K2 rotates q as it loads it from the
+# QKV row and rope_kv_write handles k / v only (q is never written or re-read)
+_prefill_rope_fused = os.environ.get("KGC_PREFILL_ROPE_FUSED", "1") != "0"
 
 
 class RMSNorm(nn.Module):
@@ -98,6 +101,17 @@ class LlamaAttention(nn.Module):
                 None if self.k_norm is None else self.k_norm.weight, self.cfg.rms_eps,
                 workspace=m.decode_workspace, grid_z=m.decode_grid_z, k_scale=ctx.k_scale,
                 v_scale=ctx.v_scale, dtype=self.qkv_proj.weight.dtype)
+            return o.view(o.shape[0], self.nq * self.cfg.head_dim)
+        if (_prefill_rope_fused and qkv.is_cuda and qkv.dim() == 2 and m.num_prefill_tokens
+                and not m.num_decodes and self.q_norm is None and self.k_norm is None
+                and m.num_prefill_tokens == qkv.shape[0]):
+            ops.kv_write_rope(qkv, positions, ctx.cos_sin, kc, vc, m.slot_mapping, self.nq,
+                              self.nkv, self.cfg.head_dim, k_scale=ctx.k_scale,
+                              v_scale=ctx.v_scale)
+            o = ops.prefill_attention_rope(
+                qkv, ctx.cos_sin, kc, vc, m.prefill_block_tables, m.query_start_loc,
+                m.prefill_seq_lens, self.attn.scale, self.nq, self.cfg.head_dim, m.work_seq,
+                m.work_mblk, k_scale=ctx.k_scale, v_scale=ctx.v_scale)
             return o.view(o.shape[0], self.nq * self.cfg.head_dim)
         q = ops.rope_kv_write(qkv, positions, ctx.cos_sin, kc, vc, ctx.attn.slot_mapping,
                               self.nq, self.nkv, self.cfg.head_dim,

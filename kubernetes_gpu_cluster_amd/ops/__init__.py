@@ -149,6 +149,19 @@ def rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Ten
     return q
 
 
+def kv_write_rope(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor,
+                  k_cache: torch.Tensor, v_cache: torch.Tensor, slot_mapping: torch.Tensor,
+                  num_heads: int, num_kv_heads: int, head_dim: int,
+                  k_norm_w: Optional[torch.Tensor] = None, eps: float = 1e-6,
+                  k_scale: float = 1.0, v_scale: float = 1.0) -> None:
+    """rope_kv_write for k / v only (GPU, bf16 / f16 qkv [T, N]): the q part is left to
+    ``prefill_attention_rope``, which rotates it as it loads it."""
+    q = torch.empty(0, dtype=qkv.dtype, device=qkv.device)
+    _k().rope_kv_write(qkv, positions, cos_sin, q, k_cache, v_cache, slot_mapping,
+                       k_norm_w, k_norm_w, num_heads, num_kv_heads, head_dim, eps, True,
+                       k_scale, v_scale)
+
+
 # ------------------------------------------------------------------ attention
 DECODE_PARTITION = 64        # tokens per wave-iteration of the decode kernel
 PREFILL_BLOCK_M = 128
@@ -266,6 +279,31 @@ def prefill_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Ten
         out = torch.empty_like(q)
     _k().prefill_attention(out, q, k_cache, v_cache, block_tables, query_start_loc, seq_lens,
                            work_seq, work_mblk, scale, k_scale, v_scale)
+    return out
+
+
+def prefill_attention_rope(qkv: torch.Tensor, cos_sin: torch.Tensor, k_cache: torch.Tensor,
+                           v_cache: torch.Tensor, block_tables: torch.Tensor,
+                           query_start_loc: torch.Tensor, seq_lens: torch.Tensor, scale: float,
+                           num_heads: int, head_dim: int, work_seq: Optional[torch.Tensor] = None,
+                           work_mblk: Optional[torch.Tensor] = None,
+                           out: Optional[torch.Tensor] = None,
+                           k_scale: float = 1.0, v_scale: float = 1.0) -> torch.Tensor:
+    """K2 on a prefill-only step whose q is still the unrotated QKV projection row: NeoX
+    RoPE (position = context start + row, as the engine numbers tokens) is applied as the
+    kernel loads q, so q is never written or re-read (k / v: ``kv_write_rope``)."""
+    T = qkv.shape[0]
+    if work_seq is None:
+        qsl = query_start_loc.tolist()
+        ws, wm = prefill_work_list([qsl[i + 1] - qsl[i] for i in range(len(qsl) - 1)],
+                                   seq_lens.tolist())
+        work_seq = torch.tensor(ws, dtype=torch.int32, device=qkv.device)
+        work_mblk = torch.tensor(wm, dtype=torch.int32, device=qkv.device)
+    if out is None:
+        out = torch.empty(T, num_heads, head_dim, dtype=qkv.dtype, device=qkv.device)
+    _k().prefill_attention_rope(out, qkv, cos_sin, k_cache, v_cache, block_tables,
+                                query_start_loc, seq_lens, work_seq, work_mblk, num_heads, scale,
+                                k_scale, v_scale)
     return out
 
 

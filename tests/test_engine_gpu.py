@@ -179,6 +179,27 @@ def test_decode_rope_fused_equals_unfused(gpu, monkeypatch):
             _assert_greedy_agrees(got, ref, 8)
 
 
+def test_prefill_rope_fused_equals_unfused(gpu, monkeypatch):
+    """Prefill-only steps with q RoPE inside the prefill attention kernel (and a k / v-only
+    rope_kv_write) give the same greedy tokens as the unfused path; mixed prefill + decode
+    steps keep the unfused path, so chunked prompts cover both (up to a near-tie)."""
+    from kubernetes_gpu_cluster_amd.models import llama
+    g = torch.Generator().manual_seed(7)
+    prompts = [torch.randint(100, 128000, (n,), generator=g).tolist() for n in (9, 300, 150)]
+    params = [SamplingParams(temperature=0.0, max_tokens=12, ignore_eos=True, logprobs=2)
+              for _ in prompts]
+    outs = {}
+    for fused in (False, True):
+        monkeypatch.setattr(llama, "_prefill_rope_fused", fused)
+        eng = _tiny_engine(enforce_eager=False)
+        outs[fused] = _run_lp(eng, prompts, params)
+        del eng
+        torch.cuda.empty_cache()
+    for got, ref in zip(outs[True], outs[False]):
+        assert len(got[0]) == 12
+        _assert_greedy_agrees(got, ref, 8)
+
+
 def test_engine_preemption_recompute(gpu):
     """A KV pool too small for the batch forces recompute preemption; every request
     still completes with the requested length."""

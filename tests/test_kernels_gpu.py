@@ -254,6 +254,53 @@ def test_prefill_attention(gpu, dt, d, nq, nkv):
     torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(dt))
 
 
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("gqa,d,nq,nkv", [("1", 128, 32, 8), ("0", 128, 32, 8),
+                                         ("1", 128, 64, 8), ("0", 64, 4, 4)])
+def test_prefill_rope_fused_equals_unfused(gpu, monkeypatch, dt, gqa, d, nq, nkv):
+    """Prefill-only step with q RoPE folded into K2's q load (kv_write_rope +
+    prefill_attention_rope) vs rope_kv_write + prefill_attention: the same K/V cache bytes,
+    the same attention output (the rotation is one shared helper, rounded the same way),
+    and both within tolerance of the fp32 reference.  Fresh prompts and chunked
+    continuations (positions = context start + row), GQA-shared and one-head kernels."""
+    monkeypatch.setenv("KGC_PREFILL_GQA", gqa)
+    torch.manual_seed(11)
+    bs = 16
+    seq_lens = [5, 130, 300, 64, 700]
+    query_lens = [5, 130, 100, 1, 257]
+    kc, vc, bt = _fill_random_cache(len(seq_lens), seq_lens, nkv, bs, d, dt, gpu)
+    qsl = [0]
+    for ql in query_lens:
+        qsl.append(qsl[-1] + ql)
+    T = qsl[-1]
+    N = (nq + 2 * nkv) * d
+    qkv = torch.randn(T, N + 64, dtype=dt, device=gpu)[:, :N]     # padded row stride
+    pos, slots = [], []
+    btc = bt.cpu()
+    for i, (L, ql) in enumerate(zip(seq_lens, query_lens)):
+        for p in range(L - ql, L):
+            pos.append(p)
+            slots.append(int(btc[i, p // bs]) * bs + p % bs)
+    pos_t = torch.tensor(pos, dtype=torch.int64, device=gpu)
+    slot_t = torch.tensor(slots, dtype=torch.int64, device=gpu)
+    cs = ref.rope_cos_sin_cache(d, 1024, 500000.0).to(gpu)
+    qsl_t = torch.tensor(qsl, dtype=torch.int32, device=gpu)
+    sl_t = torch.tensor(seq_lens, dtype=torch.int32, device=gpu)
+    kc1, vc1, kc2, vc2 = kc.clone(), vc.clone(), kc.clone(), vc.clone()
+    q = ops.rope_kv_write(qkv, pos_t, cs, kc1, vc1, slot_t, nq, nkv, d)
+    out1 = ops.prefill_attention(q, kc1, vc1, bt, qsl_t, sl_t, d ** -0.5)
+    ops.kv_write_rope(qkv, pos_t, cs, kc2, vc2, slot_t, nq, nkv, d)
+    out2 = ops.prefill_attention_rope(qkv, cs, kc2, vc2, bt, qsl_t, sl_t, d ** -0.5, nq, d)
+    torch.cuda.synchronize()
+    assert torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
+    torch.testing.assert_close(out2.cpu().float(), out1.cpu().float(), atol=1e-6, rtol=0)
+    kr, vr = kc.cpu().clone(), vc.cpu().clone()
+    qr = ref.rope_qk_kv_write(qkv.cpu().contiguous(), pos_t.cpu(), cs.cpu(), kr, vr, slot_t.cpu(), nq, nkv, d,
+                              None, None, 1e-6, True, 1.0, 1.0)
+    exp = ref.prefill_attention(qr, kr, vr, bt.cpu(), qsl_t.cpu(), sl_t.cpu(), d ** -0.5)
+    torch.testing.assert_close(out2.cpu().float(), exp.float(), **_tol(dt))
+
+
 @pytest.mark.parametrize("gqa,nq,nkv,S", [("1", 32, 8, 8192), ("0", 32, 8, 8192),
                                          ("1", 32, 8, 2048), ("1", 64, 8, 2048),
                                          ("1", 16, 2, 2048), ("0", 64, 8, 2048)])
