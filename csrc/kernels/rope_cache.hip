@@ -146,6 +146,37 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
   const int iv = it - n_qk_pad;
   if (slot < 0 || iv >= nkv * (d >> 3)) return;
   const int h = iv / (d >> 3), c = iv % (d >> 3);
+  if constexpr (KVO && !KV8) {
+    // Prefill: an 8-key group of V^T that this step writes whole (its 8 tokens are rows
+    // t0 .. t0+7 with consecutive slots) is written by its first token's thread as eight
+    // 16-byte rows (the 8 x 8 block transposed in registers) instead of 64 two-byte
+    // stores spread over eight tokens; the other seven tokens skip it.
+    const int g = (int)(slot & 7);
+    const int t0 = t - g;
+    bool full = t0 >= 0 && t0 + 7 < (int)gridDim.x;
+    if (full) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) full = full && slot_mapping[t0 + k] == slot - g + k;
+    }
+    if (full) {
+      if (g != 0) return;
+      Pack8<T> vv[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        vv[k].u = qkv8<T, SL>(qkv, (int64_t)(t0 + k) * qkv_stride + (nq + nkv) * d + h * d,
+                              c * 8, S, slice_stride);
+      T* dst = reinterpret_cast<T*>(v_cache) + (blk * nkv + h) * (int64_t)bs * d +
+               ((int64_t)(off >> 3) * d + c * 8) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        Pack8<T> o;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o.h[k] = vv[k].h[j];
+        *reinterpret_cast<u32x4*>(dst + j * 8) = o.u;
+      }
+      return;
+    }
+  }
   Pack8<T> v;
   v.u = qkv8<T, SL>(qkv, row + (nq + nkv) * d + h * d, c * 8, S, slice_stride);
   const int64_t e = (blk * nkv + h) * (int64_t)bs * d + ((int64_t)(off >> 3) * d + c * 8) * 8 +
