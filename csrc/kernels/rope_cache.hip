@@ -146,7 +146,7 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
   const int iv = it - n_qk_pad;
   if (slot < 0 || iv >= nkv * (d >> 3)) return;
   const int h = iv / (d >> 3), c = iv % (d >> 3);
-  if constexpr (KVO && !KV8) {
+  if constexpr (!KV8) {
     // Prefill: an 8-key group of V^T that this step writes whole (its 8 tokens are rows
     // t0 .. t0+7 with consecutive slots) is written by its first token's thread as eight
     // 16-byte rows (the 8 x 8 block transposed in registers) instead of 64 two-byte

@@ -299,6 +299,9 @@ def test_prefill_rope_fused_equals_unfused(gpu, monkeypatch, dt, gqa, d, nq, nkv
                               None, None, 1e-6, True, 1.0, 1.0)
     exp = ref.prefill_attention(qr, kr, vr, bt.cpu(), qsl_t.cpu(), sl_t.cpu(), d ** -0.5)
     torch.testing.assert_close(out2.cpu().float(), exp.float(), **_tol(dt))
+    # V is a pure copy: the coalesced whole-group V^T stores and the per-token scatter
+    # (partial groups, chunk boundaries) must reproduce the reference cache exactly
+    assert torch.equal(vc1.cpu(), vr)
 
 
 @pytest.mark.parametrize("gqa,nq,nkv,S", [("1", 32, 8, 8192), ("0", 32, 8, 8192),
