@@ -213,14 +213,19 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
 
   V8 qf[2][KS];
   int qpos[2];
+  // q is loaded (and, with cos_sin, rotated) AFTER the first K/V tile's loads are issued:
+  // the rotation waits for q, and vmcnt retires in order, so q loaded first put its
+  // latency in series with the block-table -> K/V chain of every workgroup's first tile
+  auto load_q = [&]() {
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int qi = mb * PF_BM + wave * 32 + qt * 16 + r16;
-    const int qc = min(qi, qlen - 1);
-    qpos[qt] = ctx0 + qc;
-    pf_load_q<T, D>(q + (int64_t)(q0 + qc) * q_stride + (int64_t)hq * D, cos_sin, cs_rows,
-                    qpos[qt], qd, qf[qt]);
-  }
+    for (int qt = 0; qt < 2; ++qt) {
+      const int qi = mb * PF_BM + wave * 32 + qt * 16 + r16;
+      const int qc = min(qi, qlen - 1);
+      qpos[qt] = ctx0 + qc;
+      pf_load_q<T, D>(q + (int64_t)(q0 + qc) * q_stride + (int64_t)hq * D, cos_sin, cs_rows,
+                      qpos[qt], qd, qf[qt]);
+    }
+  };
   const int last_q = ctx0 + min((mb + 1) * PF_BM, qlen) - 1;
   const int n_tiles = last_q / PF_BN + 1;
 
@@ -285,6 +290,7 @@ __global__ __launch_bounds__(256, 2) void prefill_attn_kernel(
 
   fetch_bt(0);
   load_tile(0);
+  load_q();
   if (n_tiles > 1) fetch_bt(1);
   store_tile(0);
   __syncthreads();
@@ -381,14 +387,19 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_gqa_kernel(
 
   V8 qf[2][KS];
   int qpos[2];
+  // q is loaded (and, with cos_sin, rotated) AFTER the first K/V tile's loads are issued:
+  // the rotation waits for q, and vmcnt retires in order, so q loaded first put its
+  // latency in series with the block-table -> K/V chain of every workgroup's first tile
+  auto load_q = [&]() {
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int qi = wq0 + qt * 16 + r16;
-    const int qc = min(qi, qlen - 1);
-    qpos[qt] = ctx0 + qc;
-    pf_load_q<T, D>(q + (int64_t)(q0 + qc) * q_stride + (int64_t)hq * D, cos_sin, cs_rows,
-                    qpos[qt], qd, qf[qt]);
-  }
+    for (int qt = 0; qt < 2; ++qt) {
+      const int qi = wq0 + qt * 16 + r16;
+      const int qc = min(qi, qlen - 1);
+      qpos[qt] = ctx0 + qc;
+      pf_load_q<T, D>(q + (int64_t)(q0 + qc) * q_stride + (int64_t)hq * D, cos_sin, cs_rows,
+                      qpos[qt], qd, qf[qt]);
+    }
+  };
   const int last_q = ctx0 + min(qbase + QB, qlen) - 1;
   const int n_tiles = last_q / PF_BN + 1;
 
@@ -455,6 +466,7 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_gqa_kernel(
 
   fetch_bt(0);
   load_tile(0);
+  load_q();
   if (n_tiles > 1) fetch_bt(1);
   store_tile(0);
   __syncthreads();

@@ -13,6 +13,7 @@
 // quantised is the T-rounded one, exactly what a T cache would store.
 #include "common.h"
 #include "launch.h"
+#include <cstdlib>
 
 namespace kgc {
 
@@ -50,7 +51,7 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
     const float* __restrict__ cos_sin, T* __restrict__ q_out, void* __restrict__ k_cache,
     void* __restrict__ v_cache, const int64_t* __restrict__ slot_mapping,
     const T* __restrict__ qn_w, const T* __restrict__ kn_w, int nq, int nkv, int d, int bs,
-    float eps, float k_inv, float v_inv, int num_blocks) {
+    float eps, float k_inv, float v_inv, int num_blocks, int vgroup) {
   // item space of one token: [q/k rotation items, padded to a wave] [v scatter items];
   // gridDim.y workgroups of ROPE_NT items share a token (fills the CUs at decode).
   const int t = blockIdx.x;
@@ -146,7 +147,7 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
   const int iv = it - n_qk_pad;
   if (slot < 0 || iv >= nkv * (d >> 3)) return;
   const int h = iv / (d >> 3), c = iv % (d >> 3);
-  if constexpr (!KV8) {
+  if (!KV8 && vgroup) {
     // Prefill: an 8-key group of V^T that this step writes whole (its 8 tokens are rows
     // t0 .. t0+7 with consecutive slots) is written by its first token's thread as eight
     // 16-byte rows (the 8 x 8 block transposed in registers) instead of 64 two-byte
@@ -199,6 +200,12 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
   }
 }
 
+// KGC_ROPE_VGROUP=0: every V element through the per-token 2-byte scatter (A/B)
+static int rope_vgroup() {
+  const char* e = getenv("KGC_ROPE_VGROUP");
+  return e ? atoi(e) : 1;
+}
+
 template <typename T, bool KV8, bool SL>
 static void rope_dispatch(const void* qkv, int64_t qkv_stride, int S, int64_t ss,
                           const int64_t* pos,
@@ -213,7 +220,7 @@ static void rope_dispatch(const void* qkv, int64_t qkv_stride, int S, int64_t ss
 #define KGC_ROPE_LAUNCH(N, R, O)                                                            \
   rope_kv_kernel<T, N, R, KV8, SL, O><<<grid, ROPE_NT, 0, s>>>(                             \
       qkv, qkv_stride, S, ss, pos, cs, (T*)q_out, kc, vc, slots, (const T*)qn,               \
-      (const T*)kn, nq, nkv, d, bs, eps, k_inv, v_inv, num_blocks)
+      (const T*)kn, nq, nkv, d, bs, eps, k_inv, v_inv, num_blocks, rope_vgroup())
   const bool norm = qn != nullptr;
   if (kvo) {                    // prefill-only steps of RoPE models without q/k norm
     if (rope && !norm) KGC_ROPE_LAUNCH(false, true, true);
