@@ -200,10 +200,13 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
   }
 }
 
-// KGC_ROPE_VGROUP=0: every V element through the per-token 2-byte scatter (A/B)
+// KGC_ROPE_VGROUP=1: the whole-group V^T stores above.  Off by default: measured slower
+// at 16K-token prefill chunks (tools/prefill_rope_bench.py: rope_kv_write 152 -> 173 us,
+// k/v-only 85 -> 94 us; the eight-token leaders serialise what 8 threads did in parallel,
+// and the L2 already merges the 2-byte stores of one line)
 static int rope_vgroup() {
   const char* e = getenv("KGC_ROPE_VGROUP");
-  return e ? atoi(e) : 1;
+  return e ? atoi(e) : 0;
 }
 
 template <typename T, bool KV8, bool SL>
