@@ -98,6 +98,10 @@ __device__ __forceinline__ void neox_rot(float a, float b, float c, float s, flo
                                          float& ob) {
   oa = __builtin_fmaf(a, c, -(b * s));
   ob = __builtin_fmaf(b, c, a * s);
+  // the fp32 results exist as such: otherwise the f16 callers' fptrunc(fma) may become a
+  // v_fma_mix (one rounding instead of fp32-then-f16) for SOME elements, chosen by the
+  // scheduler per instantiation -- 1-ulp differences between kernels that must agree
+  asm("" : "+v"(oa), "+v"(ob));
 }
 
 // ---- fp8 (OCP e4m3, gfx950) KV cache ---------------------------------------------

@@ -18,6 +18,7 @@
 namespace kgc {
 
 constexpr int ROPE_NT = 128;
+constexpr int ROPE_HG = 8;       // heads per q/k item (shared cos / sin)
 
 // 8 consecutive elements of the QKV row: T storage, or the sum of S fp32 slices
 template <typename T, bool SL>
@@ -54,10 +55,16 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
     float eps, float k_inv, float v_inv, int num_blocks, int vgroup) {
   // item space of one token: [q/k rotation items, padded to a wave] [v scatter items];
   // gridDim.y workgroups of ROPE_NT items share a token (fills the CUs at decode).
+  // A q/k item is one chunk pair (c, c + d/2) of a group of ROPE_HG heads: the position's
+  // cos / sin are loaded once for all of them and the heads' loads are all in flight
+  // together (one item per head re-read the same 64 B of cos / sin per head, ~20 KB of
+  // L2 reads per token at 40 heads).
   const int t = blockIdx.x;
-  const int tph = d >> 4;               // threads per head (pairs of 8-elem chunks)
+  const int tph = d >> 4;               // threads per head group (pairs of 8-elem chunks)
   const int half = d >> 1;
-  const int n_qk = (KVO ? nkv : nq + nkv) * tph;
+  const int nheads = KVO ? nkv : nq + nkv;
+  const int h_off = KVO ? nq : 0;       // 0..nq-1 = q, nq.. = k
+  const int n_qk = (nheads + ROPE_HG - 1) / ROPE_HG * tph;
   const int n_qk_pad = (n_qk + 63) & ~63;
   const int it = blockIdx.y * ROPE_NT + threadIdx.x;
   int64_t slot = slot_mapping[t];
@@ -67,77 +74,92 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
   const int off = slot >= 0 ? (int)(slot % bs) : 0;
   if (it < n_qk_pad) {                  // whole waves take this branch together
     const bool active = it < n_qk;
-    const int head = (active ? it / tph : 0) + (KVO ? nq : 0);   // 0..nq-1 = q, nq.. = k
+    const int h0 = (active ? it / tph : 0) * ROPE_HG;
+    const int nh = min(ROPE_HG, nheads - h0);   // the same for the tph lanes of a group
     const int c = it % tph;                     // chunk index within the first half
-    Pack8<T> a, b;
-    a.u = qkv8<T, SL>(qkv, row + head * d, c * 8, S, slice_stride);
-    b.u = qkv8<T, SL>(qkv, row + head * d, half + c * 8, S, slice_stride);
-    float4 c0, c1, s0, s1;
+    Pack8<T> a[ROPE_HG], b[ROPE_HG];
+#pragma unroll
+    for (int k = 0; k < ROPE_HG; ++k) {         // tail heads re-load the group's last head
+      const int head = h_off + h0 + min(k, nh - 1);
+      a[k].u = qkv8<T, SL>(qkv, row + head * d, c * 8, S, slice_stride);
+      b[k].u = qkv8<T, SL>(qkv, row + head * d, half + c * 8, S, slice_stride);
+    }
+    float cc[8], sn[8];
     if (ROPE) {
       const float* cs = cos_sin + positions[t] * d;
-      c0 = *reinterpret_cast<const float4*>(cs + c * 8);
-      c1 = *reinterpret_cast<const float4*>(cs + c * 8 + 4);
-      s0 = *reinterpret_cast<const float4*>(cs + half + c * 8);
-      s1 = *reinterpret_cast<const float4*>(cs + half + c * 8 + 4);
+      const float4 c0 = *reinterpret_cast<const float4*>(cs + c * 8);
+      const float4 c1 = *reinterpret_cast<const float4*>(cs + c * 8 + 4);
+      const float4 s0 = *reinterpret_cast<const float4*>(cs + half + c * 8);
+      const float4 s1 = *reinterpret_cast<const float4*>(cs + half + c * 8 + 4);
+      cc[0] = c0.x; cc[1] = c0.y; cc[2] = c0.z; cc[3] = c0.w;
+      cc[4] = c1.x; cc[5] = c1.y; cc[6] = c1.z; cc[7] = c1.w;
+      sn[0] = s0.x; sn[1] = s0.y; sn[2] = s0.z; sn[3] = s0.w;
+      sn[4] = s1.x; sn[5] = s1.y; sn[6] = s1.z; sn[7] = s1.w;
     }
-    Pack8<T> wa, wb;
+    Pack8<T> qwa, qwb, kwa, kwb;
     if (NORM) {
-      const T* nw = head < nq ? qn_w : kn_w;
-      wa.u = *reinterpret_cast<const u32x4*>(nw + c * 8);
-      wb.u = *reinterpret_cast<const u32x4*>(nw + half + c * 8);
+      qwa.u = *reinterpret_cast<const u32x4*>(qn_w + c * 8);
+      qwb.u = *reinterpret_cast<const u32x4*>(qn_w + half + c * 8);
+      kwa.u = *reinterpret_cast<const u32x4*>(kn_w + c * 8);
+      kwb.u = *reinterpret_cast<const u32x4*>(kn_w + half + c * 8);
     }
-    float xa[8], xb[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { xa[j] = to_f(a.h[j]); xb[j] = to_f(b.h[j]); }
-    if (NORM) {
-      float ss = 0.f;
+    for (int k = 0; k < ROPE_HG; ++k) {
+      if (k >= nh) break;                       // uniform within the lane group
+      const int head = h_off + h0 + k;
+      float xa[8], xb[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) ss += xa[j] * xa[j] + xb[j] * xb[j];
-      for (int o = 1; o < tph; o <<= 1) ss += __shfl_xor(ss, o, 64);
-      const float inv = rsqrtf(ss / (float)d + eps);
+      for (int j = 0; j < 8; ++j) { xa[j] = to_f(a[k].h[j]); xb[j] = to_f(b[k].h[j]); }
+      if (NORM) {
+        const Pack8<T>& wa = head < nq ? qwa : kwa;
+        const Pack8<T>& wb = head < nq ? qwb : kwb;
+        float ss = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        // round through T like the unfused reference (norm output is stored in T)
-        xa[j] = to_f(from_f<T>(xa[j] * inv * to_f(wa.h[j])));
-        xb[j] = to_f(from_f<T>(xb[j] * inv * to_f(wb.h[j])));
+        for (int j = 0; j < 8; ++j) ss += xa[j] * xa[j] + xb[j] * xb[j];
+        for (int o = 1; o < tph; o <<= 1) ss += __shfl_xor(ss, o, 64);
+        const float inv = rsqrtf(ss / (float)d + eps);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          // round through T like the unfused reference (norm output is stored in T)
+          xa[j] = to_f(from_f<T>(xa[j] * inv * to_f(wa.h[j])));
+          xb[j] = to_f(from_f<T>(xb[j] * inv * to_f(wb.h[j])));
+        }
       }
-    }
-    if (!active) return;
-    Pack8<T> oa, ob;
-    if (ROPE) {
-      const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-      const float sn[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      if (!active) continue;
+      Pack8<T> oa, ob;
+      if (ROPE) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float ra, rb;
-        neox_rot(xa[j], xb[j], cc[j], sn[j], ra, rb);
-        oa.h[j] = from_f<T>(ra);
-        ob.h[j] = from_f<T>(rb);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { oa.h[j] = from_f<T>(xa[j]); ob.h[j] = from_f<T>(xb[j]); }
-    }
-    if (!KVO && head < nq) {
-      T* dst = q_out + ((int64_t)t * nq + head) * d;
-      *reinterpret_cast<u32x4*>(dst + c * 8) = oa.u;
-      *reinterpret_cast<u32x4*>(dst + half + c * 8) = ob.u;
-    } else if (slot >= 0) {
-      const int kh = head - nq;
-      const int64_t e = ((blk * nkv + kh) * bs + off) * d;
-      if constexpr (KV8) {
-        uint8_t* dst = reinterpret_cast<uint8_t*>(k_cache) + e;
-        float fa[8], fb[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { fa[j] = to_f(oa.h[j]) * k_inv; fb[j] = to_f(ob.h[j]) * k_inv; }
-        *reinterpret_cast<u32x2*>(dst + c * 8) =
-            u32x2{fp8x4(fa[0], fa[1], fa[2], fa[3]), fp8x4(fa[4], fa[5], fa[6], fa[7])};
-        *reinterpret_cast<u32x2*>(dst + half + c * 8) =
-            u32x2{fp8x4(fb[0], fb[1], fb[2], fb[3]), fp8x4(fb[4], fb[5], fb[6], fb[7])};
+        for (int j = 0; j < 8; ++j) {
+          float ra, rb;
+          neox_rot(xa[j], xb[j], cc[j], sn[j], ra, rb);
+          oa.h[j] = from_f<T>(ra);
+          ob.h[j] = from_f<T>(rb);
+        }
       } else {
-        T* dst = reinterpret_cast<T*>(k_cache) + e;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { oa.h[j] = from_f<T>(xa[j]); ob.h[j] = from_f<T>(xb[j]); }
+      }
+      if (!KVO && head < nq) {
+        T* dst = q_out + ((int64_t)t * nq + head) * d;
         *reinterpret_cast<u32x4*>(dst + c * 8) = oa.u;
         *reinterpret_cast<u32x4*>(dst + half + c * 8) = ob.u;
+      } else if (slot >= 0) {
+        const int kh = head - nq;
+        const int64_t e = ((blk * nkv + kh) * bs + off) * d;
+        if constexpr (KV8) {
+          uint8_t* dst = reinterpret_cast<uint8_t*>(k_cache) + e;
+          float fa[8], fb[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) { fa[j] = to_f(oa.h[j]) * k_inv; fb[j] = to_f(ob.h[j]) * k_inv; }
+          *reinterpret_cast<u32x2*>(dst + c * 8) =
+              u32x2{fp8x4(fa[0], fa[1], fa[2], fa[3]), fp8x4(fa[4], fa[5], fa[6], fa[7])};
+          *reinterpret_cast<u32x2*>(dst + half + c * 8) =
+              u32x2{fp8x4(fb[0], fb[1], fb[2], fb[3]), fp8x4(fb[4], fb[5], fb[6], fb[7])};
+        } else {
+          T* dst = reinterpret_cast<T*>(k_cache) + e;
+          *reinterpret_cast<u32x4*>(dst + c * 8) = oa.u;
+          *reinterpret_cast<u32x4*>(dst + half + c * 8) = ob.u;
+        }
       }
     }
     return;
@@ -218,7 +240,8 @@ static void rope_dispatch(const void* qkv, int64_t qkv_stride, int S, int64_t ss
                           float v_inv, int num_blocks, hipStream_t s) {
   if (T_ == 0) return;
   const bool kvo = q_out == nullptr;
-  const int n_items = ((((kvo ? 0 : nq) + nkv) * (d >> 4) + 63) & ~63) + nkv * (d >> 3);
+  const int n_items = (((((kvo ? 0 : nq) + nkv) + ROPE_HG - 1) / ROPE_HG * (d >> 4) + 63) & ~63) +
+                      nkv * (d >> 3);
   const dim3 grid(T_, (n_items + ROPE_NT - 1) / ROPE_NT);
 #define KGC_ROPE_LAUNCH(N, R, O)                                                            \
   rope_kv_kernel<T, N, R, KV8, SL, O><<<grid, ROPE_NT, 0, s>>>(                             \
