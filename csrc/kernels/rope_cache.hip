@@ -19,6 +19,9 @@ namespace kgc {
 
 constexpr int ROPE_NT = 128;
 constexpr int ROPE_HG = 8;       // heads per q/k item (shared cos / sin)
+// split-K slices (decode shapes): one head per item -- 8 heads x S slices of loads per
+// thread made the small-T launch latency bound (161.7 vs 137 us, rope + decode at B = 256)
+template <bool SL> constexpr int rope_hg() { return SL ? 1 : ROPE_HG; }
 
 // 8 consecutive elements of the QKV row: T storage, or the sum of S fp32 slices
 template <typename T, bool SL>
@@ -64,7 +67,8 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
   const int half = d >> 1;
   const int nheads = KVO ? nkv : nq + nkv;
   const int h_off = KVO ? nq : 0;       // 0..nq-1 = q, nq.. = k
-  const int n_qk = (nheads + ROPE_HG - 1) / ROPE_HG * tph;
+  constexpr int HG = rope_hg<SL>();
+  const int n_qk = (nheads + HG - 1) / HG * tph;
   const int n_qk_pad = (n_qk + 63) & ~63;
   const int it = blockIdx.y * ROPE_NT + threadIdx.x;
   int64_t slot = slot_mapping[t];
@@ -74,12 +78,12 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
   const int off = slot >= 0 ? (int)(slot % bs) : 0;
   if (it < n_qk_pad) {                  // whole waves take this branch together
     const bool active = it < n_qk;
-    const int h0 = (active ? it / tph : 0) * ROPE_HG;
-    const int nh = min(ROPE_HG, nheads - h0);   // the same for the tph lanes of a group
+    const int h0 = (active ? it / tph : 0) * HG;
+    const int nh = min(HG, nheads - h0);   // the same for the tph lanes of a group
     const int c = it % tph;                     // chunk index within the first half
-    Pack8<T> a[ROPE_HG], b[ROPE_HG];
+    Pack8<T> a[HG], b[HG];
 #pragma unroll
-    for (int k = 0; k < ROPE_HG; ++k) {         // tail heads re-load the group's last head
+    for (int k = 0; k < HG; ++k) {              // tail heads re-load the group's last head
       const int head = h_off + h0 + min(k, nh - 1);
       a[k].u = qkv8<T, SL>(qkv, row + head * d, c * 8, S, slice_stride);
       b[k].u = qkv8<T, SL>(qkv, row + head * d, half + c * 8, S, slice_stride);
@@ -104,7 +108,7 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
       kwb.u = *reinterpret_cast<const u32x4*>(kn_w + half + c * 8);
     }
 #pragma unroll
-    for (int k = 0; k < ROPE_HG; ++k) {
+    for (int k = 0; k < HG; ++k) {
       if (k >= nh) break;                       // uniform within the lane group
       const int head = h_off + h0 + k;
       float xa[8], xb[8];
@@ -240,7 +244,8 @@ static void rope_dispatch(const void* qkv, int64_t qkv_stride, int S, int64_t ss
                           float v_inv, int num_blocks, hipStream_t s) {
   if (T_ == 0) return;
   const bool kvo = q_out == nullptr;
-  const int n_items = (((((kvo ? 0 : nq) + nkv) + ROPE_HG - 1) / ROPE_HG * (d >> 4) + 63) & ~63) +
+  constexpr int HG = rope_hg<SL>();
+  const int n_items = (((((kvo ? 0 : nq) + nkv) + HG - 1) / HG * (d >> 4) + 63) & ~63) +
                       nkv * (d >> 3);
   const dim3 grid(T_, (n_items + ROPE_NT - 1) / ROPE_NT);
 #define KGC_ROPE_LAUNCH(N, R, O)                                                            \
