@@ -577,7 +577,10 @@ def _tune_silu(ws, x, M: int, N: int, K: int, reps: int, margin: float) -> None:
         if t < best_t:
             best_t, best_cfg = t, cfg
     n = len(ws)
-    if best_cfg is not None and best_t < sep_t * margin:
+    # both sides are our kernels timed the same way (graphed): the fused one wins when it
+    # is faster at all (the margin guards the custom-vs-library choices; here it kept a
+    # 42.4 vs 43.7 us / layer SK_SILU out at M = 1)
+    if best_cfg is not None and best_t < sep_t:
         _plan_silu[(M, N, K)] = best_cfg
     log.info("gemm M=%d N=%d K=%d silu: plan + silu_mul %.1f us, SK_SILU %s %.1f us -> %s",
              M, N, K, sep_t * 1e3 / n, best_cfg, best_t * 1e3 / n,
