@@ -178,7 +178,9 @@ void paged_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor b
   TORCH_CHECK(ctx_lens.scalar_type() == at::kInt && ctx_lens.numel() >= B, "ctx_lens int32 [B]");
   TORCH_CHECK(max_logits.scalar_type() == at::kFloat && exp_sums.scalar_type() == at::kFloat &&
               tmp_out.scalar_type() == at::kFloat, "partials fp32");
-  const int64_t Zmax = max_logits.size(-1);
+  // K1w (one wave per z-slice) packs the partial rows Z apart, so the workspace only has
+  // to hold B * nq * Z of them; the 4-wave kernel strides them by the last dim (Zmax)
+  const int64_t Zmax = kgc::paged_decode_waves_per_slice() == 1 ? Z : max_logits.size(-1);
   TORCH_CHECK(max_logits.is_contiguous() && exp_sums.is_contiguous() && tmp_out.is_contiguous() &&
               max_logits.numel() >= B * nq * Zmax && exp_sums.numel() >= B * nq * Zmax &&
               tmp_out.numel() >= B * nq * Zmax * d, "partials too small");
@@ -236,7 +238,9 @@ void paged_decode_rope(Tensor out, Tensor qkv, Tensor positions, Tensor cos_sin,
   TORCH_CHECK(ctx_lens.scalar_type() == at::kInt && ctx_lens.numel() >= B, "ctx_lens int32 [B]");
   TORCH_CHECK(max_logits.scalar_type() == at::kFloat && exp_sums.scalar_type() == at::kFloat &&
               tmp_out.scalar_type() == at::kFloat, "partials fp32");
-  const int64_t Zmax = max_logits.size(-1);
+  // K1w (one wave per z-slice) packs the partial rows Z apart, so the workspace only has
+  // to hold B * nq * Z of them; the 4-wave kernel strides them by the last dim (Zmax)
+  const int64_t Zmax = kgc::paged_decode_waves_per_slice() == 1 ? Z : max_logits.size(-1);
   TORCH_CHECK(max_logits.is_contiguous() && exp_sums.is_contiguous() && tmp_out.is_contiguous() &&
               max_logits.numel() >= B * nq * Zmax && exp_sums.numel() >= B * nq * Zmax &&
               tmp_out.numel() >= B * nq * Zmax * d, "partials too small");
@@ -575,9 +579,6 @@ void dgemm(Tensor C, Tensor X, Tensor W, int64_t cfg, int64_t epi) {
                 "C [M, N] (epi 1) or [M, N/2] (epi 2), contiguous, W's dtype");
   }
   TORCH_CHECK((M + bm - 1) / bm * (N / bn) * S < ((int64_t)1 << 31), "grid too large");
-  // the K9v configs cover all rows with one 256-row tile (no row-block loop)
-  TORCH_CHECK(!kgc::dgemm_cfg_single_row_block((int)cfg) || M <= bm,
-              "K9v configs take M <= 256");
   if (M == 0) return;
   kgc::launch_dgemm(dt_code(W), (int)cfg, (int)epi, C.data_ptr(), X.data_ptr(), W.data_ptr(),
                     (int)M, (int)N, (int)K, X.stride(0), (int)S, ss, stream());
@@ -606,7 +607,6 @@ std::vector<int64_t> dgemm_cfg_info(int64_t cfg) {
   return {bm, bn, packed};
 }
 int64_t dgemm_num_cfgs() { return kgc::dgemm_num_cfgs(); }
-bool dgemm_cfg_single_row_block(int64_t cfg) { return kgc::dgemm_cfg_single_row_block((int)cfg); }
 
 // profiling only: the packed 256 x 128 tile with its MFMAs / DMAs / one operand's DMAs removed
 void dgemm_ablate(Tensor C, Tensor X, Tensor W, int64_t mode) {
@@ -622,69 +622,6 @@ void dgemm_ablate(Tensor C, Tensor X, Tensor W, int64_t mode) {
   kgc::launch_dgemm_ablate((int)mode, C.data_ptr<float>(), X.data_ptr(), W.data_ptr(), (int)M,
                            (int)N, (int)K, X.stride(0), (int)C.size(0), C.stride(0), stream());
 }
-
-// K9r full-K ring decode GEMM.  Wp: [N/G, K/64, G*64] from ring_pack (G-row groups).
-void ring_gemm(Tensor C, Tensor X, Tensor Wp, int64_t cfg, int64_t epi) {
-  check_gpu(X, "X");
-  c10::hip::HIPGuardMasqueradingAsCUDA g(X.device());
-  TORCH_CHECK(cfg >= 0 && cfg < kgc::ring_num_cfgs(), "unknown ring tile config");
-  int bm, bn, threads, slots;
-  kgc::ring_cfg_info((int)cfg, &bm, &bn, &threads, &slots);
-  TORCH_CHECK(epi >= 0 && epi <= 2, "epi 0 (fp32 slices), 1 (out), 2 (silu pairs)");
-  TORCH_CHECK(Wp.scalar_type() == at::kBFloat16 && X.scalar_type() == at::kBFloat16, "bf16");
-  TORCH_CHECK(Wp.dim() == 3 && Wp.is_contiguous() && Wp.size(2) % 512 == 0,
-              "packed W [N/G, K/64, G*64] contiguous");
-  const int64_t G = Wp.size(2) / 64, N = Wp.size(0) * G, K = Wp.size(1) * 64;
-  TORCH_CHECK(G == bn, "W must be packed with G = the config's BN (ring_pack)");
-  TORCH_CHECK(X.dim() == 2 && X.size(1) == K && X.stride(1) == 1 && X.stride(0) % 8 == 0 &&
-              reinterpret_cast<uintptr_t>(X.data_ptr()) % 16 == 0,
-              "X [M, K] bf16, 16-B aligned rows");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(Wp.data_ptr()) % 16 == 0, "W 16-B aligned");
-  TORCH_CHECK(X.device() == Wp.device() && C.device() == X.device(), "same device");
-  const int64_t M = X.size(0);
-  TORCH_CHECK(N % bn == 0 && K >= 64, "N % BN == 0");
-  TORCH_CHECK(M <= (int64_t)1 << 20 && N < ((int64_t)1 << 31) / 4, "size limits");
-  int64_t S = 1, ss = 0;
-  if (epi == 0) {
-    TORCH_CHECK(C.scalar_type() == at::kFloat && C.dim() == 3 && C.is_contiguous() &&
-                C.size(1) == M && C.size(2) == N, "C fp32 contiguous [S, M, N]");
-    S = C.size(0);
-    ss = C.stride(0);
-    TORCH_CHECK(S >= 1 && S <= 8 && S <= K / 64, "1 <= S <= min(8, K / 64)");
-  } else {
-    TORCH_CHECK(C.scalar_type() == at::kBFloat16 && C.dim() == 2 && C.is_contiguous() &&
-                C.size(0) == M && C.size(1) == (epi == 2 ? N / 2 : N),
-                "C [M, N] (epi 1) or [M, N/2] (epi 2), contiguous bf16");
-  }
-  TORCH_CHECK((M + bm - 1) / bm * (N / bn) * S < ((int64_t)1 << 31), "grid too large");
-  if (M == 0) return;
-  kgc::launch_ring_gemm((int)cfg, (int)epi, C.data_ptr(), X.data_ptr(), Wp.data_ptr(), (int)M,
-                        (int)N, (int)K, X.stride(0), (int)S, ss, stream());
-}
-
-// P [N/G, K/64, G*64] <- W [N, K] (silu: merged [gate; up], 8-row gate / up interleave)
-void ring_pack(Tensor P, Tensor W, bool silu) {
-  check_gpu(W, "W");
-  c10::hip::HIPGuardMasqueradingAsCUDA g(W.device());
-  TORCH_CHECK(W.dim() == 2 && W.is_contiguous() && W.scalar_type() == at::kBFloat16,
-              "W [N, K] contiguous bf16");
-  TORCH_CHECK(P.scalar_type() == at::kBFloat16 && P.dim() == 3 && P.is_contiguous() &&
-              P.size(2) % 512 == 0, "P [N/G, K/64, G*64] contiguous bf16");
-  const int64_t N = W.size(0), K = W.size(1), G = P.size(2) / 64;
-  TORCH_CHECK(K % 64 == 0 && N % G == 0 && P.size(0) == N / G && P.size(1) == K / 64,
-              "P shape [N/G, K/64, G*64] for W [N, K]");
-  TORCH_CHECK(!silu || N % 32 == 0, "silu: N % 32 == 0");
-  TORCH_CHECK(P.device() == W.device(), "same device");
-  kgc::launch_ring_pack(silu, P.data_ptr(), W.data_ptr(), (int)N, (int)K, (int)G, stream());
-}
-
-std::vector<int64_t> ring_cfg_info(int64_t cfg) {
-  TORCH_CHECK(cfg >= 0 && cfg < kgc::ring_num_cfgs(), "unknown ring tile config");
-  int bm, bn, threads, slots;
-  kgc::ring_cfg_info((int)cfg, &bm, &bn, &threads, &slots);
-  return {bm, bn, threads, slots};
-}
-int64_t ring_num_cfgs() { return kgc::ring_num_cfgs(); }
 
 void splitk_reduce(Tensor out, Tensor Cs) {
   check_gpu(Cs, "Cs");
@@ -936,7 +873,7 @@ int64_t wall_clock_rate_khz_op() { return kgc::wall_clock_rate_khz(); }
 
 void xgmi_allreduce_rms(Tensor out, Tensor in, Tensor residual, Tensor w, double eps,
                         std::vector<int64_t> data, std::vector<int64_t> sig, int64_t rank,
-                        int64_t cap_bytes) {
+                        int64_t cap_bytes, bool two_shot) {
   check_gpu(in, "in");
   check_same_dev(in, out, "out");
   check_same_dev(in, residual, "residual");
@@ -962,7 +899,55 @@ void xgmi_allreduce_rms(Tensor out, Tensor in, Tensor residual, Tensor w, double
   }
   kgc::launch_allreduce_rms(dt_code(in), P, (int)nr, (int)rank, in.data_ptr(), out.data_ptr(),
                             residual.data_ptr(), w.data_ptr(), (int)M, (int)H, (float)eps,
-                            cap_bytes / 16, stream());
+                            cap_bytes / 16, two_shot, stream());
+}
+
+// World emulation of the xGMI all-reduce kernels (tests): every rank's blocks in one launch
+// on this device.  data / sig: each rank's region for `kind` and its signal block (plain
+// device memory is enough: one device); a / b / c: per-rank operands (see launch.h).
+void xgmi_allreduce_emu(int64_t kind, std::vector<Tensor> a, std::vector<Tensor> b,
+                        std::vector<Tensor> c, std::optional<Tensor> w, std::vector<int64_t> data,
+                        std::vector<int64_t> sig, int64_t cap_bytes, double eps) {
+  const int64_t nr = (int64_t)data.size();
+  TORCH_CHECK(nr == 2 || nr == 4 || nr == 8, "emulation: 2, 4 or 8 ranks");
+  TORCH_CHECK((int64_t)sig.size() == nr && (int64_t)a.size() == nr, "one buffer per rank");
+  TORCH_CHECK(kind >= 0 && kind <= 3, "kind 0..3");
+  const Tensor& x0 = a[0];
+  check_gpu(x0, "a[0]");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x0.device());
+  TORCH_CHECK(x0.scalar_type() == at::kBFloat16 || x0.scalar_type() == at::kHalf, "bf16 / fp16");
+  const int64_t bytes = x0.numel() * x0.element_size();
+  TORCH_CHECK(bytes <= cap_bytes && bytes % (16 * nr) == 0, "message size");
+  kgc::ArPtrs P{};
+  kgc::ArWorld W{};
+  int M = 0, H = 0;
+  const void* wp = nullptr;
+  if (kind >= 2) {
+    TORCH_CHECK(x0.dim() == 2 && (int64_t)b.size() == nr && (int64_t)c.size() == nr &&
+                w.has_value(), "fused: a (in), b (out), c (residual) [M, H] per rank, w [H]");
+    M = (int)x0.size(0);
+    H = (int)x0.size(1);
+    TORCH_CHECK(H % 8 == 0 && H <= kgc::allreduce_rms_max_hidden() && w->numel() == H &&
+                w->scalar_type() == x0.scalar_type() && w->is_contiguous(), "hidden / w");
+    wp = w->data_ptr();
+  }
+  for (int64_t r = 0; r < nr; ++r) {
+    P.data[r] = (void*)(intptr_t)data[r];
+    P.sig[r] = (void*)(intptr_t)sig[r];
+    TORCH_CHECK(a[r].is_contiguous() && a[r].sizes() == x0.sizes() &&
+                a[r].scalar_type() == x0.scalar_type() && a[r].device() == x0.device(), "a[r]");
+    W.a[r] = a[r].data_ptr();
+    if (kind >= 2) {
+      TORCH_CHECK(b[r].is_contiguous() && b[r].sizes() == x0.sizes() &&
+                  c[r].is_contiguous() && c[r].sizes() == x0.sizes() &&
+                  b[r].scalar_type() == x0.scalar_type() && c[r].scalar_type() == x0.scalar_type(),
+                  "b[r] / c[r]");
+      W.b[r] = b[r].data_ptr();
+      W.c[r] = c[r].data_ptr();
+    }
+  }
+  kgc::launch_allreduce_emu(dt_code(x0), (int)kind, P, W, (int)nr, bytes / 16, wp, M, H,
+                            (float)eps, cap_bytes / 16, stream());
 }
 
 void skinny_gemm(Tensor C, Tensor X, Tensor W, std::optional<Tensor> bias, int64_t mt,
@@ -1046,6 +1031,7 @@ std::vector<int64_t> sample_stamps() {
 }
 
 int64_t decode_partition_size() { return kgc::paged_decode_partition_size(); }
+int64_t decode_waves_per_slice() { return kgc::paged_decode_waves_per_slice(); }
 int64_t prefill_block_m() { return kgc::prefill_block_m(); }
 
 }  // namespace
@@ -1079,6 +1065,7 @@ TORCH_LIBRARY(kgc, m) {
         "int vocab_off) -> ()");
   m.def("sample_vp_unpack(Tensor(a!) out, Tensor packed) -> ()");
   m.def("decode_partition_size() -> int", &decode_partition_size);
+  m.def("decode_waves_per_slice() -> int", &decode_waves_per_slice);
   m.def("moe_route(Tensor(a!) topk_w, Tensor(b!) topk_ids, Tensor logits, bool renorm) -> ()");
   m.def("moe_align(Tensor(a!) sorted_ids, Tensor(b!) block_expert, Tensor(c!) meta, "
         "Tensor topk_ids, int e0, int E_local, int bm) -> ()");
@@ -1090,13 +1077,8 @@ TORCH_LIBRARY(kgc, m) {
   m.def("dgemm(Tensor(a!) C, Tensor X, Tensor W, int cfg, int epi) -> ()");
   m.def("dgemm_cfg_info(int cfg) -> int[]", &dgemm_cfg_info);
   m.def("dgemm_num_cfgs() -> int", &dgemm_num_cfgs);
-  m.def("dgemm_cfg_single_row_block(int cfg) -> bool", &dgemm_cfg_single_row_block);
   m.def("dgemm_ablate(Tensor(a!) C, Tensor X, Tensor W, int mode) -> ()");
   m.def("dgemm_pack(Tensor(a!) P, Tensor W, bool silu) -> ()");
-  m.def("ring_gemm(Tensor(a!) C, Tensor X, Tensor Wp, int cfg, int epi) -> ()");
-  m.def("ring_pack(Tensor(a!) P, Tensor W, bool silu) -> ()");
-  m.def("ring_cfg_info(int cfg) -> int[]", &ring_cfg_info);
-  m.def("ring_num_cfgs() -> int", &ring_num_cfgs);
   m.def("splitk_reduce_silu(Tensor(a!) out, Tensor Cs) -> ()");
   m.def("splitk_add_rms_norm(Tensor(a!) out, Tensor Cs, Tensor(b!) residual, Tensor w, float eps) -> ()");
   m.def("ar_signal_bytes() -> int", &ar_signal_bytes);
@@ -1110,7 +1092,9 @@ TORCH_LIBRARY(kgc, m) {
   m.def("xgmi_allreduce(Tensor(a!) inout, int[] data, int[] sig, int rank, int cap_bytes, "
         "bool two_shot) -> ()");
   m.def("xgmi_allreduce_rms(Tensor(a!) out, Tensor inp, Tensor(b!) residual, Tensor w, float eps, "
-        "int[] data, int[] sig, int rank, int cap_bytes) -> ()");
+        "int[] data, int[] sig, int rank, int cap_bytes, bool two_shot=False) -> ()");
+  m.def("xgmi_allreduce_emu(int kind, Tensor(a!)[] a, Tensor(b!)[] b, Tensor(c!)[] c, Tensor? w, "
+        "int[] data, int[] sig, int cap_bytes, float eps) -> ()");
   m.def("allreduce_rms_max_hidden() -> int", &allreduce_rms_max_hidden_op);
   m.def("allreduce_max_blocks() -> int", &allreduce_max_blocks_op);
   m.def("peer_spin_ms() -> int", &peer_spin_ms_op);
@@ -1160,6 +1144,7 @@ TORCH_LIBRARY_IMPL(kgc, CUDA, m) {
   m.impl("sample_vp_unpack", &sample_vp_unpack);
   m.impl("xgmi_allreduce", &xgmi_allreduce);
   m.impl("xgmi_allreduce_rms", &xgmi_allreduce_rms);
+  m.impl("xgmi_allreduce_emu", &xgmi_allreduce_emu);
   m.impl("ep_dispatch", &ep_dispatch);
   m.impl("pp_send", &pp_send);
   m.impl("pp_recv", &pp_recv);
@@ -1174,8 +1159,6 @@ TORCH_LIBRARY_IMPL(kgc, CUDA, m) {
   m.impl("dgemm", &dgemm);
   m.impl("dgemm_ablate", &dgemm_ablate);
   m.impl("dgemm_pack", &dgemm_pack);
-  m.impl("ring_gemm", &ring_gemm);
-  m.impl("ring_pack", &ring_pack);
   m.impl("splitk_reduce", &splitk_reduce);
   m.impl("splitk_reduce_silu", &splitk_reduce_silu);
   m.impl("splitk_add_rms_norm", &splitk_add_rms_norm);

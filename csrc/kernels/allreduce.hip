@@ -32,7 +32,8 @@
 namespace kgc {
 
 constexpr int AR_MAX_RANKS = 8;
-constexpr int AR_MAX_BLOCKS = 64;
+constexpr int AR_MAX_BLOCKS = 64;    // one-shot / two-shot / one-shot fused grid
+constexpr int AR2_BLOCKS = 256;      // row-segmented two-shot fused grid (one row per block)
 constexpr int AR_THREADS = 512;
 
 struct ArSignal {
@@ -40,6 +41,9 @@ struct ArSignal {
   uint32_t flag[2][AR_MAX_BLOCKS][AR_MAX_RANKS];       // written by peers
   uint32_t err;
   uint32_t pad[63];
+  // the row-segmented two-shot fused kernel's own epochs and flags (its grid differs)
+  uint32_t counter2[AR2_BLOCKS];
+  uint32_t flag2[2][AR2_BLOCKS][AR_MAX_RANKS];
 };
 
 size_t allreduce_signal_bytes() { return (sizeof(ArSignal) + 4095) & ~size_t(4095); }
@@ -51,9 +55,25 @@ __device__ __forceinline__ uint32_t ar_load_flag(uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Publish this block's writes to every peer, then wait for every peer's block.
-template <int NR>
-__device__ __forceinline__ void ar_barrier(const ArPtrs& P, int rank, int phase,
+// Flag set of one grid geometry: the plain / one-shot fused kernels (AR_MAX_BLOCKS) or the
+// row-segmented fused kernel (AR2_BLOCKS) -- counter[blk] and flag[phase][blk][rank].
+template <bool TWO_FUSED>
+__device__ __forceinline__ uint32_t* ar_counter(ArSignal* s, int blk) {
+  if constexpr (TWO_FUSED) return &s->counter2[blk];
+  else return &s->counter[blk];
+}
+template <bool TWO_FUSED>
+__device__ __forceinline__ uint32_t* ar_flag(ArSignal* s, int phase, int blk, int r) {
+  if constexpr (TWO_FUSED) return &s->flag2[phase][blk][r];
+  else return &s->flag[phase][blk][r];
+}
+
+// Publish this block's writes to every peer, then wait for block `blk` of every peer.
+// `blk` is the block's index within ITS RANK's grid: blockIdx.x on a real rank, the
+// position inside the rank's slice of the grid in world emulation (all ranks' blocks in
+// one launch on one device, see launch_allreduce_emu).
+template <int NR, bool TWO_FUSED = false>
+__device__ __forceinline__ void ar_barrier(const ArPtrs& P, int rank, int blk, int phase,
                                            uint32_t epoch) {
   // every wave drains its own stores first (vmcnt is per wave; do not rely on the
   // barrier's implicit wait), then one lane per peer releases at system scope
@@ -63,9 +83,9 @@ __device__ __forceinline__ void ar_barrier(const ArPtrs& P, int rank, int phase,
     __threadfence_system();   // release: copy-in / reduced data visible system-wide
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     ArSignal* peer = reinterpret_cast<ArSignal*>(P.sig[threadIdx.x]);
-    ar_store_flag(&peer->flag[phase][blockIdx.x][rank], epoch);
+    ar_store_flag(ar_flag<TWO_FUSED>(peer, phase, blk, rank), epoch);
     ArSignal* self = reinterpret_cast<ArSignal*>(P.sig[rank]);
-    uint32_t* f = &self->flag[phase][blockIdx.x][threadIdx.x];
+    uint32_t* f = ar_flag<TWO_FUSED>(self, phase, blk, threadIdx.x);
     const unsigned long long dl = spin_deadline(KGC_PEER_SPIN_MS);
     // a group that already failed (sticky err) does not wait again: one time-out per
     // dead peer, not one per collective (graph warm-ups run dozens back to back)
@@ -92,22 +112,29 @@ __device__ __forceinline__ u32x4 ld_peer(const void* p) {
   return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
 }
 
-template <typename T, int NR, bool TWO>
-__global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArPtrs P, int rank, T* inout,
-                                                               int64_t nvec, int64_t cap_vec) {
-  ArSignal* self = reinterpret_cast<ArSignal*>(P.sig[rank]);
+// this rank's next epoch for block blk (read by thread 0, shared through LDS)
+template <bool TWO_FUSED>
+__device__ __forceinline__ uint32_t ar_epoch(const ArPtrs& P, int rank, int blk) {
   __shared__ uint32_t s_epoch;
-  if (threadIdx.x == 0) s_epoch = self->counter[blockIdx.x] + 1;
+  if (threadIdx.x == 0)
+    s_epoch = *ar_counter<TWO_FUSED>(reinterpret_cast<ArSignal*>(P.sig[rank]), blk) + 1;
   __syncthreads();
-  const uint32_t epoch = s_epoch;
+  return s_epoch;
+}
+
+// ---- plain all-reduce body: block `blk` of rank `rank` (NB blocks per rank)
+template <typename T, int NR, bool TWO>
+__device__ __forceinline__ void allreduce_body(const ArPtrs& P, int rank, int blk, T* inout,
+                                               int64_t nvec, int64_t cap_vec) {
+  const uint32_t epoch = ar_epoch<false>(P, rank, blk);
   const int64_t par_off = (int64_t)(epoch & 1) * cap_vec;
   u32x4* io = reinterpret_cast<u32x4*>(inout);
   u32x4* mine = reinterpret_cast<u32x4*>(P.data[rank]) + par_off;
-  const int64_t stride = (int64_t)gridDim.x * AR_THREADS;
-  const int64_t first = (int64_t)blockIdx.x * AR_THREADS + threadIdx.x;
+  const int64_t stride = (int64_t)AR_MAX_BLOCKS * AR_THREADS;
+  const int64_t first = (int64_t)blk * AR_THREADS + threadIdx.x;
 
   for (int64_t v = first; v < nvec; v += stride) mine[v] = io[v];
-  ar_barrier<NR>(P, rank, 0, epoch);
+  ar_barrier<NR>(P, rank, blk, 0, epoch);
 
   auto reduce_at = [&](int64_t v) {
     float acc[8];
@@ -139,13 +166,35 @@ __global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArPtrs P, int ran
     const int64_t lo = (int64_t)rank * seg, hi = lo + seg;
     for (int64_t v = first; v < nvec; v += stride)
       if (v >= lo && v < hi) mine[v] = reduce_at(v);
-    ar_barrier<NR>(P, rank, 1, epoch);
+    ar_barrier<NR>(P, rank, blk, 1, epoch);
     for (int64_t v = first; v < nvec; v += stride) {
       const int r = (int)(v / seg);   // owner of the reduced segment holding v
       io[v] = ld_peer(reinterpret_cast<const u32x4*>(P.data[r]) + par_off + v);
     }
   }
-  if (threadIdx.x == 0) self->counter[blockIdx.x] = epoch;
+  __syncthreads();
+  if (threadIdx.x == 0) *ar_counter<false>(reinterpret_cast<ArSignal*>(P.sig[rank]), blk) = epoch;
+}
+
+template <typename T, int NR, bool TWO>
+__global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArPtrs P, int rank, T* inout,
+                                                               int64_t nvec, int64_t cap_vec) {
+  allreduce_body<T, NR, TWO>(P, rank, blockIdx.x, inout, nvec, cap_vec);
+}
+
+// World emulation: every rank's blocks in ONE grid on one device, each rank with its own
+// signal / data buffers and its own input -- the 8-rank barrier, parity and segment logic
+// run exactly as on 8 GPUs.  The grid is block-major (blockIdx = blk * NR + rank): the NR
+// blocks that wait for each other are adjacent in dispatch order, so with blocks
+// dispatched in order (as observed) the oldest unfinished group is always resident and
+// the grid never deadlocks whatever its size -- which eight processes sharing one GPU
+// cannot promise (their kernels need not be co-resident at all).  A violation would show
+// as the bounded spin's error word, never a hang.
+template <typename T, int NR, bool TWO>
+__global__ __launch_bounds__(AR_THREADS) void allreduce_emu_kernel(ArPtrs P, ArWorld W,
+                                                                   int64_t nvec, int64_t cap_vec) {
+  const int rank = blockIdx.x % NR, blk = blockIdx.x / NR;
+  allreduce_body<T, NR, TWO>(P, rank, blk, reinterpret_cast<T*>(W.a[rank]), nvec, cap_vec);
 }
 
 // ---- fused one-shot all-reduce + residual add + RMSNorm (row-parallel o / down
@@ -160,25 +209,77 @@ __global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArPtrs P, int ran
 // reads memory this one overwrites.
 constexpr int ARN_MAXV = 4;   // 512 threads x 4 x 8 = 16384 = widest hidden supported
 
+// residual += h (rounded), out = rms_norm(residual) * w for one row whose all-reduced
+// values h (already rounded to T) are in hv[]; every rank computes identical bytes
+template <typename T>
+__device__ __forceinline__ void ar_add_norm_row(Pack8<T>* hv, const Pack8<T>* wv, T* residual,
+                                                T* out, int64_t row, int nv, int H, float eps,
+                                                float* scratch) {
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < ARN_MAXV; ++i) {
+    const int v = threadIdx.x + i * AR_THREADS;
+    if (v >= nv) continue;
+    const int64_t e = row * nv + v;
+    Pack8<T> res;
+    res.u = reinterpret_cast<const u32x4*>(residual)[e];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      hv[i].h[j] = from_f<T>(to_f<T>(hv[i].h[j]) + to_f<T>(res.h[j]));   // residual += h
+      const float f = to_f<T>(hv[i].h[j]);
+      ss += f * f;
+    }
+    reinterpret_cast<u32x4*>(residual)[e] = hv[i].u;
+  }
+  ss = block_sum<AR_THREADS>(ss, scratch);
+  const float inv = rsqrtf(ss / (float)H + eps);
+#pragma unroll
+  for (int i = 0; i < ARN_MAXV; ++i) {
+    const int v = threadIdx.x + i * AR_THREADS;
+    if (v >= nv) continue;
+    Pack8<T> o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      o.h[j] = from_f<T>(to_f<T>(hv[i].h[j]) * inv * to_f<T>(wv[i].h[j]));
+    reinterpret_cast<u32x4*>(out)[row * nv + v] = o.u;
+  }
+}
+
+// sum of the NR ranks' copies of 16-B vector e, rounded to T (the all-reduce's output)
 template <typename T, int NR>
-__global__ __launch_bounds__(AR_THREADS) void allreduce_rms_kernel(
-    ArPtrs P, int rank, const T* __restrict__ in, T* __restrict__ out, T* __restrict__ residual,
-    const T* __restrict__ w, int M, int H, float eps, int64_t cap_vec) {
+__device__ __forceinline__ u32x4 ar_sum_vec(const ArPtrs& P, int64_t par_off, int64_t e) {
+  Pack8<T> pk[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    pk[r].u = ld_peer(reinterpret_cast<const u32x4*>(P.data[r]) + par_off + e);
+  Pack8<T> o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float acc = 0.f;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) acc += to_f<T>(pk[r].h[j]);
+    o.h[j] = from_f<T>(acc);
+  }
+  return o.u;
+}
+
+template <typename T, int NR>
+__device__ __forceinline__ void allreduce_rms_body(const ArPtrs& P, int rank, int blk,
+                                                   const T* __restrict__ in, T* __restrict__ out,
+                                                   T* __restrict__ residual,
+                                                   const T* __restrict__ w, int M, int H,
+                                                   float eps, int64_t cap_vec) {
   __shared__ float scratch[AR_THREADS / 64];
-  ArSignal* self = reinterpret_cast<ArSignal*>(P.sig[rank]);
-  __shared__ uint32_t s_epoch;
-  if (threadIdx.x == 0) s_epoch = self->counter[blockIdx.x] + 1;
-  __syncthreads();
-  const uint32_t epoch = s_epoch;
+  const uint32_t epoch = ar_epoch<false>(P, rank, blk);
   const int64_t par_off = (int64_t)(epoch & 1) * cap_vec;
   const int nv = H >> 3;                             // 16-byte vectors per row
   const u32x4* src = reinterpret_cast<const u32x4*>(in);
   u32x4* mine = reinterpret_cast<u32x4*>(P.data[rank]) + par_off;
 
-  for (int row = blockIdx.x; row < M; row += AR_MAX_BLOCKS)
+  for (int row = blk; row < M; row += AR_MAX_BLOCKS)
     for (int v = threadIdx.x; v < nv; v += AR_THREADS)
       mine[(int64_t)row * nv + v] = src[(int64_t)row * nv + v];
-  ar_barrier<NR>(P, rank, 0, epoch);
+  ar_barrier<NR>(P, rank, blk, 0, epoch);
 
   Pack8<T> wv[ARN_MAXV];
 #pragma unroll
@@ -186,61 +287,131 @@ __global__ __launch_bounds__(AR_THREADS) void allreduce_rms_kernel(
     const int v = threadIdx.x + i * AR_THREADS;
     if (v < nv) wv[i].u = reinterpret_cast<const u32x4*>(w)[v];
   }
-  for (int row = blockIdx.x; row < M; row += AR_MAX_BLOCKS) {   // uniform per block
+  for (int row = blk; row < M; row += AR_MAX_BLOCKS) {   // uniform per block
     Pack8<T> h[ARN_MAXV];
-    float ss = 0.f;
 #pragma unroll
     for (int i = 0; i < ARN_MAXV; ++i) {
       const int v = threadIdx.x + i * AR_THREADS;
-      if (v >= nv) continue;
-      const int64_t e = (int64_t)row * nv + v;
-      Pack8<T> pk[NR];
-#pragma unroll
-      for (int r = 0; r < NR; ++r)
-        pk[r].u = ld_peer(reinterpret_cast<const u32x4*>(P.data[r]) + par_off + e);
-      Pack8<T> res;
-      res.u = reinterpret_cast<const u32x4*>(residual)[e];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float acc = 0.f;
-#pragma unroll
-        for (int r = 0; r < NR; ++r) acc += to_f<T>(pk[r].h[j]);
-        const float sum = to_f<T>(from_f<T>(acc));             // the all-reduce output
-        h[i].h[j] = from_f<T>(sum + to_f<T>(res.h[j]));          // residual += h
-        const float f = to_f<T>(h[i].h[j]);
-        ss += f * f;
-      }
-      reinterpret_cast<u32x4*>(residual)[e] = h[i].u;
+      if (v < nv) h[i].u = ar_sum_vec<T, NR>(P, par_off, (int64_t)row * nv + v);
     }
-    ss = block_sum<AR_THREADS>(ss, scratch);
-    const float inv = rsqrtf(ss / (float)H + eps);
-#pragma unroll
-    for (int i = 0; i < ARN_MAXV; ++i) {
-      const int v = threadIdx.x + i * AR_THREADS;
-      if (v >= nv) continue;
-      Pack8<T> o;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o.h[j] = from_f<T>(to_f<T>(h[i].h[j]) * inv * to_f<T>(wv[i].h[j]));
-      reinterpret_cast<u32x4*>(out)[(int64_t)row * nv + v] = o.u;
+    ar_add_norm_row<T>(h, wv, residual, out, row, nv, H, eps, scratch);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *ar_counter<false>(reinterpret_cast<ArSignal*>(P.sig[rank]), blk) = epoch;
+}
+
+template <typename T, int NR>
+__global__ __launch_bounds__(AR_THREADS) void allreduce_rms_kernel(
+    ArPtrs P, int rank, const T* __restrict__ in, T* __restrict__ out, T* __restrict__ residual,
+    const T* __restrict__ w, int M, int H, float eps, int64_t cap_vec) {
+  allreduce_rms_body<T, NR>(P, rank, blockIdx.x, in, out, residual, w, M, H, eps, cap_vec);
+}
+
+template <typename T, int NR>
+__global__ __launch_bounds__(AR_THREADS) void allreduce_rms_emu_kernel(
+    ArPtrs P, ArWorld W, const T* __restrict__ w, int M, int H, float eps, int64_t cap_vec) {
+  const int rank = blockIdx.x % NR, blk = blockIdx.x / NR;
+  allreduce_rms_body<T, NR>(P, rank, blk, reinterpret_cast<const T*>(W.a[rank]),
+                            reinterpret_cast<T*>(W.b[rank]), reinterpret_cast<T*>(W.c[rank]), w,
+                            M, H, eps, cap_vec);
+}
+
+// ---- row-segmented TWO-SHOT fused all-reduce + residual add + RMSNorm (TP = 4 / 8
+// decode at real batch sizes: 256 rows x 8192 = 4 MB per call, 16x the one-shot cap).
+//   copy-in:  block b writes its rows {row % AR2_BLOCKS == b} into the own IPC buffer;
+//   reduce:   rank r owns the rows with row % NR == r; block b sums ITS owned rows over
+//             all peers (rounded to T: the all-reduce output) in place; barrier;
+//   gather:   block b reads each of its rows from the row's owner -- whole rows, so the
+//             residual add and the RMSNorm run right there: the reduced rows are read
+//             2 (NR-1)/NR x bytes per rank like the plain two-shot, and no second kernel
+//             re-reads them for the norm.
+// Every phase maps row -> block the same way (row % AR2_BLOCKS), so block b's barriers
+// cover exactly the rows block b reads, and its own epoch counters / flags (counter2 /
+// flag2) and data regions keep calls of the other kernels out of its way.  Every rank
+// computes the same residual / out bytes from the same owner rows.
+template <typename T, int NR>
+__device__ __forceinline__ void allreduce_rms2_body(const ArPtrs& P, int rank, int blk,
+                                                    const T* __restrict__ in,
+                                                    T* __restrict__ out,
+                                                    T* __restrict__ residual,
+                                                    const T* __restrict__ w, int M, int H,
+                                                    float eps, int64_t cap_vec) {
+  __shared__ float scratch[AR_THREADS / 64];
+  const uint32_t epoch = ar_epoch<true>(P, rank, blk);
+  const int64_t par_off = (int64_t)(epoch & 1) * cap_vec;
+  const int nv = H >> 3;
+  const u32x4* src = reinterpret_cast<const u32x4*>(in);
+  u32x4* mine = reinterpret_cast<u32x4*>(P.data[rank]) + par_off;
+
+  for (int row = blk; row < M; row += AR2_BLOCKS)
+    for (int v = threadIdx.x; v < nv; v += AR_THREADS)
+      mine[(int64_t)row * nv + v] = src[(int64_t)row * nv + v];
+  ar_barrier<NR, true>(P, rank, blk, 0, epoch);
+  for (int row = blk; row < M; row += AR2_BLOCKS) {
+    if (row % NR != rank) continue;
+    for (int v = threadIdx.x; v < nv; v += AR_THREADS) {
+      const int64_t e = (int64_t)row * nv + v;
+      const u32x4 s = ar_sum_vec<T, NR>(P, par_off, e);
+      mine[e] = s;
     }
   }
-  if (threadIdx.x == 0) self->counter[blockIdx.x] = epoch;
+  ar_barrier<NR, true>(P, rank, blk, 1, epoch);
+  Pack8<T> wv[ARN_MAXV];
+#pragma unroll
+  for (int i = 0; i < ARN_MAXV; ++i) {
+    const int v = threadIdx.x + i * AR_THREADS;
+    if (v < nv) wv[i].u = reinterpret_cast<const u32x4*>(w)[v];
+  }
+  for (int row = blk; row < M; row += AR2_BLOCKS) {
+    const u32x4* owner = reinterpret_cast<const u32x4*>(P.data[row % NR]) + par_off;
+    Pack8<T> h[ARN_MAXV];
+#pragma unroll
+    for (int i = 0; i < ARN_MAXV; ++i) {
+      const int v = threadIdx.x + i * AR_THREADS;
+      if (v < nv) h[i].u = ld_peer(owner + (int64_t)row * nv + v);
+    }
+    ar_add_norm_row<T>(h, wv, residual, out, row, nv, H, eps, scratch);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *ar_counter<true>(reinterpret_cast<ArSignal*>(P.sig[rank]), blk) = epoch;
 }
+
+template <typename T, int NR>
+__global__ __launch_bounds__(AR_THREADS) void allreduce_rms2_kernel(
+    ArPtrs P, int rank, const T* __restrict__ in, T* __restrict__ out, T* __restrict__ residual,
+    const T* __restrict__ w, int M, int H, float eps, int64_t cap_vec) {
+  allreduce_rms2_body<T, NR>(P, rank, blockIdx.x, in, out, residual, w, M, H, eps, cap_vec);
+}
+
+template <typename T, int NR>
+__global__ __launch_bounds__(AR_THREADS) void allreduce_rms2_emu_kernel(
+    ArPtrs P, ArWorld W, const T* __restrict__ w, int M, int H, float eps, int64_t cap_vec) {
+  const int rank = blockIdx.x % NR, blk = blockIdx.x / NR;
+  allreduce_rms2_body<T, NR>(P, rank, blk, reinterpret_cast<const T*>(W.a[rank]),
+                             reinterpret_cast<T*>(W.b[rank]), reinterpret_cast<T*>(W.c[rank]), w,
+                             M, H, eps, cap_vec);
+}
+
+#define KGC_AR_RANKS(NR_, CALL) \
+  switch (NR_) {                \
+    case 2: CALL(2); break;     \
+    case 4: CALL(4); break;     \
+    case 8: CALL(8); break;     \
+    default: break;             \
+  }
 
 template <typename T>
 static void arn_by_ranks(int nranks, const ArPtrs& P, int rank, const void* in, void* out,
                          void* residual, const void* w, int M, int H, float eps, int64_t cap_vec,
-                         hipStream_t s) {
-  const dim3 g(AR_MAX_BLOCKS), b(AR_THREADS);
-#define KGC_ARN(NR_)                                                                          \
-  allreduce_rms_kernel<T, NR_><<<g, b, 0, s>>>(P, rank, (const T*)in, (T*)out, (T*)residual, \
-                                               (const T*)w, M, H, eps, cap_vec)
-  switch (nranks) {
-    case 2: KGC_ARN(2); break;
-    case 4: KGC_ARN(4); break;
-    case 8: KGC_ARN(8); break;
-    default: break;
-  }
+                         bool two, hipStream_t s) {
+#define KGC_ARN(NR_)                                                                             \
+  if (two)                                                                                       \
+    allreduce_rms2_kernel<T, NR_><<<AR2_BLOCKS, AR_THREADS, 0, s>>>(                             \
+        P, rank, (const T*)in, (T*)out, (T*)residual, (const T*)w, M, H, eps, cap_vec);          \
+  else                                                                                           \
+    allreduce_rms_kernel<T, NR_><<<AR_MAX_BLOCKS, AR_THREADS, 0, s>>>(                           \
+        P, rank, (const T*)in, (T*)out, (T*)residual, (const T*)w, M, H, eps, cap_vec)
+  KGC_AR_RANKS(nranks, KGC_ARN)
 #undef KGC_ARN
 }
 
@@ -248,32 +419,25 @@ int allreduce_rms_max_hidden() { return AR_THREADS * ARN_MAXV * 8; }
 
 void launch_allreduce_rms(int dtype, const ArPtrs& P, int nranks, int rank, const void* in,
                           void* out, void* residual, const void* w, int M, int H, float eps,
-                          int64_t cap_vec, hipStream_t s) {
+                          int64_t cap_vec, bool two_shot, hipStream_t s) {
   if (dtype == DT_BF16)
-    arn_by_ranks<bf16>(nranks, P, rank, in, out, residual, w, M, H, eps, cap_vec, s);
+    arn_by_ranks<bf16>(nranks, P, rank, in, out, residual, w, M, H, eps, cap_vec, two_shot, s);
   else
-    arn_by_ranks<f16>(nranks, P, rank, in, out, residual, w, M, H, eps, cap_vec, s);
-}
-
-template <typename T, int NR>
-static void ar_dispatch(const ArPtrs& P, int rank, void* inout, int64_t nvec, int64_t cap_vec,
-                        bool two, hipStream_t s) {
-  constexpr int blocks = AR_MAX_BLOCKS;
-  if (two)
-    allreduce_kernel<T, NR, true><<<blocks, AR_THREADS, 0, s>>>(P, rank, (T*)inout, nvec, cap_vec);
-  else
-    allreduce_kernel<T, NR, false><<<blocks, AR_THREADS, 0, s>>>(P, rank, (T*)inout, nvec, cap_vec);
+    arn_by_ranks<f16>(nranks, P, rank, in, out, residual, w, M, H, eps, cap_vec, two_shot, s);
 }
 
 template <typename T>
 static void ar_by_ranks(int nranks, const ArPtrs& P, int rank, void* inout, int64_t nvec,
                         int64_t cap_vec, bool two, hipStream_t s) {
-  switch (nranks) {
-    case 2: ar_dispatch<T, 2>(P, rank, inout, nvec, cap_vec, two, s); break;
-    case 4: ar_dispatch<T, 4>(P, rank, inout, nvec, cap_vec, two, s); break;
-    case 8: ar_dispatch<T, 8>(P, rank, inout, nvec, cap_vec, two, s); break;
-    default: break;
-  }
+#define KGC_AR(NR_)                                                                          \
+  if (two)                                                                                   \
+    allreduce_kernel<T, NR_, true><<<AR_MAX_BLOCKS, AR_THREADS, 0, s>>>(P, rank, (T*)inout,  \
+                                                                        nvec, cap_vec);      \
+  else                                                                                       \
+    allreduce_kernel<T, NR_, false><<<AR_MAX_BLOCKS, AR_THREADS, 0, s>>>(P, rank, (T*)inout, \
+                                                                         nvec, cap_vec)
+  KGC_AR_RANKS(nranks, KGC_AR)
+#undef KGC_AR
 }
 
 int allreduce_max_blocks() { return AR_MAX_BLOCKS; }
@@ -286,6 +450,37 @@ void launch_allreduce(int dtype, const ArPtrs& P, int nranks, int rank, void* in
     ar_by_ranks<bf16>(nranks, P, rank, inout, nvec, cap_vec, two_shot, s);
   else
     ar_by_ranks<f16>(nranks, P, rank, inout, nvec, cap_vec, two_shot, s);
+}
+
+// ---- world emulation launches (tests): kind 0 plain one-shot, 1 plain two-shot,
+// 2 fused one-shot, 3 fused two-shot (row-segmented).  W.a = inout / in, W.b = out,
+// W.c = residual of each rank; P.data = each rank's data region for the kernel kind.
+template <typename T>
+static void ar_emu_t(int kind, const ArPtrs& P, const ArWorld& W, int nranks, int64_t nvec,
+                     const void* w, int M, int H, float eps, int64_t cap_vec, hipStream_t s) {
+  const int g1 = nranks * AR_MAX_BLOCKS, g2 = nranks * AR2_BLOCKS;
+#define KGC_EMU(NR_)                                                                           \
+  switch (kind) {                                                                              \
+    case 0: allreduce_emu_kernel<T, NR_, false><<<g1, AR_THREADS, 0, s>>>(P, W, nvec, cap_vec); \
+      break;                                                                                   \
+    case 1: allreduce_emu_kernel<T, NR_, true><<<g1, AR_THREADS, 0, s>>>(P, W, nvec, cap_vec);  \
+      break;                                                                                   \
+    case 2: allreduce_rms_emu_kernel<T, NR_><<<g1, AR_THREADS, 0, s>>>(P, W, (const T*)w, M, H, \
+                                                                       eps, cap_vec);          \
+      break;                                                                                   \
+    default: allreduce_rms2_emu_kernel<T, NR_><<<g2, AR_THREADS, 0, s>>>(P, W, (const T*)w, M,  \
+                                                                         H, eps, cap_vec);     \
+      break;                                                                                   \
+  }
+  KGC_AR_RANKS(nranks, KGC_EMU)
+#undef KGC_EMU
+}
+
+void launch_allreduce_emu(int dtype, int kind, const ArPtrs& P, const ArWorld& W, int nranks,
+                          int64_t nvec, const void* w, int M, int H, float eps, int64_t cap_vec,
+                          hipStream_t s) {
+  if (dtype == DT_BF16) ar_emu_t<bf16>(kind, P, W, nranks, nvec, w, M, H, eps, cap_vec, s);
+  else ar_emu_t<f16>(kind, P, W, nranks, nvec, w, M, H, eps, cap_vec, s);
 }
 
 // ---- IPC buffer management (host) ----------------------------------------------

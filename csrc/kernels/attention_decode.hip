@@ -33,6 +33,7 @@
 // each): 149 vs 137 us for rope_kv + decode at B = 256, S = 4.
 #include "common.h"
 #include "launch.h"
+#include <cstdlib>
 #include <type_traits>
 
 namespace kgc {
@@ -430,6 +431,229 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// K1w: ONE WAVE per (seq, kv-head, z-slice), a 64-thread workgroup, its 32-key chunks
+// software-pipelined two deep (chunk c + 1's K and V loads are in flight while chunk c's
+// MFMAs and softmax run).  Why (round 4, profiles/README.md "K1w"): the 4-wave workgroup
+// above runs equal-length workgroups in lock-step rounds; every round starts with all
+// waves of a CU in their q / rope prologue and ends with all of them in the LDS merge, so
+// the CU's memory pipe idles twice per round (~10-15 % of a 125 us dispatch at B = 256),
+// and each wave's own loads stop while it computes.  Here a wave streams its whole
+// context share (B = 256: one wave per (seq, kv-head), 20 chunks at ctx 640) with the
+// next chunk always in flight; prologue and epilogue come once per wave, there is no
+// cross-wave merge and no barrier.  256 VGPRs at 2 waves per SIMD hold both chunk
+// buffers (2 x 64), O^T (32) and q (16).  Same math as paged_decode_kernel: S^T tiles
+// with the row->key map key(m) = 8*(m>>2) + (m&3), P taken from S^T's accumulator as the
+// P.V B operand, log2-domain online softmax.
+// Block ids come from wave-uniform scalar loads (one or two per chunk), never from a
+// vector load the chunk pipeline would have to wait behind.
+// Z > 1: slice z writes (max, sum, O) partials at row-major slot row * Z + z (the reduce
+// kernel runs with Zmax = Z).
+template <typename T, int D, bool KV8, bool FUSE>
+__global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
+    T* __restrict__ out, const T* __restrict__ q, const void* __restrict__ kc_,
+    const void* __restrict__ vc_, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ ctx_lens, float* __restrict__ max_logits,
+    float* __restrict__ exp_sums, float* __restrict__ tmp_out, int nq, int nkv, int bs_log2,
+    float scale_log2, float v_scale, int num_blocks, DecodeRope rp) {
+  typedef typename Vec8<T>::type V8;
+  typedef std::conditional_t<KV8, uint8_t, T> C;
+  const C* __restrict__ kc = reinterpret_cast<const C*>(kc_);
+  const C* __restrict__ vc = reinterpret_cast<const C*>(vc_);
+  auto ldf = [](const C* p) -> u32x4 {
+    if constexpr (KV8) return fp8x8_widen<T>(*reinterpret_cast<const u32x2*>(p));
+    else return *reinterpret_cast<const u32x4*>(p);
+  };
+  constexpr int KS = D / 32, DT = D / 16;
+  __shared__ __attribute__((aligned(16))) T lds_q[FUSE ? 16 : 1][FUSE ? D + 8 : 8];
+  const int b = blockIdx.x, h = blockIdx.y, z = blockIdx.z, Z = gridDim.z;
+  const int lane = threadIdx.x;
+  const int r16 = lane & 15, qd = lane >> 4;
+  const int G = nq / nkv;
+  int ctx_in = ctx_lens[b];
+  KGC_DCHECK_RANGE(ctx_in, 0, (bt_stride << bs_log2) + 1, "decode ctx_len");
+  const int ctx = min(ctx_in, bt_stride << bs_log2);
+  const int* bt = block_tables + (int64_t)b * bt_stride;
+  const int bsm = (1 << bs_log2) - 1;
+  const int64_t head_stride = (int64_t)D << bs_log2;
+  const C* kbase = kc + h * head_stride;
+  const C* vbase = vc + h * head_stride;
+  const int64_t blk_stride = (int64_t)nkv * head_stride;
+  const int keyA = 8 * (r16 >> 2) + (r16 & 3);
+
+  const int nchunk = (ctx + 31) >> 5;
+  const int c0 = (int)(((int64_t)nchunk * z) / Z);
+  const int c1 = (int)(((int64_t)nchunk * (z + 1)) / Z);
+  const int end = min(ctx, c1 << 5);          // this wave's tokens: [c0*32, end)
+  const int last_blk = max(0, (end - 1) >> bs_log2);
+
+  struct Frag {
+    Pack8<T> k[2][KS];
+    Pack8<T> v[DT];
+  };
+  // A 32-token chunk spans one block (bs >= 32) or two (bs = 16; the host keeps bs >= 16):
+  // their ids are wave-uniform scalar loads (lgkmcnt), so looking them up never waits on
+  // the vector loads in flight (a lane-shuffled register window did: its rare reload
+  // branch made the wait-count pass drain vmcnt at every chunk).
+  auto issue = [&](Frag& f, int ci) {
+    const int base = ci << 5;
+    const int blo = base >> bs_log2, bhi = min((base + 31) >> bs_log2, last_blk);
+    const int64_t plo = kgc_bt(bt, blo, bt_stride, num_blocks);
+    const int64_t phi = kgc_bt(bt, bhi, bt_stride, num_blocks);
+    auto blk_of = [&](int tok) -> int64_t { return (tok >> bs_log2) == blo ? plo : phi; };
+    const int ta = min(base + keyA, end - 1), tb = min(base + keyA + 4, end - 1);
+    const C* ka = kbase + blk_of(ta) * blk_stride + (int64_t)(ta & bsm) * D + 8 * qd;
+    const C* kb = kbase + blk_of(tb) * blk_stride + (int64_t)(tb & bsm) * D + 8 * qd;
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2) {
+      f.k[0][s2].u = ldf(ka + 32 * s2);
+      f.k[1][s2].u = ldf(kb + 32 * s2);
+    }
+    const int t0 = min(base + 8 * qd, end - 1) & ~7;
+    const C* va = vbase + blk_of(t0) * blk_stride + ((t0 & bsm) >> 3) * (D * 8) + r16 * 8;
+#pragma unroll
+    for (int t = 0; t < DT; ++t) f.v[t].u = ldf(va + 16 * t * 8);
+  };
+
+  float m_run = -INFINITY, l_run = 0.f;
+  f32x4 o[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  V8 qf[KS];
+
+  auto compute = [&](const Frag& f, int ci) {
+    const int base = ci << 5;
+    f32x4 sa = {0.f, 0.f, 0.f, 0.f}, sb = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2) {
+      sa = mfma16x16x32(f.k[0][s2].v, qf[s2], sa);
+      sb = mfma16x16x32(f.k[1][s2].v, qf[s2], sb);
+    }
+    float m = m_run;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int tok = base + 8 * qd + i;
+      sa[i] = tok < end ? sa[i] * scale_log2 : -INFINITY;
+      sb[i] = tok + 4 < end ? sb[i] * scale_log2 : -INFINITY;
+      m = fmaxf(m, fmaxf(sa[i], sb[i]));
+    }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    const float alpha = exp2f(m_run - m);
+    m_run = m;
+    l_run *= alpha;
+#pragma unroll
+    for (int t = 0; t < DT; ++t) o[t] *= alpha;
+    Pack8<T> pf;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float pa = exp2f(sa[i] - m), pb = exp2f(sb[i] - m);
+      l_run += pa + pb;
+      pf.h[i] = from_f<T>(pa);
+      pf.h[4 + i] = from_f<T>(pb);
+    }
+#pragma unroll
+    for (int t = 0; t < DT; ++t) o[t] = mfma16x16x32(f.v[t].v, pf.v, o[t]);
+  };
+
+  Frag fa, fb;
+  // FUSE: the first chunk's loads go out before the q prologue unless that chunk holds
+  // the new token this wave is about to write
+  const bool prefetched = c0 < c1 && !(FUSE && c0 == nchunk - 1);
+  if (prefetched) issue(fa, c0);
+  if constexpr (FUSE) {
+    constexpr int TPH = D / 16;
+    for (int i = lane; i < G * TPH; i += 64) {
+      const int g = i / TPH, c = i % TPH;
+      const int64_t qe = (int64_t)b * rp.qkv_stride + (int64_t)(h * G + g) * D;
+      float xa[8], xb[8];
+      qkv_row8<T>(rp, qe + c * 8, xa);
+      qkv_row8<T>(rp, qe + D / 2 + c * 8, xb);
+      if (rp.q_norm_w) {
+        float ss = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss += xa[j] * xa[j] + xb[j] * xb[j];
+#pragma unroll
+        for (int o2 = 1; o2 < TPH; o2 <<= 1) ss += __shfl_xor(ss, o2, 64);
+        const float inv = rsqrtf(ss / (float)D + rp.eps);
+        norm8<T>(xa, inv, rp.q_norm_w, c * 8);
+        norm8<T>(xb, inv, rp.q_norm_w, D / 2 + c * 8);
+      }
+      if (rp.use_rope) rope8(xa, xb, rp.cos_sin + rp.positions[b] * D, c * 8, D / 2);
+      Pack8<T> oa, ob;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { oa.h[j] = from_f<T>(xa[j]); ob.h[j] = from_f<T>(xb[j]); }
+      *reinterpret_cast<u32x4*>(&lds_q[g][c * 8]) = oa.u;
+      *reinterpret_cast<u32x4*>(&lds_q[g][D / 2 + c * 8]) = ob.u;
+    }
+    if (z == Z - 1 && ctx > 0)
+      decode_kv_write<T, D, KV8>(rp, b, h, nq, nkv, bs_log2, num_blocks,
+                                 const_cast<void*>(kc_), const_cast<void*>(vc_), lane);
+    // the k / v stores complete before any later load of the chunk that holds them
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const bool valid = r16 < G;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      Pack8<T> t;
+      t.u = *reinterpret_cast<const u32x4*>(&lds_q[valid ? r16 : 0][32 * s + 8 * qd]);
+      if (!valid) t.u = u32x4{0, 0, 0, 0};
+      qf[s] = t.v;
+    }
+  } else {
+    const bool valid = r16 < G;
+    const T* qrow = q + ((int64_t)b * nq + h * G + (valid ? r16 : 0)) * D;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      Pack8<T> t;
+      t.u = *reinterpret_cast<const u32x4*>(qrow + 32 * s + 8 * qd);
+      if (!valid) t.u = u32x4{0, 0, 0, 0};
+      qf[s] = t.v;
+    }
+  }
+  if (!prefetched && c0 < c1) issue(fa, c0);
+  // two-deep pipeline over named buffers (a runtime-indexed buffer pair would live in
+  // scratch): while one chunk computes, the next one's loads are in flight.  The loop
+  // body is straight-line -- unconditional issues (past the range they re-load the wave's
+  // last chunk: cache hits) and, for an odd chunk count, one final chunk computed fully
+  // masked (its tokens are >= end: p = 0, alpha = 1) -- because any branch between an
+  // issue and its use makes the compiler's wait-count pass merge the paths and wait for
+  // the younger buffer too (measured in the .s: vmcnt(15) instead of (31) before the
+  // first MFMA, i.e. the pipeline serialised).
+  for (int ci = c0; ci < c1; ci += 2) {
+    issue(fb, min(ci + 1, c1 - 1));
+    compute(fa, ci);
+    issue(fa, min(ci + 2, c1 - 1));
+    compute(fb, ci + 1);
+  }
+
+  l_run += __shfl_xor(l_run, 16, 64);
+  l_run += __shfl_xor(l_run, 32, 64);
+  if (r16 >= G) return;
+  const int64_t row = (int64_t)b * nq + h * G + r16;
+  if (Z == 1) {
+    const float inv = l_run > 0.f ? v_scale / l_run : 0.f;
+    T* orow = out + row * D + 4 * qd;
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      Pack4<T> pk;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pk.h[i] = from_f<T>(o[t][i] * inv);
+      *reinterpret_cast<u32x2*>(orow + 16 * t) = pk.u;
+    }
+  } else {
+    const int64_t prow = row * Z + z;
+    float* dst = tmp_out + prow * D + 4 * qd;
+#pragma unroll
+    for (int t = 0; t < DT; ++t) *reinterpret_cast<f32x4*>(dst + 16 * t) = o[t] * v_scale;
+    if (qd == 0) {
+      max_logits[prow] = m_run;
+      exp_sums[prow] = l_run;
+    }
+  }
+}
+
 // Merge the Z z-slice partials: one 64-thread wave per (seq, q-head).
 template <typename T, int D>
 __global__ __launch_bounds__(64) void paged_decode_reduce_kernel(
@@ -483,12 +707,33 @@ __global__ __launch_bounds__(64) void paged_decode_reduce_kernel(
   for (int e = 0; e < EPT; ++e) orow[tid * EPT + e] = from_f<T>(acc[e] * inv);
 }
 
+// KGC_DECODE_WAVE=0: the 4-wave workgroup kernel (A/B); default: K1w
+bool decode_wave_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("KGC_DECODE_WAVE");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 template <typename T, int D, bool KV8, bool FUSE>
 static void decode_dispatch(void* out, const void* q, const void* kc, const void* vc,
                             const int* bt, int bt_stride, const int* ctx, float* ml, float* es,
                             float* tmp, int B, int nq, int nkv, int bs_log2, int Zmax, int Z,
                             float scale_log2, float v_scale, int num_blocks,
                             const DecodeRope& rp, hipStream_t s) {
+  if (decode_wave_enabled() && bs_log2 >= 4) {
+    // partial rows are Z apart (the workspace is sized for B * Z rows per head)
+    paged_decode_wave_kernel<T, D, KV8, FUSE><<<dim3(B, nkv, Z), 64, 0, s>>>(
+        (T*)out, (const T*)q, kc, vc, bt, bt_stride, ctx, ml, es, tmp, nq, nkv, bs_log2,
+        scale_log2, v_scale, num_blocks, rp);
+    if (Z > 1)
+      paged_decode_reduce_kernel<T, D><<<dim3(B, nq), 64, 0, s>>>((T*)out, ml, es, tmp, ctx,
+                                                                  nq, Z, Z);
+    return;
+  }
+  // (the 4-wave kernel also serves blocks < 16 tokens; in K1w mode the binding passes
+  // Zmax = Z, so its partial rows are packed the same way)
   auto kern = paged_decode_kernel<T, D, true, KV8, 4, 1, FUSE>;
   kern<<<dim3(B, nkv, Z), 256, 0, s>>>(
       (T*)out, (const T*)q, kc, vc, bt, bt_stride, ctx, ml, es, tmp, nq,
@@ -545,7 +790,8 @@ void launch_paged_decode_rope(int dtype, const DecodeRope& rp, void* out, void* 
                       kv_fp8, k_scale, v_scale, num_blocks, rp, s);
 }
 
-int paged_decode_partition_size() { return DEC_PART; }
+int paged_decode_partition_size() { return decode_wave_enabled() ? 32 : DEC_PART; }
+int paged_decode_waves_per_slice() { return decode_wave_enabled() ? 1 : 4; }
 
 KGC_DEBUG_TU(attention_decode)
 

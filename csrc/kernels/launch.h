@@ -27,6 +27,8 @@ void launch_paged_decode(int dtype, void* out, const void* q, const void* k_cach
                          int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
                          float v_scale, int num_blocks, hipStream_t s);
 int paged_decode_partition_size();
+// 1: the K1w kernel (one wave per (seq, kv-head, z-slice)); 4: the 4-wave workgroup kernel
+int paged_decode_waves_per_slice();
 // K1 + K3/K5/K6 fused for decode-only steps: the decode kernel takes the QKV projection
 // row itself (T [B, qkv_stride], or S > 0 fp32 split-K slices [S, B, qkv_stride]),
 // builds q (optional per-head RMSNorm, NeoX RoPE) in the MFMA operand registers, and
@@ -122,23 +124,12 @@ void launch_dense_gemm_splitk(int dtype, int bm, float* Cs, const void* A, const
 int dgemm_num_cfgs();
 void dgemm_cfg_info(int cfg, int* bm, int* bn, int* packed);
 int dgemm_block_k();
-bool dgemm_cfg_single_row_block(int cfg);   // K9v: one BM-row tile, M <= BM
 void launch_dgemm(int dtype, int cfg, int epi, void* C, const void* X, const void* W, int M,
                   int N, int K, int64_t ldx, int S, int64_t slice_stride, hipStream_t s);
 void launch_dgemm_pack(int dtype, bool silu, void* P, const void* W, int N, int K,
                        hipStream_t s);
 void launch_dgemm_ablate(int mode, float* C, const void* X, const void* W, int M, int N, int K,
                          int64_t ldx, int S, int64_t ss, hipStream_t s);
-// K9r ring decode GEMM (gemm_ring.hip), bf16: X [M, K] . W^T with tile config `cfg`
-// (ring_cfg_info: BM, BN, threads, ring slots) over W packed by launch_ring_pack into
-// [N/G][K/64][G*64] with G = the config's BN.  epi 0: fp32 split-K slice z of C [S, M, N];
-// 1: C [M, N] bf16 (S = 1); 2: silu(gate) * up of a merged [gate; up] W packed with
-// silu = true into C [M, N/2] (S = 1)
-int ring_num_cfgs();
-void ring_cfg_info(int cfg, int* bm, int* bn, int* threads, int* slots);
-void launch_ring_gemm(int cfg, int epi, void* C, const void* X, const void* Wp, int M, int N,
-                      int K, int64_t ldx, int S, int64_t slice_stride, hipStream_t s);
-void launch_ring_pack(bool silu, void* P, const void* W, int N, int K, int G, hipStream_t s);
 // residual += sum_z Cs[z] (rounded to dtype); out = rms_norm(residual) * w, one WG per row
 void launch_splitk_add_rms_norm(int dtype, void* out, const float* Cs, void* residual,
                                 const void* w, int rows, int H, int S, int64_t slice_stride,
@@ -156,6 +147,12 @@ struct ArPtrs {
   void* data[8];
   void* sig[8];
 };
+// per-rank operand pointers of a world-emulation launch (all ranks on one device)
+struct ArWorld {
+  void* a[8];
+  void* b[8];
+  void* c[8];
+};
 size_t allreduce_signal_bytes();
 int allreduce_max_blocks();
 // spin-wait bounds (common.h) in ms: {peer (AR/PP/EP), same-kernel (sampler)}, and the
@@ -165,12 +162,19 @@ int coop_spin_ms();
 int64_t wall_clock_rate_khz();
 void launch_allreduce(int dtype, const ArPtrs& P, int nranks, int rank, void* inout,
                       int64_t nvec, int64_t cap_vec, bool two_shot, hipStream_t s);
-// fused one-shot all-reduce + residual add + RMSNorm over [M, H] rows (P.data: the
-// fused regions); H % 8 == 0 and H <= allreduce_rms_max_hidden()
+// fused all-reduce + residual add + RMSNorm over [M, H] rows (P.data: the fused regions
+// of the chosen form); H % 8 == 0 and H <= allreduce_rms_max_hidden().  two_shot: the
+// row-segmented two-shot kernel (its own regions), else one-shot
 int allreduce_rms_max_hidden();
 void launch_allreduce_rms(int dtype, const ArPtrs& P, int nranks, int rank, const void* in,
                           void* out, void* residual, const void* w, int M, int H, float eps,
-                          int64_t cap_vec, hipStream_t s);
+                          int64_t cap_vec, bool two_shot, hipStream_t s);
+// world emulation (tests): all nranks ranks' blocks in one launch on one device.
+// kind 0 / 1: plain one- / two-shot on W.a[r] (nvec 16-B vectors); 2 / 3: fused one- /
+// two-shot with in W.a[r], out W.b[r], residual W.c[r] ([M, H]) and norm weight w
+void launch_allreduce_emu(int dtype, int kind, const ArPtrs& P, const ArWorld& W, int nranks,
+                          int64_t nvec, const void* w, int M, int H, float eps, int64_t cap_vec,
+                          hipStream_t s);
 // C7 expert-parallel dispatch / combine over the same kind of IPC buffers (ep_a2a.hip)
 using EpPtrs = ArPtrs;
 size_t ep_signal_bytes();

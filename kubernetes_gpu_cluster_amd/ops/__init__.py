@@ -163,11 +163,24 @@ def kv_write_rope(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Ten
 
 
 # ------------------------------------------------------------------ attention
-DECODE_PARTITION = 64        # tokens per wave-iteration of the decode kernel
+DECODE_PARTITION = 64        # tokens per wave-iteration of the 4-wave decode kernel
+DECODE_CHUNK = 32            # tokens per pipelined step of K1w
+DECODE_TARGET_WAVES = 2048   # K1w: 8 resident waves per CU (2 per SIMD at 256 VGPRs)
 PREFILL_BLOCK_M = 128
 
 
+def decode_wave_kernel() -> bool:
+    """K1w (one wave per (seq, kv-head, z-slice), csrc/kernels/attention_decode.hip) unless
+    KGC_DECODE_WAVE=0 selects the 4-wave workgroup kernel; the C++ launcher reads the same
+    variable, so the Z chosen here and the kernel that runs always agree."""
+    return os.environ.get("KGC_DECODE_WAVE", "1") != "0"
+
+
 def decode_max_z(max_blocks: int, block_size: int) -> int:
+    if decode_wave_kernel():
+        # at least two 32-token chunks per wave (the pipeline depth)
+        chunks = math.ceil(max_blocks * block_size / DECODE_CHUNK)
+        return max(1, min(1024, math.ceil(chunks / 2)))
     parts = math.ceil(max_blocks * block_size / DECODE_PARTITION)
     return max(1, math.ceil(parts / 4))
 
@@ -175,21 +188,42 @@ def decode_max_z(max_blocks: int, block_size: int) -> int:
 def decode_partials(batch: int, num_heads: int, head_dim: int, max_blocks: int,
                     block_size: int, device) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """Per-z-slice (max, sum, O) partials of the split-context decode kernel
-    (static: graph-capturable).  Unused when the grid has a single z-slice."""
+    (static: graph-capturable).  Unused when the grid has a single z-slice.
+    K1w packs the rows of a launch Z apart, so the workspace holds (seq, z) rows: enough
+    for every Z ``decode_grid_z`` picks at any batch <= ``batch`` (B * Z <= 2 x the wave
+    target + B), flat [rows * heads]."""
     Z = decode_max_z(max_blocks, block_size)
+    if decode_wave_kernel():
+        rows = min(batch * Z, 2 * DECODE_TARGET_WAVES + batch)
+        ml = torch.empty(rows * num_heads, dtype=torch.float32, device=device)
+        es = torch.empty(rows * num_heads, dtype=torch.float32, device=device)
+        tmp = torch.empty(rows * num_heads, head_dim, dtype=torch.float32, device=device)
+        return ml, es, tmp
     ml = torch.empty(batch, num_heads, Z, dtype=torch.float32, device=device)
     es = torch.empty(batch, num_heads, Z, dtype=torch.float32, device=device)
     tmp = torch.empty(batch, num_heads, Z, head_dim, dtype=torch.float32, device=device)
     return ml, es, tmp
 
 
-def decode_grid_z(batch: int, num_kv_heads: int, max_ctx: int, target_waves: int = 4096) -> int:
-    """z-slices of the decode grid: enough waves to fill 256 CUs (4 resident waves
-    per SIMD), bounded by the 64-token partitions of the longest context and by the
-    1024 slices the reduce kernel merges.  Z == 1 (large batches) lets the kernel
+def _decode_z_cap(ws, B: int, nq: int) -> int:
+    """Largest Z the workspace holds for a batch of B rows of nq heads."""
+    ml = ws[0]
+    if decode_wave_kernel():
+        return max(1, ml.numel() // max(1, B * nq))
+    return ml.shape[-1]
+
+
+def decode_grid_z(batch: int, num_kv_heads: int, max_ctx: int, target_waves: int = 0) -> int:
+    """z-slices of the decode grid: enough waves to fill 256 CUs, bounded by the
+    context (K1w: two 32-token chunks per wave; 4-wave kernel: 64-token partitions) and by
+    the 1024 slices the reduce kernel merges.  Z == 1 (large batches) lets the kernel
     write its output directly."""
+    if decode_wave_kernel():
+        chunks = max(1, math.ceil(max_ctx / DECODE_CHUNK))
+        want = math.ceil((target_waves or DECODE_TARGET_WAVES) / max(1, batch * num_kv_heads))
+        return max(1, min(want, math.ceil(chunks / 2), 1024))
     parts = max(1, math.ceil(max_ctx / DECODE_PARTITION))
-    want = math.ceil(target_waves / max(1, batch * num_kv_heads * 4))
+    want = math.ceil((target_waves or 4096) / max(1, batch * num_kv_heads * 4))
     return max(1, min(want, math.ceil(parts / 4), 1024))
 
 
@@ -207,7 +241,7 @@ def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torc
     if workspace is None:
         workspace = decode_partials(B, nq, d, block_tables.shape[1], k_cache.shape[2], q.device)
     ml, es, tmp = workspace
-    grid_z = min(grid_z, ml.shape[-1])
+    grid_z = min(grid_z, _decode_z_cap(workspace, B, nq))
     _k().paged_decode(out, q, k_cache, v_cache, block_tables, context_lens, ml, es, tmp,
                       grid_z, scale, k_scale, v_scale)
     return out
@@ -241,7 +275,7 @@ def paged_attention_decode_rope(qkv: torch.Tensor, positions: torch.Tensor,
         workspace = decode_partials(B, num_heads, head_dim, block_tables.shape[1],
                                     k_cache.shape[2], qkv.device)
     ml, es, tmp = workspace
-    grid_z = min(grid_z, ml.shape[-1])
+    grid_z = min(grid_z, _decode_z_cap(workspace, B, num_heads))
     _k().paged_decode_rope(out, qkv, positions, cos_sin, k_cache, v_cache, slot_mapping,
                            q_norm_w, k_norm_w, block_tables, context_lens, ml, es, tmp,
                            num_heads, grid_z, scale, eps, use_rope, k_scale, v_scale)

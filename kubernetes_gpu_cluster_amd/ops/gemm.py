@@ -452,9 +452,9 @@ _DG_SPLITS = tuple(int(v) for v in
 
 
 def _dg_candidates(M: int, N: int, K: int, kind: str, packed: bool):
+    # (K9v / K9r, measured slower than K9m on every M = 256 shape, are not in the engine's
+    # library: tools/research/; profiles/README.md "Round 3: K9r" / "Round 3: K9v")
     from . import _k
-    # (K9v, cfgs 11-13, measured slower than K9m on every M = 256 shape: not a candidate;
-    # profiles/README.md "Round 3: K9v")
     cfgs = [5, 7, 2] if M <= 128 else [6, 8, 4, 0, 10]
     out = []
     for c in range(_k().dgemm_num_cfgs()):
@@ -463,8 +463,6 @@ def _dg_candidates(M: int, N: int, K: int, kind: str, packed: bool):
         bm, bn, pk = _dg_info(c)
         if (pk and not packed) or N % bn:
             continue
-        if M > bm and _k().dgemm_cfg_single_row_block(c):
-            continue            # K9v: one 256-row tile
         # S = 3, 5, 6 fill the CUs where powers of two do not (qkv at M = 256: 48
         # column tiles x 5 = 240 workgroups vs 192 at S = 4); no XCD pairing for them
         splits = (1,) if kind == "silu" else _DG_SPLITS

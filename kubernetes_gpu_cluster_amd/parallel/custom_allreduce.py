@@ -68,8 +68,10 @@ class CustomAllReduce:
             k = torch.ops.kgc
             with torch.cuda.device(device):
                 sig_bytes = int(k.ar_signal_bytes())
-                # [signal | all-reduce parity 0 | parity 1 | fused parity 0 | parity 1]
-                self._own = int(k.ar_alloc(sig_bytes + 4 * self.cap))
+                # [signal | all-reduce parity 0 | parity 1 | fused one-shot parity 0 | 1 |
+                #  fused two-shot parity 0 | 1]: each kernel form has its own regions (their
+                #  row -> workgroup maps differ, see allreduce.hip)
+                self._own = int(k.ar_alloc(sig_bytes + 6 * self.cap))
                 handle = k.ar_get_handle(self._own).tolist()
         except Exception as e:  # noqa: BLE001
             err = e
@@ -96,11 +98,16 @@ class CustomAllReduce:
         self.sig = bases
         self.data = [b + sig_bytes for b in bases]
         self.fdata = [b + sig_bytes + 2 * self.cap for b in bases]
-        # fused all-reduce + add + RMSNorm: one-shot, so the sizes where the plain
-        # all-reduce would be one-shot too (larger rows: two-shot + fused_add_rms_norm)
+        self.fdata2 = [b + sig_bytes + 4 * self.cap for b in bases]
+        # fused all-reduce + add + RMSNorm: one-shot up to KGC_AR_RMS_MAX (default: the
+        # plain one-shot limit), the row-segmented two-shot form above it up to
+        # KGC_AR_RMS2_MAX (default: the whole buffer -- TP = 8 decode at batch 256 is
+        # 4 MB of 8192-wide rows)
         self.fused_max = int(os.environ.get("KGC_AR_RMS_MAX", self.one_shot_max))
+        self.fused2_max = int(os.environ.get("KGC_AR_RMS2_MAX", self.cap))
         self.max_hidden = int(k.allreduce_rms_max_hidden())
         self.fused_calls = 0        # host-side launches (a graph capture counts once)
+        self.fused2_calls = 0       # ... of them the two-shot form
 
     def should_use(self, x: torch.Tensor) -> bool:
         if not x.is_cuda or x.dtype not in (torch.bfloat16, torch.float16):
@@ -119,8 +126,9 @@ class CustomAllReduce:
             return False
         H = x.shape[1]
         nb = x.numel() * x.element_size()
-        return (x.is_contiguous() and 0 < nb <= min(self.fused_max, self.cap) and H % 8 == 0
-                and H <= self.max_hidden)
+        return (x.is_contiguous() and 0 < nb <= min(max(self.fused_max, self.fused2_max),
+                                                      self.cap)
+                and H % 8 == 0 and H <= self.max_hidden)
 
     def all_reduce_add_rms(self, x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
                            eps: float, out: torch.Tensor = None):
@@ -129,8 +137,12 @@ class CustomAllReduce:
         if out is None:
             out = torch.empty_like(x)
         self.fused_calls += 1
-        torch.ops.kgc.xgmi_allreduce_rms(out, x, residual, w, eps, self.fdata, self.sig,
-                                         self.rank, self.cap)
+        two = x.numel() * x.element_size() > self.fused_max
+        if two:
+            self.fused2_calls += 1
+        torch.ops.kgc.xgmi_allreduce_rms(out, x, residual, w, eps,
+                                         self.fdata2 if two else self.fdata, self.sig,
+                                         self.rank, self.cap, two)
         return out, residual
 
     def check(self) -> None:
@@ -175,7 +187,8 @@ def maybe_init_custom_allreduce(ps, device: torch.device) -> Optional[CustomAllR
         log.warning("%s; using RCCL", e)
         return None
     log.info("xGMI all-reduce enabled: tp=%d cap=%d KiB (KGC_AR_CAP) one-shot<=%d KiB "
-             "(KGC_AR_ONE_SHOT_MAX) fused add+RMSNorm<=%d KiB (KGC_AR_RMS_MAX), %d workgroups",
+             "(KGC_AR_ONE_SHOT_MAX) fused add+RMSNorm one-shot<=%d KiB (KGC_AR_RMS_MAX), "
+             "two-shot<=%d KiB (KGC_AR_RMS2_MAX), %d workgroups",
              ps.tp_size, car.cap >> 10, car.one_shot_max >> 10, car.fused_max >> 10,
-             int(torch.ops.kgc.allreduce_max_blocks()))
+             car.fused2_max >> 10, int(torch.ops.kgc.allreduce_max_blocks()))
     return car

@@ -4,7 +4,6 @@ import pytest
 import torch
 
 from kubernetes_gpu_cluster_amd.engine.config import EngineConfig
-from kubernetes_gpu_cluster_amd.engine.health import AllReduceFailed
 from kubernetes_gpu_cluster_amd.engine.llm_engine import LLMEngine
 from kubernetes_gpu_cluster_amd.engine.sequence import SamplingParams
 from kubernetes_gpu_cluster_amd.models import PRESETS, build_model, full_state_dict_random
@@ -213,12 +212,12 @@ def test_engine_preemption_recompute(gpu):
     assert eng.bm.num_free == eng.bm.num_blocks - 1
 
 
-@pytest.mark.parametrize("tp,eager,name,overlap", [(2, True, "tiny-llama", False),
-                                                  (2, False, "tiny-llama", False),
-                                                  (2, False, "tiny-llama", True),
-                                                  (4, False, "tiny-llama", False),
-                                                  (8, False, "tiny-llama-gqa8", False)])
-def test_tp_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch, tp, eager, name, overlap):
+@pytest.mark.parametrize("tp,eager,name,overlap,xgmi", [(2, True, "tiny-llama", False, True),
+                                                        (2, False, "tiny-llama", False, True),
+                                                        (2, False, "tiny-llama", True, True),
+                                                        (4, False, "tiny-llama", False, True),
+                                                        (8, True, "tiny-llama-gqa8", False, False)])
+def test_tp_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch, tp, eager, name, overlap, xgmi):
     """The tensor-parallel engine on the GPU: TP ranks share cuda:0 (gloo process group,
     since RCCL refuses two ranks on one device), sharded QKV/MLP/vocab layers, the xGMI
     all-reduce kernel over IPC buffers for the row-parallel sums, multiprocess workers.
@@ -226,10 +225,15 @@ def test_tp_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch, tp, eager, name, 
     the xGMI all-reduce INSIDE the graphs, and vocab-parallel sampling after the replay
     (no logits all-gather).  overlap: the 100-token first prefill step runs as two
     halves whose all-reduces are in flight while the other half computes
-    (KGC_TP_OVERLAP_MIN_TOKENS lowered from 2048 to 16).  TP = 4 replicates tiny-llama's 2 kv heads over 4 ranks; TP = 8
-    (BASELINE config 3's degree) runs the 8-rank all-reduce instantiation with each of
-    tiny-llama-gqa8's 2 kv heads on 4 ranks.  Greedy continuations match TP=1 (bf16;
-    sharded sums round differently, so a couple of late near-tie flips are tolerated)."""
+    (KGC_TP_OVERLAP_MIN_TOKENS lowered from 2048 to 16).  TP = 4 replicates tiny-llama's
+    2 kv heads over 4 ranks.  TP = 8 (BASELINE config 3's degree: each of tiny-llama-gqa8's
+    2 kv heads on 4 ranks, the per-rank attention shape of 70B at TP = 8 -- one kv head,
+    GQA 1) runs every GPU kernel of the 8-rank engine with its sums over gloo
+    (KGC_CUSTOM_AR=0, eager): eight processes' spin kernels need not be co-resident on
+    ONE device, so the xGMI kernels' NR = 8 forms are proven by the single-launch world
+    emulation instead (test_allreduce_gpu.py::test_xgmi_world_emulation).  Greedy
+    continuations match TP=1 (bf16; sharded sums round differently, so a couple of late
+    near-tie flips are tolerated)."""
     import json
     import os
     from safetensors.torch import save_file
@@ -250,6 +254,8 @@ def test_tp_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch, tp, eager, name, 
     sp = [SamplingParams(temperature=0, max_tokens=8, ignore_eos=True)] * 3
     outs = {}
     monkeypatch.setenv("KGC_DIST_BACKEND", "gloo")
+    if not xgmi:
+        monkeypatch.setenv("KGC_CUSTOM_AR", "0")
     if overlap:
         monkeypatch.setenv("KGC_TP_OVERLAP_MIN_TOKENS", "16")
     tp_n = tp
@@ -257,25 +263,20 @@ def test_tp_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch, tp, eager, name, 
         llm = LLM(d, device="cuda", dtype="bfloat16", tensor_parallel_size=tp, enforce_eager=eager,
                   max_model_len=256, max_num_seqs=4, max_num_batched_tokens=128,
                   num_gpu_blocks_override=64)
+        car = None
         if tp > 1:
             from kubernetes_gpu_cluster_amd.parallel import comm
             car = comm.get_custom_allreduce()
-            assert car is not None, f"xGMI all-reduce was not set up for TP={tp}"
-            assert car.world == tp
-        try:
-            outs[tp] = [o.output_token_ids for o in llm.generate(prompts, sp)]
-            if tp > 1:
-                car.check()     # a time-out on ANY rank is raised in every rank's word
-        except AllReduceFailed as e:
-            llm.shutdown()
-            if tp < 8:
-                raise
-            # eight ranks' spin barriers on ONE GPU need all eight processes' kernels
-            # resident at once, which one device does not always grant
-            # (test_allreduce_gpu.py); the engine reported it instead of serving garbage
-            pytest.xfail(f"TP=8 on one GPU: {e}")
-        if tp > 1:
+            if xgmi:
+                assert car is not None, f"xGMI all-reduce was not set up for TP={tp}"
+                assert car.world == tp
+            else:
+                assert car is None, "KGC_CUSTOM_AR=0 must leave every sum to the process group"
+        outs[tp] = [o.output_token_ids for o in llm.generate(prompts, sp)]
+        if car is not None:
+            car.check()         # a time-out on ANY rank is raised in every rank's word
             assert car.fused_calls > 0, "fused all-reduce + add + RMSNorm never ran"
+        if tp > 1:
             st = llm.engine.executor.runner.stats
             assert st["vp_steps"] > 0, st
             if not eager:

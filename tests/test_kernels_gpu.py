@@ -128,8 +128,10 @@ def _fill_random_cache(B, ctx_lens, nkv, bs, d, dt, dev, nb_extra=7):
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("d,nq,nkv", [(128, 32, 8), (128, 8, 1), (128, 28, 4), (64, 12, 12),
                                       (128, 16, 16)])
-@pytest.mark.parametrize("bs", [16, 32])
+@pytest.mark.parametrize("bs", [8, 16, 32])
 def test_paged_decode(gpu, dt, d, nq, nkv, bs):
+    """K1 vs the fp32 reference at ragged lengths (1 token .. 2049), GQA 1/4/7/8 and MHA,
+    z = 1 and 3; bs = 8 runs the 4-wave kernel (K1w takes blocks of >= 16 tokens)."""
     torch.manual_seed(3)
     ctx = [1, 17, 128, 129, 300, 1000, 2049, 64]
     B = len(ctx)
@@ -144,7 +146,7 @@ def test_paged_decode(gpu, dt, d, nq, nkv, bs):
 
 
 @pytest.mark.parametrize("dt", DT)
-@pytest.mark.parametrize("d,nq,nkv", [(128, 32, 8), (64, 8, 2), (128, 16, 16)])
+@pytest.mark.parametrize("d,nq,nkv", [(128, 32, 8), (64, 8, 2), (128, 16, 16), (128, 8, 1)])
 @pytest.mark.parametrize("qk_norm", [False, True])
 @pytest.mark.parametrize("S", [0, 3, 5])
 @pytest.mark.parametrize("fp8", [False, True])
@@ -771,15 +773,14 @@ def test_tune_skinny_silu_records_plan(gpu):
         gemm.clear_plan()
 
 
-@pytest.mark.parametrize("cfg", list(range(14)))
+@pytest.mark.parametrize("cfg", list(range(11)))
 @pytest.mark.parametrize("M,N,K", [(256, 1024, 4096), (200, 768, 1024), (77, 512, 2048),
                                    (130, 256, 128)])
 def test_dgemm_matches_fp32(gpu, cfg, M, N, K):
-    """K9m / K9v decode GEMM (every tile config, packed and row-major weights) vs an fp32
+    """K9m decode GEMM (every tile config, packed and row-major weights) vs an fp32
     matmul: bf16 output (S = 1), fp32 split-K slices (S = 2, 3, 4, 5: uneven K ranges at 3
     and 5) and the fused SiLU epilogue, with M not a multiple of the row block (clamped
-    loads, masked stores).  K = 128 leaves K9v slices of one or two K-steps, fewer than its
-    prefetch depth: the filler groups and the tail waits."""
+    loads, masked stores)."""
     from kubernetes_gpu_cluster_amd.ops import gemm
     k = torch.ops.kgc
     bm, bn, pk = k.dgemm_cfg_info(cfg)
@@ -822,37 +823,6 @@ def test_dgemm_pack_layout(gpu):
     for nb, kb, r, pos in [(0, 0, 0, 0), (1, 1, 5, 3), (0, 1, 127, 7), (1, 0, 64, 2)]:
         src = wc[nb * 128 + r, kb * 64 + (pos ^ (r % 8)) * 8: kb * 64 + (pos ^ (r % 8)) * 8 + 8]
         assert torch.equal(pc[nb, kb, r, pos], src)
-
-
-@pytest.mark.parametrize("cfg", range(18))
-def test_ring_gemm_matches_fp32(gpu, cfg):
-    """K9r ring GEMM (gemm_ring.hip, every tile config) vs an fp32 matmul: bf16 output,
-    fp32 split-K slices (S = 2, 3: uneven K ranges, XCD-mapped) and the SiLU epilogue over
-    the 8-row gate / up interleave; M not a multiple of BM (clamped loads, masked rows)."""
-    k = torch.ops.kgc
-    bm, bn, thr, ns = k.ring_cfg_info(cfg)
-    N, K = bn * 16, 640
-    M = bm - 37 if bm > 64 else bm + 5
-    torch.manual_seed(cfg)
-    x = torch.randn(M, K, dtype=torch.bfloat16, device=gpu)
-    w = torch.randn(N, K, dtype=torch.bfloat16, device=gpu) * 0.02
-    ref = x.float().cpu() @ w.float().cpu().t()
-
-    def packed(silu):
-        p = torch.empty(N // bn, K // 64, bn * 64, dtype=w.dtype, device=gpu)
-        k.ring_pack(p, w, silu)
-        return p
-    out = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
-    k.ring_gemm(out, x, packed(False), cfg, 1)
-    torch.testing.assert_close(out.float().cpu(), ref, atol=3e-2, rtol=2e-2)
-    for S in (2, 3):
-        ws = torch.full((S, M, N), float("nan"), dtype=torch.float32, device=gpu)
-        k.ring_gemm(ws, x, packed(False), cfg, 0)
-        torch.testing.assert_close(ws.sum(0).cpu(), ref, atol=2e-3, rtol=2e-3)
-    act = torch.empty(M, N // 2, dtype=torch.bfloat16, device=gpu)
-    k.ring_gemm(act, x, packed(True), cfg, 2)
-    exp = torch.nn.functional.silu(ref[:, : N // 2]) * ref[:, N // 2:]
-    torch.testing.assert_close(act.float().cpu(), exp, atol=3e-2, rtol=2e-2)
 
 
 def test_linear_uses_dgemm_plan(gpu):

@@ -122,8 +122,6 @@ def main():
                 bm, bn, pk = k.dgemm_cfg_info(cid)
                 if (bm == 256 and M <= 128) or N % bn or (want_cfgs is not None and cid not in want_cfgs):
                     continue
-                if k.dgemm_cfg_single_row_block(cid) and M > bm:
-                    continue
                 for S in [int(s) for s in a.splits.split(",")]:
                     if K // 64 < S:
                         continue

@@ -35,6 +35,7 @@
 // reference deploys, /root/reference/values-01-minimal-example2.yaml:6-7).
 #include "common.h"
 #include "launch.h"
+#include "research.h"
 #include <cstdlib>
 
 namespace kgc {

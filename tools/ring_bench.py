@@ -1,4 +1,4 @@
-"""K9r full-K ring decode GEMM (csrc/kernels/gemm_ring.hip) vs hipBLASLt and K9m.
+"""K9r full-K ring decode GEMM (tools/research/gemm_ring.hip) vs hipBLASLt and K9m.
 
     python tools/ring_bench.py [--model llama-3-8b] [--ms 256] [--copies 16]
                                [--shapes qkv,o,gate_up,down] [--cfgs 0,1,...] [--g 0|16|32]
@@ -62,7 +62,10 @@ def main():
     a = ap.parse_args()
     from kubernetes_gpu_cluster_amd import ops
     ops.load_extension(strict=True)
-    k = torch.ops.kgc
+    # K9r lives in the research library (tools/research/build.py), not the engine's
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "research"))
+    import build as research_build
+    k = research_build.load()
     dev = torch.device("cuda")
     torch.manual_seed(0)
     ncfg = k.ring_num_cfgs()
