@@ -845,6 +845,12 @@ void u32_copy_async(int64_t addr, Tensor host_out, int64_t index) {
 // the cooperative sampler's sticky barrier-timeout word: its device address (current device)
 int64_t sample_err_addr() { return (int64_t)(intptr_t)kgc::sample_err_addr(); }
 
+// set one device word, stream-ordered (fault-injection tests of the sticky error words)
+void u32_fill_async(int64_t addr, int64_t value) {
+  TORCH_CHECK(hipMemsetD32Async((hipDeviceptr_t)(intptr_t)addr, (int)value, 1, stream()) ==
+              hipSuccess, "u32_fill_async");
+}
+
 // zero one device word, stream-ordered (after its value was copied out)
 void u32_clear_async(int64_t addr) {
   TORCH_CHECK(hipMemsetAsync((void*)(intptr_t)addr, 0, 4, stream()) == hipSuccess,
@@ -1103,6 +1109,7 @@ TORCH_LIBRARY(kgc, m) {
   m.def("debug_errors() -> int", &debug_errors);
   m.def("sample_err_addr() -> int", &sample_err_addr);
   m.def("u32_clear_async(int addr) -> ()", &u32_clear_async);
+  m.def("u32_fill_async(int addr, int value) -> ()", &u32_fill_async);
   m.def("ep_signal_bytes() -> int", &ep_signal_bytes_op);
   m.def("pp_signal_bytes() -> int", &pp_signal_bytes_op);
   m.def("u32_copy_async(int addr, Tensor(a!) host_out, int index) -> ()", &u32_copy_async);

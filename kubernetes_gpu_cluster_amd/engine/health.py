@@ -203,8 +203,8 @@ def watch_parent(poll: float = 1.0, on_fatal: Callable[[int, str], None] = die) 
 
 
 class Heartbeat:
-    """A non-driver rank's heartbeat: bump ``kgc_hb/<rank>`` in the rendezvous TCPStore
-    (served from the driver's process) every ``period`` s.  When a bump fails, or none
+    """A non-driver rank's heartbeat: bump ``kgc_hb/<rank>`` in its replica's TCPStore
+    (``replica_store``: served from the replica driver's process) every ``period`` s.  When a bump fails, or none
     has succeeded for ``timeout`` s (the driver's node vanished without a TCP reset),
     the rank exits (EXIT_PARENT_DEAD) -- unless ``stop()`` was called first (a clean
     shutdown tears the store down right after telling the ranks to exit)."""
@@ -247,6 +247,49 @@ class Heartbeat:
                 self._fatal(f"no heartbeat reached the engine driver for "
                             f"{time.monotonic() - self._ok:.0f} s")
                 return
+
+
+def replica_store(ps):
+    """The heartbeat store of THIS engine replica (tp x pp ranks starting at
+    ``ps.global_base``).  When the process group is exactly one replica this is the
+    rendezvous store.  When several data-parallel replicas share one world, the default
+    store is hosted by global rank 0 (or the torchrun agent) -- the node of replica 0 --
+    so heart-beating into it would tie every replica's ranks to that node: its loss
+    would end all replicas.  Each replica's driver therefore hosts a TCPStore of its own
+    (published under ``kgc/hb_store/<base>`` in the default store) and its ranks connect
+    to it.  Called by every rank of the replica (the driver first creates the store, the
+    others block until it is published).  None without a process group."""
+    import torch.distributed as dist
+    default = rendezvous_store()
+    if default is None:
+        return None
+    n = ps.tp_size * ps.pp_size
+    if dist.get_world_size() == n:
+        return default
+    import datetime
+    base = getattr(ps, "global_base", 0)
+    key = f"kgc/hb_store/{base}"
+    to = datetime.timedelta(seconds=float(os.environ.get("KGC_HB_STORE_TIMEOUT", 1800)))
+    if dist.get_rank() == base:
+        host = _local_ip()
+        st = dist.TCPStore(host, 0, is_master=True, timeout=to, wait_for_workers=False)
+        default.set(key, f"{host}:{st.port}")
+        return st
+    default.wait([key], to)
+    host, port = default.get(key).decode().rsplit(":", 1)
+    return dist.TCPStore(host, int(port), is_master=False, timeout=to)
+
+
+def _local_ip() -> str:
+    """The address this host uses to reach the rendezvous master (MASTER_ADDR)."""
+    import socket
+    master = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    try:
+        with socket.socket(socket.AF_INET, socket.SOCK_DGRAM) as sk:
+            sk.connect((master, 1))
+            return sk.getsockname()[0]
+    except OSError:
+        return "127.0.0.1"
 
 
 def rendezvous_store():

@@ -53,6 +53,7 @@ class StepPlan:
     dev_tok: int           # 1: decode input tokens come from the device-side last_tok table
     tok_bcast: int         # 1: TP ranks take the driver's sampled ids (driver-side logits processing)
     vp: int                # 1: vocab-parallel sampling (TP > 1: no logits gather this step)
+    split: int             # 1: TP prefill overlap (two token halves), decided by the driver
     i64: np.ndarray
     i32: np.ndarray
     f32: np.ndarray
@@ -62,7 +63,7 @@ class StepPlan:
 
     def header(self) -> list[int]:
         return [self.T, self.Tp, self.P, self.D, self.S, self.W, self.B, self.max_ctx,
-                self.dev_tok, self.tok_bcast, self.vp]
+                self.dev_tok, self.tok_bcast, self.vp, self.split]
 
 
 class Layout:
@@ -261,7 +262,10 @@ class ModelRunner:
         i64[L.lidx:L.lidx + P] = qsl[1:] - 1
         self.hf.numpy()[: 2 * self.L.Smax] = 1.0
         i64[L.sslots:L.sslots + P] = 0
-        plan = StepPlan(T, T, P, 0, P, len(ws), 0, 0, 0, 0, int(self.vp), i64, i32, self.hf.numpy())
+        # (no TP overlap split in the profiling step: every rank runs it from its own
+        # copy, and the unsplit step's activations are the larger ones)
+        plan = StepPlan(T, T, P, 0, P, len(ws), 0, 0, 0, 0, int(self.vp), 0, i64, i32,
+                        self.hf.numpy())
         self.run(plan)
 
     # ------------------------------------------------------------------ packing (driver)
@@ -364,8 +368,12 @@ class ModelRunner:
         vp = int(self.vp and lp is None and proc is None
                  and all((s.params.top_k <= 0 or s.params.top_k >= V) and s.params.top_p >= 1.0
                          for s in samplers))
+        # the TP prefill overlap split is decided HERE, once, and carried in the header:
+        # ranks deciding it from their own environment could split differently and issue
+        # all-reduces of different sizes (a hang or a corrupt step)
+        split = int(P > 0 and D == 0 and self._overlap_ok(Tp))
         return StepPlan(T, Tp, P, D, S, W, B, max_ctx, int(device_tokens and D > 0), bcast, vp,
-                        i64, i32, f32, lp, proc, proc_init), samplers
+                        split, i64, i32, f32, lp, proc, proc_init), samplers
 
     # ------------------------------------------------------------------ execution (all ranks)
     def _upload(self, plan: StepPlan) -> None:
@@ -381,7 +389,7 @@ class ModelRunner:
             self.d32.copy_(torch.from_numpy(plan.i32))
             self.df.copy_(torch.from_numpy(plan.f32))
 
-    def _meta(self, T, Tp, P, D, W, max_ctx, z=None) -> AttnMetadata:
+    def _meta(self, T, Tp, P, D, W, max_ctx, z=None, split: int = 0) -> AttnMetadata:
         L, mb = self.L, self.max_blocks
         d32 = self.d32
         m = AttnMetadata(slot_mapping=self.d64[L.slots:L.slots + T], num_prefill_tokens=Tp,
@@ -398,14 +406,15 @@ class ModelRunner:
             m.decode_workspace = self.workspace
             nkv = self.model.local_kv_heads()
             m.decode_grid_z = z if z is not None else ops.decode_grid_z(D, nkv, max_ctx)
-        elif P and self._overlap_ok(Tp):
+        elif P and split:
             m.split = self._split_prefill(Tp, P)
         return m
 
     # ------------------------------------------------------------------ TP prefill overlap
     def _overlap_ok(self, Tp: int) -> bool:
         """Large prefill-only steps at TP > 1 run as two token halves whose all-reduces
-        overlap the other half's GEMMs (``LlamaForCausalLM._forward_tp_overlap``).
+        overlap the other half's GEMMs (``LlamaForCausalLM._forward_tp_overlap``).  The
+        DRIVER evaluates this (build_plan) and every rank follows the plan's ``split``.
         KGC_TP_OVERLAP=0 turns it off; KGC_TP_OVERLAP_MIN_TOKENS (default 2048) is the
         smallest step it applies to (below it the all-reduces take the xGMI kernel)."""
         if self.ps.tp_size == 1 or os.environ.get("KGC_TP_OVERLAP", "1") == "0":
@@ -522,7 +531,7 @@ class ModelRunner:
         else:
             T = plan.T if not plan.B else plan.B
             D = plan.D if not plan.B else plan.B
-            meta = self._meta(T, plan.Tp, plan.P, D, plan.W, plan.max_ctx)
+            meta = self._meta(T, plan.Tp, plan.P, D, plan.W, plan.max_ctx, split=plan.split)
             out = self._forward(T, meta, hidden_in)
             self.stats["eager_steps"] += 1
             if not self.model.last:

@@ -37,7 +37,7 @@ from .config import EngineConfig
 from .model_runner import ModelRunner, StepPlan
 
 CMD_STEP, CMD_PROFILE, CMD_INIT_CACHE, CMD_CAPTURE, CMD_EXIT = 1, 2, 3, 4, 5
-N_HDR = 11                  # StepPlan.header() fields
+N_HDR = 12                  # StepPlan.header() fields
 
 
 def default_max_model_len(cfg: EngineConfig) -> int:
@@ -64,12 +64,14 @@ class Worker:
         # (engine/health.py): the driver notices a rank on another node dying, and this
         # rank notices the driver's node dying
         self.heartbeat = None
-        if self.ps.tp_size * self.ps.pp_size > 1 and dist.is_initialized() and \
-                dist.get_rank() != getattr(self.ps, "global_base", 0):
-            from .health import Heartbeat, rendezvous_store
-            store = rendezvous_store()
-            if store is not None:
-                self.heartbeat = Heartbeat(store, dist.get_rank()).start()
+        self.hb_store = None
+        if self.ps.tp_size * self.ps.pp_size > 1 and dist.is_initialized():
+            # one store per replica, hosted by its driver (engine/health.py replica_store);
+            # created before the weights load, so no rank waits on another's loading
+            from .health import Heartbeat, replica_store
+            self.hb_store = replica_store(self.ps)
+            if self.hb_store is not None and dist.get_rank() != getattr(self.ps, "global_base", 0):
+                self.heartbeat = Heartbeat(self.hb_store, dist.get_rank()).start()
         mcfg, _ = resolve_model(cfg.model)
         self.dtype = cfg.torch_dtype(torch.bfloat16 if mcfg.arch != "opt" else torch.float16)
         if dev.type == "cpu" and self.dtype == torch.float16:
@@ -201,9 +203,25 @@ def _bcast_plan_blobs(runner: ModelRunner, plan_hdr: list[int]) -> None:
         dist.broadcast(t, src=src, group=s.cpu_group)
 
 
-def _send_tokens_to_driver(tokens: torch.Tensor) -> None:
+def _send_tokens_to_driver(tokens: torch.Tensor, sampler_health=None) -> None:
+    """The last PP stage's TP leader hands the sampled ids to the driver, with ONE extra
+    trailing value: this stage's sampler error flag for the step (the driver's own word
+    belongs to stage 0, which never samples at PP > 1)."""
     s = get_state()
-    dist.send(tokens.cpu(), dst=getattr(s, "global_base", 0), group=s.cpu_group)
+    slot = sampler_health.enqueue_err_read() if sampler_health is not None else None
+    host = tokens.cpu()              # stream-ordered: the flag copy above has landed too
+    flag = int(sampler_health.failed(slot)) if slot is not None else 0
+    msg = torch.cat([host.to(torch.int64), torch.tensor([flag], dtype=torch.int64)])
+    dist.send(msg, dst=getattr(s, "global_base", 0), group=s.cpu_group)
+
+
+def _tokens_from_last_stage(t: torch.Tensor) -> list[int]:
+    """Driver side of ``_send_tokens_to_driver``: the ids, or SamplerFailed."""
+    vals = t.tolist()
+    if vals[-1]:
+        raise ops.SamplerFailed("top-k / top-p sampler on the last pipeline stage: a row's "
+                                "barrier timed out; the step's tokens are invalid")
+    return vals[:-1]
 
 
 def _release_custom_allreduce() -> None:
@@ -242,7 +260,7 @@ def worker_loop(worker: Worker) -> None:
             plan = StepPlan(*hdr, r.h64.numpy(), r.h32.numpy(), r.hf.numpy())
             out = worker.run(plan)
             if last_pp_leader and out is not None:
-                _send_tokens_to_driver(out)
+                _send_tokens_to_driver(out, worker.sampler_health)
 
 
 class LocalExecutor:
@@ -265,20 +283,20 @@ class LocalExecutor:
     def execute(self, plan: StepPlan) -> list[int]:
         out = self.worker.run(plan)
         sh = self.worker.sampler_health
-        if sh is not None:
-            sh.enqueue_err_read()
+        slot = sh.enqueue_err_read() if sh is not None else None
         res = out.tolist()              # synchronises: the error word has landed
         if sh is not None:
-            sh.raise_if_failed()
+            sh.raise_if_failed(slot)
         return res
 
     def execute_async(self, plan: StepPlan) -> "TokenFuture":
         out = self.worker.run(plan)
         sh = self.worker.sampler_health
-        if sh is not None:
-            sh.enqueue_err_read()       # ahead of the token copy: its event covers both
+        # ahead of the token copy (its event covers both), into this step's own slot
+        slot = sh.enqueue_err_read() if sh is not None else None
+        done = (lambda: sh.raise_if_failed(slot)) if sh is not None else None
         return TokenFuture(*self.runner.tokens_to_host(out), lp=self.runner.take_logprobs(),
-                           on_done=sh.raise_if_failed if sh is not None else None)
+                           on_done=done)
 
     @property
     def supports_async(self) -> bool:
@@ -328,9 +346,9 @@ class PipelinedTokenFuture:
     def result(self) -> list[int]:
         if self.values is None:
             self.work.wait()
-            self.values = self.buf.tolist()
             done, self._on_done = self._on_done, None
             done()
+            self.values = _tokens_from_last_stage(self.buf)
         return self.values
 
     def logprobs(self) -> dict:
@@ -347,12 +365,14 @@ class _DistExecutorBase:
         an async copy of the xGMI all-reduce error word checked when the step completes."""
         if begin and self.watchdog is not None:
             self.watchdog.step_begin()
-        # sticky error words of the peer-memory collectives (xGMI all-reduce, EP exchange)
+        # sticky error words of the peer-memory collectives (xGMI all-reduce, EP exchange),
+        # and this rank's sampler word when it samples (PP > 1: the last stage reports its
+        # own with the tokens, _send_tokens_to_driver)
+        sh = self.worker.sampler_health if get_state().is_last_pp else None
         checks = [c for c in (comm.get_custom_allreduce(), getattr(self.worker, "ep_a2a", None),
-                              self.worker.runner.pp_link, self.worker.sampler_health)
+                              self.worker.runner.pp_link, sh)
                   if c is not None]
-        for c in checks:
-            c.enqueue_err_read()
+        slots = [c.enqueue_err_read() for c in checks]
         # the error words land in pinned host memory behind this event: done() reads them
         # only after it, so a failure of this step is reported with this step's tokens
         ev = None
@@ -365,8 +385,8 @@ class _DistExecutorBase:
                 ev.synchronize()
             if self.watchdog is not None:
                 self.watchdog.step_end()
-            for c in checks:
-                c.raise_if_failed()
+            for c, slot in zip(checks, slots):
+                c.raise_if_failed(slot)
         return done
 
     @property
@@ -407,7 +427,7 @@ class _DistExecutorBase:
         # the error-word copies go behind this micro-batch's kernels, not ahead of them
         done = self._step_launched(begin=False)
         s = get_state()
-        t = torch.empty(plan.S, dtype=torch.int64)
+        t = torch.empty(plan.S + 1, dtype=torch.int64)      # ids + the last stage's flag
         src = getattr(s, "global_base", 0) + (s.pp_size - 1) * s.tp_size
         return PipelinedTokenFuture(dist.irecv(t, src=src, group=s.cpu_group), t, done)
 
@@ -431,13 +451,14 @@ class _DistExecutorBase:
         done = self._step_launched()
         s = get_state()
         if s.pp_size > 1:
-            t = torch.empty(plan.S, dtype=torch.int64)
+            t = torch.empty(plan.S + 1, dtype=torch.int64)  # ids + the last stage's flag
             src = getattr(s, "global_base", 0) + (s.pp_size - 1) * s.tp_size
             dist.recv(t, src=src, group=s.cpu_group)
-            res = t.tolist()
+            done()
+            res = _tokens_from_last_stage(t)
         else:
             res = out.tolist()
-        done()
+            done()
         if self.watchdog is not None:
             self.watchdog.step_end()
         return res
@@ -461,23 +482,23 @@ class ExternalExecutor(_DistExecutorBase):
 
     def __init__(self, worker: Worker):
         self.worker = worker
-        self.watchdog = _remote_watchdog([])
+        self.watchdog = _remote_watchdog([], worker)
 
 
-def _watch_heartbeats(wd: RankWatchdog) -> None:
-    """Follow the heartbeats of this engine's other ranks (every rank but the driver)."""
-    from .health import rendezvous_store
+def _watch_heartbeats(wd: RankWatchdog, worker: "Worker") -> None:
+    """Follow the heartbeats of this engine replica's other ranks (every rank but the
+    driver), in the replica's own store (engine/health.py replica_store)."""
     s = get_state()
-    store = rendezvous_store()
+    store = worker.hb_store
     n = s.tp_size * s.pp_size
     if store is not None and n > 1:
         base = getattr(s, "global_base", 0)
         wd.watch_heartbeats(store, range(base + 1, base + n))
 
 
-def _remote_watchdog(procs) -> RankWatchdog:
+def _remote_watchdog(procs, worker: "Worker") -> RankWatchdog:
     wd = RankWatchdog(procs)
-    _watch_heartbeats(wd)
+    _watch_heartbeats(wd, worker)
     return wd.start()
 
 
@@ -538,7 +559,7 @@ class MultiprocExecutor(_DistExecutorBase):
         os.environ["RANK"] = "0"
         os.environ["LOCAL_RANK"] = "0"
         self.worker = Worker(cfg, rank=0, local_device=0)
-        _watch_heartbeats(self.watchdog)
+        _watch_heartbeats(self.watchdog, self.worker)
 
     def shutdown(self) -> None:
         super().shutdown()

@@ -66,10 +66,15 @@ class RequestStream:
     whose task raised) -- the request was submitted eagerly, so without this it would
     keep decoding to max_tokens in a batch slot nobody reads."""
 
-    def __init__(self, request_id: str, q: asyncio.Queue, on_close):
+    def __init__(self, request_id: str, q: asyncio.Queue, on_close, on_drop=None):
         self.request_id = request_id
         self._q = q
         self._on_close = on_close           # on_close(request_id, abort: bool)
+        # on_drop(request_id): the finalizer's abort -- it must take NO lock (a cyclic GC
+        # pass can run __del__ on a thread that already holds the engine client's send
+        # lock or a queue's mutex, e.g. while pickling inside _send): the owner only
+        # records the id lock-free and aborts it later from a normal context
+        self._on_drop = on_drop
         self._closed = False
 
     def __aiter__(self):
@@ -110,8 +115,12 @@ class RequestStream:
         self.close()
 
     def __del__(self):
+        if self._closed:
+            return
+        self._closed = True
         try:
-            self.close()
+            if self._on_drop is not None:
+                self._on_drop(self.request_id)
         except Exception:  # noqa: BLE001 - interpreter shutdown
             pass
 
@@ -126,7 +135,9 @@ class AsyncLLMEngine:
         self.cfg = cfg
         self.engine = engine or LLMEngine(cfg)
         self._new: queue.Queue = queue.Queue()
-        self._aborts: queue.Queue = queue.Queue()
+        # request ids to abort: a deque (append / popleft are atomic and lock-free), so a
+        # stream finalizer can add to it from any context (RequestStream.__del__)
+        self._aborts: collections.deque = collections.deque()
         self._streams: dict[str, tuple[asyncio.AbstractEventLoop, asyncio.Queue]] = {}
         self._wake = threading.Event()
         self._stop = False
@@ -168,12 +179,8 @@ class AsyncLLMEngine:
                         eng.add_request(ids, params, request_id=rid, arrival_time=t)
                     except Exception as e:  # noqa: BLE001 - reported to the request
                         self._push(rid, e)
-                while True:
-                    try:
-                        rid = self._aborts.get_nowait()
-                    except queue.Empty:
-                        break
-                    eng.abort(rid)
+                while self._aborts:
+                    eng.abort(self._aborts.popleft())
                 if eng.has_unfinished():
                     t0 = time.monotonic()
                     outs = eng.step()
@@ -204,15 +211,21 @@ class AsyncLLMEngine:
         self._streams[request_id] = (loop, q)
         self._new.put((request_id, prompt_ids, params, time.monotonic()))
         self._wake.set()
-        return RequestStream(request_id, q, self._close_stream)
+        return RequestStream(request_id, q, self._close_stream, self._drop_stream)
 
     def _close_stream(self, request_id: str, abort: bool) -> None:
         self._streams.pop(request_id, None)
         if abort:
             self.abort(request_id)
 
+    def _drop_stream(self, request_id: str) -> None:
+        """Finalizer path: lock-free (dict pop and deque append); the engine thread picks
+        the abort up within one loop iteration (it waits at most 50 ms when idle)."""
+        self._streams.pop(request_id, None)
+        self._aborts.append(request_id)
+
     def abort(self, request_id: str) -> None:
-        self._aborts.put(request_id)
+        self._aborts.append(request_id)
         self._wake.set()
 
     async def metrics_text(self) -> str:

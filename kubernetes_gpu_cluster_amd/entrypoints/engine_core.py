@@ -282,6 +282,9 @@ class EngineCoreClient:
         self.error: Optional[str] = None
         self._streams: dict[str, _Stream] = {}
         self._send_lock = threading.Lock()
+        # streams dropped unfinished (RequestStream.__del__): aborted from a normal context,
+        # never from the finalizer, which may run while this thread holds _send_lock
+        self._dropped: collections.deque = collections.deque()
         self._metrics_waiters: dict[int, tuple] = {}
         self._tokens = itertools.count()
         self._reader = threading.Thread(target=self._read_loop, name="kgc-core-reader", daemon=True)
@@ -293,8 +296,12 @@ class EngineCoreClient:
         return self
 
     def _send(self, msg) -> None:
+        """msg None: only the aborts of dropped streams."""
         with self._send_lock:
-            self._conn.send(msg)
+            while self._dropped:
+                self._conn.send(("abort", self._dropped.popleft()))
+            if msg is not None:
+                self._conn.send(msg)
 
     def _read_loop(self) -> None:
         try:
@@ -347,12 +354,31 @@ class EngineCoreClient:
         q: asyncio.Queue = asyncio.Queue()
         self._streams[request_id] = _Stream(loop, q, list(prompt_ids))
         self._send(("add", request_id, list(prompt_ids), params, time.monotonic()))
-        return RequestStream(request_id, q, self._close_stream)
+        return RequestStream(request_id, q, self._close_stream, self._drop_stream)
 
     def _close_stream(self, request_id: str, abort: bool) -> None:
         self._streams.pop(request_id, None)
         if abort and self.is_alive:
             self.abort(request_id)
+
+    def _drop_stream(self, request_id: str) -> None:
+        """Finalizer path, lock-free: record the id and schedule the abort on the stream's
+        event loop (call_soon_threadsafe appends to the loop's ready deque and writes its
+        self-pipe -- no lock); _send also drains the backlog before its next message."""
+        st = self._streams.pop(request_id, None)
+        self._dropped.append(request_id)
+        if st is not None:
+            try:
+                st.loop.call_soon_threadsafe(self._drain_dropped)
+            except RuntimeError:        # loop closed: the next _send drains it
+                pass
+
+    def _drain_dropped(self) -> None:
+        if self._dropped and self.is_alive:
+            try:
+                self._send(None)
+            except OSError:
+                pass
 
     def abort(self, request_id: str) -> None:
         try:

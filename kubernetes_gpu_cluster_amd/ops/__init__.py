@@ -364,22 +364,38 @@ class SamplerFailed(RuntimeError):
 
 class SamplerHealth:
     """The cooperative sampler's sticky error word (sampling.hip ``g_smp_err``), checked
-    like the peer-memory collectives' words: ``enqueue_err_read`` queues a copy into
-    pinned memory and a clear behind the step, ``raise_if_failed`` (after the step
-    completed) raises instead of letting its tokens be served."""
+    like the peer-memory collectives' words: ``enqueue_err_read`` queues a copy into a
+    pinned host slot and a clear of the device word behind the step, and returns the slot;
+    ``raise_if_failed(slot)`` (after that step completed) raises instead of letting its
+    tokens be served.  Every in-flight step copies into its OWN slot (a ring): with async
+    scheduling step N + 1 is launched before N's tokens are read, and N + 1's copy of the
+    just-cleared word must not overwrite N's flag."""
+
+    SLOTS = 8      # > steps in flight (async: 2; PP: one per stage, <= 8)
 
     def __init__(self, device: torch.device):
         with torch.cuda.device(device):
             self.addr = int(_k().sample_err_addr())
-        self.host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self.host = torch.zeros(self.SLOTS, dtype=torch.int32, pin_memory=True)
+        self._next = 0
 
-    def enqueue_err_read(self) -> None:
-        _k().u32_copy_async(self.addr, self.host, 0)
+    def enqueue_err_read(self) -> int:
+        slot = self._next
+        self._next = (slot + 1) % self.SLOTS
+        self.host[slot] = 0
+        _k().u32_copy_async(self.addr, self.host, slot)
         _k().u32_clear_async(self.addr)
+        return slot
 
-    def raise_if_failed(self) -> None:
-        if int(self.host[0]):
-            self.host[0] = 0
+    def failed(self, slot: int) -> bool:
+        """The flag of `slot` (its step must have completed)."""
+        return bool(int(self.host[slot]))
+
+    def raise_if_failed(self, slot: Optional[int] = None) -> None:
+        if slot is None:
+            slot = (self._next - 1) % self.SLOTS
+        if int(self.host[slot]):
+            self.host[slot] = 0
             raise SamplerFailed("top-k / top-p sampler: a row's workgroups were not co-resident "
                                 "and its barrier timed out; the step's tokens are invalid")
 

@@ -157,7 +157,7 @@ class CustomAllReduce:
             self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         torch.ops.kgc.ar_err_copy_async(self.sig[self.rank], self._err_host)
 
-    def raise_if_failed(self) -> None:
+    def raise_if_failed(self, slot=None) -> None:
         """After the step that queued ``enqueue_err_read`` completed: raise on a timed-out
         barrier -- the step summed stale peer data, so its tokens must not be served."""
         if self._err_host is not None and int(self._err_host[0]):

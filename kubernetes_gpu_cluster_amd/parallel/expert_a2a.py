@@ -111,7 +111,7 @@ class ExpertAllToAll:
             self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         torch.ops.kgc.ep_err_copy_async(self.sig[self.rank], self._err_host)
 
-    def raise_if_failed(self) -> None:
+    def raise_if_failed(self, slot=None) -> None:
         h = self._err_host
         if h is not None and int(h[0]):
             raise AllReduceFailed(f"EP all-to-all: peers {bin(int(h[0]))} never arrived "

@@ -104,7 +104,7 @@ class PipelineHandoff:
         k.u32_copy_async(self.own_send_sig + self._ERR_OFFSET, self._err_host, 0)
         k.u32_copy_async(self.own_recv_sig + self._ERR_OFFSET, self._err_host, 1)
 
-    def raise_if_failed(self) -> None:
+    def raise_if_failed(self, slot=None) -> None:
         if self._err_host is not None and int(self._err_host.sum()):
             raise AllReduceFailed("PP handoff: the neighbouring stage never arrived "
                                   "(a PP rank is dead or wedged); the engine stops")

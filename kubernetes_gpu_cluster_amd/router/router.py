@@ -401,10 +401,15 @@ def run_workers(workers: int, shared: SharedOutstanding, serve) -> None:
         pid = os.fork()
         if pid == 0:
             shared.row = w
+            rc = 1                      # a worker that raises (bind failure, crash) exits 1
             try:
                 serve(shared)
+                rc = 0
+            except BaseException:       # noqa: BLE001 - reported, then a non-zero exit
+                import traceback
+                traceback.print_exc()
             finally:
-                os._exit(0)
+                os._exit(rc)
         pids.append(pid)
 
     def stop(signum, frame):

@@ -278,6 +278,33 @@ def test_stream_include_usage(client):
             assert all("usage" not in json.loads(e) for e in events[:-2])
 
 
+def test_stream_finalizer_takes_no_lock():
+    """A stream finalizer can run in the middle of EngineCoreClient._send (a cyclic GC pass
+    while pickling a message, on the thread that holds _send_lock): __del__ must not take
+    that lock (it would deadlock the event loop).  The abort is recorded lock-free and
+    sent from a normal context afterwards."""
+    import asyncio
+    import gc
+    from kubernetes_gpu_cluster_amd.engine.sequence import SamplingParams
+    from kubernetes_gpu_cluster_amd.entrypoints.engine_core import EngineCoreClient
+    eng = EngineCoreClient(_cfg())
+
+    async def body():
+        g = eng.generate([5, 6, 7], SamplingParams(max_tokens=200, ignore_eos=True), "drop-2")
+        with eng._send_lock:          # as if the GC ran inside _send on this thread
+            del g
+            gc.collect()              # returns: the finalizer only queued the abort
+        for _ in range(100):          # the scheduled drain sends it
+            if not eng._dropped:
+                break
+            await asyncio.sleep(0.02)
+        assert not eng._dropped
+    try:
+        asyncio.run(asyncio.wait_for(body(), 30))
+    finally:
+        eng.shutdown()
+
+
 @pytest.mark.parametrize("kind", ["thread", "core-process"])
 def test_unstarted_stream_aborts_request(kind):
     """A request submitted eagerly whose output stream is dropped before the first chunk

@@ -64,7 +64,8 @@ def _logits(rank, name, tp, pp, moe_mode="tp"):
         bm.allocate(seq, len(prompt))
         plan, _ = runner.build_plan([(seq, len(prompt))], [], bm.table)
         runner._upload(plan)
-        meta = runner._meta(plan.T, plan.Tp, plan.P, plan.D, plan.W, plan.max_ctx)
+        meta = runner._meta(plan.T, plan.Tp, plan.P, plan.D, plan.W, plan.max_ctx,
+                            split=plan.split)
         with torch.inference_mode():
             if s.is_first_pp:
                 h, r = runner._forward(plan.T, meta)
@@ -125,7 +126,8 @@ def _multi_logits(rank, name, tp, overlap):
     def run(prefills, decodes):
         plan, _ = runner.build_plan(prefills, decodes, bm.table)
         runner._upload(plan)
-        meta = runner._meta(plan.T, plan.Tp, plan.P, plan.D, plan.W, plan.max_ctx)
+        meta = runner._meta(plan.T, plan.Tp, plan.P, plan.D, plan.W, plan.max_ctx,
+                            split=plan.split)
         splits.append(None if meta.split is None else meta.split[0])
         with torch.inference_mode():
             h = runner._forward(plan.T, meta)

@@ -402,3 +402,18 @@ def test_prefill_first_gap_bound(monkeypatch):
     clock[0] += 0.2
     sc.add(Sequence("c", list(range(3, 19)), sp, None, 256))
     assert [s.request_id for s in sc.schedule().decodes] == ["a"]
+
+
+def test_step_plan_header_carries_the_tp_overlap_split():
+    """The TP prefill overlap split is decided once by the driver (build_plan) and sent in
+    the broadcast header, so every TP rank splits the same way whatever its environment;
+    the header length matches what the worker loop unpacks."""
+    import numpy as np
+    from kubernetes_gpu_cluster_amd.engine.model_runner import StepPlan
+    from kubernetes_gpu_cluster_amd.engine.worker import N_HDR
+    z = np.zeros(1)
+    p = StepPlan(40, 40, 2, 0, 2, 3, 0, 0, 0, 0, 1, 1, z, z, z)
+    h = p.header()
+    assert len(h) == N_HDR and h[-1] == 1
+    q = StepPlan(*h, z, z, z)
+    assert q.split == 1 and q.vp == 1 and q.T == 40

@@ -294,3 +294,40 @@ def test_driver_death_ends_worker_node(tmp_path):
         _kill_tree(server, worker)
         for f in logs:
             f.close()
+
+
+def _replica_store_rank(rank, world, port, outdir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from kubernetes_gpu_cluster_amd.parallel.state import init_parallel
+    ps = init_parallel(2, 1)                 # 2 ranks per replica -> 2 replicas in 4 ranks
+    st = health.replica_store(ps)
+    default = health.rendezvous_store()
+    base = ps.global_base
+    if rank == base:
+        dist.barrier()                       # the worker of this replica has beaten
+        beats = st.add(f"kgc_hb/{rank + 1}", 0)
+        in_default = default.add(f"kgc_hb/{rank + 1}", 0)
+        with open(os.path.join(outdir, f"r{rank}"), "w") as f:
+            json.dump({"own": st is not default, "beats": beats, "in_default": in_default}, f)
+    else:
+        hb = health.Heartbeat(st, rank, period=0.02, timeout=30, on_fatal=lambda c, m: None).start()
+        time.sleep(0.3)
+        hb.stop()
+        dist.barrier()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_replicas_heartbeat_into_their_own_driver(tmp_path):
+    """Data-parallel replicas sharing one world: each replica's ranks heart-beat into a
+    store hosted by THAT replica's driver, not into the rendezvous store of global rank 0
+    -- so the loss of replica 0's node cannot end replica 1."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_replica_store_rank, args=(4, _port(), str(tmp_path)), nprocs=4,
+                       join=True, start_method="spawn")
+    r2 = json.load(open(tmp_path / "r2"))
+    assert r2["own"] and r2["beats"] > 0 and r2["in_default"] == 0, r2
+    r0 = json.load(open(tmp_path / "r0"))
+    assert r0["own"] and r0["beats"] > 0, r0

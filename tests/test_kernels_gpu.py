@@ -1033,10 +1033,25 @@ def test_sampler_health_word(gpu):
     topp = torch.full((B,), 0.9, device=gpu)
     seeds = torch.arange(B, dtype=torch.int64, device=gpu)
     ops.sample(logits, temp, topk, topp, seeds)
-    sh.enqueue_err_read()
+    slot = sh.enqueue_err_read()
     torch.cuda.synchronize()
-    sh.raise_if_failed()                          # healthy step: no error
-    sh.host[0] = 1
+    sh.raise_if_failed(slot)                      # healthy step: no error
+    sh.host[slot] = 1
     with pytest.raises(ops.SamplerFailed):
-        sh.raise_if_failed()
-    assert int(sh.host[0]) == 0
+        sh.raise_if_failed(slot)
+    assert int(sh.host[slot]) == 0
+
+
+def test_sampler_health_async_steps_keep_their_flags(gpu):
+    """Async scheduling launches step N + 1 before step N's tokens are read: step N's
+    failure (its word set) must still be reported for N, although N + 1's copy of the
+    then-cleared word lands later -- each step copies into its own host slot."""
+    k = torch.ops.kgc
+    sh = ops.SamplerHealth(gpu)
+    k.u32_fill_async(sh.addr, 1)                  # step N: the barrier timed out
+    slot_n = sh.enqueue_err_read()                # ... its copy, then the clear
+    slot_n1 = sh.enqueue_err_read()               # step N + 1: healthy (word now 0)
+    torch.cuda.synchronize()                      # both copies landed (N + 1's last)
+    sh.raise_if_failed(slot_n1)                   # N + 1 is fine ...
+    with pytest.raises(ops.SamplerFailed):        # ... and N is still reported
+        sh.raise_if_failed(slot_n)

@@ -80,7 +80,8 @@ def _engine_logits(model, runner, prompt, chunks, decode_tokens):
     def run(prefills, decodes):
         plan, _ = runner.build_plan(prefills, decodes, bm.table)
         runner._upload(plan)
-        meta = runner._meta(plan.T, plan.Tp, plan.P, plan.D, plan.W, plan.max_ctx)
+        meta = runner._meta(plan.T, plan.Tp, plan.P, plan.D, plan.W, plan.max_ctx,
+                            split=plan.split)
         with torch.inference_mode():
             h = runner._forward(plan.T, meta)
             return model.compute_logits(h)

@@ -247,3 +247,29 @@ async def _multiworker_scenario(nbe=4, per=64, workers=3):
 
 def test_router_workers_share_load_exactly():
     asyncio.run(_multiworker_scenario())
+
+
+def test_run_workers_exits_nonzero_when_a_worker_raises():
+    import os
+    """A forked router worker whose serve() raises (bind failure, crash) exits 1, and the
+    parent stops the others and exits non-zero -- never a silent 0."""
+    import subprocess
+    import sys
+    code = r'''
+import os, sys, time
+from kubernetes_gpu_cluster_amd.router.router import run_workers, SharedOutstanding
+
+def serve(shared):
+    if shared.row == 1:
+        raise OSError("address already in use")
+    time.sleep(30)
+
+try:
+    run_workers(2, SharedOutstanding(2), serve)
+except SystemExit as e:
+    sys.exit(e.code)
+'''
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 1, (r.returncode, r.stderr[-2000:])
+    assert "address already in use" in r.stderr
