@@ -163,9 +163,17 @@ void check_kv(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, int
   check_same_dev(q, v_cache, "v_cache");
 }
 
+// tickets: int32 >= B * nkv, zeroed once (K1w's in-launch merge re-arms them)
+static int* decode_tickets(const Tensor& tickets, int64_t B, int64_t nkv, const Tensor& ref) {
+  TORCH_CHECK(tickets.scalar_type() == at::kInt && tickets.is_contiguous() &&
+              tickets.numel() >= B * nkv && tickets.device() == ref.device(),
+              "decode tickets: int32 [>= B * nkv] on the kernel's device");
+  return tickets.data_ptr<int>();
+}
+
 void paged_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables,
                   Tensor ctx_lens, Tensor max_logits, Tensor exp_sums, Tensor tmp_out,
-                  int64_t Z, double scale, double k_scale, double v_scale) {
+                  Tensor tickets, int64_t Z, double scale, double k_scale, double v_scale) {
   check_gpu(q, "q");
   c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   TORCH_CHECK(q.dim() == 3 && q.is_contiguous(), "q [B, nq, d] contiguous");
@@ -190,7 +198,9 @@ void paged_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor b
                            v_cache.data_ptr(), block_tables.data_ptr<int>(),
                            (int)block_tables.stride(0), ctx_lens.data_ptr<int>(),
                            max_logits.data_ptr<float>(), exp_sums.data_ptr<float>(),
-                           tmp_out.data_ptr<float>(), (int)B, (int)nq, (int)k_cache.size(1),
+                           tmp_out.data_ptr<float>(),
+                           decode_tickets(tickets, B, k_cache.size(1), q),
+                           (int)B, (int)nq, (int)k_cache.size(1),
                            (int)d, log2_exact(k_cache.size(2), "block_size"), (int)Zmax, (int)Z,
                            (float)scale, k_cache.scalar_type() == at::kFloat8_e4m3fn,
                            (float)k_scale, (float)v_scale, (int)k_cache.size(0), stream());
@@ -201,7 +211,8 @@ void paged_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor b
 void paged_decode_rope(Tensor out, Tensor qkv, Tensor positions, Tensor cos_sin, Tensor k_cache,
                        Tensor v_cache, Tensor slot_mapping, std::optional<Tensor> q_norm_w,
                        std::optional<Tensor> k_norm_w, Tensor block_tables, Tensor ctx_lens,
-                       Tensor max_logits, Tensor exp_sums, Tensor tmp_out, int64_t nq,
+                       Tensor max_logits, Tensor exp_sums, Tensor tmp_out, Tensor tickets,
+                       int64_t nq,
                        int64_t Z, double scale, double eps, bool use_rope, double k_scale,
                        double v_scale) {
   check_gpu(qkv, "qkv");
@@ -268,7 +279,8 @@ void paged_decode_rope(Tensor out, Tensor qkv, Tensor positions, Tensor cos_sin,
                                 v_cache.data_ptr(), block_tables.data_ptr<int>(),
                                 (int)block_tables.stride(0), ctx_lens.data_ptr<int>(),
                                 max_logits.data_ptr<float>(), exp_sums.data_ptr<float>(),
-                                tmp_out.data_ptr<float>(), (int)B, (int)nq, (int)nkv, (int)d,
+                                tmp_out.data_ptr<float>(), decode_tickets(tickets, B, nkv, out),
+                                (int)B, (int)nq, (int)nkv, (int)d,
                                 log2_exact(k_cache.size(2), "block_size"), (int)Zmax, (int)Z,
                                 (float)scale, k_cache.scalar_type() == at::kFloat8_e4m3fn,
                                 (float)k_scale, (float)v_scale, (int)k_cache.size(0), stream());
@@ -1052,12 +1064,13 @@ TORCH_LIBRARY(kgc, m) {
         "float v_scale=1.0) -> ()");
   m.def("paged_decode(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
         "Tensor block_tables, Tensor ctx_lens, Tensor(b!) max_logits, Tensor(c!) exp_sums, "
-        "Tensor(d!) tmp_out, int Z, float scale, float k_scale=1.0, float v_scale=1.0) -> ()");
+        "Tensor(d!) tmp_out, Tensor(e!) tickets, int Z, float scale, float k_scale=1.0, "
+        "float v_scale=1.0) -> ()");
   m.def("paged_decode_rope(Tensor(a!) out, Tensor qkv, Tensor positions, Tensor cos_sin, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor slot_mapping, Tensor? q_norm_w, "
         "Tensor? k_norm_w, Tensor block_tables, Tensor ctx_lens, Tensor(d!) max_logits, "
-        "Tensor(e!) exp_sums, Tensor(f!) tmp_out, int nq, int Z, float scale, float eps, "
-        "bool use_rope, float k_scale=1.0, float v_scale=1.0) -> ()");
+        "Tensor(e!) exp_sums, Tensor(f!) tmp_out, Tensor(g!) tickets, int nq, int Z, "
+        "float scale, float eps, bool use_rope, float k_scale=1.0, float v_scale=1.0) -> ()");
   m.def("prefill_attention(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
         "Tensor block_tables, Tensor query_start_loc, Tensor seq_lens, Tensor work_seq, "
         "Tensor work_mblk, float scale, float k_scale=1.0, float v_scale=1.0) -> ()");

@@ -33,7 +33,8 @@ namespace kgc {
 
 constexpr int AR_MAX_RANKS = 8;
 constexpr int AR_MAX_BLOCKS = 64;    // one-shot / two-shot / one-shot fused grid
-constexpr int AR2_BLOCKS = 256;      // row-segmented two-shot fused grid (one row per block)
+constexpr int AR2_BLOCKS = 128;      // row-segmented two-shot fused grid (2 rows per block at
+                                     // M = 256; 4 ranks' grids must fit one GPU in the tests)
 constexpr int AR_THREADS = 512;
 
 struct ArSignal {
@@ -319,8 +320,10 @@ __global__ __launch_bounds__(AR_THREADS) void allreduce_rms_emu_kernel(
 // ---- row-segmented TWO-SHOT fused all-reduce + residual add + RMSNorm (TP = 4 / 8
 // decode at real batch sizes: 256 rows x 8192 = 4 MB per call, 16x the one-shot cap).
 //   copy-in:  block b writes its rows {row % AR2_BLOCKS == b} into the own IPC buffer;
-//   reduce:   rank r owns the rows with row % NR == r; block b sums ITS owned rows over
-//             all peers (rounded to T: the all-reduce output) in place; barrier;
+//   reduce:   row `row` is owned by rank (row + row / AR2_BLOCKS) % NR -- the rows of one
+//             block have different owners, so every rank's reduce spreads over as many
+//             blocks as it owns rows; block b sums ITS owned rows over all peers (rounded
+//             to T: the all-reduce output) in place; barrier;
 //   gather:   block b reads each of its rows from the row's owner -- whole rows, so the
 //             residual add and the RMSNorm run right there: the reduced rows are read
 //             2 (NR-1)/NR x bytes per rank like the plain two-shot, and no second kernel
@@ -347,8 +350,9 @@ __device__ __forceinline__ void allreduce_rms2_body(const ArPtrs& P, int rank, i
     for (int v = threadIdx.x; v < nv; v += AR_THREADS)
       mine[(int64_t)row * nv + v] = src[(int64_t)row * nv + v];
   ar_barrier<NR, true>(P, rank, blk, 0, epoch);
+  auto owner = [](int row) { return (row + row / AR2_BLOCKS) % NR; };
   for (int row = blk; row < M; row += AR2_BLOCKS) {
-    if (row % NR != rank) continue;
+    if (owner(row) != rank) continue;
     for (int v = threadIdx.x; v < nv; v += AR_THREADS) {
       const int64_t e = (int64_t)row * nv + v;
       const u32x4 s = ar_sum_vec<T, NR>(P, par_off, e);
@@ -363,12 +367,12 @@ __device__ __forceinline__ void allreduce_rms2_body(const ArPtrs& P, int rank, i
     if (v < nv) wv[i].u = reinterpret_cast<const u32x4*>(w)[v];
   }
   for (int row = blk; row < M; row += AR2_BLOCKS) {
-    const u32x4* owner = reinterpret_cast<const u32x4*>(P.data[row % NR]) + par_off;
+    const u32x4* own = reinterpret_cast<const u32x4*>(P.data[owner(row)]) + par_off;
     Pack8<T> h[ARN_MAXV];
 #pragma unroll
     for (int i = 0; i < ARN_MAXV; ++i) {
       const int v = threadIdx.x + i * AR_THREADS;
-      if (v < nv) h[i].u = ld_peer(owner + (int64_t)row * nv + v);
+      if (v < nv) h[i].u = ld_peer(own + (int64_t)row * nv + v);
     }
     ar_add_norm_row<T>(h, wv, residual, out, row, nv, H, eps, scratch);
   }

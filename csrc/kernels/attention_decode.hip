@@ -42,6 +42,17 @@ constexpr int DEC_PART = 64;     // tokens per partition (one wave-iteration)
 constexpr int DEC_CHUNKS = DEC_PART / 32;
 constexpr int DEC_MAX_Z = 1024;  // z-slices the reduce kernel merges (host-checked)
 
+// K1w: 32-token chunks per z-slice (>= 2, the pipeline depth); slices past the context are
+// empty and the reduce stops at decode_used_slices
+__host__ __device__ __forceinline__ int decode_slice_chunks(int nchunk, int Z) {
+  const int per = (nchunk + Z - 1) / Z;
+  return per < 2 ? 2 : per;
+}
+__host__ __device__ __forceinline__ int decode_used_slices(int nchunk, int Z) {
+  const int n = (nchunk + decode_slice_chunks(nchunk, Z) - 1) / decode_slice_chunks(nchunk, Z);
+  return n < Z ? n : Z;
+}
+
 __device__ __forceinline__ u32x4 ld16(const void* p) {
   return *reinterpret_cast<const u32x4*>(p);
 }
@@ -454,8 +465,9 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
     T* __restrict__ out, const T* __restrict__ q, const void* __restrict__ kc_,
     const void* __restrict__ vc_, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ ctx_lens, float* __restrict__ max_logits,
-    float* __restrict__ exp_sums, float* __restrict__ tmp_out, int nq, int nkv, int bs_log2,
-    float scale_log2, float v_scale, int num_blocks, DecodeRope rp) {
+    float* __restrict__ exp_sums, float* __restrict__ tmp_out, int* __restrict__ tickets,
+    int nq, int nkv, int bs_log2, float scale_log2, float v_scale, int num_blocks,
+    DecodeRope rp) {
   typedef typename Vec8<T>::type V8;
   typedef std::conditional_t<KV8, uint8_t, T> C;
   const C* __restrict__ kc = reinterpret_cast<const C*>(kc_);
@@ -466,6 +478,7 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
   };
   constexpr int KS = D / 32, DT = D / 16;
   __shared__ __attribute__((aligned(16))) T lds_q[FUSE ? 16 : 1][FUSE ? D + 8 : 8];
+  __shared__ float wz_s[DEC_MAX_Z];         // Z > 1: the last slice's merge weights
   const int b = blockIdx.x, h = blockIdx.y, z = blockIdx.z, Z = gridDim.z;
   const int lane = threadIdx.x;
   const int r16 = lane & 15, qd = lane >> 4;
@@ -481,9 +494,13 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
   const int64_t blk_stride = (int64_t)nkv * head_stride;
   const int keyA = 8 * (r16 >> 2) + (r16 & 3);
 
+  // slice z owns chunks [z * per, (z + 1) * per) with per >= 2 (the pipeline depth): the
+  // non-empty slices come first and the reduce merges only those (a graph captured with
+  // Z sized for max_model_len meets short contexts: most slices are then empty)
   const int nchunk = (ctx + 31) >> 5;
-  const int c0 = (int)(((int64_t)nchunk * z) / Z);
-  const int c1 = (int)(((int64_t)nchunk * (z + 1)) / Z);
+  const int per = decode_slice_chunks(nchunk, Z);
+  const int c0 = min(nchunk, z * per);
+  const int c1 = min(nchunk, c0 + per);
   const int end = min(ctx, c1 << 5);          // this wave's tokens: [c0*32, end)
   const int last_blk = max(0, (end - 1) >> bs_log2);
 
@@ -563,32 +580,118 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
   if (prefetched) issue(fa, c0);
   if constexpr (FUSE) {
     constexpr int TPH = D / 16;
-    for (int i = lane; i < G * TPH; i += 64) {
-      const int g = i / TPH, c = i % TPH;
-      const int64_t qe = (int64_t)b * rp.qkv_stride + (int64_t)(h * G + g) * D;
+    const bool has_kv = z == Z - 1 && ctx > 0;
+    if (G * TPH <= 32) {
+      // ONE pass, every lane its own role, so the q, k and v slice loads are all in
+      // flight together (as separate branches they were three dependent round trips):
+      // lanes [0, G*TPH) a q chunk pair, [32, 32+TPH) a k chunk pair, [48, 48+D/8) a v
+      // chunk of the new token (k / v only on the wave that owns it)
+      const int kind = lane < G * TPH ? 0 : (has_kv && lane >= 32 && lane < 32 + TPH) ? 1
+                     : (has_kv && lane >= 48 && lane < 48 + D / 8) ? 2 : 3;
+      const int c = kind == 0 ? lane % TPH : kind == 1 ? lane - 32 : kind == 2 ? lane - 48 : 0;
+      const int g = kind == 0 ? lane / TPH : 0;
+      const int64_t row = (int64_t)b * rp.qkv_stride;
+      const int64_t col = kind == 0 ? (int64_t)(h * G + g) * D : kind == 1 ? (int64_t)(nq + h) * D
+                        : (int64_t)(nq + nkv + h) * D;
       float xa[8], xb[8];
-      qkv_row8<T>(rp, qe + c * 8, xa);
-      qkv_row8<T>(rp, qe + D / 2 + c * 8, xb);
-      if (rp.q_norm_w) {
+      qkv_row8<T>(rp, row + col + c * 8, xa);
+      qkv_row8<T>(rp, row + col + (kind == 2 ? 0 : D / 2) + c * 8, xb);  // v: a dummy reload
+      const void* nw = kind == 0 ? rp.q_norm_w : rp.k_norm_w;
+      if (nw) {                    // q / k norm over the head's TPH lanes (aligned groups)
         float ss = 0.f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) ss += xa[j] * xa[j] + xb[j] * xb[j];
 #pragma unroll
         for (int o2 = 1; o2 < TPH; o2 <<= 1) ss += __shfl_xor(ss, o2, 64);
-        const float inv = rsqrtf(ss / (float)D + rp.eps);
-        norm8<T>(xa, inv, rp.q_norm_w, c * 8);
-        norm8<T>(xb, inv, rp.q_norm_w, D / 2 + c * 8);
+        if (kind < 2) {
+          const float inv = rsqrtf(ss / (float)D + rp.eps);
+          norm8<T>(xa, inv, nw, c * 8);
+          norm8<T>(xb, inv, nw, D / 2 + c * 8);
+        }
       }
-      if (rp.use_rope) rope8(xa, xb, rp.cos_sin + rp.positions[b] * D, c * 8, D / 2);
+      if (rp.use_rope && kind < 2) rope8(xa, xb, rp.cos_sin + rp.positions[b] * D, c * 8, D / 2);
       Pack8<T> oa, ob;
 #pragma unroll
       for (int j = 0; j < 8; ++j) { oa.h[j] = from_f<T>(xa[j]); ob.h[j] = from_f<T>(xb[j]); }
-      *reinterpret_cast<u32x4*>(&lds_q[g][c * 8]) = oa.u;
-      *reinterpret_cast<u32x4*>(&lds_q[g][D / 2 + c * 8]) = ob.u;
+      if (kind == 0) {
+        *reinterpret_cast<u32x4*>(&lds_q[g][c * 8]) = oa.u;
+        *reinterpret_cast<u32x4*>(&lds_q[g][D / 2 + c * 8]) = ob.u;
+      } else if (kind < 3) {
+        int64_t slot = rp.slots[b];
+        KGC_DCHECK_RANGE(slot, -1, (int64_t)num_blocks << bs_log2, "decode KV slot");
+        if (slot >= 0) {
+          const int64_t blk = slot >> bs_log2;
+          const int off = (int)(slot & ((1 << bs_log2) - 1));
+          if (kind == 1) {
+            const int64_t e = ((blk * nkv + h) << bs_log2 | off) * D;
+            if constexpr (KV8) {
+              uint8_t* dst = const_cast<uint8_t*>(reinterpret_cast<const uint8_t*>(kc_)) + e;
+              float fa[8], fb[8];
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                fa[j] = to_f(oa.h[j]) * rp.k_inv;
+                fb[j] = to_f(ob.h[j]) * rp.k_inv;
+              }
+              *reinterpret_cast<u32x2*>(dst + c * 8) =
+                  u32x2{fp8x4(fa[0], fa[1], fa[2], fa[3]), fp8x4(fa[4], fa[5], fa[6], fa[7])};
+              *reinterpret_cast<u32x2*>(dst + D / 2 + c * 8) =
+                  u32x2{fp8x4(fb[0], fb[1], fb[2], fb[3]), fp8x4(fb[4], fb[5], fb[6], fb[7])};
+            } else {
+              T* dst = const_cast<T*>(reinterpret_cast<const T*>(kc_)) + e;
+              *reinterpret_cast<u32x4*>(dst + c * 8) = oa.u;
+              *reinterpret_cast<u32x4*>(dst + D / 2 + c * 8) = ob.u;
+            }
+          } else {
+            // v: the un-normed, un-rotated value row chunk into the V^T 8-key group
+            const int64_t e = ((blk * nkv + h) << bs_log2) * D +
+                              ((int64_t)(off >> 3) * D + c * 8) * 8 + (off & 7);
+            if constexpr (KV8) {
+              uint8_t* dst = const_cast<uint8_t*>(reinterpret_cast<const uint8_t*>(vc_)) + e;
+              const uint32_t w0 = fp8x4(xa[0] * rp.v_inv, xa[1] * rp.v_inv, xa[2] * rp.v_inv,
+                                        xa[3] * rp.v_inv);
+              const uint32_t w1 = fp8x4(xa[4] * rp.v_inv, xa[5] * rp.v_inv, xa[6] * rp.v_inv,
+                                        xa[7] * rp.v_inv);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                dst[j * 8] = (uint8_t)(w0 >> (8 * j));
+                dst[(j + 4) * 8] = (uint8_t)(w1 >> (8 * j));
+              }
+            } else {
+              T* dst = const_cast<T*>(reinterpret_cast<const T*>(vc_)) + e;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) dst[j * 8] = from_f<T>(xa[j]);
+            }
+          }
+        }
+      }
+    } else {
+      for (int i = lane; i < G * TPH; i += 64) {
+        const int g = i / TPH, c = i % TPH;
+        const int64_t qe = (int64_t)b * rp.qkv_stride + (int64_t)(h * G + g) * D;
+        float xa[8], xb[8];
+        qkv_row8<T>(rp, qe + c * 8, xa);
+        qkv_row8<T>(rp, qe + D / 2 + c * 8, xb);
+        if (rp.q_norm_w) {
+          float ss = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ss += xa[j] * xa[j] + xb[j] * xb[j];
+#pragma unroll
+          for (int o2 = 1; o2 < TPH; o2 <<= 1) ss += __shfl_xor(ss, o2, 64);
+          const float inv = rsqrtf(ss / (float)D + rp.eps);
+          norm8<T>(xa, inv, rp.q_norm_w, c * 8);
+          norm8<T>(xb, inv, rp.q_norm_w, D / 2 + c * 8);
+        }
+        if (rp.use_rope) rope8(xa, xb, rp.cos_sin + rp.positions[b] * D, c * 8, D / 2);
+        Pack8<T> oa, ob;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { oa.h[j] = from_f<T>(xa[j]); ob.h[j] = from_f<T>(xb[j]); }
+        *reinterpret_cast<u32x4*>(&lds_q[g][c * 8]) = oa.u;
+        *reinterpret_cast<u32x4*>(&lds_q[g][D / 2 + c * 8]) = ob.u;
+      }
+      if (has_kv)
+        decode_kv_write<T, D, KV8>(rp, b, h, nq, nkv, bs_log2, num_blocks,
+                                   const_cast<void*>(kc_), const_cast<void*>(vc_), lane);
     }
-    if (z == Z - 1 && ctx > 0)
-      decode_kv_write<T, D, KV8>(rp, b, h, nq, nkv, bs_log2, num_blocks,
-                                 const_cast<void*>(kc_), const_cast<void*>(vc_), lane);
     // the k / v stores complete before any later load of the chunk that holds them
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
@@ -630,9 +733,9 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
 
   l_run += __shfl_xor(l_run, 16, 64);
   l_run += __shfl_xor(l_run, 32, 64);
-  if (r16 >= G) return;
   const int64_t row = (int64_t)b * nq + h * G + r16;
   if (Z == 1) {
+    if (r16 >= G) return;
     const float inv = l_run > 0.f ? v_scale / l_run : 0.f;
     T* orow = out + row * D + 4 * qd;
 #pragma unroll
@@ -642,19 +745,70 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
       for (int i = 0; i < 4; ++i) pk.h[i] = from_f<T>(o[t][i] * inv);
       *reinterpret_cast<u32x2*>(orow + 16 * t) = pk.u;
     }
-  } else {
+    return;
+  }
+  // Z > 1: the used slices write (max, sum, O) partials write-through (sc1 stores: no
+  // release fence needed), then draw a ticket; the slice that draws the last one merges
+  // all of them in this launch (no reduce kernel: at B = 1 its launch cost as much as the
+  // merge) and re-arms the ticket for the next launch / graph replay.
+  const int nz = decode_used_slices(nchunk, Z);
+  if (nz == 0) {                         // empty context (graph padding): a zero row
+    if (z == 0 && r16 < G) {
+      T* orow = out + row * D + 4 * qd;
+#pragma unroll
+      for (int t = 0; t < DT; ++t) *reinterpret_cast<u32x2*>(orow + 16 * t) = u32x2{0u, 0u};
+    }
+    return;
+  }
+  if (z >= nz) return;                   // an empty slice: no partial, no ticket
+  if (r16 < G) {
     const int64_t prow = row * Z + z;
     float* dst = tmp_out + prow * D + 4 * qd;
 #pragma unroll
-    for (int t = 0; t < DT; ++t) *reinterpret_cast<f32x4*>(dst + 16 * t) = o[t] * v_scale;
+    for (int t = 0; t < DT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        __hip_atomic_store(dst + 16 * t + i, o[t][i] * v_scale, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     if (qd == 0) {
-      max_logits[prow] = m_run;
-      exp_sums[prow] = l_run;
+      __hip_atomic_store(max_logits + prow, m_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(exp_sums + prow, l_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every partial store has landed
+  int* tk = tickets + (int64_t)b * nkv + h;
+  int old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __shfl(old, 0, 64);
+  if (old != nz - 1) return;
+  if (lane == 0) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  auto ld1 = [](const float* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  for (int g = 0; g < G; ++g) {
+    const int64_t rg = ((int64_t)b * nq + h * G + g) * Z;
+    float M = -INFINITY;
+    for (int zz = lane; zz < nz; zz += 64) M = fmaxf(M, ld1(max_logits + rg + zz));
+    M = wave_max(M);
+    float Lp = 0.f;
+    for (int zz = lane; zz < nz; zz += 64) {
+      const float w = M == -INFINITY ? 0.f : exp2f(ld1(max_logits + rg + zz) - M);
+      wz_s[zz] = w;
+      Lp += w * ld1(exp_sums + rg + zz);
+    }
+    const float L = wave_sum(Lp);
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+    T* orow = out + (rg / Z) * D;
+    for (int d = lane; d < D; d += 64) {
+      float acc = 0.f;
+      for (int zz = 0; zz < nz; ++zz) acc += wz_s[zz] * ld1(tmp_out + (rg + zz) * D + d);
+      orow[d] = from_f<T>(acc * inv);
     }
   }
 }
 
-// Merge the Z z-slice partials: one 64-thread wave per (seq, q-head).
+// Merge the Z z-slice partials of the 4-wave kernel: one 64-thread wave per (seq, q-head).
+// (K1w merges in-launch: the last slice of each (seq, kv-head) does it.)
 template <typename T, int D>
 __global__ __launch_bounds__(64) void paged_decode_reduce_kernel(
     T* __restrict__ out, const float* __restrict__ max_logits,
@@ -719,21 +873,17 @@ bool decode_wave_enabled() {
 template <typename T, int D, bool KV8, bool FUSE>
 static void decode_dispatch(void* out, const void* q, const void* kc, const void* vc,
                             const int* bt, int bt_stride, const int* ctx, float* ml, float* es,
-                            float* tmp, int B, int nq, int nkv, int bs_log2, int Zmax, int Z,
+                            float* tmp, int* tickets, int B, int nq, int nkv, int bs_log2,
+                            int Zmax, int Z,
                             float scale_log2, float v_scale, int num_blocks,
                             const DecodeRope& rp, hipStream_t s) {
-  if (decode_wave_enabled() && bs_log2 >= 4) {
+  if (decode_wave_enabled()) {
     // partial rows are Z apart (the workspace is sized for B * Z rows per head)
     paged_decode_wave_kernel<T, D, KV8, FUSE><<<dim3(B, nkv, Z), 64, 0, s>>>(
-        (T*)out, (const T*)q, kc, vc, bt, bt_stride, ctx, ml, es, tmp, nq, nkv, bs_log2,
-        scale_log2, v_scale, num_blocks, rp);
-    if (Z > 1)
-      paged_decode_reduce_kernel<T, D><<<dim3(B, nq), 64, 0, s>>>((T*)out, ml, es, tmp, ctx,
-                                                                  nq, Z, Z);
+        (T*)out, (const T*)q, kc, vc, bt, bt_stride, ctx, ml, es, tmp, tickets, nq, nkv,
+        bs_log2, scale_log2, v_scale, num_blocks, rp);
     return;
   }
-  // (the 4-wave kernel also serves blocks < 16 tokens; in K1w mode the binding passes
-  // Zmax = Z, so its partial rows are packed the same way)
   auto kern = paged_decode_kernel<T, D, true, KV8, 4, 1, FUSE>;
   kern<<<dim3(B, nkv, Z), 256, 0, s>>>(
       (T*)out, (const T*)q, kc, vc, bt, bt_stride, ctx, ml, es, tmp, nq,
@@ -747,14 +897,15 @@ template <bool FUSE>
 static void decode_launch(int dtype, void* out, const void* q, const void* k_cache,
                           const void* v_cache, const int* block_tables, int bt_stride,
                           const int* ctx_lens, float* max_logits, float* exp_sums,
-                          float* tmp_out, int B, int nq, int nkv, int D, int bs_log2,
-                          int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
+                          float* tmp_out, int* tickets, int B, int nq, int nkv, int D,
+                          int bs_log2, int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
                           float v_scale, int num_blocks, const DecodeRope& rp, hipStream_t s) {
   if (B == 0) return;
   const float sl2 = scale * k_scale * 1.4426950408889634f;
 #define KGC_DEC(TT, DD, K8)                                                                 \
   decode_dispatch<TT, DD, K8, FUSE>(out, q, k_cache, v_cache, block_tables, bt_stride,       \
-                                    ctx_lens, max_logits, exp_sums, tmp_out, B, nq, nkv,     \
+                                    ctx_lens, max_logits, exp_sums, tmp_out, tickets, B, nq, \
+                                    nkv,                                                     \
                                     bs_log2, Zmax, Z, sl2, v_scale, num_blocks, rp, s)
 #define KGC_DEC_D(TT, K8) \
   if (D == 128) KGC_DEC(TT, 128, K8); else KGC_DEC(TT, 64, K8)
@@ -770,24 +921,24 @@ static void decode_launch(int dtype, void* out, const void* q, const void* k_cac
 void launch_paged_decode(int dtype, void* out, const void* q, const void* k_cache,
                          const void* v_cache, const int* block_tables, int bt_stride,
                          const int* ctx_lens, float* max_logits, float* exp_sums,
-                         float* tmp_out, int B, int nq, int nkv, int D, int bs_log2,
-                         int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
+                         float* tmp_out, int* tickets, int B, int nq, int nkv, int D,
+                         int bs_log2, int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
                          float v_scale, int num_blocks, hipStream_t s) {
   const DecodeRope none{};
   decode_launch<false>(dtype, out, q, k_cache, v_cache, block_tables, bt_stride, ctx_lens,
-                       max_logits, exp_sums, tmp_out, B, nq, nkv, D, bs_log2, Zmax, Z, scale,
-                       kv_fp8, k_scale, v_scale, num_blocks, none, s);
+                       max_logits, exp_sums, tmp_out, tickets, B, nq, nkv, D, bs_log2, Zmax, Z,
+                       scale, kv_fp8, k_scale, v_scale, num_blocks, none, s);
 }
 
 void launch_paged_decode_rope(int dtype, const DecodeRope& rp, void* out, void* k_cache,
                               void* v_cache, const int* block_tables, int bt_stride,
                               const int* ctx_lens, float* max_logits, float* exp_sums,
-                              float* tmp_out, int B, int nq, int nkv, int D, int bs_log2,
-                              int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
-                              float v_scale, int num_blocks, hipStream_t s) {
+                              float* tmp_out, int* tickets, int B, int nq, int nkv, int D,
+                              int bs_log2, int Zmax, int Z, float scale, bool kv_fp8,
+                              float k_scale, float v_scale, int num_blocks, hipStream_t s) {
   decode_launch<true>(dtype, out, nullptr, k_cache, v_cache, block_tables, bt_stride, ctx_lens,
-                      max_logits, exp_sums, tmp_out, B, nq, nkv, D, bs_log2, Zmax, Z, scale,
-                      kv_fp8, k_scale, v_scale, num_blocks, rp, s);
+                      max_logits, exp_sums, tmp_out, tickets, B, nq, nkv, D, bs_log2, Zmax, Z,
+                      scale, kv_fp8, k_scale, v_scale, num_blocks, rp, s);
 }
 
 int paged_decode_partition_size() { return decode_wave_enabled() ? 32 : DEC_PART; }

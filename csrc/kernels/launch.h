@@ -20,11 +20,13 @@ void launch_rope_kv_write(int dtype, const void* qkv, int64_t qkv_stride, int S,
                           const void* q_norm_w, const void* k_norm_w, int T, int nq, int nkv,
                           int d, int bs, float eps, bool use_rope, bool kv_fp8, float k_scale,
                           float v_scale, int num_blocks, hipStream_t s);
+// tickets: [B * nkv] int32, zero before the first launch (K1w, Z > 1: the last slice of a
+// (seq, kv-head) merges the partials in-launch and re-arms its ticket)
 void launch_paged_decode(int dtype, void* out, const void* q, const void* k_cache,
                          const void* v_cache, const int* block_tables, int bt_stride,
                          const int* ctx_lens, float* max_logits, float* exp_sums,
-                         float* tmp_out, int B, int nq, int nkv, int D, int bs_log2,
-                         int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
+                         float* tmp_out, int* tickets, int B, int nq, int nkv, int D,
+                         int bs_log2, int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
                          float v_scale, int num_blocks, hipStream_t s);
 int paged_decode_partition_size();
 // 1: the K1w kernel (one wave per (seq, kv-head, z-slice)); 4: the 4-wave workgroup kernel
@@ -50,9 +52,9 @@ struct DecodeRope {
 void launch_paged_decode_rope(int dtype, const DecodeRope& rp, void* out, void* k_cache,
                               void* v_cache, const int* block_tables, int bt_stride,
                               const int* ctx_lens, float* max_logits, float* exp_sums,
-                              float* tmp_out, int B, int nq, int nkv, int D, int bs_log2,
-                              int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
-                              float v_scale, int num_blocks, hipStream_t s);
+                              float* tmp_out, int* tickets, int B, int nq, int nkv, int D,
+                              int bs_log2, int Zmax, int Z, float scale, bool kv_fp8,
+                              float k_scale, float v_scale, int num_blocks, hipStream_t s);
 void launch_prefill_attention(int dtype, const void* q, void* out, const void* k_cache,
                               const void* v_cache, const int* block_tables, int bt_stride,
                               const int* query_start_loc, const int* seq_lens,

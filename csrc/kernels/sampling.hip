@@ -62,7 +62,7 @@ __device__ __forceinline__ float block_scan_incl(float v, float* wtot) {
 }
 
 // f(i, logit) over row[lo, hi) by a SMP_NT-thread block.  16-bit rows are read as
-// 16-byte vectors (8 logits per load, 2 loads in flight per thread): every pass over
+// 16-byte vectors (8 logits per load, 4 loads in flight per thread): every pass over
 // a 128K-entry row is then ~16 dependent round trips per thread instead of ~125.
 template <typename T, typename F>
 __device__ __forceinline__ void visit_row(const T* __restrict__ row, int lo, int hi, int tid,
@@ -72,12 +72,21 @@ __device__ __forceinline__ void visit_row(const T* __restrict__ row, int lo, int
     const int e = max(a, hi & ~7);
     if ((reinterpret_cast<uintptr_t>(row) & 15) == 0) {
       for (int i = lo + tid; i < a; i += SMP_NT) f(i, to_f(row[i]));
-#pragma unroll 2
-      for (int v = a + 8 * tid; v < e; v += 8 * SMP_NT) {
-        Pack8<T> p;
-        p.u = *reinterpret_cast<const u32x4*>(row + v);
+      // 4 vectors per thread in flight: the loads of a trip are unconditional (clamped
+      // to the last full vector) so none waits behind a branch; only f is predicated.
+      constexpr int U = 4, VS = 8 * SMP_NT;
+      for (int v = a + 8 * tid; v < e; v += U * VS) {
+        Pack8<T> p[U];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f(v + j, to_f(p.h[j]));
+        for (int u = 0; u < U; ++u)
+          p[u].u = *reinterpret_cast<const u32x4*>(row + min(v + u * VS, e - 8));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (v + u * VS < e) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f(v + u * VS + j, to_f(p[u].h[j]));
+          }
+        }
       }
       for (int i = e + tid; i < hi; i += SMP_NT) f(i, to_f(row[i]));
       return;

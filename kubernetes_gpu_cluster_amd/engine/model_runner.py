@@ -522,7 +522,12 @@ class ModelRunner:
                                out=self.d64[L.ids + plan.Tp:L.ids + plan.Tp + n])
         if graph:
             g, logits = self.graphs[plan.B]
+            link = self.pp_link
+            if link is not None:
+                link.pre_replay(plan.B)     # host link: this step's input rows (no-op: IPC)
             g.replay()
+            if link is not None:
+                link.post_replay(plan.B)    # host link: the output rows to the next stage
             self.stats["graph_steps"] += 1
             if not self.model.last:
                 return None
@@ -598,13 +603,17 @@ class ModelRunner:
         return torch.full((plan.S,), 7, dtype=torch.int64, device=self.device)
 
     def write_stage_stats(self) -> None:
-        """KGC_STAGE_STATS_DIR: this rank's fake-stage busy time and span (JSON)."""
+        """KGC_STAGE_STATS_DIR: this rank's step counters (graph replays / eager steps) and,
+        for fake stages, busy time and span (JSON, one file per rank)."""
         d = os.environ.get("KGC_STAGE_STATS_DIR")
-        if not d or not self.stage_stats["steps"]:
+        if not d or not torch.distributed.is_initialized():
             return
         import json
         with open(os.path.join(d, f"rank{torch.distributed.get_rank()}.json"), "w") as f:
-            json.dump(dict(self.stage_stats, pp_rank=self.ps.pp_rank), f)
+            json.dump(dict(self.stage_stats, pp_rank=self.ps.pp_rank,
+                           graph_steps=self.stats["graph_steps"],
+                           eager_steps=self.stats["eager_steps"],
+                           pp_link=type(self.pp_link).__name__ if self.pp_link else None), f)
 
     def _sample_vp(self, local: torch.Tensor, plan: StepPlan) -> torch.Tensor:
         S, L = plan.S, self.L
@@ -706,17 +715,19 @@ class ModelRunner:
         for B in sorted(self.buckets, reverse=True):
             z = ops.decode_grid_z(B, nkv, self.max_model_len)
             meta = self._meta(B, 0, 0, B, 0, self.max_model_len, z=z)
-            idx = self.d64[L.lidx:L.lidx + B]
 
-            def step_body(B=B, meta=meta, idx=idx):
+            def step_body(B=B, meta=meta):
                 # PP stages: receive from the previous stage / send to the next one as
-                # kernels over peer memory, so the whole stage step is one replay
+                # kernels over peer memory, so the whole stage step is one replay (host
+                # link: the graph reads / writes static rows, moved around the replay)
                 hin = self.pp_link.recv(B) if not self.model.first else None
                 h = self._forward(B, meta, hin)
                 if not self.model.last:
                     self.pp_link.send(*h)
                     return None
-                return self.model.compute_logits(h.index_select(0, idx), gather=not self.vp)
+                # graph rows sample their own hidden row (build_plan sets lidx = 0..B-1 for
+                # every graph step): no gather launch in the replay
+                return self.model.compute_logits(h, gather=not self.vp)
             for _ in range(2):   # warm up (allocator, library handles) outside capture;
                 step_body()      # PP: every stage runs the same warm-ups, in bucket order
             torch.cuda.synchronize()

@@ -113,12 +113,13 @@ class Worker:
                                   self.max_model_len, cfg.max_num_seqs, cfg.token_budget(),
                                   cfg.enforce_eager, cfg.cuda_graph_max_bs,
                                   kv_dtype=cfg.kv_torch_dtype(self.dtype))
-        if (self.ps.pp_size > 1 and dev.type == "cuda" and not cfg.enforce_eager
-                and cfg.nnodes == 1):
-            # per-stage decode graphs: the stage handoff as kernels over peer memory
-            from ..parallel.pp_handoff import maybe_init_pp_handoff
-            self.runner.pp_link = maybe_init_pp_handoff(self.ps, dev, self.runner.graph_max_bs,
-                                                        self.mcfg.hidden_size, self.dtype)
+        if self.ps.pp_size > 1 and dev.type == "cuda" and not cfg.enforce_eager:
+            # per-stage decode graphs: the stage handoff as kernels over peer memory (one
+            # node), or point-to-point sends between the stages' replays (pods on several
+            # nodes: parallel/pp_handoff.py HostPipelineLink)
+            from ..parallel.pp_handoff import init_pp_link
+            self.runner.pp_link = init_pp_link(self.ps, dev, self.runner.graph_max_bs,
+                                               self.mcfg.hidden_size, self.dtype, cfg.nnodes)
 
     def profile(self) -> int:
         if self.cfg.num_gpu_blocks_override:

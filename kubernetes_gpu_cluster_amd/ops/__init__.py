@@ -186,23 +186,25 @@ def decode_max_z(max_blocks: int, block_size: int) -> int:
 
 
 def decode_partials(batch: int, num_heads: int, head_dim: int, max_blocks: int,
-                    block_size: int, device) -> tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-    """Per-z-slice (max, sum, O) partials of the split-context decode kernel
-    (static: graph-capturable).  Unused when the grid has a single z-slice.
+                    block_size: int, device) -> tuple:
+    """Per-z-slice (max, sum, O) partials of the split-context decode kernel and its
+    merge tickets (static: graph-capturable).  Unused when the grid has a single z-slice.
     K1w packs the rows of a launch Z apart, so the workspace holds (seq, z) rows: enough
     for every Z ``decode_grid_z`` picks at any batch <= ``batch`` (B * Z <= 2 x the wave
-    target + B), flat [rows * heads]."""
+    target + B), flat [rows * heads]; the tickets ([batch * heads] int32, zero) let the
+    last slice of each (seq, kv-head) merge in the same launch and re-arm itself."""
     Z = decode_max_z(max_blocks, block_size)
+    tickets = torch.zeros(batch * num_heads, dtype=torch.int32, device=device)
     if decode_wave_kernel():
         rows = min(batch * Z, 2 * DECODE_TARGET_WAVES + batch)
         ml = torch.empty(rows * num_heads, dtype=torch.float32, device=device)
         es = torch.empty(rows * num_heads, dtype=torch.float32, device=device)
         tmp = torch.empty(rows * num_heads, head_dim, dtype=torch.float32, device=device)
-        return ml, es, tmp
+        return ml, es, tmp, tickets
     ml = torch.empty(batch, num_heads, Z, dtype=torch.float32, device=device)
     es = torch.empty(batch, num_heads, Z, dtype=torch.float32, device=device)
     tmp = torch.empty(batch, num_heads, Z, head_dim, dtype=torch.float32, device=device)
-    return ml, es, tmp
+    return ml, es, tmp, tickets
 
 
 def _decode_z_cap(ws, B: int, nq: int) -> int:
@@ -240,10 +242,10 @@ def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torc
         out = torch.empty_like(q)
     if workspace is None:
         workspace = decode_partials(B, nq, d, block_tables.shape[1], k_cache.shape[2], q.device)
-    ml, es, tmp = workspace
+    ml, es, tmp, tickets = workspace
     grid_z = min(grid_z, _decode_z_cap(workspace, B, nq))
     _k().paged_decode(out, q, k_cache, v_cache, block_tables, context_lens, ml, es, tmp,
-                      grid_z, scale, k_scale, v_scale)
+                      tickets, grid_z, scale, k_scale, v_scale)
     return out
 
 
@@ -274,10 +276,10 @@ def paged_attention_decode_rope(qkv: torch.Tensor, positions: torch.Tensor,
     if workspace is None:
         workspace = decode_partials(B, num_heads, head_dim, block_tables.shape[1],
                                     k_cache.shape[2], qkv.device)
-    ml, es, tmp = workspace
+    ml, es, tmp, tickets = workspace
     grid_z = min(grid_z, _decode_z_cap(workspace, B, num_heads))
     _k().paged_decode_rope(out, qkv, positions, cos_sin, k_cache, v_cache, slot_mapping,
-                           q_norm_w, k_norm_w, block_tables, context_lens, ml, es, tmp,
+                           q_norm_w, k_norm_w, block_tables, context_lens, ml, es, tmp, tickets,
                            num_heads, grid_z, scale, eps, use_rope, k_scale, v_scale)
     return out
 

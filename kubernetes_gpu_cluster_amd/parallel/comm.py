@@ -139,6 +139,23 @@ def pp_recv(shapes: list[tuple], dtype: torch.dtype, device) -> list[torch.Tenso
     return out
 
 
+def pp_recv_into(out: list[torch.Tensor]) -> None:
+    """C5 receive into existing (static) tensors -- the per-stage graph's input rows."""
+    s = get_state()
+    src = getattr(s, "global_base", 0) + s.rank - s.tp_size
+    for t in out:
+        if t.is_cuda and _host_staged():
+            h = torch.empty(t.shape, dtype=t.dtype)
+            dist.recv(h, src=src)
+            t.copy_(h)
+        elif t.is_contiguous():
+            dist.recv(t, src=src)
+        else:
+            tmp = torch.empty_like(t, memory_format=torch.contiguous_format)
+            dist.recv(tmp, src=src)
+            t.copy_(tmp)
+
+
 def all_reduce_min_scalar(v: int) -> int:
     """C8: agree on the KV block count across all model ranks."""
     s = get_state()

@@ -78,6 +78,12 @@ class PipelineHandoff:
         self.max_rows = max_rows
         self._err_host: Optional[torch.Tensor] = None
 
+    def pre_replay(self, rows: int) -> None:
+        """Nothing: the receive kernel is inside the stage's graph."""
+
+    def post_replay(self, rows: int) -> None:
+        """Nothing: the send kernel is inside the stage's graph."""
+
     def send(self, h: torch.Tensor, r: torch.Tensor) -> None:
         torch.ops.kgc.pp_send(h.contiguous(), r.contiguous(), self.next_data, self.next_recv_sig,
                               self.own_send_sig, self.slot_bytes, self.R)
@@ -118,6 +124,78 @@ class PipelineHandoff:
                 torch.ops.kgc.ar_free(self._own)
             self._own = 0
             self._opened = []
+
+
+class HostPipelineLink:
+    """Stage handoff for per-stage decode graphs when the stages cannot map each other's
+    memory -- pods on different nodes (``nnodes > 1``; KubeRay's multi-pod PP in the
+    reference, /root/reference/values-01-minimal-example4.yaml:17-18,42-46).  The stage's
+    decode step is still ONE graph replay, over static tensors: the graph reads its input
+    rows from ``h_in`` / ``r_in`` and copies its output rows into ``h_out`` / ``r_out``; the
+    rows move between replays by point-to-point send / recv on the stream (RCCL over the
+    pod network; gloo stages them through the host in the one-GPU test harness).
+    Warm-up calls outside capture communicate as the replays will, so every stage runs
+    the same sequence."""
+
+    def __init__(self, ps, device: torch.device, max_rows: int, hidden: int,
+                 dtype: torch.dtype):
+        self.first, self.last = ps.is_first_pp, ps.is_last_pp
+        self.max_rows = max_rows
+        z = lambda: torch.zeros(max_rows, hidden, dtype=dtype, device=device)  # noqa: E731
+        self.h_in, self.r_in, self.h_out, self.r_out = z(), z(), z(), z()
+
+    @staticmethod
+    def _capturing() -> bool:
+        return torch.cuda.is_current_stream_capturing()
+
+    def recv(self, rows: int) -> tuple[torch.Tensor, torch.Tensor]:
+        if not self._capturing():
+            self.pre_replay(rows)
+        return self.h_in[:rows], self.r_in[:rows]
+
+    def send(self, h: torch.Tensor, r: torch.Tensor) -> None:
+        rows = h.shape[0]
+        self.h_out[:rows].copy_(h)
+        self.r_out[:rows].copy_(r)
+        if not self._capturing():
+            self.post_replay(rows)
+
+    def pre_replay(self, rows: int) -> None:
+        """Before a replay: this step's rows from the previous stage into h_in / r_in."""
+        if not self.first:
+            from . import comm
+            comm.pp_recv_into([self.h_in[:rows], self.r_in[:rows]])
+
+    def post_replay(self, rows: int) -> None:
+        """After a replay: the rows the graph left in h_out / r_out to the next stage."""
+        if not self.last:
+            from . import comm
+            comm.pp_send([self.h_out[:rows], self.r_out[:rows]])
+
+    # point-to-point failures raise in the collective itself: nothing sticky to read
+    def enqueue_err_read(self):
+        return None
+
+    def raise_if_failed(self, slot=None) -> None:
+        return None
+
+    def check(self) -> None:
+        return None
+
+    def close(self) -> None:
+        return None
+
+
+def init_pp_link(ps, device: torch.device, max_rows: int, hidden: int, dtype: torch.dtype,
+                 nnodes: int):
+    """The stage link of PP decode graphs: the peer-memory kernels when every stage is on
+    this node (one IPC domain), otherwise -- or with KGC_PP_LINK=host -- point-to-point
+    sends between per-stage graph replays.  None: PP decode stays eager."""
+    if ps.pp_size == 1:
+        return None
+    if nnodes == 1 and os.environ.get("KGC_PP_LINK", "ipc") != "host":
+        return maybe_init_pp_handoff(ps, device, max_rows, hidden, dtype)
+    return HostPipelineLink(ps, device, max_rows, hidden, dtype)
 
 
 def maybe_init_pp_handoff(ps, device: torch.device, max_rows: int, hidden: int,

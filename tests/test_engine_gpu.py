@@ -461,11 +461,15 @@ def test_pp2_stage_graphs_on_one_gpu(gpu, tmp_path, monkeypatch):
     assert outs[2] == outs[1], outs
 
 
-def test_two_node_tp2_on_one_gpu(gpu, tmp_path):
+@pytest.mark.parametrize("tp,pp", [(2, 1), (1, 2)])
+def test_two_node_engine_on_one_gpu(gpu, tmp_path, tp, pp):
     """The multi-pod engine (leader/worker StatefulSet layout) on the GPU: node 0 (the
     driver, this process) and entrypoints.worker_node (node 1, a separate process)
-    rendezvous over TCP and run one TP=2 engine; both ranks use cuda:0 with a gloo group.
-    Greedy output == the single-GPU engine."""
+    rendezvous over TCP and run one engine; both ranks use cuda:0 with a gloo group.
+    TP = 2 runs eager.  PP = 2 across the two "nodes" runs per-stage decode GRAPHS: the
+    stages cannot map each other's memory across pods, so the hidden / residual rows move
+    by point-to-point sends between the stages' replays (HostPipelineLink) -- both stages
+    must report graph replays.  Greedy output == the single-GPU engine."""
     import json
     import os
     import socket
@@ -497,30 +501,45 @@ def test_two_node_tp2_on_one_gpu(gpu, tmp_path):
         port = so.getsockname()[1]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, PYTHONPATH=root, KGC_DIST_BACKEND="gloo")
+    stats = tmp_path / "stats"
+    stats.mkdir()
+    env["KGC_STAGE_STATS_DIR"] = str(stats)
+    eager = pp == 1
     worker = subprocess.Popen(
         [sys.executable, "-m", "kubernetes_gpu_cluster_amd.entrypoints.worker_node", d,
-         "--tensor-parallel-size", "2", "--nnodes", "2", "--node-rank", "1",
+         "--tensor-parallel-size", str(tp), "--pipeline-parallel-size", str(pp),
+         "--nnodes", "2", "--node-rank", "1",
          "--master-addr", "127.0.0.1", "--master-port", str(port), "--device", "cuda",
          "--dtype", "bfloat16", "--max-model-len", "256", "--max-num-seqs", "4",
-         "--max-num-batched-tokens", "128", "--num-gpu-blocks-override", "64",
-         "--enforce-eager"],
+         "--max-num-batched-tokens", "128", "--num-gpu-blocks-override", "64"]
+        + (["--enforce-eager"] if eager else []),
         cwd=root, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
-    old = os.environ.get("KGC_DIST_BACKEND")
+    saved = {k: os.environ.get(k) for k in ("KGC_DIST_BACKEND", "KGC_STAGE_STATS_DIR")}
     os.environ["KGC_DIST_BACKEND"] = "gloo"
+    os.environ["KGC_STAGE_STATS_DIR"] = str(stats)
     try:
-        llm = LLM(d, tensor_parallel_size=2, nnodes=2, node_rank=0, master_addr="127.0.0.1",
-                  master_port=port, **common)
+        llm = LLM(d, tensor_parallel_size=tp, pipeline_parallel_size=pp, nnodes=2, node_rank=0,
+                  master_addr="127.0.0.1", master_port=port,
+                  **dict(common, enforce_eager=eager))
         got = [o.output_token_ids for o in llm.generate(prompts, sp)]
         llm.shutdown()
         rc = worker.wait(timeout=120)
     finally:
-        if old is None:
-            os.environ.pop("KGC_DIST_BACKEND", None)
-        else:
-            os.environ["KGC_DIST_BACKEND"] = old
+        for k_, v_ in saved.items():
+            if v_ is None:
+                os.environ.pop(k_, None)
+            else:
+                os.environ[k_] = v_
         if worker.poll() is None:
             worker.kill()
     assert rc == 0, worker.stdout.read()[-3000:]
+    if pp == 2:
+        st = {json.loads(f.read_text())["pp_rank"]: json.loads(f.read_text())
+              for f in stats.glob("rank*.json")}
+        assert set(st) == {0, 1}, st
+        for r in (0, 1):
+            assert st[r]["pp_link"] == "HostPipelineLink", st
+            assert st[r]["graph_steps"] > 0, st
     same = sum(a == b for x, y in zip(ref, got) for a, b in zip(x, y))
     assert all(x[0] == y[0] for x, y in zip(ref, got)), (ref, got)
     assert same >= 0.8 * sum(len(x) for x in ref), (ref, got)

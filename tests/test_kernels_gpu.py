@@ -128,10 +128,11 @@ def _fill_random_cache(B, ctx_lens, nkv, bs, d, dt, dev, nb_extra=7):
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("d,nq,nkv", [(128, 32, 8), (128, 8, 1), (128, 28, 4), (64, 12, 12),
                                       (128, 16, 16)])
-@pytest.mark.parametrize("bs", [8, 16, 32])
+@pytest.mark.parametrize("bs", [16, 32])
 def test_paged_decode(gpu, dt, d, nq, nkv, bs):
     """K1 vs the fp32 reference at ragged lengths (1 token .. 2049), GQA 1/4/7/8 and MHA,
-    z = 1 and 3; bs = 8 runs the 4-wave kernel (K1w takes blocks of >= 16 tokens)."""
+    z = 1, 3 and 40 (K1w: most slices of the short rows empty, the reduce merges only the
+    used ones)."""
     torch.manual_seed(3)
     ctx = [1, 17, 128, 129, 300, 1000, 2049, 64]
     B = len(ctx)
@@ -139,7 +140,7 @@ def test_paged_decode(gpu, dt, d, nq, nkv, bs):
     q = torch.randn(B, nq, d, dtype=dt, device=gpu)
     cl = torch.tensor(ctx, dtype=torch.int32, device=gpu)
     scale = d ** -0.5
-    for z in (1, 3):
+    for z in (1, 3, 40):
         out = ops.paged_attention_decode(q, kc, vc, bt, cl, scale, grid_z=z)
         exp = ref.paged_attention_decode(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cl.cpu(), scale)
         torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(dt))
