@@ -194,6 +194,8 @@ void paged_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor b
               tmp_out.numel() >= B * nq * Zmax * d, "partials too small");
   TORCH_CHECK(Z >= 1 && Z <= Zmax && Z <= 1024,
               "kgc.paged_decode: need 1 <= Z <= min(partial slots, 1024)");
+  TORCH_CHECK(kgc::paged_decode_waves_per_slice() != 1 || Z * (nq / k_cache.size(1)) <= 1024,
+              "kgc.paged_decode: K1w merges G * Z <= 1024 partials");
   kgc::launch_paged_decode(dt_code(q), out.data_ptr(), q.data_ptr(), k_cache.data_ptr(),
                            v_cache.data_ptr(), block_tables.data_ptr<int>(),
                            (int)block_tables.stride(0), ctx_lens.data_ptr<int>(),
@@ -257,6 +259,8 @@ void paged_decode_rope(Tensor out, Tensor qkv, Tensor positions, Tensor cos_sin,
               tmp_out.numel() >= B * nq * Zmax * d, "partials too small");
   TORCH_CHECK(Z >= 1 && Z <= Zmax && Z <= 1024,
               "kgc.paged_decode_rope: need 1 <= Z <= min(partial slots, 1024)");
+  TORCH_CHECK(kgc::paged_decode_waves_per_slice() != 1 || Z * (nq / nkv) <= 1024,
+              "kgc.paged_decode_rope: K1w merges G * Z <= 1024 partials");
   TORCH_CHECK(k_scale > 0 && v_scale > 0, "kv scales must be > 0");
   for (const Tensor* t : {&qkv, &positions, &cos_sin, &slot_mapping, &block_tables, &ctx_lens})
     check_same_dev(out, *t, "paged_decode_rope operand");
@@ -1028,8 +1032,8 @@ void skinny_gemm(Tensor C, Tensor X, Tensor W, std::optional<Tensor> bias, int64
     TORCH_CHECK(norm_out.has_value() && norm_out->is_contiguous() && norm_out->size(0) == M &&
                 norm_out->size(1) == N && norm_out->scalar_type() == X.scalar_type() &&
                 norm_out->data_ptr() != C.data_ptr(), "kgc.skinny_gemm: norm_out [M, N]");
-    TORCH_CHECK(ticket.has_value() && ticket->numel() >= 1 &&
-                ticket->scalar_type() == at::kInt, "kgc.skinny_gemm: ticket int32 [>= 1]");
+    TORCH_CHECK(ticket.has_value() && ticket->numel() >= 9 &&
+                ticket->scalar_type() == at::kInt, "kgc.skinny_gemm: ticket int32 [>= 9] (top + 8 sub-counters)");
     check_same_dev(X, *norm_out, "norm_out");
     check_same_dev(X, *ticket, "ticket");
     np = norm_out->data_ptr();

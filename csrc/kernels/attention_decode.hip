@@ -41,6 +41,7 @@ namespace kgc {
 constexpr int DEC_PART = 64;     // tokens per partition (one wave-iteration)
 constexpr int DEC_CHUNKS = DEC_PART / 32;
 constexpr int DEC_MAX_Z = 1024;  // z-slices the reduce kernel merges (host-checked)
+constexpr int DEC_MERGE_MAX = 1024;  // K1w: G * Z (heads x slices) one merge holds
 
 // K1w: 32-token chunks per z-slice (>= 2, the pipeline depth); slices past the context are
 // empty and the reduce stops at decode_used_slices
@@ -478,7 +479,8 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
   };
   constexpr int KS = D / 32, DT = D / 16;
   __shared__ __attribute__((aligned(16))) T lds_q[FUSE ? 16 : 1][FUSE ? D + 8 : 8];
-  __shared__ float wz_s[DEC_MAX_Z];         // Z > 1: the last slice's merge weights
+  // Z > 1: the last slice's merge state ((g, slice) max -> weight, sum; 1/sum per head)
+  __shared__ float wz_s[DEC_MERGE_MAX], ez_s[DEC_MERGE_MAX], inv_s[16];
   const int b = blockIdx.x, h = blockIdx.y, z = blockIdx.z, Z = gridDim.z;
   const int lane = threadIdx.x;
   const int r16 = lane & 15, qd = lane >> 4;
@@ -580,7 +582,9 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
   if (prefetched) issue(fa, c0);
   if constexpr (FUSE) {
     constexpr int TPH = D / 16;
-    const bool has_kv = z == Z - 1 && ctx > 0;
+    // the new token's k / v: written by the slice that reads the context's last chunk
+    // (slices are compact: that is slice nz - 1, not Z - 1)
+    const bool has_kv = ctx > 0 && z == decode_used_slices(nchunk, Z) - 1;
     if (G * TPH <= 32) {
       // ONE pass, every lane its own role, so the q, k and v slice loads are all in
       // flight together (as separate branches they were three dependent round trips):
@@ -782,28 +786,52 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
   old = __shfl(old, 0, 64);
   if (old != nz - 1) return;
   if (lane == 0) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  auto ld1 = [](const float* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");    // the other slices' partials
+  // Merge of the G heads x nz slices, every phase with its loads issued together (a
+  // per-slice loop of dependent L2 round trips made this merge cost 35 us at B = 1):
+  //   1. (max, sum) of all (g, slice) pairs -> LDS (lane-parallel, one round trip);
+  //   2. per head: max, weights, 1/sum from LDS;
+  //   3. O: G*D/4 float4 columns per slice, 8 slices of loads in flight per lane.
+  // The host keeps G * Z <= DEC_MERGE_MAX.
+  const int64_t rb = ((int64_t)b * nq + h * G) * Z;     // (g, zz) at rb + g * Z + zz
+  const int GN = G * nz;
+  for (int i = lane; i < GN; i += 64) {
+    const int g = i / nz, zz = i - g * nz;
+    wz_s[i] = max_logits[rb + g * Z + zz];
+    ez_s[i] = exp_sums[rb + g * Z + zz];
+  }
   for (int g = 0; g < G; ++g) {
-    const int64_t rg = ((int64_t)b * nq + h * G + g) * Z;
     float M = -INFINITY;
-    for (int zz = lane; zz < nz; zz += 64) M = fmaxf(M, ld1(max_logits + rg + zz));
+    for (int zz = lane; zz < nz; zz += 64) M = fmaxf(M, wz_s[g * nz + zz]);
     M = wave_max(M);
     float Lp = 0.f;
     for (int zz = lane; zz < nz; zz += 64) {
-      const float w = M == -INFINITY ? 0.f : exp2f(ld1(max_logits + rg + zz) - M);
-      wz_s[zz] = w;
-      Lp += w * ld1(exp_sums + rg + zz);
+      const float w = M == -INFINITY ? 0.f : exp2f(wz_s[g * nz + zz] - M);
+      wz_s[g * nz + zz] = w;
+      Lp += w * ez_s[g * nz + zz];
     }
     const float L = wave_sum(Lp);
-    const float inv = L > 0.f ? 1.f / L : 0.f;
-    T* orow = out + (rg / Z) * D;
-    for (int d = lane; d < D; d += 64) {
-      float acc = 0.f;
-      for (int zz = 0; zz < nz; ++zz) acc += wz_s[zz] * ld1(tmp_out + (rg + zz) * D + d);
-      orow[d] = from_f<T>(acc * inv);
+    if (lane == 0) inv_s[g] = L > 0.f ? 1.f / L : 0.f;
+  }
+  constexpr int D4 = D / 4;
+  for (int e = lane; e < G * D4; e += 64) {
+    const int g = e / D4, c4 = e - g * D4;
+    const float* src = tmp_out + (rb + (int64_t)g * Z) * D + 4 * c4;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int z0 = 0; z0 < nz; z0 += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = *reinterpret_cast<const f32x4*>(src + (int64_t)min(z0 + j, nz - 1) * D);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (z0 + j < nz) acc += wz_s[g * nz + z0 + j] * v[j];
     }
+    const float inv = inv_s[g];
+    Pack4<T> pk;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pk.h[i] = from_f<T>(acc[i] * inv);
+    *reinterpret_cast<u32x2*>(out + ((int64_t)b * nq + h * G + g) * D + 4 * c4) = pk.u;
   }
 }
 

@@ -218,9 +218,23 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's C stores landed
     __syncthreads();
     if (threadIdx.x == 0) {
-      const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
+      // two-level fan-in: 8 sub-counters (blockIdx % 8, the XCD under round-robin
+      // placement) of <= gridDim/8 arrivals each, then the 8 sub-last workgroups on the
+      // top counter -- one device-scope counter took ~12 ns per arrival, ~3 us at 256
+      // workgroups (MI355X_MICROARCH.md "fanin"), more than the separate norm launch
+      const uint32_t sub = blockIdx.x & 7u;
+      const uint32_t nsub = (gridDim.x - sub + 7u) >> 3;
+      const uint32_t nact = min(gridDim.x, 8u);
+      bool lst = false;
+      const uint32_t t = __hip_atomic_fetch_add(ticket + 1 + sub, 1u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
-      last = t == gridDim.x - 1;
+      if (t == nsub - 1) {
+        __hip_atomic_store(ticket + 1 + sub, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t t2 = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+        lst = t2 == nact - 1;
+      }
+      last = lst;
       if (last) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -226,6 +226,122 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
   }
 }
 
+// Prefill K / V write (KVO, RoPE, no k-norm, T cache): one 256-thread workgroup per
+// 8-token group.  The per-token grid above gives a token 8 K threads in a 64-lane wave
+// and 128 V threads that each issue eight 2-byte stores; at a 16K-token chunk that kernel
+// took 137 us per layer for 134 MB of traffic.  Here a group whose 8 tokens fill one
+// 8-key group of the cache (consecutive slots, the first a multiple of 8 -- every group
+// of a sequence's aligned prefill) is written as:
+//   K: every (token, head, chunk pair) item rotated and stored as two 16-byte rows;
+//   V: thread (head, chunk) loads the chunk of all 8 tokens and writes the 8 x 8 block
+//      transposed, eight 16-byte stores (whole V^T rows of the group).
+// Other groups (sequence boundaries inside the group, padding slots) take 2-byte V stores.
+constexpr int KVG_NT = 256;
+template <typename T>
+__global__ __launch_bounds__(KVG_NT) void kv_group_kernel(
+    const T* __restrict__ qkv, int64_t qkv_stride, const int64_t* __restrict__ positions,
+    const float* __restrict__ cos_sin, T* __restrict__ k_cache, T* __restrict__ v_cache,
+    const int64_t* __restrict__ slot_mapping, int T_, int nq, int nkv, int d, int bs,
+    int num_blocks) {
+  const int t0 = blockIdx.x * 8, nt = min(8, T_ - t0);
+  const int tph = d >> 4, half = d >> 1, cpr = d >> 3;
+  __shared__ int64_t s_slot[8];
+  __shared__ int s_full;
+  if (threadIdx.x < 8) {
+    int64_t s = threadIdx.x < nt ? slot_mapping[t0 + threadIdx.x] : -1;
+    KGC_DCHECK_RANGE(s, -1, (int64_t)num_blocks * bs, "KV slot");
+    s_slot[threadIdx.x] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    bool full = nt == 8 && s_slot[0] >= 0 && (s_slot[0] & 7) == 0;
+    for (int k = 1; k < 8; ++k) full = full && s_slot[k] == s_slot[0] + k;
+    s_full = full;
+  }
+  // K: items (token k, head h, chunk pair c), two per thread with both loads in flight
+  const int nk_items = nt * nkv * tph;
+  for (int base = 0; base < nk_items; base += 2 * KVG_NT) {
+    Pack8<T> a[2], b[2];
+    int kk[2], hh[2], cc_[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int it = min(base + u * KVG_NT + (int)threadIdx.x, nk_items - 1);
+      kk[u] = it / (nkv * tph);
+      hh[u] = (it / tph) % nkv;
+      cc_[u] = it % tph;
+      const T* src = qkv + (int64_t)(t0 + kk[u]) * qkv_stride + (int64_t)(nq + hh[u]) * d;
+      a[u].u = *reinterpret_cast<const u32x4*>(src + cc_[u] * 8);
+      b[u].u = *reinterpret_cast<const u32x4*>(src + half + cc_[u] * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int it = base + u * KVG_NT + (int)threadIdx.x;
+      const int64_t slot = s_slot[kk[u]];
+      if (it >= nk_items || slot < 0) continue;
+      const float* cs = cos_sin + positions[t0 + kk[u]] * d;
+      const int c = cc_[u];
+      const float4 c0 = *reinterpret_cast<const float4*>(cs + c * 8);
+      const float4 c1 = *reinterpret_cast<const float4*>(cs + c * 8 + 4);
+      const float4 s0 = *reinterpret_cast<const float4*>(cs + half + c * 8);
+      const float4 s1 = *reinterpret_cast<const float4*>(cs + half + c * 8 + 4);
+      const float co[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      const float si[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      Pack8<T> oa, ob;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float ra, rb;
+        neox_rot(to_f(a[u].h[j]), to_f(b[u].h[j]), co[j], si[j], ra, rb);
+        oa.h[j] = from_f<T>(ra);
+        ob.h[j] = from_f<T>(rb);
+      }
+      T* dst = k_cache + (((slot / bs) * nkv + hh[u]) * bs + slot % bs) * (int64_t)d;
+      *reinterpret_cast<u32x4*>(dst + c * 8) = oa.u;
+      *reinterpret_cast<u32x4*>(dst + half + c * 8) = ob.u;
+    }
+  }
+  // V: item (head h, chunk c) over the group's tokens
+  __syncthreads();
+  const bool full = s_full;
+  for (int iv = threadIdx.x; iv < nkv * cpr; iv += KVG_NT) {
+    const int h = iv / cpr, c = iv % cpr;
+    const T* src = qkv + (int64_t)t0 * qkv_stride + (int64_t)(nq + nkv + h) * d + c * 8;
+    if (full) {
+      Pack8<T> vv[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) vv[k].u = *reinterpret_cast<const u32x4*>(src + k * qkv_stride);
+      const int64_t slot = s_slot[0];
+      const int off = (int)(slot % bs);
+      T* dst = v_cache + ((slot / bs) * nkv + h) * (int64_t)bs * d +
+               ((int64_t)(off >> 3) * d + c * 8) * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        Pack8<T> o;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o.h[k] = vv[k].h[j];
+        *reinterpret_cast<u32x4*>(dst + j * 8) = o.u;
+      }
+    } else {
+      for (int k = 0; k < nt; ++k) {
+        const int64_t slot = s_slot[k];
+        if (slot < 0) continue;
+        Pack8<T> v;
+        v.u = *reinterpret_cast<const u32x4*>(src + k * qkv_stride);
+        const int off = (int)(slot % bs);
+        T* dst = v_cache + ((slot / bs) * nkv + h) * (int64_t)bs * d +
+                 ((int64_t)(off >> 3) * d + c * 8) * 8 + (off & 7);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dst[j * 8] = v.h[j];
+      }
+    }
+  }
+}
+
+// KGC_ROPE_KVG=0: prefill K / V writes on the per-token kernel (A/B)
+static bool rope_kvg() {
+  const char* e = getenv("KGC_ROPE_KVG");
+  return !(e && atoi(e) == 0);
+}
+
 // KGC_ROPE_VGROUP=1: the whole-group V^T stores above.  Off by default: measured slower
 // at 16K-token prefill chunks (tools/prefill_rope_bench.py: rope_kv_write 152 -> 173 us,
 // k/v-only 85 -> 94 us; the eight-token leaders serialise what 8 threads did in parallel,
@@ -253,6 +369,14 @@ static void rope_dispatch(const void* qkv, int64_t qkv_stride, int S, int64_t ss
       qkv, qkv_stride, S, ss, pos, cs, (T*)q_out, kc, vc, slots, (const T*)qn,               \
       (const T*)kn, nq, nkv, d, bs, eps, k_inv, v_inv, num_blocks, rope_vgroup())
   const bool norm = qn != nullptr;
+  if constexpr (!KV8 && !SL) {
+    if (kvo && rope && !norm && rope_kvg() && (d & 15) == 0 && (bs & 7) == 0) {
+      kv_group_kernel<T><<<(T_ + 7) / 8, KVG_NT, 0, s>>>(
+          (const T*)qkv, qkv_stride, pos, cs, (T*)kc, (T*)vc, slots, T_, nq, nkv, d, bs,
+          num_blocks);
+      return;
+    }
+  }
   if (kvo) {                    // prefill-only steps of RoPE models without q/k norm
     if (rope && !norm) KGC_ROPE_LAUNCH(false, true, true);
     else if (rope) KGC_ROPE_LAUNCH(true, true, true);

@@ -215,6 +215,14 @@ def _decode_z_cap(ws, B: int, nq: int) -> int:
     return ml.shape[-1]
 
 
+def _merge_z_cap(nq: int, nkv: int) -> int:
+    """K1w merges the G = nq / nkv heads x Z slices of a (seq, kv-head) in one wave's
+    LDS (attention_decode.hip DEC_MERGE_MAX = 1024 entries)."""
+    if not decode_wave_kernel():
+        return 1024
+    return max(1, 1024 // max(1, nq // max(1, nkv)))
+
+
 def decode_grid_z(batch: int, num_kv_heads: int, max_ctx: int, target_waves: int = 0) -> int:
     """z-slices of the decode grid: enough waves to fill 256 CUs, bounded by the
     context (K1w: two 32-token chunks per wave; 4-wave kernel: 64-token partitions) and by
@@ -243,7 +251,7 @@ def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torc
     if workspace is None:
         workspace = decode_partials(B, nq, d, block_tables.shape[1], k_cache.shape[2], q.device)
     ml, es, tmp, tickets = workspace
-    grid_z = min(grid_z, _decode_z_cap(workspace, B, nq))
+    grid_z = min(grid_z, _decode_z_cap(workspace, B, nq), _merge_z_cap(nq, k_cache.shape[1]))
     _k().paged_decode(out, q, k_cache, v_cache, block_tables, context_lens, ml, es, tmp,
                       tickets, grid_z, scale, k_scale, v_scale)
     return out
@@ -277,7 +285,8 @@ def paged_attention_decode_rope(qkv: torch.Tensor, positions: torch.Tensor,
         workspace = decode_partials(B, num_heads, head_dim, block_tables.shape[1],
                                     k_cache.shape[2], qkv.device)
     ml, es, tmp, tickets = workspace
-    grid_z = min(grid_z, _decode_z_cap(workspace, B, num_heads))
+    grid_z = min(grid_z, _decode_z_cap(workspace, B, num_heads),
+                 _merge_z_cap(num_heads, num_kv_heads))
     _k().paged_decode_rope(out, qkv, positions, cos_sin, k_cache, v_cache, slot_mapping,
                            q_norm_w, k_norm_w, block_tables, context_lens, ml, es, tmp, tickets,
                            num_heads, grid_z, scale, eps, use_rope, k_scale, v_scale)

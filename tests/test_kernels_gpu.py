@@ -260,8 +260,8 @@ def test_prefill_attention(gpu, dt, d, nq, nkv):
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("gqa,d,nq,nkv", [("1", 128, 32, 8), ("0", 128, 32, 8),
                                          ("1", 128, 64, 8), ("0", 64, 4, 4)])
-@pytest.mark.parametrize("vgroup", ["0", "1"])
-def test_prefill_rope_fused_equals_unfused(gpu, monkeypatch, dt, gqa, d, nq, nkv, vgroup):
+@pytest.mark.parametrize("vgroup,kvg", [("0", "1"), ("0", "0"), ("1", "0")])
+def test_prefill_rope_fused_equals_unfused(gpu, monkeypatch, dt, gqa, d, nq, nkv, vgroup, kvg):
     """Prefill-only step with q RoPE folded into K2's q load (kv_write_rope +
     prefill_attention_rope) vs rope_kv_write + prefill_attention: the same K/V cache bytes,
     the same attention output (the rotation is one shared helper, rounded the same way),
@@ -269,6 +269,7 @@ def test_prefill_rope_fused_equals_unfused(gpu, monkeypatch, dt, gqa, d, nq, nkv
     continuations (positions = context start + row), GQA-shared and one-head kernels."""
     monkeypatch.setenv("KGC_PREFILL_GQA", gqa)
     monkeypatch.setenv("KGC_ROPE_VGROUP", vgroup)     # whole-group V^T stores on / off
+    monkeypatch.setenv("KGC_ROPE_KVG", kvg)           # 8-token-group K / V kernel on / off
     torch.manual_seed(11)
     bs = 16
     seq_lens = [5, 130, 300, 64, 700]

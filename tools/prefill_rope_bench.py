@@ -68,7 +68,8 @@ def main():
     ws = torch.tensor(ws, dtype=torch.int32, device=dev)
     wm = torch.tensor(wm, dtype=torch.int32, device=dev)
     q = ops.rope_kv_write(qkv, pos, cs, kc, vc, slots, nq, nkv, d)
-    tag = {"vgroup": os.environ.get("KGC_ROPE_VGROUP", "0"), "T": T}
+    tag = {"vgroup": os.environ.get("KGC_ROPE_VGROUP", "0"),
+           "kvg": os.environ.get("KGC_ROPE_KVG", "1"), "T": T}
     res = {
         "rope_kv_write": timeit(lambda: ops.rope_kv_write(qkv, pos, cs, kc, vc, slots, nq, nkv, d)),
         "kv_write_rope (k/v only)": timeit(lambda: ops.kv_write_rope(qkv, pos, cs, kc, vc, slots,
