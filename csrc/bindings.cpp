@@ -163,17 +163,22 @@ void check_kv(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, int
   check_same_dev(q, v_cache, "v_cache");
 }
 
-// tickets: int32 >= B * nkv, zeroed once (K1w's in-launch merge re-arms them)
-static int* decode_tickets(const Tensor& tickets, int64_t B, int64_t nkv, const Tensor& ref) {
-  TORCH_CHECK(tickets.scalar_type() == at::kInt && tickets.is_contiguous() &&
-              tickets.numel() >= B * nkv && tickets.device() == ref.device(),
-              "decode tickets: int32 [>= B * nkv] on the kernel's device");
-  return tickets.data_ptr<int>();
+// Z > 1 partials: fp32, contiguous, >= B * nq * Z rows (row (seq, q-head) * Z + z)
+static void check_partials(const Tensor& ml, const Tensor& es, const Tensor& tmp, int64_t B,
+                           int64_t nq, int64_t d, int64_t Z, const char* who) {
+  TORCH_CHECK(ml.scalar_type() == at::kFloat && es.scalar_type() == at::kFloat &&
+              tmp.scalar_type() == at::kFloat, who, ": partials fp32");
+  TORCH_CHECK(ml.is_contiguous() && es.is_contiguous() && tmp.is_contiguous() &&
+              ml.numel() >= B * nq * Z && es.numel() >= B * nq * Z &&
+              tmp.numel() >= B * nq * Z * d, who, ": partials hold fewer than B * nq * Z rows");
+  TORCH_CHECK(Z >= 1 && Z <= 1024, who, ": need 1 <= Z <= 1024");
+  TORCH_CHECK(ml.device() == tmp.device() && es.device() == tmp.device(), who,
+              ": partials on one device");
 }
 
 void paged_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_tables,
                   Tensor ctx_lens, Tensor max_logits, Tensor exp_sums, Tensor tmp_out,
-                  Tensor tickets, int64_t Z, double scale, double k_scale, double v_scale) {
+                  int64_t Z, double scale, double k_scale, double v_scale) {
   check_gpu(q, "q");
   c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
   TORCH_CHECK(q.dim() == 3 && q.is_contiguous(), "q [B, nq, d] contiguous");
@@ -184,26 +189,14 @@ void paged_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor b
   TORCH_CHECK(block_tables.scalar_type() == at::kInt && block_tables.dim() == 2 &&
               block_tables.size(0) >= B && block_tables.is_contiguous(), "block_tables int32 [B, max_blocks] contiguous");
   TORCH_CHECK(ctx_lens.scalar_type() == at::kInt && ctx_lens.numel() >= B, "ctx_lens int32 [B]");
-  TORCH_CHECK(max_logits.scalar_type() == at::kFloat && exp_sums.scalar_type() == at::kFloat &&
-              tmp_out.scalar_type() == at::kFloat, "partials fp32");
-  // K1w (one wave per z-slice) packs the partial rows Z apart, so the workspace only has
-  // to hold B * nq * Z of them; the 4-wave kernel strides them by the last dim (Zmax)
-  const int64_t Zmax = kgc::paged_decode_waves_per_slice() == 1 ? Z : max_logits.size(-1);
-  TORCH_CHECK(max_logits.is_contiguous() && exp_sums.is_contiguous() && tmp_out.is_contiguous() &&
-              max_logits.numel() >= B * nq * Zmax && exp_sums.numel() >= B * nq * Zmax &&
-              tmp_out.numel() >= B * nq * Zmax * d, "partials too small");
-  TORCH_CHECK(Z >= 1 && Z <= Zmax && Z <= 1024,
-              "kgc.paged_decode: need 1 <= Z <= min(partial slots, 1024)");
-  TORCH_CHECK(kgc::paged_decode_waves_per_slice() != 1 || Z * (nq / k_cache.size(1)) <= 1024,
-              "kgc.paged_decode: K1w merges G * Z <= 1024 partials");
+  check_partials(max_logits, exp_sums, tmp_out, B, nq, d, Z, "kgc.paged_decode");
+  check_same_dev(q, tmp_out, "partials");
   kgc::launch_paged_decode(dt_code(q), out.data_ptr(), q.data_ptr(), k_cache.data_ptr(),
                            v_cache.data_ptr(), block_tables.data_ptr<int>(),
                            (int)block_tables.stride(0), ctx_lens.data_ptr<int>(),
                            max_logits.data_ptr<float>(), exp_sums.data_ptr<float>(),
-                           tmp_out.data_ptr<float>(),
-                           decode_tickets(tickets, B, k_cache.size(1), q),
-                           (int)B, (int)nq, (int)k_cache.size(1),
-                           (int)d, log2_exact(k_cache.size(2), "block_size"), (int)Zmax, (int)Z,
+                           tmp_out.data_ptr<float>(), (int)B, (int)nq, (int)k_cache.size(1),
+                           (int)d, log2_exact(k_cache.size(2), "block_size"), (int)Z,
                            (float)scale, k_cache.scalar_type() == at::kFloat8_e4m3fn,
                            (float)k_scale, (float)v_scale, (int)k_cache.size(0), stream());
 }
@@ -213,8 +206,7 @@ void paged_decode(Tensor out, Tensor q, Tensor k_cache, Tensor v_cache, Tensor b
 void paged_decode_rope(Tensor out, Tensor qkv, Tensor positions, Tensor cos_sin, Tensor k_cache,
                        Tensor v_cache, Tensor slot_mapping, std::optional<Tensor> q_norm_w,
                        std::optional<Tensor> k_norm_w, Tensor block_tables, Tensor ctx_lens,
-                       Tensor max_logits, Tensor exp_sums, Tensor tmp_out, Tensor tickets,
-                       int64_t nq,
+                       Tensor max_logits, Tensor exp_sums, Tensor tmp_out, int64_t nq,
                        int64_t Z, double scale, double eps, bool use_rope, double k_scale,
                        double v_scale) {
   check_gpu(qkv, "qkv");
@@ -249,20 +241,10 @@ void paged_decode_rope(Tensor out, Tensor qkv, Tensor positions, Tensor cos_sin,
               block_tables.size(0) >= B && block_tables.is_contiguous(),
               "block_tables int32 [B, max_blocks] contiguous");
   TORCH_CHECK(ctx_lens.scalar_type() == at::kInt && ctx_lens.numel() >= B, "ctx_lens int32 [B]");
-  TORCH_CHECK(max_logits.scalar_type() == at::kFloat && exp_sums.scalar_type() == at::kFloat &&
-              tmp_out.scalar_type() == at::kFloat, "partials fp32");
-  // K1w (one wave per z-slice) packs the partial rows Z apart, so the workspace only has
-  // to hold B * nq * Z of them; the 4-wave kernel strides them by the last dim (Zmax)
-  const int64_t Zmax = kgc::paged_decode_waves_per_slice() == 1 ? Z : max_logits.size(-1);
-  TORCH_CHECK(max_logits.is_contiguous() && exp_sums.is_contiguous() && tmp_out.is_contiguous() &&
-              max_logits.numel() >= B * nq * Zmax && exp_sums.numel() >= B * nq * Zmax &&
-              tmp_out.numel() >= B * nq * Zmax * d, "partials too small");
-  TORCH_CHECK(Z >= 1 && Z <= Zmax && Z <= 1024,
-              "kgc.paged_decode_rope: need 1 <= Z <= min(partial slots, 1024)");
-  TORCH_CHECK(kgc::paged_decode_waves_per_slice() != 1 || Z * (nq / nkv) <= 1024,
-              "kgc.paged_decode_rope: K1w merges G * Z <= 1024 partials");
+  check_partials(max_logits, exp_sums, tmp_out, B, nq, d, Z, "kgc.paged_decode_rope");
   TORCH_CHECK(k_scale > 0 && v_scale > 0, "kv scales must be > 0");
-  for (const Tensor* t : {&qkv, &positions, &cos_sin, &slot_mapping, &block_tables, &ctx_lens})
+  for (const Tensor* t : {&qkv, &positions, &cos_sin, &slot_mapping, &block_tables, &ctx_lens,
+                          &tmp_out})
     check_same_dev(out, *t, "paged_decode_rope operand");
   if (q_norm_w.has_value()) {
     TORCH_CHECK(k_norm_w.has_value() && q_norm_w->numel() == d && k_norm_w->numel() == d &&
@@ -283,9 +265,8 @@ void paged_decode_rope(Tensor out, Tensor qkv, Tensor positions, Tensor cos_sin,
                                 v_cache.data_ptr(), block_tables.data_ptr<int>(),
                                 (int)block_tables.stride(0), ctx_lens.data_ptr<int>(),
                                 max_logits.data_ptr<float>(), exp_sums.data_ptr<float>(),
-                                tmp_out.data_ptr<float>(), decode_tickets(tickets, B, nkv, out),
-                                (int)B, (int)nq, (int)nkv, (int)d,
-                                log2_exact(k_cache.size(2), "block_size"), (int)Zmax, (int)Z,
+                                tmp_out.data_ptr<float>(), (int)B, (int)nq, (int)nkv, (int)d,
+                                log2_exact(k_cache.size(2), "block_size"), (int)Z,
                                 (float)scale, k_cache.scalar_type() == at::kFloat8_e4m3fn,
                                 (float)k_scale, (float)v_scale, (int)k_cache.size(0), stream());
 }
@@ -1052,8 +1033,7 @@ std::vector<int64_t> sample_stamps() {
   return std::vector<int64_t>(st, st + 16);
 }
 
-int64_t decode_partition_size() { return kgc::paged_decode_partition_size(); }
-int64_t decode_waves_per_slice() { return kgc::paged_decode_waves_per_slice(); }
+int64_t decode_wave_min_pairs() { return kgc::paged_decode_wave_min_pairs(); }
 int64_t prefill_block_m() { return kgc::prefill_block_m(); }
 
 }  // namespace
@@ -1068,12 +1048,12 @@ TORCH_LIBRARY(kgc, m) {
         "float v_scale=1.0) -> ()");
   m.def("paged_decode(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
         "Tensor block_tables, Tensor ctx_lens, Tensor(b!) max_logits, Tensor(c!) exp_sums, "
-        "Tensor(d!) tmp_out, Tensor(e!) tickets, int Z, float scale, float k_scale=1.0, "
+        "Tensor(d!) tmp_out, int Z, float scale, float k_scale=1.0, "
         "float v_scale=1.0) -> ()");
   m.def("paged_decode_rope(Tensor(a!) out, Tensor qkv, Tensor positions, Tensor cos_sin, "
         "Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor slot_mapping, Tensor? q_norm_w, "
         "Tensor? k_norm_w, Tensor block_tables, Tensor ctx_lens, Tensor(d!) max_logits, "
-        "Tensor(e!) exp_sums, Tensor(f!) tmp_out, Tensor(g!) tickets, int nq, int Z, "
+        "Tensor(e!) exp_sums, Tensor(f!) tmp_out, int nq, int Z, "
         "float scale, float eps, bool use_rope, float k_scale=1.0, float v_scale=1.0) -> ()");
   m.def("prefill_attention(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
         "Tensor block_tables, Tensor query_start_loc, Tensor seq_lens, Tensor work_seq, "
@@ -1087,8 +1067,7 @@ TORCH_LIBRARY(kgc, m) {
   m.def("sample_vp(Tensor(a!) packed, Tensor logits, int V, Tensor temperature, Tensor seeds, "
         "int vocab_off) -> ()");
   m.def("sample_vp_unpack(Tensor(a!) out, Tensor packed) -> ()");
-  m.def("decode_partition_size() -> int", &decode_partition_size);
-  m.def("decode_waves_per_slice() -> int", &decode_waves_per_slice);
+  m.def("decode_wave_min_pairs() -> int", &decode_wave_min_pairs);
   m.def("moe_route(Tensor(a!) topk_w, Tensor(b!) topk_ids, Tensor logits, bool renorm) -> ()");
   m.def("moe_align(Tensor(a!) sorted_ids, Tensor(b!) block_expert, Tensor(c!) meta, "
         "Tensor topk_ids, int e0, int E_local, int bm) -> ()");

@@ -41,7 +41,9 @@ namespace kgc {
 constexpr int DEC_PART = 64;     // tokens per partition (one wave-iteration)
 constexpr int DEC_CHUNKS = DEC_PART / 32;
 constexpr int DEC_MAX_Z = 1024;  // z-slices the reduce kernel merges (host-checked)
-constexpr int DEC_MERGE_MAX = 1024;  // K1w: G * Z (heads x slices) one merge holds
+// K1w runs where the grid has at least this many (seq, kv-head) pairs; smaller batches
+// take the 4-wave kernel (B = 1: 9.3 vs 12.3 us at ctx 640; ops/__init__.py mirrors it)
+constexpr int DEC_WAVE_MIN_PAIRS = 64;
 
 // K1w: 32-token chunks per z-slice (>= 2, the pipeline depth); slices past the context are
 // empty and the reduce stops at decode_used_slices
@@ -466,9 +468,8 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
     T* __restrict__ out, const T* __restrict__ q, const void* __restrict__ kc_,
     const void* __restrict__ vc_, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ ctx_lens, float* __restrict__ max_logits,
-    float* __restrict__ exp_sums, float* __restrict__ tmp_out, int* __restrict__ tickets,
-    int nq, int nkv, int bs_log2, float scale_log2, float v_scale, int num_blocks,
-    DecodeRope rp) {
+    float* __restrict__ exp_sums, float* __restrict__ tmp_out, int nq, int nkv, int bs_log2,
+    float scale_log2, float v_scale, int num_blocks, DecodeRope rp) {
   typedef typename Vec8<T>::type V8;
   typedef std::conditional_t<KV8, uint8_t, T> C;
   const C* __restrict__ kc = reinterpret_cast<const C*>(kc_);
@@ -479,8 +480,6 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
   };
   constexpr int KS = D / 32, DT = D / 16;
   __shared__ __attribute__((aligned(16))) T lds_q[FUSE ? 16 : 1][FUSE ? D + 8 : 8];
-  // Z > 1: the last slice's merge state ((g, slice) max -> weight, sum; 1/sum per head)
-  __shared__ float wz_s[DEC_MERGE_MAX], ez_s[DEC_MERGE_MAX], inv_s[16];
   const int b = blockIdx.x, h = blockIdx.y, z = blockIdx.z, Z = gridDim.z;
   const int lane = threadIdx.x;
   const int r16 = lane & 15, qd = lane >> 4;
@@ -751,103 +750,39 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
     }
     return;
   }
-  // Z > 1: the used slices write (max, sum, O) partials write-through (sc1 stores: no
-  // release fence needed), then draw a ticket; the slice that draws the last one merges
-  // all of them in this launch (no reduce kernel: at B = 1 its launch cost as much as the
-  // merge) and re-arms the ticket for the next launch / graph replay.
-  const int nz = decode_used_slices(nchunk, Z);
-  if (nz == 0) {                         // empty context (graph padding): a zero row
-    if (z == 0 && r16 < G) {
-      T* orow = out + row * D + 4 * qd;
+  // Z > 1: the used slices write (max, sum, O) partials at row * Z + z; slices past the
+  // context write nothing (paged_decode_reduce_kernel merges slices 0 .. nz - 1 only).
+  // (A merge by the last-arriving slice inside this launch -- sc1 partials, a ticket per
+  // (seq, kv-head) -- measured slower than the reduce launch at every Z > 1 shape: B = 32
+  // 59.2 vs 52.8 us, B = 1 12.9 vs 12.3 us; one wave merging G heads serialises what the
+  // reduce spreads over B * nq waves.  profiles/README.md "K1w".)
+  if (z >= decode_used_slices(nchunk, Z) || r16 >= G) return;
+  const int64_t prow = row * Z + z;
+  float* dst = tmp_out + prow * D + 4 * qd;
 #pragma unroll
-      for (int t = 0; t < DT; ++t) *reinterpret_cast<u32x2*>(orow + 16 * t) = u32x2{0u, 0u};
-    }
-    return;
-  }
-  if (z >= nz) return;                   // an empty slice: no partial, no ticket
-  if (r16 < G) {
-    const int64_t prow = row * Z + z;
-    float* dst = tmp_out + prow * D + 4 * qd;
-#pragma unroll
-    for (int t = 0; t < DT; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        __hip_atomic_store(dst + 16 * t + i, o[t][i] * v_scale, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    if (qd == 0) {
-      __hip_atomic_store(max_logits + prow, m_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(exp_sums + prow, l_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every partial store has landed
-  int* tk = tickets + (int64_t)b * nkv + h;
-  int old = 0;
-  if (lane == 0) old = __hip_atomic_fetch_add(tk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  old = __shfl(old, 0, 64);
-  if (old != nz - 1) return;
-  if (lane == 0) __hip_atomic_store(tk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");    // the other slices' partials
-  // Merge of the G heads x nz slices, every phase with its loads issued together (a
-  // per-slice loop of dependent L2 round trips made this merge cost 35 us at B = 1):
-  //   1. (max, sum) of all (g, slice) pairs -> LDS (lane-parallel, one round trip);
-  //   2. per head: max, weights, 1/sum from LDS;
-  //   3. O: G*D/4 float4 columns per slice, 8 slices of loads in flight per lane.
-  // The host keeps G * Z <= DEC_MERGE_MAX.
-  const int64_t rb = ((int64_t)b * nq + h * G) * Z;     // (g, zz) at rb + g * Z + zz
-  const int GN = G * nz;
-  for (int i = lane; i < GN; i += 64) {
-    const int g = i / nz, zz = i - g * nz;
-    wz_s[i] = max_logits[rb + g * Z + zz];
-    ez_s[i] = exp_sums[rb + g * Z + zz];
-  }
-  for (int g = 0; g < G; ++g) {
-    float M = -INFINITY;
-    for (int zz = lane; zz < nz; zz += 64) M = fmaxf(M, wz_s[g * nz + zz]);
-    M = wave_max(M);
-    float Lp = 0.f;
-    for (int zz = lane; zz < nz; zz += 64) {
-      const float w = M == -INFINITY ? 0.f : exp2f(wz_s[g * nz + zz] - M);
-      wz_s[g * nz + zz] = w;
-      Lp += w * ez_s[g * nz + zz];
-    }
-    const float L = wave_sum(Lp);
-    if (lane == 0) inv_s[g] = L > 0.f ? 1.f / L : 0.f;
-  }
-  constexpr int D4 = D / 4;
-  for (int e = lane; e < G * D4; e += 64) {
-    const int g = e / D4, c4 = e - g * D4;
-    const float* src = tmp_out + (rb + (int64_t)g * Z) * D + 4 * c4;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int z0 = 0; z0 < nz; z0 += 8) {
-      f32x4 v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        v[j] = *reinterpret_cast<const f32x4*>(src + (int64_t)min(z0 + j, nz - 1) * D);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (z0 + j < nz) acc += wz_s[g * nz + z0 + j] * v[j];
-    }
-    const float inv = inv_s[g];
-    Pack4<T> pk;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) pk.h[i] = from_f<T>(acc[i] * inv);
-    *reinterpret_cast<u32x2*>(out + ((int64_t)b * nq + h * G + g) * D + 4 * c4) = pk.u;
+  for (int t = 0; t < DT; ++t)
+    *reinterpret_cast<f32x4*>(dst + 16 * t) = o[t] * v_scale;
+  if (qd == 0) {
+    max_logits[prow] = m_run;
+    exp_sums[prow] = l_run;
   }
 }
 
-// Merge the Z z-slice partials of the 4-wave kernel: one 64-thread wave per (seq, q-head).
-// (K1w merges in-launch: the last slice of each (seq, kv-head) does it.)
-template <typename T, int D>
+// Merge the z-slice partials: one 64-thread wave per (seq, q-head).  WAVE (K1w): only the
+// sequence's used slices wrote a partial (decode_used_slices); the 4-wave kernel writes
+// all Z (empty ones with weight 0).
+template <typename T, int D, bool WAVE>
 __global__ __launch_bounds__(64) void paged_decode_reduce_kernel(
     T* __restrict__ out, const float* __restrict__ max_logits,
     const float* __restrict__ exp_sums, const float* __restrict__ tmp_out,
-    const int* __restrict__ ctx_lens, int nq, int Z, int Zmax) {
+    const int* __restrict__ ctx_lens, int nq, int Zg, int Zmax) {
   // The slice statistics are read in parallel (lane z), the weights staged in LDS,
   // and the partial rows loaded 8 slices at a time: the previous per-slice loop was a
   // chain of dependent L2 round trips (~7 us per call at B = 1; decode + reduce for
   // B = 1, ctx 565, Z = 16 went 13.0 -> 9.3 us).
   __shared__ float wz[DEC_MAX_Z];
   const int b = blockIdx.x, hq = blockIdx.y, tid = threadIdx.x;
+  const int Z = WAVE ? decode_used_slices((max(ctx_lens[b], 0) + 31) >> 5, Zg) : Zg;
   T* orow = out + ((int64_t)b * nq + hq) * D;
   constexpr int EPT = D / 64;
   const int64_t base = ((int64_t)b * nq + hq) * Zmax;
@@ -898,43 +833,56 @@ bool decode_wave_enabled() {
   return v;
 }
 
+// K1w for grids of >= DEC_WAVE_MIN_PAIRS (seq, kv-head) pairs (unless KGC_DECODE_WAVE=0),
+// else the 4-wave kernel; both write partial rows Z apart (Zmax = Z)
+// (KGC_DECODE_WAVE_MIN_PAIRS overrides the threshold: the tests run both kernels on every
+// shape; ops/__init__.py reads the same variable)
+static int decode_wave_min_pairs() {
+  const char* e = getenv("KGC_DECODE_WAVE_MIN_PAIRS");
+  return e ? atoi(e) : DEC_WAVE_MIN_PAIRS;
+}
+bool decode_use_wave(int B, int nkv) {
+  return decode_wave_enabled() && (int64_t)B * nkv >= decode_wave_min_pairs();
+}
+
 template <typename T, int D, bool KV8, bool FUSE>
 static void decode_dispatch(void* out, const void* q, const void* kc, const void* vc,
                             const int* bt, int bt_stride, const int* ctx, float* ml, float* es,
-                            float* tmp, int* tickets, int B, int nq, int nkv, int bs_log2,
-                            int Zmax, int Z,
+                            float* tmp, int B, int nq, int nkv, int bs_log2, int Z,
                             float scale_log2, float v_scale, int num_blocks,
                             const DecodeRope& rp, hipStream_t s) {
-  if (decode_wave_enabled()) {
-    // partial rows are Z apart (the workspace is sized for B * Z rows per head)
+  const bool wave = decode_use_wave(B, nkv);
+  if (wave) {
     paged_decode_wave_kernel<T, D, KV8, FUSE><<<dim3(B, nkv, Z), 64, 0, s>>>(
-        (T*)out, (const T*)q, kc, vc, bt, bt_stride, ctx, ml, es, tmp, tickets, nq, nkv,
-        bs_log2, scale_log2, v_scale, num_blocks, rp);
-    return;
+        (T*)out, (const T*)q, kc, vc, bt, bt_stride, ctx, ml, es, tmp, nq, nkv, bs_log2,
+        scale_log2, v_scale, num_blocks, rp);
+  } else {
+    paged_decode_kernel<T, D, true, KV8, 4, 1, FUSE><<<dim3(B, nkv, Z), 256, 0, s>>>(
+        (T*)out, (const T*)q, kc, vc, bt, bt_stride, ctx, ml, es, tmp, nq, nkv, bs_log2, Z,
+        scale_log2, v_scale, num_blocks, rp);
   }
-  auto kern = paged_decode_kernel<T, D, true, KV8, 4, 1, FUSE>;
-  kern<<<dim3(B, nkv, Z), 256, 0, s>>>(
-      (T*)out, (const T*)q, kc, vc, bt, bt_stride, ctx, ml, es, tmp, nq,
-      nkv, bs_log2, Zmax, scale_log2, v_scale, num_blocks, rp);
-  if (Z > 1)
-    paged_decode_reduce_kernel<T, D><<<dim3(B, nq), 64, 0, s>>>((T*)out, ml, es, tmp, ctx, nq,
-                                                                Z, Zmax);
+  if (Z == 1) return;
+  if (wave)
+    paged_decode_reduce_kernel<T, D, true><<<dim3(B, nq), 64, 0, s>>>((T*)out, ml, es, tmp, ctx,
+                                                                      nq, Z, Z);
+  else
+    paged_decode_reduce_kernel<T, D, false><<<dim3(B, nq), 64, 0, s>>>((T*)out, ml, es, tmp,
+                                                                       ctx, nq, Z, Z);
 }
 
 template <bool FUSE>
 static void decode_launch(int dtype, void* out, const void* q, const void* k_cache,
                           const void* v_cache, const int* block_tables, int bt_stride,
                           const int* ctx_lens, float* max_logits, float* exp_sums,
-                          float* tmp_out, int* tickets, int B, int nq, int nkv, int D,
-                          int bs_log2, int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
-                          float v_scale, int num_blocks, const DecodeRope& rp, hipStream_t s) {
+                          float* tmp_out, int B, int nq, int nkv, int D, int bs_log2, int Z,
+                          float scale, bool kv_fp8, float k_scale, float v_scale, int num_blocks,
+                          const DecodeRope& rp, hipStream_t s) {
   if (B == 0) return;
   const float sl2 = scale * k_scale * 1.4426950408889634f;
 #define KGC_DEC(TT, DD, K8)                                                                 \
   decode_dispatch<TT, DD, K8, FUSE>(out, q, k_cache, v_cache, block_tables, bt_stride,       \
-                                    ctx_lens, max_logits, exp_sums, tmp_out, tickets, B, nq, \
-                                    nkv,                                                     \
-                                    bs_log2, Zmax, Z, sl2, v_scale, num_blocks, rp, s)
+                                    ctx_lens, max_logits, exp_sums, tmp_out, B, nq, nkv,    \
+                                    bs_log2, Z, sl2, v_scale, num_blocks, rp, s)
 #define KGC_DEC_D(TT, K8) \
   if (D == 128) KGC_DEC(TT, 128, K8); else KGC_DEC(TT, 64, K8)
   if (dtype == DT_BF16) {
@@ -949,28 +897,27 @@ static void decode_launch(int dtype, void* out, const void* q, const void* k_cac
 void launch_paged_decode(int dtype, void* out, const void* q, const void* k_cache,
                          const void* v_cache, const int* block_tables, int bt_stride,
                          const int* ctx_lens, float* max_logits, float* exp_sums,
-                         float* tmp_out, int* tickets, int B, int nq, int nkv, int D,
-                         int bs_log2, int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
-                         float v_scale, int num_blocks, hipStream_t s) {
+                         float* tmp_out, int B, int nq, int nkv, int D, int bs_log2, int Z,
+                         float scale, bool kv_fp8, float k_scale, float v_scale, int num_blocks,
+                         hipStream_t s) {
   const DecodeRope none{};
   decode_launch<false>(dtype, out, q, k_cache, v_cache, block_tables, bt_stride, ctx_lens,
-                       max_logits, exp_sums, tmp_out, tickets, B, nq, nkv, D, bs_log2, Zmax, Z,
-                       scale, kv_fp8, k_scale, v_scale, num_blocks, none, s);
+                       max_logits, exp_sums, tmp_out, B, nq, nkv, D, bs_log2, Z, scale, kv_fp8,
+                       k_scale, v_scale, num_blocks, none, s);
 }
 
 void launch_paged_decode_rope(int dtype, const DecodeRope& rp, void* out, void* k_cache,
                               void* v_cache, const int* block_tables, int bt_stride,
                               const int* ctx_lens, float* max_logits, float* exp_sums,
-                              float* tmp_out, int* tickets, int B, int nq, int nkv, int D,
-                              int bs_log2, int Zmax, int Z, float scale, bool kv_fp8,
-                              float k_scale, float v_scale, int num_blocks, hipStream_t s) {
+                              float* tmp_out, int B, int nq, int nkv, int D, int bs_log2,
+                              int Z, float scale, bool kv_fp8, float k_scale, float v_scale,
+                              int num_blocks, hipStream_t s) {
   decode_launch<true>(dtype, out, nullptr, k_cache, v_cache, block_tables, bt_stride, ctx_lens,
-                      max_logits, exp_sums, tmp_out, tickets, B, nq, nkv, D, bs_log2, Zmax, Z,
-                      scale, kv_fp8, k_scale, v_scale, num_blocks, rp, s);
+                      max_logits, exp_sums, tmp_out, B, nq, nkv, D, bs_log2, Z, scale, kv_fp8,
+                      k_scale, v_scale, num_blocks, rp, s);
 }
 
-int paged_decode_partition_size() { return decode_wave_enabled() ? 32 : DEC_PART; }
-int paged_decode_waves_per_slice() { return decode_wave_enabled() ? 1 : 4; }
+int paged_decode_wave_min_pairs() { return decode_wave_enabled() ? decode_wave_min_pairs() : -1; }
 
 KGC_DEBUG_TU(attention_decode)
 

@@ -20,17 +20,17 @@ void launch_rope_kv_write(int dtype, const void* qkv, int64_t qkv_stride, int S,
                           const void* q_norm_w, const void* k_norm_w, int T, int nq, int nkv,
                           int d, int bs, float eps, bool use_rope, bool kv_fp8, float k_scale,
                           float v_scale, int num_blocks, hipStream_t s);
-// tickets: [B * nkv] int32, zero before the first launch (K1w, Z > 1: the last slice of a
-// (seq, kv-head) merges the partials in-launch and re-arms its ticket)
+// Z > 1: the partials hold B * nq * Z rows (row (seq, q-head) * Z + z), merged by a
+// reduce launch
 void launch_paged_decode(int dtype, void* out, const void* q, const void* k_cache,
                          const void* v_cache, const int* block_tables, int bt_stride,
                          const int* ctx_lens, float* max_logits, float* exp_sums,
-                         float* tmp_out, int* tickets, int B, int nq, int nkv, int D,
-                         int bs_log2, int Zmax, int Z, float scale, bool kv_fp8, float k_scale,
-                         float v_scale, int num_blocks, hipStream_t s);
-int paged_decode_partition_size();
-// 1: the K1w kernel (one wave per (seq, kv-head, z-slice)); 4: the 4-wave workgroup kernel
-int paged_decode_waves_per_slice();
+                         float* tmp_out, int B, int nq, int nkv, int D, int bs_log2, int Z,
+                         float scale, bool kv_fp8, float k_scale, float v_scale, int num_blocks,
+                         hipStream_t s);
+// smallest B * nkv that runs K1w (one wave per (seq, kv-head, z-slice)); -1: K1w disabled
+// (KGC_DECODE_WAVE=0) and every launch takes the 4-wave workgroup kernel
+int paged_decode_wave_min_pairs();
 // K1 + K3/K5/K6 fused for decode-only steps: the decode kernel takes the QKV projection
 // row itself (T [B, qkv_stride], or S > 0 fp32 split-K slices [S, B, qkv_stride]),
 // builds q (optional per-head RMSNorm, NeoX RoPE) in the MFMA operand registers, and
@@ -52,9 +52,9 @@ struct DecodeRope {
 void launch_paged_decode_rope(int dtype, const DecodeRope& rp, void* out, void* k_cache,
                               void* v_cache, const int* block_tables, int bt_stride,
                               const int* ctx_lens, float* max_logits, float* exp_sums,
-                              float* tmp_out, int* tickets, int B, int nq, int nkv, int D,
-                              int bs_log2, int Zmax, int Z, float scale, bool kv_fp8,
-                              float k_scale, float v_scale, int num_blocks, hipStream_t s);
+                              float* tmp_out, int B, int nq, int nkv, int D, int bs_log2,
+                              int Z, float scale, bool kv_fp8, float k_scale, float v_scale,
+                              int num_blocks, hipStream_t s);
 void launch_prefill_attention(int dtype, const void* q, void* out, const void* k_cache,
                               const void* v_cache, const int* block_tables, int bt_stride,
                               const int* query_start_loc, const int* seq_lens,

@@ -1,7 +1,7 @@
 // K10 sampler: 1024-thread workgroups over the rows of logits [B, V] (a row's vocabulary
 // split over several workgroups at small batch), then a per-row merge.
 //   temperature <= 1e-5        -> argmax (first index on ties)
-//   otherwise x = logit / temp -> optional top-k threshold (4-pass radix select on the
+//   otherwise x = logit * (1 / temp) -> optional top-k threshold (4-pass radix select on the
 //                                 order-preserving uint32 image of x), optional top-p
 //                                 threshold (radix select on softmax mass, over the top-k
 //                                 support) -> Gumbel-max over the kept support.
@@ -31,6 +31,21 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x *= 0x846ca68bu;
   x ^= x >> 16;
   return x;
+}
+
+// Gumbel noise.  Row key: both halves of the request seed through lowbias32, once per
+// row.  Column gi: ONE lowbias32 round of key ^ gi * golden ratio -> u in (0, 1) ->
+// -ln2 * log2(-log2 u) = -ln(-ln u) - ln2 * log2(ln2): a constant offset of the Gumbel
+// variate (same argmax), as 2 v_log_f32 + 1 mul.  (Two hashes and two libm logf per
+// logit made the temperature pass VALU-bound: ~70 VALU per logit, 78 us per decode step
+// at B = 256 x 128K.)  ops/reference.py uniform_noise / gumbel compute the same values.
+__device__ __forceinline__ uint32_t row_key(uint64_t seed) {
+  return mix32((uint32_t)seed ^ mix32((uint32_t)(seed >> 32) + 0x632BE5ABu));
+}
+__device__ __forceinline__ float gumbel(uint32_t key, int gi) {
+  const uint32_t h = mix32(key ^ ((uint32_t)gi * 0x9E3779B9u));
+  const float u = ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
+  return -0.69314718f * __builtin_amdgcn_logf(-__builtin_amdgcn_logf(u));
 }
 
 __device__ __forceinline__ uint32_t ord_key(float f) {
@@ -129,8 +144,6 @@ __global__ __launch_bounds__(SMP_NT) void sample_kernel(
   const int S = gridDim.y, y = blockIdx.y;
   const int i_lo = (int)((int64_t)V * y / S);
   const int i_hi = (int)((int64_t)V * (y + 1) / S);
-
-  auto xv = [&](float raw) -> float { return greedy ? raw : raw / temp; };
 
   // ---------- thresholds (kept support = x >= thr)
   // Both selects first bin the row by distance from its max (SMP_DB bins per nat, so
@@ -241,19 +254,16 @@ __global__ __launch_bounds__(SMP_NT) void sample_kernel(
   }
 
   // ---------- (Gumbel-)argmax over the support
-  const uint64_t seed = (uint64_t)seeds[b];
-  const uint32_t key = mix32((uint32_t)seed);
-  const uint32_t hi = (uint32_t)(seed >> 32);
+  const uint32_t key = row_key((uint64_t)seeds[b]);
+  const float inv_t = greedy ? 1.f : 1.f / temp;
   float best = -INFINITY;
   int besti = 0x7fffffff;
   visit_row(row, i_lo, i_hi, tid, [&](int i, float r) {
     const int gi = i + vocab_off;                 // global column (vocab-parallel shard)
-    float x = xv(r);
+    float x = r;
     if (!greedy) {
       if (r < thr) return;
-      const uint32_t h = mix32(mix32(key ^ (uint32_t)(gi * 0x9E3779B9u)) + hi);
-      const float u = ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
-      x += -logf(-logf(u));
+      x = r * inv_t + gumbel(key, gi);
     }
     argmax_merge(best, besti, x, gi);
   });
@@ -675,18 +685,15 @@ __global__ __launch_bounds__(SMP_NT) void sample_coop_kernel(
   }
   SMP_STAMP(11);
   // ---------- (Gumbel-)argmax over this workgroup's slice of the support
-  const uint64_t seed = (uint64_t)seeds[b];
-  const uint32_t key = mix32((uint32_t)seed);
-  const uint32_t hi = (uint32_t)(seed >> 32);
+  const uint32_t key = row_key((uint64_t)seeds[b]);
+  const float inv_t = greedy ? 1.f : 1.f / temp;
   float best = -INFINITY;
   int besti = 0x7fffffff;
   visit_row(row, i_lo, i_hi, tid, [&](int i, float r) {
-    float x = greedy ? r : r / temp;
+    float x = r;
     if (!greedy) {
       if (r < thr) return;
-      const uint32_t h = mix32(mix32(key ^ (uint32_t)(i * 0x9E3779B9u)) + hi);
-      const float u = ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
-      x += -logf(-logf(u));
+      x = r * inv_t + gumbel(key, i);
     }
     argmax_merge(best, besti, x, i);
   });

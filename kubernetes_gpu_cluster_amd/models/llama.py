@@ -43,11 +43,12 @@ _tp_ar_norm_enabled = os.environ.get("KGC_TP_AR_NORM", "1") != "0"
 # decode-only steps: RoPE + KV write folded into the paged-decode kernel (KGC_DECODE_ROPE_FUSED=0: off)
 _decode_rope_fused = os.environ.get("KGC_DECODE_ROPE_FUSED", "1") != "0"
 # prefill-only steps of RoPE models without q/k norm: K2 rotates q as it loads it from the
-# QKV row and rope_kv_write handles k / v only (q is never written or re-read).  Off by
-# default: measured on one box at 512-token prompts (profiles/engine_ab_prefill_rope_fused_
-# same_box.jsonl), K2 gets 1.0 ms per 16K-token chunk slower (its short-lived workgroups
-# pay the rotation in their prologue) while rope_kv gets 0.36 ms faster.
-_prefill_rope_fused = os.environ.get("KGC_PREFILL_ROPE_FUSED", "0") == "1"
+# QKV row and the k / v write runs alone (8-token-group kernel, rope_cache.hip
+# kv_group_kernel), so q is never written or re-read.  KGC_PREFILL_ROPE_FUSED=0: off.
+# Round 3 kept it off (profiles/engine_ab_prefill_rope_fused_same_box.jsonl: K2 1.0 ms per
+# 16K-token chunk slower, the per-token k / v write only 0.36 ms faster); the group kernel
+# takes the k / v write from 91 to 24 us per layer (profiles/prefill_rope_kvg_r4.jsonl).
+_prefill_rope_fused = os.environ.get("KGC_PREFILL_ROPE_FUSED", "1") == "1"
 
 
 class RMSNorm(nn.Module):

@@ -166,6 +166,7 @@ def kv_write_rope(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Ten
 DECODE_PARTITION = 64        # tokens per wave-iteration of the 4-wave decode kernel
 DECODE_CHUNK = 32            # tokens per pipelined step of K1w
 DECODE_TARGET_WAVES = 2048   # K1w: 8 resident waves per CU (2 per SIMD at 256 VGPRs)
+DECODE_WAVE_MIN_PAIRS = 64   # attention_decode.hip DEC_WAVE_MIN_PAIRS
 PREFILL_BLOCK_M = 128
 
 
@@ -176,51 +177,39 @@ def decode_wave_kernel() -> bool:
     return os.environ.get("KGC_DECODE_WAVE", "1") != "0"
 
 
+def decode_uses_wave(batch: int, num_kv_heads: int) -> bool:
+    """The kernel a launch of this grid takes: K1w from DECODE_WAVE_MIN_PAIRS (seq, kv-head)
+    pairs up (at B = 1 the 4-wave kernel's 4x finer context split wins: 9.3 vs 12.3 us)."""
+    lim = int(os.environ.get("KGC_DECODE_WAVE_MIN_PAIRS", DECODE_WAVE_MIN_PAIRS))
+    return decode_wave_kernel() and batch * num_kv_heads >= lim
+
+
 def decode_max_z(max_blocks: int, block_size: int) -> int:
-    if decode_wave_kernel():
-        # at least two 32-token chunks per wave (the pipeline depth)
-        chunks = math.ceil(max_blocks * block_size / DECODE_CHUNK)
-        return max(1, min(1024, math.ceil(chunks / 2)))
-    parts = math.ceil(max_blocks * block_size / DECODE_PARTITION)
-    return max(1, math.ceil(parts / 4))
+    """The largest Z either kernel picks for this context capacity."""
+    ctx = max_blocks * block_size
+    wave = math.ceil(math.ceil(ctx / DECODE_CHUNK) / 2)     # >= 2 chunks per K1w slice
+    four = math.ceil(math.ceil(ctx / DECODE_PARTITION) / 4)
+    return max(1, min(1024, max(wave if decode_wave_kernel() else 1, four)))
 
 
 def decode_partials(batch: int, num_heads: int, head_dim: int, max_blocks: int,
                     block_size: int, device) -> tuple:
-    """Per-z-slice (max, sum, O) partials of the split-context decode kernel and its
-    merge tickets (static: graph-capturable).  Unused when the grid has a single z-slice.
-    K1w packs the rows of a launch Z apart, so the workspace holds (seq, z) rows: enough
-    for every Z ``decode_grid_z`` picks at any batch <= ``batch`` (B * Z <= 2 x the wave
-    target + B), flat [rows * heads]; the tickets ([batch * heads] int32, zero) let the
-    last slice of each (seq, kv-head) merge in the same launch and re-arm itself."""
+    """Per-z-slice (max, sum, O) partials of the split-context decode kernels (static:
+    graph-capturable), flat: row (seq, q-head) * Z + z, for every Z ``decode_grid_z`` picks
+    at any batch <= ``batch`` (Z <= decode_max_z, and B * Z bounded by the wave targets:
+    K1w B * nkv * Z <= 2 x 2048, the 4-wave kernel B * nkv * 4 * Z <= 2 x 4096).  Unused
+    when the grid has a single z-slice."""
     Z = decode_max_z(max_blocks, block_size)
-    tickets = torch.zeros(batch * num_heads, dtype=torch.int32, device=device)
-    if decode_wave_kernel():
-        rows = min(batch * Z, 2 * DECODE_TARGET_WAVES + batch)
-        ml = torch.empty(rows * num_heads, dtype=torch.float32, device=device)
-        es = torch.empty(rows * num_heads, dtype=torch.float32, device=device)
-        tmp = torch.empty(rows * num_heads, head_dim, dtype=torch.float32, device=device)
-        return ml, es, tmp, tickets
-    ml = torch.empty(batch, num_heads, Z, dtype=torch.float32, device=device)
-    es = torch.empty(batch, num_heads, Z, dtype=torch.float32, device=device)
-    tmp = torch.empty(batch, num_heads, Z, head_dim, dtype=torch.float32, device=device)
-    return ml, es, tmp, tickets
+    rows = min(batch * Z, 2 * 4096 + batch)
+    ml = torch.empty(rows * num_heads, dtype=torch.float32, device=device)
+    es = torch.empty(rows * num_heads, dtype=torch.float32, device=device)
+    tmp = torch.empty(rows * num_heads, head_dim, dtype=torch.float32, device=device)
+    return ml, es, tmp
 
 
 def _decode_z_cap(ws, B: int, nq: int) -> int:
     """Largest Z the workspace holds for a batch of B rows of nq heads."""
-    ml = ws[0]
-    if decode_wave_kernel():
-        return max(1, ml.numel() // max(1, B * nq))
-    return ml.shape[-1]
-
-
-def _merge_z_cap(nq: int, nkv: int) -> int:
-    """K1w merges the G = nq / nkv heads x Z slices of a (seq, kv-head) in one wave's
-    LDS (attention_decode.hip DEC_MERGE_MAX = 1024 entries)."""
-    if not decode_wave_kernel():
-        return 1024
-    return max(1, 1024 // max(1, nq // max(1, nkv)))
+    return max(1, min(1024, ws[0].numel() // max(1, B * nq)))
 
 
 def decode_grid_z(batch: int, num_kv_heads: int, max_ctx: int, target_waves: int = 0) -> int:
@@ -228,12 +217,13 @@ def decode_grid_z(batch: int, num_kv_heads: int, max_ctx: int, target_waves: int
     context (K1w: two 32-token chunks per wave; 4-wave kernel: 64-token partitions) and by
     the 1024 slices the reduce kernel merges.  Z == 1 (large batches) lets the kernel
     write its output directly."""
-    if decode_wave_kernel():
+    pairs = max(1, batch * num_kv_heads)
+    if decode_uses_wave(batch, num_kv_heads):
         chunks = max(1, math.ceil(max_ctx / DECODE_CHUNK))
-        want = math.ceil((target_waves or DECODE_TARGET_WAVES) / max(1, batch * num_kv_heads))
+        want = math.ceil((target_waves or DECODE_TARGET_WAVES) / pairs)
         return max(1, min(want, math.ceil(chunks / 2), 1024))
     parts = max(1, math.ceil(max_ctx / DECODE_PARTITION))
-    want = math.ceil((target_waves or 4096) / max(1, batch * num_kv_heads * 4))
+    want = math.ceil((target_waves or 4096) / (pairs * 4))
     return max(1, min(want, math.ceil(parts / 4), 1024))
 
 
@@ -250,10 +240,10 @@ def paged_attention_decode(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torc
         out = torch.empty_like(q)
     if workspace is None:
         workspace = decode_partials(B, nq, d, block_tables.shape[1], k_cache.shape[2], q.device)
-    ml, es, tmp, tickets = workspace
-    grid_z = min(grid_z, _decode_z_cap(workspace, B, nq), _merge_z_cap(nq, k_cache.shape[1]))
+    ml, es, tmp = workspace
+    grid_z = min(grid_z, _decode_z_cap(workspace, B, nq))
     _k().paged_decode(out, q, k_cache, v_cache, block_tables, context_lens, ml, es, tmp,
-                      tickets, grid_z, scale, k_scale, v_scale)
+                      grid_z, scale, k_scale, v_scale)
     return out
 
 
@@ -284,11 +274,10 @@ def paged_attention_decode_rope(qkv: torch.Tensor, positions: torch.Tensor,
     if workspace is None:
         workspace = decode_partials(B, num_heads, head_dim, block_tables.shape[1],
                                     k_cache.shape[2], qkv.device)
-    ml, es, tmp, tickets = workspace
-    grid_z = min(grid_z, _decode_z_cap(workspace, B, num_heads),
-                 _merge_z_cap(num_heads, num_kv_heads))
+    ml, es, tmp = workspace
+    grid_z = min(grid_z, _decode_z_cap(workspace, B, num_heads))
     _k().paged_decode_rope(out, qkv, positions, cos_sin, k_cache, v_cache, slot_mapping,
-                           q_norm_w, k_norm_w, block_tables, context_lens, ml, es, tmp, tickets,
+                           q_norm_w, k_norm_w, block_tables, context_lens, ml, es, tmp,
                            num_heads, grid_z, scale, eps, use_rope, k_scale, v_scale)
     return out
 

@@ -219,23 +219,33 @@ def _mix32(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
+def _row_key(seeds: torch.Tensor) -> torch.Tensor:
+    """Per-row stream key from both halves of the int64 seed (sampling.hip row_key)."""
+    s = seeds.long()
+    hi = _mix32(((s >> 32) + 0x632BE5AB) & _M32)
+    return _mix32((s & _M32) ^ hi)
+
+
 def uniform_noise(seeds: torch.Tensor, vocab: int) -> torch.Tensor:
     """Counter-based uniform(0,1) noise, identical to the HIP sampler's generator.
     seeds: [B] int64 (per-row stream key) -> [B, V] fp32."""
-    col = torch.arange(vocab, dtype=torch.int64)
-    key = _mix32(seeds.long()[:, None] & _M32)
-    h = _mix32(key ^ ((col[None, :] * 0x9E3779B9) & _M32))
-    h = _mix32(h + ((seeds.long()[:, None] >> 32) & _M32))
-    return ((h >> 8).double() + 0.5).float() * (1.0 / 16777216.0)
+    return uniform_noise_cols(seeds, 0, vocab)
 
 
 def uniform_noise_cols(seeds: torch.Tensor, col0: int, n: int) -> torch.Tensor:
     """``uniform_noise`` restricted to the global columns col0 .. col0 + n - 1."""
     col = torch.arange(col0, col0 + n, dtype=torch.int64)
-    key = _mix32(seeds.long()[:, None] & _M32)
-    h = _mix32(key ^ ((col[None, :] * 0x9E3779B9) & _M32))
-    h = _mix32(h + ((seeds.long()[:, None] >> 32) & _M32))
+    h = _mix32(_row_key(seeds)[:, None] ^ ((col[None, :] * 0x9E3779B9) & _M32))
     return ((h >> 8).double() + 0.5).float() * (1.0 / 16777216.0)
+
+
+_LN2 = 0.69314718
+
+
+def gumbel(u: torch.Tensor) -> torch.Tensor:
+    """-ln2 * log2(-log2 u) (fp32): -ln(-ln u) up to a constant offset, so the same
+    Gumbel-max argmax (sampling.hip gumbel)."""
+    return -(torch.tensor(_LN2, dtype=torch.float32) * torch.log2(-torch.log2(u.float())))
 
 
 _VP_BIAS = 1 << 63
@@ -258,7 +268,7 @@ def sample_vp_partial(logits: torch.Tensor, temperature: torch.Tensor, seeds: to
     out = torch.empty(B, dtype=torch.int64)
     for b in range(B):
         t = float(temperature[b])
-        row = x[b] if t <= 1e-5 else x[b] / t - torch.log(-torch.log(u[b]))
+        row = x[b] if t <= 1e-5 else x[b] / t + gumbel(u[b])
         i = int(torch.argmax(row))                       # first index on ties
         packed = (_ord_key(float(row[i])) << 32) | (~(i + vocab_off) & 0xFFFFFFFF)
         out[b] = packed - _VP_BIAS                       # == (packed ^ bias) as int64
@@ -301,7 +311,7 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
             keep = (cum - sp) < p
             thr = sp[keep][-1]
             row = row.masked_fill(probs < thr, float("-inf"))
-        g = -torch.log(-torch.log(u[b]))
+        g = gumbel(u[b])
         out[b] = int(torch.argmax(row + g))
     return out.to(logits.device)
 

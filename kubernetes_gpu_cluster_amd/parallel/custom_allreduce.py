@@ -101,10 +101,14 @@ class CustomAllReduce:
         self.fdata2 = [b + sig_bytes + 4 * self.cap for b in bases]
         # fused all-reduce + add + RMSNorm: one-shot up to KGC_AR_RMS_MAX (default: the
         # plain one-shot limit), the row-segmented two-shot form above it up to
-        # KGC_AR_RMS2_MAX (default: the whole buffer -- TP = 8 decode at batch 256 is
-        # 4 MB of 8192-wide rows)
+        # KGC_AR_RMS2_MAX.  Default: the whole buffer at 2 ranks, off from 4 ranks up --
+        # measured with the ranks as processes on one GPU (tools/allreduce_rms_bench.py,
+        # profiles/allreduce_rms_fused_r4.jsonl, 256 x 8192 bf16 = 4 MB): world 2 33.4 vs
+        # 37.1 us for two-shot + fused_add_rms_norm, world 4 72.1 vs 56.3 us.  (One GPU
+        # shares its HBM and CUs between the ranks; on an xGMI node re-measure and set
+        # KGC_AR_RMS2_MAX.)
         self.fused_max = int(os.environ.get("KGC_AR_RMS_MAX", self.one_shot_max))
-        self.fused2_max = int(os.environ.get("KGC_AR_RMS2_MAX", self.cap))
+        self.fused2_max = int(os.environ.get("KGC_AR_RMS2_MAX", self.cap if world <= 2 else 0))
         self.max_hidden = int(k.allreduce_rms_max_hidden())
         self.fused_calls = 0        # host-side launches (a graph capture counts once)
         self.fused2_calls = 0       # ... of them the two-shot form

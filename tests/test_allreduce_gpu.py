@@ -163,6 +163,7 @@ def _rms_worker(rank, world, port, two_shot=False):
                           one_shot_max=4 << 20)
     if two_shot:
         car.fused_max = 0           # every fused call: the row-segmented two-shot kernel
+        car.fused2_max = car.cap
     try:
         for dtype in (torch.bfloat16, torch.float16):
             for M, H in ((1, 4096), (7, 8192), (130, 4096), (64, 16384), (3, 1024)):

@@ -125,14 +125,21 @@ def _fill_random_cache(B, ctx_lens, nkv, bs, d, dt, dev, nb_extra=7):
     return kc, vc, bt.to(dev)
 
 
+# decode kernel per launch: K1w (one wave per z-slice) from DECODE_WAVE_MIN_PAIRS (seq, kv-head)
+# pairs up, the 4-wave kernel below; the threshold override runs both on every shape
+_DECODE_KERNELS = {"wave": "1", "four": "1000000000"}
+
+
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("d,nq,nkv", [(128, 32, 8), (128, 8, 1), (128, 28, 4), (64, 12, 12),
                                       (128, 16, 16)])
 @pytest.mark.parametrize("bs", [16, 32])
-def test_paged_decode(gpu, dt, d, nq, nkv, bs):
+@pytest.mark.parametrize("kern", list(_DECODE_KERNELS))
+def test_paged_decode(gpu, monkeypatch, kern, dt, d, nq, nkv, bs):
     """K1 vs the fp32 reference at ragged lengths (1 token .. 2049), GQA 1/4/7/8 and MHA,
     z = 1, 3 and 40 (K1w: most slices of the short rows empty, the reduce merges only the
     used ones)."""
+    monkeypatch.setenv("KGC_DECODE_WAVE_MIN_PAIRS", _DECODE_KERNELS[kern])
     torch.manual_seed(3)
     ctx = [1, 17, 128, 129, 300, 1000, 2049, 64]
     B = len(ctx)
@@ -151,10 +158,12 @@ def test_paged_decode(gpu, dt, d, nq, nkv, bs):
 @pytest.mark.parametrize("qk_norm", [False, True])
 @pytest.mark.parametrize("S", [0, 3, 5])
 @pytest.mark.parametrize("fp8", [False, True])
-def test_paged_decode_rope(gpu, dt, d, nq, nkv, qk_norm, S, fp8):
+@pytest.mark.parametrize("kern", list(_DECODE_KERNELS))
+def test_paged_decode_rope(gpu, monkeypatch, kern, dt, d, nq, nkv, qk_norm, S, fp8):
     """The decode kernel with rope_kv_write folded in == rope_kv_write + paged_decode on
     the same inputs (q / k / v and the cache update), and == the fp32 reference.  One row
     is graph padding (ctx 0, slot -1): nothing of it reaches the cache."""
+    monkeypatch.setenv("KGC_DECODE_WAVE_MIN_PAIRS", _DECODE_KERNELS[kern])
     torch.manual_seed(17 + d + S)
     bs = 16
     ctx = [1, 17, 300, 1000, 0, 64, 129]
@@ -212,9 +221,11 @@ def test_paged_decode_rope(gpu, dt, d, nq, nkv, qk_norm, S, fp8):
         torch.testing.assert_close(out.cpu().float(), exp.float(), **tol)
 
 
-def test_paged_decode_workspace_reuse(gpu):
+@pytest.mark.parametrize("kern", list(_DECODE_KERNELS))
+def test_paged_decode_workspace_reuse(gpu, monkeypatch, kern):
     """One static partials workspace serves launches of any Z (incl. an empty context),
     eager or replayed from a graph."""
+    monkeypatch.setenv("KGC_DECODE_WAVE_MIN_PAIRS", _DECODE_KERNELS[kern])
     torch.manual_seed(13)
     dt, d, nq, nkv, bs = torch.bfloat16, 128, 32, 8, 32
     ctx = [1, 700, 2049, 64, 0, 333]

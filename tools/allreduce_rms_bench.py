@@ -49,6 +49,7 @@ def _worker(rank, world, port, shapes, iters, q):
             def fused(two):
                 def f():
                     car.fused_max = 0 if two else nb
+                    car.fused2_max = car.cap
                     car.all_reduce_add_rms(x, res, w, 1e-5)
                 return f
 
