@@ -243,9 +243,8 @@ _LN2 = 0.69314718
 
 
 def gumbel(u: torch.Tensor) -> torch.Tensor:
-    """-ln2 * log2(-log2 u) (fp32): -ln(-ln u) up to a constant offset, so the same
-    Gumbel-max argmax (sampling.hip gumbel)."""
-    return -(torch.tensor(_LN2, dtype=torch.float32) * torch.log2(-torch.log2(u.float())))
+    """-ln(-ln u) as sampling.hip gumbel computes it (fp32): -ln2 * log2(-ln u)."""
+    return -(torch.tensor(_LN2, dtype=torch.float32) * torch.log2(-torch.log(u.float())))
 
 
 _VP_BIAS = 1 << 63

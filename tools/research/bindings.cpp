@@ -112,6 +112,49 @@ void dgemm_vreg(Tensor C, Tensor X, Tensor W, int64_t depth, int64_t epi) {
                          (int)N, (int)K, X.stride(0), (int)S, ss, stream());
 }
 
+// K9w: weights private per wave (VGPR ring), activations through LDS; P from wv_pack
+void dgemm_wv(Tensor C, Tensor X, Tensor P, int64_t depth, int64_t epi) {
+  check_gpu(X, "X");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(X.device());
+  TORCH_CHECK(depth >= 2 && depth <= 3, "depth 2..3");
+  TORCH_CHECK(epi >= 0 && epi <= 2, "epi 0 (fp32 slices), 1 (out), 2 (silu pairs)");
+  TORCH_CHECK(P.scalar_type() == at::kBFloat16 && X.scalar_type() == at::kBFloat16, "bf16");
+  TORCH_CHECK(P.dim() == 3 && P.is_contiguous() && P.size(2) == 16384,
+              "packed W [N/256, K/64, 16384] contiguous");
+  const int64_t N = P.size(0) * 256, K = P.size(1) * 64, M = X.size(0);
+  TORCH_CHECK(X.dim() == 2 && X.size(1) == K && X.stride(1) == 1 && X.stride(0) % 8 == 0 &&
+              reinterpret_cast<uintptr_t>(X.data_ptr()) % 16 == 0, "X [M, K], 16-B rows");
+  TORCH_CHECK(M >= 1 && M <= 256, "K9w takes one 256-row tile: 1 <= M <= 256");
+  TORCH_CHECK(X.device() == P.device() && C.device() == X.device(), "same device");
+  int64_t S = 1, ss = 0;
+  if (epi == 0) {
+    TORCH_CHECK(C.scalar_type() == at::kFloat && C.dim() == 3 && C.is_contiguous() &&
+                C.size(1) == M && C.size(2) == N, "C fp32 contiguous [S, M, N]");
+    S = C.size(0);
+    ss = C.stride(0);
+    TORCH_CHECK(S >= 1 && S <= 32 && S <= K / 64, "1 <= S <= min(32, K / 64)");
+  } else {
+    TORCH_CHECK(C.scalar_type() == at::kBFloat16 && C.dim() == 2 && C.is_contiguous() &&
+                C.size(0) == M && C.size(1) == (epi == 2 ? N / 2 : N), "C [M, N] / [M, N/2] bf16");
+  }
+  kgc::launch_dgemm_wv((int)depth, (int)epi, C.data_ptr(), X.data_ptr(), P.data_ptr(), (int)M,
+                       (int)N, (int)K, X.stride(0), (int)S, ss, stream());
+}
+
+void wv_pack(Tensor P, Tensor W, bool silu) {
+  check_gpu(W, "W");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(W.device());
+  TORCH_CHECK(W.dim() == 2 && W.is_contiguous() && W.scalar_type() == at::kBFloat16,
+              "W [N, K] contiguous bf16");
+  const int64_t N = W.size(0), K = W.size(1);
+  TORCH_CHECK(N % 256 == 0 && K % 64 == 0, "N % 256 == 0, K % 64 == 0");
+  TORCH_CHECK(P.scalar_type() == at::kBFloat16 && P.is_contiguous() && P.dim() == 3 &&
+              P.size(0) == N / 256 && P.size(1) == K / 64 && P.size(2) == 16384,
+              "P [N/256, K/64, 16384] contiguous bf16");
+  TORCH_CHECK(P.device() == W.device(), "same device");
+  kgc::launch_wv_pack(silu, P.data_ptr(), W.data_ptr(), (int)N, (int)K, stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(kgc_research, m) {
@@ -120,10 +163,14 @@ TORCH_LIBRARY(kgc_research, m) {
   m.def("ring_cfg_info(int cfg) -> int[]", &ring_cfg_info);
   m.def("ring_num_cfgs() -> int", &ring_num_cfgs);
   m.def("dgemm_vreg(Tensor(a!) C, Tensor X, Tensor W, int depth, int epi) -> ()");
+  m.def("dgemm_wv(Tensor(a!) C, Tensor X, Tensor P, int depth, int epi) -> ()");
+  m.def("wv_pack(Tensor(a!) P, Tensor W, bool silu) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(kgc_research, CUDA, m) {
   m.impl("ring_gemm", &ring_gemm);
   m.impl("ring_pack", &ring_pack);
   m.impl("dgemm_vreg", &dgemm_vreg);
+  m.impl("dgemm_wv", &dgemm_wv);
+  m.impl("wv_pack", &wv_pack);
 }

@@ -34,7 +34,7 @@ def build(force: bool = False, arch: str = "gfx950") -> str:
               "-I", os.path.join(CSRC, "kernels"), "-I", HERE, "-D__HIP_PLATFORM_AMD__=1",
               "-Wno-unused-result", "-ffp-contract=fast"]
     jobs = [(os.path.join(HERE, f), ["-x", "hip"] + common)
-            for f in ("gemm_ring.hip", "gemm_vreg.hip")]
+            for f in ("gemm_ring.hip", "gemm_vreg.hip", "gemm_wv.hip")]
     jobs.append((os.path.join(HERE, "bindings.cpp"),
                  ["-x", "hip", "-O2", "-fPIC", "-std=c++17", f"--offload-arch={arch}",
                   "-I", HERE, "-isystem", inc, "-isystem", api_inc,

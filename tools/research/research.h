@@ -18,4 +18,10 @@ void launch_ring_pack(bool silu, void* P, const void* W, int N, int K, int G, hi
 // dgemm_pack ([N/128][K/64][8192]); depth = 2, 3 or 4 K-steps in flight
 void launch_dgemm_vreg(int depth, int epi, void* C, const void* X, const void* W, int M, int N,
                        int K, int64_t ldx, int S, int64_t ss, hipStream_t s);
+// K9w (gemm_wv.hip), bf16, one 256-row tile (M <= 256), 256-column tiles, weights packed by
+// launch_wv_pack into [N/256][K/64][16384] (per wave 4 x 1-KB loads per K-step; silu: merged
+// [gate; up] with gate / up columns paired per wave); depth 2 or 3 K-steps in flight
+void launch_dgemm_wv(int depth, int epi, void* C, const void* X, const void* Wp, int M, int N,
+                     int K, int64_t ldx, int S, int64_t ss, hipStream_t s);
+void launch_wv_pack(bool silu, void* P, const void* W, int N, int K, hipStream_t s);
 }  // namespace kgc

@@ -89,3 +89,33 @@ def test_vreg_gemm_matches_fp32(gpu, depth, M, N, K):
     r.dgemm_vreg(act, x, packed(True), depth, 2)
     exp = torch.nn.functional.silu(ref[:, : N // 2]) * ref[:, N // 2:]
     torch.testing.assert_close(act.float().cpu(), exp, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("depth", [2, 3])
+@pytest.mark.parametrize("M,N,K", [(256, 1024, 4096), (200, 768, 1024), (1, 512, 128),
+                                   (130, 256, 192)])
+def test_wv_gemm_matches_fp32(gpu, depth, M, N, K):
+    """K9w (weights private per wave in a VGPR ring, activations through LDS) over its own
+    packed layout vs fp32: bf16 output, fp32 split-K slices (slices of one to three K-steps,
+    fewer than the prefetch depth: filler groups and tail waits) and the SiLU epilogue."""
+    r = _research()
+    torch.manual_seed(M + N + depth)
+    x = torch.randn(M, K, dtype=torch.bfloat16, device=gpu)
+    w = torch.randn(N, K, dtype=torch.bfloat16, device=gpu) * 0.02
+    ref = x.float().cpu() @ w.float().cpu().t()
+
+    def packed(silu):
+        p = torch.empty(N // 256, K // 64, 16384, dtype=w.dtype, device=gpu)
+        r.wv_pack(p, w, silu)
+        return p
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
+    r.dgemm_wv(out, x, packed(False), depth, 1)
+    torch.testing.assert_close(out.float().cpu(), ref, atol=3e-2, rtol=2e-2)
+    for S in (s for s in (2, 3) if s <= K // 64):
+        ws = torch.full((S, M, N), float("nan"), dtype=torch.float32, device=gpu)
+        r.dgemm_wv(ws, x, packed(False), depth, 0)
+        torch.testing.assert_close(ws.sum(0).cpu(), ref, atol=2e-3, rtol=2e-3)
+    act = torch.empty(M, N // 2, dtype=torch.bfloat16, device=gpu)
+    r.dgemm_wv(act, x, packed(True), depth, 2)
+    exp = torch.nn.functional.silu(ref[:, : N // 2]) * ref[:, N // 2:]
+    torch.testing.assert_close(act.float().cpu(), exp, atol=3e-2, rtol=2e-2)
