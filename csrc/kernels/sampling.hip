@@ -35,19 +35,20 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
 
 // Gumbel noise.  Row key: both halves of the request seed through lowbias32, once per
 // row.  Column gi: ONE lowbias32 round of key ^ gi * golden ratio -> u in (0, 1) ->
-// E = -ln u (libm logf) -> G = -ln2 * log2(E) (v_log_f32) = -ln(-ln u).  (Two hashes and
-// two libm logf per logit made the temperature pass VALU-bound: ~70 VALU per logit, 78 us
-// per decode step at B = 256 x 128K.)  The inner log stays libm: for u near 1 -- small E,
-// the LARGEST Gumbel values, the likely winners -- v_log_f32's error is absolute, not
-// relative, and moved the argmax of 1 row in 200 against the fp32 reference.
-// ops/reference.py uniform_noise / gumbel compute the same values.
+// G = -ln2 * log2(-ln2 * log2 u) = -ln(-ln u) on v_log_f32.  (Two hashes and two libm
+// logf per logit made the temperature pass VALU-bound: ~70 VALU per logit, 78 us per
+// decode step at B = 256 x 128K.)  ops/reference.py uniform_noise / gumbel compute the
+// same values in fp32.
 __device__ __forceinline__ uint32_t row_key(uint64_t seed) {
   return mix32((uint32_t)seed ^ mix32((uint32_t)(seed >> 32) + 0x632BE5ABu));
 }
 __device__ __forceinline__ float gumbel(uint32_t key, int gi) {
   const uint32_t h = mix32(key ^ ((uint32_t)gi * 0x9E3779B9u));
-  const float u = ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
-  return -0.69314718f * __builtin_amdgcn_logf(-logf(u));
+  // 23 bits: u in [2^-24, 1 - 2^-24], every value exact in fp32.  (24 bits + 0.5 rounded
+  // the top value to u = 1.0 -> E = 0 -> G = +inf: that column won its row outright,
+  // whatever its logit -- for one row in ~130 at V = 128K.)
+  const float u = ((float)(h >> 9) + 0.5f) * (1.0f / 8388608.0f);
+  return -0.69314718f * __builtin_amdgcn_logf(-0.69314718f * __builtin_amdgcn_logf(u));
 }
 
 __device__ __forceinline__ uint32_t ord_key(float f) {

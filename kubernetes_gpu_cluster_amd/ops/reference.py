@@ -236,15 +236,16 @@ def uniform_noise_cols(seeds: torch.Tensor, col0: int, n: int) -> torch.Tensor:
     """``uniform_noise`` restricted to the global columns col0 .. col0 + n - 1."""
     col = torch.arange(col0, col0 + n, dtype=torch.int64)
     h = _mix32(_row_key(seeds)[:, None] ^ ((col[None, :] * 0x9E3779B9) & _M32))
-    return ((h >> 8).double() + 0.5).float() * (1.0 / 16777216.0)
+    return ((h >> 9).double() + 0.5).float() * (1.0 / 8388608.0)    # 23 bits: u < 1 exactly
 
 
 _LN2 = 0.69314718
 
 
 def gumbel(u: torch.Tensor) -> torch.Tensor:
-    """-ln(-ln u) as sampling.hip gumbel computes it (fp32): -ln2 * log2(-ln u)."""
-    return -(torch.tensor(_LN2, dtype=torch.float32) * torch.log2(-torch.log(u.float())))
+    """-ln(-ln u) as sampling.hip gumbel computes it (fp32): -ln2 * log2(-ln2 * log2 u)."""
+    ln2 = torch.tensor(_LN2, dtype=torch.float32)
+    return -(ln2 * torch.log2(-(ln2 * torch.log2(u.float()))))
 
 
 _VP_BIAS = 1 << 63
@@ -298,20 +299,21 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
             out[b] = int(torch.argmax(row))
             continue
         row = row / t
+        drop = torch.zeros(V, dtype=torch.bool)
         k = int(top_k[b])
         if 0 < k < V:
             kth = torch.topk(row, k).values[-1]
-            row = row.masked_fill(row < kth, float("-inf"))
+            drop |= row < kth
         p = float(top_p[b])
         if p < 1.0:
-            probs = torch.softmax(row, -1)
+            probs = torch.softmax(row.masked_fill(drop, float("-inf")), -1)
             sp, idx = torch.sort(probs, descending=True)
             cum = torch.cumsum(sp, 0)
             keep = (cum - sp) < p
             thr = sp[keep][-1]
-            row = row.masked_fill(probs < thr, float("-inf"))
-        g = gumbel(u[b])
-        out[b] = int(torch.argmax(row + g))
+            drop |= probs < thr
+        # noise first, then the mask: a dropped column is -inf whatever its noise
+        out[b] = int(torch.argmax((row + gumbel(u[b])).masked_fill(drop, float("-inf"))))
     return out.to(logits.device)
 
 

@@ -15,7 +15,8 @@ from test_model_parity import _engine_logits, _hf_model
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name", ["tiny-llama", "tiny-qwen3", "tiny-qwen2", "tiny-mixtral"])
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-qwen3", "tiny-qwen2", "tiny-mixtral",
+                                  "tiny-llama-gqa8", "tiny-llama-70b-shape"])
 def test_gpu_logits_match_hf(gpu, name):
     cfg = PRESETS[name]
     sd = full_state_dict_random(cfg, seed=2, std=0.05)
