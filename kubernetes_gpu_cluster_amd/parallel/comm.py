@@ -27,6 +27,14 @@ def get_custom_allreduce():
     return _custom_ar
 
 
+def _gloo_half(x: torch.Tensor, group) -> bool:
+    """gloo reduces bf16 / fp16 in that dtype, rounding after every rank's add (7 roundings
+    of the running sum at TP = 8: the 8-rank engine on one GPU drifted from TP = 1 on the
+    first token).  Those sums go through fp32 and round once, like the xGMI kernel's."""
+    return (x.dtype in (torch.bfloat16, torch.float16)
+            and dist.get_backend(group) == dist.Backend.GLOO)
+
+
 def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
     """C1/C2/C3: sum over the TP group (in place when possible)."""
     s = get_state()
@@ -35,6 +43,11 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
     car = _custom_ar
     if car is not None and car.should_use(x):
         return car.all_reduce(x)
+    if _gloo_half(x, s.tp_group):
+        acc = x.float()
+        dist.all_reduce(acc, group=s.tp_group)
+        x.copy_(acc)
+        return x
     dist.all_reduce(x, group=s.tp_group)
     return x
 
@@ -42,6 +55,17 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
 class _Done:
     def wait(self) -> None:
         pass
+
+
+class _Fp32Back:
+    """Async fp32 sum of a half-precision tensor: wait() rounds it back into the tensor."""
+
+    def __init__(self, work, acc: torch.Tensor, x: torch.Tensor):
+        self.work, self.acc, self.x = work, acc, x
+
+    def wait(self) -> None:
+        self.work.wait()
+        self.x.copy_(self.acc)
 
 
 def tp_all_reduce_async(x: torch.Tensor):
@@ -54,6 +78,9 @@ def tp_all_reduce_async(x: torch.Tensor):
     s = get_state()
     if s.tp_size == 1:
         return _Done()
+    if _gloo_half(x, s.tp_group):
+        acc = x.float()
+        return _Fp32Back(dist.all_reduce(acc, group=s.tp_group, async_op=True), acc, x)
     return dist.all_reduce(x, group=s.tp_group, async_op=True)
 
 

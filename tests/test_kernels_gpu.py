@@ -154,7 +154,7 @@ def test_paged_decode(gpu, monkeypatch, kern, dt, d, nq, nkv, bs):
 
 
 @pytest.mark.parametrize("dt", DT)
-@pytest.mark.parametrize("d,nq,nkv", [(128, 32, 8), (64, 8, 2), (128, 16, 16), (128, 8, 1)])
+@pytest.mark.parametrize("d,nq,nkv", [(128, 32, 8), (64, 8, 2), (128, 16, 16), (128, 8, 1), (64, 2, 1)])
 @pytest.mark.parametrize("qk_norm", [False, True])
 @pytest.mark.parametrize("S", [0, 3, 5])
 @pytest.mark.parametrize("fp8", [False, True])
@@ -249,7 +249,7 @@ def test_paged_decode_workspace_reuse(gpu, monkeypatch, kern):
 
 
 @pytest.mark.parametrize("dt", DT)
-@pytest.mark.parametrize("d,nq,nkv", [(128, 32, 8), (64, 4, 4), (128, 8, 1)])
+@pytest.mark.parametrize("d,nq,nkv", [(128, 32, 8), (64, 4, 4), (128, 8, 1), (64, 2, 1)])
 def test_prefill_attention(gpu, dt, d, nq, nkv):
     torch.manual_seed(4)
     bs = 16
@@ -270,7 +270,8 @@ def test_prefill_attention(gpu, dt, d, nq, nkv):
 
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("gqa,d,nq,nkv", [("1", 128, 32, 8), ("0", 128, 32, 8),
-                                         ("1", 128, 64, 8), ("0", 64, 4, 4)])
+                                         ("1", 128, 64, 8), ("0", 64, 4, 4),
+                                         ("1", 64, 2, 1), ("1", 128, 8, 1)])
 @pytest.mark.parametrize("vgroup,kvg", [("0", "1"), ("0", "0"), ("1", "0")])
 def test_prefill_rope_fused_equals_unfused(gpu, monkeypatch, dt, gqa, d, nq, nkv, vgroup, kvg):
     """Prefill-only step with q RoPE folded into K2's q load (kv_write_rope +
