@@ -417,11 +417,23 @@ class ModelRunner:
         DRIVER evaluates this (build_plan) and every rank follows the plan's ``split``.
         KGC_TP_OVERLAP=0 turns it off; KGC_TP_OVERLAP_MIN_TOKENS (default 2048) is the
         smallest step it applies to (below it the all-reduces take the xGMI kernel)."""
-        if self.ps.tp_size == 1 or os.environ.get("KGC_TP_OVERLAP", "1") == "0":
+        if self.ps.tp_size == 1:
+            return self._two_streams_ok(Tp)
+        if os.environ.get("KGC_TP_OVERLAP", "1") == "0":
             return False
         fn = getattr(self.model, "_tp_tail_fusable", None)
         return (fn is not None and fn()
                 and Tp >= int(os.environ.get("KGC_TP_OVERLAP_MIN_TOKENS", "2048")))
+
+    def _two_streams_ok(self, Tp: int) -> bool:
+        """One GPU: large prefill-only steps of several sequences run as two halves on two
+        streams (``LlamaForCausalLM._forward_two_streams``).  KGC_PREFILL_STREAMS=0 turns
+        it off; KGC_PREFILL_STREAMS_MIN_TOKENS (default 4096) is the smallest step."""
+        if not self.is_gpu or os.environ.get("KGC_PREFILL_STREAMS", "1") == "0":
+            return False
+        fn = getattr(self.model, "two_stream_ok", None)
+        return (fn is not None and fn()
+                and Tp >= int(os.environ.get("KGC_PREFILL_STREAMS_MIN_TOKENS", "4096")))
 
     def _split_prefill(self, Tp: int, P: int):
         """Split the step's prefill tokens at row a into two AttnMetadata.  A sequence
@@ -435,7 +447,15 @@ class ModelRunner:
         qsl = i32[L.qsl:L.qsl + P + 1].astype(np.int64)
         sl = i32[L.sl:L.sl + P].astype(np.int64)
         pbt = i32[L.pbt:L.pbt + P * mb].reshape(P, mb)
-        a = (Tp // 2) // 128 * 128 or Tp // 2
+        if self.ps.tp_size == 1:
+            # two streams: the halves must share no sequence -- cut at the sequence
+            # boundary nearest the middle, or not at all
+            inner = qsl[1:-1]
+            if inner.size == 0:
+                return None
+            a = int(inner[np.argmin(np.abs(inner - Tp // 2))])
+        else:
+            a = (Tp // 2) // 128 * 128 or Tp // 2
         k = int(np.searchsorted(qsl, a, side="right")) - 1      # qsl[k] <= a < qsl[k+1]
         qlens = np.diff(qsl)
         cut = a > qsl[k]

@@ -207,6 +207,8 @@ class LlamaForCausalLM(nn.Module):
             if ctx.attn.split is not None:
                 return self._forward_tp_overlap(positions, x, ctx)
             return self._forward_tp_fused(positions, x, ctx)
+        if getattr(getattr(ctx, "attn", None), "split", None) is not None and self.two_stream_ok():
+            return self._forward_two_streams(positions, x, ctx)
         for layer in self.layers:
             x, residual = layer(positions, x, residual, ctx)
         if not self.last:
@@ -330,6 +332,72 @@ class LlamaForCausalLM(nn.Module):
             xi, _ = ops.fused_add_rms_norm(h[i], res[i], self.norm.weight, self.norm.eps)
             outs.append(xi)
         return torch.cat(outs, 0)
+
+    # ------------------------------------------------------------------ two-stream prefill
+    def two_stream_ok(self) -> bool:
+        """One GPU, whole model, dense MLP: a large prefill-only step of whole sequences may
+        run as two halves on two streams (``_forward_two_streams``)."""
+        return (get_state().tp_size == 1 and self.first and self.last and bool(self.layers)
+                and not self.cfg.is_moe and self.layers[0].input_layernorm.weight.is_cuda)
+
+    def _side_stream(self, device) -> torch.cuda.Stream:
+        st = getattr(self, "_side", None)
+        if st is None:
+            st = self._side = torch.cuda.Stream(device=device)
+        return st
+
+    def _forward_two_streams(self, positions, x, ctx):
+        """A prefill-only step split at a sequence boundary (engine/model_runner.py
+        ``_split_prefill``): half A on the current stream, half B on a side stream, B's
+        attention part of layer l released by A's attention part of layer l, so B runs
+        about half a layer behind:
+
+            main:  attn(A, l)  MLP(A, l)         attn(A, l+1)  MLP(A, l+1) ...
+            side:              attn(B, l)  MLP(B, l)           attn(B, l+1) ...
+
+        The prefill GEMMs are power-capped (profiles/prefill_gemm_clock_power_r4.txt: MFMA
+        pipes busy 85 % at 1.74 GHz, 1400 W); the other half's memory-bound kernels
+        (attention, RMSNorm, SiLU-and-mul, the K / V writes) run in the headroom beside
+        them instead of after them.  The halves share no sequence, so they share no KV
+        block: the same math as the unsplit step (only the GEMMs' M differs)."""
+        a, ma, mb = ctx.attn.split
+        ctxs = (dataclasses.replace(ctx, attn=ma), dataclasses.replace(ctx, attn=mb))
+        pos = (positions[:a], positions[a:])
+        main = torch.cuda.current_stream(x.device)
+        side = self._side_stream(x.device)
+        side.wait_stream(main)                 # the embedding rows and the split metadata
+        x.record_stream(side)                  # half B reads x[a:] on the side stream
+        xs, res = [x[:a], x[a:]], [None, None]
+
+        def attn_part(i, layer):
+            ln1 = layer.input_layernorm
+            if res[i] is None:
+                res[i] = xs[i]
+                h = ln1(xs[i])
+            else:
+                h, res[i] = ln1(xs[i], res[i])
+            return layer.self_attn(pos[i], h, ctxs[i])
+
+        def mlp_part(i, layer, o):
+            h, res[i] = layer.post_attention_layernorm(o, res[i])
+            xs[i] = layer.mlp(h)
+
+        for layer in self.layers:
+            oa = attn_part(0, layer)
+            ev = torch.cuda.Event()
+            ev.record(main)
+            with torch.cuda.stream(side):
+                side.wait_event(ev)
+                ob = attn_part(1, layer)
+            mlp_part(0, layer, oa)
+            with torch.cuda.stream(side):
+                mlp_part(1, layer, ob)
+        ha, _ = self.norm(xs[0], res[0])
+        with torch.cuda.stream(side):
+            hb, _ = self.norm(xs[1], res[1])
+        main.wait_stream(side)
+        hb.record_stream(main)
+        return torch.cat([ha, hb], 0)
 
     # ------------------------------------------------------------------ fused small-M decode
     def _fused_cfgs(self, M: int):

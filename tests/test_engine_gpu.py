@@ -200,6 +200,36 @@ def test_prefill_rope_fused_equals_unfused(gpu, monkeypatch):
         _assert_greedy_agrees(got, ref, 8)
 
 
+def test_two_stream_prefill_equals_one_stream(gpu, monkeypatch):
+    """One GPU: a prefill-only step of several whole prompts split at a sequence boundary
+    into two halves on two streams (models/llama.py _forward_two_streams, B paced half a
+    layer behind A) continues like the one-stream step.  The halves share no sequence and
+    no KV block; only the GEMMs' M differs (hipBLASLt may tile M = a and M = T apart), so
+    greedy runs agree up to a near-tie."""
+    g = torch.Generator().manual_seed(9)
+    prompts = [torch.randint(100, 128000, (n,), generator=g).tolist() for n in (40, 300, 150, 7)]
+    params = [SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True, logprobs=2)
+              for _ in prompts]
+    monkeypatch.setenv("KGC_PREFILL_STREAMS_MIN_TOKENS", "16")
+    outs, calls = {}, {}
+    for on in ("0", "1"):
+        monkeypatch.setenv("KGC_PREFILL_STREAMS", on)
+        eng = _tiny_engine(enforce_eager=False, max_num_batched_tokens=1024)
+        m = eng.executor.runner.model
+        n = []
+        real = m._forward_two_streams
+        monkeypatch.setattr(m, "_forward_two_streams",
+                            lambda *a, **k: (n.append(1), real(*a, **k))[1])
+        outs[on] = _run_lp(eng, prompts, params)
+        calls[on] = len(n)
+        del eng
+        torch.cuda.empty_cache()
+    assert calls["1"] > 0 and calls["0"] == 0, calls
+    for got, ref in zip(outs["1"], outs["0"]):
+        assert len(got[0]) == 10
+        _assert_greedy_agrees(got, ref, 10)
+
+
 def test_engine_preemption_recompute(gpu):
     """A KV pool too small for the batch forces recompute preemption; every request
     still completes with the requested length."""
@@ -291,10 +321,12 @@ def test_tp_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch, tp, eager, name, 
         llm.shutdown()
     same = sum(a == b for x, y in zip(outs[1], outs[tp_n]) for a, b in zip(x, y))
     for i, (x, y) in enumerate(zip(outs[1], outs[tp_n])):
-        # the first token: TP = 1's argmax, or a near-tie of it (the random tiny model's
-        # logits have near-ties that the sharded sums' one extra rounding can flip)
+        # the first token: TP = 1's argmax, or a near-tie of it.  The random tiny model
+        # (std 0.15 weights) has logits of magnitude ~10, where one bf16 ulp is 0.06; the
+        # sharded sums round each rank's partial once more, so ties within 0.15 may flip
+        # (the CPU bf16 reference flips prompt 2 the same way at TP = 1 already)
         if x[0] != y[0]:
-            assert y[0] in top1[i] and top1[i][x[0]] - top1[i][y[0]] < 0.05, (i, top1[i], outs)
+            assert y[0] in top1[i] and top1[i][x[0]] - top1[i][y[0]] < 0.15, (i, top1[i], outs)
     assert same >= 0.6 * sum(len(x) for x in outs[1]), outs
 
 
