@@ -427,9 +427,12 @@ class ModelRunner:
 
     def _two_streams_ok(self, Tp: int) -> bool:
         """One GPU: large prefill-only steps of several sequences run as two halves on two
-        streams (``LlamaForCausalLM._forward_two_streams``).  KGC_PREFILL_STREAMS=0 turns
-        it off; KGC_PREFILL_STREAMS_MIN_TOKENS (default 4096) is the smallest step."""
-        if not self.is_gpu or os.environ.get("KGC_PREFILL_STREAMS", "1") == "0":
+        streams (``LlamaForCausalLM._forward_two_streams``) with KGC_PREFILL_STREAMS=1;
+        KGC_PREFILL_STREAMS_MIN_TOKENS (default 4096) is the smallest step.  Off by default:
+        measured on one box (profiles/engine_ab_prefill_two_streams_r4.jsonl) 17,117 vs
+        17,190 tok/s and p50 TTFT 783 vs 771 ms -- the halves' memory-bound kernels beside
+        the other half's GEMMs do not buy time back under the 1400 W cap."""
+        if not self.is_gpu or os.environ.get("KGC_PREFILL_STREAMS", "0") != "1":
             return False
         fn = getattr(self.model, "two_stream_ok", None)
         return (fn is not None and fn()

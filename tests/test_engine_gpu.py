@@ -213,7 +213,7 @@ def test_two_stream_prefill_equals_one_stream(gpu, monkeypatch):
     monkeypatch.setenv("KGC_PREFILL_STREAMS_MIN_TOKENS", "16")
     outs, calls = {}, {}
     for on in ("0", "1"):
-        monkeypatch.setenv("KGC_PREFILL_STREAMS", on)
+        monkeypatch.setenv("KGC_PREFILL_STREAMS", on)          # off by default
         eng = _tiny_engine(enforce_eager=False, max_num_batched_tokens=1024)
         m = eng.executor.runner.model
         n = []
