@@ -955,7 +955,8 @@ void xgmi_allreduce_emu(int64_t kind, std::vector<Tensor> a, std::vector<Tensor>
 
 void skinny_gemm(Tensor C, Tensor X, Tensor W, std::optional<Tensor> bias, int64_t mt,
                  int64_t nt, int64_t nw, bool ntl, int64_t epi, std::optional<Tensor> gamma,
-                 double eps, std::optional<Tensor> norm_out, std::optional<Tensor> ticket) {
+                 double eps, std::optional<Tensor> norm_out, std::optional<Tensor> ticket,
+                 std::optional<Tensor> ssp, int64_t nss) {
   check_gpu(X, "X");
   check_same_dev(X, W, "W");
   check_same_dev(X, C, "C");
@@ -974,7 +975,7 @@ void skinny_gemm(Tensor C, Tensor X, Tensor W, std::optional<Tensor> bias, int64
   TORCH_CHECK(K % (32 * nw) == 0, "kgc.skinny_gemm: K % (32*nw) != 0");
   TORCH_CHECK(X.stride(1) == 1 && X.stride(0) % 8 == 0 && X.stride(0) >= K,
               "kgc.skinny_gemm: X rows dense, 16B aligned");
-  if (epi == 3) {   // SK_SILU: merged [gate; up] weight [2I, K] -> C [M, I]
+  if (epi == 3 || epi == 7) {   // SK_SILU: merged [gate; up] weight [2I, K] -> C [M, I]
     TORCH_CHECK(nt == 2 && !bias.has_value() && N % 32 == 0,
                 "kgc.skinny_gemm: silu epilogue needs nt=2, no bias, N % 32 == 0");
     TORCH_CHECK(C.size(0) == M && C.size(1) == N / 2 && C.stride(1) == 1,
@@ -992,8 +993,23 @@ void skinny_gemm(Tensor C, Tensor X, Tensor W, std::optional<Tensor> bias, int64
     check_same_dev(X, *bias, "bias");
     bp = bias->data_ptr();
   }
-  TORCH_CHECK(epi >= 0 && epi <= 4, "kgc.skinny_gemm: epi in {0 plain, 1 norm, 2 accumulate, "
-              "3 silu(gate) * up, 4 accumulate + rms_norm}");
+  TORCH_CHECK(epi >= 0 && epi <= 7, "kgc.skinny_gemm: epi in {0 plain, 1 norm, 2 accumulate, "
+              "3 silu(gate) * up, 4 accumulate + rms_norm, 5 accumulate + row sums of squares, "
+              "6 / 7 row-scaled plain / silu pairs}");
+  float* sp = nullptr;
+  if (epi >= 5) {
+    TORCH_CHECK(ssp.has_value() && ssp->scalar_type() == at::kFloat && ssp->is_contiguous(),
+                "kgc.skinny_gemm: epi 5-7 need ssp fp32 contiguous");
+    check_same_dev(X, *ssp, "ssp");
+    if (epi == 5) {
+      TORCH_CHECK(ssp->numel() >= M * (N / (16 * nt)), "kgc.skinny_gemm: ssp [M, N / (16 nt)]");
+    } else {
+      TORCH_CHECK(nss >= 1 && nss <= 256 && ssp->numel() >= M * nss && M <= 4 * nw,
+                  "kgc.skinny_gemm: row scale needs 1 <= nss <= 256 partials per row, "
+                  "M <= 4 * nw, ssp [M, nss]");
+    }
+    sp = ssp->data_ptr<float>();
+  }
   const void* gp = nullptr;
   if (epi == 1 || epi == 4) {
     const int64_t gn = epi == 1 ? K : N;
@@ -1003,7 +1019,7 @@ void skinny_gemm(Tensor C, Tensor X, Tensor W, std::optional<Tensor> bias, int64
     check_same_dev(X, *gamma, "gamma");
     gp = gamma->data_ptr();
   }
-  if (epi == 2 || epi == 4)   // C is read and rewritten in place: it must not overlap the inputs
+  if (epi == 2 || epi == 4 || epi == 5)   // C is read and rewritten in place: no overlap
     TORCH_CHECK(C.data_ptr() != X.data_ptr(), "kgc.skinny_gemm: accumulate target aliases X");
   void* np = nullptr;
   uint32_t* tp = nullptr;
@@ -1022,7 +1038,7 @@ void skinny_gemm(Tensor C, Tensor X, Tensor W, std::optional<Tensor> bias, int64
   }
   kgc::launch_skinny_gemm(dt_code(X), (int)mt, (int)nt, (int)nw, ntl, (int)epi, C.data_ptr(),
                           X.data_ptr(), W.data_ptr(), bp, gp, (float)eps, (int)M, (int)N, (int)K,
-                          X.stride(0), C.stride(0), np, tp, stream());
+                          X.stride(0), C.stride(0), np, tp, sp, (int)nss, stream());
 }
 
 void sample_stamps_enable(bool on) { kgc::sample_stamps_enable(on); }
@@ -1130,7 +1146,7 @@ TORCH_LIBRARY(kgc, m) {
   m.def("prefill_block_m() -> int", &prefill_block_m);
   m.def("skinny_gemm(Tensor(a!) C, Tensor X, Tensor W, Tensor? bias, int mt, int nt, int nw, "
         "bool ntl, int epi=0, Tensor? gamma=None, float eps=1e-6, Tensor(b!)? norm_out=None, "
-        "Tensor(c!)? ticket=None) -> ()");
+        "Tensor(c!)? ticket=None, Tensor(d!)? ssp=None, int nss=0) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(kgc, CUDA, m) {

@@ -42,20 +42,33 @@
 //            separate norm launch and its kernel boundary disappear (o_proj -> post-
 //            attention norm, down_proj -> next input norm at small M).  The ticket is
 //            zeroed at allocation and by every last arriver; one ticket per stream.
+//   SK_ACC_SS / SK_RSCALE(_SILU): the small-M decoder layer with NO RMSNorm launch.  The
+//            norm's weight gamma is folded into the consuming weight once (W' = W diag(gamma),
+//            ops/gemm.py fold_norm_weight), so rms_norm(x) W^T = rsqrt(mean(x^2) + eps) *
+//            (x W'^T): a per-row scale of the plain GEMM.  The producer of x (o_proj /
+//            down_proj, SK_ACC_SS) adds its output into the residual and writes each row's sum
+//            of squares over ITS columns, rounded as stored, to SSP[row][workgroup]; the
+//            consumer (qkv / gate_up, SK_RSCALE / SK_RSCALE_SILU) sums the NSS partials of its
+//            rows -- loaded before its weight stream starts -- and scales them.  Two launches
+//            per layer fewer than residual add + RMSNorm kernels at batch 1.
 #include "common.h"
 #include "launch.h"
 
 namespace kgc {
 
-enum { SK_PLAIN = 0, SK_NORM = 1, SK_ACC = 2, SK_SILU = 3, SK_ACC_NORM = 4 };
+enum { SK_PLAIN = 0, SK_NORM = 1, SK_ACC = 2, SK_SILU = 3, SK_ACC_NORM = 4, SK_ACC_SS = 5,
+       SK_RSCALE = 6, SK_RSCALE_SILU = 7 };
 
 template <typename T, int MT, int NT, int NW, bool NTL, int EPI>
 __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
     T* __restrict__ C, const T* __restrict__ X, const T* __restrict__ W,
     const T* __restrict__ bias, const T* __restrict__ gamma, float eps, int M, int K,
-    int64_t ldx, int64_t ldc, T* __restrict__ NO, uint32_t* __restrict__ ticket) {
-  constexpr bool NORM = EPI == SK_NORM, SILU = EPI == SK_SILU, ACCN = EPI == SK_ACC_NORM;
-  constexpr bool ACC = EPI == SK_ACC || ACCN;
+    int64_t ldx, int64_t ldc, T* __restrict__ NO, uint32_t* __restrict__ ticket,
+    float* __restrict__ SSP, int nss) {
+  constexpr bool NORM = EPI == SK_NORM, ACCN = EPI == SK_ACC_NORM, ACCSS = EPI == SK_ACC_SS;
+  constexpr bool RS = EPI == SK_RSCALE || EPI == SK_RSCALE_SILU;
+  constexpr bool SILU = EPI == SK_SILU || EPI == SK_RSCALE_SILU;
+  constexpr bool ACC = EPI == SK_ACC || ACCN || ACCSS;
   static_assert(!SILU || NT == 2, "SK_SILU pairs n-tile 0 (gate) with n-tile 1 (up)");
   // k-steps of loads in flight per batch (SK_NORM: gamma fragments ride along, so the
   // batch is halved to keep the register sets -- and the waves per SIMD -- as they were)
@@ -142,6 +155,18 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
   XSet xa, xb;
   GSet ga, gb;
   if (nb > 0) load(wa, xa, ga, k);
+  // SK_RSCALE: the sum-of-squares partials of this wave's rows (m = wave + r * NW) ride
+  // behind the first weight batch; the host keeps nss <= 256 and M <= 4 * NW
+  float ssv[RS ? 4 : 1][RS ? 4 : 1];
+  if constexpr (RS) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = min(wave + r * NW, M - 1), j = min(lane + 64 * i, nss - 1);
+        ssv[r][i] = SSP[(int64_t)m * nss + j];
+      }
+  }
   for (int b = 0; b < nb; b += 2) {
     if (b + 1 < nb) load(wb, xb, gb, k + 32 * U);
     compute(wa, xa, ga);
@@ -170,6 +195,17 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
       *reinterpret_cast<f32x4*>(&red[wave][mt][nt][lane][0]) = acc[mt][nt];
     if constexpr (NORM) ssr[wave][mt][lane] = ss[mt];
   }
+  if constexpr (RS) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = wave + r * NW;
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) t += lane + 64 * i < nss ? ssv[r][i] : 0.f;
+      t = wave_sum(t);
+      if (lane == 0 && m < M && m < 16 * MT) inv_s[m] = rsqrtf(t / (float)K + eps);
+    }
+  }
   __syncthreads();
   constexpr int TN = SILU ? 16 : 16 * NT;
   const int rows = min(M, 16 * MT);
@@ -196,10 +232,14 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
       float u = 0.f;
 #pragma unroll
       for (int w = 0; w < NW; ++w) u += red[w][mt][1][l][i];
+      if constexpr (RS) {
+        s *= inv_s[m];
+        u *= inv_s[m];
+      }
       C[(int64_t)m * ldc + n0 + n] = from_f<T>(s / (1.f + __expf(-s)) * u);
       continue;
     }
-    if constexpr (NORM) s *= inv_s[m];
+    if constexpr (NORM || RS) s *= inv_s[m];
     if (bias != nullptr) s += to_f<T>(bias[n0 + n]);
     T* c = C + (int64_t)m * ldc + n0 + n;
     if constexpr (ACC) s += to_f<T>(*c);
@@ -209,6 +249,15 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
       const T v = from_f<T>(s);
       __hip_atomic_store(reinterpret_cast<uint16_t*>(c), __builtin_bit_cast(uint16_t, v),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if constexpr (ACCSS) {
+      // the TN lanes of a row's columns are one aligned lane group (stride NW * 64, and
+      // 64 % TN == 0): their squares of the stored values sum over the group, fixed order
+      const T v = from_f<T>(s);
+      *c = v;
+      float q = to_f<T>(v) * to_f<T>(v);
+#pragma unroll
+      for (int o = 1; o < TN; o <<= 1) q += __shfl_xor(q, o, 64);
+      if (n == 0) SSP[(int64_t)m * gridDim.x + blockIdx.x] = q;
     } else {
       *c = from_f<T>(s);
     }
@@ -278,16 +327,20 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
 template <typename T, int MT, int NT, int NW, bool NTL>
 static void sk_launch(int epi, dim3 grid, hipStream_t s, void* C, const void* X, const void* W,
                       const void* bias, const void* gamma, float eps, int M, int K,
-                      int64_t ldx, int64_t ldc, void* NO, uint32_t* ticket) {
+                      int64_t ldx, int64_t ldc, void* NO, uint32_t* ticket, float* ssp,
+                      int nss) {
 #define SK_GO(E)                                                                              \
   skinny_gemm_kernel<T, MT, NT, NW, NTL, E><<<grid, NW * 64, 0, s>>>(                        \
       (T*)C, (const T*)X, (const T*)W, (const T*)bias, (const T*)gamma, eps, M, K, ldx, ldc, \
-      (T*)NO, ticket)
+      (T*)NO, ticket, ssp, nss)
   if (epi == SK_NORM) SK_GO(SK_NORM);
   else if (epi == SK_ACC) SK_GO(SK_ACC);
   else if (epi == SK_ACC_NORM) SK_GO(SK_ACC_NORM);
+  else if (epi == SK_ACC_SS) SK_GO(SK_ACC_SS);
+  else if (epi == SK_RSCALE) SK_GO(SK_RSCALE);
   else if constexpr (NT == 2) {
     if (epi == SK_SILU) SK_GO(SK_SILU);
+    else if (epi == SK_RSCALE_SILU) SK_GO(SK_RSCALE_SILU);
     else SK_GO(SK_PLAIN);
   } else SK_GO(SK_PLAIN);
 #undef SK_GO
@@ -296,13 +349,15 @@ static void sk_launch(int epi, dim3 grid, hipStream_t s, void* C, const void* X,
 template <typename T, int MT, int NT>
 static void skinny_nw(int nw, bool ntl, int epi, void* C, const void* X, const void* W,
                       const void* bias, const void* gamma, float eps, int M, int N, int K,
-                      int64_t ldx, int64_t ldc, void* NO, uint32_t* ticket, hipStream_t s) {
-  const dim3 grid(epi == SK_SILU ? N / 32 : N / (16 * NT));   // SK_SILU: N = 2I
+                      int64_t ldx, int64_t ldc, void* NO, uint32_t* ticket, float* ssp, int nss,
+                      hipStream_t s) {
+  const bool silu = epi == SK_SILU || epi == SK_RSCALE_SILU;
+  const dim3 grid(silu ? N / 32 : N / (16 * NT));   // silu epilogues: N = 2I
 #define SK_NW(NW_)                                                                            \
   if (ntl) sk_launch<T, MT, NT, NW_, true>(epi, grid, s, C, X, W, bias, gamma, eps, M, K, ldx, ldc, \
-                                           NO, ticket);                                      \
+                                           NO, ticket, ssp, nss);                            \
   else sk_launch<T, MT, NT, NW_, false>(epi, grid, s, C, X, W, bias, gamma, eps, M, K, ldx, ldc, \
-                                        NO, ticket)
+                                        NO, ticket, ssp, nss)
   if (nw == 16) { SK_NW(16); }
   else if (nw == 8) { SK_NW(8); }
   else { SK_NW(4); }
@@ -312,12 +367,13 @@ static void skinny_nw(int nw, bool ntl, int epi, void* C, const void* X, const v
 template <typename T>
 static void skinny_t(int mt, int nt, int nw, bool ntl, int epi, void* C, const void* X,
                      const void* W, const void* bias, const void* gamma, float eps, int M, int N,
-                     int K, int64_t ldx, int64_t ldc, void* NO, uint32_t* ticket, hipStream_t s) {
+                     int K, int64_t ldx, int64_t ldc, void* NO, uint32_t* ticket, float* ssp,
+                     int nss, hipStream_t s) {
 #define SK_MT(MT_)                                                                            \
   if (nt == 2) skinny_nw<T, MT_, 2>(nw, ntl, epi, C, X, W, bias, gamma, eps, M, N, K, ldx, ldc, \
-                                    NO, ticket, s);                                           \
+                                    NO, ticket, ssp, nss, s);                                 \
   else skinny_nw<T, MT_, 1>(nw, ntl, epi, C, X, W, bias, gamma, eps, M, N, K, ldx, ldc, NO,    \
-                            ticket, s)
+                            ticket, ssp, nss, s)
   if (mt == 1) { SK_MT(1); }
   else if (mt == 2) { SK_MT(2); }
   else { SK_MT(4); }
@@ -327,14 +383,14 @@ static void skinny_t(int mt, int nt, int nw, bool ntl, int epi, void* C, const v
 void launch_skinny_gemm(int dtype, int mt, int nt, int nw, bool ntl, int epi, void* C,
                         const void* X, const void* W, const void* bias, const void* gamma,
                         float eps, int M, int N, int K, int64_t ldx, int64_t ldc, void* NO,
-                        uint32_t* ticket, hipStream_t s) {
+                        uint32_t* ticket, float* ssp, int nss, hipStream_t s) {
   if (M == 0 || N == 0) return;
   if (dtype == DT_BF16)
     skinny_t<bf16>(mt, nt, nw, ntl, epi, C, X, W, bias, gamma, eps, M, N, K, ldx, ldc, NO, ticket,
-                   s);
+                   ssp, nss, s);
   else
     skinny_t<f16>(mt, nt, nw, ntl, epi, C, X, W, bias, gamma, eps, M, N, K, ldx, ldc, NO, ticket,
-                  s);
+                  ssp, nss, s);
 }
 
 }  // namespace kgc

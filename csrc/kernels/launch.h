@@ -93,7 +93,10 @@ void launch_sample_vp_unpack(int64_t* out, const int64_t* packed, int B, hipStre
 // K9 skinny (small-M decode) GEMM: C[M, N] = X[M, K] . W[N, K]^T (+ bias), M <= 16*mt.
 // epi: 0 plain, 1 RMS-normalise X rows on the fly (gamma [K], eps), 2 accumulate into C,
 // 3 silu(gate) * up over a merged weight (C [M, N/2]), 4 accumulate into C then
-// NO = rms_norm(C) * gamma [N] in the same launch (ticket: a zeroed u32, one per stream)
+// NO = rms_norm(C) * gamma [N] in the same launch (ticket: a zeroed u32, one per stream),
+// 5 accumulate and write ssp[m][workgroup] = sum over the workgroup's columns of C[m]^2,
+// 6 / 7 C = rsqrt(sum_j ssp[m][j] / K + eps) * (X W^T) (7: the silu pairs of epi 3), nss
+// partials per row (W holds the norm weight folded in)
 // cooperative sampler phase stamps (profiling): enable, then read 16 wall-clock stamps
 void sample_stamps_enable(bool on);
 void sample_stamps_read(uint64_t* out16);
@@ -101,7 +104,7 @@ void sample_stamps_read(uint64_t* out16);
 void launch_skinny_gemm(int dtype, int mt, int nt, int nw, bool ntl, int epi, void* C,
                         const void* X, const void* W, const void* bias, const void* gamma,
                         float eps, int M, int N, int K, int64_t ldx, int64_t ldc, void* NO,
-                        uint32_t* ticket, hipStream_t s);
+                        uint32_t* ticket, float* ssp, int nss, hipStream_t s);
 
 // K13/K14 MoE: routing, expert bucketing, grouped MFMA GEMM, weighted combine.
 int moe_block_n();

@@ -93,6 +93,12 @@ class Worker:
             ws = [p for n, p in self.model.named_parameters() if p.dim() == 2
                   and id(p) not in skip and (tied or "embed" not in n)]
             gemm.pack_decode_weights(ws, silu)
+        if dev.type == "cuda":
+            # gamma-folded qkv / gate_up copies for the norm-free small-M layer (eager and
+            # graph steps alike, so both run the same arithmetic)
+            fold = getattr(self.model, "fold_rs_weights", None)
+            if fold is not None:
+                fold()
         if self.ps.tp_size > 1 and dev.type == "cuda" and not cfg.disable_custom_all_reduce:
             from ..parallel.custom_allreduce import maybe_init_custom_allreduce
             comm.set_custom_allreduce(maybe_init_custom_allreduce(self.ps, dev))

@@ -40,6 +40,8 @@ def pp_layer_range(num_layers: int, pp_size: int, pp_rank: int) -> tuple[int, in
 _tail_fusion_enabled = os.environ.get("KGC_TAIL_FUSION", "1") != "0"
 # TP > 1: all-reduce fused with the residual add + RMSNorm after o / down (KGC_TP_AR_NORM=0: off)
 _tp_ar_norm_enabled = os.environ.get("KGC_TP_AR_NORM", "1") != "0"
+# small M on one GPU: the decoder layer without RMSNorm launches (KGC_RS_LAYER=0: off)
+_rs_enabled = os.environ.get("KGC_RS_LAYER", "1") != "0"
 # decode-only steps: RoPE + KV write folded into the paged-decode kernel (KGC_DECODE_ROPE_FUSED=0: off)
 _decode_rope_fused = os.environ.get("KGC_DECODE_ROPE_FUSED", "1") != "0"
 # prefill-only steps of RoPE models without q/k norm: K2 rotates q as it loads it from the
@@ -197,6 +199,9 @@ class LlamaForCausalLM(nn.Module):
         previous stage.  Returns the final-normed hidden on the last stage, else
         (hidden, residual) for the next stage."""
         if hidden is None and residual is None:
+            rs = self._rs_cfgs(input_ids.shape[0])
+            if rs is not None:
+                return self._forward_rs(input_ids, positions, ctx, rs)
             cfgs = self._fused_cfgs(input_ids.shape[0])
             if cfgs is not None:
                 return self._forward_fused(input_ids, positions, ctx, cfgs)
@@ -398,6 +403,77 @@ class LlamaForCausalLM(nn.Module):
         main.wait_stream(side)
         hb.record_stream(main)
         return torch.cat([ha, hb], 0)
+
+    # ------------------------------------------------------------------ norm-free small-M layer
+    def fold_rs_weights(self, budget_fraction: float = 0.08) -> int:
+        """Copies of the qkv and gate_up weights with their input norm's gamma folded in
+        (ops/gemm.py fold_norm_weight) for ``_forward_rs``, plus its two sum-of-squares
+        partial buffers.  One GPU, dense bias-free Llama layers, KGC_RS_LAYER != 0, and the
+        copies within ``budget_fraction`` of device memory (Llama-3-8B: 9.1 GB).  Call
+        before the KV cache is sized.  Returns the bytes added."""
+        self._rs_w = None
+        if not (_rs_enabled and self._fusable and self.layers
+                and self.layers[0].input_layernorm.weight.is_cuda):
+            return 0
+        l0 = self.layers[0]
+        if any(p.bias is not None for p in (l0.self_attn.qkv_proj, l0.self_attn.o_proj,
+                                            l0.mlp.gate_up_proj, l0.mlp.down_proj)):
+            return 0
+        dev = l0.input_layernorm.weight.device
+        need = sum(l.self_attn.qkv_proj.weight.numel() + l.mlp.gate_up_proj.weight.numel()
+                   for l in self.layers[1:]) * l0.mlp.gate_up_proj.weight.element_size()
+        need += l0.mlp.gate_up_proj.weight.numel() * l0.mlp.gate_up_proj.weight.element_size()
+        free, total = torch.cuda.mem_get_info(dev)
+        if need > budget_fraction * total or need > free - (8 << 30):
+            return 0
+        ws = []
+        for i, l in enumerate(self.layers):
+            qkv = (None if i == 0 else
+                   gemm.fold_norm_weight(l.self_attn.qkv_proj.weight, l.input_layernorm.weight))
+            ws.append((qkv, gemm.fold_norm_weight(l.mlp.gate_up_proj.weight,
+                                                  l.post_attention_layernorm.weight)))
+        self._rs_w = ws
+        self._rs_ssp = (torch.zeros(16 * 256, dtype=torch.float32, device=dev),
+                        torch.zeros(16 * 256, dtype=torch.float32, device=dev))
+        return need
+
+    def _rs_shapes(self):
+        l0 = self.layers[0]
+        return [tuple(l0.self_attn.qkv_proj.weight.shape), tuple(l0.self_attn.o_proj.weight.shape),
+                tuple(l0.mlp.gate_up_proj.weight.shape), tuple(l0.mlp.down_proj.weight.shape)]
+
+    def _rs_cfgs(self, M: int):
+        if getattr(self, "_rs_w", None) is None or not self._fusable:
+            return None
+        return gemm.rs_plan(M, self._rs_shapes())
+
+    def _forward_rs(self, input_ids, positions, ctx, cfgs):
+        """The decoder at small M with no RMSNorm launch inside it (K9 SK_ACC_SS /
+        SK_RSCALE, gemm_skinny.hip): o_proj and down_proj add into the residual and leave
+        its per-row sums of squares; qkv and gate_up run on gamma-folded weights and scale
+        their rows by the rsqrt of those sums.  Per layer: qkv, attention, o, gate_up (SiLU
+        pairs), down -- against two more norm launches on the regular path.  Layer 0's
+        input norm (over the embedding) and the final norm stay kernels."""
+        c_qkv, c_o, c_gu, c_dn = cfgs
+        ssp_o, ssp_d = self._rs_ssp
+        res = self.embed_tokens(input_ids)
+        M = res.shape[0]
+        nss_d = 0
+        for i, layer in enumerate(self.layers):
+            at, mlp = layer.self_attn, layer.mlp
+            ln1, ln2 = layer.input_layernorm, layer.post_attention_layernorm
+            qkv_f, gu_f = self._rs_w[i]
+            if i == 0:
+                qkv = at.project_qkv(ln1(res))
+            else:
+                qkv = torch.empty(M, qkv_f.shape[0], dtype=res.dtype, device=res.device)
+                gemm.skinny_rscale(res, qkv_f, c_qkv, ssp_d, nss_d, ln1.eps, qkv)
+            a = at.attend(positions, qkv, ctx)
+            nss_o = gemm.skinny_acc_ss(res, a, at.o_proj.weight, c_o, ssp_o)
+            h = torch.empty(M, gu_f.shape[0] // 2, dtype=res.dtype, device=res.device)
+            gemm.skinny_rscale(res, gu_f, c_gu, ssp_o, nss_o, ln2.eps, h, silu=True)
+            nss_d = gemm.skinny_acc_ss(res, h, mlp.down_proj.weight, c_dn, ssp_d)
+        return self.norm(res)
 
     # ------------------------------------------------------------------ fused small-M decode
     def _fused_cfgs(self, M: int):

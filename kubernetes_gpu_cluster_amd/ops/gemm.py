@@ -43,6 +43,10 @@ _plan_silu: dict[tuple[int, int, int], tuple[int, int, int, bool]] = {}
 # plain plan + fused_add_rms_norm; and the per-device tickets that variant draws
 _plan_accnorm: dict[tuple[int, int, int], tuple[int, int, int, bool]] = {}
 _tickets: dict[torch.device, torch.Tensor] = {}
+# (M, N, K) -> the fastest skinny configuration, chosen over hipBLASLt or not: the
+# norm-free small-M layer (skinny_acc_ss / skinny_rscale) runs every projection on K9
+_best_sk: dict[tuple[int, int, int], tuple] = {}
+_best_silu: dict[tuple[int, int, int], tuple] = {}     # the same for the SiLU epilogue
 _enabled = os.environ.get("KGC_SKINNY_GEMM", "1") != "0"
 
 # K9m mid-batch decode GEMM (csrc/kernels/gemm_decode.hip), M in (SKINNY_MAX_M, DG_MAX_M]:
@@ -294,6 +298,48 @@ def skinny_acc_norm(residual: torch.Tensor, x: torch.Tensor, w: torch.Tensor,
     return out
 
 
+def fold_norm_weight(w: torch.Tensor, gamma: torch.Tensor) -> torch.Tensor:
+    """W' = W diag(gamma) in W's dtype: rms_norm(x) W^T == rsqrt(mean(x^2) + eps) * x W'^T
+    up to where the bf16 roundings fall (the norm-free small-M layer)."""
+    return (w.float() * gamma.float()[None, :]).to(w.dtype).contiguous()
+
+
+def rs_plan(M: int, shapes) -> Optional[list]:
+    """Skinny configurations of (qkv, o, gate_up, down) at this M for the norm-free layer
+    (``LlamaForCausalLM._forward_rs``), or None: every projection needs a timed skinny
+    configuration, gate_up its SiLU one, and the row scale holds M <= 4 * NW rows."""
+    if M > 16:
+        return None
+    (nq, kq), (no, ko), (ng, kg), (nd, kd) = shapes
+    try:
+        c = [_best_sk[(M, nq, kq)], _best_sk[(M, no, ko)], _best_silu[(M, ng, kg)],
+             _best_sk[(M, nd, kd)]]
+    except KeyError:
+        return None
+    if any(cfg[0] != 1 or M > 4 * cfg[2] for cfg in c):
+        return None
+    return c
+
+
+def skinny_acc_ss(residual: torch.Tensor, x: torch.Tensor, w: torch.Tensor, cfg,
+                  ssp: torch.Tensor) -> int:
+    """residual += x W^T, and ssp[m, j] = sum over workgroup j's columns of the new
+    residual row m squared (K9 SK_ACC_SS).  Returns the partials per row."""
+    from . import _k
+    _k().skinny_gemm(residual, x, w, None, *cfg, 5, None, 1e-6, None, None, ssp, 0)
+    return w.shape[0] // (16 * cfg[1])
+
+
+def skinny_rscale(x: torch.Tensor, w_folded: torch.Tensor, cfg, ssp: torch.Tensor, nss: int,
+                  eps: float, out: torch.Tensor, silu: bool = False) -> torch.Tensor:
+    """out = rsqrt(sum_j ssp[m, j] / K + eps) * x W'^T (K9 SK_RSCALE; silu: the SiLU pairs of
+    a folded merged gate_up, SK_RSCALE_SILU) -- rms_norm(x) and the GEMM in one launch."""
+    from . import _k
+    _k().skinny_gemm(out, x, w_folded, None, *cfg, 7 if silu else 6, None, eps, None, None,
+                     ssp, nss)
+    return out
+
+
 def skinny_accum(out: torch.Tensor, x: torch.Tensor, w: torch.Tensor,
                  bias: Optional[torch.Tensor], cfg) -> torch.Tensor:
     """out += x W^T (+ bias) in one launch (K9 SK_ACC epilogue: the residual add)."""
@@ -319,6 +365,8 @@ def fused_norm_plan(M: int, norm_shapes, acc_shapes):
 
 
 def clear_plan() -> None:
+    _best_sk.clear()
+    _best_silu.clear()
     _plan_accnorm.clear()
     _plan_silu.clear()
     _plan_dg.clear()
@@ -421,6 +469,8 @@ def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: floa
                 if t < sk_t:
                     sk_t, sk_cfg = t, cfg
             best = sk_cfg if sk_t < lib_t * margin else None
+            if sk_cfg is not None:
+                _best_sk[(M, N, K)] = sk_cfg
             n = len(ws)
             res[(M, N, K)] = (best, lib_t * 1e3 / n, sk_t * 1e3 / n, sk_cfg)
             _chosen_us[(M, N, K)] = (sk_t if best is not None else lib_t) * 1e3 / n
@@ -578,6 +628,8 @@ def _tune_silu(ws, x, M: int, N: int, K: int, reps: int, margin: float) -> None:
     # both sides are our kernels timed the same way (graphed): the fused one wins when it
     # is faster at all (the margin guards the custom-vs-library choices; here it kept a
     # 42.4 vs 43.7 us / layer SK_SILU out at M = 1)
+    if best_cfg is not None:
+        _best_silu[(M, N, K)] = best_cfg
     if best_cfg is not None and best_t < sep_t:
         _plan_silu[(M, N, K)] = best_cfg
     log.info("gemm M=%d N=%d K=%d silu: plan + silu_mul %.1f us, SK_SILU %s %.1f us -> %s",

@@ -87,6 +87,47 @@ def test_gpu_logits_match_hf_fused_small_m(gpu, name):
         (pos_err.max().item(), scale, cos.min().item())
 
 
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-llama-gqa8"])
+def test_gpu_logits_match_hf_norm_free_small_m(gpu, name):
+    """The norm-free small-M decoder (models/llama.py _forward_rs: o / down add into the
+    residual and leave its sums of squares, qkv / gate_up run on gamma-folded weights with
+    a per-row rsqrt scale; K9 SK_ACC_SS / SK_RSCALE(_SILU)) against HF: prefill chunks of
+    13 and 7 tokens and 1-token decode steps all take it."""
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    cfg = PRESETS[name]
+    sd = full_state_dict_random(cfg, seed=4, std=0.05)
+    hf, _ = _hf_model(cfg, sd)
+    set_state(ParallelState(device=gpu))
+    model = build_model(cfg, torch.bfloat16, gpu)
+    model.load_weights(sd.items())
+    assert model.fold_rs_weights() > 0
+    runner = ModelRunner(model, cfg, torch.bfloat16, gpu, block_size=16, max_model_len=256,
+                         max_num_seqs=4, token_budget=128, enforce_eager=True)
+    runner.init_kv_cache(48)
+    gemm.clear_plan()
+    try:
+        (nq, kq), (no, ko), (ng, kg), (nd, kd) = model._rs_shapes()
+        for M in (13, 7, 1):      # configurations as the start-up tuning records them
+            gemm._best_sk[(M, nq, kq)] = (1, 2, 4, False)
+            gemm._best_sk[(M, no, ko)] = (1, 1, 4, True)
+            gemm._best_silu[(M, ng, kg)] = (1, 2, 4, False)
+            gemm._best_sk[(M, nd, kd)] = (1, 1, 8, False)
+            assert model._rs_cfgs(M) is not None
+        g = torch.Generator().manual_seed(1)
+        prompt = torch.randint(3, cfg.vocab_size, (20,), generator=g).tolist()
+        extra = torch.randint(3, cfg.vocab_size, (4,), generator=g).tolist()
+        with torch.no_grad():
+            ref = hf(torch.tensor([prompt + extra])).logits[0].float()
+        got = _engine_logits(model, runner, prompt, [13, 7], extra).float().cpu()
+    finally:
+        gemm.clear_plan()
+    scale = ref.abs().max().item()
+    pos_err = (got - ref).abs().max(-1).values
+    cos = torch.nn.functional.cosine_similarity(got, ref, dim=-1)
+    assert bool(((pos_err < 0.03 * scale + 1e-3) & (cos > 0.999)).all()), \
+        (pos_err.max().item(), scale, cos.min().item())
+
+
 def _tiny_engine(**kw):
     PRESETS.setdefault("llama-3-8b-2l", PRESETS["llama-3-8b"].shrink(name="llama-3-8b-2l",
                                                                      num_layers=2))

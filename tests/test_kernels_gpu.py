@@ -681,6 +681,42 @@ def test_prefill_attention_fp8(gpu, dt):
     torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(dt))
 
 
+@pytest.mark.parametrize("M", [1, 5, 16])
+@pytest.mark.parametrize("nt_o,nw", [(1, 4), (2, 8)])
+def test_skinny_norm_free_pair(gpu, M, nt_o, nw):
+    """K9 SK_ACC_SS then SK_RSCALE / SK_RSCALE_SILU == residual add, RMSNorm, GEMM in fp32:
+    the producer's per-workgroup sums of squares of the stored residual, the consumer's
+    row scale on the gamma-folded weight (plain and SiLU-pair outputs)."""
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    torch.manual_seed(M + nt_o)
+    dt, H, Kin, N, I = torch.bfloat16, 4096, 1024, 512, 256
+    res = torch.randn(M, H, device=gpu).to(dt)
+    x = (torch.randn(M, Kin, device=gpu) * 0.5).to(dt)
+    wo = (torch.randn(H, Kin, device=gpu) * 0.03).to(dt)
+    gamma = (torch.rand(H, device=gpu) + 0.5).to(dt)
+    w = (torch.randn(N, H, device=gpu) * 0.02).to(dt)
+    wgu = (torch.randn(2 * I, H, device=gpu) * 0.02).to(dt)
+    ssp = torch.full((16 * 256,), float("nan"), device=gpu)
+    r_ref = (res.float() + x.float() @ wo.float().t()).to(dt)
+    nss = gemm.skinny_acc_ss(res, x, wo, (1, nt_o, nw, False), ssp)
+    assert nss == H // (16 * nt_o)
+    torch.testing.assert_close(res.float(), r_ref.float(), atol=2e-2, rtol=1e-2)
+    ss = ssp[: M * nss].view(M, nss).sum(1)
+    torch.testing.assert_close(ss, res.float().pow(2).sum(1), rtol=1e-4, atol=1e-3)
+    inv = torch.rsqrt(res.float().pow(2).mean(1, keepdim=True) + 1e-5)
+    normed = res.float() * inv * gamma.float()
+    out = torch.empty(M, N, dtype=dt, device=gpu)
+    gemm.skinny_rscale(res, gemm.fold_norm_weight(w, gamma), (1, 1, 4, False), ssp, nss, 1e-5,
+                       out)
+    torch.testing.assert_close(out.float(), normed @ w.float().t(), atol=3e-2, rtol=2e-2)
+    act = torch.empty(M, I, dtype=dt, device=gpu)
+    gemm.skinny_rscale(res, gemm.fold_norm_weight(wgu, gamma), (1, 2, 4, False), ssp, nss,
+                       1e-5, act, silu=True)
+    gu = normed @ wgu.float().t()
+    exp = torch.nn.functional.silu(gu[:, :I]) * gu[:, I:]
+    torch.testing.assert_close(act.float(), exp, atol=3e-2, rtol=2e-2)
+
+
 # ------------------------------------------------------------------ K9 skinny GEMM
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("M,N,K", [(1, 6144, 4096), (7, 4096, 14336), (16, 512, 1024),
