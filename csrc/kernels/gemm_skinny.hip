@@ -59,8 +59,16 @@ namespace kgc {
 enum { SK_PLAIN = 0, SK_NORM = 1, SK_ACC = 2, SK_SILU = 3, SK_ACC_NORM = 4, SK_ACC_SS = 5,
        SK_RSCALE = 6, SK_RSCALE_SILU = 7 };
 
+// SK_RSCALE(_SILU) at NT = 2: held to the plain variant's 4 waves per SIMD (128 VGPRs);
+// its few extra registers would otherwise cost a wave of occupancy on a weight stream
+template <int NT, int EPI>
+constexpr int sk_waves_per_eu() {
+  return ((EPI == 6 || EPI == 7) && NT == 2) ? 4 : 1;
+}
+
 template <typename T, int MT, int NT, int NW, bool NTL, int EPI>
-__global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
+__global__ __launch_bounds__(NW * 64)
+__attribute__((amdgpu_waves_per_eu(sk_waves_per_eu<NT, EPI>()))) void skinny_gemm_kernel(
     T* __restrict__ C, const T* __restrict__ X, const T* __restrict__ W,
     const T* __restrict__ bias, const T* __restrict__ gamma, float eps, int M, int K,
     int64_t ldx, int64_t ldc, T* __restrict__ NO, uint32_t* __restrict__ ticket,
@@ -76,6 +84,7 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
   __shared__ __attribute__((aligned(16))) float red[NW][MT][NT][64][4];
   __shared__ float ssr[NORM ? NW : 1][MT][64];  // per-lane partial sums of squares
   __shared__ float inv_s[16 * MT];
+  __shared__ float ssl[RS ? 16 : 1][RS ? 256 : 1];  // SK_RSCALE: the rows' partials (LDS-DMA)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r16 = lane & 15, q4 = lane >> 4;
   // SK_SILU: gridDim.x = I / 16 workgroups over the I = 16 * gridDim.x output columns
@@ -154,18 +163,24 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
   WSet wa, wb;
   XSet xa, xb;
   GSet ga, gb;
-  if (nb > 0) load(wa, xa, ga, k);
-  // SK_RSCALE: the sum-of-squares partials of this wave's rows (m = wave + r * NW) ride
-  // behind the first weight batch; the host keeps nss <= 256 and M <= 4 * NW
-  float ssv[RS ? 4 : 1][RS ? 4 : 1];
+  // SK_RSCALE: the sum-of-squares partials of this wave's rows (m = wave + r * NW) go out
+  // ahead of the first weight batch straight into LDS (LDS-DMA, addresses dead before the
+  // weight stream -- as register loads they cost a wave per SIMD of occupancy); the host
+  // keeps nss <= 256 and M <= 16
+  constexpr int RSR = (16 + NW - 1) / NW;
   if constexpr (RS) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < RSR; ++r) {
+      const int m = min(wave + r * NW, M - 1);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int m = min(wave + r * NW, M - 1), j = min(lane + 64 * i, nss - 1);
-        ssv[r][i] = SSP[(int64_t)m * nss + j];
+        const int j = min(lane + 64 * i, nss - 1);
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(SSP + (int64_t)m * nss + j),
+            (__attribute__((address_space(3))) void*)&ssl[wave + r * NW][64 * i], 4, 0, 0);
       }
+  if (nb > 0) load(wa, xa, ga, k);
+    }
   }
   for (int b = 0; b < nb; b += 2) {
     if (b + 1 < nb) load(wb, xb, gb, k + 32 * U);
@@ -196,14 +211,21 @@ __global__ __launch_bounds__(NW * 64) void skinny_gemm_kernel(
     if constexpr (NORM) ssr[wave][mt][lane] = ss[mt];
   }
   if constexpr (RS) {
+    // this wave's own partials landed (its LDS-DMAs are older than every weight load the
+    // loop above waited for; vmcnt(0) for certainty) -- and only this wave reads them
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the lane index re-derived behind an opaque move: nothing of this block is hoisted
+    // into the weight loop, where it would hold registers (and cost a wave of occupancy)
+    int ln = threadIdx.x & 63;
+    asm volatile("" : "+v"(ln));
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < RSR; ++r) {
       const int m = wave + r * NW;
       float t = 0.f;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) t += lane + 64 * i < nss ? ssv[r][i] : 0.f;
+      for (int i = 0; i < 4; ++i) t += ln + 64 * i < nss ? ssl[m < 16 ? m : 0][64 * i + ln] : 0.f;
       t = wave_sum(t);
-      if (lane == 0 && m < M && m < 16 * MT) inv_s[m] = rsqrtf(t / (float)K + eps);
+      if (ln == 0 && m < M && m < 16 * MT) inv_s[m] = rsqrtf(t / (float)K + eps);
     }
   }
   __syncthreads();
