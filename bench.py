@@ -385,8 +385,14 @@ def main_service(args):
                     if bad:
                         raise RuntimeError(f"warmup: {len(bad)} requests failed "
                                            f"(status {bad[0].status})")
+                # engine-side window opens at the LAST rank's barrier entry: every warmup
+                # request arrived before it, every timed one after (a rank that leaves the
+                # barrier early may send before this rank's t0)
+                t_lo = time.monotonic()
                 if world > 1:
-                    dist.barrier()
+                    ents = [None] * world
+                    dist.all_gather_object(ents, t_lo)
+                    t_lo = max(ents)
                 t0 = time.monotonic()
                 c0 = sc.cpu_seconds(router.pid) if router is not None else 0.0
                 for prompts in timed:
@@ -396,16 +402,16 @@ def main_service(args):
                     dist.barrier()
                 t1 = time.monotonic()
                 c1 = sc.cpu_seconds(router.pid) if router is not None else 0.0
-                return out, t0, t1 - t0, c1 - c0
+                return out, t0, t1 - t0, c1 - c0, t_lo
 
-        waves_out, t0, elapsed, router_cpu = asyncio.run(run_all())
+        waves_out, t0, elapsed, router_cpu, t_lo = asyncio.run(run_all())
         for r, lo, hi in waves_out:
             res_all += r
         # one window over all timed waves: behind the shared router a replica also serves
         # other ranks' requests, whose waves need not line up with this rank's
-        windows.append((t0, t0 + elapsed))
+        windows.append((min(t_lo, t0), t0 + elapsed))
         if leader:
-            with urllib.request.urlopen(f"{api_url}/kgc/engine_stats?since={t0 - 1.0}", timeout=30) as f:
+            with urllib.request.urlopen(f"{api_url}/kgc/engine_stats?since={t_lo - 1.0}", timeout=30) as f:
                 st = json.loads(f.read())
             eng = sc.engine_figures(st["requests"], windows)
             eng["steps"] = st["steps"]
