@@ -179,9 +179,9 @@ __attribute__((amdgpu_waves_per_eu(sk_waves_per_eu<NT, EPI>()))) void skinny_gem
             (const __attribute__((address_space(1))) void*)(SSP + (int64_t)m * nss + j),
             (__attribute__((address_space(3))) void*)&ssl[wave + r * NW][64 * i], 4, 0, 0);
       }
-  if (nb > 0) load(wa, xa, ga, k);
     }
   }
+  if (nb > 0) load(wa, xa, ga, k);
   for (int b = 0; b < nb; b += 2) {
     if (b + 1 < nb) load(wb, xb, gb, k + 32 * U);
     compute(wa, xa, ga);

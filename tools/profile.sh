@@ -23,8 +23,8 @@ fi
 rocprofv3 --kernel-trace --stats -d "$out" -o run -- "$@"
 db=$(find "$out" -name 'run_results.db' | head -1)
 if [[ -n "$db" ]]; then
-  python "$HERE/trace_summary.py" "$db" --steps | tee "$out/summary.txt"
+  python "$HERE/trace_summary.py" "$db" --steps ${DETAIL:+--detail} | tee "$out/summary.txt"
 else
   csv=$(find "$out" -name '*kernel_trace.csv' | head -1)
-  python "$HERE/trace_summary.py" "$csv" --steps | tee "$out/summary.txt"
+  python "$HERE/trace_summary.py" "$csv" --steps ${DETAIL:+--detail} | tee "$out/summary.txt"
 fi

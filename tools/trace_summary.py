@@ -76,6 +76,20 @@ def main():
             agg.update(s[3])
         for k, v in agg.most_common(16):
             print(f"   {k:38} {v / len(dec) / 1e3:9.1f} us/step")
+        if "--detail" in sys.argv:
+            # per kernel instantiation (template arguments kept): calls per step, us per call
+            byname, ncall = collections.Counter(), collections.Counter()
+            for a, b in zip(samp, samp[1:]):
+                seg = ev[a + 1:b + 1]
+                if len(seg) != nk:
+                    continue
+                for s, e, n in seg:
+                    byname[n] += e - s
+                    ncall[n] += 1
+            print("\ndecode-step kernels by instantiation (calls/step, us/call, us/step):")
+            for n, v in byname.most_common(24):
+                c = ncall[n] / len(dec)
+                print(f"   {c:6.1f} {v / ncall[n] / 1e3:8.2f} {v / len(dec) / 1e3:9.1f}  {n[:110]}")
         # prefill (chunked) steps: the ones that run the prefill attention kernel and no
         # decode-sized GEMM (start-up tuning runs those between sampler calls too)
         pre = [s for s in steps if s[3].get("prefill_attn", 0) > 0
