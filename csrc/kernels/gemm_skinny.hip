@@ -171,9 +171,11 @@ __attribute__((amdgpu_waves_per_eu(sk_waves_per_eu<NT, EPI>()))) void skinny_gem
   if constexpr (RS) {
 #pragma unroll
     for (int r = 0; r < RSR; ++r) {
-      const int m = min(wave + r * NW, M - 1);
+      const int m = wave + r * NW;
+      if (m >= M) break;                 // wave-uniform: rows past the batch load nothing
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+        if (64 * i >= nss) break;        // uniform too: nss = 64 covers one DMA per row
         const int j = min(lane + 64 * i, nss - 1);
         __builtin_amdgcn_global_load_lds(
             (const __attribute__((address_space(1))) void*)(SSP + (int64_t)m * nss + j),
@@ -221,6 +223,7 @@ __attribute__((amdgpu_waves_per_eu(sk_waves_per_eu<NT, EPI>()))) void skinny_gem
 #pragma unroll
     for (int r = 0; r < RSR; ++r) {
       const int m = wave + r * NW;
+      if (m >= M) break;
       float t = 0.f;
 #pragma unroll
       for (int i = 0; i < 4; ++i) t += ln + 64 * i < nss ? ssl[m < 16 ? m : 0][64 * i + ln] : 0.f;

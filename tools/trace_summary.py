@@ -78,14 +78,27 @@ def main():
             print(f"   {k:38} {v / len(dec) / 1e3:9.1f} us/step")
         if "--detail" in sys.argv:
             # per kernel instantiation (template arguments kept): calls per step, us per call
+            # an instantiation called k times per layer (o and down share one) is split by
+            # its occurrence index mod k: "#0", "#1" in call order
+            per_step = collections.Counter(n for s, e, n in ev[samp[0] + 1:samp[1] + 1])
+            layers = 32
+            for a, b in zip(samp, samp[1:]):
+                seg = ev[a + 1:b + 1]
+                if len(seg) == nk:
+                    per_step = collections.Counter(n for s, e, n in seg)
+                    break
             byname, ncall = collections.Counter(), collections.Counter()
             for a, b in zip(samp, samp[1:]):
                 seg = ev[a + 1:b + 1]
                 if len(seg) != nk:
                     continue
+                seen = collections.Counter()
                 for s, e, n in seg:
-                    byname[n] += e - s
-                    ncall[n] += 1
+                    k = per_step[n] // layers if per_step[n] % layers == 0 else 1
+                    key = f"#{seen[n] % k} {n}" if k > 1 else n
+                    seen[n] += 1
+                    byname[key] += e - s
+                    ncall[key] += 1
             print("\ndecode-step kernels by instantiation (calls/step, us/call, us/step):")
             for n, v in byname.most_common(24):
                 c = ncall[n] / len(dec)
