@@ -74,6 +74,8 @@ def parse():
     ap.add_argument("--enforce-eager", action="store_true")
     ap.add_argument("--gpu-memory-utilization", type=float, default=0.90)
     ap.add_argument("--dtype", default="bfloat16")
+    ap.add_argument("--num-gpu-blocks-override", type=int, default=None,
+                    help="fixed KV blocks per replica (replicas sharing one GPU: KGC_BENCH_DEVICES)")
     ap.add_argument("--temperature", type=float, default=1.0)
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--prefix-caching", type=int, default=1, choices=[0, 1],
@@ -278,7 +280,10 @@ def _server_devices(local_rank: int, tp: int, cpu: bool):
     this process may see (None on the CPU path)."""
     if cpu:
         return None
-    vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES")
+    # KGC_BENCH_DEVICES="0,0": rehearse several replicas on one GPU (each replica's
+    # --gpu-memory-utilization share must then fit beside the others')
+    vis = (os.environ.get("KGC_BENCH_DEVICES") or os.environ.get("HIP_VISIBLE_DEVICES")
+           or os.environ.get("CUDA_VISIBLE_DEVICES"))
     ids = vis.split(",") if vis else [str(i) for i in range(local_rank + tp)]
     return ",".join(ids[local_rank:local_rank + tp])
 
@@ -290,6 +295,8 @@ def _engine_args(args, cpu: bool) -> list:
           "--max-num-batched-tokens", str(args.max_num_batched_tokens),
           "--gpu-memory-utilization", str(args.gpu_memory_utilization),
           "--disable-log-requests"]
+    if args.num_gpu_blocks_override:
+        ea += ["--num-gpu-blocks-override", str(args.num_gpu_blocks_override)]
     if not args.prefix_caching:
         ea.append("--no-enable-prefix-caching")
     if args.enforce_eager:
