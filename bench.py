@@ -427,7 +427,10 @@ def main_service(args):
         if leader and procs:
             _note(f"rank {rank}: service stopped (exit codes {codes})")
     probe = None
-    if world > 1 and not cpu and args.comm_probe:
+    devs = [d for d in os.environ.get("KGC_BENCH_DEVICES", "").split(",") if d]
+    shared = len(devs) > len(set(devs))
+    if world > 1 and not cpu and args.comm_probe and not shared:
+        # (replicas sharing one GPU: RCCL takes one rank per device, so no probe)
         probe = _comm_probe(rank, world, local_rank)
     ok = [r for r in res_all if r.ok]
     mine = {"toks": sum(r.tokens for r in ok), "failed": len(res_all) - len(ok),
