@@ -59,16 +59,20 @@ namespace kgc {
 enum { SK_PLAIN = 0, SK_NORM = 1, SK_ACC = 2, SK_SILU = 3, SK_ACC_NORM = 4, SK_ACC_SS = 5,
        SK_RSCALE = 6, SK_RSCALE_SILU = 7 };
 
-// SK_RSCALE(_SILU) at NT = 2: held to the plain variant's 4 waves per SIMD (128 VGPRs);
+// SK_RSCALE(_SILU) at MT = 1, NT = 2 (the shapes the model runs): held to the plain variant's 4 waves per SIMD (128 VGPRs);
 // its few extra registers would otherwise cost a wave of occupancy on a weight stream
-template <int NT, int EPI>
+template <int MT, int NT, int EPI>
 constexpr int sk_waves_per_eu() {
-  return ((EPI == 6 || EPI == 7) && NT == 2) ? 4 : 1;
+  return ((EPI == 6 || EPI == 7) && MT == 1 && NT == 2) ? 4 : 1;
 }
+
+// s_waitcnt immediate that waits for vmcnt <= n only (gfx9 encoding: vmcnt in bits 3:0 and
+// 15:14, expcnt 6:4 and lgkmcnt 11:8 left at their maxima)
+constexpr int sk_vmcnt(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
 
 template <typename T, int MT, int NT, int NW, bool NTL, int EPI>
 __global__ __launch_bounds__(NW * 64)
-__attribute__((amdgpu_waves_per_eu(sk_waves_per_eu<NT, EPI>()))) void skinny_gemm_kernel(
+__attribute__((amdgpu_waves_per_eu(sk_waves_per_eu<MT, NT, EPI>()))) void skinny_gemm_kernel(
     T* __restrict__ C, const T* __restrict__ X, const T* __restrict__ W,
     const T* __restrict__ bias, const T* __restrict__ gamma, float eps, int M, int K,
     int64_t ldx, int64_t ldc, T* __restrict__ NO, uint32_t* __restrict__ ticket,
@@ -183,15 +187,34 @@ __attribute__((amdgpu_waves_per_eu(sk_waves_per_eu<NT, EPI>()))) void skinny_gem
       }
     }
   }
-  if (nb > 0) load(wa, xa, ga, k);
+  // Two register sets in flight; the compiler's wait-count pass places the waits.  The
+  // SK_RSCALE forms issue both batches and then retire their (older) partial DMAs with a
+  // compiler-visible wait: a DMA still counted at the loop header made every iteration
+  // wait for vmcnt(0) (qkv at batch 1: 12.4 vs 12.9 us with the DMA retired first).
+  // (A hand-placed in-order pipeline -- explicit vmcnt(loads per batch) waits fenced by
+  // sched_barrier, one straight steady-state path -- was measured: down -2.9 us, but it
+  // costs the NT = 2 forms a wave per SIMD and the decode step was no faster;
+  // profiles/README.md "Norm-free small-M decoder layer".)
+  constexpr int LB = U * (NT + MT + (NORM ? 1 : 0));   // vector loads per batch
+  auto kb = [&](int bi) { return kbeg + bi * 32 * U; };
+  if (nb > 0) load(wa, xa, ga, kb(0));
+  if constexpr (RS) {
+    if (nb > 1) {
+      load(wb, xb, gb, kb(1));
+      __builtin_amdgcn_s_waitcnt(sk_vmcnt(2 * LB));
+    } else if (nb > 0) {
+      __builtin_amdgcn_s_waitcnt(sk_vmcnt(LB));
+    } else {
+      __builtin_amdgcn_s_waitcnt(sk_vmcnt(0));
+    }
+  }
   for (int b = 0; b < nb; b += 2) {
-    if (b + 1 < nb) load(wb, xb, gb, k + 32 * U);
+    if (b + 1 < nb && !(RS && b == 0)) load(wb, xb, gb, kb(b + 1));
     compute(wa, xa, ga);
     if (b + 1 < nb) {
-      if (b + 2 < nb) load(wa, xa, ga, k + 64 * U);
+      if (b + 2 < nb) load(wa, xa, ga, kb(b + 2));
       compute(wb, xb, gb);
     }
-    k += 64 * U;
   }
   k = kbeg + nb * 32 * U;
   for (; k < kend; k += 32) {     // K-range not a multiple of 32*U

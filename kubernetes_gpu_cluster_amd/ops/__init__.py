@@ -19,6 +19,8 @@ from . import reference as ref
 DEBUG = os.environ.get("KGC_HIP_DEBUG", "0") not in ("", "0")
 _SO = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                    "_kgc_ops_debug.so" if DEBUG else "_kgc_ops.so")
+# KGC_OPS_SO=path: another build of the same library (same-box A/B of two kernel builds)
+_SO = os.environ.get("KGC_OPS_SO") or _SO
 _loaded: Optional[bool] = None
 _load_err: Optional[str] = None
 

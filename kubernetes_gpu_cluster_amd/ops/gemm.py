@@ -47,6 +47,10 @@ _tickets: dict[torch.device, torch.Tensor] = {}
 # norm-free small-M layer (skinny_acc_ss / skinny_rscale) runs every projection on K9
 _best_sk: dict[tuple[int, int, int], tuple] = {}
 _best_silu: dict[tuple[int, int, int], tuple] = {}     # the same for the SiLU epilogue
+# norm-free layer (rs_plan): the fastest configuration of each epilogue AS IT RUNS there --
+# ("ss" | "rs" | "rss", M, N, K) for SK_ACC_SS / SK_RSCALE / SK_RSCALE_SILU (the plain
+# GEMM's ranking does not carry over: the epilogues cost differently per tile shape)
+_best_rs: dict[tuple, tuple] = {}
 _enabled = os.environ.get("KGC_SKINNY_GEMM", "1") != "0"
 
 # K9m mid-batch decode GEMM (csrc/kernels/gemm_decode.hip), M in (SKINNY_MAX_M, DG_MAX_M]:
@@ -312,8 +316,10 @@ def rs_plan(M: int, shapes) -> Optional[list]:
         return None
     (nq, kq), (no, ko), (ng, kg), (nd, kd) = shapes
     try:
-        c = [_best_sk[(M, nq, kq)], _best_sk[(M, no, ko)], _best_silu[(M, ng, kg)],
-             _best_sk[(M, nd, kd)]]
+        c = [_best_rs.get(("rs", M, nq, kq)) or _best_sk[(M, nq, kq)],
+             _best_rs.get(("ss", M, no, ko)) or _best_sk[(M, no, ko)],
+             _best_rs.get(("rss", M, ng, kg)) or _best_silu[(M, ng, kg)],
+             _best_rs.get(("ss", M, nd, kd)) or _best_sk[(M, nd, kd)]]
     except KeyError:
         return None
     if any(cfg[0] != 1 or M > 4 * cfg[2] for cfg in c):
@@ -367,6 +373,7 @@ def fused_norm_plan(M: int, norm_shapes, acc_shapes):
 def clear_plan() -> None:
     _best_sk.clear()
     _best_silu.clear()
+    _best_rs.clear()
     _plan_accnorm.clear()
     _plan_silu.clear()
     _plan_dg.clear()
@@ -401,6 +408,38 @@ def accnorm_plan() -> dict:
     return dict(_plan_accnorm)
 
 
+def _tune_rs(ws, x, M: int, N: int, K: int, reps: int, kind: str) -> None:
+    """Time the norm-free layer's epilogue ``kind`` on every configuration it can run
+    (one m-tile, M <= 4 * NW; SiLU pairs: NT = 2) and record the fastest in _best_rs."""
+    ssp = torch.zeros(16 * 256, dtype=torch.float32, device=x.device)
+    best_t, best = float("inf"), None
+    for cfg in _CONFIGS:
+        mt, nt, nw, _ = cfg
+        if mt != 1 or M > 4 * nw or not skinny_ok(M, N, K, cfg) or (kind == "rss" and nt != 2):
+            continue
+        if kind == "ss":
+            if M * (N // (16 * nt)) > ssp.numel():
+                continue
+            res = torch.zeros(M, N, dtype=x.dtype, device=x.device)
+
+            def fn(cfg=cfg, res=res):
+                for w in ws:
+                    skinny_acc_ss(res, x, w, cfg, ssp)
+        else:
+            out = torch.empty(M, N // 2 if kind == "rss" else N, dtype=x.dtype, device=x.device)
+
+            def fn(cfg=cfg, out=out):
+                for w in ws:
+                    skinny_rscale(x, w, cfg, ssp, 256, 1e-6, out, silu=kind == "rss")
+        t = _time(fn, reps)
+        if t < best_t:
+            best_t, best = t, cfg
+    if best is not None:
+        _best_rs[(kind, M, N, K)] = best
+        log.info("gemm M=%d N=%d K=%d norm-free %s: %s %.1f us", M, N, K, kind, best,
+                 best_t * 1e3 / len(ws))
+
+
 def _time(fn, reps: int) -> float:
     fn()
     torch.cuda.synchronize()
@@ -428,7 +467,7 @@ def _time_graphed(body, reps: int) -> float:
 @torch.inference_mode()
 def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: float = 0.97,
                 reps: int = 3, norm_shapes=(), norm_max_m: int = 16, silu_shapes=(),
-                tail_shapes=(), qkv_dims=None) -> dict:
+                tail_shapes=(), qkv_dims=None, rs_shapes: bool = False) -> dict:
     """Time hipBLASLt against every skinny configuration for each weight shape and
     batch size M (decode buckets <= SKINNY_MAX_M) and record the skinny kernel where it
     is faster by more than ``1 - margin``.  Each timing sweeps ALL weights of the shape
@@ -438,7 +477,9 @@ def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: floa
     ``silu_shapes``: (N, K) of merged gate_up weights, whose split-K candidates are timed
     with the fused SiLU reduction against hipBLASLt + silu_mul (``linear_silu``).
     ``tail_shapes``: (N, K) of row-parallel projections feeding a residual add + RMSNorm
-    (``linear_add_rms``), timed with that norm on both sides."""
+    (``linear_add_rms``), timed with that norm on both sides.  ``rs_shapes``: also time the
+    norm-free layer's epilogues at M <= 16 (tail -> SK_ACC_SS, norm -> SK_RSCALE, silu ->
+    SK_RSCALE_SILU) for ``rs_plan``."""
     if not _enabled:
         return {}
     by_shape: dict[tuple[int, int], list[torch.Tensor]] = {}
@@ -482,6 +523,11 @@ def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: floa
                 _tune_silu(ws, x, M, N, K, reps, margin)
             if (N, K) in tail_shapes and N % 512 == 0 and N <= 8192:
                 _tune_accnorm(ws, x, M, N, K, reps, margin)
+            if M <= 16 and rs_shapes:
+                kind = ("rss" if (N, K) in silu_shapes else "ss" if (N, K) in tail_shapes
+                        else "rs" if (N, K) in norm_shapes else None)
+                if kind is not None:
+                    _tune_rs(ws, x, M, N, K, reps, kind)
             log.info("gemm M=%d N=%d K=%d: hipBLASLt %.1f us, skinny %s %.1f us -> %s", M, N, K,
                      lib_t * 1e3 / n, sk_cfg, sk_t * 1e3 / n, "skinny" if best else "hipBLASLt")
         if _dg_enabled:

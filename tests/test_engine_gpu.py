@@ -530,6 +530,12 @@ def test_pp2_stage_graphs_on_one_gpu(gpu, tmp_path, monkeypatch):
     prompts = [list(range(3, 40)), [5, 6, 7] * 20, [9, 10, 11], [4] * 9]
     sp = [SamplingParams(temperature=0, max_tokens=12, ignore_eos=True)] * 4
     monkeypatch.setenv("KGC_DIST_BACKEND", "gloo")
+    # one arithmetic on both sides: the norm-free small-M layer (PP = 1 only: it needs the
+    # whole model on one rank) rounds differently -- gamma folded into the weights, the
+    # residual not normalised before its GEMM -- and the random model's near-ties then flip
+    # greedy tokens (its own parity is tests/test_engine_gpu.py ..._norm_free_small_m)
+    from kubernetes_gpu_cluster_amd.models import llama as llama_mod
+    monkeypatch.setattr(llama_mod, "_rs_enabled", False)
     outs = {}
     for pp in (1, 2):
         llm = LLM(d, device="cuda", dtype="bfloat16", pipeline_parallel_size=pp,

@@ -823,6 +823,32 @@ def test_tune_skinny_silu_records_plan(gpu):
         gemm.clear_plan()
 
 
+def test_tune_skinny_times_norm_free_epilogues(gpu):
+    """With rs_shapes the tuner times SK_ACC_SS (tail shapes), SK_RSCALE (norm shapes) and
+    SK_RSCALE_SILU (merged gate_up) themselves at M <= 16, and rs_plan takes those
+    configurations -- each one a form the norm-free layer can run (one m-tile,
+    M <= 4 * NW, SiLU pairs at NT = 2)."""
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    torch.manual_seed(10)
+    shapes = [(768, 512), (512, 512), (2048, 512), (512, 1024)]   # qkv, o, gate_up, down
+    ws = [torch.randn(n, k, dtype=torch.bfloat16, device=gpu) * 0.02
+          for n, k in shapes for _ in range(2)]
+    try:
+        gemm.tune_skinny(ws, [1, 8], norm_shapes={shapes[0], shapes[2]},
+                         silu_shapes={shapes[2]}, tail_shapes={shapes[1], shapes[3]},
+                         rs_shapes=True)
+        for M in (1, 8):
+            plan = gemm.rs_plan(M, shapes)
+            assert plan is not None
+            want = [gemm._best_rs[("rs", M) + shapes[0]], gemm._best_rs[("ss", M) + shapes[1]],
+                    gemm._best_rs[("rss", M) + shapes[2]], gemm._best_rs[("ss", M) + shapes[3]]]
+            assert plan == want
+            assert all(c[0] == 1 and M <= 4 * c[2] for c in plan) and plan[2][1] == 2
+    finally:
+        gemm.clear_plan()
+    assert not gemm._best_rs
+
+
 @pytest.mark.parametrize("cfg", list(range(11)))
 @pytest.mark.parametrize("M,N,K", [(256, 1024, 4096), (200, 768, 1024), (77, 512, 2048),
                                    (130, 256, 128)])
