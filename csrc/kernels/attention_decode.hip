@@ -44,7 +44,6 @@ constexpr int DEC_MAX_Z = 1024;  // z-slices the reduce kernel merges (host-chec
 // K1w runs where the grid has at least this many (seq, kv-head) pairs; smaller batches
 // take the 4-wave kernel (B = 1: 9.3 vs 12.3 us at ctx 640; ops/__init__.py mirrors it)
 constexpr int DEC_WAVE_MIN_PAIRS = 64;
-constexpr int DEC_WIDE_MAX_PAIRS = 8;
 
 // K1w: 32-token chunks per z-slice (>= 2, the pipeline depth); slices past the context are
 // empty and the reduce stops at decode_used_slices
@@ -207,8 +206,8 @@ __device__ __forceinline__ void decode_kv_write(const DecodeRope& rp, int b, int
 // kc_ / vc_ themselves (const_cast), so every store and load of the cache is based on
 // the same __restrict__ pointer and the workgroup fence orders them.
 template <typename T, int D, bool PREF, bool KV8, int OCC = 3, int NCH = DEC_CHUNKS,
-          bool FUSE = false, int NWV = 4>
-__global__ __launch_bounds__(NWV * 64, OCC) void paged_decode_kernel(
+          bool FUSE = false>
+__global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
     T* __restrict__ out, const T* __restrict__ q, const void* __restrict__ kc_,
     const void* __restrict__ vc_, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ ctx_lens, float* __restrict__ max_logits,
@@ -226,8 +225,8 @@ __global__ __launch_bounds__(NWV * 64, OCC) void paged_decode_kernel(
   constexpr int DT = D / 16;      // 16-row d-tiles of O^T
   // rows padded by 4 floats: the b128 stores of lanes (head r16, qd) land in (r16 + qd) mod 16
   // bank groups, 4 lanes each (the b128 minimum), instead of 16 heads on one group
-  __shared__ __attribute__((aligned(16))) float lds_o[NWV][16][D + 4];
-  __shared__ float lds_m[NWV][16], lds_l[NWV][16];
+  __shared__ __attribute__((aligned(16))) float lds_o[4][16][D + 4];
+  __shared__ float lds_m[4][16], lds_l[4][16];
   // q rows padded by 8 elements: unpadded, the 256-B rows put the 16 heads a b128 read
   // gathers on the same 4 banks (393K bank-conflict cycles per dispatch at B = 256)
   __shared__ __attribute__((aligned(16))) T lds_q[FUSE ? 16 : 1][FUSE ? D + 8 : 8];
@@ -259,7 +258,7 @@ __global__ __launch_bounds__(NWV * 64, OCC) void paged_decode_kernel(
   // chunk; the other chunk's loads clamp to the wave's last token (cache hits) and
   // its scores are masked.
   const int nchunk = (ctx + 31) >> 5;
-  const int nwk = gridDim.z * NWV, wk = blockIdx.z * NWV + wave;
+  const int nwk = gridDim.z * 4, wk = blockIdx.z * 4 + wave;
   const int c0 = (int)(((int64_t)nchunk * wk) / nwk);
   const int c1 = (int)(((int64_t)nchunk * (wk + 1)) / nwk);
   const int end = min(ctx, c1 << 5);       // this wave's token range is [c0*32, end)
@@ -329,7 +328,7 @@ __global__ __launch_bounds__(NWV * 64, OCC) void paged_decode_kernel(
       *reinterpret_cast<u32x4*>(&lds_q[g][c * 8]) = oa.u;
       *reinterpret_cast<u32x4*>(&lds_q[g][D / 2 + c * 8]) = ob.u;
     }
-    if (wave == NWV - 1 && blockIdx.z == gridDim.z - 1 && ctx > 0)
+    if (wave == 3 && blockIdx.z == gridDim.z - 1 && ctx > 0)
       decode_kv_write<T, D, KV8>(rp, b, h, nq, nkv, bs_log2, num_blocks,
                                  const_cast<void*>(kc_), const_cast<void*>(vc_), lane);
     // release the k / v stores to the workgroup (same CU, same L1) and the LDS q
@@ -420,15 +419,13 @@ __global__ __launch_bounds__(NWV * 64, OCC) void paged_decode_kernel(
   }
   __syncthreads();
   const bool direct = gridDim.z == 1;
-  for (int e = threadIdx.x; e < G * D; e += NWV * 64) {
+  for (int e = threadIdx.x; e < G * D; e += 256) {
     const int hh = e / D, d = e % D;
-    float M = lds_m[0][hh];
-#pragma unroll
-    for (int w = 1; w < NWV; ++w) M = fmaxf(M, lds_m[w][hh]);
+    float M = fmaxf(fmaxf(lds_m[0][hh], lds_m[1][hh]), fmaxf(lds_m[2][hh], lds_m[3][hh]));
     float acc = 0.f, L = 0.f;
     if (M != -INFINITY) {
 #pragma unroll
-      for (int w = 0; w < NWV; ++w) {
+      for (int w = 0; w < 4; ++w) {
         const float f = exp2f(lds_m[w][hh] - M);
         acc += f * lds_o[w][hh][d];
         L += f * lds_l[w][hh];
@@ -848,15 +845,6 @@ bool decode_use_wave(int B, int nkv) {
   return decode_wave_enabled() && (int64_t)B * nkv >= decode_wave_min_pairs();
 }
 
-// Up to this many (seq, kv-head) pairs a grid of Z = 1 runs the 16-wave workgroup: the
-// context is split over 16 waves of one workgroup and merged in LDS, so no partials and no
-// reduce launch (batch 1: one launch per layer fewer).  KGC_DECODE_WIDE_MAX_PAIRS overrides
-// (0: off); ops/__init__.py reads the same variable to ask for Z = 1.
-static int decode_wide_max_pairs() {
-  const char* e = getenv("KGC_DECODE_WIDE_MAX_PAIRS");
-  return e ? atoi(e) : DEC_WIDE_MAX_PAIRS;
-}
-
 template <typename T, int D, bool KV8, bool FUSE>
 static void decode_dispatch(void* out, const void* q, const void* kc, const void* vc,
                             const int* bt, int bt_stride, const int* ctx, float* ml, float* es,
@@ -867,10 +855,6 @@ static void decode_dispatch(void* out, const void* q, const void* kc, const void
   if (wave) {
     paged_decode_wave_kernel<T, D, KV8, FUSE><<<dim3(B, nkv, Z), 64, 0, s>>>(
         (T*)out, (const T*)q, kc, vc, bt, bt_stride, ctx, ml, es, tmp, nq, nkv, bs_log2,
-        scale_log2, v_scale, num_blocks, rp);
-  } else if (Z == 1 && (int64_t)B * nkv <= decode_wide_max_pairs()) {
-    paged_decode_kernel<T, D, true, KV8, 1, 1, FUSE, 16><<<dim3(B, nkv, 1), 1024, 0, s>>>(
-        (T*)out, (const T*)q, kc, vc, bt, bt_stride, ctx, ml, es, tmp, nq, nkv, bs_log2, 1,
         scale_log2, v_scale, num_blocks, rp);
   } else {
     paged_decode_kernel<T, D, true, KV8, 4, 1, FUSE><<<dim3(B, nkv, Z), 256, 0, s>>>(
@@ -934,7 +918,6 @@ void launch_paged_decode_rope(int dtype, const DecodeRope& rp, void* out, void* 
 }
 
 int paged_decode_wave_min_pairs() { return decode_wave_enabled() ? decode_wave_min_pairs() : -1; }
-int paged_decode_wide_max_pairs() { return decode_wide_max_pairs(); }
 
 KGC_DEBUG_TU(attention_decode)
 

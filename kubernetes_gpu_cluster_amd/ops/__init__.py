@@ -169,7 +169,6 @@ DECODE_PARTITION = 64        # tokens per wave-iteration of the 4-wave decode ke
 DECODE_CHUNK = 32            # tokens per pipelined step of K1w
 DECODE_TARGET_WAVES = 2048   # K1w: 8 resident waves per CU (2 per SIMD at 256 VGPRs)
 DECODE_WAVE_MIN_PAIRS = 64   # attention_decode.hip DEC_WAVE_MIN_PAIRS
-DECODE_WIDE_MAX_PAIRS = 8    # attention_decode.hip DEC_WIDE_MAX_PAIRS
 PREFILL_BLOCK_M = 128
 
 
@@ -215,22 +214,12 @@ def _decode_z_cap(ws, B: int, nq: int) -> int:
     return max(1, min(1024, ws[0].numel() // max(1, B * nq)))
 
 
-def decode_uses_wide(batch: int, num_kv_heads: int) -> bool:
-    """Grids of at most DECODE_WIDE_MAX_PAIRS (seq, kv-head) pairs run Z = 1 on the 16-wave
-    workgroup (context split over its waves, merged in LDS: no reduce launch); the C++
-    launcher reads the same KGC_DECODE_WIDE_MAX_PAIRS."""
-    lim = int(os.environ.get("KGC_DECODE_WIDE_MAX_PAIRS", DECODE_WIDE_MAX_PAIRS))
-    return batch * num_kv_heads <= lim and not decode_uses_wave(batch, num_kv_heads)
-
-
 def decode_grid_z(batch: int, num_kv_heads: int, max_ctx: int, target_waves: int = 0) -> int:
     """z-slices of the decode grid: enough waves to fill 256 CUs, bounded by the
     context (K1w: two 32-token chunks per wave; 4-wave kernel: 64-token partitions) and by
-    the 1024 slices the reduce kernel merges.  Z == 1 (large batches, and the 16-wave
-    workgroup at the smallest) lets the kernel write its output directly."""
+    the 1024 slices the reduce kernel merges.  Z == 1 (large batches) lets the kernel
+    write its output directly."""
     pairs = max(1, batch * num_kv_heads)
-    if decode_uses_wide(batch, num_kv_heads):
-        return 1
     if decode_uses_wave(batch, num_kv_heads):
         chunks = max(1, math.ceil(max_ctx / DECODE_CHUNK))
         want = math.ceil((target_waves or DECODE_TARGET_WAVES) / pairs)

@@ -431,7 +431,7 @@ def _tune_rs(ws, x, M: int, N: int, K: int, reps: int, kind: str) -> None:
             def fn(cfg=cfg, out=out):
                 for w in ws:
                     skinny_rscale(x, w, cfg, ssp, 256, 1e-6, out, silu=kind == "rss")
-        t = _time(fn, reps)
+        t = _time_graphed(fn, reps)
         if t < best_t:
             best_t, best = t, cfg
     if best is not None:
@@ -496,7 +496,9 @@ def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: floa
             def lib():
                 for w in ws:
                     F.linear(x, w)
-            lib_t = _time(lib, reps)
+            # graph-replayed, as a decode step runs them: timed eagerly, a sweep of 8-us
+            # kernels measures the host's launch rate and ranks the configurations by it
+            lib_t = _time_graphed(lib, reps)
             sk_t, sk_cfg = float("inf"), None
             for cfg in _CONFIGS:
                 # the smallest batch tile that holds M
@@ -506,7 +508,7 @@ def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: floa
                 def sk(cfg=cfg):
                     for w in ws:
                         skinny_gemm(x, w, None, cfg, out)
-                t = _time(sk, reps)
+                t = _time_graphed(sk, reps)
                 if t < sk_t:
                     sk_t, sk_cfg = t, cfg
             best = sk_cfg if sk_t < lib_t * margin else None
@@ -729,7 +731,7 @@ def _tune_norm(ws, x, out, M: int, N: int, K: int, reps: int) -> None:
         def fn(cfg=cfg):
             for w in ws:
                 _k().skinny_gemm(out, x, w, None, *cfg, 1, gamma, 1e-6)
-        t = _time(fn, reps)
+        t = _time_graphed(fn, reps)
         if t < best_t:
             best_t, best_cfg = t, cfg
     if best_cfg is not None:

@@ -127,18 +127,7 @@ def _fill_random_cache(B, ctx_lens, nkv, bs, d, dt, dev, nb_extra=7):
 
 # decode kernel per launch: K1w (one wave per z-slice) from DECODE_WAVE_MIN_PAIRS (seq, kv-head)
 # pairs up, the 4-wave kernel below; the threshold override runs both on every shape
-# decode kernel per test run (env of the C++ launcher): K1w, the 4-wave workgroup, and the
-# 16-wave workgroup (every z = 1 grid; it merges the whole context in LDS)
-_DECODE_KERNELS = {"wave": {"KGC_DECODE_WAVE_MIN_PAIRS": "1", "KGC_DECODE_WIDE_MAX_PAIRS": "0"},
-                   "four": {"KGC_DECODE_WAVE_MIN_PAIRS": "1000000000",
-                            "KGC_DECODE_WIDE_MAX_PAIRS": "0"},
-                   "wide": {"KGC_DECODE_WAVE_MIN_PAIRS": "1000000000",
-                            "KGC_DECODE_WIDE_MAX_PAIRS": "1000000000"}}
-
-
-def _set_decode_kernel(monkeypatch, kern):
-    for k, v in _DECODE_KERNELS[kern].items():
-        monkeypatch.setenv(k, v)
+_DECODE_KERNELS = {"wave": "1", "four": "1000000000"}
 
 
 @pytest.mark.parametrize("dt", DT)
@@ -150,7 +139,7 @@ def test_paged_decode(gpu, monkeypatch, kern, dt, d, nq, nkv, bs):
     """K1 vs the fp32 reference at ragged lengths (1 token .. 2049), GQA 1/4/7/8 and MHA,
     z = 1, 3 and 40 (K1w: most slices of the short rows empty, the reduce merges only the
     used ones)."""
-    _set_decode_kernel(monkeypatch, kern)
+    monkeypatch.setenv("KGC_DECODE_WAVE_MIN_PAIRS", _DECODE_KERNELS[kern])
     torch.manual_seed(3)
     ctx = [1, 17, 128, 129, 300, 1000, 2049, 64]
     B = len(ctx)
@@ -174,7 +163,7 @@ def test_paged_decode_rope(gpu, monkeypatch, kern, dt, d, nq, nkv, qk_norm, S, f
     """The decode kernel with rope_kv_write folded in == rope_kv_write + paged_decode on
     the same inputs (q / k / v and the cache update), and == the fp32 reference.  One row
     is graph padding (ctx 0, slot -1): nothing of it reaches the cache."""
-    _set_decode_kernel(monkeypatch, kern)
+    monkeypatch.setenv("KGC_DECODE_WAVE_MIN_PAIRS", _DECODE_KERNELS[kern])
     torch.manual_seed(17 + d + S)
     bs = 16
     ctx = [1, 17, 300, 1000, 0, 64, 129]
@@ -236,7 +225,7 @@ def test_paged_decode_rope(gpu, monkeypatch, kern, dt, d, nq, nkv, qk_norm, S, f
 def test_paged_decode_workspace_reuse(gpu, monkeypatch, kern):
     """One static partials workspace serves launches of any Z (incl. an empty context),
     eager or replayed from a graph."""
-    _set_decode_kernel(monkeypatch, kern)
+    monkeypatch.setenv("KGC_DECODE_WAVE_MIN_PAIRS", _DECODE_KERNELS[kern])
     torch.manual_seed(13)
     dt, d, nq, nkv, bs = torch.bfloat16, 128, 32, 8, 32
     ctx = [1, 700, 2049, 64, 0, 333]
