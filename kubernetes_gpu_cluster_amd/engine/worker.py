@@ -198,7 +198,7 @@ def _bcast_cmd(cmd: int, arg: int = 0, header: Optional[list[int]] = None) -> li
 def _bcast_plan_blobs(runner: ModelRunner, plan_hdr: list[int]) -> None:
     s = get_state()
     src = getattr(s, "global_base", 0)
-    blobs = (runner.h64, runner.h32, runner.hf)
+    blobs = (runner.hblob,)     # the step's int64 / int32 / fp32 arrays: one byte blob
     if _p2p_plans(s):
         if s.rank == 0:      # the driver rewrites its blobs for the next micro-batch
             _send_to_ranks(s, [t.clone() for t in blobs])
