@@ -1,5 +1,6 @@
 set -o pipefail
 bash tools/gpu_steps.sh \
- "full|1000|python -u -m pytest -v --timeout 300 --timeout-method thread tests -m gpu -p no:cacheprovider > gpurun_out/gpu_tests_full_r4.log 2>&1; tail -5 gpurun_out/gpu_tests_full_r4.log" \
- "smoke|300|python -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke_r4.log 2>&1; tail -3 gpurun_out/smoke_r4.log" \
- "p_b1|300|DETAIL=1 bash tools/profile.sh /tmp/pb1 -- python bench.py --mode engine --num-prompts 1 --output-len 128 --steps 1 --warmup 1 > gpurun_out/r4f3_b1.log 2>&1 && cp /tmp/pb1/summary.txt gpurun_out/r4f3_b1_summary.txt"
+ "full|600|python -u -m pytest -v --timeout 300 --timeout-method thread tests -m gpu -p no:cacheprovider > gpurun_out/gpu_tests_full_r4.log 2>&1; tail -5 gpurun_out/gpu_tests_full_r4.log" \
+ "smoke|200|python -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke_r4.log 2>&1; tail -3 gpurun_out/smoke_r4.log" \
+ "bench|500|python bench.py > gpurun_out/bench_r4f.json 2> gpurun_out/bench_r4f.err" \
+ "p_b1|200|DETAIL=1 bash tools/profile.sh /tmp/pb1 -- python bench.py --mode engine --num-prompts 1 --output-len 128 --steps 1 --warmup 1 > gpurun_out/r4f3_b1.log 2>&1 && cp /tmp/pb1/summary.txt gpurun_out/r4f3_b1_summary.txt"
