@@ -370,6 +370,17 @@ def fused_norm_plan(M: int, norm_shapes, acc_shapes):
     return [c for c, _ in norm], acc
 
 
+def norm_fused_cfg(M: int, N: int, K: int):
+    """The SK_NORM configuration of a GEMM that can absorb its input RMSNorm at this M,
+    where tuning measured it cheaper than the plain GEMM plus the norm launch; else None."""
+    try:
+        cfg, t = _plan_norm[(M, N, K)]
+        plain = _chosen_us[(M, N, K)] + _rms_us[(M, K)]
+    except KeyError:
+        return None
+    return cfg if t < 0.98 * plain else None
+
+
 def clear_plan() -> None:
     _best_sk.clear()
     _best_silu.clear()

@@ -113,6 +113,11 @@ def test_gpu_logits_match_hf_norm_free_small_m(gpu, name):
             gemm._best_silu[(M, ng, kg)] = (1, 2, 4, False)
             gemm._best_sk[(M, nd, kd)] = (1, 1, 8, False)
             assert model._rs_cfgs(M) is not None
+            if M != 13:   # layer 0's input norm inside its qkv GEMM (SK_NORM) at M = 7 / 1
+                gemm._plan_norm[(M, nq, kq)] = ((1, 2, 4, False), 1.0)
+                gemm._chosen_us[(M, nq, kq)] = 10.0
+                gemm._rms_us[(M, kq)] = 5.0
+                assert gemm.norm_fused_cfg(M, nq, kq) == (1, 2, 4, False)
         g = torch.Generator().manual_seed(1)
         prompt = torch.randint(3, cfg.vocab_size, (20,), generator=g).tolist()
         extra = torch.randint(3, cfg.vocab_size, (4,), generator=g).tolist()
