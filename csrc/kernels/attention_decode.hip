@@ -775,14 +775,18 @@ template <typename T, int D, bool WAVE>
 __global__ __launch_bounds__(64) void paged_decode_reduce_kernel(
     T* __restrict__ out, const float* __restrict__ max_logits,
     const float* __restrict__ exp_sums, const float* __restrict__ tmp_out,
-    const int* __restrict__ ctx_lens, int nq, int Zg, int Zmax) {
+    const int* __restrict__ ctx_lens, int nq, int Zg, int Zmax, int ctx_cap) {
   // The slice statistics are read in parallel (lane z), the weights staged in LDS,
   // and the partial rows loaded 8 slices at a time: the previous per-slice loop was a
   // chain of dependent L2 round trips (~7 us per call at B = 1; decode + reduce for
   // B = 1, ctx 565, Z = 16 went 13.0 -> 9.3 us).
   __shared__ float wz[DEC_MAX_Z];
   const int b = blockIdx.x, hq = blockIdx.y, tid = threadIdx.x;
-  const int Z = WAVE ? decode_used_slices((max(ctx_lens[b], 0) + 31) >> 5, Zg) : Zg;
+  // the context the decode kernel covered: clamped to the block table's capacity exactly
+  // as it clamps it (ctx_cap = bt_stride << bs_log2), so a ctx_len past the table never
+  // makes this merge read slices that kernel did not write this step
+  const int ctx = min(max(ctx_lens[b], 0), ctx_cap);
+  const int Z = WAVE ? decode_used_slices((ctx + 31) >> 5, Zg) : Zg;
   T* orow = out + ((int64_t)b * nq + hq) * D;
   constexpr int EPT = D / 64;
   const int64_t base = ((int64_t)b * nq + hq) * Zmax;
@@ -793,7 +797,7 @@ __global__ __launch_bounds__(64) void paged_decode_reduce_kernel(
 #pragma unroll
   for (int e = 0; e < EPT; ++e) acc[e] = 0.f;
   float tot = 0.f;
-  if (ctx_lens[b] > 0 && m != -INFINITY) {
+  if (ctx > 0 && m != -INFINITY) {
     for (int z = tid; z < Z; z += 64) {
       const float w = exp2f(max_logits[base + z] - m);
       wz[z] = w;
@@ -864,10 +868,12 @@ static void decode_dispatch(void* out, const void* q, const void* kc, const void
   if (Z == 1) return;
   if (wave)
     paged_decode_reduce_kernel<T, D, true><<<dim3(B, nq), 64, 0, s>>>((T*)out, ml, es, tmp, ctx,
-                                                                      nq, Z, Z);
+                                                                      nq, Z, Z,
+                                                                      bt_stride << bs_log2);
   else
     paged_decode_reduce_kernel<T, D, false><<<dim3(B, nq), 64, 0, s>>>((T*)out, ml, es, tmp,
-                                                                       ctx, nq, Z, Z);
+                                                                       ctx, nq, Z, Z,
+                                                                       bt_stride << bs_log2);
 }
 
 template <bool FUSE>

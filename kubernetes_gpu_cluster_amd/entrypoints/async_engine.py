@@ -184,9 +184,13 @@ class AsyncLLMEngine:
                 if eng.has_unfinished():
                     t0 = time.monotonic()
                     outs = eng.step()
-                    self._push_step(outs)
                     self.last_step_time = time.monotonic()
+                    # logged BEFORE the outputs reach the event loop: a client that reads a
+                    # request's [DONE] and then asks /kgc/engine_stats must find it there
+                    # (pushed first, a descheduled engine thread left the last request of a
+                    # wave out of the bench's engine-side window under CPU load)
                     self.done_log.on_step(outs, self.last_step_time - t0)
+                    self._push_step(outs)
                 else:
                     self._wake.wait(0.05)
                     self._wake.clear()

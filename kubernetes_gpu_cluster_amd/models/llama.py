@@ -433,8 +433,8 @@ class LlamaForCausalLM(nn.Module):
             ws.append((qkv, gemm.fold_norm_weight(l.mlp.gate_up_proj.weight,
                                                   l.post_attention_layernorm.weight)))
         self._rs_w = ws
-        self._rs_ssp = (torch.zeros(16 * 256, dtype=torch.float32, device=dev),
-                        torch.zeros(16 * 256, dtype=torch.float32, device=dev))
+        self._rs_ssp = (torch.zeros(gemm.RS_SSP_FLOATS, dtype=torch.float32, device=dev),
+                        torch.zeros(gemm.RS_SSP_FLOATS, dtype=torch.float32, device=dev))
         return need
 
     def _rs_shapes(self):

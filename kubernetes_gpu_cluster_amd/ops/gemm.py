@@ -308,6 +308,12 @@ def fold_norm_weight(w: torch.Tensor, gamma: torch.Tensor) -> torch.Tensor:
     return (w.float() * gamma.float()[None, :]).to(w.dtype).contiguous()
 
 
+# the norm-free layer's sum-of-squares partials: a [16 * 256] fp32 buffer per producer,
+# and at most 256 partials per row for the consumer (gemm_skinny.hip ssl[16][256])
+RS_MAX_NSS = 256
+RS_SSP_FLOATS = 16 * 256
+
+
 def rs_plan(M: int, shapes) -> Optional[list]:
     """Skinny configurations of (qkv, o, gate_up, down) at this M for the norm-free layer
     (``LlamaForCausalLM._forward_rs``), or None: every projection needs a timed skinny
@@ -324,6 +330,13 @@ def rs_plan(M: int, shapes) -> Optional[list]:
         return None
     if any(cfg[0] != 1 or M > 4 * cfg[2] for cfg in c):
         return None
+    # the producers (o / down, SK_ACC_SS) leave N / (16 nt) partials per row: they must fit
+    # the [16 * 256] ssp buffer, and the consumer (SK_RSCALE, ssl[16][256] in LDS) sums at
+    # most 256 per row (kgc.skinny_gemm checks it at launch: fail here, at plan time)
+    for cfg, n in ((c[1], no), (c[3], nd)):
+        nss = n // (16 * cfg[1])
+        if nss > RS_MAX_NSS or M * nss > RS_SSP_FLOATS:
+            return None
     return c
 
 
@@ -422,14 +435,15 @@ def accnorm_plan() -> dict:
 def _tune_rs(ws, x, M: int, N: int, K: int, reps: int, kind: str) -> None:
     """Time the norm-free layer's epilogue ``kind`` on every configuration it can run
     (one m-tile, M <= 4 * NW; SiLU pairs: NT = 2) and record the fastest in _best_rs."""
-    ssp = torch.zeros(16 * 256, dtype=torch.float32, device=x.device)
+    ssp = torch.zeros(RS_SSP_FLOATS, dtype=torch.float32, device=x.device)
     best_t, best = float("inf"), None
     for cfg in _CONFIGS:
         mt, nt, nw, _ = cfg
         if mt != 1 or M > 4 * nw or not skinny_ok(M, N, K, cfg) or (kind == "rss" and nt != 2):
             continue
         if kind == "ss":
-            if M * (N // (16 * nt)) > ssp.numel():
+            # a consumer sums at most RS_MAX_NSS partials per row (rs_plan checks it again)
+            if N // (16 * nt) > RS_MAX_NSS or M * (N // (16 * nt)) > ssp.numel():
                 continue
             res = torch.zeros(M, N, dtype=x.dtype, device=x.device)
 

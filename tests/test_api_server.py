@@ -349,3 +349,41 @@ def test_unstarted_stream_aborts_request(kind):
             assert "drop-1" not in eng.engine.seqs
     finally:
         eng.shutdown()
+
+
+@pytest.mark.parametrize("kind", ["thread", "core-process"])
+def test_finished_request_is_logged_before_its_stream_ends(kind):
+    """bench.py's engine-side window reads /kgc/engine_stats right after the client's last
+    [DONE]: every request whose stream has ended must already be in the engine's done log
+    (the thread engine once pushed a step's outputs before logging them, and under CPU load
+    the last request of a wave fell out of the window)."""
+    import asyncio
+    from kubernetes_gpu_cluster_amd.engine.sequence import SamplingParams
+    cfg = _cfg()
+    if kind == "thread":
+        eng = AsyncLLMEngine(cfg)
+        # make the race deterministic: the step's outputs stall before the log would be
+        # written on the old order, so a late log is visible to the check below
+        orig = eng._push_step
+
+        def push_then_check(outs):
+            orig(outs)
+            import time as _t
+            _t.sleep(0.05)
+        eng._push_step = push_then_check
+    else:
+        from kubernetes_gpu_cluster_amd.entrypoints.engine_core import EngineCoreClient
+        eng = EngineCoreClient(cfg)
+
+    async def body():
+        for i in range(3):
+            g = eng.generate([5, 6, 7 + i], SamplingParams(max_tokens=3, ignore_eos=True),
+                             f"log-{i}")
+            outs = [o async for o in g]
+            assert outs[-1].finished
+            st = await eng.engine_stats()
+            assert sum(1 for r in st["requests"] if r[3] == 3) == i + 1, st["requests"]
+    try:
+        asyncio.run(asyncio.wait_for(body(), 60))
+    finally:
+        eng.shutdown()

@@ -61,3 +61,40 @@ def test_packed_weight_cache_drops_dead_weights():
     del w, view
     gc.collect()
     assert len(gemm._packed) == n - 1
+
+
+def test_rs_plan_rejects_producers_with_too_many_row_partials():
+    """the norm-free layer's consumer (SK_RSCALE, ssl[16][256] in LDS)
+    sums at most 256 sum-of-squares partials per row, and the producer leaves
+    N / (16 nt) of them.  At hidden 5120 (Qwen3-14B, no bias) an nt = 1 producer leaves 320
+    -- within the [16 x 256] buffer at M <= 12, but past the consumer's limit: rs_plan must
+    refuse it at plan time instead of letting the launch check fail in graph capture."""
+    M = 8
+    saved = dict(gemm._best_sk), dict(gemm._best_rs), dict(gemm._best_silu)
+    try:
+        for H, I in ((5120, 17408), (4096, 14336)):
+            shapes = [(3 * H, H), (H, H), (2 * I, H), (H, I)]
+            gemm._best_rs.clear()
+            gemm._best_sk.clear()
+            gemm._best_silu.clear()
+            # (mt, nt, nw, ntl): one m-tile, nt = 1 on the producers, nw = 4 (M <= 16)
+            gemm._best_sk[(M, 3 * H, H)] = (1, 1, 4, True)
+            gemm._best_sk[(M, H, H)] = (1, 1, 4, True)
+            gemm._best_sk[(M, H, I)] = (1, 1, 4, True)
+            gemm._best_silu[(M, 2 * I, H)] = (1, 2, 4, True)
+            p = gemm.rs_plan(M, shapes)
+            if H // 16 > gemm.RS_MAX_NSS:
+                assert p is None, (H, p)
+                # nt = 2 halves the partials: 160 per row is a valid plan again
+                gemm._best_sk[(M, H, H)] = (1, 2, 4, True)
+                gemm._best_sk[(M, H, I)] = (1, 2, 4, True)
+                assert gemm.rs_plan(M, shapes) is not None
+            else:
+                assert p is not None and H // 16 <= gemm.RS_MAX_NSS
+        # the [16 x 256] buffer also bounds M * nss: 16 rows x 256 partials fits, 17 do not
+        assert gemm.rs_plan(17, [(3 * 4096, 4096), (4096, 4096), (28672, 4096),
+                                 (4096, 14336)]) is None
+    finally:
+        for d, v in zip((gemm._best_sk, gemm._best_rs, gemm._best_silu), saved):
+            d.clear()
+            d.update(v)
