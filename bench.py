@@ -225,6 +225,9 @@ def main_engine(args):
     if rank == 0:
         value = toks / elapsed
         p50_ttft = statistics.median(ttfts) * 1e3 if ttfts else None
+        # KGC_TP_PHANTOM=N: ONE rank of a TP = N model on one GPU (parallel/state.py
+        # init_phantom) -- a per-rank measurement, never a TP = N service figure
+        phantom = int(os.environ.get("KGC_TP_PHANTOM", "0") or 0)
         out = {
             "metric": metric_name(args.model), "value": round(value, 2), "unit": "output_tokens/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -240,12 +243,17 @@ def main_engine(args):
             "config": {"model": args.model, "global_batch": args.num_prompts * replicas,
                        "seq_len": args.input_len + args.output_len, "input_len": args.input_len,
                        "output_len": args.output_len,
-                       "parallelism": f"dp{replicas}" if tp == 1 else f"tp{tp}" + (f"xdp{replicas}" if replicas > 1 else ""),
+                       "parallelism": (f"tp{phantom}-phantom-rank0" if phantom > 1 else
+                                       f"dp{replicas}" if tp == 1 else
+                                       f"tp{tp}" + (f"xdp{replicas}" if replicas > 1 else "")),
                        "max_num_seqs": args.max_num_seqs,
                        "max_num_batched_tokens": args.max_num_batched_tokens,
                        "cuda_graphs": not args.enforce_eager,
                        "scheduling": "prefill-first" if args.prefill_first else "decode-first"},
         }
+        if phantom > 1:
+            out["phantom_tp"] = phantom
+            out["data"] += "; ONE phantom TP rank (peers contribute zeros): per-rank timing only"
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:

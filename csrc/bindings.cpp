@@ -679,6 +679,14 @@ int64_t ar_open_handle(Tensor h) {
 }
 void ar_close_handle(int64_t p) { kgc::ar_close_handle((void*)(intptr_t)p); }
 int64_t ar_read_err(int64_t sig) { return (int64_t)kgc::ar_read_err((void*)(intptr_t)sig); }
+// phantom TP rank: raise the never-running peers' arrival flags in this rank's signal
+void ar_raise_peer_flags(int64_t sig, int64_t rank, int64_t nranks, int64_t value) {
+  TORCH_CHECK(sig != 0 && rank >= 0 && rank < nranks && (nranks == 2 || nranks == 4 ||
+              nranks == 8) && value > 0 && value < (int64_t(1) << 31),
+              "ar_raise_peer_flags: sig, 0 <= rank < nranks in {2, 4, 8}, 0 < value < 2^31");
+  kgc::ar_raise_peer_flags((void*)(intptr_t)sig, (int)rank, (int)nranks, (uint32_t)value,
+                           stream());
+}
 // host_out: pinned int32 [1]; valid once the current stream has passed this point
 void ar_err_copy_async(int64_t sig, Tensor host_out) {
   TORCH_CHECK(host_out.device().is_cpu() && host_out.is_pinned() &&
@@ -1106,6 +1114,8 @@ TORCH_LIBRARY(kgc, m) {
   m.def("ar_open_handle(Tensor handle) -> int", &ar_open_handle);
   m.def("ar_close_handle(int ptr) -> ()", &ar_close_handle);
   m.def("ar_read_err(int sig) -> int", &ar_read_err);
+  m.def("ar_raise_peer_flags(int sig, int rank, int nranks, int value) -> ()",
+        &ar_raise_peer_flags);
   m.def("ar_err_copy_async(int sig, Tensor(a!) host_out) -> ()", &ar_err_copy_async);
   m.def("xgmi_allreduce(Tensor(a!) inout, int[] data, int[] sig, int rank, int cap_bytes, "
         "bool two_shot) -> ()");

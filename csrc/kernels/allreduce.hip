@@ -487,6 +487,30 @@ void launch_allreduce_emu(int dtype, int kind, const ArPtrs& P, const ArWorld& W
   else ar_emu_t<f16>(kind, P, W, nranks, nvec, w, M, H, eps, cap_vec, s);
 }
 
+// ---- phantom TP rank (KGC_TP_PHANTOM, parallel/custom_allreduce.py PhantomAllReduce):
+// one process runs rank `rank`'s shard of a TP = NR model on one GPU; the NR - 1 peers are
+// local buffers that never run a kernel.  Their arrival flags in this rank's signal are
+// raised to `value` (far ahead of any epoch: the barrier's wrap-safe (flag - epoch) test
+// then passes for 2^30 calls per block), so the real kernels run their full sequence --
+// copy-in, barriers, peer reads, the fused add + norm -- inside the captured graphs.
+// Vector stores from one workgroup; a step's kernels are ordered behind it by the stream.
+__global__ __launch_bounds__(256) void ar_raise_peer_flags_kernel(ArSignal* s, int rank,
+                                                                  int nranks, uint32_t value) {
+  for (int i = threadIdx.x; i < 2 * AR_MAX_BLOCKS * AR_MAX_RANKS; i += blockDim.x) {
+    const int r = i % AR_MAX_RANKS;
+    if (r != rank && r < nranks) (&s->flag[0][0][0])[i] = value;
+  }
+  for (int i = threadIdx.x; i < 2 * AR2_BLOCKS * AR_MAX_RANKS; i += blockDim.x) {
+    const int r = i % AR_MAX_RANKS;
+    if (r != rank && r < nranks) (&s->flag2[0][0][0])[i] = value;
+  }
+}
+
+void ar_raise_peer_flags(void* sig, int rank, int nranks, uint32_t value, hipStream_t s) {
+  ar_raise_peer_flags_kernel<<<1, 256, 0, s>>>(reinterpret_cast<ArSignal*>(sig), rank, nranks,
+                                               value);
+}
+
 // ---- IPC buffer management (host) ----------------------------------------------
 static void ar_check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));

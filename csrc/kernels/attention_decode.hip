@@ -71,11 +71,13 @@ __device__ __forceinline__ void qkv_row8(const DecodeRope& rp, int64_t e, float*
     for (int j = 0; j < 8; ++j) x[j] = to_f(p.h[j]);
     return;
   }
-  // SB = 4 slices' loads in flight per round trip (clamped duplicates are not added);
+  // SB = 8 slices' loads in flight per round trip (clamped duplicates are not added: the
+  // tuner picks S <= 8, so every split is ONE round trip -- at SB = 4 the S = 5 qkv of
+  // Llama-3-8B at M = 256 took two, 132 vs 127 us per layer);
   // summed z = 0, 1, ... from 0 as rope_cache.hip does: bit-identical
   const float* src = reinterpret_cast<const float*>(rp.qkv) + e;
   f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = a;
-  constexpr int SB = 4;
+  constexpr int SB = 8;
   for (int z0 = 0; z0 < rp.S; z0 += SB) {
     f32x4 ta[SB], tb[SB];
 #pragma unroll

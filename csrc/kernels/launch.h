@@ -209,6 +209,7 @@ void ar_get_handle(void* p, uint8_t* out64);
 void* ar_open_handle(const uint8_t* in64);
 void ar_close_handle(void* p);
 uint32_t ar_read_err(void* sig);
+void ar_raise_peer_flags(void* sig, int rank, int nranks, uint32_t value, hipStream_t s);
 void ar_err_copy_async(void* sig, uint32_t* host_dst, hipStream_t s);
 
 }  // namespace kgc

@@ -32,7 +32,8 @@ from ..models import load_model, resolve_model
 from ..models.moe import set_moe_mode
 from ..parallel import comm
 from .health import RankWatchdog, watch_parent
-from ..parallel.state import destroy_parallel, get_state, init_parallel
+from ..parallel.state import (destroy_parallel, get_state, init_parallel, init_phantom,
+                              phantom_tp)
 from .config import EngineConfig
 from .model_runner import ModelRunner, StepPlan
 
@@ -59,6 +60,13 @@ class Worker:
         self.rank = rank
         set_moe_mode(cfg.moe_parallel)
         init_parallel(cfg.tensor_parallel_size, cfg.pipeline_parallel_size, device=dev)
+        ph = phantom_tp()
+        if ph > 1:
+            # KGC_TP_PHANTOM=N: this single process is rank 0 of a TP = N model (one GPU
+            # stands in for a TP node's rank: parallel/state.py init_phantom)
+            if cfg.tensor_parallel_size * cfg.pipeline_parallel_size != 1 or dev.type != "cuda":
+                raise ValueError("KGC_TP_PHANTOM needs one GPU process (tp = pp = 1)")
+            init_phantom(ph, dev)
         self.ps = get_state()
         # non-driver ranks of a multi-rank engine heart-beat into the rendezvous store
         # (engine/health.py): the driver notices a rank on another node dying, and this
@@ -79,7 +87,7 @@ class Worker:
         self.max_model_len = default_max_model_len(cfg)
         if dev.type == "cuda":
             from ..utils.gemm_tuning import enable_tuned_gemms
-            enable_tuned_gemms(mcfg.name, cfg.tensor_parallel_size)
+            enable_tuned_gemms(mcfg.name, self.ps.tp_size)
         torch.manual_seed(cfg.seed)
         self.mcfg, self.model = load_model(cfg.model, self.dtype, dev, cfg.random_init,
                                            seed=cfg.seed)
@@ -310,6 +318,7 @@ class LocalExecutor:
         return True
 
     def shutdown(self) -> None:
+        _release_custom_allreduce()          # a phantom TP rank's local peer buffers
         self.worker.runner.release()
 
 

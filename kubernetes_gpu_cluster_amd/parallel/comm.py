@@ -43,6 +43,8 @@ def tp_all_reduce(x: torch.Tensor) -> torch.Tensor:
     car = _custom_ar
     if car is not None and car.should_use(x):
         return car.all_reduce(x)
+    if s.phantom:
+        return x            # RCCL-size message of a phantom rank: no peers to sum
     if _gloo_half(x, s.tp_group):
         acc = x.float()
         dist.all_reduce(acc, group=s.tp_group)
@@ -76,7 +78,7 @@ def tp_all_reduce_async(x: torch.Tensor):
     one half's GEMMs run while the other half's all-reduce is on the links.  Always
     RCCL/gloo: the xGMI kernel would run on the compute stream and overlap nothing."""
     s = get_state()
-    if s.tp_size == 1:
+    if s.tp_size == 1 or s.phantom:
         return _Done()
     if _gloo_half(x, s.tp_group):
         acc = x.float()
@@ -99,7 +101,7 @@ def tp_all_reduce_add_rms(x: torch.Tensor, residual: torch.Tensor, w: torch.Tens
 def tp_all_reduce_max(x: torch.Tensor) -> torch.Tensor:
     """In-place MAX over the TP group (vocab-parallel sampling: 8 bytes per row)."""
     s = get_state()
-    if s.tp_size > 1:
+    if s.tp_size > 1 and not s.phantom:
         dist.all_reduce(x, op=dist.ReduceOp.MAX, group=s.tp_group)
     return x
 
@@ -112,7 +114,12 @@ def tp_all_gather(x: torch.Tensor, dim: int = -1) -> torch.Tensor:
     x = x.contiguous()
     out = torch.empty((s.tp_size * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype,
                       device=x.device)
-    dist.all_gather_into_tensor(out, x, group=s.tp_group)
+    if s.phantom:
+        # the peers' shards stand in as copies of this rank's (same bytes moved locally)
+        out.view((s.tp_size,) + tuple(x.shape)).copy_(x.unsqueeze(0).expand(
+            (s.tp_size,) + tuple(x.shape)))
+    else:
+        dist.all_gather_into_tensor(out, x, group=s.tp_group)
     if dim == 0:
         return out
     return torch.cat(out.view((s.tp_size,) + tuple(x.shape)).unbind(0), dim=dim)
@@ -128,7 +135,7 @@ def tp_gather(x: torch.Tensor, dim: int = -1) -> Optional[torch.Tensor]:
 def tp_broadcast(x: torch.Tensor, src_local: int = 0) -> torch.Tensor:
     """C6: broadcast from a TP-local rank."""
     s = get_state()
-    if s.tp_size == 1:
+    if s.tp_size == 1 or s.phantom:
         return x
     base = getattr(s, "global_base", 0) + s.pp_rank * s.tp_size
     dist.broadcast(x, src=base + src_local, group=s.tp_group)

@@ -48,17 +48,7 @@ class CustomAllReduce:
         if world not in SUPPORTED_WORLD:
             raise ValueError(f"xGMI all-reduce supports {SUPPORTED_WORLD} ranks, not {world}")
         self.rank, self.world, self.device = rank, world, device
-        # Thresholds (logged at start-up; env-tunable because the one-shot / two-shot
-        # crossover and the RCCL hand-over point depend on the node's xGMI topology and
-        # have only been measured at 2 / 4 ranks on one GPU): KGC_AR_CAP -- largest
-        # message this path takes (bytes; above it RCCL), KGC_AR_ONE_SHOT_MAX -- largest
-        # one-shot message (one-shot reads (N-1) x bytes, two-shot 2(N-1)/N x bytes but
-        # pays two barriers).
-        self.cap = int(cap_bytes if cap_bytes is not None else
-                       os.environ.get("KGC_AR_CAP", 8 << 20))
-        env_os = os.environ.get("KGC_AR_ONE_SHOT_MAX")
-        self.one_shot_max = int(one_shot_max if one_shot_max is not None else
-                                env_os if env_os else (512 << 10 if world <= 2 else 256 << 10))
+        self._thresholds(cap_bytes, one_shot_max)
         self._own, self._opened = 0, []
         self._err_host: Optional[torch.Tensor] = None
         handle, err = None, None
@@ -95,10 +85,21 @@ class CustomAllReduce:
         if not _agree(err is None, cpu_group):
             self.close()
             raise RuntimeError(f"xGMI all-reduce peer mapping failed: {err}")
-        self.sig = bases
-        self.data = [b + sig_bytes for b in bases]
-        self.fdata = [b + sig_bytes + 2 * self.cap for b in bases]
-        self.fdata2 = [b + sig_bytes + 4 * self.cap for b in bases]
+        self._set_bases(bases, sig_bytes)
+
+    def _thresholds(self, cap_bytes: Optional[int], one_shot_max: Optional[int]) -> None:
+        """Thresholds (logged at start-up; env-tunable because the one-shot / two-shot
+        crossover and the RCCL hand-over point depend on the node's xGMI topology and
+        have only been measured at 2 / 4 ranks on one GPU): KGC_AR_CAP -- largest message
+        this path takes (bytes; above it RCCL), KGC_AR_ONE_SHOT_MAX -- largest one-shot
+        message (one-shot reads (N-1) x bytes, two-shot 2(N-1)/N x bytes but pays two
+        barriers)."""
+        world = self.world
+        self.cap = int(cap_bytes if cap_bytes is not None else
+                       os.environ.get("KGC_AR_CAP", 8 << 20))
+        env_os = os.environ.get("KGC_AR_ONE_SHOT_MAX")
+        self.one_shot_max = int(one_shot_max if one_shot_max is not None else
+                                env_os if env_os else (512 << 10 if world <= 2 else 256 << 10))
         # fused all-reduce + add + RMSNorm: one-shot up to KGC_AR_RMS_MAX (default: the
         # plain one-shot limit), the row-segmented two-shot form above it up to
         # KGC_AR_RMS2_MAX.  Default: the whole buffer at 2 ranks, off from 4 ranks up --
@@ -109,9 +110,15 @@ class CustomAllReduce:
         # KGC_AR_RMS2_MAX.)
         self.fused_max = int(os.environ.get("KGC_AR_RMS_MAX", self.one_shot_max))
         self.fused2_max = int(os.environ.get("KGC_AR_RMS2_MAX", self.cap if world <= 2 else 0))
-        self.max_hidden = int(k.allreduce_rms_max_hidden())
         self.fused_calls = 0        # host-side launches (a graph capture counts once)
         self.fused2_calls = 0       # ... of them the two-shot form
+
+    def _set_bases(self, bases: list, sig_bytes: int) -> None:
+        self.sig = bases
+        self.data = [b + sig_bytes for b in bases]
+        self.fdata = [b + sig_bytes + 2 * self.cap for b in bases]
+        self.fdata2 = [b + sig_bytes + 4 * self.cap for b in bases]
+        self.max_hidden = int(torch.ops.kgc.allreduce_rms_max_hidden())
 
     def should_use(self, x: torch.Tensor) -> bool:
         if not x.is_cuda or x.dtype not in (torch.bfloat16, torch.float16):
@@ -180,11 +187,59 @@ class CustomAllReduce:
             self._opened = []
 
 
+class PhantomAllReduce(CustomAllReduce):
+    """The xGMI all-reduce of rank ``rank`` of a TP = ``world`` group whose peers do not
+    exist (KGC_TP_PHANTOM, parallel/state.py init_phantom): this rank's buffer and ``world
+    - 1`` peer buffers are all local allocations, and the peers' arrival flags in this
+    rank's signal are raised far ahead of any epoch (kgc.ar_raise_peer_flags), so every
+    kernel form -- one-shot, two-shot, fused one- / two-shot add + RMSNorm -- runs its
+    full copy-in / barrier / peer-read / reduce sequence, captured in the decode graphs,
+    without waiting.  The peers' data regions hold zeros: the sums are this rank's
+    partials only.  Peer reads come from local HBM, not over xGMI links, so the kernels'
+    TIMES are not a TP node's; what the phantom measures is every other kernel of the
+    rank's step at its real per-rank shapes, and the graph / epoch machinery."""
+
+    # far ahead of any epoch, within the barrier's wrap-safe int32 window (2^30 calls per
+    # block: ~18 h of 70B TP = 8 decode at 100 steps / s)
+    FLAG_VALUE = 1 << 30
+
+    def __init__(self, rank: int, world: int, device: torch.device,
+                 cap_bytes: Optional[int] = None, one_shot_max: Optional[int] = None):
+        if world not in SUPPORTED_WORLD:
+            raise ValueError(f"xGMI all-reduce supports {SUPPORTED_WORLD} ranks, not {world}")
+        from .. import ops
+        ops.load_extension(strict=True)
+        k = torch.ops.kgc
+        self.rank, self.world, self.device = rank, world, device
+        self._thresholds(cap_bytes, one_shot_max)
+        self._err_host = None
+        with torch.cuda.device(device):
+            sig_bytes = int(k.ar_signal_bytes())
+            bases = [int(k.ar_alloc(sig_bytes + 6 * self.cap)) for _ in range(world)]
+            k.ar_raise_peer_flags(bases[rank], rank, world, self.FLAG_VALUE)
+            torch.cuda.synchronize(device)
+        self._own, self._opened = bases[rank], []
+        self._peers = [b for r, b in enumerate(bases) if r != rank]
+        self._set_bases(bases, sig_bytes)
+
+    def close(self) -> None:
+        if self._own:
+            torch.cuda.synchronize(self.device)
+            for p in self._peers + [self._own]:
+                torch.ops.kgc.ar_free(p)
+            self._own, self._peers = 0, []
+
+
 def maybe_init_custom_allreduce(ps, device: torch.device) -> Optional[CustomAllReduce]:
     """Build the xGMI all-reduce for this rank's TP group, or None (RCCL only).
     All TP ranks agree: if any rank cannot set it up, none uses it."""
     if os.environ.get("KGC_CUSTOM_AR", "1") == "0" or ps.tp_size not in SUPPORTED_WORLD:
         return None
+    if getattr(ps, "phantom", False):
+        car = PhantomAllReduce(ps.tp_rank, ps.tp_size, device)
+        log.info("phantom TP rank %d of %d: xGMI all-reduce against local peer buffers",
+                 ps.tp_rank, ps.tp_size)
+        return car
     try:
         car = CustomAllReduce(ps.tp_cpu_group, ps.tp_rank, ps.tp_size, device)
     except RuntimeError as e:

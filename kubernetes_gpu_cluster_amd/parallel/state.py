@@ -35,6 +35,9 @@ class ParallelState:
     tp_cpu_group: Optional[object] = None
     backend: str = "none"
     device: torch.device = dataclasses.field(default_factory=lambda: torch.device("cpu"))
+    # phantom TP rank (KGC_TP_PHANTOM=N, init_phantom): ONE process holds rank 0's shard
+    # of a TP = N model; there are no peer processes and no process groups
+    phantom: bool = False
 
     @property
     def is_first_pp(self) -> bool:
@@ -125,6 +128,28 @@ def init_parallel(tp: int = 1, pp: int = 1, backend: Optional[str] = None,
     s.global_base = base  # type: ignore[attr-defined]
     set_state(s)
     return s
+
+
+def init_phantom(tp: int, device: torch.device) -> ParallelState:
+    """Rank 0 of a TP = ``tp`` model as a single process on one GPU (KGC_TP_PHANTOM=tp):
+    every layer holds rank 0's shard (70B at TP = 8: nq 8, nkv 1, I / 8, vocab / 8), the
+    row-parallel sums run the real xGMI kernels against peer buffers that never arrive
+    with data (parallel/custom_allreduce.py PhantomAllReduce), and the other collectives
+    are local stand-ins of the same shapes (parallel/comm.py).  It exercises -- and lets
+    rocprof time -- one rank's decode step with its real kernel sequence inside the
+    captured graphs, on a box with one GPU.  Outputs are not a TP = tp model's outputs
+    (the peers contribute zeros): a measurement and capture harness, never a server."""
+    assert tp in (2, 4, 8), f"phantom TP size {tp} not in (2, 4, 8)"
+    s = ParallelState(world_size=1, rank=0, tp_size=tp, tp_rank=0, pp_size=1, pp_rank=0,
+                      backend="phantom", device=device, phantom=True)
+    set_state(s)
+    return s
+
+
+def phantom_tp() -> int:
+    """KGC_TP_PHANTOM as an int (0: off)."""
+    v = os.environ.get("KGC_TP_PHANTOM", "0") or "0"
+    return int(v)
 
 
 def destroy_parallel() -> None:

@@ -322,3 +322,65 @@ def test_comm_probe_two_ranks_on_one_gpu(gpu, tmp_path):
     assert len(res["rccl"]) == 4 and all(r["us"] > 0 for r in res["rccl"])
     assert len(res["xgmi"]) == 6 and all(r["correct"] for r in res["xgmi"])
     assert len(res["crossover"]["best_per_size"]) == 6
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_phantom_rank_runs_every_form_without_waiting(world, gpu):
+    """KGC_TP_PHANTOM's all-reduce (parallel/custom_allreduce.py PhantomAllReduce): rank 0
+    of a TP = ``world`` group whose peers never run.  Their arrival flags are raised
+    ahead of every epoch, so each kernel form completes its whole sequence without a
+    time-out, and with zero peer data its outputs have an exact structure:
+      one-shot: x (this rank's input + zeros);
+      two-shot: x on this rank's owned segment, zeros on the peers' (their reduced
+                segments are read from their buffers);
+      fused one- / two-shot add + RMSNorm: residual + (x on the rows this rank reduces).
+    Run twice per form (both data parities) and inside a captured graph."""
+    from kubernetes_gpu_cluster_amd import ops
+    from kubernetes_gpu_cluster_amd.parallel.custom_allreduce import PhantomAllReduce
+    dev = torch.device("cuda", 0)
+    car = PhantomAllReduce(0, world, dev, cap_bytes=4 << 20, one_shot_max=256 << 10)
+    car.fused_max, car.fused2_max = 256 << 10, 4 << 20
+    try:
+        g = torch.Generator().manual_seed(3)
+        for rep in range(2):
+            small = torch.randint(-8, 9, (64, 512), generator=g).to(torch.bfloat16).to(dev)
+            y = small.clone()
+            car.all_reduce(y)
+            assert torch.equal(y, small)
+            big = torch.randint(-8, 9, (256, 4096), generator=g).to(torch.bfloat16).to(dev)
+            y = big.clone()
+            car.all_reduce(y)                      # 2 MB > one-shot max: two-shot
+            flat, seg = big.view(-1), big.numel() // world
+            exp = torch.zeros_like(flat)
+            exp[:seg] = flat[:seg]
+            assert torch.equal(y.view(-1), exp)
+            for rows in (16, 256):                 # 128 KB fused one-shot, 2 MB two-shot
+                x = torch.randint(-8, 9, (rows, 4096), generator=g).to(torch.bfloat16).to(dev)
+                res = torch.randint(-8, 9, (rows, 4096), generator=g).to(torch.bfloat16).to(dev)
+                w = torch.ones(4096, dtype=torch.bfloat16, device=dev)
+                r2 = res.clone()
+                out, r2 = car.all_reduce_add_rms(x, r2, w, 1e-6)
+                h = x.clone()
+                if rows * 4096 * 2 > car.fused_max:
+                    # row-segmented: this rank reduces the rows it owns, (row + row / 128) % NR
+                    own = torch.tensor([(r + r // 128) % world == 0 for r in range(rows)],
+                                       device=dev)
+                    h[~own] = 0
+                ref_res = (res.float() + h.float()).to(torch.bfloat16)
+                assert torch.equal(r2, ref_res)
+                ref_out = ops.reference.rms_norm(ref_res.float(), w.float(), 1e-6)
+                torch.testing.assert_close(out.float(), ref_out, atol=2e-2, rtol=2e-2)
+        # the same kernels captured and replayed (epochs come from device memory)
+        x = torch.randint(-8, 9, (64, 512), generator=g).to(torch.bfloat16).to(dev)
+        y = x.clone()
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            y.copy_(x)
+            car.all_reduce(y)
+        for _ in range(3):
+            gr.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(y, x)
+        car.check()                                # no barrier ever timed out
+    finally:
+        car.close()

@@ -393,3 +393,39 @@ def test_pp2_rejects_logprobs():
         assert len(outs[0].output_token_ids) == 3
     finally:
         llm.shutdown()
+
+
+def test_phantom_tp_rank_shards_and_local_collectives():
+    """KGC_TP_PHANTOM (parallel/state.py init_phantom): one process holds rank 0's shard of
+    a TP = 8 model -- the per-rank shapes of Llama-3-70B at TP = 8 (qkv N 1280, o K 1024,
+    gate_up N 7168, down K 3584, vocab / 8) -- and the non-all-reduce collectives are local
+    stand-ins of the same shapes: all-gather replicates the shard, broadcast and MAX are
+    identities, the async all-reduce is a no-op handle."""
+    from kubernetes_gpu_cluster_amd.models import build_model
+    from kubernetes_gpu_cluster_amd.parallel import comm
+    from kubernetes_gpu_cluster_amd.parallel.state import (ParallelState, get_state,
+                                                           init_phantom, set_state)
+    cfg = PRESETS["llama-3-70b"].shrink(name="llama-3-70b-1l", num_layers=1)
+    try:
+        s = init_phantom(8, torch.device("cpu"))
+        assert s.phantom and s.tp_size == 8 and s.tp_rank == 0 and get_state() is s
+        with torch.device("meta"):
+            m = build_model(cfg, torch.bfloat16, torch.device("meta"))
+        l0 = m.layers[0]
+        assert tuple(l0.self_attn.qkv_proj.weight.shape) == (1280, 8192)
+        assert tuple(l0.self_attn.o_proj.weight.shape) == (8192, 1024)
+        assert tuple(l0.mlp.gate_up_proj.weight.shape) == (7168, 8192)
+        assert tuple(l0.mlp.down_proj.weight.shape) == (8192, 3584)
+        assert l0.self_attn.nq == 8 and l0.self_attn.nkv == 1
+        # vocab / 8 per rank, padded to the layer's row granule
+        assert 128256 // 8 <= m.lm_head.per < 128256 // 8 + 64
+        x = torch.arange(12, dtype=torch.float32).view(3, 4)
+        g = comm.tp_all_gather(x, -1)
+        assert g.shape == (3, 32) and torch.equal(g[:, 4:8], x) and torch.equal(g[:, 28:], x)
+        assert torch.equal(comm.tp_all_gather(x, 0), x.repeat(8, 1))
+        y = x.clone()
+        assert comm.tp_broadcast(y) is y and comm.tp_all_reduce_max(y) is y
+        comm.tp_all_reduce_async(y).wait()
+        assert torch.equal(comm.tp_all_reduce(y), x)     # no xGMI object: no peers to sum
+    finally:
+        set_state(ParallelState())

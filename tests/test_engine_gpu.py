@@ -638,3 +638,53 @@ def test_two_node_engine_on_one_gpu(gpu, tmp_path, tp, pp):
     same = sum(a == b for x, y in zip(ref, got) for a, b in zip(x, y))
     assert all(x[0] == y[0] for x, y in zip(ref, got)), (ref, got)
     assert same >= 0.8 * sum(len(x) for x in ref), (ref, got)
+
+
+def test_phantom_tp8_rank_of_70b_captures_and_replays(gpu, monkeypatch):
+    """KGC_TP_PHANTOM=8: one process runs rank 0 of Llama-3-70B at TP = 8 (2 of its layers)
+    -- BASELINE config 3's per-rank decode step on one GPU.  The decode steps replay from
+    hipGraphs with the xGMI all-reduce (plain for the embedding, fused add + RMSNorm for
+    o / down) INSIDE the graphs; the peers never run, their flags are pre-raised, and no
+    barrier times out.  Every non-all-reduce kernel sees the TP = 1 model's shard shapes:
+    qkv N = 1280, o K = 1024, gate_up N = 7168, down K = 3584, vocab / 8, one kv head."""
+    from kubernetes_gpu_cluster_amd.parallel import comm
+    from kubernetes_gpu_cluster_amd.parallel.custom_allreduce import PhantomAllReduce
+    from kubernetes_gpu_cluster_amd.parallel.state import get_state
+    PRESETS.setdefault("llama-3-70b-2l", PRESETS["llama-3-70b"].shrink(name="llama-3-70b-2l",
+                                                                       num_layers=2))
+    monkeypatch.setenv("KGC_TP_PHANTOM", "8")
+    eng = LLMEngine(EngineConfig(model="llama-3-70b-2l", random_init=True, max_model_len=1024,
+                                 max_num_seqs=16, max_num_batched_tokens=2048,
+                                 num_gpu_blocks_override=256, cuda_graph_max_bs=16))
+    try:
+        s = get_state()
+        assert s.phantom and s.tp_size == 8 and s.tp_rank == 0
+        m = eng.executor.runner.model
+        l0 = m.layers[0]
+        full = PRESETS["llama-3-70b"]
+        assert tuple(l0.self_attn.qkv_proj.weight.shape) == (
+            (full.num_heads + 2 * full.num_kv_heads) // 8 * full.head_dim, full.hidden_size)
+        assert tuple(l0.self_attn.o_proj.weight.shape) == (full.hidden_size,
+                                                           full.num_heads // 8 * full.head_dim)
+        assert tuple(l0.mlp.gate_up_proj.weight.shape) == (2 * full.intermediate_size // 8,
+                                                           full.hidden_size)
+        assert tuple(l0.mlp.down_proj.weight.shape) == (full.hidden_size,
+                                                        full.intermediate_size // 8)
+        assert m.local_kv_heads() == 1
+        car = comm.get_custom_allreduce()
+        assert isinstance(car, PhantomAllReduce) and car.world == 8
+        g = torch.Generator().manual_seed(4)
+        prompts = [torch.randint(100, 128000, (n,), generator=g).tolist() for n in (5, 90, 300)]
+        params = [SamplingParams(temperature=1.0, seed=i, max_tokens=12, ignore_eos=True)
+                  for i in range(len(prompts))]
+        outs = _run(eng, prompts, params)
+        assert all(len(o) == 12 for o in outs)
+        st = eng.executor.runner.stats
+        assert st["graph_steps"] > 0, st
+        assert car.fused_calls > 0, "fused all-reduce + add + RMSNorm never ran"
+        car.check()
+    finally:
+        eng.shutdown()
+        from kubernetes_gpu_cluster_amd.engine.worker import _release_custom_allreduce
+        _release_custom_allreduce()
+        set_state(ParallelState())
