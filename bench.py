@@ -208,6 +208,10 @@ def main_engine(args):
     if tp == 1:
         barrier()
     elapsed = time.monotonic() - t0
+    from kubernetes_gpu_cluster_amd.parallel import comm
+    # the all-reduce policy this node's start-up calibration chose (read before shutdown
+    # releases the xGMI buffers)
+    ar_cal = getattr(comm.get_custom_allreduce(), "calibration", None)
     if is_driver:
         engine.shutdown()
     # aggregate over replicas (drivers) -- every rank participates in the collectives
@@ -251,6 +255,8 @@ def main_engine(args):
                        "cuda_graphs": not args.enforce_eager,
                        "scheduling": "prefill-first" if args.prefill_first else "decode-first"},
         }
+        if tp > 1:
+            out["ar_calibration"] = ar_cal
         if phantom > 1:
             out["phantom_tp"] = phantom
             out["data"] += "; ONE phantom TP rank (peers contribute zeros): per-rank timing only"

@@ -632,7 +632,7 @@ void splitk_reduce(Tensor out, Tensor Cs) {
                             out.numel(), Cs.stride(0), stream());
 }
 
-void splitk_reduce_silu(Tensor out, Tensor Cs) {
+void splitk_reduce_silu(Tensor out, Tensor Cs, bool interleaved) {
   check_gpu(Cs, "Cs");
   c10::hip::HIPGuardMasqueradingAsCUDA g(Cs.device());
   TORCH_CHECK(Cs.scalar_type() == at::kFloat && Cs.dim() == 3 && Cs.is_contiguous(), "Cs fp32 [S, M, 2I]");
@@ -642,8 +642,9 @@ void splitk_reduce_silu(Tensor out, Tensor Cs) {
               "out [M, I] contiguous");
   TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kHalf, "bf16 / fp16");
   if (M == 0) return;
+  TORCH_CHECK(!interleaved || I % 64 == 0, "interleaved (packed SiLU tiles): I % 64 == 0");
   kgc::launch_splitk_reduce_silu(dt_code(out), out.data_ptr(), Cs.data_ptr<float>(), (int)Cs.size(0),
-                                 (int)M, (int)I, Cs.stride(0), stream());
+                                 (int)M, (int)I, Cs.stride(0), interleaved, stream());
 }
 
 void splitk_add_rms_norm(Tensor out, Tensor Cs, Tensor residual, Tensor w, double eps) {
@@ -1058,6 +1059,7 @@ std::vector<int64_t> sample_stamps() {
 }
 
 int64_t decode_wave_min_pairs() { return kgc::paged_decode_wave_min_pairs(); }
+int64_t decode_deep_max_waves() { return kgc::paged_decode_deep_max_waves(); }
 int64_t prefill_block_m() { return kgc::prefill_block_m(); }
 
 }  // namespace
@@ -1092,6 +1094,7 @@ TORCH_LIBRARY(kgc, m) {
         "int vocab_off) -> ()");
   m.def("sample_vp_unpack(Tensor(a!) out, Tensor packed) -> ()");
   m.def("decode_wave_min_pairs() -> int", &decode_wave_min_pairs);
+  m.def("decode_deep_max_waves() -> int", &decode_deep_max_waves);
   m.def("moe_route(Tensor(a!) topk_w, Tensor(b!) topk_ids, Tensor logits, bool renorm) -> ()");
   m.def("moe_align(Tensor(a!) sorted_ids, Tensor(b!) block_expert, Tensor(c!) meta, "
         "Tensor topk_ids, int e0, int E_local, int bm) -> ()");
@@ -1105,7 +1108,7 @@ TORCH_LIBRARY(kgc, m) {
   m.def("dgemm_num_cfgs() -> int", &dgemm_num_cfgs);
   m.def("dgemm_ablate(Tensor(a!) C, Tensor X, Tensor W, int mode) -> ()");
   m.def("dgemm_pack(Tensor(a!) P, Tensor W, bool silu) -> ()");
-  m.def("splitk_reduce_silu(Tensor(a!) out, Tensor Cs) -> ()");
+  m.def("splitk_reduce_silu(Tensor(a!) out, Tensor Cs, bool interleaved=False) -> ()");
   m.def("splitk_add_rms_norm(Tensor(a!) out, Tensor Cs, Tensor(b!) residual, Tensor w, float eps) -> ()");
   m.def("ar_signal_bytes() -> int", &ar_signal_bytes);
   m.def("ar_alloc(int bytes) -> int", &ar_alloc);

@@ -44,6 +44,8 @@ constexpr int DEC_MAX_Z = 1024;  // z-slices the reduce kernel merges (host-chec
 // K1w runs where the grid has at least this many (seq, kv-head) pairs; smaller batches
 // take the 4-wave kernel (B = 1: 9.3 vs 12.3 us at ctx 640; ops/__init__.py mirrors it)
 constexpr int DEC_WAVE_MIN_PAIRS = 64;
+// ... and grids of at most this many waves use its four-deep pipeline
+constexpr int DEC_DEEP_MAX_WAVES = 1024;
 
 // K1w: 32-token chunks per z-slice (>= 2, the pipeline depth); slices past the context are
 // empty and the reduce stops at decode_used_slices
@@ -465,8 +467,12 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
 // vector load the chunk pipeline would have to wait behind.
 // Z > 1: slice z writes (max, sum, O) partials at row-major slot row * Z + z (the reduce
 // kernel runs with Zmax = Z).
-template <typename T, int D, bool KV8, bool FUSE>
-__global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
+// DEEP: the chunk pipeline four deep instead of two (four named buffers, 64 more VGPRs
+// than fit two waves per SIMD): for grids of few waves per CU -- e.g. the 70B TP = 8 rank
+// at batch 256, 256 (seq, kv-head) pairs -- where two chunks in flight per wave cannot
+// keep a CU's HBM queue full.
+template <typename T, int D, bool KV8, bool FUSE, bool DEEP = false>
+__global__ __launch_bounds__(64, DEEP ? 1 : 2) void paged_decode_wave_kernel(
     T* __restrict__ out, const T* __restrict__ q, const void* __restrict__ kc_,
     const void* __restrict__ vc_, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ ctx_lens, float* __restrict__ max_logits,
@@ -729,11 +735,29 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
   // issue and its use makes the compiler's wait-count pass merge the paths and wait for
   // the younger buffer too (measured in the .s: vmcnt(15) instead of (31) before the
   // first MFMA, i.e. the pipeline serialised).
-  for (int ci = c0; ci < c1; ci += 2) {
-    issue(fb, min(ci + 1, c1 - 1));
-    compute(fa, ci);
-    issue(fa, min(ci + 2, c1 - 1));
-    compute(fb, ci + 1);
+  if constexpr (DEEP) {
+    // four deep: three chunks in flight while one computes (the same straight-line,
+    // clamped-issue / masked-compute form as the two-deep loop)
+    Frag fc, fd;
+    issue(fb, min(c0 + 1, c1 - 1));
+    issue(fc, min(c0 + 2, c1 - 1));
+    for (int ci = c0; ci < c1; ci += 4) {
+      issue(fd, min(ci + 3, c1 - 1));
+      compute(fa, ci);
+      issue(fa, min(ci + 4, c1 - 1));
+      compute(fb, ci + 1);
+      issue(fb, min(ci + 5, c1 - 1));
+      compute(fc, ci + 2);
+      issue(fc, min(ci + 6, c1 - 1));
+      compute(fd, ci + 3);
+    }
+  } else {
+    for (int ci = c0; ci < c1; ci += 2) {
+      issue(fb, min(ci + 1, c1 - 1));
+      compute(fa, ci);
+      issue(fa, min(ci + 2, c1 - 1));
+      compute(fb, ci + 1);
+    }
   }
 
   l_run += __shfl_xor(l_run, 16, 64);
@@ -851,6 +875,15 @@ bool decode_use_wave(int B, int nkv) {
   return decode_wave_enabled() && (int64_t)B * nkv >= decode_wave_min_pairs();
 }
 
+// K1w grids of at most this many waves run the four-deep pipeline (DEEP): below it a CU
+// holds too few waves to keep its HBM queue full two chunks at a time
+// (KGC_DECODE_DEEP_MAX_WAVES overrides; 0 turns it off; ops/__init__.py mirrors it)
+static int decode_deep_max_waves() {
+  const char* e = getenv("KGC_DECODE_DEEP_MAX_WAVES");
+  return e ? atoi(e) : DEC_DEEP_MAX_WAVES;
+}
+int paged_decode_deep_max_waves() { return decode_deep_max_waves(); }
+
 template <typename T, int D, bool KV8, bool FUSE>
 static void decode_dispatch(void* out, const void* q, const void* kc, const void* vc,
                             const int* bt, int bt_stride, const int* ctx, float* ml, float* es,
@@ -858,7 +891,11 @@ static void decode_dispatch(void* out, const void* q, const void* kc, const void
                             float scale_log2, float v_scale, int num_blocks,
                             const DecodeRope& rp, hipStream_t s) {
   const bool wave = decode_use_wave(B, nkv);
-  if (wave) {
+  if (wave && (int64_t)B * nkv * Z <= decode_deep_max_waves()) {
+    paged_decode_wave_kernel<T, D, KV8, FUSE, true><<<dim3(B, nkv, Z), 64, 0, s>>>(
+        (T*)out, (const T*)q, kc, vc, bt, bt_stride, ctx, ml, es, tmp, nq, nkv, bs_log2,
+        scale_log2, v_scale, num_blocks, rp);
+  } else if (wave) {
     paged_decode_wave_kernel<T, D, KV8, FUSE><<<dim3(B, nkv, Z), 64, 0, s>>>(
         (T*)out, (const T*)q, kc, vc, bt, bt_stride, ctx, ml, es, tmp, nq, nkv, bs_log2,
         scale_log2, v_scale, num_blocks, rp);

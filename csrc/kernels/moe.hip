@@ -281,7 +281,12 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(T* __restrict__ out,
 // g = sum_z Cs[z, m, i], u = sum_z Cs[z, m, I + i].  The [M, 2I] bf16 gate_up output
 // is never written, and the separate silu_mul launch disappears from the decode step.
 // grid (ceil(I/8/256), M): one 8-wide column group per thread, no index division.
-template <typename T, int SK>
+// IL: the slices come from K9m's PACKED SiLU weights (gemm_decode.hip weight_row, EPI_SILU
+// layout): in each 128-column tile, 16-column groups alternate gate / up, so output column
+// c's gate is partial column (c / 64) * 128 + ((c % 64) / 16) * 32 + c % 16 and its up the
+// 16 after it (the split-K form of the packed gate_up, used where S = 1 leaves most CUs
+// idle: Llama-3-70B at TP = 8 has 56 column tiles at M = 256).
+template <typename T, int SK, bool IL = false>
 __global__ __launch_bounds__(256) void splitk_reduce_silu_kernel(T* __restrict__ out,
                                                                  const float* __restrict__ Cs,
                                                                  int S_, int I,
@@ -290,15 +295,17 @@ __global__ __launch_bounds__(256) void splitk_reduce_silu_kernel(T* __restrict__
   const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
   if (c >= I) return;
   const int64_t m = blockIdx.y;
-  const float* row = Cs + m * 2 * I + c;
+  const int64_t gcol = IL ? (int64_t)(c >> 6) * 128 + ((c & 63) >> 4) * 32 + (c & 15) : c;
+  const int64_t ucol = IL ? gcol + 16 : (int64_t)c + I;
+  const float* row = Cs + m * 2 * I;
   f32x4 g0 = f32x4{0.f, 0.f, 0.f, 0.f}, g1 = g0, u0 = g0, u1 = g0;
 #pragma unroll
   for (int z = 0; z < S; ++z) {
     const float* src = row + z * slice_stride;
-    g0 += *reinterpret_cast<const f32x4*>(src);
-    g1 += *reinterpret_cast<const f32x4*>(src + 4);
-    u0 += *reinterpret_cast<const f32x4*>(src + I);
-    u1 += *reinterpret_cast<const f32x4*>(src + I + 4);
+    g0 += *reinterpret_cast<const f32x4*>(src + gcol);
+    g1 += *reinterpret_cast<const f32x4*>(src + gcol + 4);
+    u0 += *reinterpret_cast<const f32x4*>(src + ucol);
+    u1 += *reinterpret_cast<const f32x4*>(src + ucol + 4);
   }
   Pack8<T> o;
 #pragma unroll
@@ -458,28 +465,39 @@ void launch_splitk_reduce(int dtype, void* out, const float* Cs, int S, int64_t 
   else splitk_reduce_t<f16>((f16*)out, Cs, S, n8, slice_stride, s);
 }
 
-template <typename T>
+template <typename T, bool IL>
 static void splitk_reduce_silu_t(T* out, const float* Cs, int S, int n, int I, int64_t ss,
                                  hipStream_t s) {
   const dim3 grid((unsigned)((I / 8 + 255) / 256), (unsigned)n);
-#define SKS(K) splitk_reduce_silu_kernel<T, K><<<grid, 256, 0, s>>>(out, Cs, S, I, ss)
+#define SKS(K) splitk_reduce_silu_kernel<T, K, IL><<<grid, 256, 0, s>>>(out, Cs, S, I, ss)
   switch (S) {
     case 2: SKS(2); break;
+    case 3: SKS(3); break;
     case 4: SKS(4); break;
+    case 5: SKS(5); break;
+    case 6: SKS(6); break;
+    case 8: SKS(8); break;
     default: SKS(0); break;
   }
 #undef SKS
 }
 
 void launch_splitk_reduce_silu(int dtype, void* out, const float* Cs, int S, int M, int I,
-                               int64_t slice_stride, hipStream_t s) {
+                               int64_t slice_stride, bool interleaved, hipStream_t s) {
   for (int m0 = 0; m0 < M; m0 += 65535) {   // gridDim.y <= 65535
     const int n = std::min(M - m0, 65535);
     const float* c = Cs + (int64_t)m0 * 2 * I;
-    if (dtype == DT_BF16)
-      splitk_reduce_silu_t<bf16>((bf16*)out + (int64_t)m0 * I, c, S, n, I, slice_stride, s);
-    else
-      splitk_reduce_silu_t<f16>((f16*)out + (int64_t)m0 * I, c, S, n, I, slice_stride, s);
+    if (dtype == DT_BF16) {
+      if (interleaved)
+        splitk_reduce_silu_t<bf16, true>((bf16*)out + (int64_t)m0 * I, c, S, n, I, slice_stride, s);
+      else
+        splitk_reduce_silu_t<bf16, false>((bf16*)out + (int64_t)m0 * I, c, S, n, I, slice_stride, s);
+    } else {
+      if (interleaved)
+        splitk_reduce_silu_t<f16, true>((f16*)out + (int64_t)m0 * I, c, S, n, I, slice_stride, s);
+      else
+        splitk_reduce_silu_t<f16, false>((f16*)out + (int64_t)m0 * I, c, S, n, I, slice_stride, s);
+    }
   }
 }
 

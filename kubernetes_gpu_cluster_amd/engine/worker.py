@@ -17,6 +17,7 @@ Executors:
 """
 from __future__ import annotations
 
+import logging
 import os
 import pickle
 import socket
@@ -37,6 +38,8 @@ from ..parallel.state import (destroy_parallel, get_state, init_parallel, init_p
 from .config import EngineConfig
 from .model_runner import ModelRunner, StepPlan
 
+log = logging.getLogger("kgc.worker")
+
 CMD_STEP, CMD_PROFILE, CMD_INIT_CACHE, CMD_CAPTURE, CMD_EXIT = 1, 2, 3, 4, 5
 N_HDR = 12                  # StepPlan.header() fields
 
@@ -44,6 +47,23 @@ N_HDR = 12                  # StepPlan.header() fields
 def default_max_model_len(cfg: EngineConfig) -> int:
     mcfg, _ = resolve_model(cfg.model)
     return cfg.max_model_len or mcfg.max_position
+
+
+def _fault_perturb_shard(model, ps) -> None:
+    """Fault injection for the TP parity oracles (tests/test_engine_gpu.py): with
+    KGC_FAULT_PERTURB_TP_RANK=r, TP rank r adds noise to its shard of every o_proj weight
+    after loading -- one wrong shard, which a teacher-forced comparison against TP = 1
+    must catch.  Unset in every real deployment."""
+    r = os.environ.get("KGC_FAULT_PERTURB_TP_RANK")
+    if r is None or ps.tp_size == 1 or int(r) != ps.tp_rank:
+        return
+    g = torch.Generator(device="cpu").manual_seed(1234)
+    with torch.no_grad():
+        for name, p in model.named_parameters():
+            if name.endswith("o_proj.weight"):
+                noise = torch.randn(p.shape, generator=g).to(p.device, p.dtype)
+                p.add_(noise * p.float().std().item())
+    log.warning("fault injection: TP rank %s perturbed its o_proj shards", r)
 
 
 class Worker:
@@ -91,6 +111,7 @@ class Worker:
         torch.manual_seed(cfg.seed)
         self.mcfg, self.model = load_model(cfg.model, self.dtype, dev, cfg.random_init,
                                            seed=cfg.seed)
+        _fault_perturb_shard(self.model, self.ps)
         if dev.type == "cuda" and not cfg.enforce_eager:
             # packed copies of the decode-GEMM weights for the K9m tiles, made before the
             # KV cache is sized so the pool accounts for them (ops/gemm.py)
@@ -108,8 +129,11 @@ class Worker:
             if fold is not None:
                 fold()
         if self.ps.tp_size > 1 and dev.type == "cuda" and not cfg.disable_custom_all_reduce:
-            from ..parallel.custom_allreduce import maybe_init_custom_allreduce
-            comm.set_custom_allreduce(maybe_init_custom_allreduce(self.ps, dev))
+            from ..parallel.custom_allreduce import calibration_rows, maybe_init_custom_allreduce
+            rows = (calibration_rows(min(cfg.cuda_graph_max_bs, cfg.max_num_seqs))
+                    if not self.ps.phantom else None)
+            comm.set_custom_allreduce(maybe_init_custom_allreduce(
+                self.ps, dev, self.mcfg.hidden_size, self.dtype, rows))
         # the cooperative sampler's error word (last PP stage samples)
         self.sampler_health = ops.SamplerHealth(dev) if dev.type == "cuda" else None
         self.ep_a2a = None

@@ -145,12 +145,14 @@ def _dg_weight(w: torch.Tensor, cfg: int, silu: bool) -> Optional[torch.Tensor]:
 
 
 def dgemm(x: torch.Tensor, w: torch.Tensor, cfg: int, S: int, epi: int = 1,
-          out: Optional[torch.Tensor] = None) -> torch.Tensor:
+          out: Optional[torch.Tensor] = None, silu_w: bool = False) -> torch.Tensor:
     """K9m: S == 1 -> x W^T in x's dtype (epi 1) or silu-paired [M, N/2] (epi 2);
-    S > 1 -> the [S, M, N] fp32 K-slices (the caller's consumer sums them)."""
+    S > 1 -> the [S, M, N] fp32 K-slices (the caller's consumer sums them).  silu_w: a
+    merged gate_up weight's slices from its SiLU-packed copy (packed cfgs: gate / up
+    16-column groups interleaved per tile, ``splitk_reduce_silu(interleaved=True)``)."""
     from . import _k
     M, N = x.shape[0], w.shape[0]
-    wk = _dg_weight(w, cfg, epi == 2)
+    wk = _dg_weight(w, cfg, epi == 2 or silu_w)
     if wk is None:
         raise RuntimeError("K9m plan names a packed tile but the weight was not packed")
     if S > 1:
@@ -184,9 +186,9 @@ def linear_silu(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] =
             cfg, S = p
             if S == 1:
                 return dgemm(x, w, cfg, 1, epi=2)
-            ws = dgemm(x, w, cfg, S)
+            ws = dgemm(x, w, cfg, S, silu_w=True)
             out = torch.empty(x.shape[0], w.shape[0] // 2, dtype=x.dtype, device=x.device)
-            _k().splitk_reduce_silu(out, ws)
+            _k().splitk_reduce_silu(out, ws, _dg_info(cfg)[2])
             return out
     return silu_mul(linear(x, w, bias))
 
@@ -587,8 +589,12 @@ def _dg_candidates(M: int, N: int, K: int, kind: str, packed: bool):
         if (pk and not packed) or N % bn:
             continue
         # S = 3, 5, 6 fill the CUs where powers of two do not (qkv at M = 256: 48
-        # column tiles x 5 = 240 workgroups vs 192 at S = 4); no XCD pairing for them
-        splits = (1,) if kind == "silu" else _DG_SPLITS
+        # column tiles x 5 = 240 workgroups vs 192 at S = 4); no XCD pairing for them.
+        # gate_up + SiLU: the fused epilogue (S = 1) where its column tiles fill the chip,
+        # split-K slices + the SiLU reduction where they do not (Llama-3-70B at TP = 8:
+        # 56 tiles at M = 256, 73 us on hipBLASLt in the phantom-rank anatomy)
+        tiles = ((M + bm - 1) // bm) * (N // bn)
+        splits = (1,) if kind == "silu" and tiles >= 192 else _DG_SPLITS
         for S in splits:
             if S <= K // 64:
                 out.append((c, S))
@@ -636,12 +642,13 @@ def _tune_dgemm(ws, N: int, K: int, ms, margin: float, reps: int, res: dict,
         best_t, best_cfg = float("inf"), None
         for cfg, S in _dg_candidates(M, N, K, kind, packed):
             wl = [_dg_weight(w, cfg, kind == "silu") for w in ws]
+            il = kind == "silu" and _dg_info(cfg)[2]      # packed SiLU tiles: interleaved
             buf = (torch.empty(S, M, N, dtype=torch.float32, device=x.device) if S > 1 else
                    torch.empty(M, N // 2 if kind == "silu" else N, dtype=x.dtype,
                                device=x.device))
             red = torch.empty(M, N // 2 if kind == "silu" else N, dtype=x.dtype, device=x.device)
 
-            def run(cfg=cfg, S=S, wl=wl, buf=buf, red=red):
+            def run(cfg=cfg, S=S, wl=wl, buf=buf, red=red, il=il):
                 for w in wl:
                     if S == 1:
                         _k().dgemm(buf, x, w, cfg, 2 if kind == "silu" else 1)
@@ -654,7 +661,7 @@ def _tune_dgemm(ws, N: int, K: int, ms, margin: float, reps: int, res: dict,
                         if kind == "qkv":
                             consume(buf)
                         elif kind == "silu":
-                            _k().splitk_reduce_silu(red, buf)
+                            _k().splitk_reduce_silu(red, buf, il)
                         elif kind == "tail":
                             _k().splitk_add_rms_norm(red, buf, res_t, gamma, 1e-6)
                         else:

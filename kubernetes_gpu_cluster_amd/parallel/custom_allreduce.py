@@ -18,6 +18,7 @@ other kernel.  ``--disable-custom-all-reduce`` (reference
 """
 from __future__ import annotations
 
+import collections
 import logging
 import os
 from typing import Optional
@@ -112,6 +113,11 @@ class CustomAllReduce:
         self.fused2_max = int(os.environ.get("KGC_AR_RMS2_MAX", self.cap if world <= 2 else 0))
         self.fused_calls = 0        # host-side launches (a graph capture counts once)
         self.fused2_calls = 0       # ... of them the two-shot form
+        # start-up calibration (calibrate): [(bytes, plain form, fused form)] ascending,
+        # consulted by every call up to its largest size; None: the thresholds above
+        self.table: Optional[list] = None
+        self.calibration: Optional[dict] = None
+        self.launches: collections.Counter = collections.Counter()   # form -> host launches
 
     def _set_bases(self, bases: list, sig_bytes: int) -> None:
         self.sig = bases
@@ -120,16 +126,49 @@ class CustomAllReduce:
         self.fdata2 = [b + sig_bytes + 4 * self.cap for b in bases]
         self.max_hidden = int(torch.ops.kgc.allreduce_rms_max_hidden())
 
+    # ------------------------------------------------------------------ policy
+    def _entry(self, nb: int) -> Optional[tuple]:
+        """The calibrated (bytes, plain, fused) entry covering a message of nb bytes: the
+        smallest calibrated size >= nb (None past the table or without one)."""
+        if not self.table:
+            return None
+        for e in self.table:
+            if nb <= e[0]:
+                return e
+        return None
+
+    def plain_form(self, nb: int) -> str:
+        """'one' | 'two' | 'rccl' for a plain all-reduce of nb bytes."""
+        e = self._entry(nb)
+        if e is not None:
+            return e[1]
+        if nb > self.cap:
+            return "rccl"
+        return "two" if nb > self.one_shot_max else "one"
+
+    def fused_form(self, nb: int) -> str:
+        """'fused1' | 'fused2' | 'split' (the plain form, then fused_add_rms_norm)."""
+        e = self._entry(nb)
+        if e is not None:
+            return e[2]
+        if nb <= min(self.fused_max, self.cap):
+            return "fused1"
+        if nb <= min(self.fused2_max, self.cap):
+            return "fused2"
+        return "split"
+
     def should_use(self, x: torch.Tensor) -> bool:
         if not x.is_cuda or x.dtype not in (torch.bfloat16, torch.float16):
             return False
         nb = x.numel() * x.element_size()
-        return x.is_contiguous() and 0 < nb <= self.cap and nb % (16 * self.world) == 0
+        return (x.is_contiguous() and 0 < nb <= self.cap and nb % (16 * self.world) == 0
+                and self.plain_form(nb) != "rccl")
 
     def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         nb = x.numel() * x.element_size()
-        torch.ops.kgc.xgmi_allreduce(x, self.data, self.sig, self.rank, self.cap,
-                                     nb > self.one_shot_max)
+        two = self.plain_form(nb) == "two"
+        self.launches["two" if two else "one"] += 1
+        torch.ops.kgc.xgmi_allreduce(x, self.data, self.sig, self.rank, self.cap, two)
         return x
 
     def can_fuse(self, x: torch.Tensor) -> bool:
@@ -137,9 +176,8 @@ class CustomAllReduce:
             return False
         H = x.shape[1]
         nb = x.numel() * x.element_size()
-        return (x.is_contiguous() and 0 < nb <= min(max(self.fused_max, self.fused2_max),
-                                                      self.cap)
-                and H % 8 == 0 and H <= self.max_hidden)
+        return (x.is_contiguous() and 0 < nb <= self.cap and H % 8 == 0
+                and H <= self.max_hidden and self.fused_form(nb) != "split")
 
     def all_reduce_add_rms(self, x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
                            eps: float, out: torch.Tensor = None):
@@ -148,13 +186,109 @@ class CustomAllReduce:
         if out is None:
             out = torch.empty_like(x)
         self.fused_calls += 1
-        two = x.numel() * x.element_size() > self.fused_max
+        two = self.fused_form(x.numel() * x.element_size()) == "fused2"
         if two:
             self.fused2_calls += 1
+        self.launches["fused2" if two else "fused1"] += 1
         torch.ops.kgc.xgmi_allreduce_rms(out, x, residual, w, eps,
                                          self.fdata2 if two else self.fdata, self.sig,
                                          self.rank, self.cap, two)
         return out, residual
+
+    # ------------------------------------------------------------------ calibration
+    def calibrate(self, hidden: int, dtype: torch.dtype, rows: list[int], tp_group, cpu_group,
+                  reps: int = 20) -> dict:
+        """Time every form on THIS node at each decode message size (rows x hidden) and
+        make the fastest the policy (the crossovers were fixed from a
+        one-GPU rehearsal).  Collective over the TP group: every rank runs the same
+        launches in the same order (the kernels wait for their peers), the per-rank times
+        are MAX-reduced, so every rank derives the same table.  Forms:
+          plain  'one' / 'two' (xGMI one- / two-shot) / 'rccl' (the process group);
+          fused  'fused1' / 'fused2' (one launch with the residual add + RMSNorm) /
+                 'split' (the plain choice, then fused_add_rms_norm).
+        The thresholds stay the fallback past the largest calibrated size."""
+        from .. import ops
+        dev = self.device
+        res = {"hidden": hidden, "rows": [], "bytes": [], "us": {}}
+        forms = ("one", "two", "rccl", "fused1", "fused2", "split")
+        times = []
+        w = torch.ones(hidden, dtype=dtype, device=dev)
+        saved = self.table
+        self.table = None
+        for m in rows:
+            nb = m * hidden * torch.finfo(dtype).bits // 8
+            x0 = (torch.randn(m, hidden, device=dev) * 0.01).to(dtype)
+            x, out = x0.clone(), torch.empty_like(x0)
+            resid = torch.zeros_like(x0)
+            ok_x = nb <= self.cap and nb % (16 * self.world) == 0
+            ok_f = nb <= self.cap and hidden % 8 == 0 and hidden <= self.max_hidden
+
+            def run(form, x=x, out=out, resid=resid, nb=nb):
+                if form in ("one", "two"):
+                    torch.ops.kgc.xgmi_allreduce(x, self.data, self.sig, self.rank, self.cap,
+                                                 form == "two")
+                elif form == "rccl":
+                    if dist.get_backend(tp_group) == dist.Backend.GLOO:
+                        xf = x.float()              # gloo: the fp32 path comm.py takes
+                        dist.all_reduce(xf, group=tp_group)
+                        x.copy_(xf)
+                    else:
+                        dist.all_reduce(x, group=tp_group)
+                elif form in ("fused1", "fused2"):
+                    torch.ops.kgc.xgmi_allreduce_rms(out, x, resid, w, 1e-6,
+                                                     self.fdata2 if form == "fused2" else
+                                                     self.fdata, self.sig, self.rank,
+                                                     self.cap, form == "fused2")
+            row = []
+            for form in forms:
+                if (form in ("one", "two") and not ok_x) or (form in ("fused1", "fused2")
+                                                            and not ok_f) or form == "split":
+                    row.append(float("inf"))
+                    continue
+                torch.cuda.synchronize(dev)
+                dist.barrier(group=cpu_group)
+                for _ in range(3):
+                    x.copy_(x0)
+                    run(form)
+                torch.cuda.synchronize(dev)
+                dist.barrier(group=cpu_group)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(reps):
+                    run(form)
+                e1.record()
+                e1.synchronize()
+                row.append(e0.elapsed_time(e1) * 1e3 / reps)
+            # 'split' = the fastest plain form + one fused_add_rms_norm launch
+            torch.cuda.synchronize(dev)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                ops.fused_add_rms_norm(x, resid, w, 1e-6)
+            e1.record()
+            e1.synchronize()
+            row[forms.index("split")] = min(row[:3]) + e0.elapsed_time(e1) * 1e3 / reps
+            times.append(row)
+            res["rows"].append(m)
+            res["bytes"].append(nb)
+        t = torch.tensor(times, dtype=torch.float64)
+        t[torch.isinf(t)] = 1e30
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=cpu_group)
+        table = []
+        for i, nb in enumerate(res["bytes"]):
+            tr = t[i].tolist()
+            plain = min(("one", "two", "rccl"), key=lambda f: tr[forms.index(f)])
+            fused = min(("fused1", "fused2", "split"), key=lambda f: tr[forms.index(f)])
+            table.append((nb, plain, fused))
+            for f in forms:
+                v = tr[forms.index(f)]
+                res["us"].setdefault(f, []).append(None if v >= 1e29 else round(v, 2))
+        res["table"] = [list(e) for e in table]
+        self.table, self.calibration = table, res
+        del saved
+        torch.cuda.synchronize(dev)
+        dist.barrier(group=cpu_group)
+        return res
 
     def check(self) -> None:
         """Raise if any barrier timed out waiting for a peer (see allreduce.hip)."""
@@ -230,9 +364,34 @@ class PhantomAllReduce(CustomAllReduce):
             self._own, self._peers = 0, []
 
 
-def maybe_init_custom_allreduce(ps, device: torch.device) -> Optional[CustomAllReduce]:
+def _calibration_wanted() -> bool:
+    """Start-up calibration of the all-reduce policy, unless KGC_AR_CALIBRATE=0 or an
+    operator fixed a threshold (KGC_AR_ONE_SHOT_MAX / KGC_AR_RMS_MAX / KGC_AR_RMS2_MAX /
+    KGC_AR_CAP): the environment overrides, the measurement is the default."""
+    if os.environ.get("KGC_AR_CALIBRATE", "1") == "0":
+        return False
+    return not any(os.environ.get(k) for k in ("KGC_AR_ONE_SHOT_MAX", "KGC_AR_RMS_MAX",
+                                                "KGC_AR_RMS2_MAX", "KGC_AR_CAP"))
+
+
+def calibration_rows(max_rows: int) -> list[int]:
+    """Decode message sizes the calibration times: powers of two up to the largest graph
+    bucket (the table is a step function between them)."""
+    rows, r = [], 1
+    while r < max_rows:
+        rows.append(r)
+        r *= 2
+    rows.append(max_rows)
+    return rows
+
+
+def maybe_init_custom_allreduce(ps, device: torch.device, hidden: int = 0,
+                                dtype: torch.dtype = torch.bfloat16,
+                                calibrate_rows: Optional[list] = None
+                                ) -> Optional[CustomAllReduce]:
     """Build the xGMI all-reduce for this rank's TP group, or None (RCCL only).
-    All TP ranks agree: if any rank cannot set it up, none uses it."""
+    All TP ranks agree: if any rank cannot set it up, none uses it.  With
+    ``calibrate_rows`` the per-size policy is timed on this node (CustomAllReduce.calibrate)."""
     if os.environ.get("KGC_CUSTOM_AR", "1") == "0" or ps.tp_size not in SUPPORTED_WORLD:
         return None
     if getattr(ps, "phantom", False):
@@ -245,6 +404,10 @@ def maybe_init_custom_allreduce(ps, device: torch.device) -> Optional[CustomAllR
     except RuntimeError as e:
         log.warning("%s; using RCCL", e)
         return None
+    if calibrate_rows and hidden and _calibration_wanted():
+        cal = car.calibrate(hidden, dtype, calibrate_rows, ps.tp_group, ps.tp_cpu_group)
+        log.info("xGMI all-reduce policy calibrated on this node (hidden %d): %s", hidden,
+                 " ".join(f"{r}r:{p}/{f}" for r, (_, p, f) in zip(cal["rows"], cal["table"])))
     log.info("xGMI all-reduce enabled: tp=%d cap=%d KiB (KGC_AR_CAP) one-shot<=%d KiB "
              "(KGC_AR_ONE_SHOT_MAX) fused add+RMSNorm one-shot<=%d KiB (KGC_AR_RMS_MAX), "
              "two-shot<=%d KiB (KGC_AR_RMS2_MAX), %d workgroups",

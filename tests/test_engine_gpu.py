@@ -1,5 +1,7 @@
 """Engine-level checks on the MI355X: model parity through the HIP kernels,
 hipGraph decode replay == eager, async engine loop, Llama-3-8B-dims smoke."""
+import os
+
 import pytest
 import torch
 
@@ -289,36 +291,13 @@ def test_engine_preemption_recompute(gpu):
     assert eng.bm.num_free == eng.bm.num_blocks - 1
 
 
-@pytest.mark.parametrize("tp,eager,name,overlap,xgmi", [(2, True, "tiny-llama", False, True),
-                                                        (2, False, "tiny-llama", False, True),
-                                                        (2, False, "tiny-llama", True, True),
-                                                        (4, False, "tiny-llama", False, True),
-                                                        (8, True, "tiny-llama-gqa8", False, False)])
-def test_tp_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch, tp, eager, name, overlap, xgmi):
-    """The tensor-parallel engine on the GPU: TP ranks share cuda:0 (gloo process group,
-    since RCCL refuses two ranks on one device), sharded QKV/MLP/vocab layers, the xGMI
-    all-reduce kernel over IPC buffers for the row-parallel sums, multiprocess workers.
-    eager=False is the production decode path: hipGraph-captured decode buckets with
-    the xGMI all-reduce INSIDE the graphs, and vocab-parallel sampling after the replay
-    (no logits all-gather).  overlap: the 100-token first prefill step runs as two
-    halves whose all-reduces are in flight while the other half computes
-    (KGC_TP_OVERLAP_MIN_TOKENS lowered from 2048 to 16).  TP = 4 replicates tiny-llama's
-    2 kv heads over 4 ranks.  TP = 8 (BASELINE config 3's degree: each of tiny-llama-gqa8's
-    2 kv heads on 4 ranks, the per-rank attention shape of 70B at TP = 8 -- one kv head,
-    GQA 1) runs every GPU kernel of the 8-rank engine with its sums over gloo
-    (KGC_CUSTOM_AR=0, eager): eight processes' spin kernels need not be co-resident on
-    ONE device, so the xGMI kernels' NR = 8 forms are proven by the single-launch world
-    emulation instead (test_allreduce_gpu.py::test_xgmi_world_emulation).  Greedy
-    continuations match TP=1 (bf16; sharded sums round differently, so a couple of late
-    near-tie flips are tolerated)."""
+def _write_hf_dir(tmp_path, cfg, std=0.08, seed=5):
     import json
     import os
     from safetensors.torch import save_file
-    from kubernetes_gpu_cluster_amd.engine.llm_engine import LLM
-    cfg = PRESETS[name]
     d = str(tmp_path / "m")
     os.makedirs(d)
-    save_file({k: v.contiguous() for k, v in full_state_dict_random(cfg, seed=5, std=0.15).items()},
+    save_file({k: v.contiguous() for k, v in full_state_dict_random(cfg, seed=seed, std=std).items()},
               os.path.join(d, "model.safetensors"))
     json.dump({"model_type": "llama", "hidden_size": cfg.hidden_size,
                "num_hidden_layers": cfg.num_layers, "num_attention_heads": cfg.num_heads,
@@ -327,53 +306,124 @@ def test_tp_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch, tp, eager, name, 
                "max_position_embeddings": 512, "rope_theta": cfg.rope_theta,
                "rms_norm_eps": cfg.rms_eps, "eos_token_id": 2, "bos_token_id": 1},
               open(os.path.join(d, "config.json"), "w"))
+    return d
+
+
+def _teacher_forced_deltas(d, prompts, runs):
+    """TP = 1 evaluates, by prefill, every prefix that the TP = N run decoded from:
+    prompt + its first j generated tokens, j = 0 .. n-1.  For each position returns
+    |logprob_N(y_j) - logprob_1(y_j)| (y_j = the token TP = N chose there) and whether
+    y_j is TP = 1's argmax or a near-tie of it (0.05 nats)."""
+    from kubernetes_gpu_cluster_amd.engine.llm_engine import LLM
+    reqs, keys = [], []
+    for i, (p, (toks, lps)) in enumerate(zip(prompts, runs)):
+        for j in range(len(toks)):
+            reqs.append(p + toks[:j])
+            keys.append((i, j))
+    llm = LLM(d, device="cuda", dtype="bfloat16", tensor_parallel_size=1, enforce_eager=True,
+              max_model_len=256, max_num_seqs=16, max_num_batched_tokens=512,
+              num_gpu_blocks_override=128, enable_prefix_caching=False)
+    try:
+        res = llm.generate(reqs, [SamplingParams(temperature=0, max_tokens=1, logprobs=5)] *
+                           len(reqs))
+    finally:
+        llm.shutdown()
+    out = []
+    for (i, j), r in zip(keys, res):
+        toks, lps = runs[i]
+        y, lp_n = toks[j], lps[j][1]
+        top1 = dict(r.logprobs[0][2])
+        best = max(top1.values())
+        lp_1 = top1.get(y)
+        out.append((i, j, None if lp_1 is None else abs(lp_n - lp_1),
+                    lp_1 is not None and best - lp_1 < 0.05))
+    return out
+
+
+@pytest.mark.parametrize("tp,eager,name,overlap,xgmi,perturb",
+                         [(2, True, "tiny-llama", False, True, False),
+                          (2, False, "tiny-llama", False, True, False),
+                          (2, False, "tiny-llama", True, True, False),
+                          (4, False, "tiny-llama", False, True, False),
+                          (8, True, "tiny-llama-gqa8", False, False, False),
+                          (2, False, "tiny-llama", False, True, True)])
+def test_tp_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch, tp, eager, name, overlap, xgmi,
+                                   perturb):
+    """The tensor-parallel engine on the GPU against TP = 1, TEACHER-FORCED: TP ranks share
+    cuda:0 (gloo process group, since RCCL refuses two ranks on one device), sharded
+    QKV/MLP/vocab layers, the xGMI all-reduce kernel over IPC buffers for the row-parallel
+    sums, multiprocess workers.  eager=False is the production decode path:
+    hipGraph-captured decode buckets with the xGMI all-reduce INSIDE the graphs.
+    overlap: the 100-token first prefill step runs as two halves whose all-reduces are in
+    flight while the other half computes (KGC_TP_OVERLAP_MIN_TOKENS lowered to 16).  TP = 4
+    replicates tiny-llama's 2 kv heads over 4 ranks.  TP = 8 (BASELINE config 3's degree:
+    one kv head per rank, the per-rank attention shape of 70B at TP = 8) runs every GPU
+    kernel of the 8-rank engine with its sums over gloo (KGC_CUSTOM_AR=0, eager); the
+    xGMI kernels' NR = 8 forms are proven by the single-launch world emulation and the
+    phantom rank (test_allreduce_gpu.py).
+
+    The oracle: TP = N decodes greedily and reports the logprob of every token it chose;
+    TP = 1 then prefills each prefix TP = N decoded from (the same tokens, not its own
+    continuation) and must give each chosen token the same logprob within 0.1 nats and
+    rank it first (or within a 0.05-nat near-tie).  A second TP = N pass without logprobs
+    (vocab-parallel sampling, no logits all-gather) must choose the same tokens.
+    perturb: rank 1 adds noise to its o_proj shards (KGC_FAULT_PERTURB_TP_RANK) -- the
+    oracle must then FAIL, i.e. it does catch one wrong shard."""
+    from kubernetes_gpu_cluster_amd.engine.llm_engine import LLM
+    cfg = PRESETS[name]
+    d = _write_hf_dir(tmp_path, cfg)
     prompts = [list(range(3, 40)), [5, 6, 7] * 20, [9, 10, 11]]
-    sp = [SamplingParams(temperature=0, max_tokens=8, ignore_eos=True)] * 3
-    # TP = 1 also reports its top-5 alternatives (TP > 1 keeps vocab-parallel sampling)
-    sp1 = [SamplingParams(temperature=0, max_tokens=8, ignore_eos=True, logprobs=5)] * 3
-    outs, top1 = {}, None
+    n_out = 8
     monkeypatch.setenv("KGC_DIST_BACKEND", "gloo")
     if not xgmi:
         monkeypatch.setenv("KGC_CUSTOM_AR", "0")
     if overlap:
         monkeypatch.setenv("KGC_TP_OVERLAP_MIN_TOKENS", "16")
-    tp_n = tp
-    for tp in (1, tp_n):
-        llm = LLM(d, device="cuda", dtype="bfloat16", tensor_parallel_size=tp, enforce_eager=eager,
-                  max_model_len=256, max_num_seqs=4, max_num_batched_tokens=128,
-                  num_gpu_blocks_override=64)
-        car = None
-        if tp > 1:
-            from kubernetes_gpu_cluster_amd.parallel import comm
-            car = comm.get_custom_allreduce()
-            if xgmi:
-                assert car is not None, f"xGMI all-reduce was not set up for TP={tp}"
-                assert car.world == tp
-            else:
-                assert car is None, "KGC_CUSTOM_AR=0 must leave every sum to the process group"
-        res = llm.generate(prompts, sp1 if tp == 1 else sp)
-        outs[tp] = [o.output_token_ids for o in res]
-        if tp == 1:
-            top1 = [dict(o.logprobs[0][2]) for o in res]
+    if perturb:
+        monkeypatch.setenv("KGC_FAULT_PERTURB_TP_RANK", "1")
+    llm = LLM(d, device="cuda", dtype="bfloat16", tensor_parallel_size=tp, enforce_eager=eager,
+              max_model_len=256, max_num_seqs=4, max_num_batched_tokens=128,
+              num_gpu_blocks_override=64)
+    try:
+        from kubernetes_gpu_cluster_amd.parallel import comm
+        car = comm.get_custom_allreduce()
+        if xgmi:
+            assert car is not None and car.world == tp, f"xGMI all-reduce not set up for TP={tp}"
+            # the per-size policy was timed on this box at start-up (every rank agrees on it:
+            # the times are MAX-reduced) and it is what the captured graphs launched
+            cal = car.calibration
+            assert car.table and cal["rows"][0] == 1 and cal["rows"][-1] >= 4, cal
+            table_forms = {f for _, p, fu in car.table for f in (p, fu)}
+        else:
+            assert car is None, "KGC_CUSTOM_AR=0 must leave every sum to the process group"
+        res = llm.generate(prompts, [SamplingParams(temperature=0, max_tokens=n_out,
+                                                    ignore_eos=True, logprobs=5)] * 3)
+        runs = [(o.output_token_ids, o.logprobs) for o in res]
+        plain = llm.generate(prompts, [SamplingParams(temperature=0, max_tokens=n_out,
+                                                      ignore_eos=True)] * 3)
+        st = llm.engine.executor.runner.stats
         if car is not None:
             car.check()         # a time-out on ANY rank is raised in every rank's word
-            assert car.fused_calls > 0, "fused all-reduce + add + RMSNorm never ran"
-        if tp > 1:
-            st = llm.engine.executor.runner.stats
-            if os.environ.get("KGC_VP_SAMPLING", "1") != "0":
-                assert st["vp_steps"] > 0, st
-            if not eager:
-                assert st["graph_steps"] > 0, st
+            assert sum(car.launches.values()) > 0, "the xGMI kernels never ran"
+            assert set(car.launches) <= table_forms, (dict(car.launches), car.table)
+            if table_forms & {"fused1", "fused2"}:
+                assert car.fused_calls > 0, "fused all-reduce + add + RMSNorm never ran"
+        if os.environ.get("KGC_VP_SAMPLING", "1") != "0":
+            assert st["vp_steps"] > 0, st
+        if not eager:
+            assert st["graph_steps"] > 0, st
+    finally:
         llm.shutdown()
-    same = sum(a == b for x, y in zip(outs[1], outs[tp_n]) for a, b in zip(x, y))
-    for i, (x, y) in enumerate(zip(outs[1], outs[tp_n])):
-        # the first token: TP = 1's argmax, or a near-tie of it.  The random tiny model
-        # (std 0.15 weights) has logits of magnitude ~10, where one bf16 ulp is 0.06; the
-        # sharded sums round each rank's partial once more, so ties within 0.15 may flip
-        # (the CPU bf16 reference flips prompt 2 the same way at TP = 1 already)
-        if x[0] != y[0]:
-            assert y[0] in top1[i] and top1[i][x[0]] - top1[i][y[0]] < 0.15, (i, top1[i], outs)
-    assert same >= 0.6 * sum(len(x) for x in outs[1]), outs
+    for (toks, _), o in zip(runs, plain):
+        assert o.output_token_ids == toks, "vocab-parallel sampling chose other tokens"
+    monkeypatch.delenv("KGC_FAULT_PERTURB_TP_RANK", raising=False)
+    deltas = _teacher_forced_deltas(d, prompts, runs)
+    bad = [(i, j, dlt, top) for i, j, dlt, top in deltas if dlt is None or dlt > 0.1 or not top]
+    worst = max((dlt for _, _, dlt, _ in deltas if dlt is not None), default=None)
+    if perturb:
+        assert bad, f"one perturbed shard went unnoticed (max delta {worst})"
+    else:
+        assert not bad, (bad, worst)
 
 
 def test_logprobs_through_decode_graphs(gpu):

@@ -126,8 +126,15 @@ def _fill_random_cache(B, ctx_lens, nkv, bs, d, dt, dev, nb_extra=7):
 
 
 # decode kernel per launch: K1w (one wave per z-slice) from DECODE_WAVE_MIN_PAIRS (seq, kv-head)
-# pairs up, the 4-wave kernel below; the threshold override runs both on every shape
-_DECODE_KERNELS = {"wave": "1", "four": "1000000000"}
+# pairs up -- its four-deep pipeline for grids of at most DEC_DEEP_MAX_WAVES waves -- and the
+# 4-wave kernel below; the threshold overrides run all three on every shape
+_DECODE_KERNELS = {"wave": ("1", "0"), "deep": ("1", "1000000000"), "four": ("1000000000", "0")}
+
+
+def _use_decode_kernel(monkeypatch, kern):
+    pairs, deep = _DECODE_KERNELS[kern]
+    monkeypatch.setenv("KGC_DECODE_WAVE_MIN_PAIRS", pairs)
+    monkeypatch.setenv("KGC_DECODE_DEEP_MAX_WAVES", deep)
 
 
 @pytest.mark.parametrize("dt", DT)
@@ -139,7 +146,7 @@ def test_paged_decode(gpu, monkeypatch, kern, dt, d, nq, nkv, bs):
     """K1 vs the fp32 reference at ragged lengths (1 token .. 2049), GQA 1/4/7/8 and MHA,
     z = 1, 3 and 40 (K1w: most slices of the short rows empty, the reduce merges only the
     used ones)."""
-    monkeypatch.setenv("KGC_DECODE_WAVE_MIN_PAIRS", _DECODE_KERNELS[kern])
+    _use_decode_kernel(monkeypatch, kern)
     torch.manual_seed(3)
     ctx = [1, 17, 128, 129, 300, 1000, 2049, 64]
     B = len(ctx)
@@ -163,7 +170,7 @@ def test_paged_decode_rope(gpu, monkeypatch, kern, dt, d, nq, nkv, qk_norm, S, f
     """The decode kernel with rope_kv_write folded in == rope_kv_write + paged_decode on
     the same inputs (q / k / v and the cache update), and == the fp32 reference.  One row
     is graph padding (ctx 0, slot -1): nothing of it reaches the cache."""
-    monkeypatch.setenv("KGC_DECODE_WAVE_MIN_PAIRS", _DECODE_KERNELS[kern])
+    _use_decode_kernel(monkeypatch, kern)
     torch.manual_seed(17 + d + S)
     bs = 16
     ctx = [1, 17, 300, 1000, 0, 64, 129]
@@ -225,7 +232,7 @@ def test_paged_decode_rope(gpu, monkeypatch, kern, dt, d, nq, nkv, qk_norm, S, f
 def test_paged_decode_workspace_reuse(gpu, monkeypatch, kern):
     """One static partials workspace serves launches of any Z (incl. an empty context),
     eager or replayed from a graph."""
-    monkeypatch.setenv("KGC_DECODE_WAVE_MIN_PAIRS", _DECODE_KERNELS[kern])
+    _use_decode_kernel(monkeypatch, kern)
     torch.manual_seed(13)
     dt, d, nq, nkv, bs = torch.bfloat16, 128, 32, 8, 32
     ctx = [1, 700, 2049, 64, 0, 333]
@@ -932,17 +939,21 @@ def test_linear_uses_tuned_plan(gpu):
 
 
 @pytest.mark.parametrize("M,N,K,plan", [(256, 2048, 4096, (8, 1)), (80, 1536, 2048, (5, 1)),
-                                         (144, 1024, 1024, (0, 2)), (96, 2048, 2048, (2, 1))])
+                                         (144, 1024, 1024, (0, 2)), (96, 2048, 2048, (2, 1)),
+                                         (256, 2048, 4096, (4, 2)), (256, 7168, 1024, (6, 5)),
+                                         (200, 1024, 2048, (9, 3))])
 def test_linear_silu_dgemm_matches_fp32(gpu, M, N, K, plan):
     """gate_up through the K9m plan -- fused SiLU epilogue (S = 1, packed silu weights) or
-    split-K slices summed by splitk_reduce_silu -- vs an fp32 silu(g) * u reference."""
+    split-K slices summed by splitk_reduce_silu (row-major tiles: [gate | up] halves; packed
+    tiles: the interleaved 16-column groups of the SiLU packing) -- vs an fp32 silu(g) * u
+    reference.  Only the SiLU-packed copy exists, as in the engine."""
     from kubernetes_gpu_cluster_amd.ops import gemm
     torch.manual_seed(M + N + 1)
     x = torch.randn(M, K, dtype=torch.bfloat16, device=gpu)
     w = torch.randn(N, K, dtype=torch.bfloat16, device=gpu) * 0.03
     y = x.float().cpu() @ w.float().cpu().t()
     ref = torch.nn.functional.silu(y[:, : N // 2]) * y[:, N // 2:]
-    gemm.pack_decode_weights([w], [w])
+    gemm.pack_decode_weights([], [w])
     gemm._plan_dg[(M, N, K, "silu")] = plan
     try:
         got = gemm.linear_silu(x, w)
