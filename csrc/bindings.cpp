@@ -1059,7 +1059,6 @@ std::vector<int64_t> sample_stamps() {
 }
 
 int64_t decode_wave_min_pairs() { return kgc::paged_decode_wave_min_pairs(); }
-int64_t decode_deep_max_waves() { return kgc::paged_decode_deep_max_waves(); }
 int64_t prefill_block_m() { return kgc::prefill_block_m(); }
 
 }  // namespace
@@ -1094,7 +1093,6 @@ TORCH_LIBRARY(kgc, m) {
         "int vocab_off) -> ()");
   m.def("sample_vp_unpack(Tensor(a!) out, Tensor packed) -> ()");
   m.def("decode_wave_min_pairs() -> int", &decode_wave_min_pairs);
-  m.def("decode_deep_max_waves() -> int", &decode_deep_max_waves);
   m.def("moe_route(Tensor(a!) topk_w, Tensor(b!) topk_ids, Tensor logits, bool renorm) -> ()");
   m.def("moe_align(Tensor(a!) sorted_ids, Tensor(b!) block_expert, Tensor(c!) meta, "
         "Tensor topk_ids, int e0, int E_local, int bm) -> ()");

@@ -44,17 +44,23 @@ constexpr int DEC_MAX_Z = 1024;  // z-slices the reduce kernel merges (host-chec
 // K1w runs where the grid has at least this many (seq, kv-head) pairs; smaller batches
 // take the 4-wave kernel (B = 1: 9.3 vs 12.3 us at ctx 640; ops/__init__.py mirrors it)
 constexpr int DEC_WAVE_MIN_PAIRS = 64;
-// ... and grids of at most this many waves use its four-deep pipeline
-constexpr int DEC_DEEP_MAX_WAVES = 1024;
+// ... and from this many pairs up a context of up to DEC_LONG_MIN_CHUNKS chunks is one slice
+constexpr int DEC_LONG_PAIRS = 256;
+constexpr int DEC_LONG_MIN_CHUNKS = 24;
 
-// K1w: 32-token chunks per z-slice (>= 2, the pipeline depth); slices past the context are
-// empty and the reduce stops at decode_used_slices
-__host__ __device__ __forceinline__ int decode_slice_chunks(int nchunk, int Z) {
+// K1w: 32-token chunks per z-slice (>= min_per, at least 2: the pipeline depth); slices
+// past the context are empty and the reduce stops at decode_used_slices.  min_per is a
+// per-launch host choice (decode_min_chunks): the graph's Z is sized for max_model_len,
+// and with many (seq, kv-head) pairs short contexts run best as ONE slice per pair (the
+// 70B TP = 8 rank at B = 256, ctx 640: 17.5 us at one slice vs 23.2 at seven of three
+// chunks + the merge, profiles/README.md "Round 5").
+__host__ __device__ __forceinline__ int decode_slice_chunks(int nchunk, int Z, int min_per) {
   const int per = (nchunk + Z - 1) / Z;
-  return per < 2 ? 2 : per;
+  return per < min_per ? min_per : per;
 }
-__host__ __device__ __forceinline__ int decode_used_slices(int nchunk, int Z) {
-  const int n = (nchunk + decode_slice_chunks(nchunk, Z) - 1) / decode_slice_chunks(nchunk, Z);
+__host__ __device__ __forceinline__ int decode_used_slices(int nchunk, int Z, int min_per) {
+  const int per = decode_slice_chunks(nchunk, Z, min_per);
+  const int n = (nchunk + per - 1) / per;
   return n < Z ? n : Z;
 }
 
@@ -467,17 +473,15 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
 // vector load the chunk pipeline would have to wait behind.
 // Z > 1: slice z writes (max, sum, O) partials at row-major slot row * Z + z (the reduce
 // kernel runs with Zmax = Z).
-// DEEP: the chunk pipeline four deep instead of two (four named buffers, 64 more VGPRs
-// than fit two waves per SIMD): for grids of few waves per CU -- e.g. the 70B TP = 8 rank
-// at batch 256, 256 (seq, kv-head) pairs -- where two chunks in flight per wave cannot
-// keep a CU's HBM queue full.
-template <typename T, int D, bool KV8, bool FUSE, bool DEEP = false>
-__global__ __launch_bounds__(64, DEEP ? 1 : 2) void paged_decode_wave_kernel(
+// (A four-deep variant -- four named chunk buffers at one wave per SIMD -- measured slower
+// at every shape, e.g. 21.5 vs 17.5 us at B = 256, nq 8 / nkv 1, one slice: removed.)
+template <typename T, int D, bool KV8, bool FUSE>
+__global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
     T* __restrict__ out, const T* __restrict__ q, const void* __restrict__ kc_,
     const void* __restrict__ vc_, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ ctx_lens, float* __restrict__ max_logits,
     float* __restrict__ exp_sums, float* __restrict__ tmp_out, int nq, int nkv, int bs_log2,
-    float scale_log2, float v_scale, int num_blocks, DecodeRope rp) {
+    float scale_log2, float v_scale, int num_blocks, DecodeRope rp, int min_per) {
   typedef typename Vec8<T>::type V8;
   typedef std::conditional_t<KV8, uint8_t, T> C;
   const C* __restrict__ kc = reinterpret_cast<const C*>(kc_);
@@ -507,7 +511,8 @@ __global__ __launch_bounds__(64, DEEP ? 1 : 2) void paged_decode_wave_kernel(
   // non-empty slices come first and the reduce merges only those (a graph captured with
   // Z sized for max_model_len meets short contexts: most slices are then empty)
   const int nchunk = (ctx + 31) >> 5;
-  const int per = decode_slice_chunks(nchunk, Z);
+  const int per = decode_slice_chunks(nchunk, Z, min_per);
+  const int nused = decode_used_slices(nchunk, Z, min_per);
   const int c0 = min(nchunk, z * per);
   const int c1 = min(nchunk, c0 + per);
   const int end = min(ctx, c1 << 5);          // this wave's tokens: [c0*32, end)
@@ -591,7 +596,7 @@ __global__ __launch_bounds__(64, DEEP ? 1 : 2) void paged_decode_wave_kernel(
     constexpr int TPH = D / 16;
     // the new token's k / v: written by the slice that reads the context's last chunk
     // (slices are compact: that is slice nz - 1, not Z - 1)
-    const bool has_kv = ctx > 0 && z == decode_used_slices(nchunk, Z) - 1;
+    const bool has_kv = ctx > 0 && z == nused - 1;
     if (G * TPH <= 32) {
       // ONE pass, every lane its own role, so the q, k and v slice loads are all in
       // flight together (as separate branches they were three dependent round trips):
@@ -735,35 +740,20 @@ __global__ __launch_bounds__(64, DEEP ? 1 : 2) void paged_decode_wave_kernel(
   // issue and its use makes the compiler's wait-count pass merge the paths and wait for
   // the younger buffer too (measured in the .s: vmcnt(15) instead of (31) before the
   // first MFMA, i.e. the pipeline serialised).
-  if constexpr (DEEP) {
-    // four deep: three chunks in flight while one computes (the same straight-line,
-    // clamped-issue / masked-compute form as the two-deep loop)
-    Frag fc, fd;
-    issue(fb, min(c0 + 1, c1 - 1));
-    issue(fc, min(c0 + 2, c1 - 1));
-    for (int ci = c0; ci < c1; ci += 4) {
-      issue(fd, min(ci + 3, c1 - 1));
-      compute(fa, ci);
-      issue(fa, min(ci + 4, c1 - 1));
-      compute(fb, ci + 1);
-      issue(fb, min(ci + 5, c1 - 1));
-      compute(fc, ci + 2);
-      issue(fc, min(ci + 6, c1 - 1));
-      compute(fd, ci + 3);
-    }
-  } else {
-    for (int ci = c0; ci < c1; ci += 2) {
-      issue(fb, min(ci + 1, c1 - 1));
-      compute(fa, ci);
-      issue(fa, min(ci + 2, c1 - 1));
-      compute(fb, ci + 1);
-    }
+  for (int ci = c0; ci < c1; ci += 2) {
+    issue(fb, min(ci + 1, c1 - 1));
+    compute(fa, ci);
+    issue(fa, min(ci + 2, c1 - 1));
+    compute(fb, ci + 1);
   }
 
   l_run += __shfl_xor(l_run, 16, 64);
   l_run += __shfl_xor(l_run, 32, 64);
   const int64_t row = (int64_t)b * nq + h * G + r16;
-  if (Z == 1) {
+  // one slice covers the whole context (Z == 1, or min_per >= the context's chunks): the
+  // normalised output directly -- the reduce skips such a row
+  if (Z == 1 || nused == 1) {
+    if (z > 0) return;
     if (r16 >= G) return;
     const float inv = l_run > 0.f ? v_scale / l_run : 0.f;
     T* orow = out + row * D + 4 * qd;
@@ -782,7 +772,7 @@ __global__ __launch_bounds__(64, DEEP ? 1 : 2) void paged_decode_wave_kernel(
   // (seq, kv-head) -- measured slower than the reduce launch at every Z > 1 shape: B = 32
   // 59.2 vs 52.8 us, B = 1 12.9 vs 12.3 us; one wave merging G heads serialises what the
   // reduce spreads over B * nq waves.  profiles/README.md "K1w".)
-  if (z >= decode_used_slices(nchunk, Z) || r16 >= G) return;
+  if (z >= nused || r16 >= G) return;
   const int64_t prow = row * Z + z;
   float* dst = tmp_out + prow * D + 4 * qd;
 #pragma unroll
@@ -801,7 +791,7 @@ template <typename T, int D, bool WAVE>
 __global__ __launch_bounds__(64) void paged_decode_reduce_kernel(
     T* __restrict__ out, const float* __restrict__ max_logits,
     const float* __restrict__ exp_sums, const float* __restrict__ tmp_out,
-    const int* __restrict__ ctx_lens, int nq, int Zg, int Zmax, int ctx_cap) {
+    const int* __restrict__ ctx_lens, int nq, int Zg, int Zmax, int ctx_cap, int min_per) {
   // The slice statistics are read in parallel (lane z), the weights staged in LDS,
   // and the partial rows loaded 8 slices at a time: the previous per-slice loop was a
   // chain of dependent L2 round trips (~7 us per call at B = 1; decode + reduce for
@@ -812,7 +802,8 @@ __global__ __launch_bounds__(64) void paged_decode_reduce_kernel(
   // as it clamps it (ctx_cap = bt_stride << bs_log2), so a ctx_len past the table never
   // makes this merge read slices that kernel did not write this step
   const int ctx = min(max(ctx_lens[b], 0), ctx_cap);
-  const int Z = WAVE ? decode_used_slices((ctx + 31) >> 5, Zg) : Zg;
+  const int Z = WAVE ? decode_used_slices((ctx + 31) >> 5, Zg, min_per) : Zg;
+  if (WAVE && Z == 1 && ctx > 0) return;     // the decode kernel wrote this row itself
   T* orow = out + ((int64_t)b * nq + hq) * D;
   constexpr int EPT = D / 64;
   const int64_t base = ((int64_t)b * nq + hq) * Zmax;
@@ -875,14 +866,15 @@ bool decode_use_wave(int B, int nkv) {
   return decode_wave_enabled() && (int64_t)B * nkv >= decode_wave_min_pairs();
 }
 
-// K1w grids of at most this many waves run the four-deep pipeline (DEEP): below it a CU
-// holds too few waves to keep its HBM queue full two chunks at a time
-// (KGC_DECODE_DEEP_MAX_WAVES overrides; 0 turns it off; ops/__init__.py mirrors it)
-static int decode_deep_max_waves() {
-  const char* e = getenv("KGC_DECODE_DEEP_MAX_WAVES");
-  return e ? atoi(e) : DEC_DEEP_MAX_WAVES;
+// K1w's minimum 32-token chunks per z-slice for a launch of B x nkv pairs: from
+// DEC_LONG_PAIRS pairs up the chip is filled by the pairs themselves, so a context of up to
+// DEC_LONG_MIN_CHUNKS chunks stays one slice (no partials, no merge); below it slices of 2
+// (KGC_DECODE_MIN_CHUNKS overrides for every launch).
+static int decode_min_chunks(int B, int nkv) {
+  const char* e = getenv("KGC_DECODE_MIN_CHUNKS");
+  if (e) return atoi(e) < 2 ? 2 : atoi(e);
+  return (int64_t)B * nkv >= DEC_LONG_PAIRS ? DEC_LONG_MIN_CHUNKS : 2;
 }
-int paged_decode_deep_max_waves() { return decode_deep_max_waves(); }
 
 template <typename T, int D, bool KV8, bool FUSE>
 static void decode_dispatch(void* out, const void* q, const void* kc, const void* vc,
@@ -891,14 +883,11 @@ static void decode_dispatch(void* out, const void* q, const void* kc, const void
                             float scale_log2, float v_scale, int num_blocks,
                             const DecodeRope& rp, hipStream_t s) {
   const bool wave = decode_use_wave(B, nkv);
-  if (wave && (int64_t)B * nkv * Z <= decode_deep_max_waves()) {
-    paged_decode_wave_kernel<T, D, KV8, FUSE, true><<<dim3(B, nkv, Z), 64, 0, s>>>(
-        (T*)out, (const T*)q, kc, vc, bt, bt_stride, ctx, ml, es, tmp, nq, nkv, bs_log2,
-        scale_log2, v_scale, num_blocks, rp);
-  } else if (wave) {
+  const int min_per = decode_min_chunks(B, nkv);
+  if (wave) {
     paged_decode_wave_kernel<T, D, KV8, FUSE><<<dim3(B, nkv, Z), 64, 0, s>>>(
         (T*)out, (const T*)q, kc, vc, bt, bt_stride, ctx, ml, es, tmp, nq, nkv, bs_log2,
-        scale_log2, v_scale, num_blocks, rp);
+        scale_log2, v_scale, num_blocks, rp, min_per);
   } else {
     paged_decode_kernel<T, D, true, KV8, 4, 1, FUSE><<<dim3(B, nkv, Z), 256, 0, s>>>(
         (T*)out, (const T*)q, kc, vc, bt, bt_stride, ctx, ml, es, tmp, nq, nkv, bs_log2, Z,
@@ -908,11 +897,13 @@ static void decode_dispatch(void* out, const void* q, const void* kc, const void
   if (wave)
     paged_decode_reduce_kernel<T, D, true><<<dim3(B, nq), 64, 0, s>>>((T*)out, ml, es, tmp, ctx,
                                                                       nq, Z, Z,
-                                                                      bt_stride << bs_log2);
+                                                                      bt_stride << bs_log2,
+                                                                      min_per);
   else
     paged_decode_reduce_kernel<T, D, false><<<dim3(B, nq), 64, 0, s>>>((T*)out, ml, es, tmp,
                                                                        ctx, nq, Z, Z,
-                                                                       bt_stride << bs_log2);
+                                                                       bt_stride << bs_log2,
+                                                                       min_per);
 }
 
 template <bool FUSE>

@@ -31,7 +31,6 @@ void launch_paged_decode(int dtype, void* out, const void* q, const void* k_cach
 // smallest B * nkv that runs K1w (one wave per (seq, kv-head, z-slice)); -1: K1w disabled
 // (KGC_DECODE_WAVE=0) and every launch takes the 4-wave workgroup kernel
 int paged_decode_wave_min_pairs();
-int paged_decode_deep_max_waves();
 // K1 + K3/K5/K6 fused for decode-only steps: the decode kernel takes the QKV projection
 // row itself (T [B, qkv_stride], or S > 0 fp32 split-K slices [S, B, qkv_stride]),
 // builds q (optional per-head RMSNorm, NeoX RoPE) in the MFMA operand registers, and

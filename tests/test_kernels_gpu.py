@@ -126,15 +126,16 @@ def _fill_random_cache(B, ctx_lens, nkv, bs, d, dt, dev, nb_extra=7):
 
 
 # decode kernel per launch: K1w (one wave per z-slice) from DECODE_WAVE_MIN_PAIRS (seq, kv-head)
-# pairs up -- its four-deep pipeline for grids of at most DEC_DEEP_MAX_WAVES waves -- and the
-# 4-wave kernel below; the threshold overrides run all three on every shape
-_DECODE_KERNELS = {"wave": ("1", "0"), "deep": ("1", "1000000000"), "four": ("1000000000", "0")}
+# pairs up -- with slices of at least 2 chunks, or ("wave1") a minimum so large that every
+# context is ONE slice writing its output directly (the many-pairs form) -- and the 4-wave
+# kernel below; the overrides run all three on every shape
+_DECODE_KERNELS = {"wave": ("1", "2"), "wave1": ("1", "100000"), "four": ("1000000000", "2")}
 
 
 def _use_decode_kernel(monkeypatch, kern):
-    pairs, deep = _DECODE_KERNELS[kern]
+    pairs, min_chunks = _DECODE_KERNELS[kern]
     monkeypatch.setenv("KGC_DECODE_WAVE_MIN_PAIRS", pairs)
-    monkeypatch.setenv("KGC_DECODE_DEEP_MAX_WAVES", deep)
+    monkeypatch.setenv("KGC_DECODE_MIN_CHUNKS", min_chunks)
 
 
 @pytest.mark.parametrize("dt", DT)
