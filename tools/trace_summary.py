@@ -31,14 +31,43 @@ def family(name: str) -> str:
     return n[:60]
 
 
+GRID = {}    # kernel dispatch (start, name) -> workgroups, where the trace records it
+
+
+def _grid_cols(cols) -> list:
+    """The grid-size columns of a rocpd kernels view / kernel-trace CSV, x / y / z order."""
+    out = []
+    for axis in ("x", "y", "z"):
+        for c in cols:
+            lc = c.lower()
+            if "grid" in lc and lc.endswith(axis) and "workgroup" not in lc:
+                out.append(c)
+                break
+    return out
+
+
 def load(path: str):
     """(start_ns, end_ns, kernel name) of every dispatch, from a rocprofv3 kernel-trace
-    CSV or a rocpd SQLite database (rocprofv3's default output format on ROCm 7)."""
+    CSV or a rocpd SQLite database (rocprofv3's default output format on ROCm 7).  Grid
+    sizes, where present, go to GRID (the per-instantiation view splits shapes by them)."""
     if path.endswith(".db"):
         import sqlite3
         con = sqlite3.connect(path)
+        cols = [r[1] for r in con.execute("pragma table_info(kernels)")]
+        g = _grid_cols(cols)
+        wg = [c for c in cols if "workgroup_size" in c.lower() or c.lower().startswith("workgroup_")]
+        if g:
+            q = "select start, end, name, " + ", ".join(g + wg[:3]) + " from kernels"
+            rows = list(con.execute(q))
+            for r in rows:
+                GRID[(r[0], r[2])] = tuple(r[3:])
+            return sorted((r[0], r[1], r[2]) for r in rows)
         return sorted(con.execute("select start, end, name from kernels"))
     rows = list(csv.DictReader(open(path)))
+    g = _grid_cols(rows[0].keys()) if rows else []
+    for r in rows:
+        if g:
+            GRID[(int(r["Start_Timestamp"]), r["Kernel_Name"])] = tuple(r[c] for c in g)
     return sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
                   for r in rows)
 
@@ -80,20 +109,28 @@ def main():
             # per kernel instantiation (template arguments kept): calls per step, us per call
             # an instantiation called k times per layer (o and down share one) is split by
             # its occurrence index mod k: "#0", "#1" in call order
-            per_step = collections.Counter(n for s, e, n in ev[samp[0] + 1:samp[1] + 1])
-            layers = 32
+            # an instantiation launched with different grids (shapes) is split by grid
+            # when the trace records it ("[g x,y,z]")
+            def name_of(s, n):
+                g = GRID.get((s, n))
+                return f"{n} [g {','.join(str(v) for v in g)}]" if g else n
+            per_step = collections.Counter(name_of(s, n) for s, e, n in ev[samp[0] + 1:samp[1] + 1])
             for a, b in zip(samp, samp[1:]):
                 seg = ev[a + 1:b + 1]
                 if len(seg) == nk:
-                    per_step = collections.Counter(n for s, e, n in seg)
+                    per_step = collections.Counter(name_of(s, n) for s, e, n in seg)
                     break
+            # layers per step: the attention launches (one per layer)
+            layers = max(1, sum(v for n, v in per_step.items()
+                                if "paged_decode" in n and "reduce" not in n)) or 32
             byname, ncall = collections.Counter(), collections.Counter()
             for a, b in zip(samp, samp[1:]):
                 seg = ev[a + 1:b + 1]
                 if len(seg) != nk:
                     continue
                 seen = collections.Counter()
-                for s, e, n in seg:
+                for s, e, n0 in seg:
+                    n = name_of(s, n0)
                     k = per_step[n] // layers if per_step[n] % layers == 0 else 1
                     key = f"#{seen[n] % k} {n}" if k > 1 else n
                     seen[n] += 1
@@ -102,7 +139,7 @@ def main():
             print("\ndecode-step kernels by instantiation (calls/step, us/call, us/step):")
             for n, v in byname.most_common(24):
                 c = ncall[n] / len(dec)
-                print(f"   {c:6.1f} {v / ncall[n] / 1e3:8.2f} {v / len(dec) / 1e3:9.1f}  {n[:110]}")
+                print(f"   {c:6.1f} {v / ncall[n] / 1e3:8.2f} {v / len(dec) / 1e3:9.1f}  {n[:150]}")
         # prefill (chunked) steps: the ones that run the prefill attention kernel and no
         # decode-sized GEMM (start-up tuning runs those between sampler calls too)
         pre = [s for s in steps if s[3].get("prefill_attn", 0) > 0
