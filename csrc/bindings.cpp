@@ -698,7 +698,7 @@ void ar_err_copy_async(int64_t sig, Tensor host_out) {
 }
 
 void xgmi_allreduce(Tensor inout, std::vector<int64_t> data, std::vector<int64_t> sig, int64_t rank,
-                    int64_t cap_bytes, bool two_shot) {
+                    int64_t cap_bytes, bool two_shot, bool wide) {
   check_gpu(inout, "inout");
   c10::hip::HIPGuardMasqueradingAsCUDA g(inout.device());
   const int64_t nr = (int64_t)data.size();
@@ -715,8 +715,9 @@ void xgmi_allreduce(Tensor inout, std::vector<int64_t> data, std::vector<int64_t
     P.data[r] = (void*)(intptr_t)data[r];
     P.sig[r] = (void*)(intptr_t)sig[r];
   }
+  TORCH_CHECK(!wide || two_shot, "the wide grid is a two-shot form");
   kgc::launch_allreduce(dt_code(inout), P, (int)nr, (int)rank, inout.data_ptr(), bytes / 16,
-                        cap_bytes / 16, two_shot, stream());
+                        cap_bytes / 16, two_shot, wide, stream());
 }
 
 // ---- C7 expert-parallel all-to-all over IPC peer memory
@@ -923,7 +924,7 @@ void xgmi_allreduce_emu(int64_t kind, std::vector<Tensor> a, std::vector<Tensor>
   const int64_t nr = (int64_t)data.size();
   TORCH_CHECK(nr == 2 || nr == 4 || nr == 8, "emulation: 2, 4 or 8 ranks");
   TORCH_CHECK((int64_t)sig.size() == nr && (int64_t)a.size() == nr, "one buffer per rank");
-  TORCH_CHECK(kind >= 0 && kind <= 3, "kind 0..3");
+  TORCH_CHECK(kind >= 0 && kind <= 4, "kind 0..4");
   const Tensor& x0 = a[0];
   check_gpu(x0, "a[0]");
   c10::hip::HIPGuardMasqueradingAsCUDA g(x0.device());
@@ -934,7 +935,7 @@ void xgmi_allreduce_emu(int64_t kind, std::vector<Tensor> a, std::vector<Tensor>
   kgc::ArWorld W{};
   int M = 0, H = 0;
   const void* wp = nullptr;
-  if (kind >= 2) {
+  if (kind == 2 || kind == 3) {
     TORCH_CHECK(x0.dim() == 2 && (int64_t)b.size() == nr && (int64_t)c.size() == nr &&
                 w.has_value(), "fused: a (in), b (out), c (residual) [M, H] per rank, w [H]");
     M = (int)x0.size(0);
@@ -949,7 +950,7 @@ void xgmi_allreduce_emu(int64_t kind, std::vector<Tensor> a, std::vector<Tensor>
     TORCH_CHECK(a[r].is_contiguous() && a[r].sizes() == x0.sizes() &&
                 a[r].scalar_type() == x0.scalar_type() && a[r].device() == x0.device(), "a[r]");
     W.a[r] = a[r].data_ptr();
-    if (kind >= 2) {
+    if (kind == 2 || kind == 3) {
       TORCH_CHECK(b[r].is_contiguous() && b[r].sizes() == x0.sizes() &&
                   c[r].is_contiguous() && c[r].sizes() == x0.sizes() &&
                   b[r].scalar_type() == x0.scalar_type() && c[r].scalar_type() == x0.scalar_type(),
@@ -1119,7 +1120,7 @@ TORCH_LIBRARY(kgc, m) {
         &ar_raise_peer_flags);
   m.def("ar_err_copy_async(int sig, Tensor(a!) host_out) -> ()", &ar_err_copy_async);
   m.def("xgmi_allreduce(Tensor(a!) inout, int[] data, int[] sig, int rank, int cap_bytes, "
-        "bool two_shot) -> ()");
+        "bool two_shot, bool wide=False) -> ()");
   m.def("xgmi_allreduce_rms(Tensor(a!) out, Tensor inp, Tensor(b!) residual, Tensor w, float eps, "
         "int[] data, int[] sig, int rank, int cap_bytes, bool two_shot=False) -> ()");
   m.def("xgmi_allreduce_emu(int kind, Tensor(a!)[] a, Tensor(b!)[] b, Tensor(c!)[] c, Tensor? w, "

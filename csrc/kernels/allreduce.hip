@@ -36,6 +36,8 @@ constexpr int AR_MAX_BLOCKS = 64;    // one-shot / two-shot / one-shot fused gri
 constexpr int AR2_BLOCKS = 128;      // row-segmented two-shot fused grid (2 rows per block at
                                      // M = 256; 4 ranks' grids must fit one GPU in the tests)
 constexpr int AR_THREADS = 512;
+constexpr int AR3_BLOCKS = 256;      // the WIDE plain two-shot grid (large decode messages:
+                                     // 4x the loads in flight of the 64-block grid)
 
 struct ArSignal {
   uint32_t counter[AR_MAX_BLOCKS];                     // local: last epoch per block
@@ -45,6 +47,9 @@ struct ArSignal {
   // the row-segmented two-shot fused kernel's own epochs and flags (its grid differs)
   uint32_t counter2[AR2_BLOCKS];
   uint32_t flag2[2][AR2_BLOCKS][AR_MAX_RANKS];
+  // the wide plain two-shot kernel's own epochs and flags (its grid differs again)
+  uint32_t counter3[AR3_BLOCKS];
+  uint32_t flag3[2][AR3_BLOCKS][AR_MAX_RANKS];
 };
 
 size_t allreduce_signal_bytes() { return (sizeof(ArSignal) + 4095) & ~size_t(4095); }
@@ -56,24 +61,29 @@ __device__ __forceinline__ uint32_t ar_load_flag(uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Flag set of one grid geometry: the plain / one-shot fused kernels (AR_MAX_BLOCKS) or the
-// row-segmented fused kernel (AR2_BLOCKS) -- counter[blk] and flag[phase][blk][rank].
-template <bool TWO_FUSED>
+// Flag set of one grid geometry (SET): 0 the plain / one-shot fused kernels
+// (AR_MAX_BLOCKS), 1 the row-segmented fused kernel (AR2_BLOCKS), 2 the wide plain
+// two-shot kernel (AR3_BLOCKS) -- counter[blk] and flag[phase][blk][rank] of each.
+template <int SET>
 __device__ __forceinline__ uint32_t* ar_counter(ArSignal* s, int blk) {
-  if constexpr (TWO_FUSED) return &s->counter2[blk];
+  if constexpr (SET == 1) return &s->counter2[blk];
+  else if constexpr (SET == 2) return &s->counter3[blk];
   else return &s->counter[blk];
 }
-template <bool TWO_FUSED>
+template <int SET>
 __device__ __forceinline__ uint32_t* ar_flag(ArSignal* s, int phase, int blk, int r) {
-  if constexpr (TWO_FUSED) return &s->flag2[phase][blk][r];
+  if constexpr (SET == 1) return &s->flag2[phase][blk][r];
+  else if constexpr (SET == 2) return &s->flag3[phase][blk][r];
   else return &s->flag[phase][blk][r];
 }
+template <int SET>
+constexpr int ar_grid() { return SET == 1 ? AR2_BLOCKS : SET == 2 ? AR3_BLOCKS : AR_MAX_BLOCKS; }
 
 // Publish this block's writes to every peer, then wait for block `blk` of every peer.
 // `blk` is the block's index within ITS RANK's grid: blockIdx.x on a real rank, the
 // position inside the rank's slice of the grid in world emulation (all ranks' blocks in
 // one launch on one device, see launch_allreduce_emu).
-template <int NR, bool TWO_FUSED = false>
+template <int NR, int SET = 0>
 __device__ __forceinline__ void ar_barrier(const ArPtrs& P, int rank, int blk, int phase,
                                            uint32_t epoch) {
   // every wave drains its own stores first (vmcnt is per wave; do not rely on the
@@ -84,9 +94,9 @@ __device__ __forceinline__ void ar_barrier(const ArPtrs& P, int rank, int blk, i
     __threadfence_system();   // release: copy-in / reduced data visible system-wide
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     ArSignal* peer = reinterpret_cast<ArSignal*>(P.sig[threadIdx.x]);
-    ar_store_flag(ar_flag<TWO_FUSED>(peer, phase, blk, rank), epoch);
+    ar_store_flag(ar_flag<SET>(peer, phase, blk, rank), epoch);
     ArSignal* self = reinterpret_cast<ArSignal*>(P.sig[rank]);
-    uint32_t* f = ar_flag<TWO_FUSED>(self, phase, blk, threadIdx.x);
+    uint32_t* f = ar_flag<SET>(self, phase, blk, threadIdx.x);
     const unsigned long long dl = spin_deadline(KGC_PEER_SPIN_MS);
     // a group that already failed (sticky err) does not wait again: one time-out per
     // dead peer, not one per collective (graph warm-ups run dozens back to back)
@@ -114,28 +124,31 @@ __device__ __forceinline__ u32x4 ld_peer(const void* p) {
 }
 
 // this rank's next epoch for block blk (read by thread 0, shared through LDS)
-template <bool TWO_FUSED>
+template <int SET>
 __device__ __forceinline__ uint32_t ar_epoch(const ArPtrs& P, int rank, int blk) {
   __shared__ uint32_t s_epoch;
   if (threadIdx.x == 0)
-    s_epoch = *ar_counter<TWO_FUSED>(reinterpret_cast<ArSignal*>(P.sig[rank]), blk) + 1;
+    s_epoch = *ar_counter<SET>(reinterpret_cast<ArSignal*>(P.sig[rank]), blk) + 1;
   __syncthreads();
   return s_epoch;
 }
 
-// ---- plain all-reduce body: block `blk` of rank `rank` (NB blocks per rank)
-template <typename T, int NR, bool TWO>
+// ---- plain all-reduce body: block `blk` of rank `rank` (ar_grid<SET>() blocks per rank;
+// SET 0 the 64-block grid of both forms, SET 2 the wide two-shot grid with its own epochs,
+// flags and data regions -- element v -> block (v / AR_THREADS) % grid must be the same in
+// every call of a set, so the two grids never share them)
+template <typename T, int NR, bool TWO, int SET = 0>
 __device__ __forceinline__ void allreduce_body(const ArPtrs& P, int rank, int blk, T* inout,
                                                int64_t nvec, int64_t cap_vec) {
-  const uint32_t epoch = ar_epoch<false>(P, rank, blk);
+  const uint32_t epoch = ar_epoch<SET>(P, rank, blk);
   const int64_t par_off = (int64_t)(epoch & 1) * cap_vec;
   u32x4* io = reinterpret_cast<u32x4*>(inout);
   u32x4* mine = reinterpret_cast<u32x4*>(P.data[rank]) + par_off;
-  const int64_t stride = (int64_t)AR_MAX_BLOCKS * AR_THREADS;
+  const int64_t stride = (int64_t)ar_grid<SET>() * AR_THREADS;
   const int64_t first = (int64_t)blk * AR_THREADS + threadIdx.x;
 
   for (int64_t v = first; v < nvec; v += stride) mine[v] = io[v];
-  ar_barrier<NR>(P, rank, blk, 0, epoch);
+  ar_barrier<NR, SET>(P, rank, blk, 0, epoch);
 
   auto reduce_at = [&](int64_t v) {
     float acc[8];
@@ -167,20 +180,20 @@ __device__ __forceinline__ void allreduce_body(const ArPtrs& P, int rank, int bl
     const int64_t lo = (int64_t)rank * seg, hi = lo + seg;
     for (int64_t v = first; v < nvec; v += stride)
       if (v >= lo && v < hi) mine[v] = reduce_at(v);
-    ar_barrier<NR>(P, rank, blk, 1, epoch);
+    ar_barrier<NR, SET>(P, rank, blk, 1, epoch);
     for (int64_t v = first; v < nvec; v += stride) {
       const int r = (int)(v / seg);   // owner of the reduced segment holding v
       io[v] = ld_peer(reinterpret_cast<const u32x4*>(P.data[r]) + par_off + v);
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) *ar_counter<false>(reinterpret_cast<ArSignal*>(P.sig[rank]), blk) = epoch;
+  if (threadIdx.x == 0) *ar_counter<SET>(reinterpret_cast<ArSignal*>(P.sig[rank]), blk) = epoch;
 }
 
-template <typename T, int NR, bool TWO>
+template <typename T, int NR, bool TWO, int SET = 0>
 __global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArPtrs P, int rank, T* inout,
                                                                int64_t nvec, int64_t cap_vec) {
-  allreduce_body<T, NR, TWO>(P, rank, blockIdx.x, inout, nvec, cap_vec);
+  allreduce_body<T, NR, TWO, SET>(P, rank, blockIdx.x, inout, nvec, cap_vec);
 }
 
 // World emulation: every rank's blocks in ONE grid on one device, each rank with its own
@@ -191,11 +204,11 @@ __global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArPtrs P, int ran
 // the grid never deadlocks whatever its size -- which eight processes sharing one GPU
 // cannot promise (their kernels need not be co-resident at all).  A violation would show
 // as the bounded spin's error word, never a hang.
-template <typename T, int NR, bool TWO>
+template <typename T, int NR, bool TWO, int SET = 0>
 __global__ __launch_bounds__(AR_THREADS) void allreduce_emu_kernel(ArPtrs P, ArWorld W,
                                                                    int64_t nvec, int64_t cap_vec) {
   const int rank = blockIdx.x % NR, blk = blockIdx.x / NR;
-  allreduce_body<T, NR, TWO>(P, rank, blk, reinterpret_cast<T*>(W.a[rank]), nvec, cap_vec);
+  allreduce_body<T, NR, TWO, SET>(P, rank, blk, reinterpret_cast<T*>(W.a[rank]), nvec, cap_vec);
 }
 
 // ---- fused one-shot all-reduce + residual add + RMSNorm (row-parallel o / down
@@ -271,7 +284,7 @@ __device__ __forceinline__ void allreduce_rms_body(const ArPtrs& P, int rank, in
                                                    const T* __restrict__ w, int M, int H,
                                                    float eps, int64_t cap_vec) {
   __shared__ float scratch[AR_THREADS / 64];
-  const uint32_t epoch = ar_epoch<false>(P, rank, blk);
+  const uint32_t epoch = ar_epoch<0>(P, rank, blk);
   const int64_t par_off = (int64_t)(epoch & 1) * cap_vec;
   const int nv = H >> 3;                             // 16-byte vectors per row
   const u32x4* src = reinterpret_cast<const u32x4*>(in);
@@ -298,7 +311,7 @@ __device__ __forceinline__ void allreduce_rms_body(const ArPtrs& P, int rank, in
     ar_add_norm_row<T>(h, wv, residual, out, row, nv, H, eps, scratch);
   }
   __syncthreads();
-  if (threadIdx.x == 0) *ar_counter<false>(reinterpret_cast<ArSignal*>(P.sig[rank]), blk) = epoch;
+  if (threadIdx.x == 0) *ar_counter<0>(reinterpret_cast<ArSignal*>(P.sig[rank]), blk) = epoch;
 }
 
 template <typename T, int NR>
@@ -340,7 +353,7 @@ __device__ __forceinline__ void allreduce_rms2_body(const ArPtrs& P, int rank, i
                                                     const T* __restrict__ w, int M, int H,
                                                     float eps, int64_t cap_vec) {
   __shared__ float scratch[AR_THREADS / 64];
-  const uint32_t epoch = ar_epoch<true>(P, rank, blk);
+  const uint32_t epoch = ar_epoch<1>(P, rank, blk);
   const int64_t par_off = (int64_t)(epoch & 1) * cap_vec;
   const int nv = H >> 3;
   const u32x4* src = reinterpret_cast<const u32x4*>(in);
@@ -349,7 +362,7 @@ __device__ __forceinline__ void allreduce_rms2_body(const ArPtrs& P, int rank, i
   for (int row = blk; row < M; row += AR2_BLOCKS)
     for (int v = threadIdx.x; v < nv; v += AR_THREADS)
       mine[(int64_t)row * nv + v] = src[(int64_t)row * nv + v];
-  ar_barrier<NR, true>(P, rank, blk, 0, epoch);
+  ar_barrier<NR, 1>(P, rank, blk, 0, epoch);
   auto owner = [](int row) { return (row + row / AR2_BLOCKS) % NR; };
   for (int row = blk; row < M; row += AR2_BLOCKS) {
     if (owner(row) != rank) continue;
@@ -359,7 +372,7 @@ __device__ __forceinline__ void allreduce_rms2_body(const ArPtrs& P, int rank, i
       mine[e] = s;
     }
   }
-  ar_barrier<NR, true>(P, rank, blk, 1, epoch);
+  ar_barrier<NR, 1>(P, rank, blk, 1, epoch);
   Pack8<T> wv[ARN_MAXV];
 #pragma unroll
   for (int i = 0; i < ARN_MAXV; ++i) {
@@ -377,7 +390,7 @@ __device__ __forceinline__ void allreduce_rms2_body(const ArPtrs& P, int rank, i
     ar_add_norm_row<T>(h, wv, residual, out, row, nv, H, eps, scratch);
   }
   __syncthreads();
-  if (threadIdx.x == 0) *ar_counter<true>(reinterpret_cast<ArSignal*>(P.sig[rank]), blk) = epoch;
+  if (threadIdx.x == 0) *ar_counter<1>(reinterpret_cast<ArSignal*>(P.sig[rank]), blk) = epoch;
 }
 
 template <typename T, int NR>
@@ -432,9 +445,12 @@ void launch_allreduce_rms(int dtype, const ArPtrs& P, int nranks, int rank, cons
 
 template <typename T>
 static void ar_by_ranks(int nranks, const ArPtrs& P, int rank, void* inout, int64_t nvec,
-                        int64_t cap_vec, bool two, hipStream_t s) {
+                        int64_t cap_vec, bool two, bool wide, hipStream_t s) {
 #define KGC_AR(NR_)                                                                          \
-  if (two)                                                                                   \
+  if (two && wide)                                                                           \
+    allreduce_kernel<T, NR_, true, 2><<<AR3_BLOCKS, AR_THREADS, 0, s>>>(P, rank, (T*)inout,  \
+                                                                        nvec, cap_vec);      \
+  else if (two)                                                                              \
     allreduce_kernel<T, NR_, true><<<AR_MAX_BLOCKS, AR_THREADS, 0, s>>>(P, rank, (T*)inout,  \
                                                                         nvec, cap_vec);      \
   else                                                                                       \
@@ -449,11 +465,11 @@ int peer_spin_ms() { return KGC_PEER_SPIN_MS; }
 int coop_spin_ms() { return KGC_COOP_SPIN_MS; }
 
 void launch_allreduce(int dtype, const ArPtrs& P, int nranks, int rank, void* inout,
-                      int64_t nvec, int64_t cap_vec, bool two_shot, hipStream_t s) {
+                      int64_t nvec, int64_t cap_vec, bool two_shot, bool wide, hipStream_t s) {
   if (dtype == DT_BF16)
-    ar_by_ranks<bf16>(nranks, P, rank, inout, nvec, cap_vec, two_shot, s);
+    ar_by_ranks<bf16>(nranks, P, rank, inout, nvec, cap_vec, two_shot, wide, s);
   else
-    ar_by_ranks<f16>(nranks, P, rank, inout, nvec, cap_vec, two_shot, s);
+    ar_by_ranks<f16>(nranks, P, rank, inout, nvec, cap_vec, two_shot, wide, s);
 }
 
 // ---- world emulation launches (tests): kind 0 plain one-shot, 1 plain two-shot,
@@ -462,7 +478,7 @@ void launch_allreduce(int dtype, const ArPtrs& P, int nranks, int rank, void* in
 template <typename T>
 static void ar_emu_t(int kind, const ArPtrs& P, const ArWorld& W, int nranks, int64_t nvec,
                      const void* w, int M, int H, float eps, int64_t cap_vec, hipStream_t s) {
-  const int g1 = nranks * AR_MAX_BLOCKS, g2 = nranks * AR2_BLOCKS;
+  const int g1 = nranks * AR_MAX_BLOCKS, g2 = nranks * AR2_BLOCKS, g3 = nranks * AR3_BLOCKS;
 #define KGC_EMU(NR_)                                                                           \
   switch (kind) {                                                                              \
     case 0: allreduce_emu_kernel<T, NR_, false><<<g1, AR_THREADS, 0, s>>>(P, W, nvec, cap_vec); \
@@ -471,6 +487,8 @@ static void ar_emu_t(int kind, const ArPtrs& P, const ArWorld& W, int nranks, in
       break;                                                                                   \
     case 2: allreduce_rms_emu_kernel<T, NR_><<<g1, AR_THREADS, 0, s>>>(P, W, (const T*)w, M, H, \
                                                                        eps, cap_vec);          \
+      break;                                                                                   \
+    case 4: allreduce_emu_kernel<T, NR_, true, 2><<<g3, AR_THREADS, 0, s>>>(P, W, nvec, cap_vec); \
       break;                                                                                   \
     default: allreduce_rms2_emu_kernel<T, NR_><<<g2, AR_THREADS, 0, s>>>(P, W, (const T*)w, M,  \
                                                                          H, eps, cap_vec);     \
@@ -503,6 +521,10 @@ __global__ __launch_bounds__(256) void ar_raise_peer_flags_kernel(ArSignal* s, i
   for (int i = threadIdx.x; i < 2 * AR2_BLOCKS * AR_MAX_RANKS; i += blockDim.x) {
     const int r = i % AR_MAX_RANKS;
     if (r != rank && r < nranks) (&s->flag2[0][0][0])[i] = value;
+  }
+  for (int i = threadIdx.x; i < 2 * AR3_BLOCKS * AR_MAX_RANKS; i += blockDim.x) {
+    const int r = i % AR_MAX_RANKS;
+    if (r != rank && r < nranks) (&s->flag3[0][0][0])[i] = value;
   }
 }
 

@@ -165,8 +165,10 @@ int allreduce_max_blocks();
 int peer_spin_ms();
 int coop_spin_ms();
 int64_t wall_clock_rate_khz();
+// wide: the two-shot form on its 256-block grid (its own epochs / flags; P.data: its own
+// regions), else the 64-block grid of both forms
 void launch_allreduce(int dtype, const ArPtrs& P, int nranks, int rank, void* inout,
-                      int64_t nvec, int64_t cap_vec, bool two_shot, hipStream_t s);
+                      int64_t nvec, int64_t cap_vec, bool two_shot, bool wide, hipStream_t s);
 // fused all-reduce + residual add + RMSNorm over [M, H] rows (P.data: the fused regions
 // of the chosen form); H % 8 == 0 and H <= allreduce_rms_max_hidden().  two_shot: the
 // row-segmented two-shot kernel (its own regions), else one-shot

@@ -605,9 +605,11 @@ def _tune_dgemm(ws, N: int, K: int, ms, margin: float, reps: int, res: dict,
                 kind: str, qkv_dims=None) -> None:
     """hipBLASLt vs the K9m candidates at each M in ``ms``, over all weights of the shape
     (HBM-resident, as in a decode step), each side timed WITH its consumer: "silu" the
-    SiLU-and-mul, "tail" the residual add + RMSNorm, "qkv" the RoPE / KV-write kernel
-    (which sums the K-slices itself), "plain" the split-K reduction."""
-    from . import _k, fused_add_rms_norm, rope_kv_write, silu_mul
+    SiLU-and-mul, "tail" the residual add + RMSNorm, "qkv" the fused RoPE / KV-write /
+    decode-attention kernel (which sums the K-slices in its prologue), "plain" the split-K
+    reduction."""
+    from . import (_k, decode_partials, fused_add_rms_norm, paged_attention_decode_rope,
+                   silu_mul)
     packed = all(packed_weight(w, kind == "silu") is not None for w in ws)
     for M in sorted(set(ms)):
         if not dgemm_ok(M, N, K) or (kind == "tail" and N > 8192):
@@ -618,16 +620,23 @@ def _tune_dgemm(ws, N: int, K: int, ms, margin: float, reps: int, res: dict,
         gamma = torch.ones(N, dtype=dt, device=dev) if kind == "tail" else None
         act = torch.empty(M, N // 2, dtype=dt, device=dev) if kind == "silu" else None
         if kind == "qkv":
-            # the RoPE / KV-write consumer on a scratch cache (every token to block 1)
+            # the decode step's real consumer: the fused RoPE / KV-write / attention kernel,
+            # whose prologue sums the K-slices -- over a one-token context per row, so what
+            # it adds per split factor is that prologue, not the attention itself (the
+            # earlier rope_kv_write stand-in read the slices differently)
             nq, nkv, hd = qkv_dims
             pos = torch.zeros(M, dtype=torch.int64, device=dev)
-            slots = torch.arange(M, dtype=torch.int64, device=dev) % 32 + 32
+            slots = (torch.arange(M, dtype=torch.int64, device=dev) + 1) * 32
             cs = torch.zeros(1, hd, dtype=torch.float32, device=dev)
-            kc = torch.zeros(2, nkv, 32, hd, dtype=dt, device=dev)
-            vc = torch.zeros(2, nkv, 4, hd, 8, dtype=dt, device=dev)
+            kc = torch.zeros(M + 1, nkv, 32, hd, dtype=dt, device=dev)
+            vc = torch.zeros(M + 1, nkv, 4, hd, 8, dtype=dt, device=dev)
+            bt = (torch.arange(M, dtype=torch.int32, device=dev) + 1).view(M, 1)
+            cl = torch.ones(M, dtype=torch.int32, device=dev)
+            wsp = decode_partials(M, nq, hd, 1, 32, dev)
 
             def consume(y):
-                rope_kv_write(y, pos, cs, kc, vc, slots, nq, nkv, hd, dtype=dt)
+                paged_attention_decode_rope(y, pos, cs, kc, vc, slots, nq, nkv, hd, bt, cl,
+                                            hd ** -0.5, workspace=wsp, grid_z=1, dtype=dt)
 
         def lib():
             for w in ws:

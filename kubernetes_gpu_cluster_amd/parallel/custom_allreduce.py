@@ -60,9 +60,10 @@ class CustomAllReduce:
             with torch.cuda.device(device):
                 sig_bytes = int(k.ar_signal_bytes())
                 # [signal | all-reduce parity 0 | parity 1 | fused one-shot parity 0 | 1 |
-                #  fused two-shot parity 0 | 1]: each kernel form has its own regions (their
-                #  row -> workgroup maps differ, see allreduce.hip)
-                self._own = int(k.ar_alloc(sig_bytes + 6 * self.cap))
+                #  fused two-shot parity 0 | 1 | wide two-shot parity 0 | 1]: each kernel
+                #  grid has its own regions (their element -> workgroup maps differ, see
+                #  allreduce.hip)
+                self._own = int(k.ar_alloc(sig_bytes + 8 * self.cap))
                 handle = k.ar_get_handle(self._own).tolist()
         except Exception as e:  # noqa: BLE001
             err = e
@@ -109,6 +110,7 @@ class CustomAllReduce:
         # 37.1 us for two-shot + fused_add_rms_norm, world 4 72.1 vs 56.3 us.  (One GPU
         # shares its HBM and CUs between the ranks; on an xGMI node re-measure and set
         # KGC_AR_RMS2_MAX.)
+        self.wide_min = int(os.environ.get("KGC_AR_WIDE_MIN", 1 << 62))
         self.fused_max = int(os.environ.get("KGC_AR_RMS_MAX", self.one_shot_max))
         self.fused2_max = int(os.environ.get("KGC_AR_RMS2_MAX", self.cap if world <= 2 else 0))
         self.fused_calls = 0        # host-side launches (a graph capture counts once)
@@ -124,6 +126,7 @@ class CustomAllReduce:
         self.data = [b + sig_bytes for b in bases]
         self.fdata = [b + sig_bytes + 2 * self.cap for b in bases]
         self.fdata2 = [b + sig_bytes + 4 * self.cap for b in bases]
+        self.wdata = [b + sig_bytes + 6 * self.cap for b in bases]
         self.max_hidden = int(torch.ops.kgc.allreduce_rms_max_hidden())
 
     # ------------------------------------------------------------------ policy
@@ -138,13 +141,17 @@ class CustomAllReduce:
         return None
 
     def plain_form(self, nb: int) -> str:
-        """'one' | 'two' | 'rccl' for a plain all-reduce of nb bytes."""
+        """'one' | 'two' | 'two_wide' | 'rccl' for a plain all-reduce of nb bytes
+        ('two_wide': the two-shot form on its 256-workgroup grid; the thresholds, without a
+        calibration table, pick it from KGC_AR_WIDE_MIN bytes up -- default never)."""
         e = self._entry(nb)
         if e is not None:
             return e[1]
         if nb > self.cap:
             return "rccl"
-        return "two" if nb > self.one_shot_max else "one"
+        if nb > self.one_shot_max:
+            return "two_wide" if nb >= self.wide_min else "two"
+        return "one"
 
     def fused_form(self, nb: int) -> str:
         """'fused1' | 'fused2' | 'split' (the plain form, then fused_add_rms_norm)."""
@@ -166,10 +173,15 @@ class CustomAllReduce:
 
     def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
         nb = x.numel() * x.element_size()
-        two = self.plain_form(nb) == "two"
-        self.launches["two" if two else "one"] += 1
-        torch.ops.kgc.xgmi_allreduce(x, self.data, self.sig, self.rank, self.cap, two)
+        form = self.plain_form(nb)
+        self._launch_plain(x, form)
+        self.launches[form] += 1
         return x
+
+    def _launch_plain(self, x: torch.Tensor, form: str) -> None:
+        wide = form == "two_wide"
+        torch.ops.kgc.xgmi_allreduce(x, self.wdata if wide else self.data, self.sig, self.rank,
+                                     self.cap, form != "one", wide)
 
     def can_fuse(self, x: torch.Tensor) -> bool:
         if not x.is_cuda or x.dtype not in (torch.bfloat16, torch.float16) or x.dim() != 2:
@@ -203,14 +215,16 @@ class CustomAllReduce:
         one-GPU rehearsal).  Collective over the TP group: every rank runs the same
         launches in the same order (the kernels wait for their peers), the per-rank times
         are MAX-reduced, so every rank derives the same table.  Forms:
-          plain  'one' / 'two' (xGMI one- / two-shot) / 'rccl' (the process group);
+          plain  'one' / 'two' (xGMI one- / two-shot, 64 workgroups) / 'two_wide' (two-shot
+                 on 256 workgroups: the grid sized for large messages) / 'rccl';
           fused  'fused1' / 'fused2' (one launch with the residual add + RMSNorm) /
                  'split' (the plain choice, then fused_add_rms_norm).
         The thresholds stay the fallback past the largest calibrated size."""
         from .. import ops
         dev = self.device
         res = {"hidden": hidden, "rows": [], "bytes": [], "us": {}}
-        forms = ("one", "two", "rccl", "fused1", "fused2", "split")
+        forms = ("one", "two", "two_wide", "rccl", "fused1", "fused2", "split")
+        plain_forms = forms[:4]
         times = []
         w = torch.ones(hidden, dtype=dtype, device=dev)
         saved = self.table
@@ -224,9 +238,8 @@ class CustomAllReduce:
             ok_f = nb <= self.cap and hidden % 8 == 0 and hidden <= self.max_hidden
 
             def run(form, x=x, out=out, resid=resid, nb=nb):
-                if form in ("one", "two"):
-                    torch.ops.kgc.xgmi_allreduce(x, self.data, self.sig, self.rank, self.cap,
-                                                 form == "two")
+                if form in ("one", "two", "two_wide"):
+                    self._launch_plain(x, form)
                 elif form == "rccl":
                     if dist.get_backend(tp_group) == dist.Backend.GLOO:
                         xf = x.float()              # gloo: the fp32 path comm.py takes
@@ -241,8 +254,8 @@ class CustomAllReduce:
                                                      self.cap, form == "fused2")
             row = []
             for form in forms:
-                if (form in ("one", "two") and not ok_x) or (form in ("fused1", "fused2")
-                                                            and not ok_f) or form == "split":
+                if (form in ("one", "two", "two_wide") and not ok_x) or (
+                        form in ("fused1", "fused2") and not ok_f) or form == "split":
                     row.append(float("inf"))
                     continue
                 torch.cuda.synchronize(dev)
@@ -267,7 +280,7 @@ class CustomAllReduce:
                 ops.fused_add_rms_norm(x, resid, w, 1e-6)
             e1.record()
             e1.synchronize()
-            row[forms.index("split")] = min(row[:3]) + e0.elapsed_time(e1) * 1e3 / reps
+            row[forms.index("split")] = min(row[:len(plain_forms)]) + e0.elapsed_time(e1) * 1e3 / reps
             times.append(row)
             res["rows"].append(m)
             res["bytes"].append(nb)
@@ -277,7 +290,7 @@ class CustomAllReduce:
         table = []
         for i, nb in enumerate(res["bytes"]):
             tr = t[i].tolist()
-            plain = min(("one", "two", "rccl"), key=lambda f: tr[forms.index(f)])
+            plain = min(plain_forms, key=lambda f: tr[forms.index(f)])
             fused = min(("fused1", "fused2", "split"), key=lambda f: tr[forms.index(f)])
             table.append((nb, plain, fused))
             for f in forms:
@@ -349,7 +362,7 @@ class PhantomAllReduce(CustomAllReduce):
         self._err_host = None
         with torch.cuda.device(device):
             sig_bytes = int(k.ar_signal_bytes())
-            bases = [int(k.ar_alloc(sig_bytes + 6 * self.cap)) for _ in range(world)]
+            bases = [int(k.ar_alloc(sig_bytes + 8 * self.cap)) for _ in range(world)]
             k.ar_raise_peer_flags(bases[rank], rank, world, self.FLAG_VALUE)
             torch.cuda.synchronize(device)
         self._own, self._opened = bases[rank], []

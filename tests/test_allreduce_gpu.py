@@ -251,16 +251,19 @@ def test_xgmi_world_emulation(world, gpu):
     dev = gpu
     cap = 4 << 20
     sig_b = int(k.ar_signal_bytes())
-    bases = [int(k.ar_alloc(sig_b + 6 * cap)) for _ in range(world)]
+    bases = [int(k.ar_alloc(sig_b + 8 * cap)) for _ in range(world)]
     try:
         sig = bases
         regions = {0: [b + sig_b for b in bases], 1: [b + sig_b for b in bases],
-                   2: [b + sig_b + 2 * cap for b in bases], 3: [b + sig_b + 4 * cap for b in bases]}
+                   2: [b + sig_b + 2 * cap for b in bases], 3: [b + sig_b + 4 * cap for b in bases],
+                   4: [b + sig_b + 6 * cap for b in bases]}
         seed = 0
         for it in range(3):
             for dtype in (torch.bfloat16, torch.float16):
                 # plain one-shot / two-shot: exact integers (any order sums exactly)
-                for kind, n in ((0, 64 * 1024), (1, 1024 * 1024), (0, 8 * world), (1, 16 * world)):
+                # (kind 4: the wide two-shot grid, its own epochs / flags / regions)
+                for kind, n in ((0, 64 * 1024), (1, 1024 * 1024), (0, 8 * world), (1, 16 * world),
+                                (4, 1024 * 1024), (4, 16 * world), (4, 8 * 4096 * 8 + 8 * world)):
                     seed += 1
                     xs = [_inputs(r, n, seed, dtype, True).to(dev) for r in range(world)]
                     k.xgmi_allreduce_emu(kind, xs, [], [], None, regions[kind], sig, cap, 1e-5)
@@ -348,12 +351,15 @@ def test_phantom_rank_runs_every_form_without_waiting(world, gpu):
             car.all_reduce(y)
             assert torch.equal(y, small)
             big = torch.randint(-8, 9, (256, 4096), generator=g).to(torch.bfloat16).to(dev)
-            y = big.clone()
-            car.all_reduce(y)                      # 2 MB > one-shot max: two-shot
             flat, seg = big.view(-1), big.numel() // world
             exp = torch.zeros_like(flat)
             exp[:seg] = flat[:seg]
-            assert torch.equal(y.view(-1), exp)
+            for wide in (False, True):             # 2 MB > one-shot max: two-shot
+                car.wide_min = 0 if wide else 1 << 62
+                y = big.clone()
+                car.all_reduce(y)
+                assert torch.equal(y.view(-1), exp), wide
+            assert car.launches["two_wide"] > 0 and car.launches["two"] > 0
             for rows in (16, 256):                 # 128 KB fused one-shot, 2 MB two-shot
                 x = torch.randint(-8, 9, (rows, 4096), generator=g).to(torch.bfloat16).to(dev)
                 res = torch.randint(-8, 9, (rows, 4096), generator=g).to(torch.bfloat16).to(dev)

@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--ragged", type=float, default=0.25,
                     help="context lengths uniform in [ctx*(1-r), ctx] (0: all equal, as in bench.py)")
     ap.add_argument("--z", type=int, default=0, help="force the z-split (0: engine heuristic)")
+    ap.add_argument("--copies", type=int, default=0,
+                    help="KV copies cycled per call (0: enough for 1.5 GB, past the Infinity Cache)")
     ap.add_argument("--rope", type=int, default=-1,
                     help=">= 0: also time rope_kv_write + decode vs the fused decode kernel "
                          "(0: bf16 QKV, S > 0: S fp32 split-K slices)")
@@ -52,13 +54,21 @@ def main():
     dev = torch.device("cuda")
     B, d, bs = a.batch, a.d, a.bs
     nblk = math.ceil(a.ctx / bs)
-    NB = B * nblk + 16
+    NB1 = B * nblk + 16
+    # L "layers": disjoint copies of the KV blocks, one per call in turn, so the timed
+    # calls stream from HBM as a decode step's layers do -- one copy of a small shape
+    # (e.g. 84 MB at B = 256, one kv head) stays in the 256 MB Infinity Cache between
+    # back-to-back calls and times the cache, not HBM
+    per_copy = NB1 * a.nkv * bs * d * 2 * 2
+    L = a.copies or max(1, math.ceil((1536 << 20) / per_copy))
+    NB = NB1 * L
     kc = torch.randn(NB, a.nkv, bs, d, device=dev, dtype=torch.bfloat16)
     vc = torch.randn(NB, a.nkv, bs // 8, d, 8, device=dev, dtype=torch.bfloat16)
     maxb = math.ceil(a.max_len / bs)
-    perm = torch.randperm(NB - 1, device=dev)[: B * nblk] + 1
+    perm = torch.randperm(NB1 - 1, device=dev)[: B * nblk] + 1
     bt = torch.zeros(B, maxb, dtype=torch.int32, device=dev)
     bt[:, :nblk] = perm.view(B, nblk).int()
+    bts = [torch.where(bt > 0, bt + l * NB1, bt).contiguous() for l in range(L)]
     # ragged contexts around --ctx (uniform +-25%)
     ctx = (a.ctx * (1 - a.ragged + a.ragged * torch.rand(B, device=dev))).int().clamp(1, nblk * bs)
     q = torch.randn(B, a.nq, d, device=dev, dtype=torch.bfloat16)
@@ -69,11 +79,18 @@ def main():
     n = min(B, 8)
     ref = R.paged_attention_decode(q[:n].float(), kc.float(), vc.float(), bt[:n], ctx[:n], d ** -0.5)
     err = (out[:n].float() - ref).abs().max().item()
-    t = timeit(lambda: ops.paged_attention_decode(q, kc, vc, bt, ctx, d ** -0.5, ws, z))
+    it = [0]
+
+    def layer_bt():
+        it[0] += 1
+        return bts[it[0] % L]
+    t = timeit(lambda: ops.paged_attention_decode(q, kc, vc, layer_bt(), ctx, d ** -0.5, ws, z),
+               iters=max(30, 2 * L))
     kv_bytes = int(ctx.sum()) * a.nkv * d * 2 * 2
     print(json.dumps({"kernel": "paged_decode", "batch": B, "ctx_mean": float(ctx.float().mean()),
                       "z": z, "max_err": round(err, 4), "us": round(t * 1e6, 2), "kv_TBps": round(kv_bytes / t / 1e12, 3),
-                      "variant": os.environ.get("KGC_DEC_VARIANT", "0")}))
+                      "kv_copies": L, "min_chunks": os.environ.get("KGC_DECODE_MIN_CHUNKS"),
+                      "nq": a.nq, "nkv": a.nkv}))
     if a.rope >= 0:
         # rope_kv_write + paged_decode vs the fused decode kernel, the QKV projection
         # handed over as bf16 (--rope 0) or as S K9m split-K slices (--rope S)
@@ -87,16 +104,19 @@ def main():
         cs = R.rope_cos_sin_cache(d, a.max_len, 5e5).to(dev)
         nq, nkv = a.nq, a.nkv
 
-        def unfused():
+        def unfused(btl=None):
+            btl = bt if btl is None else btl
             qq = ops.rope_kv_write(qkv, pos, cs, kc, vc, slots, nq, nkv, d, dtype=torch.bfloat16)
-            return ops.paged_attention_decode(qq, kc, vc, bt, ctx, d ** -0.5, ws, z)
+            return ops.paged_attention_decode(qq, kc, vc, btl, ctx, d ** -0.5, ws, z)
 
-        def fused():
-            return ops.paged_attention_decode_rope(qkv, pos, cs, kc, vc, slots, nq, nkv, d, bt,
+        def fused(btl=None):
+            btl = bt if btl is None else btl
+            return ops.paged_attention_decode_rope(qkv, pos, cs, kc, vc, slots, nq, nkv, d, btl,
                                                    ctx, d ** -0.5, workspace=ws, grid_z=z,
                                                    dtype=torch.bfloat16)
         e = (unfused().float() - fused().float()).abs().max().item()
-        tu, tf = timeit(unfused), timeit(fused)
+        tu = timeit(lambda: unfused(layer_bt()), iters=max(30, 2 * L))
+        tf = timeit(lambda: fused(layer_bt()), iters=max(30, 2 * L))
         print(json.dumps({"kernel": "rope_kv + paged_decode vs paged_decode_rope", "batch": B,
                           "ctx_mean": float(ctx.float().mean()), "z": z, "S": S,
                           "unfused_us": round(tu * 1e6, 2), "fused_us": round(tf * 1e6, 2),
