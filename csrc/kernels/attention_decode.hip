@@ -44,16 +44,20 @@ constexpr int DEC_MAX_Z = 1024;  // z-slices the reduce kernel merges (host-chec
 // K1w runs where the grid has at least this many (seq, kv-head) pairs; smaller batches
 // take the 4-wave kernel (B = 1: 9.3 vs 12.3 us at ctx 640; ops/__init__.py mirrors it)
 constexpr int DEC_WAVE_MIN_PAIRS = 64;
-// ... and from this many pairs up a context of up to DEC_LONG_MIN_CHUNKS chunks is one slice
+// ... and from this many pairs up a z-slice holds at least DEC_LONG_MIN_CHUNKS chunks
+// (ops/__init__.py also aims such grids at ~4 waves per CU instead of 8): with the KV
+// streamed from HBM (tools/attn_bench.py cycles copies past the Infinity Cache), fewer,
+// longer slices won at every many-pairs shape measured -- B = 256 nq 8 / nkv 1 ctx 640:
+// 23.2 us at 2 slices of 10 chunks vs 26.9 at 7 of 3; B = 128 nq 32 / nkv 8: 65.0 vs
+// 68.8 us at one slice; B = 32 ctx 2300: 61.9 vs 66.5 (profiles/attn_decode_r5.jsonl)
 constexpr int DEC_LONG_PAIRS = 256;
-constexpr int DEC_LONG_MIN_CHUNKS = 24;
+constexpr int DEC_LONG_MIN_CHUNKS = 10;
 
 // K1w: 32-token chunks per z-slice (>= min_per, at least 2: the pipeline depth); slices
 // past the context are empty and the reduce stops at decode_used_slices.  min_per is a
 // per-launch host choice (decode_min_chunks): the graph's Z is sized for max_model_len,
-// and with many (seq, kv-head) pairs short contexts run best as ONE slice per pair (the
-// 70B TP = 8 rank at B = 256, ctx 640: 17.5 us at one slice vs 23.2 at seven of three
-// chunks + the merge, profiles/README.md "Round 5").
+// so at short contexts many-pairs grids would otherwise cut each context into slices of
+// 2-3 chunks, each paying the q prologue and a partial write for little streaming.
 __host__ __device__ __forceinline__ int decode_slice_chunks(int nchunk, int Z, int min_per) {
   const int per = (nchunk + Z - 1) / Z;
   return per < min_per ? min_per : per;
@@ -105,6 +109,56 @@ __device__ __forceinline__ void qkv_row8(const DecodeRope& rp, int64_t e, float*
   }
 }
 
+// The pair (xa at e_a, xb at e_b) of one lane's NeoX chunks in ONE round trip: with the
+// slice count a compile-time constant every slice load of both chunks is issued before the
+// first add -- 4 S loads, no clamped duplicates (qkv_row8's batches of SB re-load slice
+// S - 1 to fill a batch) -- summed in slice order from 0, bit-identical to qkv_row8.
+template <typename T, int S>
+__device__ __forceinline__ void qkv_pair8_s(const DecodeRope& rp, int64_t ea, int64_t eb,
+                                            float* xa, float* xb) {
+  const float* pa = reinterpret_cast<const float*>(rp.qkv) + ea;
+  const float* pb = reinterpret_cast<const float*>(rp.qkv) + eb;
+  f32x4 t[S][4];
+#pragma unroll
+  for (int z = 0; z < S; ++z) {
+    t[z][0] = *reinterpret_cast<const f32x4*>(pa + z * rp.slice_stride);
+    t[z][1] = *reinterpret_cast<const f32x4*>(pa + z * rp.slice_stride + 4);
+    t[z][2] = *reinterpret_cast<const f32x4*>(pb + z * rp.slice_stride);
+    t[z][3] = *reinterpret_cast<const f32x4*>(pb + z * rp.slice_stride + 4);
+  }
+  f32x4 a0 = t[0][0], a1 = t[0][1], b0 = t[0][2], b1 = t[0][3];
+#pragma unroll
+  for (int z = 1; z < S; ++z) {
+    a0 += t[z][0];
+    a1 += t[z][1];
+    b0 += t[z][2];
+    b1 += t[z][3];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    xa[q] = to_f(from_f<T>(a0[q]));
+    xa[4 + q] = to_f(from_f<T>(a1[q]));
+    xb[q] = to_f(from_f<T>(b0[q]));
+    xb[4 + q] = to_f(from_f<T>(b1[q]));
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void qkv_pair8(const DecodeRope& rp, int64_t ea, int64_t eb,
+                                          float* xa, float* xb) {
+  switch (rp.S) {        // wave-uniform: the K9m split factors the tuner picks
+    case 2: qkv_pair8_s<T, 2>(rp, ea, eb, xa, xb); return;
+    case 3: qkv_pair8_s<T, 3>(rp, ea, eb, xa, xb); return;
+    case 4: qkv_pair8_s<T, 4>(rp, ea, eb, xa, xb); return;
+    case 5: qkv_pair8_s<T, 5>(rp, ea, eb, xa, xb); return;
+    case 6: qkv_pair8_s<T, 6>(rp, ea, eb, xa, xb); return;
+    case 8: qkv_pair8_s<T, 8>(rp, ea, eb, xa, xb); return;
+    default:
+      qkv_row8<T>(rp, ea, xa);
+      qkv_row8<T>(rp, eb, xb);
+  }
+}
+
 // x * inv * w[col..col+7], rounded through T
 template <typename T>
 __device__ __forceinline__ void norm8(float* x, float inv, const void* w, int col) {
@@ -145,8 +199,8 @@ __device__ __forceinline__ void decode_kv_write(const DecodeRope& rp, int b, int
   if (lane < TPH) {
     const int c = lane;
     float xa[8], xb[8];
-    qkv_row8<T>(rp, row + (int64_t)(nq + h) * D + c * 8, xa);
-    qkv_row8<T>(rp, row + (int64_t)(nq + h) * D + half + c * 8, xb);
+    qkv_pair8<T>(rp, row + (int64_t)(nq + h) * D + c * 8, row + (int64_t)(nq + h) * D + half + c * 8,
+                 xa, xb);
     if (rp.k_norm_w) {
       float ss = 0.f;
 #pragma unroll
@@ -610,8 +664,8 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
       const int64_t col = kind == 0 ? (int64_t)(h * G + g) * D : kind == 1 ? (int64_t)(nq + h) * D
                         : (int64_t)(nq + nkv + h) * D;
       float xa[8], xb[8];
-      qkv_row8<T>(rp, row + col + c * 8, xa);
-      qkv_row8<T>(rp, row + col + (kind == 2 ? 0 : D / 2) + c * 8, xb);  // v: a dummy reload
+      qkv_pair8<T>(rp, row + col + c * 8, row + col + (kind == 2 ? 0 : D / 2) + c * 8, xa,
+                   xb);                                         // v: xb a dummy reload
       const void* nw = kind == 0 ? rp.q_norm_w : rp.k_norm_w;
       if (nw) {                    // q / k norm over the head's TPH lanes (aligned groups)
         float ss = 0.f;
@@ -685,8 +739,7 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
         const int g = i / TPH, c = i % TPH;
         const int64_t qe = (int64_t)b * rp.qkv_stride + (int64_t)(h * G + g) * D;
         float xa[8], xb[8];
-        qkv_row8<T>(rp, qe + c * 8, xa);
-        qkv_row8<T>(rp, qe + D / 2 + c * 8, xb);
+        qkv_pair8<T>(rp, qe + c * 8, qe + D / 2 + c * 8, xa, xb);
         if (rp.q_norm_w) {
           float ss = 0.f;
 #pragma unroll

@@ -169,6 +169,8 @@ DECODE_PARTITION = 64        # tokens per wave-iteration of the 4-wave decode ke
 DECODE_CHUNK = 32            # tokens per pipelined step of K1w
 DECODE_TARGET_WAVES = 2048   # K1w: 8 resident waves per CU (2 per SIMD at 256 VGPRs)
 DECODE_WAVE_MIN_PAIRS = 64   # attention_decode.hip DEC_WAVE_MIN_PAIRS
+DECODE_LONG_PAIRS = 256      # attention_decode.hip DEC_LONG_PAIRS
+DECODE_LONG_TARGET_WAVES = 1024
 PREFILL_BLOCK_M = 128
 
 
@@ -222,7 +224,11 @@ def decode_grid_z(batch: int, num_kv_heads: int, max_ctx: int, target_waves: int
     pairs = max(1, batch * num_kv_heads)
     if decode_uses_wave(batch, num_kv_heads):
         chunks = max(1, math.ceil(max_ctx / DECODE_CHUNK))
-        want = math.ceil((target_waves or DECODE_TARGET_WAVES) / pairs)
+        # from DECODE_LONG_PAIRS pairs up: ~4 waves per CU of longer slices (the kernel
+        # also keeps those slices >= 10 chunks, attention_decode.hip DEC_LONG_MIN_CHUNKS)
+        tgt = target_waves or (DECODE_LONG_TARGET_WAVES if pairs >= DECODE_LONG_PAIRS
+                               else DECODE_TARGET_WAVES)
+        want = math.ceil(tgt / pairs)
         return max(1, min(want, math.ceil(chunks / 2), 1024))
     parts = max(1, math.ceil(max_ctx / DECODE_PARTITION))
     want = math.ceil((target_waves or 4096) / (pairs * 4))
