@@ -29,6 +29,7 @@ import itertools
 import json
 import logging
 import os
+import sys
 import ssl
 import time
 from typing import Optional
@@ -382,8 +383,10 @@ def main(argv=None):
                    k8s_selector=a.k8s_label_selector, k8s_namespace=a.k8s_namespace,
                    k8s_port=a.k8s_port, dns_service=a.dns_service,
                    backend_api_key=a.backend_api_key, shared=shared)
+        # the banner goes to stderr: a launcher's stdout (bench.py's one JSON line) stays clean
         web.run_app(r.app(), host=a.host, port=a.port, reuse_port=workers > 1,
-                    print=None if workers > 1 else print)
+                    print=None if workers > 1 else
+                    (lambda *m, **k: print(*m, file=sys.stderr, flush=True)))
 
     if workers == 1:
         serve(None)

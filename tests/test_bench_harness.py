@@ -31,6 +31,9 @@ def test_bench_single_rank():
     assert r.returncode == 0, r.stderr[-2000:]
     lines = _json_lines(r.stdout)
     assert len(lines) == 1
+    # stdout is the driver's contract: that ONE line and nothing else (the router's
+    # aiohttp banner once went there too)
+    assert [l for l in r.stdout.splitlines() if l.strip()] == [r.stdout.strip()], r.stdout
     j = lines[0]
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
