@@ -580,7 +580,7 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
   // their ids are wave-uniform scalar loads (lgkmcnt), so looking them up never waits on
   // the vector loads in flight (a lane-shuffled register window did: its rare reload
   // branch made the wait-count pass drain vmcnt at every chunk).
-  auto issue = [&](Frag& f, int ci) {
+  auto issue_part = [&](Frag& f, int ci, bool dok, bool dov) {
     const int base = ci << 5;
     const int blo = base >> bs_log2, bhi = min((base + 31) >> bs_log2, last_blk);
     const int64_t plo = kgc_bt(bt, blo, bt_stride, num_blocks);
@@ -589,16 +589,21 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
     const int ta = min(base + keyA, end - 1), tb = min(base + keyA + 4, end - 1);
     const C* ka = kbase + blk_of(ta) * blk_stride + (int64_t)(ta & bsm) * D + 8 * qd;
     const C* kb = kbase + blk_of(tb) * blk_stride + (int64_t)(tb & bsm) * D + 8 * qd;
+    if (dok) {
 #pragma unroll
-    for (int s2 = 0; s2 < KS; ++s2) {
-      f.k[0][s2].u = ldf(ka + 32 * s2);
-      f.k[1][s2].u = ldf(kb + 32 * s2);
+      for (int s2 = 0; s2 < KS; ++s2) {
+        f.k[0][s2].u = ldf(ka + 32 * s2);
+        f.k[1][s2].u = ldf(kb + 32 * s2);
+      }
     }
     const int t0 = min(base + 8 * qd, end - 1) & ~7;
     const C* va = vbase + blk_of(t0) * blk_stride + ((t0 & bsm) >> 3) * (D * 8) + r16 * 8;
+    if (dov) {
 #pragma unroll
-    for (int t = 0; t < DT; ++t) f.v[t].u = ldf(va + 16 * t * 8);
+      for (int t = 0; t < DT; ++t) f.v[t].u = ldf(va + 16 * t * 8);
+    }
   };
+  auto issue = [&](Frag& f, int ci) { issue_part(f, ci, true, true); };
 
   float m_run = -INFINITY, l_run = 0.f;
   f32x4 o[DT];
@@ -644,8 +649,14 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
   Frag fa, fb;
   // FUSE: the first chunk's loads go out before the q prologue unless that chunk holds
   // the new token this wave is about to write
-  const bool prefetched = c0 < c1 && !(FUSE && c0 == nchunk - 1);
-  if (prefetched) issue(fa, c0);
+  // the slice's first chunk and the second one's keys go out before the q prologue (unless one of them holds the
+  // new token this wave is about to write): every wave of the (one-round) grid starts
+  // with its prologue, so the K / V stream must already be in flight beside the prologue's
+  // split-K slice reads (Llama-3-8B at B = 256: 31.5 MB of fp32 q/k/v slices per layer)
+  const bool pre_a = c0 < c1 && !(FUSE && c0 == nchunk - 1);
+  const bool pre_b = pre_a && !(FUSE && min(c0 + 1, c1 - 1) == nchunk - 1);
+  if (pre_a) issue(fa, c0);
+  if (pre_b) issue_part(fb, min(c0 + 1, c1 - 1), true, false);
   if constexpr (FUSE) {
     constexpr int TPH = D / 16;
     // the new token's k / v: written by the slice that reads the context's last chunk
@@ -784,7 +795,8 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
       qf[s] = t.v;
     }
   }
-  if (!prefetched && c0 < c1) issue(fa, c0);
+  if (!pre_a && c0 < c1) issue(fa, c0);
+  if (c0 < c1) issue_part(fb, min(c0 + 1, c1 - 1), !pre_b, true);
   // two-deep pipeline over named buffers (a runtime-indexed buffer pair would live in
   // scratch): while one chunk computes, the next one's loads are in flight.  The loop
   // body is straight-line -- unconditional issues (past the range they re-load the wave's
@@ -792,12 +804,13 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
   // masked (its tokens are >= end: p = 0, alpha = 1) -- because any branch between an
   // issue and its use makes the compiler's wait-count pass merge the paths and wait for
   // the younger buffer too (measured in the .s: vmcnt(15) instead of (31) before the
-  // first MFMA, i.e. the pipeline serialised).
+  // first MFMA, i.e. the pipeline serialised).  The two buffers' first chunks were issued
+  // above, so each iteration computes one buffer and refills it two chunks ahead.
   for (int ci = c0; ci < c1; ci += 2) {
-    issue(fb, min(ci + 1, c1 - 1));
     compute(fa, ci);
     issue(fa, min(ci + 2, c1 - 1));
     compute(fb, ci + 1);
+    issue(fb, min(ci + 3, c1 - 1));
   }
 
   l_run += __shfl_xor(l_run, 16, 64);
