@@ -274,18 +274,37 @@ def _note(msg: str) -> None:
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
+_port_locks: list = []
+
+
 def _free_port(local_rank: int, slot: int) -> int:
     """A free port from this rank's own range (ranks of one node never race for the
-    same number): 18000 + 64 * local_rank + slot, stepping by 1024 when busy."""
+    same number): 18000 + 64 * local_rank + slot, stepping by 1024 when busy.  The port
+    is also claimed by an flock on a per-port file held for this process's lifetime: the
+    API server binds with SO_REUSEPORT (its --api-server-count frontends share the port)
+    and loads its model before it binds, so a second bench on the same host that probed
+    the same still-unbound port would otherwise join the same port and the kernel would
+    spread each job's requests over both jobs' servers (seen as a bench whose
+    /kgc/engine_stats missed requests its client had completed)."""
+    import fcntl
     import socket
+    import tempfile
     for step in range(16):
         port = 18000 + 64 * local_rank + slot + 1024 * step
+        f = open(os.path.join(tempfile.gettempdir(), f"kgc-bench-port-{port}.lock"), "a")
+        try:
+            fcntl.flock(f, fcntl.LOCK_EX | fcntl.LOCK_NB)
+        except OSError:
+            f.close()
+            continue
         with socket.socket() as s:
             try:
                 s.bind(("127.0.0.1", port))
             except OSError:
+                f.close()
                 continue
-            return port
+        _port_locks.append(f)
+        return port
     raise RuntimeError(f"no free port for rank {local_rank}")
 
 
