@@ -208,7 +208,7 @@ void paged_decode_rope(Tensor out, Tensor qkv, Tensor positions, Tensor cos_sin,
                        std::optional<Tensor> k_norm_w, Tensor block_tables, Tensor ctx_lens,
                        Tensor max_logits, Tensor exp_sums, Tensor tmp_out, int64_t nq,
                        int64_t Z, double scale, double eps, bool use_rope, double k_scale,
-                       double v_scale) {
+                       double v_scale, std::optional<Tensor> row_scale) {
   check_gpu(qkv, "qkv");
   c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
   TORCH_CHECK(out.dim() == 3 && out.is_contiguous() && out.size(1) == nq,
@@ -252,6 +252,12 @@ void paged_decode_rope(Tensor out, Tensor qkv, Tensor positions, Tensor cos_sin,
                 k_norm_w->scalar_type() == out.scalar_type(), "qk norm weights [d]");
     rp.q_norm_w = q_norm_w->data_ptr();
     rp.k_norm_w = k_norm_w->data_ptr();
+  }
+  if (row_scale.has_value()) {
+    TORCH_CHECK(row_scale->scalar_type() == at::kFloat && row_scale->is_contiguous() &&
+                row_scale->numel() >= B, "row_scale fp32 [>= B] contiguous");
+    check_same_dev(out, *row_scale, "paged_decode_rope row_scale");
+    rp.row_scale = row_scale->data_ptr<float>();
   }
   rp.qkv = qkv.data_ptr();
   rp.use_rope = use_rope ? 1 : 0;
@@ -544,7 +550,8 @@ static void dgemm_shape(const Tensor& W, bool packed, int64_t* N, int64_t* K) {
   }
 }
 
-void dgemm(Tensor C, Tensor X, Tensor W, int64_t cfg, int64_t epi) {
+void dgemm(Tensor C, Tensor X, Tensor W, int64_t cfg, int64_t epi,
+           std::optional<Tensor> rscale) {
   check_gpu(X, "X");
   c10::hip::HIPGuardMasqueradingAsCUDA g(X.device());
   TORCH_CHECK(cfg >= 0 && cfg < kgc::dgemm_num_cfgs(), "unknown dgemm tile config");
@@ -576,9 +583,70 @@ void dgemm(Tensor C, Tensor X, Tensor W, int64_t cfg, int64_t epi) {
                 "C [M, N] (epi 1) or [M, N/2] (epi 2), contiguous, W's dtype");
   }
   TORCH_CHECK((M + bm - 1) / bm * (N / bn) * S < ((int64_t)1 << 31), "grid too large");
+  kgc::DgAux aux{};
+  if (rscale.has_value()) {
+    TORCH_CHECK(epi != 0 && kgc::dgemm_cfg_has_aux((int)cfg),
+                "rscale: epilogues 1 / 2 of a config with the row-scale epilogue");
+    TORCH_CHECK(rscale->scalar_type() == at::kFloat && rscale->is_contiguous() &&
+                rscale->numel() >= M, "rscale fp32 [>= M] contiguous");
+    check_same_dev(X, *rscale, "dgemm rscale");
+    aux.rsc = rscale->data_ptr<float>();
+  }
   if (M == 0) return;
   kgc::launch_dgemm(dt_code(W), (int)cfg, (int)epi, C.data_ptr(), X.data_ptr(), W.data_ptr(),
-                    (int)M, (int)N, (int)K, X.stride(0), (int)S, ss, stream());
+                    (int)M, (int)N, (int)K, X.stride(0), (int)S, ss, aux, stream());
+}
+
+// K9m with the split-K combine, residual add and row norms in the launch (EPI_FANIN):
+// R [M, N] += X W^T; ssp [>= M * N/BN] per-tile row sums of squares; rs [>= M] =
+// rsqrt(mean(R^2) + eps); Cs [S, M, N] fp32 slab workspace; cnt int32 [>= MB*N/BN + MB],
+// all zero before the first call (each launch leaves them zero).
+void dgemm_fanin(Tensor Cs, Tensor X, Tensor W, int64_t cfg, Tensor R, Tensor ssp, Tensor rs,
+                 Tensor cnt, double eps) {
+  check_gpu(X, "X");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(X.device());
+  TORCH_CHECK(cfg >= 0 && cfg < kgc::dgemm_num_cfgs() && kgc::dgemm_cfg_has_aux((int)cfg),
+              "dgemm_fanin: a tile config with the fan-in epilogue");
+  int bm, bn, packed;
+  kgc::dgemm_cfg_info((int)cfg, &bm, &bn, &packed);
+  TORCH_CHECK(W.scalar_type() == at::kBFloat16 || W.scalar_type() == at::kHalf, "bf16 / fp16");
+  int64_t N, K;
+  dgemm_shape(W, packed, &N, &K);
+  const int64_t bk = kgc::dgemm_block_k();
+  TORCH_CHECK(X.scalar_type() == W.scalar_type() && X.dim() == 2 && X.size(1) == K &&
+              X.stride(1) == 1 && X.stride(0) % 8 == 0 &&
+              reinterpret_cast<uintptr_t>(X.data_ptr()) % 16 == 0, "X [M, K] in W's dtype, "
+              "16-B aligned rows");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(W.data_ptr()) % 16 == 0, "W 16-B aligned");
+  const int64_t M = X.size(0);
+  TORCH_CHECK(N % bn == 0 && K % bk == 0 && K >= bk, "N % BN == 0, K % 64 == 0");
+  TORCH_CHECK(M <= (int64_t)1 << 20 && N < ((int64_t)1 << 31) / 4, "size limits");
+  TORCH_CHECK(Cs.scalar_type() == at::kFloat && Cs.dim() == 3 && Cs.is_contiguous() &&
+              Cs.size(1) == M && Cs.size(2) == N, "Cs fp32 contiguous [S, M, N]");
+  const int64_t S = Cs.size(0);
+  TORCH_CHECK(S == 1 || S == 2 || S == 3 || S == 4 || S == 5 || S == 6 || S == 8,
+              "dgemm_fanin: S in {1, 2, 3, 4, 5, 6, 8}");
+  TORCH_CHECK(S <= K / bk, "S <= K / 64");
+  TORCH_CHECK(R.scalar_type() == W.scalar_type() && R.dim() == 2 && R.is_contiguous() &&
+              R.size(0) == M && R.size(1) == N, "R [M, N] contiguous in W's dtype");
+  const int64_t MB = (M + bm - 1) / bm, NBT = N / bn;
+  TORCH_CHECK(ssp.scalar_type() == at::kFloat && ssp.is_contiguous() && ssp.numel() >= M * NBT,
+              "ssp fp32 [>= M * N/BN]");
+  TORCH_CHECK(rs.scalar_type() == at::kFloat && rs.is_contiguous() && rs.numel() >= M,
+              "rs fp32 [>= M]");
+  TORCH_CHECK(cnt.scalar_type() == at::kInt && cnt.is_contiguous() &&
+              cnt.numel() >= MB * NBT + MB, "cnt int32 [>= MB * N/BN + MB]");
+  for (const Tensor* t : {&Cs, &W, &R, &ssp, &rs, &cnt}) check_same_dev(X, *t, "dgemm_fanin operand");
+  TORCH_CHECK(MB * NBT * S < ((int64_t)1 << 31), "grid too large");
+  if (M == 0) return;
+  static const int ablate = [] {
+    const char* e = getenv("KGC_FANIN_ABLATE");
+    return e ? atoi(e) : 0;
+  }();
+  kgc::DgAux aux{R.data_ptr(), ssp.data_ptr<float>(), rs.data_ptr<float>(), cnt.data_ptr<int>(),
+                 nullptr, (float)eps, ablate};
+  kgc::launch_dgemm(dt_code(W), (int)cfg, 3, Cs.data_ptr(), X.data_ptr(), W.data_ptr(), (int)M,
+                    (int)N, (int)K, X.stride(0), (int)S, Cs.stride(0), aux, stream());
 }
 
 // P [N/128, K/64, 8192] <- W [N, K] re-laid out for the packed K9m configs
@@ -604,6 +672,10 @@ std::vector<int64_t> dgemm_cfg_info(int64_t cfg) {
   return {bm, bn, packed};
 }
 int64_t dgemm_num_cfgs() { return kgc::dgemm_num_cfgs(); }
+bool dgemm_cfg_has_aux(int64_t cfg) {
+  TORCH_CHECK(cfg >= 0 && cfg < kgc::dgemm_num_cfgs(), "unknown dgemm tile config");
+  return kgc::dgemm_cfg_has_aux((int)cfg);
+}
 
 // profiling only: the packed 256 x 128 tile with its MFMAs / DMAs / one operand's DMAs removed
 void dgemm_ablate(Tensor C, Tensor X, Tensor W, int64_t mode) {
@@ -632,7 +704,7 @@ void splitk_reduce(Tensor out, Tensor Cs) {
                             out.numel(), Cs.stride(0), stream());
 }
 
-void splitk_reduce_silu(Tensor out, Tensor Cs, bool interleaved) {
+void splitk_reduce_silu(Tensor out, Tensor Cs, bool interleaved, std::optional<Tensor> rscale) {
   check_gpu(Cs, "Cs");
   c10::hip::HIPGuardMasqueradingAsCUDA g(Cs.device());
   TORCH_CHECK(Cs.scalar_type() == at::kFloat && Cs.dim() == 3 && Cs.is_contiguous(), "Cs fp32 [S, M, 2I]");
@@ -643,8 +715,15 @@ void splitk_reduce_silu(Tensor out, Tensor Cs, bool interleaved) {
   TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kHalf, "bf16 / fp16");
   if (M == 0) return;
   TORCH_CHECK(!interleaved || I % 64 == 0, "interleaved (packed SiLU tiles): I % 64 == 0");
+  const float* rsc = nullptr;
+  if (rscale.has_value()) {
+    TORCH_CHECK(rscale->scalar_type() == at::kFloat && rscale->is_contiguous() &&
+                rscale->numel() >= M, "rscale fp32 [>= M] contiguous");
+    check_same_dev(Cs, *rscale, "splitk_reduce_silu rscale");
+    rsc = rscale->data_ptr<float>();
+  }
   kgc::launch_splitk_reduce_silu(dt_code(out), out.data_ptr(), Cs.data_ptr<float>(), (int)Cs.size(0),
-                                 (int)M, (int)I, Cs.stride(0), interleaved, stream());
+                                 (int)M, (int)I, Cs.stride(0), interleaved, rsc, stream());
 }
 
 void splitk_add_rms_norm(Tensor out, Tensor Cs, Tensor residual, Tensor w, double eps) {
@@ -1080,7 +1159,8 @@ TORCH_LIBRARY(kgc, m) {
         "Tensor(b!) k_cache, Tensor(c!) v_cache, Tensor slot_mapping, Tensor? q_norm_w, "
         "Tensor? k_norm_w, Tensor block_tables, Tensor ctx_lens, Tensor(d!) max_logits, "
         "Tensor(e!) exp_sums, Tensor(f!) tmp_out, int nq, int Z, "
-        "float scale, float eps, bool use_rope, float k_scale=1.0, float v_scale=1.0) -> ()");
+        "float scale, float eps, bool use_rope, float k_scale=1.0, float v_scale=1.0, "
+        "Tensor? row_scale=None) -> ()");
   m.def("prefill_attention(Tensor(a!) out, Tensor q, Tensor k_cache, Tensor v_cache, "
         "Tensor block_tables, Tensor query_start_loc, Tensor seq_lens, Tensor work_seq, "
         "Tensor work_mblk, float scale, float k_scale=1.0, float v_scale=1.0) -> ()");
@@ -1102,12 +1182,16 @@ TORCH_LIBRARY(kgc, m) {
   m.def("moe_combine(Tensor(a!) out, Tensor y, Tensor topk_w) -> ()");
   m.def("dense_gemm_splitk(Tensor(a!) Cs, Tensor A, Tensor W, int bm) -> ()");
   m.def("splitk_reduce(Tensor(a!) out, Tensor Cs) -> ()");
-  m.def("dgemm(Tensor(a!) C, Tensor X, Tensor W, int cfg, int epi) -> ()");
+  m.def("dgemm(Tensor(a!) C, Tensor X, Tensor W, int cfg, int epi, Tensor? rscale=None) -> ()");
+  m.def("dgemm_fanin(Tensor(a!) Cs, Tensor X, Tensor W, int cfg, Tensor(b!) R, Tensor(c!) ssp, "
+        "Tensor(d!) rs, Tensor(e!) cnt, float eps) -> ()");
   m.def("dgemm_cfg_info(int cfg) -> int[]", &dgemm_cfg_info);
   m.def("dgemm_num_cfgs() -> int", &dgemm_num_cfgs);
+  m.def("dgemm_cfg_has_aux(int cfg) -> bool", &dgemm_cfg_has_aux);
   m.def("dgemm_ablate(Tensor(a!) C, Tensor X, Tensor W, int mode) -> ()");
   m.def("dgemm_pack(Tensor(a!) P, Tensor W, bool silu) -> ()");
-  m.def("splitk_reduce_silu(Tensor(a!) out, Tensor Cs, bool interleaved=False) -> ()");
+  m.def("splitk_reduce_silu(Tensor(a!) out, Tensor Cs, bool interleaved=False, "
+        "Tensor? rscale=None) -> ()");
   m.def("splitk_add_rms_norm(Tensor(a!) out, Tensor Cs, Tensor(b!) residual, Tensor w, float eps) -> ()");
   m.def("ar_signal_bytes() -> int", &ar_signal_bytes);
   m.def("ar_alloc(int bytes) -> int", &ar_alloc);
@@ -1188,6 +1272,7 @@ TORCH_LIBRARY_IMPL(kgc, CUDA, m) {
   m.impl("moe_combine", &moe_combine);
   m.impl("dense_gemm_splitk", &dense_gemm_splitk);
   m.impl("dgemm", &dgemm);
+  m.impl("dgemm_fanin", &dgemm_fanin);
   m.impl("dgemm_ablate", &dgemm_ablate);
   m.impl("dgemm_pack", &dgemm_pack);
   m.impl("splitk_reduce", &splitk_reduce);

@@ -75,12 +75,12 @@ __device__ __forceinline__ u32x4 ld16(const void* p) {
 // ---- FUSE prologue helpers (rope_cache.hip computes the same values for the general
 // case; the roundings to T match it: summed slices, normed values and rotated outputs)
 template <typename T>
-__device__ __forceinline__ void qkv_row8(const DecodeRope& rp, int64_t e, float* x) {
+__device__ __forceinline__ void qkv_row8(const DecodeRope& rp, int64_t e, float* x, float sc) {
   if (rp.S == 0) {
     Pack8<T> p;
     p.u = ld16(reinterpret_cast<const T*>(rp.qkv) + e);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) x[j] = to_f(p.h[j]);
+    for (int j = 0; j < 8; ++j) x[j] = rp.row_scale ? to_f(from_f<T>(to_f(p.h[j]) * sc)) : to_f(p.h[j]);
     return;
   }
   // SB = 8 slices' loads in flight per round trip (clamped duplicates are not added: the
@@ -104,8 +104,8 @@ __device__ __forceinline__ void qkv_row8(const DecodeRope& rp, int64_t e, float*
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    x[q] = to_f(from_f<T>(a[q]));
-    x[4 + q] = to_f(from_f<T>(b[q]));
+    x[q] = to_f(from_f<T>(a[q] * sc));
+    x[4 + q] = to_f(from_f<T>(b[q] * sc));
   }
 }
 
@@ -115,7 +115,7 @@ __device__ __forceinline__ void qkv_row8(const DecodeRope& rp, int64_t e, float*
 // S - 1 to fill a batch) -- summed in slice order from 0, bit-identical to qkv_row8.
 template <typename T, int S>
 __device__ __forceinline__ void qkv_pair8_s(const DecodeRope& rp, int64_t ea, int64_t eb,
-                                            float* xa, float* xb) {
+                                            float* xa, float* xb, float sc) {
   const float* pa = reinterpret_cast<const float*>(rp.qkv) + ea;
   const float* pb = reinterpret_cast<const float*>(rp.qkv) + eb;
   f32x4 t[S][4];
@@ -136,27 +136,32 @@ __device__ __forceinline__ void qkv_pair8_s(const DecodeRope& rp, int64_t ea, in
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    xa[q] = to_f(from_f<T>(a0[q]));
-    xa[4 + q] = to_f(from_f<T>(a1[q]));
-    xb[q] = to_f(from_f<T>(b0[q]));
-    xb[4 + q] = to_f(from_f<T>(b1[q]));
+    xa[q] = to_f(from_f<T>(a0[q] * sc));
+    xa[4 + q] = to_f(from_f<T>(a1[q] * sc));
+    xb[q] = to_f(from_f<T>(b0[q] * sc));
+    xb[4 + q] = to_f(from_f<T>(b1[q] * sc));
   }
 }
 
 template <typename T>
 __device__ __forceinline__ void qkv_pair8(const DecodeRope& rp, int64_t ea, int64_t eb,
-                                          float* xa, float* xb) {
+                                          float* xa, float* xb, float sc) {
   switch (rp.S) {        // wave-uniform: the K9m split factors the tuner picks
-    case 2: qkv_pair8_s<T, 2>(rp, ea, eb, xa, xb); return;
-    case 3: qkv_pair8_s<T, 3>(rp, ea, eb, xa, xb); return;
-    case 4: qkv_pair8_s<T, 4>(rp, ea, eb, xa, xb); return;
-    case 5: qkv_pair8_s<T, 5>(rp, ea, eb, xa, xb); return;
-    case 6: qkv_pair8_s<T, 6>(rp, ea, eb, xa, xb); return;
-    case 8: qkv_pair8_s<T, 8>(rp, ea, eb, xa, xb); return;
+    case 2: qkv_pair8_s<T, 2>(rp, ea, eb, xa, xb, sc); return;
+    case 3: qkv_pair8_s<T, 3>(rp, ea, eb, xa, xb, sc); return;
+    case 4: qkv_pair8_s<T, 4>(rp, ea, eb, xa, xb, sc); return;
+    case 5: qkv_pair8_s<T, 5>(rp, ea, eb, xa, xb, sc); return;
+    case 6: qkv_pair8_s<T, 6>(rp, ea, eb, xa, xb, sc); return;
+    case 8: qkv_pair8_s<T, 8>(rp, ea, eb, xa, xb, sc); return;
     default:
-      qkv_row8<T>(rp, ea, xa);
-      qkv_row8<T>(rp, eb, xb);
+      qkv_row8<T>(rp, ea, xa, sc);
+      qkv_row8<T>(rp, eb, xb, sc);
   }
+}
+
+// the projection row's scale (1 unless the norm-free layer runs)
+__device__ __forceinline__ float qkv_row_scale(const DecodeRope& rp, int b) {
+  return rp.row_scale ? rp.row_scale[b] : 1.f;
 }
 
 // x * inv * w[col..col+7], rounded through T
@@ -200,7 +205,7 @@ __device__ __forceinline__ void decode_kv_write(const DecodeRope& rp, int b, int
     const int c = lane;
     float xa[8], xb[8];
     qkv_pair8<T>(rp, row + (int64_t)(nq + h) * D + c * 8, row + (int64_t)(nq + h) * D + half + c * 8,
-                 xa, xb);
+                 xa, xb, qkv_row_scale(rp, b));
     if (rp.k_norm_w) {
       float ss = 0.f;
 #pragma unroll
@@ -233,7 +238,7 @@ __device__ __forceinline__ void decode_kv_write(const DecodeRope& rp, int b, int
   } else if (lane >= 16 && lane < 16 + D / 8) {
     const int c = lane - 16;
     float xv[8];
-    qkv_row8<T>(rp, row + (int64_t)(nq + nkv + h) * D + c * 8, xv);
+    qkv_row8<T>(rp, row + (int64_t)(nq + nkv + h) * D + c * 8, xv, qkv_row_scale(rp, b));
     const int64_t e = ((blk * nkv + h) << bs_log2) * D + ((int64_t)(off >> 3) * D + c * 8) * 8 +
                       (off & 7);
     if constexpr (KV8) {
@@ -373,8 +378,9 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
       const int g = tid / TPH, c = tid % TPH;
       const int64_t qe = (int64_t)b * rp.qkv_stride + (int64_t)(h * G + g) * D;
       float xa[8], xb[8];
-      qkv_row8<T>(rp, qe + c * 8, xa);
-      qkv_row8<T>(rp, qe + D / 2 + c * 8, xb);
+      const float sc = qkv_row_scale(rp, b);
+      qkv_row8<T>(rp, qe + c * 8, xa, sc);
+      qkv_row8<T>(rp, qe + D / 2 + c * 8, xb, sc);
       if (rp.q_norm_w) {
         float ss = 0.f;
 #pragma unroll
@@ -676,7 +682,7 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
                         : (int64_t)(nq + nkv + h) * D;
       float xa[8], xb[8];
       qkv_pair8<T>(rp, row + col + c * 8, row + col + (kind == 2 ? 0 : D / 2) + c * 8, xa,
-                   xb);                                         // v: xb a dummy reload
+                   xb, qkv_row_scale(rp, b));                   // v: xb a dummy reload
       const void* nw = kind == 0 ? rp.q_norm_w : rp.k_norm_w;
       if (nw) {                    // q / k norm over the head's TPH lanes (aligned groups)
         float ss = 0.f;
@@ -750,7 +756,7 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
         const int g = i / TPH, c = i % TPH;
         const int64_t qe = (int64_t)b * rp.qkv_stride + (int64_t)(h * G + g) * D;
         float xa[8], xb[8];
-        qkv_pair8<T>(rp, qe + c * 8, qe + D / 2 + c * 8, xa, xb);
+        qkv_pair8<T>(rp, qe + c * 8, qe + D / 2 + c * 8, xa, xb, qkv_row_scale(rp, b));
         if (rp.q_norm_w) {
           float ss = 0.f;
 #pragma unroll

@@ -45,7 +45,7 @@ namespace {
 constexpr int DG_THREADS = 512;     // 8 waves: 4 along M x 2 along N
 constexpr int DG_BK = 64, DG_NS = 3, DG_ROWB = 128;
 
-enum { EPI_PARTIAL = 0, EPI_OUT = 1, EPI_SILU = 2 };
+enum { EPI_PARTIAL = 0, EPI_OUT = 1, EPI_SILU = 2, EPI_FANIN = 3 };
 // ablation builds (tools/dgemm_bench.py --ablate): one K-step without its MFMAs, without
 // its DMAs, or without one operand's DMAs
 enum { ABL_NONE = 0, ABL_NO_MFMA = 1, ABL_NO_DMA = 2, ABL_NO_A = 3, ABL_NO_B = 4 };
@@ -109,12 +109,173 @@ static int partial_wt() {
   return v;
 }
 
+// EPI_FANIN: the split-K combine, residual add and row norms of a row-parallel
+// projection (o / down) inside its own launch -- the norm-free layer at M = 65..512:
+//   1. every K-slice workgroup publishes its fp32 slab [z][M][N] write-through (sc1), drains
+//      (vmcnt 0), barriers, and draws a ticket on its tile's counter; the one that draws
+//      S - 1 is the tile's reducer (agent acquire; the other S - 1 exit);
+//   2. the reducer re-maps the tile to 16-B column quads (BN / 4 threads per row, all S
+//      slabs of a batch of rows in flight at once), sums the S slabs in slice order
+//      (deterministic whichever slice arrived last), adds the residual, stores it rounded
+//      to T and leaves each row's sum of squares over its BN columns in ssp[row][nb];
+//   3. it then draws a ticket on its row block's counter; the one that draws N / BN - 1
+//      (the row block's last tile) sums each row's N / BN partials into
+//      rs[row] = rsqrt(mean(R[row]^2) + eps): the scale its consumers (the QKV decode-
+//      attention prologue, the SiLU GEMM epilogue) apply to their gamma-folded outputs.
+// Counters are left at zero by the workgroup that draws the last ticket.  Slabs, partials
+// and counters follow the sc1-publish / agent-acquire recipe, so the result does not
+// depend on which XCD runs which slice.  S = 1 runs the same path (one slab, one ticket).
+template <typename T, int BM, int BN, int S, int MAXQ>
+__device__ __forceinline__ void fanin_reduce(const float* slab, int64_t slice_stride, T* R,
+                                             float* ssp, int M, int N, int m0, int nb) {
+  // rows per batch: up to MAXQ float4 slab loads per thread in flight (32: 128 VGPRs; the slabs
+  // are read at the cross-XCD rate, ~2-3 us per round trip under load: one batch for a
+  // 128 x 128 tile at S <= 4 measured 8.5 us for the two-batch combine)
+  constexpr int TPR = BN / 4, RPP = DG_THREADS / TPR, NP = BM / RPP;
+  constexpr int Q = MAXQ / S;
+  constexpr int PB0 = Q >= 32 ? 32 : Q >= 16 ? 16 : Q >= 8 ? 8 : Q >= 4 ? 4 : 2;
+  constexpr int PB = PB0 < NP ? PB0 : NP;
+  static_assert(NP % PB == 0, "row passes per batch");
+  const int tid = threadIdx.x, NBT = N / BN;
+  const int rr = tid / TPR, q = tid % TPR;
+  const int64_t colg = (int64_t)nb * BN + q * 4;
+#pragma unroll 1
+  for (int p0 = 0; p0 < NP; p0 += PB) {
+    f32x4 v[PB][S];
+    u32x2 rv[PB];
+#pragma unroll
+    for (int p = 0; p < PB; ++p) {
+      const int row = min(m0 + (p0 + p) * RPP + rr, M - 1);    // clamped: in-bounds loads
+      const float* sp = slab + (int64_t)row * N + colg;
+#pragma unroll
+      for (int zz = 0; zz < S; ++zz)
+        v[p][zz] = *reinterpret_cast<const f32x4*>(sp + zz * slice_stride);
+      rv[p] = *reinterpret_cast<const u32x2*>(R + (int64_t)row * N + colg);
+    }
+#pragma unroll
+    for (int p = 0; p < PB; ++p) {
+      const int row = m0 + (p0 + p) * RPP + rr;
+      f32x4 a = v[p][0];
+#pragma unroll
+      for (int zz = 1; zz < S; ++zz) a += v[p][zz];
+      Pack4<T> r, o;
+      r.u = rv[p];
+      float sq = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o.h[j] = from_f<T>(a[j] + to_f(r.h[j]));
+        const float f = to_f(o.h[j]);
+        sq += f * f;
+      }
+      if (row < M) *reinterpret_cast<u32x2*>(R + (int64_t)row * N + colg) = o.u;
+#pragma unroll
+      for (int off = 1; off < TPR; off <<= 1) sq += __shfl_xor(sq, off, 64);
+      if (row < M && q == 0)
+        __hip_atomic_store(ssp + (int64_t)row * NBT + nb, sq, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+template <typename T, int BM, int BN, int MT, int NT, int MAXQ>
+__device__ __forceinline__ void dgemm_fanin_epilogue(f32x4 (&acc)[MT][NT], bool consumer,
+                                                     char* lds, void* Cv, int M, int N, int S,
+                                                     int MB, int mb, int nb, int z,
+                                                     int64_t slice_stride, const DgAux& aux) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) & 3, wn = wave & 1, fr = lane & 15, fq = lane >> 4;
+  const int m0 = mb * BM, NBT = N / BN, tile = mb * NBT + nb;
+  float* slab = reinterpret_cast<float*>(Cv);
+  int* flag = reinterpret_cast<int*>(lds);
+  // 1. publish the slice, draw the tile ticket
+  if (consumer) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = m0 + wm * (BM / 4) + i * 16 + fq * 4 + e;
+        if (row >= M) continue;
+        float* cp = slab + z * slice_stride + (int64_t)row * N + nb * BN + wn * (BN / 2) + fr;
+#pragma unroll
+        for (int n = 0; n < NT; ++n) store_partial(cp + n * 16, acc[i][n][e], 1);
+      }
+  }
+  wait_vm<0>();
+  __syncthreads();
+  if (tid == 0) {
+    const int t = __hip_atomic_fetch_add(aux.cnt + tile, 1, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == S - 1;
+    if (last) {
+      __hip_atomic_store(aux.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      wait_vm<0>();
+    }
+    flag[0] = last;
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  // 2. the tile's reducer
+  if (tid < DG_THREADS && !(aux.ablate & 1)) {
+    T* R = reinterpret_cast<T*>(aux.R);
+    switch (S) {
+#define FANIN_S(SS) \
+      case SS: fanin_reduce<T, BM, BN, SS, MAXQ>(slab, slice_stride, R, aux.ssp, M, N, m0, nb); \
+        break;
+      FANIN_S(1) FANIN_S(2) FANIN_S(3) FANIN_S(4) FANIN_S(5) FANIN_S(6) FANIN_S(8)
+#undef FANIN_S
+      default: break;            // the host admits only these split factors
+    }
+  }
+  wait_vm<0>();
+  __syncthreads();
+  // 3. the row block's last tile: the rows' norm scales
+  if (aux.ablate & 2) return;
+  if (tid == 0) {
+    int* c2 = aux.cnt + MB * NBT + mb;
+    const int t = __hip_atomic_fetch_add(c2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == NBT - 1;
+    if (last) {
+      __hip_atomic_store(c2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      wait_vm<0>();
+    }
+    flag[1] = last;
+  }
+  __syncthreads();
+  if (!flag[1]) return;
+  // DG_THREADS / BM threads per row, each summing every TPRR-th partial with all of its
+  // loads in flight (a per-row loop of dependent batches was a round trip per 4 partials)
+  constexpr int TPRR = DG_THREADS / BM;
+  static_assert(TPRR >= 1 && (TPRR & (TPRR - 1)) == 0, "threads per row");
+  if (tid < DG_THREADS) {
+    const int r = tid / TPRR, part = tid % TPRR, row = m0 + r;
+    const float* pp = aux.ssp + (int64_t)min(row, M - 1) * NBT;
+    float v[8];
+    float s = 0.f;
+#pragma unroll 1
+    for (int j0 = part; j0 < NBT; j0 += 8 * TPRR) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int j = j0 + k * TPRR;
+        v[k] = pp[min(j, NBT - 1)];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (j0 + k * TPRR < NBT) s += v[k];
+    }
+#pragma unroll
+    for (int off = 1; off < TPRR; off <<= 1) s += __shfl_xor(s, off, 64);
+    if (row < M && part == 0) aux.rs[row] = rsqrtf(s / (float)N + aux.eps);
+  }
+}
+
 // LDW = 4: four extra loader waves issue every DMA and the 8 MFMA waves never stall on
 // DMA issue (one s_barrier per step for all 12 waves); LDW = 0: the MFMA waves issue too.
 template <typename T, int BM, int BN, int EPI, bool PK, int ABL = ABL_NONE, int LDW = 0>
 __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
     void* __restrict__ Cv, const T* __restrict__ X, const T* __restrict__ W, int M, int N,
-    int K, int64_t ldx, int S, int MB, int64_t slice_stride, int xmap, int wt) {
+    int K, int64_t ldx, int S, int MB, int64_t slice_stride, int xmap, int wt, DgAux aux) {
   constexpr int MT = BM / 4 / 16;                 // 16-row MFMA tiles per wave
   constexpr int NT = BN / 2 / 16;                 // 16-col MFMA tiles per wave
   constexpr int NIW = LDW > 0 ? LDW : 8;          // waves issuing DMAs
@@ -208,6 +369,22 @@ __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
   const int fr = lane & 15, fq = lane >> 4;
   const int a_row0 = wm * (BM / 4) + fr;
   const int b_row0 = wn * (BN / 2) + fr;
+  // EPI_OUT / EPI_SILU with a row scale (the norm-free layer's rsqrt of the producer's
+  // row norms): the lane's rows' scales, loaded before the K walk hides their latency
+  float rsv[MT][4];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) rsv[i][e] = 1.f;
+  if constexpr (EPI == EPI_OUT || EPI == EPI_SILU) {
+    if (aux.rsc != nullptr && consumer) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          rsv[i][e] = aux.rsc[min(m0 + wm * (BM / 4) + i * 16 + fq * 4 + e, M - 1)];
+    }
+  }
 
   issue(0, 0);
   if (nk > 1) issue(1, 1);
@@ -253,6 +430,20 @@ __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
   }
 
   // ---- epilogue: lane holds C[4*fq + e][fr] of every 16x16 tile
+  if constexpr (EPI == EPI_OUT || EPI == EPI_SILU) {
+    // one wait for the row scales here, unconditionally: waited for inside the per-row
+    // branches below, each row's wait also drained the previous rows' stores
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(rsv[i][e]));
+  }
+  if constexpr (EPI == EPI_FANIN) {
+    // the 12-wave (loader) variants run 3 waves per SIMD: 16 loads per thread (no spill)
+    dgemm_fanin_epilogue<T, BM, BN, MT, NT, (LDW > 0 ? 16 : 32)>(acc, consumer, lds, Cv, M, N, S,
+                                                               MB, mb, nb, z, slice_stride, aux);
+    return;
+  }
   if (!consumer) return;
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
@@ -268,13 +459,14 @@ __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
       } else if constexpr (EPI == EPI_OUT) {
         T* cp = reinterpret_cast<T*>(Cv) + (int64_t)row * N + nb * BN + wn * (BN / 2) + fr;
 #pragma unroll
-        for (int n = 0; n < NT; ++n) cp[n * 16] = from_f<T>(acc[i][n][e]);
+        for (int n = 0; n < NT; ++n) cp[n * 16] = from_f<T>(acc[i][n][e] * rsv[i][e]);
       } else {
         const int I = N >> 1;
+        const float sc = rsv[i][e];
         T* cp = reinterpret_cast<T*>(Cv) + (int64_t)row * I + nb * (BN / 2) + wn * (BN / 4) + fr;
 #pragma unroll
         for (int n = 0; n < NT; n += 2)
-          cp[(n >> 1) * 16] = from_f<T>(silu_f(acc[i][n][e]) * acc[i][n + 1][e]);
+          cp[(n >> 1) * 16] = from_f<T>(silu_f(acc[i][n][e] * sc) * (acc[i][n + 1][e] * sc));
       }
     }
   }
@@ -479,35 +671,36 @@ static const int kCfg[kNumCfgs][3] = {{256, 128, 0}, {256, 64, 0},  {128, 128, 0
 
 template <typename T, int BM, int BN, bool PK, int LDW = 0>
 void dgemm_cfg(int epi, void* C, const void* X, const void* W, int M, int N, int K, int64_t ldx,
-               int S, int64_t ss, hipStream_t s, int xmap = 0) {
+               int S, int64_t ss, const DgAux& aux, hipStream_t s, int xmap = 0) {
   const int MB = (M + BM - 1) / BM;
   const dim3 grid((unsigned)(MB * (N / BN) * S));
   // the XCD pairing needs S | 8 and whole groups of 8 / S column tiles
   const int xm = (xmap && MB > 1 && 8 % S == 0 && (N / BN) % (8 / S) == 0) ? 1 : 0;
 #define DG_LAUNCH(E)                                                             \
   dgemm_kernel<T, BM, BN, E, PK, ABL_NONE, LDW><<<grid, DG_THREADS + LDW * 64, 0, s>>>( \
-      C, (const T*)X, (const T*)W, M, N, K, ldx, S, MB, ss, xm, partial_wt())
+      C, (const T*)X, (const T*)W, M, N, K, ldx, S, MB, ss, xm, partial_wt(), aux)
   if (epi == EPI_PARTIAL) DG_LAUNCH(EPI_PARTIAL);
   else if (epi == EPI_OUT) DG_LAUNCH(EPI_OUT);
-  else DG_LAUNCH(EPI_SILU);
+  else if (epi == EPI_SILU) DG_LAUNCH(EPI_SILU);
+  else DG_LAUNCH(EPI_FANIN);
 #undef DG_LAUNCH
 }
 
 template <typename T>
 void dgemm_t(int cfg, int epi, void* C, const void* X, const void* W, int M, int N, int K,
-             int64_t ldx, int S, int64_t ss, hipStream_t s) {
+             int64_t ldx, int S, int64_t ss, const DgAux& a, hipStream_t s) {
   switch (cfg) {
-    case 0: dgemm_cfg<T, 256, 128, false>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
-    case 1: dgemm_cfg<T, 256, 64, false>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
-    case 2: dgemm_cfg<T, 128, 128, false>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
-    case 3: dgemm_cfg<T, 128, 64, false>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
-    case 4: dgemm_cfg<T, 256, 128, true>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
-    case 5: dgemm_cfg<T, 128, 128, true>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
-    case 6: dgemm_cfg<T, 256, 128, true, 4>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
-    case 7: dgemm_cfg<T, 128, 128, true, 4>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
+    case 0: dgemm_cfg<T, 256, 128, false>(epi, C, X, W, M, N, K, ldx, S, ss, a, s); break;
+    case 1: dgemm_cfg<T, 256, 64, false>(epi, C, X, W, M, N, K, ldx, S, ss, a, s); break;
+    case 2: dgemm_cfg<T, 128, 128, false>(epi, C, X, W, M, N, K, ldx, S, ss, a, s); break;
+    case 3: dgemm_cfg<T, 128, 64, false>(epi, C, X, W, M, N, K, ldx, S, ss, a, s); break;
+    case 4: dgemm_cfg<T, 256, 128, true>(epi, C, X, W, M, N, K, ldx, S, ss, a, s); break;
+    case 5: dgemm_cfg<T, 128, 128, true>(epi, C, X, W, M, N, K, ldx, S, ss, a, s); break;
+    case 6: dgemm_cfg<T, 256, 128, true, 4>(epi, C, X, W, M, N, K, ldx, S, ss, a, s); break;
+    case 7: dgemm_cfg<T, 128, 128, true, 4>(epi, C, X, W, M, N, K, ldx, S, ss, a, s); break;
     case 8: dgemm_sl_cfg<T, 256, 128, 4>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
     case 9: dgemm_sl_cfg<T, 128, 128, 6>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
-    default: dgemm_cfg<T, 128, 128, true>(epi, C, X, W, M, N, K, ldx, S, ss, s, 1); break;
+    default: dgemm_cfg<T, 128, 128, true>(epi, C, X, W, M, N, K, ldx, S, ss, a, s, 1); break;
   }
 }
 
@@ -520,11 +713,14 @@ void dgemm_cfg_info(int cfg, int* bm, int* bn, int* packed) {
   *packed = kCfg[cfg][2];
 }
 int dgemm_block_k() { return DG_BK; }
+// the split-loader configs (8, 9) have no fan-in or row-scale epilogue
+bool dgemm_cfg_has_aux(int cfg) { return cfg != 8 && cfg != 9; }
 
 void launch_dgemm(int dtype, int cfg, int epi, void* C, const void* X, const void* W, int M,
-                  int N, int K, int64_t ldx, int S, int64_t slice_stride, hipStream_t s) {
-  if (dtype == DT_BF16) dgemm_t<bf16>(cfg, epi, C, X, W, M, N, K, ldx, S, slice_stride, s);
-  else dgemm_t<f16>(cfg, epi, C, X, W, M, N, K, ldx, S, slice_stride, s);
+                  int N, int K, int64_t ldx, int S, int64_t slice_stride, const DgAux& aux,
+                  hipStream_t s) {
+  if (dtype == DT_BF16) dgemm_t<bf16>(cfg, epi, C, X, W, M, N, K, ldx, S, slice_stride, aux, s);
+  else dgemm_t<f16>(cfg, epi, C, X, W, M, N, K, ldx, S, slice_stride, aux, s);
 }
 
 void launch_dgemm_pack(int dtype, bool silu, void* P, const void* W, int N, int K,
@@ -550,7 +746,7 @@ void launch_dgemm_ablate(int mode, float* C, const void* X, const void* W, int M
   const dim3 grid((unsigned)(MB * (N / 128) * S));
 #define AB(MODE)                                                                     \
   dgemm_kernel<bf16, 256, 128, EPI_PARTIAL, true, MODE><<<grid, DG_THREADS, 0, s>>>( \
-      C, (const bf16*)X, (const bf16*)W, M, N, K, ldx, S, MB, ss, 0, partial_wt())
+      C, (const bf16*)X, (const bf16*)W, M, N, K, ldx, S, MB, ss, 0, partial_wt(), DgAux{})
   switch (mode) {
     case ABL_NO_MFMA: AB(ABL_NO_MFMA); break;
     case ABL_NO_DMA: AB(ABL_NO_DMA); break;

@@ -48,6 +48,9 @@ struct DecodeRope {
   const void* q_norm_w;      // nullptr: no q/k RMSNorm
   const void* k_norm_w;
   float eps, k_inv, v_inv;
+  // [B] fp32 or nullptr: row b of the projection is scaled by row_scale[b] before its
+  // rounding (the norm-free layer's rsqrt(mean(x^2) + eps) of a gamma-folded QKV weight)
+  const float* row_scale;
 };
 void launch_paged_decode_rope(int dtype, const DecodeRope& rp, void* out, void* k_cache,
                               void* v_cache, const int* block_tables, int bt_stride,
@@ -126,11 +129,26 @@ void launch_dense_gemm_splitk(int dtype, int bm, float* Cs, const void* A, const
 // launch_dgemm_pack rather than [N, K]).  epi 0: fp32 split-K slice z of C [S, M, N];
 // 1: C [M, N] in X's dtype (S = 1); 2: silu(gate) * up of a merged [gate; up] W into
 // C [M, N/2] (S = 1; a packed W must have been packed with silu = true)
+// 3: split-K combine + residual add + row norms in the launch (the norm-free layer's o /
+// down projections): C holds the S fp32 slabs; R [M, N] += their sum, ssp [M, N/BN] and
+// rs [M] = rsqrt(mean(R^2) + eps) out; cnt [MB * N/BN + MB] zeroed tickets.  epi 1 / 2 with
+// rsc != nullptr: output row m scaled by rsc[m] (before the SiLU).
+struct DgAux {
+  void* R;
+  float* ssp;
+  float* rs;
+  int* cnt;
+  const float* rsc;
+  float eps;
+  int ablate;     // fan-in cost breakdown (tools/fanin_bench.py): bit 0 no combine, bit 1 no rs
+};
 int dgemm_num_cfgs();
 void dgemm_cfg_info(int cfg, int* bm, int* bn, int* packed);
 int dgemm_block_k();
+bool dgemm_cfg_has_aux(int cfg);
 void launch_dgemm(int dtype, int cfg, int epi, void* C, const void* X, const void* W, int M,
-                  int N, int K, int64_t ldx, int S, int64_t slice_stride, hipStream_t s);
+                  int N, int K, int64_t ldx, int S, int64_t slice_stride, const DgAux& aux,
+                  hipStream_t s);
 void launch_dgemm_pack(int dtype, bool silu, void* P, const void* W, int N, int K,
                        hipStream_t s);
 void launch_dgemm_ablate(int mode, float* C, const void* X, const void* W, int M, int N, int K,
@@ -143,7 +161,8 @@ void launch_splitk_reduce(int dtype, void* out, const float* Cs, int S, int64_t 
                           int64_t slice_stride, hipStream_t s);
 // silu(gate) * up of the summed gate_up split-K slices: Cs [S, M, 2I] -> out [M, I]
 void launch_splitk_reduce_silu(int dtype, void* out, const float* Cs, int S, int M, int I,
-                               int64_t slice_stride, bool interleaved, hipStream_t s);
+                               int64_t slice_stride, bool interleaved, const float* rsc,
+                               hipStream_t s);
 void launch_moe_combine(int dtype, void* out, const void* y, const float* topk_w, int ntok, int k,
                         int H, int splitk, int64_t slice_stride, hipStream_t s);
 

@@ -290,11 +290,14 @@ template <typename T, int SK, bool IL = false>
 __global__ __launch_bounds__(256) void splitk_reduce_silu_kernel(T* __restrict__ out,
                                                                  const float* __restrict__ Cs,
                                                                  int S_, int I,
-                                                                 int64_t slice_stride) {
+                                                                 int64_t slice_stride,
+                                                                 const float* __restrict__ rsc) {
   const int S = SK > 0 ? SK : S_;
   const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
   if (c >= I) return;
   const int64_t m = blockIdx.y;
+  // the norm-free layer: the row's rsqrt(mean(x^2) + eps) over a gamma-folded weight
+  const float sc = rsc ? rsc[m] : 1.f;
   const int64_t gcol = IL ? (int64_t)(c >> 6) * 128 + ((c & 63) >> 4) * 32 + (c & 15) : c;
   const int64_t ucol = IL ? gcol + 16 : (int64_t)c + I;
   const float* row = Cs + m * 2 * I;
@@ -307,6 +310,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_silu_kernel(T* __restrict__
     u0 += *reinterpret_cast<const f32x4*>(src + ucol);
     u1 += *reinterpret_cast<const f32x4*>(src + ucol + 4);
   }
+  g0 *= sc;
+  g1 *= sc;
+  u0 *= sc;
+  u1 *= sc;
   Pack8<T> o;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -467,9 +474,9 @@ void launch_splitk_reduce(int dtype, void* out, const float* Cs, int S, int64_t 
 
 template <typename T, bool IL>
 static void splitk_reduce_silu_t(T* out, const float* Cs, int S, int n, int I, int64_t ss,
-                                 hipStream_t s) {
+                                 const float* rsc, hipStream_t s) {
   const dim3 grid((unsigned)((I / 8 + 255) / 256), (unsigned)n);
-#define SKS(K) splitk_reduce_silu_kernel<T, K, IL><<<grid, 256, 0, s>>>(out, Cs, S, I, ss)
+#define SKS(K) splitk_reduce_silu_kernel<T, K, IL><<<grid, 256, 0, s>>>(out, Cs, S, I, ss, rsc)
   switch (S) {
     case 2: SKS(2); break;
     case 3: SKS(3); break;
@@ -483,20 +490,22 @@ static void splitk_reduce_silu_t(T* out, const float* Cs, int S, int n, int I, i
 }
 
 void launch_splitk_reduce_silu(int dtype, void* out, const float* Cs, int S, int M, int I,
-                               int64_t slice_stride, bool interleaved, hipStream_t s) {
+                               int64_t slice_stride, bool interleaved, const float* rsc,
+                               hipStream_t s) {
   for (int m0 = 0; m0 < M; m0 += 65535) {   // gridDim.y <= 65535
     const int n = std::min(M - m0, 65535);
     const float* c = Cs + (int64_t)m0 * 2 * I;
+    const float* r = rsc ? rsc + m0 : nullptr;
     if (dtype == DT_BF16) {
       if (interleaved)
-        splitk_reduce_silu_t<bf16, true>((bf16*)out + (int64_t)m0 * I, c, S, n, I, slice_stride, s);
+        splitk_reduce_silu_t<bf16, true>((bf16*)out + (int64_t)m0 * I, c, S, n, I, slice_stride, r, s);
       else
-        splitk_reduce_silu_t<bf16, false>((bf16*)out + (int64_t)m0 * I, c, S, n, I, slice_stride, s);
+        splitk_reduce_silu_t<bf16, false>((bf16*)out + (int64_t)m0 * I, c, S, n, I, slice_stride, r, s);
     } else {
       if (interleaved)
-        splitk_reduce_silu_t<f16, true>((f16*)out + (int64_t)m0 * I, c, S, n, I, slice_stride, s);
+        splitk_reduce_silu_t<f16, true>((f16*)out + (int64_t)m0 * I, c, S, n, I, slice_stride, r, s);
       else
-        splitk_reduce_silu_t<f16, false>((f16*)out + (int64_t)m0 * I, c, S, n, I, slice_stride, s);
+        splitk_reduce_silu_t<f16, false>((f16*)out + (int64_t)m0 * I, c, S, n, I, slice_stride, r, s);
     }
   }
 }

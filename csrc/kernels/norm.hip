@@ -129,6 +129,66 @@ __global__ __launch_bounds__(NORM_NT) void splitk_add_rms_norm_kernel(
   }
 }
 
+// The same for H = NVT * 2048 and a compile-time slice count: no per-vector guards, so
+// every slice, residual and weight load of a thread is issued before the first add (the
+// guarded loop above issued vector i + 1's loads only after vector i's adds: at H = 4096
+// two dependent round trips per row)
+template <typename T, int SK, int NVT>
+__global__ __launch_bounds__(NORM_NT) void splitk_add_rms_norm_nv_kernel(
+    T* __restrict__ out, const float* __restrict__ Cs, T* __restrict__ residual,
+    const T* __restrict__ w, int H, int64_t slice_stride, float eps) {
+  __shared__ float scratch[NORM_NT / 64];
+  const int row = blockIdx.x;
+  const float* cr = Cs + (int64_t)row * H;
+  T* rr = residual + (int64_t)row * H;
+  f32x4 a[NVT][SK], b[NVT][SK];
+  Pack8<T> r[NVT], wv[NVT];
+#pragma unroll
+  for (int i = 0; i < NVT; ++i) {
+    const int idx = threadIdx.x + i * NORM_NT;
+#pragma unroll
+    for (int z = 0; z < SK; ++z) {
+      const float* src = cr + z * slice_stride + idx * 8;
+      a[i][z] = *reinterpret_cast<const f32x4*>(src);
+      b[i][z] = *reinterpret_cast<const f32x4*>(src + 4);
+    }
+    r[i].u = *reinterpret_cast<const u32x4*>(rr + idx * 8);
+    wv[i].u = *reinterpret_cast<const u32x4*>(w + idx * 8);
+  }
+  float ss = 0.f;
+  Pack8<T> v[NVT];
+#pragma unroll
+  for (int i = 0; i < NVT; ++i) {
+    f32x4 sa = a[i][0], sb = b[i][0];
+#pragma unroll
+    for (int z = 1; z < SK; ++z) {
+      sa += a[i][z];
+      sb += b[i][z];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[i].h[q] = from_f<T>(to_f(from_f<T>(sa[q])) + to_f(r[i].h[q]));
+      v[i].h[4 + q] = from_f<T>(to_f(from_f<T>(sb[q])) + to_f(r[i].h[4 + q]));
+    }
+    *reinterpret_cast<u32x4*>(rr + (threadIdx.x + i * NORM_NT) * 8) = v[i].u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float f = to_f(v[i].h[j]);
+      ss += f * f;
+    }
+  }
+  ss = block_sum<NORM_NT>(ss, scratch);
+  const float inv = rsqrtf(ss / (float)H + eps);
+  T* orow = out + (int64_t)row * H;
+#pragma unroll
+  for (int i = 0; i < NVT; ++i) {
+    Pack8<T> o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o.h[j] = from_f<T>(to_f(v[i].h[j]) * inv * to_f(wv[i].h[j]));
+    *reinterpret_cast<u32x4*>(orow + (threadIdx.x + i * NORM_NT) * 8) = o.u;
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(NORM_NT) void layer_norm_kernel(
     T* __restrict__ out, const T* __restrict__ x, const T* __restrict__ w,
@@ -196,9 +256,30 @@ void launch_rms_norm(int dtype, void* out, const void* x, void* residual, const 
   else rms_dispatch<f16>(out, x, residual, w, rows, H, x_stride, eps, s);
 }
 
+template <typename T, int NVT>
+static bool splitk_add_rms_nv(T* out, const float* Cs, T* residual, const T* w, int rows, int H,
+                              int S, int64_t ss, float eps, hipStream_t s) {
+#define SKV(K)                                                                              \
+  splitk_add_rms_norm_nv_kernel<T, K, NVT><<<rows, NORM_NT, 0, s>>>(out, Cs, residual, w, H, \
+                                                                    ss, eps)
+  switch (S) {
+    case 2: SKV(2); return true;
+    case 3: SKV(3); return true;
+    case 4: SKV(4); return true;
+    case 5: SKV(5); return true;
+    case 6: SKV(6); return true;
+    case 8: if (NVT <= 2) { SKV(8); return true; } return false;
+    default: return false;
+  }
+#undef SKV
+}
+
 template <typename T>
 static void splitk_add_rms_dispatch(T* out, const float* Cs, T* residual, const T* w, int rows,
                                     int H, int S, int64_t ss, float eps, hipStream_t s) {
+  if (H == 2048 && splitk_add_rms_nv<T, 1>(out, Cs, residual, w, rows, H, S, ss, eps, s)) return;
+  if (H == 4096 && splitk_add_rms_nv<T, 2>(out, Cs, residual, w, rows, H, S, ss, eps, s)) return;
+  if (H == 8192 && splitk_add_rms_nv<T, 4>(out, Cs, residual, w, rows, H, S, ss, eps, s)) return;
 #define SKN(K) splitk_add_rms_norm_kernel<T, K><<<rows, NORM_NT, 0, s>>>(out, Cs, residual, w, \
                                                                          H, S, ss, eps)
   switch (S) {

@@ -729,7 +729,8 @@ class ModelRunner:
                              silu_shapes=getattr(self.model, "silu_shapes", lambda: set())(),
                              tail_shapes=getattr(self.model, "tail_shapes", lambda: set())(),
                              qkv_dims=getattr(self.model, "qkv_dims", lambda: {})(),
-                             rs_shapes=getattr(self.model, "_rs_w", None) is not None)
+                             rs_shapes=getattr(self.model, "_rs_w", None) is not None,
+                             nf=getattr(self.model, "_nf_w", None) is not None)
         whole = self.model.first and self.model.last
         if (not self.use_graphs or not (whole or self.pp_link is not None)
                 or not getattr(self.model, "graph_safe", True)):

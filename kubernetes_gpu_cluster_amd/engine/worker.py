@@ -128,6 +128,11 @@ class Worker:
             fold = getattr(self.model, "fold_rs_weights", None)
             if fold is not None:
                 fold()
+            if not cfg.enforce_eager:
+                # packed gamma-folded copies for the norm-free mid-M layer (graph steps)
+                fold = getattr(self.model, "fold_nf_weights", None)
+                if fold is not None:
+                    fold()
         if self.ps.tp_size > 1 and dev.type == "cuda" and not cfg.disable_custom_all_reduce:
             from ..parallel.custom_allreduce import calibration_rows, maybe_init_custom_allreduce
             rows = (calibration_rows(min(cfg.cuda_graph_max_bs, cfg.max_num_seqs))

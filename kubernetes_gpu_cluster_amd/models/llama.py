@@ -42,6 +42,9 @@ _tail_fusion_enabled = os.environ.get("KGC_TAIL_FUSION", "1") != "0"
 _tp_ar_norm_enabled = os.environ.get("KGC_TP_AR_NORM", "1") != "0"
 # small M on one GPU: the decoder layer without RMSNorm launches (KGC_RS_LAYER=0: off)
 _rs_enabled = os.environ.get("KGC_RS_LAYER", "1") != "0"
+# M = 65..512 on one GPU: the norm-free layer on K9m, the o / down split-K combine + residual
+# add + row norms inside their GEMM launches (KGC_NF_LAYER=0: off)
+_nf_enabled = os.environ.get("KGC_NF_LAYER", "1") != "0"
 # decode-only steps: RoPE + KV write folded into the paged-decode kernel (KGC_DECODE_ROPE_FUSED=0: off)
 _decode_rope_fused = os.environ.get("KGC_DECODE_ROPE_FUSED", "1") != "0"
 # prefill-only steps of RoPE models without q/k norm: K2 rotates q as it loads it from the
@@ -85,6 +88,13 @@ class LlamaAttention(nn.Module):
     def forward(self, positions, x, ctx: ForwardContext):
         return self.o_proj(self.attend(positions, self.project_qkv(x), ctx))
 
+    @staticmethod
+    def _scaled_rows(qkv, row_scale, dtype):
+        """The norm-free layer's QKV where no fused decode kernel applies its row scale:
+        (summed K-slices of) the projection times rsqrt(mean(x^2) + eps), rounded."""
+        y = qkv.sum(0) if qkv.dim() == 3 else qkv.float()
+        return (y * row_scale[:, None]).to(dtype)
+
     def project_qkv(self, x):
         """The QKV projection; where the decode plan runs it as K9m split-K, the fp32
         K-slices themselves (the RoPE / KV-write kernel sums them, ops/gemm.py linear_qkv)."""
@@ -93,8 +103,10 @@ class LlamaAttention(nn.Module):
             return gemm.linear_qkv(x, p.weight)
         return p(x)
 
-    def attend(self, positions, qkv, ctx: ForwardContext):
-        """RoPE + KV-cache write + paged attention on a QKV projection -> [T, nq*d]."""
+    def attend(self, positions, qkv, ctx: ForwardContext, row_scale=None):
+        """RoPE + KV-cache write + paged attention on a QKV projection -> [T, nq*d].
+        ``row_scale`` [T] fp32: the norm-free layer's per-row rsqrt(mean(x^2) + eps) of a
+        projection computed on the raw residual with gamma folded into the weight."""
         kc, vc = ctx.kv_caches[self.attn.layer_idx]
         m = ctx.attn
         if (_decode_rope_fused and qkv.is_cuda and not m.num_prefill_tokens and m.num_decodes
@@ -106,8 +118,10 @@ class LlamaAttention(nn.Module):
                 None if self.q_norm is None else self.q_norm.weight,
                 None if self.k_norm is None else self.k_norm.weight, self.cfg.rms_eps,
                 workspace=m.decode_workspace, grid_z=m.decode_grid_z, k_scale=ctx.k_scale,
-                v_scale=ctx.v_scale, dtype=self.qkv_proj.weight.dtype)
+                v_scale=ctx.v_scale, dtype=self.qkv_proj.weight.dtype, row_scale=row_scale)
             return o.view(o.shape[0], self.nq * self.cfg.head_dim)
+        if row_scale is not None:
+            qkv = self._scaled_rows(qkv, row_scale, self.qkv_proj.weight.dtype)
         if (_prefill_rope_fused and qkv.is_cuda and qkv.dim() == 2 and m.num_prefill_tokens
                 and not m.num_decodes and self.q_norm is None and self.k_norm is None
                 and m.num_prefill_tokens == qkv.shape[0]):
@@ -207,6 +221,9 @@ class LlamaForCausalLM(nn.Module):
                 return self._forward_fused(input_ids, positions, ctx, cfgs)
         x = self.embed_tokens(input_ids) if self.first else hidden
         if self._tail_fusable(x):
+            nf = self._nf_cfgs(x.shape[0])
+            if nf is not None:
+                return self._forward_nf(positions, x, ctx, nf)
             return self._forward_tail_fused(positions, x, ctx)
         if self._tp_tail_fusable():
             if ctx.attn.split is not None:
@@ -257,6 +274,79 @@ class LlamaForCausalLM(nn.Module):
         x, _ = gemm.linear_add_rms(h, prev.mlp.down_proj.weight, residual, self.norm.weight,
                                    self.norm.eps)
         return x
+
+    # ------------------------------------------------------------------ norm-free mid-M layer
+    def fold_nf_weights(self, budget_fraction: float = 0.08) -> int:
+        """K9m-packed copies of the qkv (layers 1..) and gate_up weights with their input
+        norm's gamma folded in, for ``_forward_nf``: made where the regular packed copies
+        exist (ops/gemm.py pack_decode_weights) and the copies fit ``budget_fraction`` of
+        device memory (Llama-3-8B: 9.1 GB).  Call before the KV cache is sized."""
+        self._nf_w = None
+        if not (_nf_enabled and _tail_fusion_enabled and self._fusable and self.layers
+                and self.layers[0].input_layernorm.weight.is_cuda):
+            return 0
+        l0 = self.layers[0]
+        if any(p.bias is not None for p in (l0.self_attn.qkv_proj, l0.self_attn.o_proj,
+                                            l0.mlp.gate_up_proj, l0.mlp.down_proj)):
+            return 0
+        if any(gemm.packed_weight(l.self_attn.qkv_proj.weight) is None
+               or gemm.packed_weight(l.mlp.gate_up_proj.weight, True) is None
+               for l in self.layers):
+            return 0
+        need = sum(l.self_attn.qkv_proj.weight.numel() + l.mlp.gate_up_proj.weight.numel()
+                   for l in self.layers[1:]) * l0.mlp.gate_up_proj.weight.element_size()
+        need += l0.mlp.gate_up_proj.weight.numel() * l0.mlp.gate_up_proj.weight.element_size()
+        free, total = torch.cuda.mem_get_info(l0.input_layernorm.weight.device)
+        if need > budget_fraction * total or need > free - (8 << 30):
+            return 0
+        ws = []
+        for i, l in enumerate(self.layers):
+            qkv = (None if i == 0 else gemm.pack_folded(l.self_attn.qkv_proj.weight,
+                                                        l.input_layernorm.weight, False))
+            ws.append((qkv, gemm.pack_folded(l.mlp.gate_up_proj.weight,
+                                             l.post_attention_layernorm.weight, True)))
+        self._nf_w = ws
+        return need
+
+    def _nf_cfgs(self, M: int):
+        """K9m plans (qkv, o, gate_up, down) of the norm-free layer at this M, or None:
+        folded copies made, packed tiles for qkv / gate_up, and ``gemm.nf_plan``."""
+        if getattr(self, "_nf_w", None) is None:
+            return None
+        p = gemm.nf_plan(M, self._rs_shapes())
+        if p is None or not (gemm.cfg_packed(p[0][0]) and gemm.cfg_packed(p[2][0])):
+            return None
+        return p
+
+    def _forward_nf(self, positions, x, ctx, cfgs):
+        """The decoder at M = 65..512 with no RMSNorm or split-K reduction launch: o_proj
+        and down_proj run K9m's fan-in epilogue (the last K-slice of each column tile sums
+        the slabs, adds the residual and leaves row sums of squares; the last tile of a row
+        block turns them into r = rsqrt(mean(residual^2) + eps)); qkv and gate_up run on the
+        raw residual with gamma folded into their weights, and r scales their rows -- in the
+        decode-attention prologue (qkv) and in the SiLU epilogue (gate_up).  Per layer:
+        qkv, attention, o, gate_up, down: 5 launches against 7 on the tail-fused path.
+        Layer 0's input norm over the embedding stays a kernel (its qkv weight unfolded);
+        the final norm too."""
+        (cq, sq), (co, so), (cg, sg), (cd, sd) = cfgs
+        res = x
+        rs = None
+        n = len(self.layers)
+        for i, layer in enumerate(self.layers):
+            at, mlp = layer.self_attn, layer.mlp
+            qkv_f, gu_f = self._nf_w[i]
+            if i == 0:
+                qkv = gemm.dgemm(layer.input_layernorm(res), at.qkv_proj.weight, cq, sq)
+                a = at.attend(positions, qkv, ctx)
+            else:
+                qkv = gemm.dgemm(res, at.qkv_proj.weight, cq, sq, wk=qkv_f)
+                a = at.attend(positions, qkv, ctx, row_scale=rs)
+            rs = gemm.dgemm_fanin(a, at.o_proj.weight, co, so, res,
+                                  layer.post_attention_layernorm.eps)
+            h = gemm.nf_silu(res, mlp.gate_up_proj.weight, gu_f, cg, sg, rs)
+            eps = self.layers[i + 1].input_layernorm.eps if i + 1 < n else self.norm.eps
+            rs = gemm.dgemm_fanin(h, mlp.down_proj.weight, cd, sd, res, eps)
+        return self.norm(res)
 
     def _tp_tail_fusable(self) -> bool:
         """TP > 1, whole model, dense bias-free o / down projections: each row-parallel

@@ -264,12 +264,18 @@ def paged_attention_decode_rope(qkv: torch.Tensor, positions: torch.Tensor,
                                 k_norm_w: Optional[torch.Tensor] = None, eps: float = 1e-6,
                                 use_rope: bool = True, workspace=None, grid_z: int = 1,
                                 k_scale: float = 1.0, v_scale: float = 1.0,
-                                dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+                                dtype: Optional[torch.dtype] = None,
+                                row_scale: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``rope_kv_write`` + ``paged_attention_decode`` of a decode-only batch in ONE
     launch (K1 with K3/K5/K6 as its prologue): q is built in registers from the QKV
     projection (or its K9m fp32 split-K slices [S, B, N]), the new token's k / v are
-    written to the cache by the workgroup that reads them back.  -> [B, nq, d]."""
+    written to the cache by the workgroup that reads them back.  -> [B, nq, d].
+    ``row_scale`` [B] fp32: projection row b is scaled by it before its rounding (the
+    norm-free layer's rsqrt(mean(x^2) + eps) over a gamma-folded QKV weight)."""
     if not _gpu(qkv):
+        if row_scale is not None:
+            qkv = (qkv.float().sum(0) if qkv.dim() == 3 else qkv.float()) * row_scale[:, None]
+            qkv = qkv.to(dtype or torch.float32)
         q = ref.rope_qk_kv_write(qkv, positions, cos_sin, k_cache, v_cache, slot_mapping,
                                  num_heads, num_kv_heads, head_dim, q_norm_w, k_norm_w, eps,
                                  use_rope, k_scale, v_scale)
@@ -286,7 +292,8 @@ def paged_attention_decode_rope(qkv: torch.Tensor, positions: torch.Tensor,
     grid_z = min(grid_z, _decode_z_cap(workspace, B, num_heads))
     _k().paged_decode_rope(out, qkv, positions, cos_sin, k_cache, v_cache, slot_mapping,
                            q_norm_w, k_norm_w, block_tables, context_lens, ml, es, tmp,
-                           num_heads, grid_z, scale, eps, use_rope, k_scale, v_scale)
+                           num_heads, grid_z, scale, eps, use_rope, k_scale, v_scale,
+                           row_scale)
     return out
 
 

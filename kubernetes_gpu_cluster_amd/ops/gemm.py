@@ -59,6 +59,14 @@ _enabled = os.environ.get("KGC_SKINNY_GEMM", "1") != "0"
 # "tail" (o / down -> residual add + RMSNorm).  S > 1: fp32 K-slices summed by the consumer.
 DG_MAX_M = 512
 _plan_dg: dict[tuple[int, int, int, str], tuple[int, int]] = {}
+# the norm-free layer at M = 65..512 (``nf_plan``): (M, N, K) of an o / down projection ->
+# (cfg, S, fan-in us, tail us): its fastest EPI_FANIN configuration and, graph-timed in the
+# same interleaved rounds, the regular tail it would replace (the "tail" plan + its
+# splitk_add_rms_norm / fused_add_rms_norm)
+_plan_fanin: dict[tuple[int, int, int], tuple[int, int, float, float]] = {}
+_fanin_enabled = os.environ.get("KGC_FANIN", "1") != "0"
+# A/B: run the norm-free layer wherever its plans exist, measured faster or not
+_nf_force = os.environ.get("KGC_NF_FORCE", "0") == "1"
 _dg_enabled = os.environ.get("KGC_DGEMM", "1") != "0"
 # packed weight copies for the packed K9m tiles: (data_ptr, silu) -> [N/128, K/64, 8192]
 # (data_ptr, silu) -> (weakref to the source weight, packed copy).  The weakref drops the
@@ -140,19 +148,39 @@ def packed_weight(w: torch.Tensor, silu: bool = False) -> Optional[torch.Tensor]
     return _packed_get(w, silu)
 
 
+def pack_folded(w: torch.Tensor, gamma: torch.Tensor, silu: bool) -> torch.Tensor:
+    """The packed K9m tiles of W diag(gamma) (``fold_norm_weight``): the norm-free layer's
+    qkv / gate_up operand (the row-major folded copy is freed again)."""
+    from . import _k
+    f = fold_norm_weight(w, gamma)
+    N, K = w.shape
+    p = torch.empty(N // 128, K // 64, 8192, dtype=w.dtype, device=w.device)
+    _k().dgemm_pack(p, f, silu)
+    return p
+
+
+def cfg_packed(cfg: int) -> bool:
+    return _dg_info(cfg)[2]
+
+
 def _dg_weight(w: torch.Tensor, cfg: int, silu: bool) -> Optional[torch.Tensor]:
     return packed_weight(w, silu) if _dg_info(cfg)[2] else w
 
 
 def dgemm(x: torch.Tensor, w: torch.Tensor, cfg: int, S: int, epi: int = 1,
-          out: Optional[torch.Tensor] = None, silu_w: bool = False) -> torch.Tensor:
+          out: Optional[torch.Tensor] = None, silu_w: bool = False,
+          rscale: Optional[torch.Tensor] = None, wk: Optional[torch.Tensor] = None) -> torch.Tensor:
     """K9m: S == 1 -> x W^T in x's dtype (epi 1) or silu-paired [M, N/2] (epi 2);
     S > 1 -> the [S, M, N] fp32 K-slices (the caller's consumer sums them).  silu_w: a
     merged gate_up weight's slices from its SiLU-packed copy (packed cfgs: gate / up
-    16-column groups interleaved per tile, ``splitk_reduce_silu(interleaved=True)``)."""
+    16-column groups interleaved per tile, ``splitk_reduce_silu(interleaved=True)``).
+    rscale [M] fp32 (S == 1): output row m scaled by rscale[m] (before the SiLU).  wk: the
+    weight in the layout ``cfg`` streams (default: ``w``'s packed copy or ``w``) -- the
+    norm-free layer's gamma-folded copies."""
     from . import _k
     M, N = x.shape[0], w.shape[0]
-    wk = _dg_weight(w, cfg, epi == 2 or silu_w)
+    if wk is None:
+        wk = _dg_weight(w, cfg, epi == 2 or silu_w)
     if wk is None:
         raise RuntimeError("K9m plan names a packed tile but the weight was not packed")
     if S > 1:
@@ -161,14 +189,66 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, cfg: int, S: int, epi: int = 1,
     else:
         if out is None:
             out = torch.empty(M, N // 2 if epi == 2 else N, dtype=x.dtype, device=x.device)
-        _k().dgemm(out, x, wk, cfg, epi)
+        _k().dgemm(out, x, wk, cfg, epi, rscale)
     return out
+
+
+class _NormFreeBuffers:
+    """Per-device state of the K9m fan-in epilogue (EPI_FANIN): per-tile row sums of
+    squares, the row scales rs = rsqrt(mean(x^2) + eps) its consumers read, and the
+    ticket counters (zero between launches: every launch leaves them zero)."""
+
+    def __init__(self, device):
+        self.ssp = torch.zeros(DG_MAX_M * 128, dtype=torch.float32, device=device)
+        self.rs = torch.zeros(DG_MAX_M, dtype=torch.float32, device=device)
+        self.cnt = torch.zeros(1024, dtype=torch.int32, device=device)
+
+
+_nf_bufs: dict = {}
+
+
+def _nf_state(device: torch.device) -> _NormFreeBuffers:
+    b = _nf_bufs.get(device)
+    if b is None:
+        b = _nf_bufs[device] = _NormFreeBuffers(device)
+    return b
+
+
+def dgemm_fanin(x: torch.Tensor, w: torch.Tensor, cfg: int, S: int, residual: torch.Tensor,
+                eps: float) -> torch.Tensor:
+    """residual += x W^T with the split-K combine, the residual add and the row norms in
+    ONE K9m launch (EPI_FANIN, gemm_decode.hip): returns rs [M] fp32 =
+    rsqrt(mean(residual^2) + eps), the row scale of the next RMSNorm, which the norm-free
+    layer's consumers apply to their gamma-folded weights' outputs.  rs lives in a
+    per-device buffer that the next fan-in launch overwrites."""
+    from . import _k
+    M, N = x.shape[0], w.shape[0]
+    wk = _dg_weight(w, cfg, False)
+    if wk is None:
+        raise RuntimeError("K9m plan names a packed tile but the weight was not packed")
+    st = _nf_state(x.device)
+    ws = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
+    _k().dgemm_fanin(ws, x, wk, cfg, residual, st.ssp, st.rs, st.cnt, eps)
+    return st.rs[:M]
 
 
 def _dg_plan(x: torch.Tensor, w: torch.Tensor, kind: str):
     if not _plan_dg or not x.is_cuda or x.dim() != 2 or x.stride(1) != 1 or x.stride(0) % 8:
         return None
     return _plan_dg.get((x.shape[0], w.shape[0], w.shape[1], kind))
+
+
+def nf_silu(x: torch.Tensor, w: torch.Tensor, wf: torch.Tensor, cfg: int, S: int,
+            rscale: torch.Tensor) -> torch.Tensor:
+    """silu(r * g) * (r * u) of the norm-free layer's merged gate_up: x the raw residual,
+    ``wf`` the gamma-folded weight in ``cfg``'s layout, r = ``rscale`` per row."""
+    from . import _k
+    if S == 1:
+        return dgemm(x, w, cfg, 1, epi=2, rscale=rscale, wk=wf)
+    ws = dgemm(x, w, cfg, S, wk=wf)
+    out = torch.empty(x.shape[0], w.shape[0] // 2, dtype=x.dtype, device=x.device)
+    _k().splitk_reduce_silu(out, ws, _dg_info(cfg)[2], rscale)
+    return out
 
 
 def linear_silu(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -396,7 +476,35 @@ def norm_fused_cfg(M: int, N: int, K: int):
     return cfg if t < 0.98 * plain else None
 
 
+def nf_plan(M: int, shapes) -> Optional[list]:
+    """K9m plans of (qkv, o, gate_up, down) at this M for the norm-free layer
+    (``LlamaForCausalLM._forward_nf``), or None: qkv / gate_up run on K9m ("qkv" / "silu"
+    plans; gate_up's S = 1 epilogue needs a config with the row-scale epilogue), o / down on
+    their fan-in plans, and tuning measured the two fan-in launches faster than the
+    regular tails they replace."""
+    if not (_fanin_enabled and SKINNY_MAX_M < M <= DG_MAX_M):
+        return None
+    from . import _k
+    (nq, kq), (no, ko), (ng, kg), (nd, kd) = shapes
+    q = _plan_dg.get((M, nq, kq, "qkv"))
+    g = _plan_dg.get((M, ng, kg, "silu"))
+    o = _plan_fanin.get((M, no, ko))
+    d = _plan_fanin.get((M, nd, kd))
+    if q is None or g is None or o is None or d is None:
+        return None
+    if g[1] == 1 and not _k().dgemm_cfg_has_aux(g[0]):
+        return None
+    if o[2] + d[2] >= o[3] + d[3] and not _nf_force:
+        return None
+    return [q, (o[0], o[1]), g, (d[0], d[1])]
+
+
+def fanin_plan() -> dict:
+    return dict(_plan_fanin)
+
+
 def clear_plan() -> None:
+    _plan_fanin.clear()
     _best_sk.clear()
     _best_silu.clear()
     _best_rs.clear()
@@ -494,7 +602,8 @@ def _time_graphed(body, reps: int) -> float:
 @torch.inference_mode()
 def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: float = 0.97,
                 reps: int = 3, norm_shapes=(), norm_max_m: int = 16, silu_shapes=(),
-                tail_shapes=(), qkv_dims=None, rs_shapes: bool = False) -> dict:
+                tail_shapes=(), qkv_dims=None, rs_shapes: bool = False,
+                nf: bool = False) -> dict:
     """Time hipBLASLt against every skinny configuration for each weight shape and
     batch size M (decode buckets <= SKINNY_MAX_M) and record the skinny kernel where it
     is faster by more than ``1 - margin``.  Each timing sweeps ALL weights of the shape
@@ -506,7 +615,9 @@ def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: floa
     ``tail_shapes``: (N, K) of row-parallel projections feeding a residual add + RMSNorm
     (``linear_add_rms``), timed with that norm on both sides.  ``rs_shapes``: also time the
     norm-free layer's epilogues at M <= 16 (tail -> SK_ACC_SS, norm -> SK_RSCALE, silu ->
-    SK_RSCALE_SILU) for ``rs_plan``."""
+    SK_RSCALE_SILU) for ``rs_plan``.  ``nf``: also time the o / down projections' K9m
+    fan-in epilogue against their regular tails for ``nf_plan`` (the norm-free layer at
+    M = 65..512)."""
     if not _enabled:
         return {}
     by_shape: dict[tuple[int, int], list[torch.Tensor]] = {}
@@ -564,7 +675,7 @@ def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: floa
             kind = ("silu" if (N, K) in silu_shapes else
                     "tail" if (N, K) in tail_shapes else "qkv" if qd else "plain")
             _tune_dgemm(ws, N, K, [m for m in ms if SKINNY_MAX_M < m <= DG_MAX_M], margin,
-                        reps, res, kind, qd)
+                        reps, res, kind, qd, fanin=nf)
     log.info("GEMM tuning: %d shapes in %.1f s", len(res), time.time() - t0)
     return res
 
@@ -606,7 +717,7 @@ def _dg_candidates(M: int, N: int, K: int, kind: str, packed: bool):
 
 
 def _tune_dgemm(ws, N: int, K: int, ms, margin: float, reps: int, res: dict,
-                kind: str, qkv_dims=None) -> None:
+                kind: str, qkv_dims=None, fanin: bool = False) -> None:
     """hipBLASLt vs the K9m candidates at each M in ``ms``, over all weights of the shape
     (HBM-resident, as in a decode step), each side timed WITH its consumer: "silu" the
     SiLU-and-mul, "tail" the residual add + RMSNorm, "qkv" the fused RoPE / KV-write /
@@ -707,6 +818,59 @@ def _tune_dgemm(ws, N: int, K: int, ms, margin: float, reps: int, res: dict,
         log.info("gemm M=%d N=%d K=%d %s: hipBLASLt %.1f us, K9m %s %.1f us -> %s", M, N, K,
                  kind, lib_t * 1e3 / n, best_cfg, best_t * 1e3 / n,
                  "K9m" if chosen else "hipBLASLt")
+        if kind == "tail" and fanin and _fanin_enabled:
+            tail_fn = dict((c, fn) for _, c, fn in timed).get(chosen, lib)
+            _tune_fanin(ws, x, M, N, K, reps, packed, tail_fn, res)
+
+
+_FANIN_SPLITS = (1, 2, 3, 4, 5, 6, 8)      # the S values gemm_decode.hip's reducer unrolls
+
+
+def _tune_fanin(ws, x, M: int, N: int, K: int, reps: int, packed: bool, tail_fn,
+                res: dict) -> None:
+    """The EPI_FANIN candidates of an o / down projection (split-K combine + residual add +
+    row norms in the launch) against the regular tail the norm-free layer would replace
+    (``tail_fn``: the chosen K9m / hipBLASLt GEMM + its norm kernel).  One eager pass ranks
+    the candidates; the fastest few and the tail are then re-timed graph-captured (the
+    tail's extra launch boundary counts as it does in a decode step) in interleaved
+    rounds, medians decide."""
+    from . import _k
+    dev, dt = x.device, x.dtype
+    resid = torch.zeros(M, N, dtype=dt, device=dev)
+    timed = []
+    cfgs = [5, 7, 2] if M <= 128 else [6, 4, 0, 10, 5, 7]
+    for c in cfgs:
+        bm, bn, pk = _dg_info(c)
+        if (pk and not packed) or N % bn or not _k().dgemm_cfg_has_aux(c):
+            continue
+        for S in _FANIN_SPLITS:
+            if S > K // 64:
+                continue
+
+            def run(c=c, S=S):
+                for w in ws:
+                    dgemm_fanin(x, w, c, S, resid, 1e-6)
+            timed.append((_time(run, reps), (c, S), run))
+            log.debug("gemm M=%d N=%d K=%d fan-in %s: %.1f us", M, N, K, (c, S),
+                      timed[-1][0] * 1e3 / len(ws))
+    if not timed:
+        return
+    timed.sort(key=lambda e: e[0])
+    top = timed[:_DG_REFINE]
+    rounds: dict = {c: [] for _, c, _ in top}
+    tail_r = []
+    for _ in range(_DG_REFINE_ROUNDS):
+        tail_r.append(_time_graphed(tail_fn, reps))
+        for _, c, fn in top:
+            rounds[c].append(_time_graphed(fn, reps))
+    med = {c: sorted(v)[len(v) // 2] for c, v in rounds.items()}
+    best = min(med, key=med.get)
+    n = len(ws)
+    fan_us, tail_us = med[best] * 1e3 / n, sorted(tail_r)[len(tail_r) // 2] * 1e3 / n
+    _plan_fanin[(M, N, K)] = (best[0], best[1], fan_us, tail_us)
+    res[(M, N, K, "fanin")] = (best, tail_us, fan_us, best)
+    log.info("gemm M=%d N=%d K=%d fan-in: tail %.1f us, EPI_FANIN %s %.1f us", M, N, K,
+             tail_us, best, fan_us)
 
 
 def _tune_silu(ws, x, M: int, N: int, K: int, reps: int, margin: float) -> None:

@@ -1028,6 +1028,179 @@ def test_tail_fused_model_matches_regular_path(gpu):
     torch.testing.assert_close(got.float(), ref_out.float(), atol=6e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("M,N,K,cfg,S", [(256, 4096, 4096, 6, 4), (256, 4096, 14336, 6, 8),
+                                         (256, 4096, 4096, 5, 4), (200, 4096, 4096, 10, 2),
+                                         (96, 1024, 2048, 5, 3), (130, 2048, 1024, 4, 1),
+                                         (256, 1024, 2048, 1, 5), (72, 1024, 1024, 3, 6),
+                                         (256, 4096, 4096, 7, 2), (256, 2048, 2048, 0, 2)])
+def test_dgemm_fanin_matches_fp32(gpu, M, N, K, cfg, S):
+    """K9m EPI_FANIN (the norm-free layer's o / down): split-K combine by the last slice of
+    each tile, residual add and row norms in one launch, vs fp32: residual += x W^T and
+    rs = rsqrt(mean(residual^2) + eps) of the residual as stored.  Repeated calls and graph
+    replays re-arm the tickets (counters back at zero), and the combine is deterministic
+    (slices summed in slice order whichever arrives last: bit-identical reruns)."""
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    torch.manual_seed(M + N + S)
+    x = torch.randn(M, K, dtype=torch.bfloat16, device=gpu)
+    w = torch.randn(N, K, dtype=torch.bfloat16, device=gpu) * K ** -0.5
+    res0 = torch.randn(M, N, dtype=torch.bfloat16, device=gpu)
+    eps = 1e-5
+    if gemm.cfg_packed(cfg):
+        gemm.pack_decode_weights([w], [])
+    try:
+        r32 = res0.float().cpu() + x.float().cpu() @ w.float().cpu().t()
+        outs = []
+        for _ in range(3):
+            res = res0.clone()
+            rs = gemm.dgemm_fanin(x, w, cfg, S, res, eps)
+            torch.cuda.synchronize()
+            torch.testing.assert_close(res.float().cpu(), r32, atol=5e-2, rtol=2e-2)
+            rb = res.float().cpu()
+            exact = torch.rsqrt(rb.pow(2).mean(-1) + eps)
+            torch.testing.assert_close(rs.cpu(), exact, atol=0, rtol=1e-4)
+            outs.append(res.clone())
+        assert all(torch.equal(o, outs[0]) for o in outs[1:])
+        st = gemm._nf_state(x.device)
+        assert int(st.cnt.abs().sum()) == 0
+        res = res0.clone()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            rs_g = gemm.dgemm_fanin(x, w, cfg, S, res, eps)
+        for _ in range(2):
+            res.copy_(res0)
+            st.rs.fill_(float("nan"))
+            g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(res, outs[0])
+            torch.testing.assert_close(rs_g.cpu(), exact, atol=0, rtol=1e-4)
+        assert int(st.cnt.abs().sum()) == 0
+    finally:
+        gemm._packed.clear()
+
+
+@pytest.mark.parametrize("M,N,K,cfg,S", [(256, 4096, 2048, 6, 1), (96, 2048, 1024, 5, 1),
+                                         (256, 2048, 1024, 4, 3), (100, 1024, 1024, 2, 2),
+                                         (256, 1024, 1024, 0, 1)])
+def test_dgemm_row_scale_silu_matches_fp32(gpu, M, N, K, cfg, S):
+    """The norm-free gate_up: silu(r * g) * (r * u) over a merged weight, r per row -- in
+    the K9m SiLU epilogue (S = 1) or in splitk_reduce_silu (S > 1) -- vs fp32; and the
+    EPI_OUT row scale."""
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    torch.manual_seed(M + K)
+    x = torch.randn(M, K, dtype=torch.bfloat16, device=gpu)
+    w = torch.randn(N, K, dtype=torch.bfloat16, device=gpu) * K ** -0.5
+    r = torch.rand(M, dtype=torch.float32, device=gpu) + 0.5
+    y = (x.float().cpu() @ w.float().cpu().t()) * r.cpu()[:, None]
+    ref = torch.nn.functional.silu(y[:, : N // 2]) * y[:, N // 2:]
+    pk = gemm.cfg_packed(cfg)
+    wk = gemm.pack_folded(w, torch.ones(K, dtype=w.dtype, device=gpu), True) if pk else w
+    got = gemm.nf_silu(x, w, wk, cfg, S, r)
+    torch.testing.assert_close(got.float().cpu(), ref, atol=3e-2, rtol=2e-2)
+    wo = gemm.pack_folded(w, torch.ones(K, dtype=w.dtype, device=gpu), False) if pk else w
+    out = gemm.dgemm(x, w, cfg, 1, epi=1, rscale=r, wk=wo)
+    torch.testing.assert_close(out.float().cpu(), y, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("S", [0, 4, 5])
+def test_paged_decode_rope_row_scale(gpu, monkeypatch, S):
+    """The fused decode-attention prologue with the norm-free row scale: slices (or the bf16
+    projection) scaled per row inside the kernel == the same kernel fed the pre-scaled
+    projection, for the attention output and the written K / V."""
+    torch.manual_seed(S + 3)
+    B, nq, nkv, d, bs = 96, 32, 8, 128, 32
+    N = (nq + 2 * nkv) * d
+    ctx_len = 200
+    nblk = (ctx_len + bs - 1) // bs
+    kc0 = torch.randn(B * nblk + 1, nkv, bs, d, dtype=torch.bfloat16, device=gpu) * 0.5
+    vc0 = torch.randn(B * nblk + 1, nkv, bs // 8, d, 8, dtype=torch.bfloat16, device=gpu) * 0.5
+    bt = (torch.arange(B * nblk, dtype=torch.int32, device=gpu) + 1).view(B, nblk)
+    cl = torch.full((B,), ctx_len, dtype=torch.int32, device=gpu)
+    pos = (cl - 1).to(torch.int64)
+    slots = (bt[:, (ctx_len - 1) // bs].to(torch.int64) * bs + (ctx_len - 1) % bs)
+    cs = torch.randn(4096, d, dtype=torch.float32, device=gpu)
+    r = torch.rand(B, dtype=torch.float32, device=gpu) + 0.5
+    if S:
+        sl = torch.randn(S, B, N, dtype=torch.float32, device=gpu) * 0.5
+        pre = (sl.sum(0) * r[:, None]).to(torch.bfloat16)
+        raw = sl
+    else:
+        raw = torch.randn(B, N, dtype=torch.bfloat16, device=gpu)
+        pre = (raw.float() * r[:, None]).to(torch.bfloat16)
+
+    def run(qkv, rsc):
+        kc, vc = kc0.clone(), vc0.clone()
+        o = ops.paged_attention_decode_rope(qkv, pos, cs, kc, vc, slots, nq, nkv, d, bt, cl,
+                                            d ** -0.5, dtype=torch.bfloat16, row_scale=rsc)
+        return o, kc, vc
+    o1, k1, v1 = run(raw, r)
+    o2, k2, v2 = run(pre, None)
+    torch.testing.assert_close(o1.float(), o2.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(k1.float(), k2.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(v1.float(), v2.float(), atol=2e-2, rtol=2e-2)
+
+
+def test_nf_model_matches_regular_path(gpu):
+    """Whole-model forward through the norm-free mid-M layer (forced plans: K9m qkv split-K
+    on a gamma-folded copy, the o / down fan-in epilogues, the row-scaled SiLU epilogue) vs
+    the regular layer loop on the same weights, with non-unit norm weights so the folding
+    is exercised."""
+    from kubernetes_gpu_cluster_amd.models import configs
+    from kubernetes_gpu_cluster_amd.models.llama import LlamaAttention, LlamaForCausalLM
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    from kubernetes_gpu_cluster_amd.models import llama as llama_mod
+    cfg = configs.PRESETS["llama-3-8b"].shrink(name="nf-layer", num_layers=3)
+    torch.manual_seed(2)
+    model = LlamaForCausalLM(cfg, torch.bfloat16, gpu)
+    for n, p in model.named_parameters():
+        if p.dim() == 2:
+            p.data.normal_(0, 0.02)
+        else:
+            p.data.uniform_(0.6, 1.4)
+    M = 96
+    ids = torch.randint(0, cfg.vocab_size, (M,), device=gpu)
+
+    class _Ctx:
+        pass
+    for l in model.layers:
+        def stub(positions, qkv, ctx, row_scale=None, nq=l.self_attn.nq * cfg.head_dim):
+            if row_scale is not None:
+                qkv = LlamaAttention._scaled_rows(qkv, row_scale, torch.bfloat16)
+            elif qkv.dim() == 3:
+                qkv = qkv.sum(0).to(torch.bfloat16)
+            return qkv[:, :nq].contiguous()
+        l.self_attn.attend = stub
+    l0 = model.layers[0]
+    plain = [w for l in model.layers for w in (l.self_attn.qkv_proj.weight,
+                                                l.self_attn.o_proj.weight, l.mlp.down_proj.weight)]
+    gemm.pack_decode_weights(plain, [l.mlp.gate_up_proj.weight for l in model.layers])
+    try:
+        llama_mod._tail_fusion_enabled = False
+        ref_out = model(ids, None, _Ctx())
+        llama_mod._tail_fusion_enabled = True
+        assert model.fold_nf_weights() > 0
+        sh = model._rs_shapes()
+        gemm._plan_dg[(M, *sh[0], "qkv")] = (5, 2)
+        gemm._plan_dg[(M, *sh[2], "silu")] = (5, 1)
+        gemm._plan_dg[(M, *sh[1], "tail")] = (5, 4)
+        gemm._plan_dg[(M, *sh[3], "tail")] = (5, 4)
+        gemm._plan_fanin[(M, *sh[1])] = (5, 4, 1.0, 2.0)
+        gemm._plan_fanin[(M, *sh[3])] = (7, 8, 1.0, 2.0)
+        x = model.embed_tokens(ids)
+        assert model._tail_fusable(x) and model._nf_cfgs(M) is not None
+        got = model(ids, None, _Ctx())
+        # the regular tail-fused path on the same plans, for scale
+        gemm._plan_fanin.clear()
+        assert model._nf_cfgs(M) is None
+        tail = model(ids, None, _Ctx())
+    finally:
+        gemm.clear_plan()
+        gemm._packed.clear()
+        llama_mod._tail_fusion_enabled = True
+        model._nf_w = None
+    torch.testing.assert_close(tail.float(), ref_out.float(), atol=6e-2, rtol=3e-2)
+    torch.testing.assert_close(got.float(), ref_out.float(), atol=6e-2, rtol=3e-2)
+
+
 @pytest.mark.parametrize("M,N,K,cfg", [(1, 4096, 4096, (1, 1, 4, True)),
                                        (5, 4096, 14336, (1, 2, 8, False)),
                                        (16, 1024, 2048, (1, 1, 16, True)),
