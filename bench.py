@@ -114,6 +114,16 @@ def _k9m_plan() -> dict:
     return gemm.dgemm_plan()
 
 
+def _k9m_top() -> dict:
+    """The K9m selections at the largest decode M (the batch-256 step), "NxK:kind" ->
+    [cfg, S]: which kernels the timed decode steps ran."""
+    plan = _k9m_plan()
+    if not plan:
+        return {}
+    mx = max(k[0] for k in plan)
+    return {f"{n}x{k}:{kind}": list(v) for (m, n, k, kind), v in sorted(plan.items()) if m == mx}
+
+
 def run_wave(engine, args, wave: int, rank: int):
     from kubernetes_gpu_cluster_amd.engine.sequence import SamplingParams
     g = torch.Generator().manual_seed(1000 * wave + rank)
@@ -212,6 +222,7 @@ def main_engine(args):
     # the all-reduce policy this node's start-up calibration chose (read before shutdown
     # releases the xGMI buffers)
     ar_cal = getattr(comm.get_custom_allreduce(), "calibration", None)
+    nf = _nf_report(engine) if is_driver and not cpu else None
     if is_driver:
         engine.shutdown()
     # aggregate over replicas (drivers) -- every rank participates in the collectives
@@ -244,6 +255,7 @@ def main_engine(args):
             "engine_steps": steps,
             "k9_skinny_gemm_shapes": len(_k9_plan()),
             "k9m_gemm_shapes": len(_k9m_plan()),
+            "k9m_plan_max_m": _k9m_top(),
             "config": {"model": args.model, "global_batch": args.num_prompts * replicas,
                        "seq_len": args.input_len + args.output_len, "input_len": args.input_len,
                        "output_len": args.output_len,
@@ -257,6 +269,8 @@ def main_engine(args):
         }
         if tp > 1:
             out["ar_calibration"] = ar_cal
+        if nf is not None:
+            out["nf_layer"] = nf
         if phantom > 1:
             out["phantom_tp"] = phantom
             out["data"] += "; ONE phantom TP rank (peers contribute zeros): per-rank timing only"
@@ -275,6 +289,23 @@ def _note(msg: str) -> None:
 
 
 _port_locks: list = []
+
+
+def _nf_report(engine):
+    """The norm-free mid-M layer's start-up decision (models/llama.py _forward_nf): whether
+    the gamma-folded copies exist, the tuner's fan-in vs regular-tail timings per (M, N, K)
+    and the decode sizes that run it."""
+    try:
+        from kubernetes_gpu_cluster_amd.ops import gemm
+        model = engine.executor.worker.model
+    except AttributeError:
+        return None
+    folded = getattr(model, "_nf_w", None) is not None
+    plans = {f"{m}x{n}x{k}": {"cfg": c, "S": s, "fanin_us": round(f, 2), "tail_us": round(t, 2)}
+             for (m, n, k), (c, s, f, t) in sorted(gemm.fanin_plan().items())}
+    ms = sorted({m for (m, _, _) in gemm.fanin_plan()})
+    runs = [m for m in ms if folded and model._nf_cfgs(m) is not None]
+    return {"folded": folded, "fanin_vs_tail": plans, "runs_at_m": runs}
 
 
 def _free_port(local_rank: int, slot: int) -> int:

@@ -723,6 +723,9 @@ class ModelRunner:
             # K9: per decode bucket and weight shape, hipBLASLt or the skinny GEMM --
             # whichever measured faster on this model's weights (ops/gemm.py)
             from ..ops import gemm
+            # offline K9m selections for this model, where a table was made (the start-up
+            # tuner then times only what the table does not cover)
+            gemm.load_dg_table(self.mcfg.name, self.ps.tp_size)
             ns = getattr(self.model, "fused_norm_shapes", lambda: set())()
             gemm.tune_skinny([p for p in self.model.parameters() if p.dim() == 2],
                              self.buckets, norm_shapes=ns,

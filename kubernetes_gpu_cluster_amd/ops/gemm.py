@@ -476,6 +476,56 @@ def norm_fused_cfg(M: int, N: int, K: int):
     return cfg if t < 0.98 * plain else None
 
 
+# offline K9m selections (tools/tune_dgemm_table.py): (M, N, K, kind) -> (cfg, S), or None
+# where hipBLASLt won.  Start-up tuning skips these: its short interleaved timing picked
+# configurations up to ~0.35 ms per batch-256 decode step apart from one engine start to
+# the next; the offline table is the median of many more rounds, and makes the chosen
+# kernels the same in every run.  Empty unless ``load_dg_table`` found a table.
+_dg_table: dict[tuple[int, int, int, str], Optional[tuple[int, int]]] = {}
+
+
+def dg_table_path(model: str, tp: int = 1) -> str:
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    return os.path.join(root, "profiles", "tunableop", f"k9m_{model}_tp{tp}_gfx950.json")
+
+
+def load_dg_table(model: str, tp: int = 1) -> int:
+    """Read the offline K9m table of this model / TP degree (KGC_DGEMM_TABLE: another file;
+    "0": none).  Returns the entries loaded."""
+    import json
+    _dg_table.clear()
+    path = os.environ.get("KGC_DGEMM_TABLE") or dg_table_path(model, tp)
+    if path == "0" or not os.path.exists(path):
+        return 0
+    with open(path) as f:
+        t = json.load(f)
+    for e in t.get("entries", []):
+        key = (int(e["M"]), int(e["N"]), int(e["K"]), str(e["kind"]))
+        _dg_table[key] = None if e.get("cfg") is None else (int(e["cfg"]), int(e["S"]))
+    log.info("K9m: %d offline selections from %s", len(_dg_table), path)
+    return len(_dg_table)
+
+
+def save_dg_table(path: str, res: dict, meta: dict) -> int:
+    """Write the K9m decisions of a tuner run (``tune_skinny``'s result dict)."""
+    import json
+    ent = []
+    for key, v in sorted(res.items()):
+        if len(key) != 4 or key[3] not in ("plain", "silu", "tail", "qkv"):
+            continue
+        M, N, K, kind = key
+        chosen, lib_us, best_us, best = v
+        ent.append({"M": M, "N": N, "K": K, "kind": kind,
+                    "cfg": None if chosen is None else chosen[0],
+                    "S": None if chosen is None else chosen[1],
+                    "k9m_us": round(best_us, 2), "hipblaslt_us": round(lib_us, 2),
+                    "best_k9m": list(best) if best else None})
+    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+    with open(path, "w") as f:
+        json.dump(dict(meta, entries=ent), f, indent=1)
+    return len(ent)
+
+
 def nf_plan(M: int, shapes) -> Optional[list]:
     """K9m plans of (qkv, o, gate_up, down) at this M for the norm-free layer
     (``LlamaForCausalLM._forward_nf``), or None: qkv / gate_up run on K9m ("qkv" / "silu"
@@ -504,6 +554,7 @@ def fanin_plan() -> dict:
 
 
 def clear_plan() -> None:
+    _dg_table.clear()
     _plan_fanin.clear()
     _best_sk.clear()
     _best_silu.clear()
@@ -729,6 +780,17 @@ def _tune_dgemm(ws, N: int, K: int, ms, margin: float, reps: int, res: dict,
     for M in sorted(set(ms)):
         if not dgemm_ok(M, N, K) or (kind == "tail" and N > 8192):
             continue
+        key = (M, N, K, kind)
+        if key in _dg_table:
+            fixed = _dg_table[key]
+            if fixed is None or packed or not _dg_info(fixed[0])[2]:
+                if fixed is not None:
+                    _plan_dg[key] = fixed
+                res[key] = (fixed, float("nan"), float("nan"), fixed)
+                if kind == "tail" and fanin and _fanin_enabled:
+                    x = torch.randn(M, K, dtype=ws[0].dtype, device=ws[0].device)
+                    _tune_fanin(ws, x, M, N, K, reps, packed, _tail_runner(ws, x, fixed), res)
+                continue
         dev, dt = ws[0].device, ws[0].dtype
         x = torch.randn(M, K, dtype=dt, device=dev)
         res_t = torch.zeros(M, N, dtype=dt, device=dev) if kind == "tail" else None
@@ -824,6 +886,35 @@ def _tune_dgemm(ws, N: int, K: int, ms, margin: float, reps: int, res: dict,
 
 
 _FANIN_SPLITS = (1, 2, 3, 4, 5, 6, 8)      # the S values gemm_decode.hip's reducer unrolls
+
+
+def _tail_runner(ws, x, plan):
+    """The regular tail of a row-parallel projection under ``plan`` ((cfg, S) or None =
+    hipBLASLt): GEMM + its residual add / RMSNorm kernel, over every weight of the shape."""
+    from . import _k, fused_add_rms_norm
+    M, N = x.shape[0], ws[0].shape[0]
+    res_t = torch.zeros(M, N, dtype=x.dtype, device=x.device)
+    gamma = torch.ones(N, dtype=x.dtype, device=x.device)
+    red = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    if plan is None:
+        def run():
+            for w in ws:
+                fused_add_rms_norm(F.linear(x, w), res_t, gamma, 1e-6)
+        return run
+    cfg, S = plan
+    wl = [_dg_weight(w, cfg, False) for w in ws]
+    buf = (torch.empty(S, M, N, dtype=torch.float32, device=x.device) if S > 1 else
+           torch.empty(M, N, dtype=x.dtype, device=x.device))
+
+    def run():
+        for w in wl:
+            if S == 1:
+                _k().dgemm(buf, x, w, cfg, 1)
+                fused_add_rms_norm(buf, res_t, gamma, 1e-6)
+            else:
+                _k().dgemm(buf, x, w, cfg, 0)
+                _k().splitk_add_rms_norm(red, buf, res_t, gamma, 1e-6)
+    return run
 
 
 def _tune_fanin(ws, x, M: int, N: int, K: int, reps: int, packed: bool, tail_fn,
