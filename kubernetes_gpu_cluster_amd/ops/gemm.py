@@ -638,6 +638,16 @@ def _time(fn, reps: int) -> float:
     return e0.elapsed_time(e1) / reps
 
 
+def _graph_of(body):
+    """``body`` captured once into a hipGraph; returns its replay."""
+    body()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        body()
+    return g.replay
+
+
 def _time_graphed(body, reps: int) -> float:
     """``_time`` of ``body`` captured in one hipGraph: candidates that differ in launch
     count are compared as a decode graph replays them (eager timing would add the host's
@@ -858,16 +868,22 @@ def _tune_dgemm(ws, N: int, K: int, ms, margin: float, reps: int, res: dict,
         # refine: the few fastest candidates and the library re-timed in interleaved
         # rounds, median of each -- one short pass ranked near-ties by clock noise (the
         # same tree picked configurations 1-3 us per call apart from one engine start to
-        # the next: ~0.25 ms of a batch-256 decode step)
+        # the next: ~0.25 ms of a batch-256 decode step).  The rounds replay each side
+        # captured in a hipGraph, as the decode step runs it: eagerly timed, Llama-3-8B's
+        # down_proj ranked S = 6 ahead of S = 8, which runs 41.5 vs 33.4 us in the engine's
+        # graphs (profiles/k9m_tuner_eager_vs_graph_r5.txt)
         timed.sort(key=lambda e: e[0])
         top = timed[:_DG_REFINE]
         if top:
             rounds: dict = {c: [] for _, c, _ in top}
             lib_r = []
+            lib_g = _graph_of(lib)
+            graphs = [(c, _graph_of(fn)) for _, c, fn in top]
             for _ in range(_DG_REFINE_ROUNDS):
-                lib_r.append(_time(lib, reps))
-                for _, c, fn in top:
-                    rounds[c].append(_time(fn, reps))
+                lib_r.append(_time(lib_g, reps))
+                for c, g in graphs:
+                    rounds[c].append(_time(g, reps))
+            del graphs, lib_g
             med = {c: sorted(v)[len(v) // 2] for c, v in rounds.items()}
             best_cfg = min(med, key=med.get)
             best_t = med[best_cfg]
