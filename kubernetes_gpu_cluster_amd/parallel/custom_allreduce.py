@@ -120,6 +120,8 @@ class CustomAllReduce:
         self.table: Optional[list] = None
         self.calibration: Optional[dict] = None
         self.launches: collections.Counter = collections.Counter()   # form -> host launches
+        # ... of them decided by a calibrated table entry (the rest: sizes past the table)
+        self.table_launches: collections.Counter = collections.Counter()
 
     def _set_bases(self, bases: list, sig_bytes: int) -> None:
         self.sig = bases
@@ -149,6 +151,11 @@ class CustomAllReduce:
             return e[1]
         if nb > self.cap:
             return "rccl"
+        if self.table and self.table[-1][1] != "one":
+            # past the calibrated sizes (prefill-sized messages): the largest calibrated
+            # size's bandwidth form, not the one-shot threshold default (a larger message
+            # never favours one-shot over the form that beat it at the largest size)
+            return self.table[-1][1]
         if nb > self.one_shot_max:
             return "two_wide" if nb >= self.wide_min else "two"
         return "one"
@@ -158,6 +165,9 @@ class CustomAllReduce:
         e = self._entry(nb)
         if e is not None:
             return e[2]
+        if self.table and self.table[-1][2] != "fused1":
+            last = self.table[-1][2]
+            return last if last == "split" or nb <= self.cap else "split"
         if nb <= min(self.fused_max, self.cap):
             return "fused1"
         if nb <= min(self.fused2_max, self.cap):
@@ -176,6 +186,8 @@ class CustomAllReduce:
         form = self.plain_form(nb)
         self._launch_plain(x, form)
         self.launches[form] += 1
+        if self._entry(nb) is not None:
+            self.table_launches[form] += 1
         return x
 
     def _launch_plain(self, x: torch.Tensor, form: str) -> None:
@@ -198,10 +210,13 @@ class CustomAllReduce:
         if out is None:
             out = torch.empty_like(x)
         self.fused_calls += 1
-        two = self.fused_form(x.numel() * x.element_size()) == "fused2"
+        nb = x.numel() * x.element_size()
+        two = self.fused_form(nb) == "fused2"
         if two:
             self.fused2_calls += 1
         self.launches["fused2" if two else "fused1"] += 1
+        if self._entry(nb) is not None:
+            self.table_launches["fused2" if two else "fused1"] += 1
         torch.ops.kgc.xgmi_allreduce_rms(out, x, residual, w, eps,
                                          self.fdata2 if two else self.fdata, self.sig,
                                          self.rank, self.cap, two)

@@ -429,3 +429,24 @@ def test_phantom_tp_rank_shards_and_local_collectives():
         assert torch.equal(comm.tp_all_reduce(y), x)     # no xGMI object: no peers to sum
     finally:
         set_state(ParallelState())
+
+
+def test_allreduce_policy_past_the_calibrated_sizes():
+    """Messages larger than the start-up calibration's largest size (prefill-sized
+    all-reduces) take that size's bandwidth form, not the one-shot threshold default; a
+    table whose largest size chose one-shot leaves larger messages to the thresholds."""
+    from kubernetes_gpu_cluster_amd.parallel.custom_allreduce import CustomAllReduce
+    car = object.__new__(CustomAllReduce)
+    car.cap, car.one_shot_max, car.wide_min = 8 << 20, 256 << 10, 1 << 62
+    car.fused_max, car.fused2_max = 256 << 10, 8 << 20
+    car.table = [(512, "one", "fused1"), (4096, "two", "fused2")]
+    assert car.plain_form(256) == "one" and car.fused_form(256) == "fused1"
+    assert car.plain_form(4096) == "two" and car.fused_form(4000) == "fused2"
+    assert car.plain_form(64 << 10) == "two"          # threshold default would say "one"
+    assert car.fused_form(64 << 10) == "fused2"
+    assert car.plain_form(16 << 20) == "rccl"         # past the buffer
+    car.table = [(512, "two", "fused1"), (4096, "one", "fused1")]
+    assert car.plain_form(64 << 10) == "one" and car.plain_form(1 << 20) == "two"
+    assert car.fused_form(64 << 10) == "fused1" and car.fused_form(1 << 20) == "fused2"
+    car.table = None
+    assert car.plain_form(64 << 10) == "one" and car.plain_form(1 << 20) == "two"
