@@ -879,6 +879,52 @@ __global__ __launch_bounds__(64) void paged_decode_reduce_kernel(
   T* orow = out + ((int64_t)b * nq + hq) * D;
   constexpr int EPT = D / 64;
   const int64_t base = ((int64_t)b * nq + hq) * Zmax;
+  if (Z <= 64) {
+    // one round trip: lane z's (max, sum) and the first 16 slices' partial rows are all
+    // loaded before any of them is used; the weights travel by lane shuffles, not LDS (the
+    // batch-1 step ran this merge as ~4 dependent round trips: 4.8 us x 32 layers)
+    const float mz = tid < Z ? max_logits[base + tid] : -INFINITY;
+    const float ez = tid < Z ? exp_sums[base + tid] : 0.f;
+    constexpr int ZB = 16;
+    float v[ZB][EPT];
+#pragma unroll
+    for (int j = 0; j < ZB; ++j) {
+      const float* src = tmp_out + (base + min(j, Z - 1)) * D + tid * EPT;
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) v[j][e] = src[e];
+    }
+    const float m = wave_max(mz);
+    const bool live = ctx > 0 && m != -INFINITY;
+    const float wl = live && tid < Z ? exp2f(mz - m) : 0.f;
+    const float tot = wave_sum(wl * ez);
+    float acc[EPT];
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int j = 0; j < ZB; ++j) {
+      const float w = __shfl(wl, j, 64);          // 0 past Z: lane j >= Z holds wl = 0
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) acc[e] += w * v[j][e];
+    }
+    for (int z0 = ZB; z0 < Z; z0 += ZB) {
+#pragma unroll
+      for (int j = 0; j < ZB; ++j) {
+        const float* src = tmp_out + (base + min(z0 + j, Z - 1)) * D + tid * EPT;
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) v[j][e] = src[e];
+      }
+#pragma unroll
+      for (int j = 0; j < ZB; ++j) {
+        const float w = __shfl(wl, z0 + j, 64);
+#pragma unroll
+        for (int e = 0; e < EPT; ++e) acc[e] += w * v[j][e];
+      }
+    }
+    const float inv = tot > 0.f ? 1.f / tot : 0.f;
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) orow[tid * EPT + e] = from_f<T>(acc[e] * inv);
+    return;
+  }
   float m = -INFINITY;
   for (int z = tid; z < Z; z += 64) m = fmaxf(m, max_logits[base + z]);
   m = wave_max(m);
