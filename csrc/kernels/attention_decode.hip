@@ -68,6 +68,19 @@ __host__ __device__ __forceinline__ int decode_used_slices(int nchunk, int Z, in
   return n < Z ? n : Z;
 }
 
+// max of x over lanes l and l ^ 16 / l ^ 32: the gfx950 permlane swaps hand each lane its
+// partner's value in the second register (VALU, no LDS round trip)
+__device__ __forceinline__ float max_xor16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false,
+                                                  false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float max_xor32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false,
+                                                  false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
 __device__ __forceinline__ u32x4 ld16(const void* p) {
   return *reinterpret_cast<const u32x4*>(p);
 }
@@ -453,9 +466,9 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
         m = fmaxf(m, fmaxf(sa[c][i], sb[c][i]));
       }
     }
-    m = fmaxf(m, __shfl_xor(m, 16, 64));
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
-    const float alpha = exp2f(m_run - m);     // 0 on the first partition
+    m = max_xor16(m);
+    m = max_xor32(m);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m);     // 0 on the first partition
     m_run = m;
     l_run *= alpha;
 #pragma unroll
@@ -466,7 +479,8 @@ __global__ __launch_bounds__(256, OCC) void paged_decode_kernel(
       Pack8<T> pf;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float pa = exp2f(sa[c][i] - m), pb = exp2f(sb[c][i] - m);
+        const float pa = __builtin_amdgcn_exp2f(sa[c][i] - m);
+        const float pb = __builtin_amdgcn_exp2f(sb[c][i] - m);
         l_run += pa + pb;
         pf.h[i] = from_f<T>(pa);
         pf.h[4 + i] = from_f<T>(pb);
@@ -626,16 +640,32 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
       sb = mfma16x16x32(f.k[1][s2].v, qf[s2], sb);
     }
     float m = m_run;
+    if (base + 32 <= end) {
+      // a whole chunk inside the slice (every chunk but the context's last): no mask
+      // (wave-uniform branch with VALU only: it moves no load across the pipeline)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int tok = base + 8 * qd + i;
-      sa[i] = tok < end ? sa[i] * scale_log2 : -INFINITY;
-      sb[i] = tok + 4 < end ? sb[i] * scale_log2 : -INFINITY;
-      m = fmaxf(m, fmaxf(sa[i], sb[i]));
+      for (int i = 0; i < 4; ++i) {
+        sa[i] *= scale_log2;
+        sb[i] *= scale_log2;
+        m = fmaxf(m, fmaxf(sa[i], sb[i]));
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int tok = base + 8 * qd + i;
+        sa[i] = tok < end ? sa[i] * scale_log2 : -INFINITY;
+        sb[i] = tok + 4 < end ? sb[i] * scale_log2 : -INFINITY;
+        m = fmaxf(m, fmaxf(sa[i], sb[i]));
+      }
     }
-    m = fmaxf(m, __shfl_xor(m, 16, 64));
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
-    const float alpha = exp2f(m_run - m);
+    // row max over the 4 key groups (lanes xor 16 / 32): permlane swaps on the VALU, not
+    // two ds_bpermute round trips on the chunk's critical path
+    m = max_xor16(m);
+    m = max_xor32(m);
+    // v_exp_f32 directly (exp2f adds a denormal range fix-up: compare, two selects and a
+    // ldexp per call, ~35 % of the loop's VALU); exponents here are <= 0 and results that
+    // would be denormal only ever weight a probability by ~0
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m);
     m_run = m;
     l_run *= alpha;
 #pragma unroll
@@ -643,7 +673,7 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
     Pack8<T> pf;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float pa = exp2f(sa[i] - m), pb = exp2f(sb[i] - m);
+      const float pa = __builtin_amdgcn_exp2f(sa[i] - m), pb = __builtin_amdgcn_exp2f(sb[i] - m);
       l_run += pa + pb;
       pf.h[i] = from_f<T>(pa);
       pf.h[4 + i] = from_f<T>(pb);
@@ -653,10 +683,8 @@ __global__ __launch_bounds__(64, 2) void paged_decode_wave_kernel(
   };
 
   Frag fa, fb;
-  // FUSE: the first chunk's loads go out before the q prologue unless that chunk holds
-  // the new token this wave is about to write
-  // the slice's first chunk and the second one's keys go out before the q prologue (unless one of them holds the
-  // new token this wave is about to write): every wave of the (one-round) grid starts
+  // the slice's first chunk and the second one's keys go out before the q prologue (unless
+  // one of them holds the new token this wave is about to write): every wave of the grid starts
   // with its prologue, so the K / V stream must already be in flight beside the prologue's
   // split-K slice reads (Llama-3-8B at B = 256: 31.5 MB of fp32 q/k/v slices per layer)
   const bool pre_a = c0 < c1 && !(FUSE && c0 == nchunk - 1);
