@@ -77,6 +77,38 @@ __global__ __launch_bounds__(64, 2) void probe_depth(const char* __restrict__ bu
   sink[w * 64 + lane] = acc;
 }
 
+// contiguous runs of RUN 8-KB sub-chunks (a KV block of 32 * RUN tokens per head): the
+// wave's chunk c reads sub-chunk c % RUN of run chunk_of[c / RUN]
+template <int RUN>
+__global__ __launch_bounds__(64, 2) void probe_run(const char* __restrict__ buf,
+                                                   const int* __restrict__ chunk_of, int per_wave,
+                                                   u32x4* __restrict__ sink) {
+  const int lane = threadIdx.x, m = lane & 15, qd = lane >> 4;
+  const int w = blockIdx.x;
+  u32x4 acc = {0, 0, 0, 0};
+  u32x4 a[8], b[8];
+  auto issue = [&](u32x4* f, int c) {
+    const char* base =
+        buf + ((int64_t)chunk_of[(int64_t)w * (per_wave / RUN) + c / RUN] * RUN + c % RUN) * 8192;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int key = 8 * (m >> 2) + (m & 3) + 4 * (i >> 2);
+      f[i] = *reinterpret_cast<const u32x4*>(base + key * 256 + (i & 3) * 64 + qd * 16);
+    }
+  };
+  issue(a, 0);
+  issue(b, 1);
+  for (int c = 0; c < per_wave; c += 2) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc ^= a[i];
+    issue(a, min(c + 2, per_wave - 1));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc ^= b[i];
+    issue(b, min(c + 3, per_wave - 1));
+  }
+  sink[w * 64 + lane] = acc;
+}
+
 int main() {
   const int waves = 2048, per_wave = 20;
   const int64_t nchunks = (int64_t)1536 << 20 >> 13;       // 1.5 GB of 8 KB chunks
@@ -140,6 +172,36 @@ int main() {
       printf("{\"shape\": \"A depth %d, %d waves\", \"us\": %.2f, \"TBps\": %.3f}\n", depth, nw,
              best * 1e3, bytes / (best * 1e-3) / 1e12);
     }
+  }
+  // KV block size: runs of 1 / 2 / 4 sub-chunks (32 / 64 / 128 tokens per block and head),
+  // random run placement (run indices < nchunks / RUN)
+  for (int run = 1; run <= 4; run *= 2) {
+    std::vector<int> rp(nchunks / run);
+    for (size_t i = 0; i < rp.size(); ++i) rp[i] = (int)i;
+    std::shuffle(rp.begin(), rp.end(), rng);
+    int* d_runs;
+    hipMalloc(&d_runs, rp.size() * sizeof(int));
+    hipMemcpy(d_runs, rp.data(), rp.size() * sizeof(int), hipMemcpyHostToDevice);
+    const int64_t per_set = (int64_t)waves * per_wave / run;
+    const int sets = (int)(rp.size() / per_set);
+    float best = 1e9;
+    for (int it = 0; it < 20; ++it) {
+      const int* ch = d_runs + (int64_t)(it % sets) * per_set;
+      hipEventRecord(e0);
+      // the kernel reads chunk_of[w * (per_wave / RUN) + c / RUN]: per_set entries per set
+      if (run == 1) probe_run<1><<<waves, 64>>>(buf, ch, per_wave, sink);
+      else if (run == 2) probe_run<2><<<waves, 64>>>(buf, ch, per_wave, sink);
+      else probe_run<4><<<waves, 64>>>(buf, ch, per_wave, sink);
+      hipEventRecord(e1);
+      hipEventSynchronize(e1);
+      float ms;
+      hipEventElapsedTime(&ms, e0, e1);
+      if (it >= 2) best = std::min(best, ms);
+    }
+    const double bytes = (double)waves * per_wave * 8192;
+    printf("{\"shape\": \"A, %d-token KV blocks (runs of %d x 8 KB)\", \"us\": %.2f, \"TBps\": %.3f}\n",
+           32 * run, run, best * 1e3, bytes / (best * 1e-3) / 1e12);
+    hipFree(d_runs);
   }
   return 0;
 }
