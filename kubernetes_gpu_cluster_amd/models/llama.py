@@ -43,8 +43,11 @@ _tp_ar_norm_enabled = os.environ.get("KGC_TP_AR_NORM", "1") != "0"
 # small M on one GPU: the decoder layer without RMSNorm launches (KGC_RS_LAYER=0: off)
 _rs_enabled = os.environ.get("KGC_RS_LAYER", "1") != "0"
 # M = 65..512 on one GPU: the norm-free layer on K9m, the o / down split-K combine + residual
-# add + row norms inside their GEMM launches (KGC_NF_LAYER=0: off)
-_nf_enabled = os.environ.get("KGC_NF_LAYER", "1") != "0"
+# add + row norms inside their GEMM launches.  Opt-in (KGC_NF_LAYER=1): measured slower than
+# GEMM + norm kernel at every Llama-3-8B M = 256 configuration (profiles/k9m_fanin_vs_tail_r5
+# .jsonl), so by default neither its 9 GB of folded copies nor its start-up timing is spent;
+# with it on, start-up tuning still runs it only where it measures faster (gemm.nf_plan)
+_nf_enabled = os.environ.get("KGC_NF_LAYER", "0") == "1"
 # decode-only steps: RoPE + KV write folded into the paged-decode kernel (KGC_DECODE_ROPE_FUSED=0: off)
 _decode_rope_fused = os.environ.get("KGC_DECODE_ROPE_FUSED", "1") != "0"
 # prefill-only steps of RoPE models without q/k norm: K2 rotates q as it loads it from the
