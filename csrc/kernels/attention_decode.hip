@@ -907,6 +907,13 @@ __global__ __launch_bounds__(64) void paged_decode_reduce_kernel(
   T* orow = out + ((int64_t)b * nq + hq) * D;
   constexpr int EPT = D / 64;
   const int64_t base = ((int64_t)b * nq + hq) * Zmax;
+  if (Z <= 0) {
+    // no slice wrote a partial (an empty context: the graphs' idle rows): zeros, and no
+    // partial row is read (the clamped loads below would index slice -1)
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) orow[tid * EPT + e] = from_f<T>(0.f);
+    return;
+  }
   if (Z <= 64) {
     // one round trip: lane z's (max, sum) and the first 16 slices' partial rows are all
     // loaded before any of them is used; the weights travel by lane shuffles, not LDS (the
