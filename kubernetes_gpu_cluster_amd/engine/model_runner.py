@@ -727,8 +727,13 @@ class ModelRunner:
             # tuner then times only what the table does not cover)
             gemm.load_dg_table(self.mcfg.name, self.ps.tp_size)
             ns = getattr(self.model, "fused_norm_shapes", lambda: set())()
-            gemm.tune_skinny([p for p in self.model.parameters() if p.dim() == 2],
-                             self.buckets, norm_shapes=ns,
+            # the linear layers' weights: an untied embedding table shares lm_head's shape
+            # but is never a GEMM operand (and is not packed: timed with it, lm_head could
+            # never take a packed K9m tile)
+            tied = getattr(self.mcfg, "tie_embeddings", False)
+            lin = [p for n, p in self.model.named_parameters()
+                   if p.dim() == 2 and (tied or "embed" not in n)]
+            gemm.tune_skinny(lin, self.buckets, norm_shapes=ns,
                              silu_shapes=getattr(self.model, "silu_shapes", lambda: set())(),
                              tail_shapes=getattr(self.model, "tail_shapes", lambda: set())(),
                              qkv_dims=getattr(self.model, "qkv_dims", lambda: {})(),

@@ -44,7 +44,7 @@ def main():
     ms = ([int(m) for m in a.ms.split(",")] if a.ms else
           [m for m in graph_buckets(a.max_bs) if gemm.SKINNY_MAX_M < m <= gemm.DG_MAX_M])
     t0 = time.time()
-    res = gemm.tune_skinny([p for p in model.parameters() if p.dim() == 2], ms,
+    res = gemm.tune_skinny(plain + silu, ms,
                            silu_shapes=model.silu_shapes(), tail_shapes=model.tail_shapes(),
                            qkv_dims=model.qkv_dims())
     path = a.out or gemm.dg_table_path(mcfg.name, 1)
