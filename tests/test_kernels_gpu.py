@@ -943,7 +943,7 @@ def test_linear_uses_tuned_plan(gpu):
 @pytest.mark.parametrize("M,N,K,plan", [(256, 2048, 4096, (8, 1)), (80, 1536, 2048, (5, 1)),
                                          (144, 1024, 1024, (0, 2)), (96, 2048, 2048, (2, 1)),
                                          (256, 2048, 4096, (4, 2)), (256, 7168, 1024, (6, 5)),
-                                         (200, 1024, 2048, (9, 3))])
+                                         (200, 1024, 2048, (9, 3)), (256, 2048, 4096, (6, 1))])
 def test_linear_silu_dgemm_matches_fp32(gpu, M, N, K, plan):
     """gate_up through the K9m plan -- fused SiLU epilogue (S = 1, packed silu weights) or
     split-K slices summed by splitk_reduce_silu (row-major tiles: [gate | up] halves; packed
