@@ -71,6 +71,8 @@ def parse():
     ap.add_argument("--max-num-batched-tokens", type=int, default=16384)
     ap.add_argument("--max-model-len", type=int, default=4096)
     ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--moe-parallel", default="tp", choices=["tp", "ep"],
+                    help="Mixtral expert placement over the TP group (engine --moe-parallel)")
     ap.add_argument("--enforce-eager", action="store_true")
     ap.add_argument("--gpu-memory-utilization", type=float, default=0.90)
     ap.add_argument("--dtype", default="bfloat16")
@@ -181,7 +183,8 @@ def main_engine(args):
                        gpu_memory_utilization=args.gpu_memory_utilization,
                        enforce_eager=args.enforce_eager, random_init=True, seed=0,
                        device=args.device, enable_prefix_caching=bool(args.prefix_caching),
-                       prefill_first=args.prefill_first)
+                       prefill_first=args.prefill_first, moe_parallel=args.moe_parallel,
+                       allow_phantom=args.mode == "engine")
     engine = None
     if tp > 1:
         assert world % tp == 0
@@ -222,7 +225,6 @@ def main_engine(args):
     # the all-reduce policy this node's start-up calibration chose (read before shutdown
     # releases the xGMI buffers)
     ar_cal = getattr(comm.get_custom_allreduce(), "calibration", None)
-    nf = _nf_report(engine) if is_driver and not cpu else None
     if is_driver:
         engine.shutdown()
     # aggregate over replicas (drivers) -- every rank participates in the collectives
@@ -269,8 +271,6 @@ def main_engine(args):
         }
         if tp > 1:
             out["ar_calibration"] = ar_cal
-        if nf is not None:
-            out["nf_layer"] = nf
         if phantom > 1:
             out["phantom_tp"] = phantom
             out["data"] += "; ONE phantom TP rank (peers contribute zeros): per-rank timing only"
@@ -289,23 +289,6 @@ def _note(msg: str) -> None:
 
 
 _port_locks: list = []
-
-
-def _nf_report(engine):
-    """The norm-free mid-M layer's start-up decision (models/llama.py _forward_nf): whether
-    the gamma-folded copies exist, the tuner's fan-in vs regular-tail timings per (M, N, K)
-    and the decode sizes that run it."""
-    try:
-        from kubernetes_gpu_cluster_amd.ops import gemm
-        model = engine.executor.worker.model
-    except AttributeError:
-        return None
-    folded = getattr(model, "_nf_w", None) is not None
-    plans = {f"{m}x{n}x{k}": {"cfg": c, "S": s, "fanin_us": round(f, 2), "tail_us": round(t, 2)}
-             for (m, n, k), (c, s, f, t) in sorted(gemm.fanin_plan().items())}
-    ms = sorted({m for (m, _, _) in gemm.fanin_plan()})
-    runs = [m for m in ms if folded and model._nf_cfgs(m) is not None]
-    return {"folded": folded, "fanin_vs_tail": plans, "runs_at_m": runs}
 
 
 def _free_port(local_rank: int, slot: int) -> int:
@@ -354,7 +337,7 @@ def _server_devices(local_rank: int, tp: int, cpu: bool):
 
 def _engine_args(args, cpu: bool) -> list:
     ea = ["--load-format", "dummy", "--dtype", args.dtype, "--seed", "0",
-          "--tensor-parallel-size", str(args.tp),
+          "--tensor-parallel-size", str(args.tp), "--moe-parallel", args.moe_parallel,
           "--max-model-len", str(args.max_model_len), "--max-num-seqs", str(args.max_num_seqs),
           "--max-num-batched-tokens", str(args.max_num_batched_tokens),
           "--gpu-memory-utilization", str(args.gpu_memory_utilization),

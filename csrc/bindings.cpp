@@ -495,6 +495,55 @@ void moe_gemm(Tensor C, Tensor A, Tensor W, Tensor sorted_ids, Tensor block_expe
                        splitk > 1 ? C.stride(0) : 0, stream());
 }
 
+// K14m: the grouped MoE projections on the K9m LDS-DMA pipeline over per-expert packed
+// weights Wp [E, N/128, K/64, 8192] (dgemm_pack per expert; w13 SiLU-packed).
+// mode 1: C = act [rows, N/2] = silu(g) * u of x's gathered rows (sorted-row order);
+// mode 2: C = [npairs, N] (W's dtype) or fp32 slices [S, npairs, N], rows scattered.
+void moe_dgemm(Tensor C, Tensor A, Tensor Wp, Tensor sorted_ids, Tensor block_expert,
+               Tensor meta, int64_t npairs, int64_t topk, int64_t bm, int64_t mode) {
+  check_gpu(A, "A");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(A.device());
+  TORCH_CHECK(bm == 64 || bm == 128, "row block 64 or 128");
+  TORCH_CHECK(mode == 1 || mode == 2, "mode 1 (gate_up + SiLU, gathered) or 2 (down, scattered)");
+  TORCH_CHECK(Wp.dim() == 4 && Wp.is_contiguous() && Wp.size(3) == 128 * kgc::dgemm_block_k(),
+              "Wp packed [E, N/128, K/64, 8192] contiguous");
+  TORCH_CHECK(Wp.scalar_type() == at::kBFloat16 || Wp.scalar_type() == at::kHalf, "bf16 / fp16");
+  TORCH_CHECK(A.scalar_type() == Wp.scalar_type(), "A in W's dtype");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(Wp.data_ptr()) % 16 == 0 &&
+              reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0, "16-B aligned");
+  const int64_t N = Wp.size(1) * 128, K = Wp.size(2) * kgc::dgemm_block_k();
+  const int64_t rows = sorted_ids.numel();
+  TORCH_CHECK(A.dim() == 2 && A.size(1) == K && A.stride(1) == 1 && A.stride(0) % 8 == 0,
+              "A [*, K], 16-B aligned rows");
+  TORCH_CHECK(sorted_ids.scalar_type() == at::kInt && block_expert.scalar_type() == at::kInt &&
+              meta.scalar_type() == at::kInt && rows % bm == 0 &&
+              block_expert.numel() >= rows / bm && meta.numel() >= 1, "moe_align outputs");
+  TORCH_CHECK(npairs >= 0 && topk >= 1 && npairs <= rows, "pairs");
+  int64_t S = 1, ss = 0;
+  if (mode == 1) {
+    TORCH_CHECK(A.size(0) * topk >= npairs, "A has fewer token rows than pairs / k");
+    TORCH_CHECK(C.scalar_type() == Wp.scalar_type() && C.dim() == 2 && C.is_contiguous() &&
+                C.size(0) >= rows && C.size(1) == N / 2, "act [rows, N/2] contiguous");
+  } else {
+    TORCH_CHECK(A.size(0) >= rows, "A must hold every padded row");
+    if (C.dim() == 3) {
+      TORCH_CHECK(C.scalar_type() == at::kFloat && C.is_contiguous() && C.size(1) >= npairs &&
+                  C.size(2) == N, "fp32 slices [S, >= npairs, N] contiguous");
+      S = C.size(0);
+      ss = C.stride(0);
+      TORCH_CHECK(S >= 2 && S <= 16 && S <= K / kgc::dgemm_block_k(), "2 <= S <= 16");
+    } else {
+      TORCH_CHECK(C.scalar_type() == Wp.scalar_type() && C.dim() == 2 && C.is_contiguous() &&
+                  C.size(0) >= npairs && C.size(1) == N, "C [>= npairs, N] contiguous");
+    }
+  }
+  if (rows == 0) return;
+  kgc::launch_moe_dgemm(dt_code(Wp), (int)mode, C.data_ptr(), A.data_ptr(), Wp.data_ptr(),
+                        (int)rows, (int)N, (int)K, A.stride(0), (int)S, ss, (int)bm,
+                        sorted_ids.data_ptr<int>(), block_expert.data_ptr<int>(),
+                        meta.data_ptr<int>(), (int)npairs, (int)topk, stream());
+}
+
 void moe_combine(Tensor out, Tensor y, Tensor topk_w) {
   check_gpu(y, "y");
   c10::hip::HIPGuardMasqueradingAsCUDA g(y.device());
@@ -558,6 +607,8 @@ void dgemm(Tensor C, Tensor X, Tensor W, int64_t cfg, int64_t epi,
   int bm, bn, packed;
   kgc::dgemm_cfg_info((int)cfg, &bm, &bn, &packed);
   TORCH_CHECK(epi >= 0 && epi <= 2, "epi 0 (fp32 slices), 1 (out), 2 (silu pairs)");
+  TORCH_CHECK((kgc::dgemm_cfg_epis((int)cfg) >> epi) & 1,
+              "dgemm: this tile config has no such epilogue (dgemm_cfg_epis)");
   TORCH_CHECK(W.scalar_type() == at::kBFloat16 || W.scalar_type() == at::kHalf, "bf16 / fp16");
   int64_t N, K;
   dgemm_shape(W, packed, &N, &K);
@@ -597,57 +648,6 @@ void dgemm(Tensor C, Tensor X, Tensor W, int64_t cfg, int64_t epi,
                     (int)M, (int)N, (int)K, X.stride(0), (int)S, ss, aux, stream());
 }
 
-// K9m with the split-K combine, residual add and row norms in the launch (EPI_FANIN):
-// R [M, N] += X W^T; ssp [>= M * N/BN] per-tile row sums of squares; rs [>= M] =
-// rsqrt(mean(R^2) + eps); Cs [S, M, N] fp32 slab workspace; cnt int32 [>= MB*N/BN + MB],
-// all zero before the first call (each launch leaves them zero).
-void dgemm_fanin(Tensor Cs, Tensor X, Tensor W, int64_t cfg, Tensor R, Tensor ssp, Tensor rs,
-                 Tensor cnt, double eps) {
-  check_gpu(X, "X");
-  c10::hip::HIPGuardMasqueradingAsCUDA g(X.device());
-  TORCH_CHECK(cfg >= 0 && cfg < kgc::dgemm_num_cfgs() && kgc::dgemm_cfg_has_aux((int)cfg),
-              "dgemm_fanin: a tile config with the fan-in epilogue");
-  int bm, bn, packed;
-  kgc::dgemm_cfg_info((int)cfg, &bm, &bn, &packed);
-  TORCH_CHECK(W.scalar_type() == at::kBFloat16 || W.scalar_type() == at::kHalf, "bf16 / fp16");
-  int64_t N, K;
-  dgemm_shape(W, packed, &N, &K);
-  const int64_t bk = kgc::dgemm_block_k();
-  TORCH_CHECK(X.scalar_type() == W.scalar_type() && X.dim() == 2 && X.size(1) == K &&
-              X.stride(1) == 1 && X.stride(0) % 8 == 0 &&
-              reinterpret_cast<uintptr_t>(X.data_ptr()) % 16 == 0, "X [M, K] in W's dtype, "
-              "16-B aligned rows");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(W.data_ptr()) % 16 == 0, "W 16-B aligned");
-  const int64_t M = X.size(0);
-  TORCH_CHECK(N % bn == 0 && K % bk == 0 && K >= bk, "N % BN == 0, K % 64 == 0");
-  TORCH_CHECK(M <= (int64_t)1 << 20 && N < ((int64_t)1 << 31) / 4, "size limits");
-  TORCH_CHECK(Cs.scalar_type() == at::kFloat && Cs.dim() == 3 && Cs.is_contiguous() &&
-              Cs.size(1) == M && Cs.size(2) == N, "Cs fp32 contiguous [S, M, N]");
-  const int64_t S = Cs.size(0);
-  TORCH_CHECK(S == 1 || S == 2 || S == 3 || S == 4 || S == 5 || S == 6 || S == 8,
-              "dgemm_fanin: S in {1, 2, 3, 4, 5, 6, 8}");
-  TORCH_CHECK(S <= K / bk, "S <= K / 64");
-  TORCH_CHECK(R.scalar_type() == W.scalar_type() && R.dim() == 2 && R.is_contiguous() &&
-              R.size(0) == M && R.size(1) == N, "R [M, N] contiguous in W's dtype");
-  const int64_t MB = (M + bm - 1) / bm, NBT = N / bn;
-  TORCH_CHECK(ssp.scalar_type() == at::kFloat && ssp.is_contiguous() && ssp.numel() >= M * NBT,
-              "ssp fp32 [>= M * N/BN]");
-  TORCH_CHECK(rs.scalar_type() == at::kFloat && rs.is_contiguous() && rs.numel() >= M,
-              "rs fp32 [>= M]");
-  TORCH_CHECK(cnt.scalar_type() == at::kInt && cnt.is_contiguous() &&
-              cnt.numel() >= MB * NBT + MB, "cnt int32 [>= MB * N/BN + MB]");
-  for (const Tensor* t : {&Cs, &W, &R, &ssp, &rs, &cnt}) check_same_dev(X, *t, "dgemm_fanin operand");
-  TORCH_CHECK(MB * NBT * S < ((int64_t)1 << 31), "grid too large");
-  if (M == 0) return;
-  static const int ablate = [] {
-    const char* e = getenv("KGC_FANIN_ABLATE");
-    return e ? atoi(e) : 0;
-  }();
-  kgc::DgAux aux{R.data_ptr(), ssp.data_ptr<float>(), rs.data_ptr<float>(), cnt.data_ptr<int>(),
-                 nullptr, (float)eps, ablate};
-  kgc::launch_dgemm(dt_code(W), (int)cfg, 3, Cs.data_ptr(), X.data_ptr(), W.data_ptr(), (int)M,
-                    (int)N, (int)K, X.stride(0), (int)S, Cs.stride(0), aux, stream());
-}
 
 // P [N/128, K/64, 8192] <- W [N, K] re-laid out for the packed K9m configs
 void dgemm_pack(Tensor P, Tensor W, bool silu) {
@@ -672,6 +672,10 @@ std::vector<int64_t> dgemm_cfg_info(int64_t cfg) {
   return {bm, bn, packed};
 }
 int64_t dgemm_num_cfgs() { return kgc::dgemm_num_cfgs(); }
+int64_t dgemm_cfg_epis(int64_t cfg) {
+  TORCH_CHECK(cfg >= 0 && cfg < kgc::dgemm_num_cfgs(), "unknown dgemm tile config");
+  return kgc::dgemm_cfg_epis((int)cfg);
+}
 bool dgemm_cfg_has_aux(int64_t cfg) {
   TORCH_CHECK(cfg >= 0 && cfg < kgc::dgemm_num_cfgs(), "unknown dgemm tile config");
   return kgc::dgemm_cfg_has_aux((int)cfg);
@@ -760,6 +764,15 @@ int64_t ar_open_handle(Tensor h) {
 void ar_close_handle(int64_t p) { kgc::ar_close_handle((void*)(intptr_t)p); }
 int64_t ar_read_err(int64_t sig) { return (int64_t)kgc::ar_read_err((void*)(intptr_t)sig); }
 // phantom TP rank: raise the never-running peers' arrival flags in this rank's signal
+void ep_raise_peer_flags_op(int64_t sig, int64_t rank, int64_t nranks, int64_t value) {
+  TORCH_CHECK(sig != 0 && rank >= 0 && rank < nranks &&
+                  (nranks == 2 || nranks == 4 || nranks == 8) && value > 0 &&
+                  value < ((int64_t)1 << 31),
+              "ep_raise_peer_flags: sig, 0 <= rank < nranks in {2, 4, 8}, 0 < value < 2^31");
+  kgc::ep_raise_peer_flags((void*)(intptr_t)sig, (int)rank, (int)nranks, (uint32_t)value,
+                           stream());
+}
+
 void ar_raise_peer_flags(int64_t sig, int64_t rank, int64_t nranks, int64_t value) {
   TORCH_CHECK(sig != 0 && rank >= 0 && rank < nranks && (nranks == 2 || nranks == 4 ||
               nranks == 8) && value > 0 && value < (int64_t(1) << 31),
@@ -1179,15 +1192,16 @@ TORCH_LIBRARY(kgc, m) {
         "Tensor topk_ids, int e0, int E_local, int bm) -> ()");
   m.def("moe_gemm(Tensor(a!) C, Tensor A, Tensor W, Tensor sorted_ids, Tensor block_expert, "
         "Tensor meta, int npairs, int topk, int bm, bool gather, bool scatter, int splitk=1) -> ()");
+  m.def("moe_dgemm(Tensor(a!) C, Tensor A, Tensor Wp, Tensor sorted_ids, Tensor block_expert, "
+        "Tensor meta, int npairs, int topk, int bm, int mode) -> ()");
   m.def("moe_combine(Tensor(a!) out, Tensor y, Tensor topk_w) -> ()");
   m.def("dense_gemm_splitk(Tensor(a!) Cs, Tensor A, Tensor W, int bm) -> ()");
   m.def("splitk_reduce(Tensor(a!) out, Tensor Cs) -> ()");
   m.def("dgemm(Tensor(a!) C, Tensor X, Tensor W, int cfg, int epi, Tensor? rscale=None) -> ()");
-  m.def("dgemm_fanin(Tensor(a!) Cs, Tensor X, Tensor W, int cfg, Tensor(b!) R, Tensor(c!) ssp, "
-        "Tensor(d!) rs, Tensor(e!) cnt, float eps) -> ()");
   m.def("dgemm_cfg_info(int cfg) -> int[]", &dgemm_cfg_info);
   m.def("dgemm_num_cfgs() -> int", &dgemm_num_cfgs);
   m.def("dgemm_cfg_has_aux(int cfg) -> bool", &dgemm_cfg_has_aux);
+  m.def("dgemm_cfg_epis(int cfg) -> int", &dgemm_cfg_epis);
   m.def("dgemm_ablate(Tensor(a!) C, Tensor X, Tensor W, int mode) -> ()");
   m.def("dgemm_pack(Tensor(a!) P, Tensor W, bool silu) -> ()");
   m.def("splitk_reduce_silu(Tensor(a!) out, Tensor Cs, bool interleaved=False, "
@@ -1202,6 +1216,8 @@ TORCH_LIBRARY(kgc, m) {
   m.def("ar_read_err(int sig) -> int", &ar_read_err);
   m.def("ar_raise_peer_flags(int sig, int rank, int nranks, int value) -> ()",
         &ar_raise_peer_flags);
+  m.def("ep_raise_peer_flags(int sig, int rank, int nranks, int value) -> ()",
+        &ep_raise_peer_flags_op);
   m.def("ar_err_copy_async(int sig, Tensor(a!) host_out) -> ()", &ar_err_copy_async);
   m.def("xgmi_allreduce(Tensor(a!) inout, int[] data, int[] sig, int rank, int cap_bytes, "
         "bool two_shot, bool wide=False) -> ()");
@@ -1269,10 +1285,10 @@ TORCH_LIBRARY_IMPL(kgc, CUDA, m) {
   m.impl("moe_route", &moe_route);
   m.impl("moe_align", &moe_align);
   m.impl("moe_gemm", &moe_gemm);
+  m.impl("moe_dgemm", &moe_dgemm);
   m.impl("moe_combine", &moe_combine);
   m.impl("dense_gemm_splitk", &dense_gemm_splitk);
   m.impl("dgemm", &dgemm);
-  m.impl("dgemm_fanin", &dgemm_fanin);
   m.impl("dgemm_ablate", &dgemm_ablate);
   m.impl("dgemm_pack", &dgemm_pack);
   m.impl("splitk_reduce", &splitk_reduce);

@@ -1036,6 +1036,11 @@ static void decode_dispatch(void* out, const void* q, const void* kc, const void
                             float scale_log2, float v_scale, int num_blocks,
                             const DecodeRope& rp, hipStream_t s) {
   const bool wave = decode_use_wave(B, nkv);
+  // ONE min_per value feeds both launches below: the decode kernel and its merge derive the
+  // same slice plan from it (decode_used_slices), and the merge trusts the decode kernel to
+  // have written exactly the rows that plan names -- a single-slice row directly (nused ==
+  // 1), the others as partials (tests/test_kernels_gpu.py
+  // ::test_paged_decode_single_slice_rows_many_pairs)
   const int min_per = decode_min_chunks(B, nkv);
   if (wave) {
     paged_decode_wave_kernel<T, D, KV8, FUSE><<<dim3(B, nkv, Z), 64, 0, s>>>(

@@ -264,6 +264,24 @@ __global__ __launch_bounds__(EP_THREADS) void ep_combine_kernel(
     }
 }
 
+// A phantom EP rank (KGC_TP_PHANTOM with --moe-parallel ep: rank `rank` of an EP group
+// whose peers do not exist): every peer's arrival flag in this rank's signal, both phases,
+// raised far ahead of any epoch (vector stores), so dispatch / receive / return / combine
+// run their full sequence in the decode graphs without waiting; the peers' regions hold
+// zero counts, so the owner's grouped MLP sees this rank's own rows only.
+__global__ void ep_raise_peer_flags_kernel(EpSignal* s, int rank, int nranks, uint32_t value) {
+  const int i = threadIdx.x;
+  if (i < 2 * EP_MAX_RANKS) {
+    const int r = i % EP_MAX_RANKS;
+    if (r != rank && r < nranks) ep_store(&(&s->flag[0][0])[i], value);
+  }
+}
+
+void ep_raise_peer_flags(void* sig, int rank, int nranks, uint32_t value, hipStream_t s) {
+  ep_raise_peer_flags_kernel<<<1, 64, 0, s>>>(reinterpret_cast<EpSignal*>(sig), rank, nranks,
+                                              value);
+}
+
 // after the combine (stream order: every kernel of the call has read the epoch)
 __global__ void ep_bump_kernel(EpPtrs P, int rank) {
   EpSignal* self = reinterpret_cast<EpSignal*>(P.sig[rank]);

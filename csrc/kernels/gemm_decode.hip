@@ -45,7 +45,7 @@ namespace {
 constexpr int DG_THREADS = 512;     // 8 waves: 4 along M x 2 along N
 constexpr int DG_BK = 64, DG_NS = 3, DG_ROWB = 128;
 
-enum { EPI_PARTIAL = 0, EPI_OUT = 1, EPI_SILU = 2, EPI_FANIN = 3 };
+enum { EPI_PARTIAL = 0, EPI_OUT = 1, EPI_SILU = 2 };
 // ablation builds (tools/dgemm_bench.py --ablate): one K-step without its MFMAs, without
 // its DMAs, or without one operand's DMAs
 enum { ABL_NONE = 0, ABL_NO_MFMA = 1, ABL_NO_DMA = 2, ABL_NO_A = 3, ABL_NO_B = 4 };
@@ -109,178 +109,33 @@ static int partial_wt() {
   return v;
 }
 
-// EPI_FANIN: the split-K combine, residual add and row norms of a row-parallel
-// projection (o / down) inside its own launch -- the norm-free layer at M = 65..512:
-//   1. every K-slice workgroup publishes its fp32 slab [z][M][N] write-through (sc1), drains
-//      (vmcnt 0), barriers, and draws a ticket on its tile's counter; the one that draws
-//      S - 1 is the tile's reducer (agent acquire; the other S - 1 exit);
-//   2. the reducer re-maps the tile to 16-B column quads (BN / 4 threads per row, all S
-//      slabs of a batch of rows in flight at once), sums the S slabs in slice order
-//      (deterministic whichever slice arrived last), adds the residual, stores it rounded
-//      to T and leaves each row's sum of squares over its BN columns in ssp[row][nb];
-//   3. it then draws a ticket on its row block's counter; the one that draws N / BN - 1
-//      (the row block's last tile) sums each row's N / BN partials into
-//      rs[row] = rsqrt(mean(R[row]^2) + eps): the scale its consumers (the QKV decode-
-//      attention prologue, the SiLU GEMM epilogue) apply to their gamma-folded outputs.
-// Counters are left at zero by the workgroup that draws the last ticket.  Slabs, partials
-// and counters follow the sc1-publish / agent-acquire recipe, so the result does not
-// depend on which XCD runs which slice.  S = 1 runs the same path (one slab, one ticket).
-template <typename T, int BM, int BN, int S, int MAXQ>
-__device__ __forceinline__ void fanin_reduce(const float* slab, int64_t slice_stride, T* R,
-                                             float* ssp, int M, int N, int m0, int nb) {
-  // rows per batch: up to MAXQ float4 slab loads per thread in flight (32: 128 VGPRs; the slabs
-  // are read at the cross-XCD rate, ~2-3 us per round trip under load: one batch for a
-  // 128 x 128 tile at S <= 4 measured 8.5 us for the two-batch combine)
-  constexpr int TPR = BN / 4, RPP = DG_THREADS / TPR, NP = BM / RPP;
-  constexpr int Q = MAXQ / S;
-  constexpr int PB0 = Q >= 32 ? 32 : Q >= 16 ? 16 : Q >= 8 ? 8 : Q >= 4 ? 4 : 2;
-  constexpr int PB = PB0 < NP ? PB0 : NP;
-  static_assert(NP % PB == 0, "row passes per batch");
-  const int tid = threadIdx.x, NBT = N / BN;
-  const int rr = tid / TPR, q = tid % TPR;
-  const int64_t colg = (int64_t)nb * BN + q * 4;
-#pragma unroll 1
-  for (int p0 = 0; p0 < NP; p0 += PB) {
-    f32x4 v[PB][S];
-    u32x2 rv[PB];
-#pragma unroll
-    for (int p = 0; p < PB; ++p) {
-      const int row = min(m0 + (p0 + p) * RPP + rr, M - 1);    // clamped: in-bounds loads
-      const float* sp = slab + (int64_t)row * N + colg;
-#pragma unroll
-      for (int zz = 0; zz < S; ++zz)
-        v[p][zz] = *reinterpret_cast<const f32x4*>(sp + zz * slice_stride);
-      rv[p] = *reinterpret_cast<const u32x2*>(R + (int64_t)row * N + colg);
-    }
-#pragma unroll
-    for (int p = 0; p < PB; ++p) {
-      const int row = m0 + (p0 + p) * RPP + rr;
-      f32x4 a = v[p][0];
-#pragma unroll
-      for (int zz = 1; zz < S; ++zz) a += v[p][zz];
-      Pack4<T> r, o;
-      r.u = rv[p];
-      float sq = 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        o.h[j] = from_f<T>(a[j] + to_f(r.h[j]));
-        const float f = to_f(o.h[j]);
-        sq += f * f;
-      }
-      if (row < M) *reinterpret_cast<u32x2*>(R + (int64_t)row * N + colg) = o.u;
-#pragma unroll
-      for (int off = 1; off < TPR; off <<= 1) sq += __shfl_xor(sq, off, 64);
-      if (row < M && q == 0)
-        __hip_atomic_store(ssp + (int64_t)row * NBT + nb, sq, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-template <typename T, int BM, int BN, int MT, int NT, int MAXQ>
-__device__ __forceinline__ void dgemm_fanin_epilogue(f32x4 (&acc)[MT][NT], bool consumer,
-                                                     char* lds, void* Cv, int M, int N, int S,
-                                                     int MB, int mb, int nb, int z,
-                                                     int64_t slice_stride, const DgAux& aux) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave >> 1) & 3, wn = wave & 1, fr = lane & 15, fq = lane >> 4;
-  const int m0 = mb * BM, NBT = N / BN, tile = mb * NBT + nb;
-  float* slab = reinterpret_cast<float*>(Cv);
-  int* flag = reinterpret_cast<int*>(lds);
-  // 1. publish the slice, draw the tile ticket
-  if (consumer) {
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = m0 + wm * (BM / 4) + i * 16 + fq * 4 + e;
-        if (row >= M) continue;
-        float* cp = slab + z * slice_stride + (int64_t)row * N + nb * BN + wn * (BN / 2) + fr;
-#pragma unroll
-        for (int n = 0; n < NT; ++n) store_partial(cp + n * 16, acc[i][n][e], 1);
-      }
-  }
-  wait_vm<0>();
-  __syncthreads();
-  if (tid == 0) {
-    const int t = __hip_atomic_fetch_add(aux.cnt + tile, 1, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-    const int last = t == S - 1;
-    if (last) {
-      __hip_atomic_store(aux.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      wait_vm<0>();
-    }
-    flag[0] = last;
-  }
-  __syncthreads();
-  if (!flag[0]) return;
-  // 2. the tile's reducer
-  if (tid < DG_THREADS && !(aux.ablate & 1)) {
-    T* R = reinterpret_cast<T*>(aux.R);
-    switch (S) {
-#define FANIN_S(SS) \
-      case SS: fanin_reduce<T, BM, BN, SS, MAXQ>(slab, slice_stride, R, aux.ssp, M, N, m0, nb); \
-        break;
-      FANIN_S(1) FANIN_S(2) FANIN_S(3) FANIN_S(4) FANIN_S(5) FANIN_S(6) FANIN_S(8)
-#undef FANIN_S
-      default: break;            // the host admits only these split factors
-    }
-  }
-  wait_vm<0>();
-  __syncthreads();
-  // 3. the row block's last tile: the rows' norm scales
-  if (aux.ablate & 2) return;
-  if (tid == 0) {
-    int* c2 = aux.cnt + MB * NBT + mb;
-    const int t = __hip_atomic_fetch_add(c2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = t == NBT - 1;
-    if (last) {
-      __hip_atomic_store(c2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      wait_vm<0>();
-    }
-    flag[1] = last;
-  }
-  __syncthreads();
-  if (!flag[1]) return;
-  // DG_THREADS / BM threads per row, each summing every TPRR-th partial with all of its
-  // loads in flight (a per-row loop of dependent batches was a round trip per 4 partials)
-  constexpr int TPRR = DG_THREADS / BM;
-  static_assert(TPRR >= 1 && (TPRR & (TPRR - 1)) == 0, "threads per row");
-  if (tid < DG_THREADS) {
-    const int r = tid / TPRR, part = tid % TPRR, row = m0 + r;
-    const float* pp = aux.ssp + (int64_t)min(row, M - 1) * NBT;
-    float v[8];
-    float s = 0.f;
-#pragma unroll 1
-    for (int j0 = part; j0 < NBT; j0 += 8 * TPRR) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int j = j0 + k * TPRR;
-        v[k] = pp[min(j, NBT - 1)];
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (j0 + k * TPRR < NBT) s += v[k];
-    }
-#pragma unroll
-    for (int off = 1; off < TPRR; off <<= 1) s += __shfl_xor(s, off, 64);
-    if (row < M && part == 0) aux.rs[row] = rsqrtf(s / (float)N + aux.eps);
-  }
-}
-
 // LDW = 4: four extra loader waves issue every DMA and the 8 MFMA waves never stall on
 // DMA issue (one s_barrier per step for all 12 waves); LDW = 0: the MFMA waves issue too.
-template <typename T, int BM, int BN, int EPI, bool PK, int ABL = ABL_NONE, int LDW = 0>
+// WN: MFMA waves along N (2: a 4 x 2 wave grid; 1: all 8 waves along M, each reading every
+// column of the tile -- the narrow / odd column tiles (BN = 80, 112, 224) whose 16-column
+// groups do not split in two, or whose SiLU gate / up pairs must stay in one wave).
+// Column tiles of any multiple of 16 read the same packed [N/128][K/64][128 x 64] weight
+// blocks: each 1-KiB DMA piece is 8 packed rows, which never straddle a 128-row block.
+// A wave whose share of a step's pieces is short re-issues its last piece (the same bytes
+// to the same LDS rows), so every issuing wave counts the same DMAs per step in vmcnt.
+// MOE (K14m, launch_moe_dgemm): 1 = the grouped gate_up, A rows gathered from the tokens
+// (sorted_ids[r] / topk), 2 = the grouped down, output rows scattered to pair order; the
+// workgroup's row block names its expert (block_expert), whose packed weights it streams.
+template <typename T, int BM, int BN, int EPI, bool PK, int ABL = ABL_NONE, int LDW = 0,
+          int WN = 2, int MOE = 0>
 __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
     void* __restrict__ Cv, const T* __restrict__ X, const T* __restrict__ W, int M, int N,
     int K, int64_t ldx, int S, int MB, int64_t slice_stride, int xmap, int wt, DgAux aux) {
-  constexpr int MT = BM / 4 / 16;                 // 16-row MFMA tiles per wave
-  constexpr int NT = BN / 2 / 16;                 // 16-col MFMA tiles per wave
+  static_assert(WN == 1 || WN == 2, "waves along N");
+  constexpr int WM = 8 / WN;                      // MFMA waves along M
+  constexpr int MT = BM / WM / 16;                // 16-row MFMA tiles per wave
+  constexpr int NT = BN / WN / 16;                // 16-col MFMA tiles per wave
+  static_assert(MT * WM * 16 == BM && NT * WN * 16 == BN, "wave tiling");
+  static_assert(EPI != EPI_SILU || NT % 2 == 0, "SiLU gate / up pairs inside one wave");
   constexpr int NIW = LDW > 0 ? LDW : 8;          // waves issuing DMAs
-  constexpr int LA = BM / 8 / NIW, LB = BN / 8 / NIW;   // 1-KiB DMAs per issuing wave per step
-  static_assert(LA * 8 * NIW == BM && LB * 8 * NIW == BN, "DMA split");
+  constexpr int PA = BM / 8, PB = BN / 8;         // 1-KiB pieces per step
+  constexpr int LA = (PA + NIW - 1) / NIW, LB = (PB + NIW - 1) / NIW;   // per issuing wave
+  static_assert(PA % NIW == 0 && (PK || PB % NIW == 0), "DMA split");
   constexpr int L = LA + LB;
   constexpr int A_BYTES = BM * DG_ROWB, SLOT_BYTES = (BM + BN) * DG_ROWB;
   static_assert(DG_NS * SLOT_BYTES <= 163840, "LDS ring exceeds 160 KiB");
@@ -292,7 +147,7 @@ __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
   const bool loader = LDW > 0 && wave >= 8;
   const bool consumer = LDW == 0 || wave < 8;
   const int iw = LDW > 0 ? wave - 8 : wave;       // index among the issuing waves
-  const int wm = (wave >> 1) & 3, wn = wave & 1;
+  const int wm = WN == 2 ? (wave >> 1) & 3 : wave & 7, wn = WN == 2 ? wave & 1 : 0;
   int z, j, mb, nb;
   if (xmap) {
     // XCD-paired row blocks (host: S | 8, (N / BN) % (8 / S) == 0): workgroups L and L + 8
@@ -311,6 +166,14 @@ __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
     nb = j / MB;
   }
   const int m0 = mb * BM;
+  if constexpr (MOE != 0) {
+    // row blocks past the ones moe_align filled, or of another rank's experts: no work
+    // (workgroup-uniform, before any barrier)
+    if (mb >= aux.meta[0]) return;
+    const int e = aux.block_expert[mb];
+    if (e < 0) return;
+    W += (int64_t)e * aux.wexp;
+  }
 
   // ---- DMA sources: lane l of instruction i fills LDS row 8i + l/8, 16-B slot l%8 with
   // global chunk (l%8) ^ (row%8)  (row%8 == l/8): the swizzle lives in the source address
@@ -320,6 +183,13 @@ __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
   for (int t = 0; t < LA; ++t) {
     int r = m0 + (iw * LA + t) * 8 + drow;
     r = r < M ? r : M - 1;                        // padded rows re-read the last row
+    if constexpr (MOE == 1) {
+      // the token of sorted pair row r; a padding row (p == npairs) re-reads the block's
+      // first pair's token (an L2 hit; its output row is never stored)
+      int p = aux.sorted_ids[r];
+      if (p >= aux.npairs) p = aux.sorted_ids[m0];
+      r = p / aux.topk;
+    }
     a_src[t] = X + (int64_t)r * ldx + dchunk * 8;
   }
   const int nk_all = K / DG_BK;
@@ -327,8 +197,11 @@ __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
 #pragma unroll
   for (int t = 0; t < LB; ++t) {
     if constexpr (PK) {
-      // packed [N/BN][K/BK][BN*BK], swizzle baked in: linear 1-KiB pieces of the tile
-      b_src[t] = W + (int64_t)nb * nk_all * (BN * DG_BK) + (iw * LB + t) * 512 + lane * 8;
+      // packed [N/128][K/BK][128*BK], swizzle baked in: piece p = 8 packed rows starting at
+      // row n = nb * BN + 8p, inside 128-row block n / 128 (BN == 128: linear pieces)
+      const int p = min(iw * LB + t, PB - 1);
+      const int n = nb * BN + 8 * p;
+      b_src[t] = W + (int64_t)(n >> 7) * nk_all * (128 * DG_BK) + (n & 127) * DG_BK + lane * 8;
     } else {
       const int r = (iw * LB + t) * 8 + drow;
       b_src[t] = W + weight_row<BN, EPI>(nb, r, N) * K + dchunk * 8;
@@ -354,9 +227,10 @@ __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
         glds16<0>(a_src[t] + kb * DG_BK, sa + (iw * LA + t) * 1024);
     }
     if constexpr (ABL != ABL_NO_B) {
-      const int64_t bo = PK ? (int64_t)kb * (BN * DG_BK) : (int64_t)kb * DG_BK;
+      const int64_t bo = PK ? (int64_t)kb * (128 * DG_BK) : (int64_t)kb * DG_BK;
 #pragma unroll
-      for (int t = 0; t < LB; ++t) glds16<2>(b_src[t] + bo, sb + (iw * LB + t) * 1024);
+      for (int t = 0; t < LB; ++t)
+        glds16<2>(b_src[t] + bo, sb + min(iw * LB + t, PB - 1) * 1024);
     }
   };
 
@@ -367,8 +241,8 @@ __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
     for (int n = 0; n < NT; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int fr = lane & 15, fq = lane >> 4;
-  const int a_row0 = wm * (BM / 4) + fr;
-  const int b_row0 = wn * (BN / 2) + fr;
+  const int a_row0 = wm * (BM / WM) + fr;
+  const int b_row0 = wn * (BN / WN) + fr;
   // EPI_OUT / EPI_SILU with a row scale (the norm-free layer's rsqrt of the producer's
   // row norms): the lane's rows' scales, loaded before the K walk hides their latency
   float rsv[MT][4];
@@ -382,7 +256,7 @@ __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          rsv[i][e] = aux.rsc[min(m0 + wm * (BM / 4) + i * 16 + fq * 4 + e, M - 1)];
+          rsv[i][e] = aux.rsc[min(m0 + wm * (BM / WM) + i * 16 + fq * 4 + e, M - 1)];
     }
   }
 
@@ -438,32 +312,31 @@ __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
 #pragma unroll
       for (int e = 0; e < 4; ++e) asm volatile("" : "+v"(rsv[i][e]));
   }
-  if constexpr (EPI == EPI_FANIN) {
-    // the 12-wave (loader) variants run 3 waves per SIMD: 16 loads per thread (no spill)
-    dgemm_fanin_epilogue<T, BM, BN, MT, NT, (LDW > 0 ? 16 : 32)>(acc, consumer, lds, Cv, M, N, S,
-                                                               MB, mb, nb, z, slice_stride, aux);
-    return;
-  }
   if (!consumer) return;
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int row = m0 + wm * (BM / 4) + i * 16 + fq * 4 + e;
+      int row = m0 + wm * (BM / WM) + i * 16 + fq * 4 + e;
       if (row >= M) continue;
+      if constexpr (MOE == 2) {
+        row = aux.sorted_ids[row];                // scattered back to pair order
+        if (row >= aux.npairs) continue;          // a padding row
+      }
       if constexpr (EPI == EPI_PARTIAL) {
         float* cp = reinterpret_cast<float*>(Cv) + z * slice_stride + (int64_t)row * N +
-                    nb * BN + wn * (BN / 2) + fr;
+                    nb * BN + wn * (BN / WN) + fr;
 #pragma unroll
         for (int n = 0; n < NT; ++n) store_partial(cp + n * 16, acc[i][n][e], wt);
       } else if constexpr (EPI == EPI_OUT) {
-        T* cp = reinterpret_cast<T*>(Cv) + (int64_t)row * N + nb * BN + wn * (BN / 2) + fr;
+        T* cp = reinterpret_cast<T*>(Cv) + (int64_t)row * N + nb * BN + wn * (BN / WN) + fr;
 #pragma unroll
         for (int n = 0; n < NT; ++n) cp[n * 16] = from_f<T>(acc[i][n][e] * rsv[i][e]);
       } else {
         const int I = N >> 1;
         const float sc = rsv[i][e];
-        T* cp = reinterpret_cast<T*>(Cv) + (int64_t)row * I + nb * (BN / 2) + wn * (BN / 4) + fr;
+        T* cp = reinterpret_cast<T*>(Cv) + (int64_t)row * I + nb * (BN / 2) +
+                wn * (BN / WN / 2) + fr;
 #pragma unroll
         for (int n = 0; n < NT; n += 2)
           cp[(n >> 1) * 16] = from_f<T>(silu_f(acc[i][n][e] * sc) * (acc[i][n + 1][e] * sc));
@@ -664,25 +537,50 @@ __global__ __launch_bounds__(256) void dgemm_pack_kernel(T* __restrict__ P,
 // down, with or without the pairing (profiles/k9m_dgemm_bench_r2_sweep.jsonl).
 // K9v (activations in a VGPR ring, round 3) measured slower on every shape and lives in
 // tools/research/ (its own library), out of the engine's.
-constexpr int kNumCfgs = 11;
-static const int kCfg[kNumCfgs][3] = {{256, 128, 0}, {256, 64, 0},  {128, 128, 0}, {128, 64, 0},
-                                      {256, 128, 1}, {128, 128, 1}, {256, 128, 1}, {128, 128, 1},
-                                      {256, 128, 1}, {128, 128, 1}, {128, 128, 1}};
+// ids 11-14 (round 6): packed column tiles of 64 / 80 / 112 for the narrow shards of a
+// TP = 8 rank (profiles/README.md "Round 6: full-grid K9m tiles"):
+//   11  256 x  64, 8 issuing waves           70B TP = 8 o at S = 2 (128 tiles)
+//   12  256 x  80, 4 loaders, WN = 1         70B TP = 8 qkv (N 1280: 16 tiles x S 16)
+//   13  256 x 112, 4 loaders, WN = 1         70B TP = 8 gate_up slices (64 tiles x S 4)
+//   14  128 x  64, 8 issuing waves, XCD      70B TP = 8 o at S = 1, ahead of its all-reduce
+// Measured and not kept: 256 x 96 (Llama-3-8B qkv at S = 4, 256 workgroups), 128 x 224 with
+// the SiLU epilogue (gate_up at S = 1, 256 workgroups) and 128 x 192: filling all 256 CUs
+// did not beat the 192 / 224-workgroup 256 x 128 tiles at M = 256 (the extra activation
+// re-reads of narrower tiles cost more than the idle CUs: profiles/k9m_full_grid_r6.jsonl).
+struct DgCfg {
+  int bm, bn, pk, ldw, wn, xmap;
+};
+constexpr int kNumCfgs = 15;
+static const DgCfg kCfg[kNumCfgs] = {
+    {256, 128, 0, 0, 2, 0}, {256, 64, 0, 0, 2, 0}, {128, 128, 0, 0, 2, 0}, {128, 64, 0, 0, 2, 0},
+    {256, 128, 1, 0, 2, 0}, {128, 128, 1, 0, 2, 0}, {256, 128, 1, 4, 2, 0}, {128, 128, 1, 4, 2, 0},
+    {256, 128, 1, 0, 2, 0}, {128, 128, 1, 0, 2, 0}, {128, 128, 1, 0, 2, 1},
+    {256, 64, 1, 0, 2, 0},  {256, 80, 1, 4, 1, 0},  {256, 112, 1, 4, 1, 0}, {128, 64, 1, 0, 2, 1}};
 
-template <typename T, int BM, int BN, bool PK, int LDW = 0>
+// epilogues a tile runs: bit EPI (PARTIAL / OUT always; SILU where each wave holds whole
+// gate / up 16-column pairs)
+template <int BN, int WN>
+constexpr int dg_epis() {
+  return (1 << EPI_PARTIAL) | (1 << EPI_OUT) |
+         ((BN % 32 == 0 && (BN / WN / 16) % 2 == 0) ? (1 << EPI_SILU) : 0);
+}
+
+template <typename T, int BM, int BN, bool PK, int LDW = 0, int WN = 2>
 void dgemm_cfg(int epi, void* C, const void* X, const void* W, int M, int N, int K, int64_t ldx,
                int S, int64_t ss, const DgAux& aux, hipStream_t s, int xmap = 0) {
   const int MB = (M + BM - 1) / BM;
   const dim3 grid((unsigned)(MB * (N / BN) * S));
   // the XCD pairing needs S | 8 and whole groups of 8 / S column tiles
   const int xm = (xmap && MB > 1 && 8 % S == 0 && (N / BN) % (8 / S) == 0) ? 1 : 0;
-#define DG_LAUNCH(E)                                                             \
-  dgemm_kernel<T, BM, BN, E, PK, ABL_NONE, LDW><<<grid, DG_THREADS + LDW * 64, 0, s>>>( \
+  constexpr int E = dg_epis<BN, WN>();
+#define DG_LAUNCH(EP)                                                                       \
+  dgemm_kernel<T, BM, BN, EP, PK, ABL_NONE, LDW, WN><<<grid, DG_THREADS + LDW * 64, 0, s>>>( \
       C, (const T*)X, (const T*)W, M, N, K, ldx, S, MB, ss, xm, partial_wt(), aux)
   if (epi == EPI_PARTIAL) DG_LAUNCH(EPI_PARTIAL);
   else if (epi == EPI_OUT) DG_LAUNCH(EPI_OUT);
-  else if (epi == EPI_SILU) DG_LAUNCH(EPI_SILU);
-  else DG_LAUNCH(EPI_FANIN);
+  else if (epi == EPI_SILU) {
+    if constexpr ((E >> EPI_SILU) & 1) DG_LAUNCH(EPI_SILU);
+  }
 #undef DG_LAUNCH
 }
 
@@ -700,18 +598,77 @@ void dgemm_t(int cfg, int epi, void* C, const void* X, const void* W, int M, int
     case 7: dgemm_cfg<T, 128, 128, true, 4>(epi, C, X, W, M, N, K, ldx, S, ss, a, s); break;
     case 8: dgemm_sl_cfg<T, 256, 128, 4>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
     case 9: dgemm_sl_cfg<T, 128, 128, 6>(epi, C, X, W, M, N, K, ldx, S, ss, s); break;
-    default: dgemm_cfg<T, 128, 128, true>(epi, C, X, W, M, N, K, ldx, S, ss, a, s, 1); break;
+    case 10: dgemm_cfg<T, 128, 128, true>(epi, C, X, W, M, N, K, ldx, S, ss, a, s, 1); break;
+    case 11: dgemm_cfg<T, 256, 64, true>(epi, C, X, W, M, N, K, ldx, S, ss, a, s); break;
+    case 12: dgemm_cfg<T, 256, 80, true, 4, 1>(epi, C, X, W, M, N, K, ldx, S, ss, a, s); break;
+    case 13: dgemm_cfg<T, 256, 112, true, 4, 1>(epi, C, X, W, M, N, K, ldx, S, ss, a, s); break;
+    case 14: dgemm_cfg<T, 128, 64, true>(epi, C, X, W, M, N, K, ldx, S, ss, a, s, 1); break;
+    default: break;                 // the host checks cfg < dgemm_num_cfgs()
   }
+}
+
+int dg_cfg_epis(int cfg) {
+  switch (cfg) {
+    case 8: case 9: return (1 << EPI_PARTIAL) | (1 << EPI_OUT) | (1 << EPI_SILU);
+    case 12: return dg_epis<80, 1>();
+    case 13: return dg_epis<112, 1>();
+    case 1: case 3: case 11: case 14: return dg_epis<64, 2>();
+    default: return dg_epis<128, 2>();
+  }
+}
+
+template <typename T, int BM, int MOE>
+void moe_dgemm_t(int epi, void* C, const void* A, const void* Wp, int max_rows, int N, int K,
+                 int64_t lda, int S, int64_t ss, const DgAux& aux, hipStream_t s) {
+  // 1-D grid, row blocks fastest: a column tile's blocks (one expert each) are dispatched
+  // together, so each XCD's L2 holds the activation rows of the experts it is dealt
+  const int MB = max_rows / BM;
+  const dim3 grid((unsigned)(MB * (N / 128) * S));
+#define MOE_LAUNCH(EP)                                                                      \
+  dgemm_kernel<T, BM, 128, EP, true, ABL_NONE, 0, 2, MOE><<<grid, DG_THREADS, 0, s>>>(      \
+      C, (const T*)A, (const T*)Wp, max_rows, N, K, lda, S, MB, ss, 0, partial_wt(), aux)
+  if constexpr (MOE == 1) {
+    MOE_LAUNCH(EPI_SILU);
+  } else {
+    if (epi == EPI_PARTIAL) MOE_LAUNCH(EPI_PARTIAL);
+    else MOE_LAUNCH(EPI_OUT);
+  }
+#undef MOE_LAUNCH
 }
 
 }  // namespace
 
+void launch_moe_dgemm(int dtype, int mode, void* C, const void* A, const void* Wp, int max_rows,
+                      int N, int K, int64_t lda, int S, int64_t slice_stride, int bm,
+                      const int* sorted_ids, const int* block_expert, const int* meta,
+                      int npairs, int topk, hipStream_t s) {
+  DgAux aux{};
+  aux.sorted_ids = sorted_ids;
+  aux.block_expert = block_expert;
+  aux.meta = meta;
+  aux.npairs = npairs;
+  aux.topk = topk;
+  aux.wexp = (int64_t)N * K;                     // one expert's packed weight, elements
+  const int epi = mode == 1 ? EPI_SILU : S > 1 ? EPI_PARTIAL : EPI_OUT;
+#define MOE_T(TT)                                                                           \
+  if (mode == 1) {                                                                          \
+    if (bm == 64) moe_dgemm_t<TT, 64, 1>(epi, C, A, Wp, max_rows, N, K, lda, S, slice_stride, aux, s); \
+    else moe_dgemm_t<TT, 128, 1>(epi, C, A, Wp, max_rows, N, K, lda, S, slice_stride, aux, s); \
+  } else {                                                                                  \
+    if (bm == 64) moe_dgemm_t<TT, 64, 2>(epi, C, A, Wp, max_rows, N, K, lda, S, slice_stride, aux, s); \
+    else moe_dgemm_t<TT, 128, 2>(epi, C, A, Wp, max_rows, N, K, lda, S, slice_stride, aux, s); \
+  }
+  if (dtype == DT_BF16) { MOE_T(bf16) } else { MOE_T(f16) }
+#undef MOE_T
+}
+
 int dgemm_num_cfgs() { return kNumCfgs; }
 void dgemm_cfg_info(int cfg, int* bm, int* bn, int* packed) {
-  *bm = kCfg[cfg][0];
-  *bn = kCfg[cfg][1];
-  *packed = kCfg[cfg][2];
+  *bm = kCfg[cfg].bm;
+  *bn = kCfg[cfg].bn;
+  *packed = kCfg[cfg].pk;
 }
+int dgemm_cfg_epis(int cfg) { return cfg >= 0 && cfg < kNumCfgs ? dg_cfg_epis(cfg) : 0; }
 int dgemm_block_k() { return DG_BK; }
 // the split-loader configs (8, 9) have no fan-in or row-scale epilogue
 bool dgemm_cfg_has_aux(int cfg) { return cfg != 8 && cfg != 9; }

@@ -128,24 +128,33 @@ void launch_dense_gemm_splitk(int dtype, int bm, float* Cs, const void* A, const
 // (dgemm_cfg_info: BM x BN, and whether W is the packed [N/128][K/64][128*64] layout of
 // launch_dgemm_pack rather than [N, K]).  epi 0: fp32 split-K slice z of C [S, M, N];
 // 1: C [M, N] in X's dtype (S = 1); 2: silu(gate) * up of a merged [gate; up] W into
-// C [M, N/2] (S = 1; a packed W must have been packed with silu = true)
-// 3: split-K combine + residual add + row norms in the launch (the norm-free layer's o /
-// down projections): C holds the S fp32 slabs; R [M, N] += their sum, ssp [M, N/BN] and
-// rs [M] = rsqrt(mean(R^2) + eps) out; cnt [MB * N/BN + MB] zeroed tickets.  epi 1 / 2 with
+// C [M, N/2] (S = 1; a packed W must have been packed with silu = true).  epi 1 / 2 with
 // rsc != nullptr: output row m scaled by rsc[m] (before the SiLU).
 struct DgAux {
-  void* R;
-  float* ssp;
-  float* rs;
-  int* cnt;
   const float* rsc;
-  float eps;
-  int ablate;     // fan-in cost breakdown (tools/fanin_bench.py): bit 0 no combine, bit 1 no rs
+  // K14m (the MoE grouped GEMM on the K9m pipeline, launch_moe_dgemm): row blocks of one
+  // expert each (moe_align), per-expert packed weights wexp elements apart
+  const int* sorted_ids;
+  const int* block_expert;
+  const int* meta;
+  int npairs, topk;
+  int64_t wexp;
 };
+// K14m: one grouped MoE projection on the K9m pipeline over per-expert PACKED weights
+// Wp [E][N/128][K/64][128*64]: mode 1 = gate_up (A rows gathered from x by sorted_ids / topk,
+// SiLU epilogue over the SiLU-packed w13, act [rows, N/2] in sorted-row order); mode 2 =
+// down (A = act rows, C rows scattered to pair order; S > 1: fp32 slices [S][npairs][N]).
+// bm = 64 | 128 row blocks (moe_align's), max_rows = rows of sorted_ids.
+void launch_moe_dgemm(int dtype, int mode, void* C, const void* A, const void* Wp, int max_rows,
+                      int N, int K, int64_t lda, int S, int64_t slice_stride, int bm,
+                      const int* sorted_ids, const int* block_expert, const int* meta,
+                      int npairs, int topk, hipStream_t s);
 int dgemm_num_cfgs();
 void dgemm_cfg_info(int cfg, int* bm, int* bn, int* packed);
 int dgemm_block_k();
 bool dgemm_cfg_has_aux(int cfg);
+// epilogues a tile config runs: bit 0 fp32 slices, 1 out, 2 SiLU pairs
+int dgemm_cfg_epis(int cfg);
 void launch_dgemm(int dtype, int cfg, int epi, void* C, const void* X, const void* W, int M,
                   int N, int K, int64_t ldx, int S, int64_t slice_stride, const DgAux& aux,
                   hipStream_t s);
@@ -206,6 +215,7 @@ using EpPtrs = ArPtrs;
 size_t ep_signal_bytes();
 int64_t ep_region_bytes(int nr, int C, int H, int esz);
 int ep_max_pairs();
+void ep_raise_peer_flags(void* sig, int rank, int nranks, uint32_t value, hipStream_t s);
 void launch_ep_dispatch(int dtype, const EpPtrs& P, int nr, int rank, const void* x,
                         const int* topk_ids, int npairs, int k, int H, int E_local, int C,
                         hipStream_t s);

@@ -60,6 +60,11 @@ class EngineConfig:
     node_rank: int = 0
     master_addr: Optional[str] = None
     master_port: int = 29500
+    # KGC_TP_PHANTOM (parallel/state.py init_phantom) is a one-GPU per-rank MEASUREMENT
+    # stand-in whose missing peers contribute zeros to every all-reduce: its completions are
+    # wrong by construction.  Only bench.py --mode engine and the tests set this; every other
+    # entrypoint (API server, LLM) leaves it False, and the worker then refuses the mode.
+    allow_phantom: bool = False
 
     def torch_dtype(self, model_default: torch.dtype = torch.bfloat16) -> torch.dtype:
         d = _DTYPES.get(self.dtype.lower())

@@ -432,25 +432,12 @@ class ModelRunner:
         KGC_TP_OVERLAP=0 turns it off; KGC_TP_OVERLAP_MIN_TOKENS (default 2048) is the
         smallest step it applies to (below it the all-reduces take the xGMI kernel)."""
         if self.ps.tp_size == 1:
-            return self._two_streams_ok(Tp)
+            return False
         if os.environ.get("KGC_TP_OVERLAP", "1") == "0":
             return False
         fn = getattr(self.model, "_tp_tail_fusable", None)
         return (fn is not None and fn()
                 and Tp >= int(os.environ.get("KGC_TP_OVERLAP_MIN_TOKENS", "2048")))
-
-    def _two_streams_ok(self, Tp: int) -> bool:
-        """One GPU: large prefill-only steps of several sequences run as two halves on two
-        streams (``LlamaForCausalLM._forward_two_streams``) with KGC_PREFILL_STREAMS=1;
-        KGC_PREFILL_STREAMS_MIN_TOKENS (default 4096) is the smallest step.  Off by default:
-        measured on one box (profiles/engine_ab_prefill_two_streams_r4.jsonl) 17,117 vs
-        17,190 tok/s and p50 TTFT 783 vs 771 ms -- the halves' memory-bound kernels beside
-        the other half's GEMMs do not buy time back under the 1400 W cap."""
-        if not self.is_gpu or os.environ.get("KGC_PREFILL_STREAMS", "0") != "1":
-            return False
-        fn = getattr(self.model, "two_stream_ok", None)
-        return (fn is not None and fn()
-                and Tp >= int(os.environ.get("KGC_PREFILL_STREAMS_MIN_TOKENS", "4096")))
 
     def _split_prefill(self, Tp: int, P: int):
         """Split the step's prefill tokens at row a into two AttnMetadata.  A sequence
@@ -464,15 +451,7 @@ class ModelRunner:
         qsl = i32[L.qsl:L.qsl + P + 1].astype(np.int64)
         sl = i32[L.sl:L.sl + P].astype(np.int64)
         pbt = i32[L.pbt:L.pbt + P * mb].reshape(P, mb)
-        if self.ps.tp_size == 1:
-            # two streams: the halves must share no sequence -- cut at the sequence
-            # boundary nearest the middle, or not at all
-            inner = qsl[1:-1]
-            if inner.size == 0:
-                return None
-            a = int(inner[np.argmin(np.abs(inner - Tp // 2))])
-        else:
-            a = (Tp // 2) // 128 * 128 or Tp // 2
+        a = (Tp // 2) // 128 * 128 or Tp // 2
         k = int(np.searchsorted(qsl, a, side="right")) - 1      # qsl[k] <= a < qsl[k+1]
         qlens = np.diff(qsl)
         cut = a > qsl[k]
@@ -737,8 +716,7 @@ class ModelRunner:
                              silu_shapes=getattr(self.model, "silu_shapes", lambda: set())(),
                              tail_shapes=getattr(self.model, "tail_shapes", lambda: set())(),
                              qkv_dims=getattr(self.model, "qkv_dims", lambda: {})(),
-                             rs_shapes=getattr(self.model, "_rs_w", None) is not None,
-                             nf=getattr(self.model, "_nf_w", None) is not None)
+                             rs_shapes=getattr(self.model, "_rs_w", None) is not None)
         whole = self.model.first and self.model.last
         if (not self.use_graphs or not (whole or self.pp_link is not None)
                 or not getattr(self.model, "graph_safe", True)):

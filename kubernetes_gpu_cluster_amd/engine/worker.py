@@ -53,9 +53,13 @@ def _fault_perturb_shard(model, ps) -> None:
     """Fault injection for the TP parity oracles (tests/test_engine_gpu.py): with
     KGC_FAULT_PERTURB_TP_RANK=r, TP rank r adds noise to its shard of every o_proj weight
     after loading -- one wrong shard, which a teacher-forced comparison against TP = 1
-    must catch.  Unset in every real deployment."""
+    must catch.  Armed only together with KGC_TESTING=1 (the test sets both), so the
+    variable alone -- left in a deployment by accident -- changes nothing but a warning."""
     r = os.environ.get("KGC_FAULT_PERTURB_TP_RANK")
     if r is None or ps.tp_size == 1 or int(r) != ps.tp_rank:
+        return
+    if os.environ.get("KGC_TESTING") != "1":
+        log.warning("KGC_FAULT_PERTURB_TP_RANK ignored: fault injection needs KGC_TESTING=1")
         return
     g = torch.Generator(device="cpu").manual_seed(1234)
     with torch.no_grad():
@@ -84,8 +88,15 @@ class Worker:
         if ph > 1:
             # KGC_TP_PHANTOM=N: this single process is rank 0 of a TP = N model (one GPU
             # stands in for a TP node's rank: parallel/state.py init_phantom)
+            if not cfg.allow_phantom:
+                raise ValueError(
+                    "KGC_TP_PHANTOM is set: a phantom TP rank serves rank 0's shard with zero "
+                    "peers (wrong completions by construction). It is a per-rank measurement "
+                    "mode for bench.py --mode engine and the tests only; unset it to serve.")
             if cfg.tensor_parallel_size * cfg.pipeline_parallel_size != 1 or dev.type != "cuda":
                 raise ValueError("KGC_TP_PHANTOM needs one GPU process (tp = pp = 1)")
+            log.warning("PHANTOM TP rank 0 of %d: per-rank timing only, outputs are not a "
+                        "model's", ph)
             init_phantom(ph, dev)
         self.ps = get_state()
         # non-driver ranks of a multi-rank engine heart-beat into the rendezvous store
@@ -122,21 +133,17 @@ class Worker:
             ws = [p for n, p in self.model.named_parameters() if p.dim() == 2
                   and id(p) not in skip and (tied or "embed" not in n)]
             gemm.pack_decode_weights(ws, silu)
+            from ..models.moe import pack_moe_experts
+            pack_moe_experts(self.model)
         if dev.type == "cuda":
             # gamma-folded qkv / gate_up copies for the norm-free small-M layer (eager and
             # graph steps alike, so both run the same arithmetic)
             fold = getattr(self.model, "fold_rs_weights", None)
             if fold is not None:
                 fold()
-            if not cfg.enforce_eager:
-                # packed gamma-folded copies for the norm-free mid-M layer (graph steps)
-                fold = getattr(self.model, "fold_nf_weights", None)
-                if fold is not None:
-                    fold()
         if self.ps.tp_size > 1 and dev.type == "cuda" and not cfg.disable_custom_all_reduce:
             from ..parallel.custom_allreduce import calibration_rows, maybe_init_custom_allreduce
-            rows = (calibration_rows(min(cfg.cuda_graph_max_bs, cfg.max_num_seqs))
-                    if not self.ps.phantom else None)
+            rows = calibration_rows(min(cfg.cuda_graph_max_bs, cfg.max_num_seqs))
             comm.set_custom_allreduce(maybe_init_custom_allreduce(
                 self.ps, dev, self.mcfg.hidden_size, self.dtype, rows))
         # the cooperative sampler's error word (last PP stage samples)

@@ -42,12 +42,10 @@ _tail_fusion_enabled = os.environ.get("KGC_TAIL_FUSION", "1") != "0"
 _tp_ar_norm_enabled = os.environ.get("KGC_TP_AR_NORM", "1") != "0"
 # small M on one GPU: the decoder layer without RMSNorm launches (KGC_RS_LAYER=0: off)
 _rs_enabled = os.environ.get("KGC_RS_LAYER", "1") != "0"
-# M = 65..512 on one GPU: the norm-free layer on K9m, the o / down split-K combine + residual
-# add + row norms inside their GEMM launches.  Opt-in (KGC_NF_LAYER=1): measured slower than
-# GEMM + norm kernel at every Llama-3-8B M = 256 configuration (profiles/k9m_fanin_vs_tail_r5
-# .jsonl), so by default neither its 9 GB of folded copies nor its start-up timing is spent;
-# with it on, start-up tuning still runs it only where it measures faster (gemm.nf_plan)
-_nf_enabled = os.environ.get("KGC_NF_LAYER", "0") == "1"
+# (Removed in round 6, measured slower and off by default: the norm-free mid-M layer --
+# K9m's fan-in epilogue doing the o / down split-K combine + residual add + row norms in the
+# GEMM launch, profiles/k9m_fanin_vs_tail_r5.jsonl -- and two-stream prefill,
+# profiles/engine_ab_prefill_two_streams_r4.jsonl.  Last present at commit 4d8a38e.)
 # decode-only steps: RoPE + KV write folded into the paged-decode kernel (KGC_DECODE_ROPE_FUSED=0: off)
 _decode_rope_fused = os.environ.get("KGC_DECODE_ROPE_FUSED", "1") != "0"
 # prefill-only steps of RoPE models without q/k norm: K2 rotates q as it loads it from the
@@ -224,16 +222,11 @@ class LlamaForCausalLM(nn.Module):
                 return self._forward_fused(input_ids, positions, ctx, cfgs)
         x = self.embed_tokens(input_ids) if self.first else hidden
         if self._tail_fusable(x):
-            nf = self._nf_cfgs(x.shape[0])
-            if nf is not None:
-                return self._forward_nf(positions, x, ctx, nf)
             return self._forward_tail_fused(positions, x, ctx)
         if self._tp_tail_fusable():
             if ctx.attn.split is not None:
                 return self._forward_tp_overlap(positions, x, ctx)
             return self._forward_tp_fused(positions, x, ctx)
-        if getattr(getattr(ctx, "attn", None), "split", None) is not None and self.two_stream_ok():
-            return self._forward_two_streams(positions, x, ctx)
         for layer in self.layers:
             x, residual = layer(positions, x, residual, ctx)
         if not self.last:
@@ -277,79 +270,6 @@ class LlamaForCausalLM(nn.Module):
         x, _ = gemm.linear_add_rms(h, prev.mlp.down_proj.weight, residual, self.norm.weight,
                                    self.norm.eps)
         return x
-
-    # ------------------------------------------------------------------ norm-free mid-M layer
-    def fold_nf_weights(self, budget_fraction: float = 0.08) -> int:
-        """K9m-packed copies of the qkv (layers 1..) and gate_up weights with their input
-        norm's gamma folded in, for ``_forward_nf``: made where the regular packed copies
-        exist (ops/gemm.py pack_decode_weights) and the copies fit ``budget_fraction`` of
-        device memory (Llama-3-8B: 9.1 GB).  Call before the KV cache is sized."""
-        self._nf_w = None
-        if not (_nf_enabled and _tail_fusion_enabled and self._fusable and self.layers
-                and self.layers[0].input_layernorm.weight.is_cuda):
-            return 0
-        l0 = self.layers[0]
-        if any(p.bias is not None for p in (l0.self_attn.qkv_proj, l0.self_attn.o_proj,
-                                            l0.mlp.gate_up_proj, l0.mlp.down_proj)):
-            return 0
-        if any(gemm.packed_weight(l.self_attn.qkv_proj.weight) is None
-               or gemm.packed_weight(l.mlp.gate_up_proj.weight, True) is None
-               for l in self.layers):
-            return 0
-        need = sum(l.self_attn.qkv_proj.weight.numel() + l.mlp.gate_up_proj.weight.numel()
-                   for l in self.layers[1:]) * l0.mlp.gate_up_proj.weight.element_size()
-        need += l0.mlp.gate_up_proj.weight.numel() * l0.mlp.gate_up_proj.weight.element_size()
-        free, total = torch.cuda.mem_get_info(l0.input_layernorm.weight.device)
-        if need > budget_fraction * total or need > free - (8 << 30):
-            return 0
-        ws = []
-        for i, l in enumerate(self.layers):
-            qkv = (None if i == 0 else gemm.pack_folded(l.self_attn.qkv_proj.weight,
-                                                        l.input_layernorm.weight, False))
-            ws.append((qkv, gemm.pack_folded(l.mlp.gate_up_proj.weight,
-                                             l.post_attention_layernorm.weight, True)))
-        self._nf_w = ws
-        return need
-
-    def _nf_cfgs(self, M: int):
-        """K9m plans (qkv, o, gate_up, down) of the norm-free layer at this M, or None:
-        folded copies made, packed tiles for qkv / gate_up, and ``gemm.nf_plan``."""
-        if getattr(self, "_nf_w", None) is None:
-            return None
-        p = gemm.nf_plan(M, self._rs_shapes())
-        if p is None or not (gemm.cfg_packed(p[0][0]) and gemm.cfg_packed(p[2][0])):
-            return None
-        return p
-
-    def _forward_nf(self, positions, x, ctx, cfgs):
-        """The decoder at M = 65..512 with no RMSNorm or split-K reduction launch: o_proj
-        and down_proj run K9m's fan-in epilogue (the last K-slice of each column tile sums
-        the slabs, adds the residual and leaves row sums of squares; the last tile of a row
-        block turns them into r = rsqrt(mean(residual^2) + eps)); qkv and gate_up run on the
-        raw residual with gamma folded into their weights, and r scales their rows -- in the
-        decode-attention prologue (qkv) and in the SiLU epilogue (gate_up).  Per layer:
-        qkv, attention, o, gate_up, down: 5 launches against 7 on the tail-fused path.
-        Layer 0's input norm over the embedding stays a kernel (its qkv weight unfolded);
-        the final norm too."""
-        (cq, sq), (co, so), (cg, sg), (cd, sd) = cfgs
-        res = x
-        rs = None
-        n = len(self.layers)
-        for i, layer in enumerate(self.layers):
-            at, mlp = layer.self_attn, layer.mlp
-            qkv_f, gu_f = self._nf_w[i]
-            if i == 0:
-                qkv = gemm.dgemm(layer.input_layernorm(res), at.qkv_proj.weight, cq, sq)
-                a = at.attend(positions, qkv, ctx)
-            else:
-                qkv = gemm.dgemm(res, at.qkv_proj.weight, cq, sq, wk=qkv_f)
-                a = at.attend(positions, qkv, ctx, row_scale=rs)
-            rs = gemm.dgemm_fanin(a, at.o_proj.weight, co, so, res,
-                                  layer.post_attention_layernorm.eps)
-            h = gemm.nf_silu(res, mlp.gate_up_proj.weight, gu_f, cg, sg, rs)
-            eps = self.layers[i + 1].input_layernorm.eps if i + 1 < n else self.norm.eps
-            rs = gemm.dgemm_fanin(h, mlp.down_proj.weight, cd, sd, res, eps)
-        return self.norm(res)
 
     def _tp_tail_fusable(self) -> bool:
         """TP > 1, whole model, dense bias-free o / down projections: each row-parallel
@@ -430,72 +350,6 @@ class LlamaForCausalLM(nn.Module):
             xi, _ = ops.fused_add_rms_norm(h[i], res[i], self.norm.weight, self.norm.eps)
             outs.append(xi)
         return torch.cat(outs, 0)
-
-    # ------------------------------------------------------------------ two-stream prefill
-    def two_stream_ok(self) -> bool:
-        """One GPU, whole model, dense MLP: a large prefill-only step of whole sequences may
-        run as two halves on two streams (``_forward_two_streams``)."""
-        return (get_state().tp_size == 1 and self.first and self.last and bool(self.layers)
-                and not self.cfg.is_moe and self.layers[0].input_layernorm.weight.is_cuda)
-
-    def _side_stream(self, device) -> torch.cuda.Stream:
-        st = getattr(self, "_side", None)
-        if st is None:
-            st = self._side = torch.cuda.Stream(device=device)
-        return st
-
-    def _forward_two_streams(self, positions, x, ctx):
-        """A prefill-only step split at a sequence boundary (engine/model_runner.py
-        ``_split_prefill``): half A on the current stream, half B on a side stream, B's
-        attention part of layer l released by A's attention part of layer l, so B runs
-        about half a layer behind:
-
-            main:  attn(A, l)  MLP(A, l)         attn(A, l+1)  MLP(A, l+1) ...
-            side:              attn(B, l)  MLP(B, l)           attn(B, l+1) ...
-
-        The prefill GEMMs are power-capped (profiles/prefill_gemm_clock_power_r4.txt: MFMA
-        pipes busy 85 % at 1.74 GHz, 1400 W); the other half's memory-bound kernels
-        (attention, RMSNorm, SiLU-and-mul, the K / V writes) run in the headroom beside
-        them instead of after them.  The halves share no sequence, so they share no KV
-        block: the same math as the unsplit step (only the GEMMs' M differs)."""
-        a, ma, mb = ctx.attn.split
-        ctxs = (dataclasses.replace(ctx, attn=ma), dataclasses.replace(ctx, attn=mb))
-        pos = (positions[:a], positions[a:])
-        main = torch.cuda.current_stream(x.device)
-        side = self._side_stream(x.device)
-        side.wait_stream(main)                 # the embedding rows and the split metadata
-        x.record_stream(side)                  # half B reads x[a:] on the side stream
-        xs, res = [x[:a], x[a:]], [None, None]
-
-        def attn_part(i, layer):
-            ln1 = layer.input_layernorm
-            if res[i] is None:
-                res[i] = xs[i]
-                h = ln1(xs[i])
-            else:
-                h, res[i] = ln1(xs[i], res[i])
-            return layer.self_attn(pos[i], h, ctxs[i])
-
-        def mlp_part(i, layer, o):
-            h, res[i] = layer.post_attention_layernorm(o, res[i])
-            xs[i] = layer.mlp(h)
-
-        for layer in self.layers:
-            oa = attn_part(0, layer)
-            ev = torch.cuda.Event()
-            ev.record(main)
-            with torch.cuda.stream(side):
-                side.wait_event(ev)
-                ob = attn_part(1, layer)
-            mlp_part(0, layer, oa)
-            with torch.cuda.stream(side):
-                mlp_part(1, layer, ob)
-        ha, _ = self.norm(xs[0], res[0])
-        with torch.cuda.stream(side):
-            hb, _ = self.norm(xs[1], res[1])
-        main.wait_stream(side)
-        hb.record_stream(main)
-        return torch.cat([ha, hb], 0)
 
     # ------------------------------------------------------------------ norm-free small-M layer
     def fold_rs_weights(self, budget_fraction: float = 0.08) -> int:

@@ -41,6 +41,26 @@ def set_moe_mode(mode: str) -> None:
     MOE_MODE["mode"] = mode
 
 
+def pack_moe_experts(model: nn.Module, budget_fraction: float = 0.45) -> int:
+    """K14m's packed expert copies for every MoE block of ``model`` (Mixtral 8x7B bf16:
+    ~93 GB more on a 288 GB GPU), skipped when they would exceed ``budget_fraction`` of the
+    device or leave less than 16 GB free (KGC_MOE_PACK=0: never, for A/B runs).  Call
+    before the KV cache is sized.  Returns the bytes packed."""
+    import os
+    blocks = [m for m in model.modules() if isinstance(m, MoEBlock) and m.native]
+    if not blocks or os.environ.get("KGC_MOE_PACK", "1") == "0":
+        return 0
+    need = sum((b.w13.numel() + b.w2.numel()) * b.w13.element_size() for b in blocks)
+    free, total = torch.cuda.mem_get_info(blocks[0].w13.device)
+    if need > budget_fraction * total or need > free - (16 << 30):
+        log.info("K14m: %.1f GB of packed experts exceeds the budget; register-staged "
+                 "grouped GEMM", need / 1e9)
+        return 0
+    got = sum(b.pack_experts() for b in blocks)
+    log.info("K14m: packed the experts of %d MoE blocks (%.1f GB)", len(blocks), got / 1e9)
+    return got
+
+
 def grouped_expert_mlp(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor,
                        topk_w: torch.Tensor, topk_ids: torch.Tensor,
                        expert_offset: int = 0) -> torch.Tensor:
@@ -96,6 +116,19 @@ class MoEBlock(nn.Module):
         # ep mode on one node: the device-side all-to-all over xGMI peer memory
         # (parallel/expert_a2a.py), attached by the worker once the EP group exists
         self.ep_a2a = None
+        # K14m packed per-expert copies (ops.moe_pack), made by the worker before the KV
+        # cache is sized (pack_moe_experts); None: the register-staged grouped GEMM
+        self.w13p = None
+        self.w2p = None
+
+    def pack_experts(self) -> int:
+        """Packed K9m-layout copies of this block's experts for K14m (decode path).
+        Returns the bytes added."""
+        if not self.native or not ops.moe_packable(self.w13, self.w2) or self.w13p is not None:
+            return 0
+        self.w13p = ops.moe_pack(self.w13.data, True)
+        self.w2p = ops.moe_pack(self.w2.data, False)
+        return (self.w13p.numel() + self.w2p.numel()) * self.w13p.element_size()
 
     @property
     def graph_safe(self) -> bool:
@@ -108,7 +141,8 @@ class MoEBlock(nn.Module):
         # (host sync is fine there -- prefill is never graph-captured)
         small = topk_ids.numel() <= ops.MOE_NATIVE_MAX_ROWS * self.E_local
         if self.native and x.is_cuda and (small or torch.cuda.is_current_stream_capturing()):
-            return ops.fused_moe(x, self.w13, self.w2, topk_w, topk_ids, expert_offset, all_local)
+            return ops.fused_moe(x, self.w13, self.w2, topk_w, topk_ids, expert_offset, all_local,
+                                 self.w13p, self.w2p)
         return grouped_expert_mlp(x, self.w13, self.w2, topk_w, topk_ids, expert_offset)
 
     def map_weight(self, rest: str):
@@ -164,9 +198,14 @@ class MoEBlock(nn.Module):
         if a2a is not None and self.native and a2a.fits(x, topk_ids):
             return a2a.forward(x, topk_w, topk_ids,
                                lambda xs, w, ids, off: ops.fused_moe(xs, self.w13, self.w2, w,
-                                                                     ids, off),
+                                                                     ids, off, True, self.w13p,
+                                                                     self.w2p),
                                self.E_local)
         s = get_state()
+        if getattr(s, "phantom", False):
+            # phantom EP rank (no peers, no group): this rank's own expert work -- its local
+            # experts over every pair routed to them; the other ranks' shares are zeros
+            return self.experts(x, topk_w, topk_ids, expert_offset=self.e0, all_local=False)
         tp = s.tp_size
         T, H = x.shape
         flat_ids = topk_ids.reshape(-1).long()

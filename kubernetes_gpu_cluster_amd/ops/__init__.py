@@ -443,7 +443,7 @@ def sample_vp_finish(packed: torch.Tensor, out: Optional[torch.Tensor] = None) -
 
 __all__ = ["load_extension", "rms_norm", "fused_add_rms_norm", "layer_norm", "silu_mul",
            "rope_kv_write", "paged_attention_decode", "paged_attention_decode_rope", "prefill_attention", "sample", "sample_vp_partial", "sample_vp_finish",
-           "decode_partials", "decode_grid_z", "prefill_work_list", "ref"]
+           "decode_partials", "decode_grid_z", "moe_pack", "moe_packable", "prefill_work_list", "ref"]
 
 
 # ------------------------------------------------------------------ MoE (K13 / K14)
@@ -479,13 +479,48 @@ def moe_splitk(npairs: int, E: int, N: int, K: int, bm: int) -> int:
     return S
 
 
+def moe_pack(w: torch.Tensor, silu: bool) -> torch.Tensor:
+    """Per-expert K9m packed copy [E, N/128, K/64, 8192] of an expert weight stack
+    [E, N, K] (``dgemm_pack`` per expert; w13 SiLU-packed: gate / up 16-row groups
+    interleaved per 128-row tile), the operand of ``moe_dgemm`` (K14m)."""
+    E, N, K = w.shape
+    p = torch.empty(E, N // 128, K // 64, 8192, dtype=w.dtype, device=w.device)
+    for e in range(E):
+        _k().dgemm_pack(p[e], w[e], silu)
+    return p
+
+
+def moe_packable(w13: torch.Tensor, w2: torch.Tensor) -> bool:
+    """Shapes K14m's packed tiles cover: 2I % 128, I % 64, H % 128, K % 64."""
+    I2, H = w13.shape[1], w13.shape[2]
+    return I2 % 128 == 0 and (I2 // 2) % 64 == 0 and H % 128 == 0 and w2.shape[2] % 64 == 0
+
+
+def moe_dgemm_splitk(npairs: int, E: int, N: int, K: int, bm: int) -> int:
+    """K-slices of K14m's down projection: the used row blocks (at most npairs/bm + E)
+    times N/128 column tiles times S near one workgroup per CU, each slice >= 8 K-steps
+    (KGC_MOE_SPLITK overrides, as for the register-staged kernel)."""
+    if os.environ.get("KGC_MOE_SPLITK") is not None:
+        return max(1, int(os.environ["KGC_MOE_SPLITK"]))
+    blocks = min((npairs + bm - 1) // bm + E, max(1, npairs))
+    wgs = blocks * (N // 128)
+    S = 1
+    while S < 16 and wgs * S * 2 <= 320 and K // 64 // (2 * S) >= 8:
+        S *= 2
+    return S
+
+
 def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
               topk_ids: torch.Tensor, expert_offset: int = 0,
-              all_local: bool = True) -> torch.Tensor:
+              all_local: bool = True, w13p: Optional[torch.Tensor] = None,
+              w2p: Optional[torch.Tensor] = None) -> torch.Tensor:
     """K14: sum_j topk_w[t, j] * MLP_{topk_ids[t, j]}(x[t]) for the experts held here
     (global ids ``expert_offset .. expert_offset + w13.shape[0]``).  x [T, H];
     w13 [E, 2I, H] (gate rows then up rows); w2 [E, H, I].  No host synchronisation:
-    bucket sizes stay on the device, so the block is captured in decode graphs."""
+    bucket sizes stay on the device, so the block is captured in decode graphs.
+    ``w13p`` / ``w2p`` (``moe_pack``): K14m -- both projections on the K9m LDS-DMA
+    pipeline over packed per-expert tiles, the SiLU in the gate_up epilogue (no [rows, 2I]
+    intermediate, no silu_mul launch); else the register-staged grouped GEMM."""
     if not _gpu(x):
         return ref.moe_mlp_local(x, w13, w2, topk_w, topk_ids, expert_offset)
     k = _k()
@@ -501,6 +536,20 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     meta = torch.empty(1, dtype=torch.int32, device=dev)
     ids = topk_ids.contiguous()
     k.moe_align(sorted_ids, block_expert, meta, ids, expert_offset, E, bm)
+    if w13p is not None and w2p is not None:
+        act = torch.empty(rows, I2 // 2, dtype=x.dtype, device=dev)
+        k.moe_dgemm(act, x.contiguous(), w13p, sorted_ids, block_expert, meta, npairs, topk,
+                    bm, 1)
+        S = moe_dgemm_splitk(npairs, E, H, I2 // 2, bm)
+        alloc = torch.empty if all_local else torch.zeros
+        if S > 1:
+            y = alloc(S, npairs, H, dtype=torch.float32, device=dev)
+        else:
+            y = alloc(npairs, H, dtype=x.dtype, device=dev)
+        k.moe_dgemm(y, act, w2p, sorted_ids, block_expert, meta, npairs, topk, bm, 2)
+        out = torch.empty(T, H, dtype=x.dtype, device=dev)
+        k.moe_combine(out, y, topk_w.contiguous().float())
+        return out
     inter = torch.empty(rows, I2, dtype=x.dtype, device=dev)
     k.moe_gemm(inter, x.contiguous(), w13, sorted_ids, block_expert, meta, npairs, topk, bm,
                True, False)

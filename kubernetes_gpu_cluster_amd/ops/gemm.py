@@ -59,14 +59,6 @@ _enabled = os.environ.get("KGC_SKINNY_GEMM", "1") != "0"
 # "tail" (o / down -> residual add + RMSNorm).  S > 1: fp32 K-slices summed by the consumer.
 DG_MAX_M = 512
 _plan_dg: dict[tuple[int, int, int, str], tuple[int, int]] = {}
-# the norm-free layer at M = 65..512 (``nf_plan``): (M, N, K) of an o / down projection ->
-# (cfg, S, fan-in us, tail us): its fastest EPI_FANIN configuration and, graph-timed in the
-# same interleaved rounds, the regular tail it would replace (the "tail" plan + its
-# splitk_add_rms_norm / fused_add_rms_norm)
-_plan_fanin: dict[tuple[int, int, int], tuple[int, int, float, float]] = {}
-_fanin_enabled = os.environ.get("KGC_FANIN", "1") != "0"
-# A/B: run the norm-free layer wherever its plans exist, measured faster or not
-_nf_force = os.environ.get("KGC_NF_FORCE", "0") == "1"
 _dg_enabled = os.environ.get("KGC_DGEMM", "1") != "0"
 # packed weight copies for the packed K9m tiles: (data_ptr, silu) -> [N/128, K/64, 8192]
 # (data_ptr, silu) -> (weakref to the source weight, packed copy).  The weakref drops the
@@ -148,17 +140,6 @@ def packed_weight(w: torch.Tensor, silu: bool = False) -> Optional[torch.Tensor]
     return _packed_get(w, silu)
 
 
-def pack_folded(w: torch.Tensor, gamma: torch.Tensor, silu: bool) -> torch.Tensor:
-    """The packed K9m tiles of W diag(gamma) (``fold_norm_weight``): the norm-free layer's
-    qkv / gate_up operand (the row-major folded copy is freed again)."""
-    from . import _k
-    f = fold_norm_weight(w, gamma)
-    N, K = w.shape
-    p = torch.empty(N // 128, K // 64, 8192, dtype=w.dtype, device=w.device)
-    _k().dgemm_pack(p, f, silu)
-    return p
-
-
 def cfg_packed(cfg: int) -> bool:
     return _dg_info(cfg)[2]
 
@@ -193,62 +174,10 @@ def dgemm(x: torch.Tensor, w: torch.Tensor, cfg: int, S: int, epi: int = 1,
     return out
 
 
-class _NormFreeBuffers:
-    """Per-device state of the K9m fan-in epilogue (EPI_FANIN): per-tile row sums of
-    squares, the row scales rs = rsqrt(mean(x^2) + eps) its consumers read, and the
-    ticket counters (zero between launches: every launch leaves them zero)."""
-
-    def __init__(self, device):
-        self.ssp = torch.zeros(DG_MAX_M * 128, dtype=torch.float32, device=device)
-        self.rs = torch.zeros(DG_MAX_M, dtype=torch.float32, device=device)
-        self.cnt = torch.zeros(1024, dtype=torch.int32, device=device)
-
-
-_nf_bufs: dict = {}
-
-
-def _nf_state(device: torch.device) -> _NormFreeBuffers:
-    b = _nf_bufs.get(device)
-    if b is None:
-        b = _nf_bufs[device] = _NormFreeBuffers(device)
-    return b
-
-
-def dgemm_fanin(x: torch.Tensor, w: torch.Tensor, cfg: int, S: int, residual: torch.Tensor,
-                eps: float) -> torch.Tensor:
-    """residual += x W^T with the split-K combine, the residual add and the row norms in
-    ONE K9m launch (EPI_FANIN, gemm_decode.hip): returns rs [M] fp32 =
-    rsqrt(mean(residual^2) + eps), the row scale of the next RMSNorm, which the norm-free
-    layer's consumers apply to their gamma-folded weights' outputs.  rs lives in a
-    per-device buffer that the next fan-in launch overwrites."""
-    from . import _k
-    M, N = x.shape[0], w.shape[0]
-    wk = _dg_weight(w, cfg, False)
-    if wk is None:
-        raise RuntimeError("K9m plan names a packed tile but the weight was not packed")
-    st = _nf_state(x.device)
-    ws = torch.empty(S, M, N, dtype=torch.float32, device=x.device)
-    _k().dgemm_fanin(ws, x, wk, cfg, residual, st.ssp, st.rs, st.cnt, eps)
-    return st.rs[:M]
-
-
 def _dg_plan(x: torch.Tensor, w: torch.Tensor, kind: str):
     if not _plan_dg or not x.is_cuda or x.dim() != 2 or x.stride(1) != 1 or x.stride(0) % 8:
         return None
     return _plan_dg.get((x.shape[0], w.shape[0], w.shape[1], kind))
-
-
-def nf_silu(x: torch.Tensor, w: torch.Tensor, wf: torch.Tensor, cfg: int, S: int,
-            rscale: torch.Tensor) -> torch.Tensor:
-    """silu(r * g) * (r * u) of the norm-free layer's merged gate_up: x the raw residual,
-    ``wf`` the gamma-folded weight in ``cfg``'s layout, r = ``rscale`` per row."""
-    from . import _k
-    if S == 1:
-        return dgemm(x, w, cfg, 1, epi=2, rscale=rscale, wk=wf)
-    ws = dgemm(x, w, cfg, S, wk=wf)
-    out = torch.empty(x.shape[0], w.shape[0] // 2, dtype=x.dtype, device=x.device)
-    _k().splitk_reduce_silu(out, ws, _dg_info(cfg)[2], rscale)
-    return out
 
 
 def linear_silu(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -489,9 +418,24 @@ def dg_table_path(model: str, tp: int = 1) -> str:
     return os.path.join(root, "profiles", "tunableop", f"k9m_{model}_tp{tp}_gfx950.json")
 
 
+def dg_fingerprint() -> dict:
+    """What an offline K9m table's (cfg, S) picks depend on: the GPU architecture and
+    device name, and the id -> tile map of the loaded kernel library (ids index kCfg in
+    gemm_decode.hip; a renumbered or retiled id would silently mean another kernel)."""
+    from . import _k
+    props = torch.cuda.get_device_properties(torch.cuda.current_device())
+    n = int(_k().dgemm_num_cfgs())
+    return {"arch": str(getattr(props, "gcnArchName", "")).split(":")[0], "device": props.name,
+            "num_cfgs": n, "cfgs": [list(_dg_info(c)[:2]) + [int(_dg_info(c)[2])]
+                                    for c in range(n)]}
+
+
 def load_dg_table(model: str, tp: int = 1) -> int:
     """Read the offline K9m table of this model / TP degree (KGC_DGEMM_TABLE: another file;
-    "0": none).  Returns the entries loaded."""
+    "0": none).  Returns the entries loaded.  The table's fingerprint (``dg_fingerprint``)
+    must match the running GPU and kernel library, or the whole table is dropped and
+    start-up tuning runs; each entry must also fit its shape (N % BN == 0,
+    S <= K / 64) or it is dropped alone."""
     import json
     _dg_table.clear()
     path = os.environ.get("KGC_DGEMM_TABLE") or dg_table_path(model, tp)
@@ -499,15 +443,37 @@ def load_dg_table(model: str, tp: int = 1) -> int:
         return 0
     with open(path) as f:
         t = json.load(f)
+    fp = t.get("fingerprint")
+    cur = dg_fingerprint()
+    if fp is None:
+        log.warning("K9m: %s has no fingerprint; ignored (start-up tuning runs)", path)
+        return 0
+    if fp != cur:
+        diff = sorted(k for k in set(fp) | set(cur) if fp.get(k) != cur.get(k))
+        log.warning("K9m: %s was tuned for another GPU or kernel library (%s differ); "
+                    "ignored, start-up tuning runs", path, ", ".join(diff))
+        return 0
+    dropped = 0
     for e in t.get("entries", []):
         key = (int(e["M"]), int(e["N"]), int(e["K"]), str(e["kind"]))
-        _dg_table[key] = None if e.get("cfg") is None else (int(e["cfg"]), int(e["S"]))
+        if e.get("cfg") is None:
+            _dg_table[key] = None
+            continue
+        cfg, S = int(e["cfg"]), int(e["S"])
+        if not (0 <= cfg < cur["num_cfgs"]) or key[1] % cur["cfgs"][cfg][1] or not (
+                1 <= S <= key[2] // 64):
+            dropped += 1
+            continue
+        _dg_table[key] = (cfg, S)
+    if dropped:
+        log.warning("K9m: %d entries of %s do not fit their shapes; dropped", dropped, path)
     log.info("K9m: %d offline selections from %s", len(_dg_table), path)
     return len(_dg_table)
 
 
 def save_dg_table(path: str, res: dict, meta: dict) -> int:
-    """Write the K9m decisions of a tuner run (``tune_skinny``'s result dict)."""
+    """Write the K9m decisions of a tuner run (``tune_skinny``'s result dict), with the
+    fingerprint ``load_dg_table`` checks."""
     import json
     ent = []
     for key, v in sorted(res.items()):
@@ -522,40 +488,12 @@ def save_dg_table(path: str, res: dict, meta: dict) -> int:
                     "best_k9m": list(best) if best else None})
     os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
     with open(path, "w") as f:
-        json.dump(dict(meta, entries=ent), f, indent=1)
+        json.dump(dict(meta, fingerprint=dg_fingerprint(), entries=ent), f, indent=1)
     return len(ent)
-
-
-def nf_plan(M: int, shapes) -> Optional[list]:
-    """K9m plans of (qkv, o, gate_up, down) at this M for the norm-free layer
-    (``LlamaForCausalLM._forward_nf``), or None: qkv / gate_up run on K9m ("qkv" / "silu"
-    plans; gate_up's S = 1 epilogue needs a config with the row-scale epilogue), o / down on
-    their fan-in plans, and tuning measured the two fan-in launches faster than the
-    regular tails they replace."""
-    if not (_fanin_enabled and SKINNY_MAX_M < M <= DG_MAX_M):
-        return None
-    from . import _k
-    (nq, kq), (no, ko), (ng, kg), (nd, kd) = shapes
-    q = _plan_dg.get((M, nq, kq, "qkv"))
-    g = _plan_dg.get((M, ng, kg, "silu"))
-    o = _plan_fanin.get((M, no, ko))
-    d = _plan_fanin.get((M, nd, kd))
-    if q is None or g is None or o is None or d is None:
-        return None
-    if g[1] == 1 and not _k().dgemm_cfg_has_aux(g[0]):
-        return None
-    if o[2] + d[2] >= o[3] + d[3] and not _nf_force:
-        return None
-    return [q, (o[0], o[1]), g, (d[0], d[1])]
-
-
-def fanin_plan() -> dict:
-    return dict(_plan_fanin)
 
 
 def clear_plan() -> None:
     _dg_table.clear()
-    _plan_fanin.clear()
     _best_sk.clear()
     _best_silu.clear()
     _best_rs.clear()
@@ -663,8 +601,7 @@ def _time_graphed(body, reps: int) -> float:
 @torch.inference_mode()
 def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: float = 0.97,
                 reps: int = 3, norm_shapes=(), norm_max_m: int = 16, silu_shapes=(),
-                tail_shapes=(), qkv_dims=None, rs_shapes: bool = False,
-                nf: bool = False) -> dict:
+                tail_shapes=(), qkv_dims=None, rs_shapes: bool = False) -> dict:
     """Time hipBLASLt against every skinny configuration for each weight shape and
     batch size M (decode buckets <= SKINNY_MAX_M) and record the skinny kernel where it
     is faster by more than ``1 - margin``.  Each timing sweeps ALL weights of the shape
@@ -676,9 +613,7 @@ def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: floa
     ``tail_shapes``: (N, K) of row-parallel projections feeding a residual add + RMSNorm
     (``linear_add_rms``), timed with that norm on both sides.  ``rs_shapes``: also time the
     norm-free layer's epilogues at M <= 16 (tail -> SK_ACC_SS, norm -> SK_RSCALE, silu ->
-    SK_RSCALE_SILU) for ``rs_plan``.  ``nf``: also time the o / down projections' K9m
-    fan-in epilogue against their regular tails for ``nf_plan`` (the norm-free layer at
-    M = 65..512)."""
+    SK_RSCALE_SILU) for ``rs_plan``."""
     if not _enabled:
         return {}
     by_shape: dict[tuple[int, int], list[torch.Tensor]] = {}
@@ -736,7 +671,7 @@ def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: floa
             kind = ("silu" if (N, K) in silu_shapes else
                     "tail" if (N, K) in tail_shapes else "qkv" if qd else "plain")
             _tune_dgemm(ws, N, K, [m for m in ms if SKINNY_MAX_M < m <= DG_MAX_M], margin,
-                        reps, res, kind, qd, fanin=nf)
+                        reps, res, kind, qd)
     log.info("GEMM tuning: %d shapes in %.1f s", len(res), time.time() - t0)
     return res
 
@@ -745,7 +680,10 @@ def tune_skinny(weights: Iterable[torch.Tensor], ms: Iterable[int], margin: floa
 # was packed; 4 loader waves (6, 7), split loaders (8, 9) and XCD-paired 128-row blocks (10)
 # per tools/dgemm_bench.py.
 _DG_SPLITS = tuple(int(v) for v in
-                   os.environ.get("KGC_DGEMM_SPLITS", "1,2,3,4,5,6,8").split(","))
+                   os.environ.get("KGC_DGEMM_SPLITS", "1,2,3,4,5,6,8,12,16").split(","))
+# a K9m launch runs ONE workgroup per CU: candidates whose grid exceeds the 256 CUs by more
+# than this are a second round of workgroups behind the first and are not timed
+_DG_MAX_GRID = 264
 # the tuner's refinement: this many fastest K9m candidates re-timed (with hipBLASLt) in
 # this many interleaved rounds, the median decides
 _DG_REFINE = int(os.environ.get("KGC_DGEMM_REFINE", "3"))
@@ -756,7 +694,9 @@ def _dg_candidates(M: int, N: int, K: int, kind: str, packed: bool):
     # (K9v / K9r, measured slower than K9m on every M = 256 shape, are not in the engine's
     # library: tools/research/; profiles/README.md "Round 3: K9r" / "Round 3: K9v")
     from . import _k
-    cfgs = [5, 7, 2] if M <= 128 else [6, 8, 4, 0, 10]
+    # 11-14: packed 64 / 80 / 112-wide column tiles (gemm_decode.hip kCfg) for the narrow
+    # shards of a TP = 8 rank
+    cfgs = [5, 7, 2, 14, 11] if M <= 128 else [6, 8, 4, 0, 10, 11, 12, 13, 14]
     out = []
     for c in range(_k().dgemm_num_cfgs()):
         if c not in cfgs:
@@ -764,6 +704,9 @@ def _dg_candidates(M: int, N: int, K: int, kind: str, packed: bool):
         bm, bn, pk = _dg_info(c)
         if (pk and not packed) or N % bn:
             continue
+        epis = int(_k().dgemm_cfg_epis(c))
+        if kind == "silu" and not (epis >> 2) & 1 and ((M + bm - 1) // bm) * (N // bn) >= 192:
+            continue            # S = 1 would need the SiLU epilogue this tile does not have
         # S = 3, 5, 6 fill the CUs where powers of two do not (qkv at M = 256: 48
         # column tiles x 5 = 240 workgroups vs 192 at S = 4); no XCD pairing for them.
         # gate_up + SiLU: the fused epilogue (S = 1) where its column tiles fill the chip,
@@ -772,13 +715,16 @@ def _dg_candidates(M: int, N: int, K: int, kind: str, packed: bool):
         tiles = ((M + bm - 1) // bm) * (N // bn)
         splits = (1,) if kind == "silu" and tiles >= 192 else _DG_SPLITS
         for S in splits:
-            if S <= K // 64:
-                out.append((c, S))
+            if S > K // 64 or (S > 1 and tiles * S > _DG_MAX_GRID):
+                continue
+            if S == 1 and kind == "silu" and not (epis >> 2) & 1:
+                continue
+            out.append((c, S))
     return out
 
 
 def _tune_dgemm(ws, N: int, K: int, ms, margin: float, reps: int, res: dict,
-                kind: str, qkv_dims=None, fanin: bool = False) -> None:
+                kind: str, qkv_dims=None) -> None:
     """hipBLASLt vs the K9m candidates at each M in ``ms``, over all weights of the shape
     (HBM-resident, as in a decode step), each side timed WITH its consumer: "silu" the
     SiLU-and-mul, "tail" the residual add + RMSNorm, "qkv" the fused RoPE / KV-write /
@@ -797,9 +743,6 @@ def _tune_dgemm(ws, N: int, K: int, ms, margin: float, reps: int, res: dict,
                 if fixed is not None:
                     _plan_dg[key] = fixed
                 res[key] = (fixed, float("nan"), float("nan"), fixed)
-                if kind == "tail" and fanin and _fanin_enabled:
-                    x = torch.randn(M, K, dtype=ws[0].dtype, device=ws[0].device)
-                    _tune_fanin(ws, x, M, N, K, reps, packed, _tail_runner(ws, x, fixed), res)
                 continue
         dev, dt = ws[0].device, ws[0].dtype
         x = torch.randn(M, K, dtype=dt, device=dev)
@@ -896,88 +839,6 @@ def _tune_dgemm(ws, N: int, K: int, ms, margin: float, reps: int, res: dict,
         log.info("gemm M=%d N=%d K=%d %s: hipBLASLt %.1f us, K9m %s %.1f us -> %s", M, N, K,
                  kind, lib_t * 1e3 / n, best_cfg, best_t * 1e3 / n,
                  "K9m" if chosen else "hipBLASLt")
-        if kind == "tail" and fanin and _fanin_enabled:
-            tail_fn = dict((c, fn) for _, c, fn in timed).get(chosen, lib)
-            _tune_fanin(ws, x, M, N, K, reps, packed, tail_fn, res)
-
-
-_FANIN_SPLITS = (1, 2, 3, 4, 5, 6, 8)      # the S values gemm_decode.hip's reducer unrolls
-
-
-def _tail_runner(ws, x, plan):
-    """The regular tail of a row-parallel projection under ``plan`` ((cfg, S) or None =
-    hipBLASLt): GEMM + its residual add / RMSNorm kernel, over every weight of the shape."""
-    from . import _k, fused_add_rms_norm
-    M, N = x.shape[0], ws[0].shape[0]
-    res_t = torch.zeros(M, N, dtype=x.dtype, device=x.device)
-    gamma = torch.ones(N, dtype=x.dtype, device=x.device)
-    red = torch.empty(M, N, dtype=x.dtype, device=x.device)
-    if plan is None:
-        def run():
-            for w in ws:
-                fused_add_rms_norm(F.linear(x, w), res_t, gamma, 1e-6)
-        return run
-    cfg, S = plan
-    wl = [_dg_weight(w, cfg, False) for w in ws]
-    buf = (torch.empty(S, M, N, dtype=torch.float32, device=x.device) if S > 1 else
-           torch.empty(M, N, dtype=x.dtype, device=x.device))
-
-    def run():
-        for w in wl:
-            if S == 1:
-                _k().dgemm(buf, x, w, cfg, 1)
-                fused_add_rms_norm(buf, res_t, gamma, 1e-6)
-            else:
-                _k().dgemm(buf, x, w, cfg, 0)
-                _k().splitk_add_rms_norm(red, buf, res_t, gamma, 1e-6)
-    return run
-
-
-def _tune_fanin(ws, x, M: int, N: int, K: int, reps: int, packed: bool, tail_fn,
-                res: dict) -> None:
-    """The EPI_FANIN candidates of an o / down projection (split-K combine + residual add +
-    row norms in the launch) against the regular tail the norm-free layer would replace
-    (``tail_fn``: the chosen K9m / hipBLASLt GEMM + its norm kernel).  One eager pass ranks
-    the candidates; the fastest few and the tail are then re-timed graph-captured (the
-    tail's extra launch boundary counts as it does in a decode step) in interleaved
-    rounds, medians decide."""
-    from . import _k
-    dev, dt = x.device, x.dtype
-    resid = torch.zeros(M, N, dtype=dt, device=dev)
-    timed = []
-    cfgs = [5, 7, 2] if M <= 128 else [6, 4, 0, 10, 5, 7]
-    for c in cfgs:
-        bm, bn, pk = _dg_info(c)
-        if (pk and not packed) or N % bn or not _k().dgemm_cfg_has_aux(c):
-            continue
-        for S in _FANIN_SPLITS:
-            if S > K // 64:
-                continue
-
-            def run(c=c, S=S):
-                for w in ws:
-                    dgemm_fanin(x, w, c, S, resid, 1e-6)
-            timed.append((_time(run, reps), (c, S), run))
-            log.debug("gemm M=%d N=%d K=%d fan-in %s: %.1f us", M, N, K, (c, S),
-                      timed[-1][0] * 1e3 / len(ws))
-    if not timed:
-        return
-    timed.sort(key=lambda e: e[0])
-    top = timed[:_DG_REFINE]
-    rounds: dict = {c: [] for _, c, _ in top}
-    tail_r = []
-    for _ in range(_DG_REFINE_ROUNDS):
-        tail_r.append(_time_graphed(tail_fn, reps))
-        for _, c, fn in top:
-            rounds[c].append(_time_graphed(fn, reps))
-    med = {c: sorted(v)[len(v) // 2] for c, v in rounds.items()}
-    best = min(med, key=med.get)
-    n = len(ws)
-    fan_us, tail_us = med[best] * 1e3 / n, sorted(tail_r)[len(tail_r) // 2] * 1e3 / n
-    _plan_fanin[(M, N, K)] = (best[0], best[1], fan_us, tail_us)
-    res[(M, N, K, "fanin")] = (best, tail_us, fan_us, best)
-    log.info("gemm M=%d N=%d K=%d fan-in: tail %.1f us, EPI_FANIN %s %.1f us", M, N, K,
-             tail_us, best, fan_us)
 
 
 def _tune_silu(ws, x, M: int, N: int, K: int, reps: int, margin: float) -> None:

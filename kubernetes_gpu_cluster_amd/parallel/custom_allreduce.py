@@ -224,7 +224,7 @@ class CustomAllReduce:
 
     # ------------------------------------------------------------------ calibration
     def calibrate(self, hidden: int, dtype: torch.dtype, rows: list[int], tp_group, cpu_group,
-                  reps: int = 20) -> dict:
+                  reps: int = 20, graphs: bool = True) -> dict:
         """Time every form on THIS node at each decode message size (rows x hidden) and
         make the fastest the policy (the crossovers were fixed from a
         one-GPU rehearsal).  Collective over the TP group: every rank runs the same
@@ -234,13 +234,63 @@ class CustomAllReduce:
                  on 256 workgroups: the grid sized for large messages) / 'rccl';
           fused  'fused1' / 'fused2' (one launch with the residual add + RMSNorm) /
                  'split' (the plain choice, then fused_add_rms_norm).
+        ``graphs``: each form's ``reps``-call loop is captured in a hipGraph and the table is
+        chosen on REPLAY times, as the decode graphs run these kernels (at
+        8-64 KB the eager launch rate is comparable to the kernel time, and eager timing
+        misranked K9m candidates against the graphs); the eager times are kept beside them
+        (``eager_us``, ``graph_minus_eager_us``).  'rccl' is a candidate only where it can
+        be captured: not over gloo (ADVICE r5 -- a host-staged gloo all-reduce inside a
+        decode graph cannot be captured).  ``cpu_group`` None: a phantom rank (no peers
+        to synchronise with or reduce over).
         The thresholds stay the fallback past the largest calibrated size."""
         from .. import ops
         dev = self.device
-        res = {"hidden": hidden, "rows": [], "bytes": [], "us": {}}
+        res = {"hidden": hidden, "rows": [], "bytes": [], "us": {}, "eager_us": {},
+               "timing": "graph" if graphs else "eager"}
         forms = ("one", "two", "two_wide", "rccl", "fused1", "fused2", "split")
         plain_forms = forms[:4]
-        times = []
+        gloo = tp_group is None or dist.get_backend(tp_group) == dist.Backend.GLOO
+        rccl_ok = tp_group is not None and not (graphs and gloo)
+
+        def barrier():
+            if cpu_group is not None:
+                dist.barrier(group=cpu_group)
+
+        def timed(fn):
+            """(eager us, graph us) per call of fn over ``reps`` calls."""
+            torch.cuda.synchronize(dev)
+            barrier()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                fn()
+            e1.record()
+            e1.synchronize()
+            eager = e0.elapsed_time(e1) * 1e3 / reps
+            if not graphs:
+                return eager, eager
+            g = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize(dev)
+            barrier()
+            with torch.cuda.graph(g):
+                for _ in range(reps):
+                    fn()
+            torch.cuda.synchronize(dev)
+            barrier()
+            g.replay()                                   # warm replay
+            torch.cuda.synchronize(dev)
+            ts = []
+            for _ in range(3):
+                barrier()
+                e0.record()
+                g.replay()
+                e1.record()
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1) * 1e3 / reps)
+            del g
+            return eager, sorted(ts)[1]
+
+        times, etimes = [], []
         w = torch.ones(hidden, dtype=dtype, device=dev)
         saved = self.table
         self.table = None
@@ -256,7 +306,7 @@ class CustomAllReduce:
                 if form in ("one", "two", "two_wide"):
                     self._launch_plain(x, form)
                 elif form == "rccl":
-                    if dist.get_backend(tp_group) == dist.Backend.GLOO:
+                    if gloo:
                         xf = x.float()              # gloo: the fp32 path comm.py takes
                         dist.all_reduce(xf, group=tp_group)
                         x.copy_(xf)
@@ -267,55 +317,60 @@ class CustomAllReduce:
                                                      self.fdata2 if form == "fused2" else
                                                      self.fdata, self.sig, self.rank,
                                                      self.cap, form == "fused2")
-            row = []
+            row, erow = [], []
             for form in forms:
                 if (form in ("one", "two", "two_wide") and not ok_x) or (
-                        form in ("fused1", "fused2") and not ok_f) or form == "split":
+                        form in ("fused1", "fused2") and not ok_f) or form == "split" or (
+                        form == "rccl" and not rccl_ok):
                     row.append(float("inf"))
+                    erow.append(float("inf"))
                     continue
                 torch.cuda.synchronize(dev)
-                dist.barrier(group=cpu_group)
+                barrier()
                 for _ in range(3):
                     x.copy_(x0)
                     run(form)
-                torch.cuda.synchronize(dev)
-                dist.barrier(group=cpu_group)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(reps):
-                    run(form)
-                e1.record()
-                e1.synchronize()
-                row.append(e0.elapsed_time(e1) * 1e3 / reps)
+                x.copy_(x0)
+                try:
+                    e, g = timed(lambda form=form: run(form))
+                except RuntimeError as ex:          # e.g. a backend that cannot be captured
+                    log.warning("all-reduce calibration: %s not timed (%s)", form, ex)
+                    e = g = float("inf")
+                row.append(g)
+                erow.append(e)
             # 'split' = the fastest plain form + one fused_add_rms_norm launch
-            torch.cuda.synchronize(dev)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(reps):
-                ops.fused_add_rms_norm(x, resid, w, 1e-6)
-            e1.record()
-            e1.synchronize()
-            row[forms.index("split")] = min(row[:len(plain_forms)]) + e0.elapsed_time(e1) * 1e3 / reps
+            e, g = timed(lambda: ops.fused_add_rms_norm(x, resid, w, 1e-6))
+            row[forms.index("split")] = min(row[:len(plain_forms)]) + g
+            erow[forms.index("split")] = min(erow[:len(plain_forms)]) + e
             times.append(row)
+            etimes.append(erow)
             res["rows"].append(m)
             res["bytes"].append(nb)
-        t = torch.tensor(times, dtype=torch.float64)
+        t = torch.tensor([times, etimes], dtype=torch.float64)
         t[torch.isinf(t)] = 1e30
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=cpu_group)
+        if cpu_group is not None:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=cpu_group)
         table = []
         for i, nb in enumerate(res["bytes"]):
-            tr = t[i].tolist()
+            tr, te = t[0, i].tolist(), t[1, i].tolist()
             plain = min(plain_forms, key=lambda f: tr[forms.index(f)])
             fused = min(("fused1", "fused2", "split"), key=lambda f: tr[forms.index(f)])
             table.append((nb, plain, fused))
             for f in forms:
-                v = tr[forms.index(f)]
+                v, ve = tr[forms.index(f)], te[forms.index(f)]
                 res["us"].setdefault(f, []).append(None if v >= 1e29 else round(v, 2))
+                res["eager_us"].setdefault(f, []).append(None if ve >= 1e29 else round(ve, 2))
+                res.setdefault("graph_minus_eager_us", {}).setdefault(f, []).append(
+                    None if v >= 1e29 or ve >= 1e29 else round(v - ve, 2))
+            # would eager timing have chosen differently at this size?
+            pe = min(plain_forms, key=lambda f: te[forms.index(f)])
+            fe = min(("fused1", "fused2", "split"), key=lambda f: te[forms.index(f)])
+            res.setdefault("eager_choice_differs", []).append(pe != plain or fe != fused)
         res["table"] = [list(e) for e in table]
         self.table, self.calibration = table, res
         del saved
         torch.cuda.synchronize(dev)
-        dist.barrier(group=cpu_group)
+        barrier()
         return res
 
     def check(self) -> None:
@@ -426,6 +481,10 @@ def maybe_init_custom_allreduce(ps, device: torch.device, hidden: int = 0,
         car = PhantomAllReduce(ps.tp_rank, ps.tp_size, device)
         log.info("phantom TP rank %d of %d: xGMI all-reduce against local peer buffers",
                  ps.tp_rank, ps.tp_size)
+        if calibrate_rows and hidden and _calibration_wanted():
+            # the same graph-timed calibration, over local peer buffers (no group to sync or
+            # reduce over): the phantom's policy comes from its own replay times
+            car.calibrate(hidden, dtype, calibrate_rows, None, None)
         return car
     try:
         car = CustomAllReduce(ps.tp_cpu_group, ps.tp_rank, ps.tp_size, device)

@@ -128,11 +128,63 @@ class ExpertAllToAll:
             self._opened = []
 
 
+class PhantomExpertAllToAll(ExpertAllToAll):
+    """The device-side EP all-to-all of rank ``rank`` of an EP = ``world`` group whose peers
+    do not exist (KGC_TP_PHANTOM with ``--moe-parallel ep``, the analogue of
+    ``PhantomAllReduce``): every peer buffer is a local allocation and the peers' arrival
+    flags in this rank's signal are raised far ahead of any epoch
+    (kgc.ep_raise_peer_flags), so dispatch / receive / grouped MLP / return / combine run
+    their full per-rank sequence inside the captured decode graphs without waiting.  The
+    rows this rank sends to its "peers" land in local HBM, not over xGMI, and the peers'
+    receive regions stay empty (zero counts): the owner's grouped MLP sees this rank's own
+    rows only and the combine reads zeros for the others -- per-rank TIMING of the EP
+    decode step at its real shapes, never a model's outputs."""
+
+    FLAG_VALUE = 1 << 30
+
+    def __init__(self, rank: int, world: int, device: torch.device, max_pairs: int,
+                 hidden: int, dtype: torch.dtype):
+        if world not in SUPPORTED_WORLD:
+            raise ValueError(f"EP all-to-all supports {SUPPORTED_WORLD} ranks, not {world}")
+        from .. import ops
+        ops.load_extension(strict=True)
+        k = torch.ops.kgc
+        if max_pairs > int(k.ep_max_pairs()):
+            raise ValueError(f"{max_pairs} pairs per call > kernel limit {int(k.ep_max_pairs())}")
+        self.rank, self.world, self.device = rank, world, device
+        self.C, self.H, self.dtype = int(max_pairs), int(hidden), dtype
+        self._err_host = None
+        with torch.cuda.device(device):
+            self.sig_bytes = int(k.ep_signal_bytes())
+            nbytes = self.sig_bytes + int(k.ep_region_bytes(world, self.C, self.H,
+                                                            torch.finfo(dtype).bits // 8))
+            bases = [int(k.ar_alloc(nbytes)) for _ in range(world)]
+            k.ep_raise_peer_flags(bases[rank], rank, world, self.FLAG_VALUE)
+            torch.cuda.synchronize(device)
+        self._own, self._opened = bases[rank], []
+        self._peers = [b for r, b in enumerate(bases) if r != rank]
+        self.sig = bases
+        self.data = [b + self.sig_bytes for b in bases]
+
+    def close(self) -> None:
+        if self._own:
+            torch.cuda.synchronize(self.device)
+            for p in self._peers + [self._own]:
+                torch.ops.kgc.ar_free(p)
+            self._own, self._peers = 0, []
+
+
 def maybe_init_expert_a2a(ps, device: torch.device, max_tokens: int, top_k: int, hidden: int,
                           dtype: torch.dtype) -> Optional[ExpertAllToAll]:
-    """The device-side EP all-to-all for this rank's TP group, or None (eager all-to-all)."""
+    """The device-side EP all-to-all for this rank's TP group, or None (eager all-to-all).
+    A phantom TP rank (parallel/state.py init_phantom) gets ``PhantomExpertAllToAll``."""
     if os.environ.get("KGC_EP_IPC", "1") == "0" or ps.tp_size not in SUPPORTED_WORLD:
         return None
+    if getattr(ps, "phantom", False):
+        log.info("phantom EP rank %d of %d: device all-to-all against local peer buffers",
+                 ps.tp_rank, ps.tp_size)
+        return PhantomExpertAllToAll(ps.tp_rank, ps.tp_size, device, max_tokens * top_k,
+                                     hidden, dtype)
     try:
         return ExpertAllToAll(ps.tp_cpu_group, ps.tp_rank, ps.tp_size, device,
                               max_tokens * top_k, hidden, dtype)

@@ -450,3 +450,35 @@ def test_allreduce_policy_past_the_calibrated_sizes():
     assert car.fused_form(64 << 10) == "fused1" and car.fused_form(1 << 20) == "fused2"
     car.table = None
     assert car.plain_form(64 << 10) == "one" and car.plain_form(1 << 20) == "two"
+
+
+def test_phantom_mode_is_refused_without_the_measurement_opt_in(monkeypatch):
+    """KGC_TP_PHANTOM serves rank 0's shard with zero peers, so its completions are wrong by
+    construction: a Worker built by any serving entrypoint (allow_phantom left
+    False) refuses the mode instead of serving; the fault-injection hook stays inert
+    without KGC_TESTING=1."""
+    import pytest
+    from kubernetes_gpu_cluster_amd.engine import worker as W
+    from kubernetes_gpu_cluster_amd.engine.config import EngineConfig
+    from kubernetes_gpu_cluster_amd.parallel.state import ParallelState, set_state
+    monkeypatch.setenv("KGC_TP_PHANTOM", "8")
+    try:
+        with pytest.raises(ValueError, match="per-rank measurement"):
+            W.Worker(EngineConfig(model="tiny-llama", random_init=True, device="cpu"))
+    finally:
+        set_state(ParallelState())
+    monkeypatch.delenv("KGC_TP_PHANTOM")
+    monkeypatch.setenv("KGC_FAULT_PERTURB_TP_RANK", "1")
+    monkeypatch.delenv("KGC_TESTING", raising=False)
+
+    class _PS:
+        tp_size, tp_rank = 2, 1
+    lin = torch.nn.Linear(4, 4, bias=False)
+    model = torch.nn.Module()
+    model.o_proj = lin
+    before = lin.weight.detach().clone()
+    W._fault_perturb_shard(model, _PS())
+    assert torch.equal(lin.weight, before)
+    monkeypatch.setenv("KGC_TESTING", "1")
+    W._fault_perturb_shard(model, _PS())
+    assert not torch.equal(lin.weight, before)

@@ -248,36 +248,6 @@ def test_prefill_rope_fused_equals_unfused(gpu, monkeypatch):
         _assert_greedy_agrees(got, ref, 8)
 
 
-def test_two_stream_prefill_equals_one_stream(gpu, monkeypatch):
-    """One GPU: a prefill-only step of several whole prompts split at a sequence boundary
-    into two halves on two streams (models/llama.py _forward_two_streams, B paced half a
-    layer behind A) continues like the one-stream step.  The halves share no sequence and
-    no KV block; only the GEMMs' M differs (hipBLASLt may tile M = a and M = T apart), so
-    greedy runs agree up to a near-tie."""
-    g = torch.Generator().manual_seed(9)
-    prompts = [torch.randint(100, 128000, (n,), generator=g).tolist() for n in (40, 300, 150, 7)]
-    params = [SamplingParams(temperature=0.0, max_tokens=10, ignore_eos=True, logprobs=2)
-              for _ in prompts]
-    monkeypatch.setenv("KGC_PREFILL_STREAMS_MIN_TOKENS", "16")
-    outs, calls = {}, {}
-    for on in ("0", "1"):
-        monkeypatch.setenv("KGC_PREFILL_STREAMS", on)          # off by default
-        eng = _tiny_engine(enforce_eager=False, max_num_batched_tokens=1024)
-        m = eng.executor.runner.model
-        n = []
-        real = m._forward_two_streams
-        monkeypatch.setattr(m, "_forward_two_streams",
-                            lambda *a, **k: (n.append(1), real(*a, **k))[1])
-        outs[on] = _run_lp(eng, prompts, params)
-        calls[on] = len(n)
-        del eng
-        torch.cuda.empty_cache()
-    assert calls["1"] > 0 and calls["0"] == 0, calls
-    for got, ref in zip(outs["1"], outs["0"]):
-        assert len(got[0]) == 10
-        _assert_greedy_agrees(got, ref, 10)
-
-
 def test_engine_preemption_recompute(gpu):
     """A KV pool too small for the batch forces recompute preemption; every request
     still completes with the requested length."""
@@ -381,6 +351,7 @@ def test_tp_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch, tp, eager, name, 
         monkeypatch.setenv("KGC_TP_OVERLAP_MIN_TOKENS", "16")
     if perturb:
         monkeypatch.setenv("KGC_FAULT_PERTURB_TP_RANK", "1")
+        monkeypatch.setenv("KGC_TESTING", "1")
     llm = LLM(d, device="cuda", dtype="bfloat16", tensor_parallel_size=tp, enforce_eager=eager,
               max_model_len=256, max_num_seqs=4, max_num_batched_tokens=128,
               num_gpu_blocks_override=64)
@@ -393,6 +364,12 @@ def test_tp_on_one_gpu_matches_tp1(gpu, tmp_path, monkeypatch, tp, eager, name, 
             # the times are MAX-reduced) and it is what the captured graphs launched
             cal = car.calibration
             assert car.table and cal["rows"][0] == 1 and cal["rows"][-1] >= 4, cal
+            # chosen on hipGraph REPLAY times (the decode graphs' launch pattern), with the
+            # eager times and their delta logged beside them; no uncapturable gloo 'rccl'
+            assert cal["timing"] == "graph", cal
+            assert len(cal["graph_minus_eager_us"]["one"]) == len(cal["rows"]), cal
+            assert all(v is None for v in cal["us"]["rccl"]), cal
+            assert all(p != "rccl" for _, p, _ in car.table), car.table
             table_forms = {f for _, p, fu in car.table for f in (p, fu)}
         else:
             assert car is None, "KGC_CUSTOM_AR=0 must leave every sum to the process group"
@@ -698,6 +675,50 @@ def test_two_node_engine_on_one_gpu(gpu, tmp_path, tp, pp):
     assert same >= 0.8 * sum(len(x) for x in ref), (ref, got)
 
 
+def test_phantom_ep8_rank_of_mixtral_captures_and_replays(gpu, monkeypatch):
+    """KGC_TP_PHANTOM=8 with --moe-parallel ep: one process runs rank 0 of Mixtral 8x7B at
+    EP = TP = 8 (2 of its layers) -- BASELINE config 4's per-rank decode step on one GPU.
+    Rank 0 owns ONE whole expert; attention is the TP = 8 shard (nq 4, nkv 1).  The decode
+    steps replay from hipGraphs with the device-side expert all-to-all (dispatch / receive /
+    grouped MLP / return / combine, parallel/expert_a2a.py PhantomExpertAllToAll: peer
+    buffers local, their flags pre-raised) and the xGMI all-reduce INSIDE the graphs; no
+    barrier times out and the sticky error words stay clear."""
+    from kubernetes_gpu_cluster_amd.models.moe import MoEBlock
+    from kubernetes_gpu_cluster_amd.parallel import comm
+    from kubernetes_gpu_cluster_amd.parallel.expert_a2a import PhantomExpertAllToAll
+    from kubernetes_gpu_cluster_amd.parallel.state import get_state
+    PRESETS.setdefault("mixtral-8x7b-2l", PRESETS["mixtral-8x7b"].shrink(name="mixtral-8x7b-2l",
+                                                                         num_layers=2))
+    monkeypatch.setenv("KGC_TP_PHANTOM", "8")
+    eng = LLMEngine(EngineConfig(model="mixtral-8x7b-2l", random_init=True, max_model_len=1024,
+                                 max_num_seqs=16, max_num_batched_tokens=2048,
+                                 num_gpu_blocks_override=256, cuda_graph_max_bs=16,
+                                 moe_parallel="ep", allow_phantom=True))
+    try:
+        s = get_state()
+        assert s.phantom and s.tp_size == 8 and s.tp_rank == 0
+        m = eng.executor.runner.model
+        blk = m.layers[0].mlp
+        assert isinstance(blk, MoEBlock) and blk.mode == "ep" and blk.E_local == 1
+        assert isinstance(blk.ep_a2a, PhantomExpertAllToAll) and blk.ep_a2a.world == 8
+        assert m.local_kv_heads() == 1
+        g = torch.Generator().manual_seed(6)
+        prompts = [torch.randint(100, 31000, (n,), generator=g).tolist() for n in (7, 64, 200)]
+        params = [SamplingParams(temperature=1.0, seed=i, max_tokens=12, ignore_eos=True)
+                  for i in range(len(prompts))]
+        outs = _run(eng, prompts, params)
+        assert all(len(o) == 12 for o in outs)
+        st = eng.executor.runner.stats
+        assert st["graph_steps"] > 0, st
+        blk.ep_a2a.check()
+        comm.get_custom_allreduce().check()
+    finally:
+        eng.shutdown()
+        from kubernetes_gpu_cluster_amd.engine.worker import _release_custom_allreduce
+        _release_custom_allreduce()
+        set_state(ParallelState())
+
+
 def test_phantom_tp8_rank_of_70b_captures_and_replays(gpu, monkeypatch):
     """KGC_TP_PHANTOM=8: one process runs rank 0 of Llama-3-70B at TP = 8 (2 of its layers)
     -- BASELINE config 3's per-rank decode step on one GPU.  The decode steps replay from
@@ -713,7 +734,8 @@ def test_phantom_tp8_rank_of_70b_captures_and_replays(gpu, monkeypatch):
     monkeypatch.setenv("KGC_TP_PHANTOM", "8")
     eng = LLMEngine(EngineConfig(model="llama-3-70b-2l", random_init=True, max_model_len=1024,
                                  max_num_seqs=16, max_num_batched_tokens=2048,
-                                 num_gpu_blocks_override=256, cuda_graph_max_bs=16))
+                                 num_gpu_blocks_override=256, cuda_graph_max_bs=16,
+                                 allow_phantom=True))
     try:
         s = get_state()
         assert s.phantom and s.tp_size == 8 and s.tp_rank == 0
@@ -731,6 +753,12 @@ def test_phantom_tp8_rank_of_70b_captures_and_replays(gpu, monkeypatch):
         assert m.local_kv_heads() == 1
         car = comm.get_custom_allreduce()
         assert isinstance(car, PhantomAllReduce) and car.world == 8
+        # the phantom's policy is graph-timed too, and the eager-vs-graph delta is logged
+        cal = car.calibration
+        assert cal is not None and cal["timing"] == "graph" and car.table, cal
+        deltas = [v for f in ("one", "two", "fused1") for v in cal["graph_minus_eager_us"][f]
+                  if v is not None]
+        assert deltas and len(cal["eager_choice_differs"]) == len(cal["rows"]), cal
         g = torch.Generator().manual_seed(4)
         prompts = [torch.randint(100, 128000, (n,), generator=g).tolist() for n in (5, 90, 300)]
         params = [SamplingParams(temperature=1.0, seed=i, max_tokens=12, ignore_eos=True)

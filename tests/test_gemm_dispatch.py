@@ -98,38 +98,3 @@ def test_rs_plan_rejects_producers_with_too_many_row_partials():
         for d, v in zip((gemm._best_sk, gemm._best_rs, gemm._best_silu), saved):
             d.clear()
             d.update(v)
-
-
-def test_nf_plan_needs_every_projection_and_a_measured_gain():
-    """The norm-free mid-M layer (K9m fan-in o / down, row-scaled qkv / gate_up) runs only
-    where every projection has its K9m plan and tuning measured the two fan-in launches
-    faster than the regular tails they replace; gate_up's fused SiLU epilogue (S = 1) needs
-    a tile config with the row-scale epilogue (not the split-loader ones, 8 / 9)."""
-    M = 256
-    shapes = [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]
-    saved = dict(gemm._plan_dg), dict(gemm._plan_fanin)
-    try:
-        gemm._plan_dg.clear()
-        gemm._plan_fanin.clear()
-        assert gemm.nf_plan(M, shapes) is None
-        gemm._plan_dg[(M, 6144, 4096, "qkv")] = (6, 5)
-        gemm._plan_dg[(M, 28672, 4096, "silu")] = (6, 1)
-        gemm._plan_fanin[(M, 4096, 4096)] = (5, 4, 15.0, 26.0)
-        assert gemm.nf_plan(M, shapes) is None            # down has no fan-in plan
-        gemm._plan_fanin[(M, 4096, 14336)] = (6, 4, 36.0, 41.0)
-        assert gemm.nf_plan(M, shapes) == [(6, 5), (5, 4), (6, 1), (6, 4)]
-        # measured slower in sum: the tails stay
-        gemm._plan_fanin[(M, 4096, 14336)] = (6, 4, 60.0, 41.0)
-        assert gemm.nf_plan(M, shapes) is None
-        gemm._plan_fanin[(M, 4096, 14336)] = (6, 4, 36.0, 41.0)
-        # a split-loader SiLU epilogue has no row scale
-        gemm._plan_dg[(M, 28672, 4096, "silu")] = (8, 1)
-        assert gemm.nf_plan(M, shapes) is None
-        gemm._plan_dg[(M, 28672, 4096, "silu")] = (8, 2)   # splitk_reduce_silu scales
-        assert gemm.nf_plan(M, shapes) is not None
-        # small M belongs to the skinny kernels
-        assert gemm.nf_plan(16, shapes) is None
-    finally:
-        for d, v in zip((gemm._plan_dg, gemm._plan_fanin), saved):
-            d.clear()
-            d.update(v)

@@ -68,7 +68,11 @@ def test_debug_build_reports_bad_indices(gpu):
     so = os.path.join(ROOT, "kubernetes_gpu_cluster_amd", "_kgc_ops_debug.so")
     if not os.path.exists(so):
         pytest.fail("debug build missing: run KGC_HIP_DEBUG=1 python csrc/build.py")
-    env = dict(os.environ, KGC_HIP_DEBUG="1", PYTHONPATH=ROOT)
+    # ROOT appended to (never replacing) the inherited PYTHONPATH: whatever the parent's
+    # environment puts on the path (e.g. a harness's library-load observer) reaches the child
+    pp = os.environ.get("PYTHONPATH", "")
+    env = dict(os.environ, KGC_HIP_DEBUG="1",
+               PYTHONPATH=os.pathsep.join([p for p in pp.split(os.pathsep) if p] + [ROOT]))
     r = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True,
                        timeout=300, cwd=ROOT)
     assert r.returncode == 0 and "DEBUG-BUILD-OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]

@@ -230,6 +230,36 @@ def test_paged_decode_rope(gpu, monkeypatch, kern, dt, d, nq, nkv, qk_norm, S, f
         torch.testing.assert_close(out.cpu().float(), exp.float(), **tol)
 
 
+def test_paged_decode_single_slice_rows_many_pairs(gpu, monkeypatch):
+    """at >= DECODE_LONG_PAIRS (seq, kv-head) pairs K1w keeps contexts of up to
+    10 chunks in ONE slice, written directly (nused == 1), while longer contexts in the same
+    launch write partials for the merge -- both kernels must derive the same plan from the
+    one min_per value.  B = 256, nq 8 / nkv 1 (the 70B TP = 8 rank's heads), contexts of 0
+    (graph idle rows), 1 .. 320 (one slice) and 321 .. 1500 (several), at the engine's grid
+    and at a forced deep grid; the idle rows must come out zero."""
+    for v in ("KGC_DECODE_WAVE_MIN_PAIRS", "KGC_DECODE_MIN_CHUNKS"):
+        monkeypatch.delenv(v, raising=False)
+    torch.manual_seed(21)
+    B, nq, nkv, d, bs = 256, 8, 1, 128, 32
+    g = torch.Generator().manual_seed(5)
+    ctx = torch.randint(1, 1500, (B,), generator=g)
+    ctx[::7] = torch.randint(1, 320, (len(ctx[::7]),), generator=g)
+    ctx[3::11] = 0
+    ctx[5] = 320
+    ctx[6] = 321
+    kc, vc, bt = _fill_random_cache(B, [max(int(c), 1) for c in ctx], nkv, bs, d,
+                                    torch.bfloat16, gpu)
+    q = torch.randn(B, nq, d, dtype=torch.bfloat16, device=gpu)
+    cl = ctx.to(torch.int32).to(gpu)
+    exp = ref.paged_attention_decode(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), cl.cpu(), d ** -0.5)
+    assert ops.decode_uses_wave(B, nkv)
+    for z in (ops.decode_grid_z(B, nkv, 4096), 16):
+        out = torch.full_like(q, float("nan"))
+        out = ops.paged_attention_decode(q, kc, vc, bt, cl, d ** -0.5, grid_z=z, out=out)
+        torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(torch.bfloat16))
+        assert torch.all(out[ctx.to(gpu) == 0] == 0)
+
+
 @pytest.mark.parametrize("kern", list(_DECODE_KERNELS))
 def test_paged_decode_workspace_reuse(gpu, monkeypatch, kern):
     """One static partials workspace serves launches of any Z (incl. an empty context),
@@ -600,6 +630,53 @@ def test_fused_moe_splitk(gpu, monkeypatch, S, T, all_local):
     torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(torch.bfloat16))
 
 
+@pytest.mark.parametrize("T", [1, 5, 64, 256, 300])
+@pytest.mark.parametrize("bm", [64, 128])
+@pytest.mark.parametrize("S", [1, 2, 4])
+def test_fused_moe_packed_k14m(gpu, monkeypatch, T, bm, S):
+    """K14m (moe_dgemm: the grouped gate_up with its SiLU epilogue and the grouped down
+    with its row scatter, on the K9m LDS-DMA pipeline over per-expert packed tiles) vs the
+    fp32 reference: row blocks of 64 / 128 (padding rows gathered but never stored), the
+    down projection's fp32 K-slices summed in moe_combine, and an expert-parallel shard
+    (experts 2..7 here; pairs of the others add 0)."""
+    monkeypatch.setenv("KGC_MOE_BM", str(bm))
+    monkeypatch.setenv("KGC_MOE_SPLITK", str(S))
+    x, w13, w2, tw, tid = _moe_case(torch.bfloat16, T, 8, 2, 512, 1024, gpu, seed=11 + T)
+    w13p, w2p = ops.moe_pack(w13, True), ops.moe_pack(w2, False)
+    out = ops.fused_moe(x, w13, w2, tw, tid, w13p=w13p, w2p=w2p)
+    exp = ref.moe_mlp_local(x.cpu(), w13.cpu(), w2.cpu(), tw.cpu(), tid.cpu())
+    torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(torch.bfloat16))
+    # the same kernels' result equals the register-staged grouped GEMM's within rounding
+    base = ops.fused_moe(x, w13, w2, tw, tid)
+    torch.testing.assert_close(out.float(), base.float(), **_tol(torch.bfloat16))
+    lo = 2
+    w13s, w2s = w13[lo:].contiguous(), w2[lo:].contiguous()
+    out = ops.fused_moe(x, w13s, w2s, tw, tid, expert_offset=lo, all_local=False,
+                        w13p=ops.moe_pack(w13s, True), w2p=ops.moe_pack(w2s, False))
+    exp = ref.moe_mlp_local(x.cpu(), w13s.cpu(), w2s.cpu(), tw.cpu(), tid.cpu(), lo)
+    torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(torch.bfloat16))
+
+
+def test_fused_moe_packed_graph_capture(gpu):
+    """K14m captures into a hipGraph (row counts stay on the device) and replays with new
+    routes: the decode graphs' form of the Mixtral block."""
+    x, w13, w2, tw, tid = _moe_case(torch.bfloat16, 64, 8, 2, 256, 256, gpu, seed=4)
+    w13p, w2p = ops.moe_pack(w13, True), ops.moe_pack(w2, False)
+    ops.fused_moe(x, w13, w2, tw, tid, w13p=w13p, w2p=w2p)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = ops.fused_moe(x, w13, w2, tw, tid, w13p=w13p, w2p=w2p)
+    for seed in (7, 8):
+        x2, _, _, tw2, tid2 = _moe_case(torch.bfloat16, 64, 8, 2, 256, 256, gpu, seed=seed)
+        x.copy_(x2)
+        tw.copy_(tw2)
+        tid.copy_(tid2)
+        g.replay()
+        exp = ref.moe_mlp_local(x.cpu(), w13.cpu(), w2.cpu(), tw.cpu(), tid.cpu())
+        torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(torch.bfloat16))
+
+
 def test_fused_moe_graph_capture(gpu):
     """No host sync inside: the block captures into a hipGraph and replays with new routes."""
     x, w13, w2, tw, tid = _moe_case(torch.bfloat16, 64, 8, 2, 256, 256, gpu, seed=4)
@@ -858,19 +935,25 @@ def test_tune_skinny_times_norm_free_epilogues(gpu):
     assert not gemm._best_rs
 
 
-@pytest.mark.parametrize("cfg", list(range(11)))
+@pytest.mark.parametrize("cfg", list(range(15)))
 @pytest.mark.parametrize("M,N,K", [(256, 1024, 4096), (200, 768, 1024), (77, 512, 2048),
-                                   (130, 256, 128)])
+                                   (130, 256, 128), (256, 1280, 1024), (200, 1792, 512),
+                                   (96, 896, 256)])
 def test_dgemm_matches_fp32(gpu, cfg, M, N, K):
     """K9m decode GEMM (every tile config, packed and row-major weights) vs an fp32
     matmul: bf16 output (S = 1), fp32 split-K slices (S = 2, 3, 4, 5: uneven K ranges at 3
-    and 5) and the fused SiLU epilogue, with M not a multiple of the row block (clamped
-    loads, masked stores)."""
+    and 5; 16 where K allows: the TP = 8 qkv split) and the fused SiLU epilogue where the
+    tile has it, with M not a multiple of the row block (clamped loads, masked stores).
+    The round-6 narrow tiles (11-14: BN 64 / 80 / 112, one or two waves along N, 128-row
+    blocks XCD-paired) read pieces of the 128-row packed blocks; N = 1280 / 1792 / 896 put
+    their column tiles across those blocks' boundaries."""
     from kubernetes_gpu_cluster_amd.ops import gemm
     k = torch.ops.kgc
+    assert k.dgemm_num_cfgs() == 15
     bm, bn, pk = k.dgemm_cfg_info(cfg)
     if N % bn:
         pytest.skip("N not a multiple of BN")
+    epis = k.dgemm_cfg_epis(cfg)
     torch.manual_seed(M + N + cfg)
     x = torch.randn(M, K, dtype=torch.bfloat16, device=gpu)
     w = torch.randn(N, K, dtype=torch.bfloat16, device=gpu) * 0.02
@@ -885,15 +968,27 @@ def test_dgemm_matches_fp32(gpu, cfg, M, N, K):
     out = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
     k.dgemm(out, x, weight(False), cfg, 1)
     torch.testing.assert_close(out.float().cpu(), ref, atol=3e-2, rtol=2e-2)
-    for S in (s for s in (2, 3, 4, 5) if s <= K // 64):
+    for S in (s for s in (2, 3, 4, 5, 16) if s <= K // 64):
         ws = torch.full((S, M, N), float("nan"), dtype=torch.float32, device=gpu)
         k.dgemm(ws, x, weight(False), cfg, 0)
         # every slice row was written (no NaN left) and the slices sum to the product
         torch.testing.assert_close(ws.sum(0).cpu(), ref, atol=2e-3, rtol=2e-3)
     act = torch.empty(M, N // 2, dtype=torch.bfloat16, device=gpu)
+    if not (epis >> 2) & 1:
+        with pytest.raises(RuntimeError, match="no such epilogue"):
+            k.dgemm(act, x, weight(True), cfg, 2)
+        return
     k.dgemm(act, x, weight(True), cfg, 2)
     exp = torch.nn.functional.silu(ref[:, : N // 2]) * ref[:, N // 2:]
     torch.testing.assert_close(act.float().cpu(), exp, atol=3e-2, rtol=2e-2)
+    # the SiLU-packed weight's fp32 slices, reduced by splitk_reduce_silu (interleaved
+    # gate / up 16-column groups in packed tiles): the split-K path of gate_up
+    if K // 64 >= 4:
+        ws = torch.empty(4, M, N, dtype=torch.float32, device=gpu)
+        k.dgemm(ws, x, weight(True), cfg, 0)
+        red = torch.empty(M, N // 2, dtype=torch.bfloat16, device=gpu)
+        k.splitk_reduce_silu(red, ws, bool(pk))
+        torch.testing.assert_close(red.float().cpu(), exp, atol=3e-2, rtol=2e-2)
 
 
 def test_dgemm_pack_layout(gpu):
@@ -1029,63 +1124,13 @@ def test_tail_fused_model_matches_regular_path(gpu):
     torch.testing.assert_close(got.float(), ref_out.float(), atol=6e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("M,N,K,cfg,S", [(256, 4096, 4096, 6, 4), (256, 4096, 14336, 6, 8),
-                                         (256, 4096, 4096, 5, 4), (200, 4096, 4096, 10, 2),
-                                         (96, 1024, 2048, 5, 3), (130, 2048, 1024, 4, 1),
-                                         (256, 1024, 2048, 1, 5), (72, 1024, 1024, 3, 6),
-                                         (256, 4096, 4096, 7, 2), (256, 2048, 2048, 0, 2)])
-def test_dgemm_fanin_matches_fp32(gpu, M, N, K, cfg, S):
-    """K9m EPI_FANIN (the norm-free layer's o / down): split-K combine by the last slice of
-    each tile, residual add and row norms in one launch, vs fp32: residual += x W^T and
-    rs = rsqrt(mean(residual^2) + eps) of the residual as stored.  Repeated calls and graph
-    replays re-arm the tickets (counters back at zero), and the combine is deterministic
-    (slices summed in slice order whichever arrives last: bit-identical reruns)."""
-    from kubernetes_gpu_cluster_amd.ops import gemm
-    torch.manual_seed(M + N + S)
-    x = torch.randn(M, K, dtype=torch.bfloat16, device=gpu)
-    w = torch.randn(N, K, dtype=torch.bfloat16, device=gpu) * K ** -0.5
-    res0 = torch.randn(M, N, dtype=torch.bfloat16, device=gpu)
-    eps = 1e-5
-    if gemm.cfg_packed(cfg):
-        gemm.pack_decode_weights([w], [])
-    try:
-        r32 = res0.float().cpu() + x.float().cpu() @ w.float().cpu().t()
-        outs = []
-        for _ in range(3):
-            res = res0.clone()
-            rs = gemm.dgemm_fanin(x, w, cfg, S, res, eps)
-            torch.cuda.synchronize()
-            torch.testing.assert_close(res.float().cpu(), r32, atol=5e-2, rtol=2e-2)
-            rb = res.float().cpu()
-            exact = torch.rsqrt(rb.pow(2).mean(-1) + eps)
-            torch.testing.assert_close(rs.cpu(), exact, atol=0, rtol=1e-4)
-            outs.append(res.clone())
-        assert all(torch.equal(o, outs[0]) for o in outs[1:])
-        st = gemm._nf_state(x.device)
-        assert int(st.cnt.abs().sum()) == 0
-        res = res0.clone()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            rs_g = gemm.dgemm_fanin(x, w, cfg, S, res, eps)
-        for _ in range(2):
-            res.copy_(res0)
-            st.rs.fill_(float("nan"))
-            g.replay()
-            torch.cuda.synchronize()
-            assert torch.equal(res, outs[0])
-            torch.testing.assert_close(rs_g.cpu(), exact, atol=0, rtol=1e-4)
-        assert int(st.cnt.abs().sum()) == 0
-    finally:
-        gemm._packed.clear()
-
-
 @pytest.mark.parametrize("M,N,K,cfg,S", [(256, 4096, 2048, 6, 1), (96, 2048, 1024, 5, 1),
                                          (256, 2048, 1024, 4, 3), (100, 1024, 1024, 2, 2),
                                          (256, 1024, 1024, 0, 1)])
 def test_dgemm_row_scale_silu_matches_fp32(gpu, M, N, K, cfg, S):
-    """The norm-free gate_up: silu(r * g) * (r * u) over a merged weight, r per row -- in
-    the K9m SiLU epilogue (S = 1) or in splitk_reduce_silu (S > 1) -- vs fp32; and the
-    EPI_OUT row scale."""
+    """The K9m row-scale epilogue: silu(r * g) * (r * u) over a merged gate_up weight, r per
+    row -- in the SiLU epilogue (S = 1) or in splitk_reduce_silu (S > 1) -- vs fp32; and
+    the EPI_OUT row scale."""
     from kubernetes_gpu_cluster_amd.ops import gemm
     torch.manual_seed(M + K)
     x = torch.randn(M, K, dtype=torch.bfloat16, device=gpu)
@@ -1094,11 +1139,21 @@ def test_dgemm_row_scale_silu_matches_fp32(gpu, M, N, K, cfg, S):
     y = (x.float().cpu() @ w.float().cpu().t()) * r.cpu()[:, None]
     ref = torch.nn.functional.silu(y[:, : N // 2]) * y[:, N // 2:]
     pk = gemm.cfg_packed(cfg)
-    wk = gemm.pack_folded(w, torch.ones(K, dtype=w.dtype, device=gpu), True) if pk else w
-    got = gemm.nf_silu(x, w, wk, cfg, S, r)
+
+    def packed(silu):
+        if not pk:
+            return w
+        p = torch.empty(N // 128, K // 64, 8192, dtype=w.dtype, device=gpu)
+        torch.ops.kgc.dgemm_pack(p, w, silu)
+        return p
+    wk = packed(True)
+    if S == 1:
+        got = gemm.dgemm(x, w, cfg, 1, epi=2, rscale=r, wk=wk)
+    else:
+        got = torch.empty(M, N // 2, dtype=x.dtype, device=gpu)
+        torch.ops.kgc.splitk_reduce_silu(got, gemm.dgemm(x, w, cfg, S, wk=wk), pk, r)
     torch.testing.assert_close(got.float().cpu(), ref, atol=3e-2, rtol=2e-2)
-    wo = gemm.pack_folded(w, torch.ones(K, dtype=w.dtype, device=gpu), False) if pk else w
-    out = gemm.dgemm(x, w, cfg, 1, epi=1, rscale=r, wk=wo)
+    out = gemm.dgemm(x, w, cfg, 1, epi=1, rscale=r, wk=packed(False))
     torch.testing.assert_close(out.float().cpu(), y, atol=3e-2, rtol=2e-2)
 
 
@@ -1138,70 +1193,6 @@ def test_paged_decode_rope_row_scale(gpu, monkeypatch, S):
     torch.testing.assert_close(o1.float(), o2.float(), atol=2e-2, rtol=2e-2)
     torch.testing.assert_close(k1.float(), k2.float(), atol=2e-2, rtol=2e-2)
     torch.testing.assert_close(v1.float(), v2.float(), atol=2e-2, rtol=2e-2)
-
-
-def test_nf_model_matches_regular_path(gpu):
-    """Whole-model forward through the norm-free mid-M layer (forced plans: K9m qkv split-K
-    on a gamma-folded copy, the o / down fan-in epilogues, the row-scaled SiLU epilogue) vs
-    the regular layer loop on the same weights, with non-unit norm weights so the folding
-    is exercised."""
-    from kubernetes_gpu_cluster_amd.models import configs
-    from kubernetes_gpu_cluster_amd.models.llama import LlamaAttention, LlamaForCausalLM
-    from kubernetes_gpu_cluster_amd.ops import gemm
-    from kubernetes_gpu_cluster_amd.models import llama as llama_mod
-    cfg = configs.PRESETS["llama-3-8b"].shrink(name="nf-layer", num_layers=3)
-    torch.manual_seed(2)
-    model = LlamaForCausalLM(cfg, torch.bfloat16, gpu)
-    for n, p in model.named_parameters():
-        if p.dim() == 2:
-            p.data.normal_(0, 0.02)
-        else:
-            p.data.uniform_(0.6, 1.4)
-    M = 96
-    ids = torch.randint(0, cfg.vocab_size, (M,), device=gpu)
-
-    class _Ctx:
-        pass
-    for l in model.layers:
-        def stub(positions, qkv, ctx, row_scale=None, nq=l.self_attn.nq * cfg.head_dim):
-            if row_scale is not None:
-                qkv = LlamaAttention._scaled_rows(qkv, row_scale, torch.bfloat16)
-            elif qkv.dim() == 3:
-                qkv = qkv.sum(0).to(torch.bfloat16)
-            return qkv[:, :nq].contiguous()
-        l.self_attn.attend = stub
-    l0 = model.layers[0]
-    plain = [w for l in model.layers for w in (l.self_attn.qkv_proj.weight,
-                                                l.self_attn.o_proj.weight, l.mlp.down_proj.weight)]
-    gemm.pack_decode_weights(plain, [l.mlp.gate_up_proj.weight for l in model.layers])
-    try:
-        llama_mod._tail_fusion_enabled = False
-        ref_out = model(ids, None, _Ctx())
-        llama_mod._tail_fusion_enabled = True
-        llama_mod._nf_enabled = True          # opt-in path (KGC_NF_LAYER=1)
-        assert model.fold_nf_weights() > 0
-        sh = model._rs_shapes()
-        gemm._plan_dg[(M, *sh[0], "qkv")] = (5, 2)
-        gemm._plan_dg[(M, *sh[2], "silu")] = (5, 1)
-        gemm._plan_dg[(M, *sh[1], "tail")] = (5, 4)
-        gemm._plan_dg[(M, *sh[3], "tail")] = (5, 4)
-        gemm._plan_fanin[(M, *sh[1])] = (5, 4, 1.0, 2.0)
-        gemm._plan_fanin[(M, *sh[3])] = (7, 8, 1.0, 2.0)
-        x = model.embed_tokens(ids)
-        assert model._tail_fusable(x) and model._nf_cfgs(M) is not None
-        got = model(ids, None, _Ctx())
-        # the regular tail-fused path on the same plans, for scale
-        gemm._plan_fanin.clear()
-        assert model._nf_cfgs(M) is None
-        tail = model(ids, None, _Ctx())
-    finally:
-        gemm.clear_plan()
-        gemm._packed.clear()
-        llama_mod._tail_fusion_enabled = True
-        llama_mod._nf_enabled = os.environ.get("KGC_NF_LAYER", "0") == "1"
-        model._nf_w = None
-    torch.testing.assert_close(tail.float(), ref_out.float(), atol=6e-2, rtol=3e-2)
-    torch.testing.assert_close(got.float(), ref_out.float(), atol=6e-2, rtol=3e-2)
 
 
 @pytest.mark.parametrize("M,N,K,cfg", [(1, 4096, 4096, (1, 1, 4, True)),
@@ -1319,3 +1310,36 @@ def test_sampler_health_async_steps_keep_their_flags(gpu):
     sh.raise_if_failed(slot_n1)                   # N + 1 is fine ...
     with pytest.raises(ops.SamplerFailed):        # ... and N is still reported
         sh.raise_if_failed(slot_n)
+
+
+def test_dg_table_fingerprint_guards_stale_tables(gpu, tmp_path, monkeypatch):
+    """an offline K9m table is trusted only when its fingerprint (GPU arch and
+    name, the library's tile-config list) matches the running build; a mismatching or
+    unfingerprinted table is dropped whole (start-up tuning runs), and an entry whose tile
+    does not divide its N or whose split exceeds K / 64 is dropped alone."""
+    import json
+    from kubernetes_gpu_cluster_amd.ops import gemm
+    fp = gemm.dg_fingerprint()
+    assert fp["num_cfgs"] == torch.ops.kgc.dgemm_num_cfgs() and len(fp["cfgs"]) == fp["num_cfgs"]
+    ent = [{"M": 256, "N": 4096, "K": 4096, "kind": "tail", "cfg": 6, "S": 4},
+           {"M": 256, "N": 1280, "K": 8192, "kind": "plain", "cfg": 6, "S": 4},   # 1280 % 128 ok
+           {"M": 256, "N": 1280, "K": 8192, "kind": "qkv", "cfg": 12, "S": 16},   # BN 80
+           {"M": 256, "N": 1280, "K": 1024, "kind": "tail", "cfg": 12, "S": 32},  # S > K/64
+           {"M": 256, "N": 1000, "K": 4096, "kind": "plain", "cfg": 4, "S": 1}]   # N % BN
+    path = tmp_path / "t.json"
+    monkeypatch.setenv("KGC_DGEMM_TABLE", str(path))
+    try:
+        path.write_text(json.dumps({"fingerprint": fp, "entries": ent}))
+        assert gemm.load_dg_table("x") == 3
+        bad = dict(fp, cfgs=fp["cfgs"][:-1], num_cfgs=fp["num_cfgs"] - 1)
+        path.write_text(json.dumps({"fingerprint": bad, "entries": ent}))
+        assert gemm.load_dg_table("x") == 0
+        path.write_text(json.dumps({"fingerprint": dict(fp, arch="gfx942"), "entries": ent}))
+        assert gemm.load_dg_table("x") == 0
+        path.write_text(json.dumps({"entries": ent}))
+        assert gemm.load_dg_table("x") == 0
+        # the committed table matches this library
+        monkeypatch.delenv("KGC_DGEMM_TABLE")
+        assert gemm.load_dg_table("llama-3-8b") > 0
+    finally:
+        gemm.clear_plan()

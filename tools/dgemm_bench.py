@@ -23,12 +23,14 @@ import torch.nn.functional as F
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def shapes(model):
+def shapes(model, tp=1):
+    """(N, K) of each projection of one TP rank's shard (tp = 1: the whole model)."""
     from kubernetes_gpu_cluster_amd.models.configs import PRESETS
     c = PRESETS[model]
     H, I, d = c.hidden_size, c.intermediate_size, c.head_dim
-    return {"qkv": ((c.num_heads + 2 * c.num_kv_heads) * d, H), "o": (H, c.num_heads * d),
-            "gate_up": (2 * I, H), "down": (H, I), "lm_head": (c.vocab_size, H)}
+    nq, nkv = c.num_heads // tp, max(1, c.num_kv_heads // tp)
+    return {"qkv": ((nq + 2 * nkv) * d, H), "o": (H, nq * d),
+            "gate_up": (2 * I // tp, H), "down": (H, I // tp), "lm_head": (c.vocab_size // tp, H)}
 
 
 def bench(fn, iters):
@@ -52,6 +54,7 @@ def bench(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="llama-3-8b")
+    ap.add_argument("--tp", type=int, default=1, help="time one TP rank's shard shapes")
     ap.add_argument("--ms", default="256")
     ap.add_argument("--copies", type=int, default=16)
     ap.add_argument("--shapes", default="qkv,o,gate_up,down,lm_head")
@@ -61,6 +64,8 @@ def main():
                     help="cfg:S:epi -- time just this configuration (profiling runs)")
     ap.add_argument("--no-lib", action="store_true", help="skip the hipBLASLt baseline")
     ap.add_argument("--cfgs", default=None, help="comma list: only these tile configs")
+    ap.add_argument("--max-grid", type=int, default=264,
+                    help="skip split-K candidates with more workgroups than this")
     ap.add_argument("--ablate", default=None,
                     help="S value: time the packed 256 x 128 tile with modes full / no-MFMA / "
                          "no-DMA / no-A-DMA / no-B-DMA at this split")
@@ -75,7 +80,7 @@ def main():
         torch.cuda.tunable.read_file(a.table)
     dev = torch.device("cuda")
     torch.manual_seed(0)
-    for name, (N, K) in shapes(a.model).items():
+    for name, (N, K) in shapes(a.model, a.tp).items():
         if name not in a.shapes.split(","):
             continue
         copies = a.copies if N * K * 2 * a.copies < 8e9 else max(2, int(4e9 // (N * K * 2)))
@@ -122,11 +127,12 @@ def main():
                 bm, bn, pk = k.dgemm_cfg_info(cid)
                 if (bm == 256 and M <= 128) or N % bn or (want_cfgs is not None and cid not in want_cfgs):
                     continue
+                tiles = ((M + bm - 1) // bm) * (N // bn)
                 for S in [int(s) for s in a.splits.split(",")]:
-                    if K // 64 < S:
+                    if K // 64 < S or (S > 1 and tiles * S > a.max_grid):
                         continue
                     cfgs.append((cid, S, 0 if S > 1 else 1))
-                if name == "gate_up":
+                if name == "gate_up" and (k.dgemm_cfg_epis(cid) >> 2) & 1:
                     cfgs.append((cid, 1, 2))
             if a.only:
                 cfgs = [tuple(int(v) for v in a.only.split(":"))]
