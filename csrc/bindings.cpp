@@ -438,7 +438,7 @@ void moe_align(Tensor sorted_ids, Tensor block_expert, Tensor meta, Tensor topk_
                int64_t E_local, int64_t bm) {
   check_gpu(topk_ids, "topk_ids");
   c10::hip::HIPGuardMasqueradingAsCUDA g(topk_ids.device());
-  TORCH_CHECK(bm == 64 || bm == 128, "row block 64 or 128");
+  TORCH_CHECK(bm == 64 || bm == 96 || bm == 128, "row block 64, 96 or 128");
   const int64_t npairs = topk_ids.numel();
   const int64_t rows = sorted_ids.numel();
   TORCH_CHECK(topk_ids.scalar_type() == at::kInt && topk_ids.is_contiguous(), "topk_ids int32");
@@ -500,11 +500,13 @@ void moe_gemm(Tensor C, Tensor A, Tensor W, Tensor sorted_ids, Tensor block_expe
 // mode 1: C = act [rows, N/2] = silu(g) * u of x's gathered rows (sorted-row order);
 // mode 2: C = [npairs, N] (W's dtype) or fp32 slices [S, npairs, N], rows scattered.
 void moe_dgemm(Tensor C, Tensor A, Tensor Wp, Tensor sorted_ids, Tensor block_expert,
-               Tensor meta, int64_t npairs, int64_t topk, int64_t bm, int64_t mode) {
+               Tensor meta, int64_t npairs, int64_t topk, int64_t bm, int64_t mode,
+               int64_t bn) {
   check_gpu(A, "A");
   c10::hip::HIPGuardMasqueradingAsCUDA g(A.device());
-  TORCH_CHECK(bm == 64 || bm == 128, "row block 64 or 128");
+  TORCH_CHECK(bm == 64 || bm == 96 || bm == 128, "row block 64, 96 or 128");
   TORCH_CHECK(mode == 1 || mode == 2, "mode 1 (gate_up + SiLU, gathered) or 2 (down, scattered)");
+  TORCH_CHECK(bn == 128 || bn == 256, "column tile 128 or 256");
   TORCH_CHECK(Wp.dim() == 4 && Wp.is_contiguous() && Wp.size(3) == 128 * kgc::dgemm_block_k(),
               "Wp packed [E, N/128, K/64, 8192] contiguous");
   TORCH_CHECK(Wp.scalar_type() == at::kBFloat16 || Wp.scalar_type() == at::kHalf, "bf16 / fp16");
@@ -513,6 +515,7 @@ void moe_dgemm(Tensor C, Tensor A, Tensor Wp, Tensor sorted_ids, Tensor block_ex
               reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0, "16-B aligned");
   const int64_t N = Wp.size(1) * 128, K = Wp.size(2) * kgc::dgemm_block_k();
   const int64_t rows = sorted_ids.numel();
+  TORCH_CHECK(N % bn == 0, "N % bn == 0");
   TORCH_CHECK(A.dim() == 2 && A.size(1) == K && A.stride(1) == 1 && A.stride(0) % 8 == 0,
               "A [*, K], 16-B aligned rows");
   TORCH_CHECK(sorted_ids.scalar_type() == at::kInt && block_expert.scalar_type() == at::kInt &&
@@ -539,7 +542,7 @@ void moe_dgemm(Tensor C, Tensor A, Tensor Wp, Tensor sorted_ids, Tensor block_ex
   }
   if (rows == 0) return;
   kgc::launch_moe_dgemm(dt_code(Wp), (int)mode, C.data_ptr(), A.data_ptr(), Wp.data_ptr(),
-                        (int)rows, (int)N, (int)K, A.stride(0), (int)S, ss, (int)bm,
+                        (int)rows, (int)N, (int)K, A.stride(0), (int)S, ss, (int)bm, (int)bn,
                         sorted_ids.data_ptr<int>(), block_expert.data_ptr<int>(),
                         meta.data_ptr<int>(), (int)npairs, (int)topk, stream());
 }
@@ -1193,7 +1196,7 @@ TORCH_LIBRARY(kgc, m) {
   m.def("moe_gemm(Tensor(a!) C, Tensor A, Tensor W, Tensor sorted_ids, Tensor block_expert, "
         "Tensor meta, int npairs, int topk, int bm, bool gather, bool scatter, int splitk=1) -> ()");
   m.def("moe_dgemm(Tensor(a!) C, Tensor A, Tensor Wp, Tensor sorted_ids, Tensor block_expert, "
-        "Tensor meta, int npairs, int topk, int bm, int mode) -> ()");
+        "Tensor meta, int npairs, int topk, int bm, int mode, int bn=256) -> ()");
   m.def("moe_combine(Tensor(a!) out, Tensor y, Tensor topk_w) -> ()");
   m.def("dense_gemm_splitk(Tensor(a!) Cs, Tensor A, Tensor W, int bm) -> ()");
   m.def("splitk_reduce(Tensor(a!) out, Tensor Cs) -> ()");

@@ -126,7 +126,7 @@ template <typename T, int BM, int BN, int EPI, bool PK, int ABL = ABL_NONE, int 
 __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
     void* __restrict__ Cv, const T* __restrict__ X, const T* __restrict__ W, int M, int N,
     int K, int64_t ldx, int S, int MB, int64_t slice_stride, int xmap, int wt, DgAux aux) {
-  static_assert(WN == 1 || WN == 2, "waves along N");
+  static_assert(WN == 1 || WN == 2 || WN == 4, "waves along N");
   constexpr int WM = 8 / WN;                      // MFMA waves along M
   constexpr int MT = BM / WM / 16;                // 16-row MFMA tiles per wave
   constexpr int NT = BN / WN / 16;                // 16-col MFMA tiles per wave
@@ -147,7 +147,8 @@ __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
   const bool loader = LDW > 0 && wave >= 8;
   const bool consumer = LDW == 0 || wave < 8;
   const int iw = LDW > 0 ? wave - 8 : wave;       // index among the issuing waves
-  const int wm = WN == 2 ? (wave >> 1) & 3 : wave & 7, wn = WN == 2 ? wave & 1 : 0;
+  // (WN = 4: a 2 x 4 wave grid, the 96-row K14m blocks: 48 rows x 32 columns per wave)
+  const int wm = (wave & 7) / WN, wn = wave % WN;
   int z, j, mb, nb;
   if (xmap) {
     // XCD-paired row blocks (host: S | 8, (N / BN) % (8 / S) == 0): workgroups L and L + 8
@@ -617,16 +618,24 @@ int dg_cfg_epis(int cfg) {
   }
 }
 
-template <typename T, int BM, int MOE>
+template <typename T, int BM, int BN, int MOE>
 void moe_dgemm_t(int epi, void* C, const void* A, const void* Wp, int max_rows, int N, int K,
                  int64_t lda, int S, int64_t ss, const DgAux& aux, hipStream_t s) {
   // 1-D grid, row blocks fastest: a column tile's blocks (one expert each) are dispatched
-  // together, so each XCD's L2 holds the activation rows of the experts it is dealt
+  // together, so each XCD's L2 holds the activation rows of the experts it is dealt.
+  // BM = 96 (a decode step's ~64 +- 3 sd pairs per expert in ONE block, a third fewer
+  // padding rows than 128): 2 x 4 MFMA waves and 4 loader waves (12 A pieces per step).
+  // BN = 256 (2 x 4 waves of 64 columns): a block's gathered rows are re-read by half as
+  // many column tiles -- at ~64 rows per expert the activation stream is 0.375 of the
+  // weight stream instead of 0.75.
+  constexpr int WN = (BN == 256 || BM == 96) ? 4 : 2;
+  constexpr int LDW = (BM == 96 || (BN == 256 && BM == 128)) ? 4 : 0;
   const int MB = max_rows / BM;
-  const dim3 grid((unsigned)(MB * (N / 128) * S));
+  const dim3 grid((unsigned)(MB * (N / BN) * S));
 #define MOE_LAUNCH(EP)                                                                      \
-  dgemm_kernel<T, BM, 128, EP, true, ABL_NONE, 0, 2, MOE><<<grid, DG_THREADS, 0, s>>>(      \
-      C, (const T*)A, (const T*)Wp, max_rows, N, K, lda, S, MB, ss, 0, partial_wt(), aux)
+  dgemm_kernel<T, BM, BN, EP, true, ABL_NONE, LDW, WN, MOE>                                 \
+      <<<grid, DG_THREADS + LDW * 64, 0, s>>>(C, (const T*)A, (const T*)Wp, max_rows, N, K, \
+                                              lda, S, MB, ss, 0, partial_wt(), aux)
   if constexpr (MOE == 1) {
     MOE_LAUNCH(EPI_SILU);
   } else {
@@ -639,7 +648,7 @@ void moe_dgemm_t(int epi, void* C, const void* A, const void* Wp, int max_rows, 
 }  // namespace
 
 void launch_moe_dgemm(int dtype, int mode, void* C, const void* A, const void* Wp, int max_rows,
-                      int N, int K, int64_t lda, int S, int64_t slice_stride, int bm,
+                      int N, int K, int64_t lda, int S, int64_t slice_stride, int bm, int bn,
                       const int* sorted_ids, const int* block_expert, const int* meta,
                       int npairs, int topk, hipStream_t s) {
   DgAux aux{};
@@ -650,16 +659,23 @@ void launch_moe_dgemm(int dtype, int mode, void* C, const void* A, const void* W
   aux.topk = topk;
   aux.wexp = (int64_t)N * K;                     // one expert's packed weight, elements
   const int epi = mode == 1 ? EPI_SILU : S > 1 ? EPI_PARTIAL : EPI_OUT;
+#define MOE_BN(TT, BMM, MODE)                                                               \
+  if (bn == 256) moe_dgemm_t<TT, BMM, 256, MODE>(epi, C, A, Wp, max_rows, N, K, lda, S, slice_stride, aux, s); \
+  else moe_dgemm_t<TT, BMM, 128, MODE>(epi, C, A, Wp, max_rows, N, K, lda, S, slice_stride, aux, s);
+#define MOE_BM(TT, MODE)                                                                    \
+  if (bm == 64) { MOE_BN(TT, 64, MODE) }                                                    \
+  else if (bm == 96) { MOE_BN(TT, 96, MODE) }                                               \
+  else { MOE_BN(TT, 128, MODE) }
 #define MOE_T(TT)                                                                           \
   if (mode == 1) {                                                                          \
-    if (bm == 64) moe_dgemm_t<TT, 64, 1>(epi, C, A, Wp, max_rows, N, K, lda, S, slice_stride, aux, s); \
-    else moe_dgemm_t<TT, 128, 1>(epi, C, A, Wp, max_rows, N, K, lda, S, slice_stride, aux, s); \
+    MOE_BM(TT, 1)                                                                           \
   } else {                                                                                  \
-    if (bm == 64) moe_dgemm_t<TT, 64, 2>(epi, C, A, Wp, max_rows, N, K, lda, S, slice_stride, aux, s); \
-    else moe_dgemm_t<TT, 128, 2>(epi, C, A, Wp, max_rows, N, K, lda, S, slice_stride, aux, s); \
+    MOE_BM(TT, 2)                                                                           \
   }
   if (dtype == DT_BF16) { MOE_T(bf16) } else { MOE_T(f16) }
 #undef MOE_T
+#undef MOE_BM
+#undef MOE_BN
 }
 
 int dgemm_num_cfgs() { return kNumCfgs; }

@@ -144,9 +144,10 @@ struct DgAux {
 // Wp [E][N/128][K/64][128*64]: mode 1 = gate_up (A rows gathered from x by sorted_ids / topk,
 // SiLU epilogue over the SiLU-packed w13, act [rows, N/2] in sorted-row order); mode 2 =
 // down (A = act rows, C rows scattered to pair order; S > 1: fp32 slices [S][npairs][N]).
-// bm = 64 | 128 row blocks (moe_align's), max_rows = rows of sorted_ids.
+// bm = 64 | 96 | 128 row blocks (moe_align's), bn = 128 | 256 column tiles, max_rows = rows
+// of sorted_ids.
 void launch_moe_dgemm(int dtype, int mode, void* C, const void* A, const void* Wp, int max_rows,
-                      int N, int K, int64_t lda, int S, int64_t slice_stride, int bm,
+                      int N, int K, int64_t lda, int S, int64_t slice_stride, int bm, int bn,
                       const int* sorted_ids, const int* block_expert, const int* meta,
                       int npairs, int topk, hipStream_t s);
 int dgemm_num_cfgs();

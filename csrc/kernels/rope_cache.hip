@@ -55,7 +55,7 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
     const float* __restrict__ cos_sin, T* __restrict__ q_out, void* __restrict__ k_cache,
     void* __restrict__ v_cache, const int64_t* __restrict__ slot_mapping,
     const T* __restrict__ qn_w, const T* __restrict__ kn_w, int nq, int nkv, int d, int bs,
-    float eps, float k_inv, float v_inv, int num_blocks, int vgroup) {
+    float eps, float k_inv, float v_inv, int num_blocks) {
   // item space of one token: [q/k rotation items, padded to a wave] [v scatter items];
   // gridDim.y workgroups of ROPE_NT items share a token (fills the CUs at decode).
   // A q/k item is one chunk pair (c, c + d/2) of a group of ROPE_HG heads: the position's
@@ -173,37 +173,6 @@ __global__ __launch_bounds__(ROPE_NT) void rope_kv_kernel(
   const int iv = it - n_qk_pad;
   if (slot < 0 || iv >= nkv * (d >> 3)) return;
   const int h = iv / (d >> 3), c = iv % (d >> 3);
-  if (!KV8 && vgroup) {
-    // Prefill: an 8-key group of V^T that this step writes whole (its 8 tokens are rows
-    // t0 .. t0+7 with consecutive slots) is written by its first token's thread as eight
-    // 16-byte rows (the 8 x 8 block transposed in registers) instead of 64 two-byte
-    // stores spread over eight tokens; the other seven tokens skip it.
-    const int g = (int)(slot & 7);
-    const int t0 = t - g;
-    bool full = t0 >= 0 && t0 + 7 < (int)gridDim.x;
-    if (full) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) full = full && slot_mapping[t0 + k] == slot - g + k;
-    }
-    if (full) {
-      if (g != 0) return;
-      Pack8<T> vv[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        vv[k].u = qkv8<T, SL>(qkv, (int64_t)(t0 + k) * qkv_stride + (nq + nkv) * d + h * d,
-                              c * 8, S, slice_stride);
-      T* dst = reinterpret_cast<T*>(v_cache) + (blk * nkv + h) * (int64_t)bs * d +
-               ((int64_t)(off >> 3) * d + c * 8) * 8;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        Pack8<T> o;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) o.h[k] = vv[k].h[j];
-        *reinterpret_cast<u32x4*>(dst + j * 8) = o.u;
-      }
-      return;
-    }
-  }
   Pack8<T> v;
   v.u = qkv8<T, SL>(qkv, row + (nq + nkv) * d + h * d, c * 8, S, slice_stride);
   const int64_t e = (blk * nkv + h) * (int64_t)bs * d + ((int64_t)(off >> 3) * d + c * 8) * 8 +
@@ -342,14 +311,9 @@ static bool rope_kvg() {
   return !(e && atoi(e) == 0);
 }
 
-// KGC_ROPE_VGROUP=1: the whole-group V^T stores above.  Off by default: measured slower
-// at 16K-token prefill chunks (tools/prefill_rope_bench.py: rope_kv_write 152 -> 173 us,
-// k/v-only 85 -> 94 us; the eight-token leaders serialise what 8 threads did in parallel,
-// and the L2 already merges the 2-byte stores of one line)
-static int rope_vgroup() {
-  const char* e = getenv("KGC_ROPE_VGROUP");
-  return e ? atoi(e) : 0;
-}
+// (A whole-8-key-group V^T store by the group's first token -- KGC_ROPE_VGROUP, round 3 --
+// measured slower at 16K-token prefill chunks, 152 -> 173 us: removed in round 6; the
+// 8-token-group kernel below is the prefill K / V writer)
 
 template <typename T, bool KV8, bool SL>
 static void rope_dispatch(const void* qkv, int64_t qkv_stride, int S, int64_t ss,
@@ -367,7 +331,7 @@ static void rope_dispatch(const void* qkv, int64_t qkv_stride, int S, int64_t ss
 #define KGC_ROPE_LAUNCH(N, R, O)                                                            \
   rope_kv_kernel<T, N, R, KV8, SL, O><<<grid, ROPE_NT, 0, s>>>(                             \
       qkv, qkv_stride, S, ss, pos, cs, (T*)q_out, kc, vc, slots, (const T*)qn,               \
-      (const T*)kn, nq, nkv, d, bs, eps, k_inv, v_inv, num_blocks, rope_vgroup())
+      (const T*)kn, nq, nkv, d, bs, eps, k_inv, v_inv, num_blocks)
   const bool norm = qn != nullptr;
   if constexpr (!KV8 && !SL) {
     if (kvo && rope && !norm && rope_kvg() && (d & 15) == 0 && (bs & 7) == 0) {

@@ -496,14 +496,31 @@ def moe_packable(w13: torch.Tensor, w2: torch.Tensor) -> bool:
     return I2 % 128 == 0 and (I2 // 2) % 64 == 0 and H % 128 == 0 and w2.shape[2] % 64 == 0
 
 
-def moe_dgemm_splitk(npairs: int, E: int, N: int, K: int, bm: int) -> int:
+def moe_k14m_bm(npairs: int, E: int) -> int:
+    """K14m row block for a call of ``npairs`` (token, expert) pairs over E local experts:
+    the smallest of 64 / 96 / 128 that holds a typical expert's pairs in ONE block (an
+    expert with more rows than a block streams its weights once per block): routed
+    uniformly, a bucket is ~npairs / E +- 3 sd (Mixtral 8x7B decode at batch 256: 64 per
+    expert, max ~80 -> 96)."""
+    mean = npairs / max(1, E)
+    if mean <= 44:
+        return 64
+    return 96 if mean <= 72 else 128
+
+
+def moe_k14m_bn() -> int:
+    """K14m column tile: 256 (KGC_MOE_BN=128 for A/B)."""
+    return 128 if os.environ.get("KGC_MOE_BN") == "128" else 256
+
+
+def moe_dgemm_splitk(npairs: int, E: int, N: int, K: int, bm: int, bn: int = 128) -> int:
     """K-slices of K14m's down projection: the used row blocks (at most npairs/bm + E)
-    times N/128 column tiles times S near one workgroup per CU, each slice >= 8 K-steps
+    times N/bn column tiles times S near one workgroup per CU, each slice >= 8 K-steps
     (KGC_MOE_SPLITK overrides, as for the register-staged kernel)."""
     if os.environ.get("KGC_MOE_SPLITK") is not None:
         return max(1, int(os.environ["KGC_MOE_SPLITK"]))
     blocks = min((npairs + bm - 1) // bm + E, max(1, npairs))
-    wgs = blocks * (N // 128)
+    wgs = blocks * (N // bn)
     S = 1
     while S < 16 and wgs * S * 2 <= 320 and K // 64 // (2 * S) >= 8:
         S *= 2
@@ -528,7 +545,11 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     E, I2 = w13.shape[0], w13.shape[1]
     topk = topk_ids.shape[1]
     npairs = T * topk
-    bm = int(os.environ.get("KGC_MOE_BM", 0)) or (64 if npairs <= 40 * E else 128)
+    packed = w13p is not None and w2p is not None
+    bm = int(os.environ.get("KGC_MOE_BM", 0)) or (moe_k14m_bm(npairs, E) if packed else
+                                                  (64 if npairs <= 40 * E else 128))
+    if bm == 96 and not packed:
+        bm = 128                    # the register-staged kernel has 64 / 128-row tiles only
     rows = (npairs + E * (bm - 1) + bm - 1) // bm * bm
     dev = x.device
     sorted_ids = torch.empty(rows, dtype=torch.int32, device=dev)
@@ -536,17 +557,19 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     meta = torch.empty(1, dtype=torch.int32, device=dev)
     ids = topk_ids.contiguous()
     k.moe_align(sorted_ids, block_expert, meta, ids, expert_offset, E, bm)
-    if w13p is not None and w2p is not None:
+    if packed:
+        bn = moe_k14m_bn()
         act = torch.empty(rows, I2 // 2, dtype=x.dtype, device=dev)
         k.moe_dgemm(act, x.contiguous(), w13p, sorted_ids, block_expert, meta, npairs, topk,
-                    bm, 1)
-        S = moe_dgemm_splitk(npairs, E, H, I2 // 2, bm)
+                    bm, 1, bn if I2 % bn == 0 else 128)
+        bn2 = bn if H % bn == 0 else 128
+        S = moe_dgemm_splitk(npairs, E, H, I2 // 2, bm, bn2)
         alloc = torch.empty if all_local else torch.zeros
         if S > 1:
             y = alloc(S, npairs, H, dtype=torch.float32, device=dev)
         else:
             y = alloc(npairs, H, dtype=x.dtype, device=dev)
-        k.moe_dgemm(y, act, w2p, sorted_ids, block_expert, meta, npairs, topk, bm, 2)
+        k.moe_dgemm(y, act, w2p, sorted_ids, block_expert, meta, npairs, topk, bm, 2, bn2)
         out = torch.empty(T, H, dtype=x.dtype, device=dev)
         k.moe_combine(out, y, topk_w.contiguous().float())
         return out

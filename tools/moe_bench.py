@@ -55,16 +55,18 @@ def main():
                "loop_us": round(t_loop * 1e6, 1),
                "native_TFLOPs": round(flops / t_nat / 1e12, 1),
                "native_w_TBps": round(wbytes / t_nat / 1e12, 2)}
-        for kbm in (64, 128):
+        for kbm, kbn in ((64, 256), (96, 256), (128, 256), (64, 128), (96, 128), (128, 128)):
             os.environ["KGC_MOE_BM"] = str(kbm)
+            os.environ["KGC_MOE_BN"] = str(kbn)
             got = ops.fused_moe(x, w13, w2, tw, tid, w13p=w13p, w2p=w2p).float()
             err = ((got - exp).abs().max() / exp.abs().max().clamp_min(1e-6)).item()
             t = timeit(lambda: ops.fused_moe(x, w13, w2, tw, tid, w13p=w13p, w2p=w2p))
-            row[f"k14m_bm{kbm}_us"] = round(t * 1e6, 1)
-            row[f"k14m_bm{kbm}_w_TBps"] = round(wbytes / t / 1e12, 2)
-            row[f"k14m_bm{kbm}_S"] = ops.moe_dgemm_splitk(npairs, a.E, a.H, a.I, kbm)
-            row[f"k14m_bm{kbm}_rel_err"] = float(f"{err:.2e}")
+            row[f"k14m_bm{kbm}_bn{kbn}_us"] = round(t * 1e6, 1)
+            row[f"k14m_bm{kbm}_bn{kbn}_w_TBps"] = round(wbytes / t / 1e12, 2)
+            row[f"k14m_bm{kbm}_bn{kbn}_S"] = ops.moe_dgemm_splitk(npairs, a.E, a.H, a.I, kbm, kbn)
+            row[f"k14m_bm{kbm}_bn{kbn}_rel_err"] = float(f"{err:.2e}")
         os.environ.pop("KGC_MOE_BM", None)
+        os.environ.pop("KGC_MOE_BN", None)
         print(json.dumps(row), flush=True)
 
 

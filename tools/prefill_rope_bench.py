@@ -4,7 +4,7 @@
 
 One JSON line per variant: rope_kv_write (q + k + v), the k / v-only write the fused path
 uses, K2 on a rotated q, and K2 rotating q itself (prefill_attention_rope).  Run under
-KGC_ROPE_VGROUP=0 / 1 to A/B the whole-group V^T stores.
+KGC_ROPE_KVG=0 / 1 to A/B the 8-token-group K / V writer.
 """
 import argparse
 import json
@@ -68,8 +68,7 @@ def main():
     ws = torch.tensor(ws, dtype=torch.int32, device=dev)
     wm = torch.tensor(wm, dtype=torch.int32, device=dev)
     q = ops.rope_kv_write(qkv, pos, cs, kc, vc, slots, nq, nkv, d)
-    tag = {"vgroup": os.environ.get("KGC_ROPE_VGROUP", "0"),
-           "kvg": os.environ.get("KGC_ROPE_KVG", "1"), "T": T}
+    tag = {"kvg": os.environ.get("KGC_ROPE_KVG", "1"), "T": T}
     res = {
         "rope_kv_write": timeit(lambda: ops.rope_kv_write(qkv, pos, cs, kc, vc, slots, nq, nkv, d)),
         "kv_write_rope (k/v only)": timeit(lambda: ops.kv_write_rope(qkv, pos, cs, kc, vc, slots,
