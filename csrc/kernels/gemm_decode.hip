@@ -183,13 +183,18 @@ __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
 #pragma unroll
   for (int t = 0; t < LA; ++t) {
     int r = m0 + (iw * LA + t) * 8 + drow;
-    r = r < M ? r : M - 1;                        // padded rows re-read the last row
+    // padded rows re-read the last row; the MFMA waves of a loader-wave kernel (iw < 0)
+    // never issue, their (clamped) rows are never read
+    r = r < M ? (r < 0 ? 0 : r) : M - 1;
     if constexpr (MOE == 1) {
       // the token of sorted pair row r; a padding row (p == npairs) re-reads the block's
-      // first pair's token (an L2 hit; its output row is never stored)
-      int p = aux.sorted_ids[r];
-      if (p >= aux.npairs) p = aux.sorted_ids[m0];
-      r = p / aux.topk;
+      // first pair's token (an L2 hit; its output row is never stored).  Only the waves
+      // that issue DMAs read the row map.
+      if (LDW == 0 || loader) {
+        int p = aux.sorted_ids[r];
+        if (p >= aux.npairs) p = aux.sorted_ids[m0];
+        r = p / aux.topk;
+      }
     }
     a_src[t] = X + (int64_t)r * ldx + dchunk * 8;
   }

@@ -133,6 +133,9 @@ class Worker:
             ws = [p for n, p in self.model.named_parameters() if p.dim() == 2
                   and id(p) not in skip and (tied or "embed" not in n)]
             gemm.pack_decode_weights(ws, silu)
+        if dev.type == "cuda":
+            # K14m's packed expert copies serve eager and graph steps alike (the same
+            # kernels, so an eager engine computes exactly what the graphs compute)
             from ..models.moe import pack_moe_experts
             pack_moe_experts(self.model)
         if dev.type == "cuda":

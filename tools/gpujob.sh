@@ -22,6 +22,7 @@
 #   phantom   Llama-3-70B TP = 8 rank-0 stand-in (one GPU), engine mode + anatomy
 #   dgemm8    K9m microbench at M = 256 on the Llama-3-70B TP = 8 shard shapes
 #   prof_mix  rocprofv3 anatomy of one Mixtral 8x7B engine wave (DETAIL=1)
+#   phantom_mix  Mixtral 8x7B EP = 8 rank-0 stand-in (one GPU), engine mode + anatomy
 set -o pipefail
 TAG="${TAG:-job}"
 K="${K:-}"
@@ -43,6 +44,7 @@ for r in "$@"; do
     attn)    steps+=("attn|300|python tools/attn_bench.py --batch 256 --ctx 640 --ragged 0 --rope 4 > ${O}_attn.jsonl && python tools/attn_bench.py --batch 32 --ctx 2600 --ragged 0.25 >> ${O}_attn.jsonl && python tools/attn_bench.py --batch 1 --ctx 640 --ragged 0 --rope 0 >> ${O}_attn.jsonl && python tools/attn_bench.py --batch 256 --ctx 640 --ragged 0 --nq 8 --nkv 1 --rope 4 >> ${O}_attn.jsonl") ;;
     moe)     steps+=("moe|400|python tools/moe_bench.py --tokens 1 16 64 128 256 --no-loop > ${O}_moe.jsonl 2> ${O}_moe.err") ;;
     dgemm)   steps+=("dgemm|500|python tools/dgemm_bench.py --ms 256 --splits 1,2,3,4,5,6,8,12,16 > ${O}_dgemm.jsonl 2> ${O}_dgemm.err") ;;
+    phantom_mix) steps+=("phantom_mix|600|env $ENVS KGC_TP_PHANTOM=8 DETAIL=1 bash tools/profile.sh /tmp/phm_${TAG} -- python bench.py --mode engine --model mixtral-8x7b --moe-parallel ep --steps 1 --warmup 1 > ${O}_phantom_mix.log 2>&1 && cp /tmp/phm_${TAG}/summary.txt ${O}_phantom_mix_summary.txt") ;;
     dgemm8)  steps+=("dgemm8|500|python tools/dgemm_bench.py --model llama-3-70b --tp 8 --ms 256 --copies 8 --shapes qkv,o,gate_up,down --splits 1,2,3,4,6,8,12,16 > ${O}_dgemm8.jsonl 2> ${O}_dgemm8.err") ;;
     prof_mix) steps+=("prof_mix|900|env $ENVS DETAIL=1 bash tools/profile.sh /tmp/pmix_${TAG} -- python bench.py --mode engine --model mixtral-8x7b --steps 1 --warmup 1 > ${O}_prof_mix.log 2>&1 && cp /tmp/pmix_${TAG}/summary.txt ${O}_prof_mix_summary.txt") ;;
     b70)     steps+=("b70|1100|env $ENVS python bench.py --model llama-3-70b --steps 1 --warmup 1 > ${O}_b70.json 2> ${O}_b70.err") ;;
