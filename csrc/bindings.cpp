@@ -434,6 +434,29 @@ void moe_route(Tensor topk_w, Tensor topk_ids, Tensor logits, bool renorm) {
                         (int)k, renorm, topk_w.data_ptr<float>(), topk_ids.data_ptr<int>(), stream());
 }
 
+void moe_gate_route(Tensor topk_w, Tensor topk_ids, Tensor x, Tensor wg, bool renorm) {
+  check_gpu(x, "x");
+  c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "x [T, H], 16-B aligned rows");
+  TORCH_CHECK(wg.dim() == 2 && wg.is_contiguous() && wg.scalar_type() == x.scalar_type() &&
+                  (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf),
+              "wg [E, H] contiguous, x's dtype (bf16 / fp16)");
+  const int64_t T = x.size(0), H = x.size(1), E = wg.size(0), k = topk_w.size(-1);
+  TORCH_CHECK(wg.size(1) == H && H % 512 == 0, "H % 512 == 0");
+  TORCH_CHECK(E >= 1 && E <= 16 && k >= 1 && k <= E, "1 <= k <= E <= 16");
+  TORCH_CHECK(topk_w.scalar_type() == at::kFloat && topk_w.is_contiguous() && topk_w.numel() == T * k,
+              "topk_w fp32 [T, k]");
+  TORCH_CHECK(topk_ids.scalar_type() == at::kInt && topk_ids.is_contiguous() &&
+              topk_ids.numel() == T * k, "topk_ids int32 [T, k]");
+  check_same_dev(x, wg, "moe_gate_route");
+  if (T == 0) return;
+  kgc::launch_moe_gate_route(dt_code(x), x.data_ptr(), x.stride(0), wg.data_ptr(), (int)H, (int)E,
+                             (int)T, (int)k, renorm, topk_w.data_ptr<float>(),
+                             topk_ids.data_ptr<int>(), stream());
+}
+
 void moe_align(Tensor sorted_ids, Tensor block_expert, Tensor meta, Tensor topk_ids, int64_t e0,
                int64_t E_local, int64_t bm) {
   check_gpu(topk_ids, "topk_ids");
@@ -1191,6 +1214,8 @@ TORCH_LIBRARY(kgc, m) {
   m.def("sample_vp_unpack(Tensor(a!) out, Tensor packed) -> ()");
   m.def("decode_wave_min_pairs() -> int", &decode_wave_min_pairs);
   m.def("moe_route(Tensor(a!) topk_w, Tensor(b!) topk_ids, Tensor logits, bool renorm) -> ()");
+  m.def("moe_gate_route(Tensor(a!) topk_w, Tensor(b!) topk_ids, Tensor x, Tensor wg, "
+        "bool renorm) -> ()");
   m.def("moe_align(Tensor(a!) sorted_ids, Tensor(b!) block_expert, Tensor(c!) meta, "
         "Tensor topk_ids, int e0, int E_local, int bm) -> ()");
   m.def("moe_gemm(Tensor(a!) C, Tensor A, Tensor W, Tensor sorted_ids, Tensor block_expert, "
@@ -1286,6 +1311,7 @@ TORCH_LIBRARY_IMPL(kgc, CUDA, m) {
   m.impl("ep_return", &ep_return);
   m.impl("ep_combine", &ep_combine);
   m.impl("moe_route", &moe_route);
+  m.impl("moe_gate_route", &moe_gate_route);
   m.impl("moe_align", &moe_align);
   m.impl("moe_gemm", &moe_gemm);
   m.impl("moe_dgemm", &moe_dgemm);

@@ -114,6 +114,11 @@ int moe_block_n();
 int moe_block_k();
 void launch_moe_route(int dtype, const void* logits, int64_t stride, int ntok, int E, int k,
                       bool renorm, float* topk_w, int* topk_ids, hipStream_t s);
+// router GEMM + moe_route in one launch: x [T, H] (rows ldx apart) . wg [E, H]^T, E <= 16,
+// H % 512 == 0 -> topk_w fp32 / topk_ids int32 [T, k]
+void launch_moe_gate_route(int dtype, const void* x, int64_t ldx, const void* wg, int H, int E,
+                           int ntok, int k, bool renorm, float* topk_w, int* topk_ids,
+                           hipStream_t s);
 void launch_moe_align(const int* topk_ids, int npairs, int e0, int E_local, int bm, int max_rows,
                       int* sorted_ids, int* block_expert, int* meta, hipStream_t s);
 // splitk > 1 (scatter only): C is S fp32 slices of slice_stride elements each

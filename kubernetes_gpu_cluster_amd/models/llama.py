@@ -241,11 +241,15 @@ class LlamaForCausalLM(nn.Module):
         """One GPU, whole model, dense bias-free MLP / o_proj, and a fused-tail plan at this
         M (K9m split-K, or K9 SK_ACC_NORM at small M): the o / down projections then run
         with their reduction / residual add fused into the next norm."""
-        if not (x.is_cuda and self.first and self.last and self.layers and not self.cfg.is_moe
+        if not (x.is_cuda and self.first and self.last and self.layers
                 and get_state().tp_size == 1 and gemm.tail_plan_has_m(x.shape[0])
                 and _tail_fusion_enabled):
             return False
         l0 = self.layers[0]
+        if self.cfg.is_moe:
+            # MoE (TP = 1): o_proj's tail is fused; the MoE block's output meets the next
+            # norm through fused_add_rms_norm
+            return l0.self_attn.o_proj.bias is None
         return (l0.self_attn.o_proj.bias is None and l0.mlp.down_proj.bias is None
                 and l0.mlp.gate_up_proj.bias is None)
 
@@ -255,18 +259,24 @@ class LlamaForCausalLM(nn.Module):
         the next layer's input norm (the last one -> the final norm).  Same math and
         rounding points as ``LlamaDecoderLayer.forward``."""
         residual, h, prev = x, None, None
+        moe = self.cfg.is_moe
         for layer in self.layers:
             ln1 = layer.input_layernorm
             if prev is None:
                 x = ln1(x)
+            elif moe:
+                x, residual = ln1(h, residual)
             else:
                 x, residual = gemm.linear_add_rms(h, prev.mlp.down_proj.weight, residual,
                                                   ln1.weight, ln1.eps)
             at, ln2 = layer.self_attn, layer.post_attention_layernorm
             a = at.attend(positions, at.project_qkv(x), ctx)
             x, residual = gemm.linear_add_rms(a, at.o_proj.weight, residual, ln2.weight, ln2.eps)
-            h = gemm.linear_silu(x, layer.mlp.gate_up_proj.weight)
+            h = layer.mlp(x) if moe else gemm.linear_silu(x, layer.mlp.gate_up_proj.weight)
             prev = layer
+        if moe:
+            x, _ = self.norm(h, residual)
+            return x
         x, _ = gemm.linear_add_rms(h, prev.mlp.down_proj.weight, residual, self.norm.weight,
                                    self.norm.eps)
         return x
@@ -472,10 +482,12 @@ class LlamaForCausalLM(nn.Module):
     def tail_shapes(self) -> set:
         """(N, K) of the o / down projections whose split-K reduction the following
         residual add + RMSNorm absorbs (``_forward_tail_fused``), when that path can run."""
-        if not (self.first and self.last and self.layers and not self.cfg.is_moe
+        if not (self.first and self.last and self.layers
                 and get_state().tp_size == 1 and _tail_fusion_enabled):
             return set()
         l0 = self.layers[0]
+        if self.cfg.is_moe:
+            return {tuple(l0.self_attn.o_proj.weight.shape)}
         return {tuple(l0.self_attn.o_proj.weight.shape), tuple(l0.mlp.down_proj.weight.shape)}
 
     def fused_norm_shapes(self) -> set:

@@ -447,6 +447,7 @@ __all__ = ["load_extension", "rms_norm", "fused_add_rms_norm", "layer_norm", "si
 
 
 # ------------------------------------------------------------------ MoE (K13 / K14)
+MOE_GATE_FUSED_MAX_T = 1024  # tokens up to which the router GEMM runs inside the top-k kernel
 MOE_NATIVE_MAX_ROWS = 128   # mean rows per expert above which hipBLASLt per expert wins
 
 
@@ -463,6 +464,22 @@ def moe_topk_softmax(router_logits: torch.Tensor, k: int, renormalize: bool = Tr
     w = torch.empty(T, k, dtype=torch.float32, device=router_logits.device)
     ids = torch.empty(T, k, dtype=torch.int32, device=router_logits.device)
     _k().moe_route(w, ids, router_logits, renormalize)
+    return w, ids
+
+
+def moe_gate_topk(x: torch.Tensor, wg: torch.Tensor, k: int,
+                  renormalize: bool = True) -> Optional[tuple]:
+    """K13 with the router GEMM folded in: (weights fp32 [T, k], expert ids int32 [T, k])
+    of x [T, H] . wg [E, H]^T in one launch, or None where the fused kernel does not apply
+    (CPU, E > 16, H % 512 != 0): the caller then runs the GEMM and ``moe_topk_softmax``."""
+    if (not _gpu(x) or x.dim() != 2 or wg.shape[0] > 16 or x.shape[1] % 512
+            or x.dtype not in (torch.bfloat16, torch.float16) or wg.dtype != x.dtype
+            or x.stride(1) != 1 or x.stride(0) % 8):
+        return None
+    T = x.shape[0]
+    w = torch.empty(T, k, dtype=torch.float32, device=x.device)
+    ids = torch.empty(T, k, dtype=torch.int32, device=x.device)
+    _k().moe_gate_route(w, ids, x, wg.contiguous(), renormalize)
     return w, ids
 
 

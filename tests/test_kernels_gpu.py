@@ -587,6 +587,33 @@ def test_moe_route(gpu, dt, E, k):
     torch.testing.assert_close(w.cpu(), rw, atol=1e-5, rtol=1e-5)
 
 
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("E,k,H", [(8, 2, 4096), (8, 2, 512), (4, 1, 1024), (16, 4, 2048),
+                                   (6, 2, 512)])
+@pytest.mark.parametrize("T", [1, 7, 256, 300])
+def test_moe_gate_topk_matches_gemm_then_route(gpu, dt, E, k, H, T):
+    """The router GEMM fused into the top-k kernel (ops.moe_gate_topk) == the GEMM (logits
+    rounded to the activation dtype) followed by the fp32 softmax / top-k reference: the
+    same experts where the top-k logits are untied, weights within fp32 rounding."""
+    torch.manual_seed(E * 100 + T + H)
+    x = (torch.randn(T, H, device=gpu) * 0.5).to(dt)
+    wg = (torch.randn(E, H, device=gpu) / H ** 0.5).to(dt)
+    got = ops.moe_gate_topk(x, wg, k)
+    assert got is not None
+    w, ids = got
+    logits = (x.float().cpu() @ wg.float().cpu().t()).to(dt).float()
+    rw, rids = ref.moe_topk_softmax(logits, k)
+    ids = ids.cpu().long()
+    # the fused dot products sum in another order than the fp32 reference: compare the
+    # selected logits (a near-tie may pick either expert), ids where clearly separated
+    torch.testing.assert_close(logits.gather(1, ids), logits.gather(1, rids.long()),
+                               atol=2e-2, rtol=2e-2)
+    srt = logits.sort(1, descending=True).values
+    clear = (srt[:, k - 1] - srt[:, k]).abs() > 5e-2
+    assert torch.equal(ids[clear].sort(1).values, rids.long()[clear].sort(1).values)
+    torch.testing.assert_close(w.cpu()[clear], rw[clear], atol=2e-2, rtol=2e-2)
+
+
 def _moe_case(dt, T, E, k, H, I, dev, seed=0):
     g = torch.Generator().manual_seed(seed)
     x = (torch.randn(T, H, generator=g) * 0.5).to(dt).to(dev)
