@@ -570,21 +570,36 @@ void moe_dgemm(Tensor C, Tensor A, Tensor Wp, Tensor sorted_ids, Tensor block_ex
                         meta.data_ptr<int>(), (int)npairs, (int)topk, stream());
 }
 
-void moe_combine(Tensor out, Tensor y, Tensor topk_w) {
+void moe_combine(Tensor out, Tensor y, Tensor topk_w, const c10::optional<Tensor>& row_map) {
   check_gpu(y, "y");
   c10::hip::HIPGuardMasqueradingAsCUDA g(y.device());
   const int64_t T = out.size(0), H = out.size(1), k = topk_w.size(-1);
   TORCH_CHECK(out.is_contiguous() && y.is_contiguous() && H % 8 == 0, "contiguous, H % 8 == 0");
-  // y: [T*k, H] in out's dtype, or fp32 split-K slices [S, rows >= T*k, H]
-  const bool slices = y.dim() == 3;
-  TORCH_CHECK(slices ? (y.scalar_type() == at::kFloat && y.size(2) == H && y.size(1) >= T * k)
-                     : (y.scalar_type() == out.scalar_type() && y.numel() >= T * k * H),
-              "y [T*k, H] or fp32 [S, >= T*k, H]");
   TORCH_CHECK(topk_w.numel() == T * k && topk_w.scalar_type() == at::kFloat, "topk_w fp32 [T, k]");
   TORCH_CHECK(T <= 65535, "at most 65535 tokens per call");
+  const int* map = nullptr;
+  int64_t nrows = T * k;
+  if (row_map.has_value()) {
+    // y: [rows, H] in out's dtype, pair p read from row row_map[p] (-1 = no row); the
+    // kernel skips indices outside [0, rows)
+    const Tensor& rm = *row_map;
+    TORCH_CHECK(y.dim() == 2 && y.size(1) == H && y.scalar_type() == out.scalar_type(),
+                "y [rows, H] in out's dtype");
+    TORCH_CHECK(rm.scalar_type() == at::kInt && rm.is_contiguous() && rm.numel() == T * k &&
+                    rm.device() == y.device(),
+                "row_map int32 [T*k] on y's device");
+    map = rm.data_ptr<int>();
+    nrows = y.size(0);
+  }
+  // y: [T*k, H] in out's dtype, or fp32 split-K slices [S, rows >= T*k, H]
+  const bool slices = y.dim() == 3;
+  if (!map)
+    TORCH_CHECK(slices ? (y.scalar_type() == at::kFloat && y.size(2) == H && y.size(1) >= T * k)
+                       : (y.scalar_type() == out.scalar_type() && y.numel() >= T * k * H),
+                "y [T*k, H] or fp32 [S, >= T*k, H]");
   if (T == 0) return;
   kgc::launch_moe_combine(dt_code(out), out.data_ptr(), y.data_ptr(), topk_w.data_ptr<float>(),
-                          (int)T, (int)k, (int)H, slices ? (int)y.size(0) : 1,
+                          map, nrows, (int)T, (int)k, (int)H, slices ? (int)y.size(0) : 1,
                           slices ? y.stride(0) : 0, stream());
 }
 
@@ -892,13 +907,31 @@ void ep_receive(Tensor x_local, Tensor ids, Tensor route, std::vector<int64_t> d
 }
 
 void ep_return(Tensor y, Tensor route, std::vector<int64_t> data, std::vector<int64_t> sig,
-               int64_t rank, int64_t C) {
-  ep_check_rows(y, "y");
+               int64_t rank, int64_t C, c10::optional<at::ScalarType> out_dtype) {
+  // y: [NR * C, H] bf16 / fp16, or the down projection's fp32 split-K slices
+  // [S, >= NR * C, H] (summed by the kernel, written in out_dtype)
+  check_gpu(y, "y");
   c10::hip::HIPGuardMasqueradingAsCUDA g(y.device());
-  TORCH_CHECK(y.size(0) == (int64_t)data.size() * C && route.numel() == y.size(0) &&
-              route.scalar_type() == at::kInt, "y [NR * C, H], route int32 [NR * C]");
+  const int64_t rows = (int64_t)data.size() * C;
+  TORCH_CHECK(route.numel() == rows && route.scalar_type() == at::kInt && route.is_contiguous(),
+              "route int32 [NR * C]");
+  if (y.dim() == 3) {
+    TORCH_CHECK(y.scalar_type() == at::kFloat && y.is_contiguous() && y.size(1) >= rows &&
+                    y.size(2) % 8 == 0 && out_dtype.has_value() &&
+                    (*out_dtype == at::kBFloat16 || *out_dtype == at::kHalf),
+                "fp32 slices [S, >= NR * C, H] need out_dtype bf16 / fp16");
+    kgc::launch_ep_return(*out_dtype == at::kBFloat16 ? kgc::DT_BF16 : kgc::DT_F16,
+                          ep_ptrs(data, sig, rank), (int)data.size(), (int)rank, y.data_ptr(),
+                          (int)y.size(0), y.stride(0), route.data_ptr<int>(), (int)y.size(2),
+                          (int)C, stream());
+    return;
+  }
+  ep_check_rows(y, "y");
+  TORCH_CHECK(y.size(0) == rows && (!out_dtype.has_value() || *out_dtype == y.scalar_type()),
+              "y [NR * C, H]");
   kgc::launch_ep_return(dt_code(y), ep_ptrs(data, sig, rank), (int)data.size(), (int)rank,
-                        y.data_ptr(), route.data_ptr<int>(), (int)y.size(1), (int)C, stream());
+                        y.data_ptr(), 0, 0, route.data_ptr<int>(), (int)y.size(1), (int)C,
+                        stream());
 }
 
 void ep_combine(Tensor out, Tensor topk_w, std::vector<int64_t> data, std::vector<int64_t> sig,
@@ -1222,7 +1255,7 @@ TORCH_LIBRARY(kgc, m) {
         "Tensor meta, int npairs, int topk, int bm, bool gather, bool scatter, int splitk=1) -> ()");
   m.def("moe_dgemm(Tensor(a!) C, Tensor A, Tensor Wp, Tensor sorted_ids, Tensor block_expert, "
         "Tensor meta, int npairs, int topk, int bm, int mode, int bn=256) -> ()");
-  m.def("moe_combine(Tensor(a!) out, Tensor y, Tensor topk_w) -> ()");
+  m.def("moe_combine(Tensor(a!) out, Tensor y, Tensor topk_w, Tensor? row_map=None) -> ()");
   m.def("dense_gemm_splitk(Tensor(a!) Cs, Tensor A, Tensor W, int bm) -> ()");
   m.def("splitk_reduce(Tensor(a!) out, Tensor Cs) -> ()");
   m.def("dgemm(Tensor(a!) C, Tensor X, Tensor W, int cfg, int epi, Tensor? rscale=None) -> ()");
@@ -1278,7 +1311,8 @@ TORCH_LIBRARY(kgc, m) {
         "int C) -> ()");
   m.def("ep_receive(Tensor(a!) x_local, Tensor(b!) ids, Tensor(c!) route, int[] data, int[] sig, "
         "int rank, int E_local, int C) -> ()");
-  m.def("ep_return(Tensor y, Tensor route, int[] data, int[] sig, int rank, int C) -> ()");
+  m.def("ep_return(Tensor y, Tensor route, int[] data, int[] sig, int rank, int C, "
+        "ScalarType? out_dtype=None) -> ()");
   m.def("ep_combine(Tensor(a!) out, Tensor topk_w, int[] data, int[] sig, int rank, int C) -> ()");
   m.def("debug_build() -> bool", &debug_build);
   m.def("sample_stamps_enable(bool on) -> ()", &sample_stamps_enable);

@@ -27,7 +27,11 @@ namespace kgc {
 
 constexpr int EP_MAX_RANKS = 8;
 constexpr int EP_THREADS = 512;
-constexpr int EP_BLOCKS = 64;
+constexpr int EP_WAVES = EP_THREADS / 64;
+// one wave per row (pair / slot / token): 1,024 rows in flight.  One workgroup per row over
+// 64 workgroups walked the 4,096 receive slots 64 deep, a dependent route / count load per
+// step (~20 us per phase at Mixtral's EP = 8 decode shapes)
+constexpr int EP_BLOCKS = 128;
 constexpr int EP_MAX_PAIRS = 4096;   // T * k of one call (decode buckets)
 
 struct EpSignal {
@@ -169,14 +173,15 @@ __global__ __launch_bounds__(EP_THREADS) void ep_dispatch_kernel(
   const EpLayout L(NR, C, H, sizeof(T), par);
   ep_positions<NR>(topk_ids, npairs, E_local, s_dest, s_pos, s_cnt);
   const int nv = H >> 3;
-  for (int p = blockIdx.x; p < npairs; p += gridDim.x) {
+  const int lane = threadIdx.x & 63;
+  for (int p = blockIdx.x * EP_WAVES + (threadIdx.x >> 6); p < npairs; p += gridDim.x * EP_WAVES) {
     const int d = s_dest[p], pos = s_pos[p];
     char* base = reinterpret_cast<char*>(P.data[d]);
     const int64_t slot = (int64_t)rank * C + pos;               // d's region for source `rank`
     const u32x4* src = reinterpret_cast<const u32x4*>(x + (int64_t)(p / k) * H);
     u32x4* dst = reinterpret_cast<u32x4*>(base + L.x) + slot * nv;
-    for (int v = threadIdx.x; v < nv; v += EP_THREADS) dst[v] = src[v];
-    if (threadIdx.x == 0) {
+    for (int v = lane; v < nv; v += 64) dst[v] = src[v];
+    if (lane == 0) {
       int* meta = reinterpret_cast<int*>(base + L.meta) + 2 * slot;
       meta[0] = topk_ids[p] - d * E_local;                     // owner-local expert
       meta[1] = p;                                             // pair index at the source
@@ -201,36 +206,68 @@ __global__ __launch_bounds__(EP_THREADS) void ep_receive_kernel(
   const char* base = reinterpret_cast<const char*>(P.data[rank]);
   const int* cnt = reinterpret_cast<const int*>(base + L.cnt);
   const int* meta = reinterpret_cast<const int*>(base + L.meta);
+  __shared__ int s_cnt[NR];
+  if (threadIdx.x < NR) s_cnt[threadIdx.x] = cnt[threadIdx.x];
+  __syncthreads();
   const int nv = H >> 3;
-  for (int slot = blockIdx.x; slot < NR * C; slot += gridDim.x) {
+  const int lane = threadIdx.x & 63;
+  for (int slot = blockIdx.x * EP_WAVES + (threadIdx.x >> 6); slot < NR * C;
+       slot += gridDim.x * EP_WAVES) {
     const int s = slot / C, i = slot % C;
-    const bool valid = i < cnt[s];
-    if (threadIdx.x == 0) {
+    const bool valid = i < s_cnt[s];
+    if (lane == 0) {
       ids[slot] = valid ? meta[2 * slot] + rank * E_local : -1;
       route[slot] = valid ? meta[2 * slot + 1] : -1;
     }
     if (!valid) continue;
     const u32x4* src = reinterpret_cast<const u32x4*>(base + L.x) + (int64_t)slot * nv;
     u32x4* dst = reinterpret_cast<u32x4*>(x_local) + (int64_t)slot * nv;
-    for (int v = threadIdx.x; v < nv; v += EP_THREADS) dst[v] = src[v];
+    for (int v = lane; v < nv; v += 64) dst[v] = src[v];
   }
 }
 
-// owner: each valid result row back to its source's return region at its pair index
+// owner: each valid result row back to its source's return region at its pair index.
+// y is the grouped MLP's output in T ([NR * C, H], S = 0) or its down projection's fp32
+// split-K slices ([S, >= NR * C, H], summed here and rounded once): the slices never go
+// through a separate combine pass, and empty slots are never read.
 template <typename T, int NR>
 __global__ __launch_bounds__(EP_THREADS) void ep_return_kernel(
-    EpPtrs P, int rank, const T* __restrict__ y, const int* __restrict__ route, int H, int C) {
+    EpPtrs P, int rank, const void* __restrict__ y, int S, int64_t slice_stride,
+    const int* __restrict__ route, int H, int C) {
   const uint32_t epoch = ep_epoch(P, rank);
   const EpLayout L(NR, C, H, sizeof(T), epoch & 1);
   const int nv = H >> 3;
-  for (int slot = blockIdx.x; slot < NR * C; slot += gridDim.x) {
+  const int lane = threadIdx.x & 63;
+  for (int slot = blockIdx.x * EP_WAVES + (threadIdx.x >> 6); slot < NR * C;
+       slot += gridDim.x * EP_WAVES) {
     const int p = route[slot];
     if (p < 0) continue;
     const int s = slot / C;
     u32x4* dst = reinterpret_cast<u32x4*>(reinterpret_cast<char*>(P.data[s]) + L.ret) +
                  (int64_t)p * nv;
-    const u32x4* src = reinterpret_cast<const u32x4*>(y) + (int64_t)slot * nv;
-    for (int v = threadIdx.x; v < nv; v += EP_THREADS) dst[v] = src[v];
+    if (S == 0) {
+      const u32x4* src = reinterpret_cast<const u32x4*>(y) + (int64_t)slot * nv;
+      for (int v = lane; v < nv; v += 64) dst[v] = src[v];
+    } else {
+      const float* rowp = reinterpret_cast<const float*>(y) + (int64_t)slot * H;
+      for (int v = lane; v < nv; v += 64) {
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int z = 0; z < S; ++z) {
+          const float* src = rowp + z * slice_stride + v * 8;
+          const f32x4 a = *reinterpret_cast<const f32x4*>(src);
+          const f32x4 b = *reinterpret_cast<const f32x4*>(src + 4);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            acc[q] += a[q];
+            acc[4 + q] += b[q];
+          }
+        }
+        Pack8<T> o;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) o.h[q] = from_f<T>(acc[q]);
+        dst[v] = o.u;
+      }
+    }
   }
   ep_grid_publish<NR>(P, rank, 1, epoch);
 }
@@ -245,8 +282,9 @@ __global__ __launch_bounds__(EP_THREADS) void ep_combine_kernel(
   ep_wait_all<NR>(P, rank, 1, epoch);
   const T* ret = reinterpret_cast<const T*>(reinterpret_cast<const char*>(P.data[rank]) + L.ret);
   const int nv = H >> 3;
-  for (int t = blockIdx.x; t < ntok; t += gridDim.x)
-    for (int v = threadIdx.x; v < nv; v += EP_THREADS) {
+  const int lane = threadIdx.x & 63;
+  for (int t = blockIdx.x * EP_WAVES + (threadIdx.x >> 6); t < ntok; t += gridDim.x * EP_WAVES)
+    for (int v = lane; v < nv; v += 64) {
       float acc[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] = 0.f;
@@ -330,18 +368,19 @@ void launch_ep_receive(int dtype, const EpPtrs& P, int nr, int rank, void* x_loc
 }
 
 template <typename T>
-static void ep_return_t(const EpPtrs& P, int nr, int rank, const void* y, const int* route, int H,
-                        int C, hipStream_t s) {
+static void ep_return_t(const EpPtrs& P, int nr, int rank, const void* y, int S,
+                        int64_t slice_stride, const int* route, int H, int C, hipStream_t s) {
 #define KGC_EPT(NR)                                                                          \
-  ep_return_kernel<T, NR><<<EP_BLOCKS, EP_THREADS, 0, s>>>(P, rank, (const T*)y, route, H, C)
+  ep_return_kernel<T, NR><<<EP_BLOCKS, EP_THREADS, 0, s>>>(P, rank, y, S, slice_stride, route, \
+                                                           H, C)
   KGC_EP_RANKS(nr, KGC_EPT)
 #undef KGC_EPT
 }
 
-void launch_ep_return(int dtype, const EpPtrs& P, int nr, int rank, const void* y,
-                      const int* route, int H, int C, hipStream_t s) {
-  if (dtype == DT_BF16) ep_return_t<bf16>(P, nr, rank, y, route, H, C, s);
-  else ep_return_t<f16>(P, nr, rank, y, route, H, C, s);
+void launch_ep_return(int dtype, const EpPtrs& P, int nr, int rank, const void* y, int S,
+                      int64_t slice_stride, const int* route, int H, int C, hipStream_t s) {
+  if (dtype == DT_BF16) ep_return_t<bf16>(P, nr, rank, y, S, slice_stride, route, H, C, s);
+  else ep_return_t<f16>(P, nr, rank, y, S, slice_stride, route, H, C, s);
 }
 
 template <typename T>

@@ -178,8 +178,9 @@ void launch_splitk_reduce(int dtype, void* out, const float* Cs, int S, int64_t 
 void launch_splitk_reduce_silu(int dtype, void* out, const float* Cs, int S, int M, int I,
                                int64_t slice_stride, bool interleaved, const float* rsc,
                                hipStream_t s);
-void launch_moe_combine(int dtype, void* out, const void* y, const float* topk_w, int ntok, int k,
-                        int H, int splitk, int64_t slice_stride, hipStream_t s);
+void launch_moe_combine(int dtype, void* out, const void* y, const float* topk_w,
+                        const int* row_map, int64_t nrows, int ntok, int k, int H,
+                        int splitk, int64_t slice_stride, hipStream_t s);
 
 // K12 xGMI all-reduce: per-rank [signal | data parity 0 | data parity 1] IPC buffers.
 struct ArPtrs {
@@ -227,8 +228,8 @@ void launch_ep_dispatch(int dtype, const EpPtrs& P, int nr, int rank, const void
                         hipStream_t s);
 void launch_ep_receive(int dtype, const EpPtrs& P, int nr, int rank, void* x_local, int* ids,
                        int* route, int H, int E_local, int C, hipStream_t s);
-void launch_ep_return(int dtype, const EpPtrs& P, int nr, int rank, const void* y,
-                      const int* route, int H, int C, hipStream_t s);
+void launch_ep_return(int dtype, const EpPtrs& P, int nr, int rank, const void* y, int S,
+                      int64_t slice_stride, const int* route, int H, int C, hipStream_t s);
 void launch_ep_combine(int dtype, const EpPtrs& P, int nr, int rank, void* out,
                        const float* topk_w, int ntok, int k, int H, int C, hipStream_t s);
 uint32_t ep_read_err(void* sig);

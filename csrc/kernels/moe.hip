@@ -59,8 +59,8 @@ __global__ __launch_bounds__(256) void moe_route_kernel(const T* __restrict__ lo
 }
 
 // ---------------------------------------------------------------------------- gate + route
-// The router GEMM (x [T, H] . Wg [E, H]^T, E <= 16) fused with moe_route: one wave per
-// token, each lane a 16-byte column chunk of H per pass (every expert's dot product in
+// The router GEMM (x [T, H] . Wg [E, H]^T, E <= 16) fused with moe_route: one workgroup
+// per token, each lane a 16-byte column chunk of H per pass (every expert's dot product in
 // registers, the 64 KB gate weight an L2 hit), a butterfly sum, then the logits -- rounded
 // to T, as the GEMM's output would be -- go through the same softmax / top-k as
 // moe_route_kernel.  At decode sizes this replaces a hipBLASLt launch that ran a 256 x 8
@@ -73,14 +73,19 @@ __global__ __launch_bounds__(256) void moe_gate_route_kernel(const T* __restrict
                                                              int renorm,
                                                              float* __restrict__ topk_w,
                                                              int* __restrict__ topk_ids) {
-  const int lane = threadIdx.x & 63;
-  const int t = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (t >= ntok) return;
+  // one workgroup per token: the 4 waves split the H dot product (interleaved 512-element
+  // strips, so each wave keeps both of its strips' loads in flight at H = 4096) and meet in
+  // LDS; wave 0 does the softmax / top-k.  One wave per token left 3/4 of the CUs idle at
+  // decode batch 256 and ran 8 dependent strips per wave.
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int t = blockIdx.x;
+  if (t >= ntok) return;                                  // workgroup-uniform
+  __shared__ float red[4][E];
   float acc[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) acc[e] = 0.f;
   const T* xr = x + (int64_t)t * ldx;
-  for (int c = lane * 8; c < H; c += 512) {
+  for (int c = (wave * 64 + lane) * 8; c < H; c += 2048) {
     Pack8<T> xv;
     xv.u = *reinterpret_cast<const u32x4*>(xr + c);
 #pragma unroll
@@ -94,6 +99,14 @@ __global__ __launch_bounds__(256) void moe_gate_route_kernel(const T* __restrict
   }
 #pragma unroll
   for (int e = 0; e < E; ++e) acc[e] = wave_sum(acc[e]);
+  if (lane == 0) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) red[wave][e] = acc[e];
+  }
+  __syncthreads();
+  if (wave != 0) return;
+#pragma unroll
+  for (int e = 0; e < E; ++e) acc[e] = red[0][e] + red[1][e] + red[2][e] + red[3][e];
   float v = -INFINITY;
 #pragma unroll
   for (int e = 0; e < E; ++e)
@@ -392,7 +405,8 @@ template <typename T>
 __global__ __launch_bounds__(256) void moe_combine_kernel(T* __restrict__ out,
                                                           const void* __restrict__ y,
                                                           const float* __restrict__ topk_w,
-                                                          int k, int H, int S,
+                                                          const int* __restrict__ row_map,
+                                                          int64_t nrows, int k, int H, int S,
                                                           int64_t slice_stride) {
   const int t = blockIdx.y;
   const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
@@ -400,7 +414,12 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(T* __restrict__ out,
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int j = 0; j < k; ++j) {
     const float w = topk_w[(int64_t)t * k + j];
-    const int64_t row = ((int64_t)t * k + j) * H + c;
+    // row_map: pair -> row of y (expert-sorted rows, no scatter back to pair order);
+    // -1 = the pair has no row (expert not local) and contributes nothing; rows past y's
+    // end are skipped the same way
+    const int64_t pr = row_map ? (int64_t)row_map[(int64_t)t * k + j] : (int64_t)t * k + j;
+    if (pr < 0 || pr >= nrows) continue;
+    const int64_t row = pr * H + c;
     if (S == 0) {
       Pack8<T> v;
       v.u = *reinterpret_cast<const u32x4*>(reinterpret_cast<const T*>(y) + row);
@@ -446,7 +465,7 @@ void launch_moe_route(int dtype, const void* logits, int64_t stride, int ntok, i
 void launch_moe_gate_route(int dtype, const void* x, int64_t ldx, const void* wg, int H, int E,
                            int ntok, int k, bool renorm, float* topk_w, int* topk_ids,
                            hipStream_t s) {
-  const dim3 grid((ntok + 3) / 4);
+  const dim3 grid(ntok);
 #define GR(TT, EE)                                                                          \
   moe_gate_route_kernel<TT, EE><<<grid, 256, 0, s>>>((const TT*)x, ldx, (const TT*)wg, H, E, \
                                                       ntok, k, renorm, topk_w, topk_ids)
@@ -589,14 +608,17 @@ void launch_splitk_reduce_silu(int dtype, void* out, const float* Cs, int S, int
   }
 }
 
-void launch_moe_combine(int dtype, void* out, const void* y, const float* topk_w, int ntok, int k,
-                        int H, int splitk, int64_t slice_stride, hipStream_t s) {
+void launch_moe_combine(int dtype, void* out, const void* y, const float* topk_w,
+                        const int* row_map, int64_t nrows, int ntok, int k, int H,
+                        int splitk, int64_t slice_stride, hipStream_t s) {
   const dim3 grid((H / 8 + 255) / 256, ntok);
   const int S = splitk > 1 ? splitk : 0;
   if (dtype == DT_BF16)
-    moe_combine_kernel<bf16><<<grid, 256, 0, s>>>((bf16*)out, y, topk_w, k, H, S, slice_stride);
+    moe_combine_kernel<bf16><<<grid, 256, 0, s>>>((bf16*)out, y, topk_w, row_map, nrows, k, H,
+                                                   S, slice_stride);
   else
-    moe_combine_kernel<f16><<<grid, 256, 0, s>>>((f16*)out, y, topk_w, k, H, S, slice_stride);
+    moe_combine_kernel<f16><<<grid, 256, 0, s>>>((f16*)out, y, topk_w, row_map, nrows, k, H,
+                                                  S, slice_stride);
 }
 
 }  // namespace kgc

@@ -11,9 +11,10 @@ Expert placement over the TP group (``--moe-parallel``):
 On the GPU the whole block is native and host-sync free (so decode graphs capture
 it): router GEMM -> ``moe_route`` (K13) -> ``moe_align`` bucketing -> grouped MFMA
 GEMM (gate/up, rows gathered) -> silu_mul (K7) -> grouped GEMM (down, rows
-scattered back) -> weighted ``moe_combine`` (csrc/kernels/moe.hip).  The CPU path
-(and shapes the grouped-GEMM tiles do not cover) sorts the pairs by expert and runs
-one GEMM pair per non-empty expert.  ``ep`` mode exchanges decode-size batches through
+scattered back) -> weighted ``moe_combine`` (csrc/kernels/moe.hip).  Prefill chunks
+(and shapes the grouped-GEMM tiles do not cover) sort the pairs by expert and run
+one GEMM pair per non-empty expert; on the GPU the combine reads the expert-sorted rows
+through the inverse permutation.  ``ep`` mode exchanges decode-size batches through
 the device-side all-to-all over xGMI peer memory (``parallel/expert_a2a.py``, captured
 in decode graphs); larger calls use an RCCL all_to_all with host-side counts.
 """
@@ -75,9 +76,10 @@ def grouped_expert_mlp(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor,
     tok = order // k
     if x.is_cuda and ops.moe_supported(H, w2.shape[2]):
         # GPU (prefill chunks): ONE row gather, the experts' GEMMs written straight into
-        # their sorted rows, ONE row scatter back to pair order and the weighted combine
-        # kernel -- instead of a gather, an fp32 up-cast, a scaling and an atomic
-        # index_add_ per expert (~40 ms of a Mixtral 16K-token chunk's 409 ms)
+        # their sorted rows, and the weighted combine kernel reading those rows through the
+        # inverse permutation (row_map) -- instead of a gather, an fp32 up-cast, a scaling and
+        # an atomic index_add_ per expert (~40 ms of a Mixtral 16K-token chunk's 409 ms), or
+        # a scatter back to pair order (index_put, 12 ms of the chunk)
         nv = sum(counts)
         xs = x[tok[:nv]]
         ys = torch.empty(nv, H, dtype=x.dtype, device=x.device)
@@ -87,11 +89,11 @@ def grouped_expert_mlp(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor,
                 h = ops.silu_mul(F.linear(xs[start:start + c], w13[e]))
                 torch.mm(h, w2[e].t(), out=ys[start:start + c])
             start += c
-        yp = (torch.empty if nv == T * k else torch.zeros)(T * k, H, dtype=x.dtype,
-                                                           device=x.device)
-        yp[order[:nv]] = ys
+        rows = torch.arange(T * k, dtype=torch.int32, device=x.device)
+        row_map = torch.empty_like(rows).scatter_(0, order, rows)
+        row_map = torch.where(row_map < nv, row_map, -1).to(torch.int32)
         out = torch.empty(T, H, dtype=x.dtype, device=x.device)
-        torch.ops.kgc.moe_combine(out, yp, topk_w.contiguous().float())
+        torch.ops.kgc.moe_combine(out, ys, topk_w.contiguous().float(), row_map)
         return out
     out = torch.zeros(T, H, dtype=torch.float32, device=x.device)
     start = 0
@@ -221,10 +223,14 @@ class MoEBlock(nn.Module):
         larger calls an RCCL all_to_all with host-side counts."""
         a2a = self.ep_a2a
         if a2a is not None and self.native and a2a.fits(x, topk_ids):
+            # the owner's receive slots hold ~T x k rows of its NR x C (this rank's own pair
+            # count, on average); the down projection's split-K slices go straight to
+            # ep_return, which sums them while writing the rows back
+            hint = topk_ids.numel()
             return a2a.forward(x, topk_w, topk_ids,
-                               lambda xs, w, ids, off: ops.fused_moe(xs, self.w13, self.w2, w,
-                                                                     ids, off, True, self.w13p,
-                                                                     self.w2p),
+                               lambda xs, w, ids, off: ops.fused_moe(
+                                   xs, self.w13, self.w2, w, ids, off, True, self.w13p,
+                                   self.w2p, rows_hint=hint, combine=False),
                                self.E_local)
         s = get_state()
         if getattr(s, "phantom", False):

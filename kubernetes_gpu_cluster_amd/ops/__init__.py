@@ -547,14 +547,22 @@ def moe_dgemm_splitk(npairs: int, E: int, N: int, K: int, bm: int, bn: int = 128
 def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torch.Tensor,
               topk_ids: torch.Tensor, expert_offset: int = 0,
               all_local: bool = True, w13p: Optional[torch.Tensor] = None,
-              w2p: Optional[torch.Tensor] = None) -> torch.Tensor:
+              w2p: Optional[torch.Tensor] = None, rows_hint: Optional[int] = None,
+              combine: bool = True) -> torch.Tensor:
     """K14: sum_j topk_w[t, j] * MLP_{topk_ids[t, j]}(x[t]) for the experts held here
     (global ids ``expert_offset .. expert_offset + w13.shape[0]``).  x [T, H];
     w13 [E, 2I, H] (gate rows then up rows); w2 [E, H, I].  No host synchronisation:
     bucket sizes stay on the device, so the block is captured in decode graphs.
     ``w13p`` / ``w2p`` (``moe_pack``): K14m -- both projections on the K9m LDS-DMA
     pipeline over packed per-expert tiles, the SiLU in the gate_up epilogue (no [rows, 2I]
-    intermediate, no silu_mul launch); else the register-staged grouped GEMM."""
+    intermediate, no silu_mul launch); else the register-staged grouped GEMM.
+
+    ``rows_hint``: the number of pairs expected to carry rows when ``topk_ids`` has room
+    for more (the EP owner's receive slots: NR x C slots, ~T x k of them used); it sizes
+    the row block and the down projection's split-K.  ``combine=False`` returns the down
+    projection's output per pair instead of the weighted sum -- [npairs, H] in x's dtype,
+    or its fp32 split-K slices [S, npairs, H] -- for a consumer that sums the slices
+    itself (``ep_return``)."""
     if not _gpu(x):
         return ref.moe_mlp_local(x, w13, w2, topk_w, topk_ids, expert_offset)
     k = _k()
@@ -562,9 +570,10 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     E, I2 = w13.shape[0], w13.shape[1]
     topk = topk_ids.shape[1]
     npairs = T * topk
+    used = min(npairs, rows_hint) if rows_hint else npairs
     packed = w13p is not None and w2p is not None
-    bm = int(os.environ.get("KGC_MOE_BM", 0)) or (moe_k14m_bm(npairs, E) if packed else
-                                                  (64 if npairs <= 40 * E else 128))
+    bm = int(os.environ.get("KGC_MOE_BM", 0)) or (moe_k14m_bm(used, E) if packed else
+                                                  (64 if used <= 40 * E else 128))
     if bm == 96 and not packed:
         bm = 128                    # the register-staged kernel has 64 / 128-row tiles only
     rows = (npairs + E * (bm - 1) + bm - 1) // bm * bm
@@ -580,13 +589,15 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
         k.moe_dgemm(act, x.contiguous(), w13p, sorted_ids, block_expert, meta, npairs, topk,
                     bm, 1, bn if I2 % bn == 0 else 128)
         bn2 = bn if H % bn == 0 else 128
-        S = moe_dgemm_splitk(npairs, E, H, I2 // 2, bm, bn2)
+        S = moe_dgemm_splitk(used, E, H, I2 // 2, bm, bn2)
         alloc = torch.empty if all_local else torch.zeros
         if S > 1:
             y = alloc(S, npairs, H, dtype=torch.float32, device=dev)
         else:
             y = alloc(npairs, H, dtype=x.dtype, device=dev)
         k.moe_dgemm(y, act, w2p, sorted_ids, block_expert, meta, npairs, topk, bm, 2, bn2)
+        if not combine:
+            return y
         out = torch.empty(T, H, dtype=x.dtype, device=dev)
         k.moe_combine(out, y, topk_w.contiguous().float())
         return out
@@ -594,13 +605,15 @@ def fused_moe(x: torch.Tensor, w13: torch.Tensor, w2: torch.Tensor, topk_w: torc
     k.moe_gemm(inter, x.contiguous(), w13, sorted_ids, block_expert, meta, npairs, topk, bm,
                True, False)
     act = silu_mul(inter)
-    S = moe_splitk(npairs, E, H, w2.shape[2], bm)
+    S = moe_splitk(used, E, H, w2.shape[2], bm)
     alloc = torch.empty if all_local else torch.zeros   # EP: pairs of remote experts add 0
     if S > 1:
         y = alloc(S, npairs, H, dtype=torch.float32, device=dev)
     else:
         y = alloc(npairs, H, dtype=x.dtype, device=dev)
     k.moe_gemm(y, act, w2, sorted_ids, block_expert, meta, npairs, topk, bm, False, True, S)
+    if not combine:
+        return y
     out = torch.empty(T, H, dtype=x.dtype, device=dev)
     k.moe_combine(out, y, topk_w.contiguous().float())
     return out

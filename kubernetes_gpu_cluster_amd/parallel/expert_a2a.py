@@ -84,7 +84,8 @@ class ExpertAllToAll:
                 experts, E_local: int) -> torch.Tensor:
         """sum_j topk_w[t, j] * expert_{topk_ids[t, j]}(x[t]) with the experts spread over
         the EP ranks; ``experts(x_local, ones, ids, expert_offset)`` is the owner's grouped
-        MLP (rows whose id is not local come back as zeros and are never returned)."""
+        MLP: one row per receive slot ([NR * C, H] in x's dtype) or fp32 split-K slices of
+        it ([S, >= NR * C, H], summed by ep_return); rows of empty slots are never read."""
         k = torch.ops.kgc
         ids = topk_ids.to(torch.int32).contiguous()
         k.ep_dispatch(x.contiguous(), ids, self.data, self.sig, self.rank, E_local, self.C)
@@ -95,7 +96,7 @@ class ExpertAllToAll:
         k.ep_receive(x_local, sids, route, self.data, self.sig, self.rank, E_local, self.C)
         ones = torch.ones(slots, 1, dtype=torch.float32, device=x.device)
         y = experts(x_local, ones, sids.view(slots, 1), self.rank * E_local)
-        k.ep_return(y.contiguous(), route, self.data, self.sig, self.rank, self.C)
+        k.ep_return(y.contiguous(), route, self.data, self.sig, self.rank, self.C, x.dtype)
         out = torch.empty_like(x)
         k.ep_combine(out, topk_w.float().contiguous(), self.data, self.sig, self.rank, self.C)
         return out

@@ -1,7 +1,9 @@
 """Device-side expert-parallel all-to-all over IPC peer memory (csrc/kernels/ep_a2a.hip,
 parallel/expert_a2a.py) == the MoE block with every expert local, eager and replayed
 from a hipGraph.  Two EP ranks share cuda:0 (gloo process group, as in the xGMI
-all-reduce tests): the puts, flags and parity buffers run exactly as across GPUs."""
+all-reduce tests): the puts, flags and parity buffers run exactly as across GPUs.
+Parametrised over the owner's grouped MLP: register-staged or K14m-packed experts, and
+a forced down-projection split-K whose fp32 slices ep_return sums on the way back."""
 import os
 import socket
 
@@ -18,10 +20,12 @@ def _port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port):
+def _worker(rank, world, port, packed, splitk):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), KGC_DIST_BACKEND="gloo")
+    if splitk:
+        os.environ["KGC_MOE_SPLITK"] = splitk
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     from kubernetes_gpu_cluster_amd import ops
@@ -44,6 +48,8 @@ def _worker(rank, world, port):
     blk.w13.data.copy_(w13[e0:e0 + El])
     blk.w2.data.copy_(w2[e0:e0 + El])
     blk.gate.weight.data.copy_(gate)
+    if packed:
+        assert blk.pack_experts() > 0
     ps = get_state()
     a2a = ExpertAllToAll(ps.tp_cpu_group, ps.tp_rank, ps.tp_size, dev, 64 * blk.k, H,
                          torch.bfloat16)
@@ -83,5 +89,7 @@ def _worker(rank, world, port):
         destroy_parallel()
 
 
-def test_expert_a2a_matches_local_experts(gpu):
-    mp.start_processes(_worker, args=(2, _port()), nprocs=2, join=True, start_method="spawn")
+@pytest.mark.parametrize("packed,splitk", [(False, None), (True, "2"), (False, "2")])
+def test_expert_a2a_matches_local_experts(gpu, packed, splitk):
+    mp.start_processes(_worker, args=(2, _port(), packed, splitk), nprocs=2, join=True,
+                       start_method="spawn")

@@ -642,6 +642,36 @@ def test_fused_moe_expert_subset(gpu):
     torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(torch.bfloat16))
 
 
+@pytest.mark.parametrize("T,lo", [(1, 0), (257, 0), (2048, 0), (300, 4), (1, 4)])
+def test_grouped_expert_mlp_row_map_combine(gpu, T, lo):
+    """The prefill-size MoE path (models/moe.grouped_expert_mlp: one GEMM pair per expert
+    over the expert-sorted rows, the weighted combine reading them through the inverse
+    permutation, pairs of non-local experts mapped to -1) == the fp32 reference."""
+    from kubernetes_gpu_cluster_amd.models.moe import grouped_expert_mlp
+    x, w13, w2, tw, tid = _moe_case(torch.bfloat16, T, 8, 2, 512, 384, gpu, seed=T + lo)
+    out = grouped_expert_mlp(x, w13[lo:].contiguous(), w2[lo:].contiguous(), tw, tid, lo)
+    exp = ref.moe_mlp_local(x.cpu(), w13[lo:].cpu(), w2[lo:].cpu(), tw.cpu(), tid.cpu(), lo)
+    torch.testing.assert_close(out.cpu().float(), exp.float(), **_tol(torch.bfloat16))
+
+
+def test_moe_combine_row_map_bounds(gpu):
+    """moe_combine's row map: -1 and indices past y's rows contribute nothing."""
+    T, k, H = 4, 2, 256
+    y = torch.randn(3, H, device=gpu).to(torch.bfloat16)
+    w = torch.rand(T, k, device=gpu)
+    rm = torch.tensor([0, -1, 2, 1, 7, -1, 1, 3], dtype=torch.int32, device=gpu)
+    out = torch.empty(T, H, dtype=torch.bfloat16, device=gpu)
+    torch.ops.kgc.moe_combine(out, y, w, rm)
+    yf, wc, rc = y.float().cpu(), w.cpu(), rm.cpu().view(T, k)
+    exp = torch.zeros(T, H)
+    for t in range(T):
+        for j in range(k):
+            r = int(rc[t, j])
+            if 0 <= r < 3:
+                exp[t] += wc[t, j] * yf[r]
+    torch.testing.assert_close(out.float().cpu(), exp, atol=2e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("S", [1, 3, 8])
 @pytest.mark.parametrize("T,all_local", [(5, True), (300, True), (40, False)])
 def test_fused_moe_splitk(gpu, monkeypatch, S, T, all_local):
