@@ -28,10 +28,14 @@ namespace kgc {
 constexpr int EP_MAX_RANKS = 8;
 constexpr int EP_THREADS = 512;
 constexpr int EP_WAVES = EP_THREADS / 64;
-// one wave per row (pair / slot / token): 1,024 rows in flight.  One workgroup per row over
-// 64 workgroups walked the 4,096 receive slots 64 deep, a dependent route / count load per
-// step (~20 us per phase at Mixtral's EP = 8 decode shapes)
-constexpr int EP_BLOCKS = 128;
+// dispatch / receive / return: one wave per row (pair / slot), 512 rows in flight.  One
+// workgroup per row walked the 4,096 receive slots 64 deep, a dependent route / count load
+// per step (~20 us per phase at Mixtral's EP = 8 decode shapes).  The grid stays at 64
+// workgroups: each one that publishes pays a system-scope fence and a serialised atomic
+// on the uncached signal (128 workgroups measured slower for dispatch / return)
+constexpr int EP_BLOCKS = 64;
+// the combine publishes nothing and runs a workgroup per token
+constexpr int EP_COMBINE_BLOCKS = 128;
 constexpr int EP_MAX_PAIRS = 4096;   // T * k of one call (decode buckets)
 
 struct EpSignal {
@@ -282,9 +286,10 @@ __global__ __launch_bounds__(EP_THREADS) void ep_combine_kernel(
   ep_wait_all<NR>(P, rank, 1, epoch);
   const T* ret = reinterpret_cast<const T*>(reinterpret_cast<const char*>(P.data[rank]) + L.ret);
   const int nv = H >> 3;
-  const int lane = threadIdx.x & 63;
-  for (int t = blockIdx.x * EP_WAVES + (threadIdx.x >> 6); t < ntok; t += gridDim.x * EP_WAVES)
-    for (int v = lane; v < nv; v += 64) {
+  // a workgroup per token (the whole row in one pass at H = 4096): ntok is only T here, so
+  // a wave per token would leave most of the grid idle
+  for (int t = blockIdx.x; t < ntok; t += gridDim.x)
+    for (int v = threadIdx.x; v < nv; v += EP_THREADS) {
       float acc[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] = 0.f;
@@ -387,7 +392,7 @@ template <typename T>
 static void ep_combine_t(const EpPtrs& P, int nr, int rank, void* out, const float* topk_w,
                          int ntok, int k, int H, int C, hipStream_t s) {
 #define KGC_EPC(NR)                                                                          \
-  ep_combine_kernel<T, NR><<<EP_BLOCKS, EP_THREADS, 0, s>>>(P, rank, (T*)out, topk_w, ntok, k, \
+  ep_combine_kernel<T, NR><<<EP_COMBINE_BLOCKS, EP_THREADS, 0, s>>>(P, rank, (T*)out, topk_w, ntok, k, \
                                                              H, C)
   KGC_EP_RANKS(nr, KGC_EPC)
 #undef KGC_EPC

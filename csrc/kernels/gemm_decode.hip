@@ -122,7 +122,7 @@ static int partial_wt() {
 // (sorted_ids[r] / topk), 2 = the grouped down, output rows scattered to pair order; the
 // workgroup's row block names its expert (block_expert), whose packed weights it streams.
 template <typename T, int BM, int BN, int EPI, bool PK, int ABL = ABL_NONE, int LDW = 0,
-          int WN = 2, int MOE = 0>
+          int WN = 2, int MOE = 0, int NS = DG_NS>
 __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
     void* __restrict__ Cv, const T* __restrict__ X, const T* __restrict__ W, int M, int N,
     int K, int64_t ldx, int S, int MB, int64_t slice_stride, int xmap, int wt, DgAux aux) {
@@ -138,10 +138,10 @@ __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
   static_assert(PA % NIW == 0 && (PK || PB % NIW == 0), "DMA split");
   constexpr int L = LA + LB;
   constexpr int A_BYTES = BM * DG_ROWB, SLOT_BYTES = (BM + BN) * DG_ROWB;
-  static_assert(DG_NS * SLOT_BYTES <= 163840, "LDS ring exceeds 160 KiB");
+  static_assert(NS >= 3 && NS <= 6 && NS * SLOT_BYTES <= 163840, "LDS ring: 3..6 slots, 160 KiB");
   // ONE shared array for the whole ring (a second __shared__ object can make hipcc emit a
   // vmcnt(0) before the first ds_read of every step)
-  __shared__ __attribute__((aligned(16))) char lds[DG_NS * SLOT_BYTES];
+  __shared__ __attribute__((aligned(16))) char lds[NS * SLOT_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool loader = LDW > 0 && wave >= 8;
@@ -266,26 +266,29 @@ __global__ __launch_bounds__(DG_THREADS + LDW * 64, 1) void dgemm_kernel(
     }
   }
 
-  issue(0, 0);
-  if (nk > 1) issue(1, 1);
+  // NS-slot ring: NS - 1 steps issued ahead, NS - 2 of them in flight behind the one read
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < nk) issue(p, p);
   int slot = 0;
   for (int it = 0; it < nk; ++it) {
-    // step `it` must have landed; step it + 1 (if issued) may stay in flight
+    // step `it` must have landed; the (up to NS - 2) younger steps may stay in flight
     if (LDW > 0 && !loader) {
       // MFMA waves have no DMAs of their own: the barrier below orders them after the
       // loaders' waits
     } else if constexpr (ABL == ABL_NO_A) {
-      if (it + 1 < nk) wait_vm<LB>(); else wait_vm<0>();
+      wait_younger<LB, NS - 2>(nk - 1 - it);
     } else if constexpr (ABL == ABL_NO_B) {
-      if (it + 1 < nk) wait_vm<LA>(); else wait_vm<0>();
+      wait_younger<LA, NS - 2>(nk - 1 - it);
     } else if constexpr (ABL != ABL_NO_DMA) {
-      if (it + 1 < nk) wait_vm<L>(); else wait_vm<0>();
+      wait_younger<L, NS - 2>(nk - 1 - it);
     }
     __builtin_amdgcn_s_barrier();
-    if (it + 2 < nk) issue(slot == 0 ? 2 : slot - 1, it + 2);
+    // the slot read in iteration it - 1 (every wave has passed the barrier since)
+    if (it + NS - 1 < nk) issue(slot == 0 ? NS - 1 : slot - 1, it + NS - 1);
     const char* sa = lds + slot * SLOT_BYTES;
     const char* sb = sa + A_BYTES;
-    slot = slot == DG_NS - 1 ? 0 : slot + 1;
+    slot = slot == NS - 1 ? 0 : slot + 1;
     if constexpr (ABL == ABL_NO_MFMA) continue;
     if (!consumer) continue;
 #pragma unroll
@@ -553,15 +556,22 @@ __global__ __launch_bounds__(256) void dgemm_pack_kernel(T* __restrict__ P,
 // the SiLU epilogue (gate_up at S = 1, 256 workgroups) and 128 x 192: filling all 256 CUs
 // did not beat the 192 / 224-workgroup 256 x 128 tiles at M = 256 (the extra activation
 // re-reads of narrower tiles cost more than the idle CUs: profiles/k9m_full_grid_r6.jsonl).
+// Also measured and not kept: 64-row blocks over the whole K (no split-K partials), the
+// four row blocks of a column tile XCD-grouped, with a 3- or 6-slot ring (NS): 64 x 128 /
+// 64 x 96 qkv 35.0 / 36.3 us against 28.0 us for 256 x 128 at S = 5 with its reduction,
+// o 25.9-27.1 against 23.6, down 72-121 against 42.9 (profiles/k9m_64row_fullk_r6.jsonl):
+// every workgroup then takes in a whole-K strip of weights AND activations, and the
+// per-CU intake (bytes in flight / latency), not HBM, is what bounds K9m at M = 256.
 struct DgCfg {
-  int bm, bn, pk, ldw, wn, xmap;
+  int bm, bn, pk, ldw, wn, xmap, ns;
 };
 constexpr int kNumCfgs = 15;
 static const DgCfg kCfg[kNumCfgs] = {
-    {256, 128, 0, 0, 2, 0}, {256, 64, 0, 0, 2, 0}, {128, 128, 0, 0, 2, 0}, {128, 64, 0, 0, 2, 0},
-    {256, 128, 1, 0, 2, 0}, {128, 128, 1, 0, 2, 0}, {256, 128, 1, 4, 2, 0}, {128, 128, 1, 4, 2, 0},
-    {256, 128, 1, 0, 2, 0}, {128, 128, 1, 0, 2, 0}, {128, 128, 1, 0, 2, 1},
-    {256, 64, 1, 0, 2, 0},  {256, 80, 1, 4, 1, 0},  {256, 112, 1, 4, 1, 0}, {128, 64, 1, 0, 2, 1}};
+    {256, 128, 0, 0, 2, 0, 3}, {256, 64, 0, 0, 2, 0, 3}, {128, 128, 0, 0, 2, 0, 3},
+    {128, 64, 0, 0, 2, 0, 3},  {256, 128, 1, 0, 2, 0, 3}, {128, 128, 1, 0, 2, 0, 3},
+    {256, 128, 1, 4, 2, 0, 3}, {128, 128, 1, 4, 2, 0, 3}, {256, 128, 1, 0, 2, 0, 3},
+    {128, 128, 1, 0, 2, 0, 3}, {128, 128, 1, 0, 2, 1, 3}, {256, 64, 1, 0, 2, 0, 3},
+    {256, 80, 1, 4, 1, 0, 3},  {256, 112, 1, 4, 1, 0, 3}, {128, 64, 1, 0, 2, 1, 3}};
 
 // epilogues a tile runs: bit EPI (PARTIAL / OUT always; SILU where each wave holds whole
 // gate / up 16-column pairs)
@@ -571,7 +581,7 @@ constexpr int dg_epis() {
          ((BN % 32 == 0 && (BN / WN / 16) % 2 == 0) ? (1 << EPI_SILU) : 0);
 }
 
-template <typename T, int BM, int BN, bool PK, int LDW = 0, int WN = 2>
+template <typename T, int BM, int BN, bool PK, int LDW = 0, int WN = 2, int NS = DG_NS>
 void dgemm_cfg(int epi, void* C, const void* X, const void* W, int M, int N, int K, int64_t ldx,
                int S, int64_t ss, const DgAux& aux, hipStream_t s, int xmap = 0) {
   const int MB = (M + BM - 1) / BM;
@@ -580,7 +590,8 @@ void dgemm_cfg(int epi, void* C, const void* X, const void* W, int M, int N, int
   const int xm = (xmap && MB > 1 && 8 % S == 0 && (N / BN) % (8 / S) == 0) ? 1 : 0;
   constexpr int E = dg_epis<BN, WN>();
 #define DG_LAUNCH(EP)                                                                       \
-  dgemm_kernel<T, BM, BN, EP, PK, ABL_NONE, LDW, WN><<<grid, DG_THREADS + LDW * 64, 0, s>>>( \
+  dgemm_kernel<T, BM, BN, EP, PK, ABL_NONE, LDW, WN, 0, NS>                                 \
+      <<<grid, DG_THREADS + LDW * 64, 0, s>>>(                                              \
       C, (const T*)X, (const T*)W, M, N, K, ldx, S, MB, ss, xm, partial_wt(), aux)
   if (epi == EPI_PARTIAL) DG_LAUNCH(EPI_PARTIAL);
   else if (epi == EPI_OUT) DG_LAUNCH(EPI_OUT);

@@ -998,7 +998,7 @@ def test_tune_skinny_times_norm_free_epilogues(gpu):
 @pytest.mark.parametrize("cfg", list(range(15)))
 @pytest.mark.parametrize("M,N,K", [(256, 1024, 4096), (200, 768, 1024), (77, 512, 2048),
                                    (130, 256, 128), (256, 1280, 1024), (200, 1792, 512),
-                                   (96, 896, 256)])
+                                   (96, 896, 256), (256, 1536, 2048)])
 def test_dgemm_matches_fp32(gpu, cfg, M, N, K):
     """K9m decode GEMM (every tile config, packed and row-major weights) vs an fp32
     matmul: bf16 output (S = 1), fp32 split-K slices (S = 2, 3, 4, 5: uneven K ranges at 3

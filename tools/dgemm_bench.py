@@ -64,6 +64,8 @@ def main():
                     help="cfg:S:epi -- time just this configuration (profiling runs)")
     ap.add_argument("--no-lib", action="store_true", help="skip the hipBLASLt baseline")
     ap.add_argument("--cfgs", default=None, help="comma list: only these tile configs")
+    ap.add_argument("--reduce", action="store_true",
+                    help="time split-K candidates with their splitk_reduce to bf16")
     ap.add_argument("--max-grid", type=int, default=264,
                     help="skip split-K candidates with more workgroups than this")
     ap.add_argument("--ablate", default=None,
@@ -158,12 +160,17 @@ def main():
                 err = ((got - want).abs().max() / want.abs().max().clamp_min(1e-6)).item()
                 ok = err < 2e-2
 
-                def run(C=C, cid=cid, epi=epi, wl=wl):
+                red = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+
+                def run(C=C, cid=cid, epi=epi, wl=wl, red=red):
                     for w in wl:
                         k.dgemm(C, x, w, cid, epi)
+                        if epi == 0 and a.reduce:
+                            k.splitk_reduce(red, C)
                 t = bench(run, max(1, 64 // copies)) / copies
                 print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "kernel": "k9m",
                                   "cfg": cid, "bm": bm, "bn": bn, "packed": pk, "S": S, "epi": epi,
+                                  "with_reduce": bool(a.reduce and epi == 0),
                                   "us": round(t * 1e6, 2), "w_TBps": round(wb / t / 1e12, 2),
                                   "TFLOPs": round(2 * M * N * K / t / 1e12, 1),
                                   "rel_err": float(f"{err:.2e}"), "ok": ok}), flush=True)
