@@ -225,6 +225,7 @@ def main_engine(args):
     # the all-reduce policy this node's start-up calibration chose (read before shutdown
     # releases the xGMI buffers)
     ar_cal = getattr(comm.get_custom_allreduce(), "calibration", None)
+    host_t = engine.host_timing() if is_driver and hasattr(engine, "host_timing") else None
     if is_driver:
         engine.shutdown()
     # aggregate over replicas (drivers) -- every rank participates in the collectives
@@ -258,6 +259,7 @@ def main_engine(args):
             "k9_skinny_gemm_shapes": len(_k9_plan()),
             "k9m_gemm_shapes": len(_k9m_plan()),
             "k9m_plan_max_m": _k9m_top(),
+            **({"host_us_per_step": host_t} if host_t else {}),
             "config": {"model": args.model, "global_batch": args.num_prompts * replicas,
                        "seq_len": args.input_len + args.output_len, "input_len": args.input_len,
                        "output_len": args.output_len,

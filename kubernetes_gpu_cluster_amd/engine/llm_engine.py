@@ -9,6 +9,7 @@ max_model_len) finish sequences and free their KV blocks.
 """
 from __future__ import annotations
 
+import collections
 import itertools
 import logging
 import os
@@ -109,6 +110,8 @@ class LLMEngine:
         self._inflight = None
         self._debug = os.environ.get("KGC_DEBUG", "0") == "1"
         self._prof = _StepProfiler.from_env()
+        self._host_t = (collections.defaultdict(float)
+                        if os.environ.get("KGC_HOST_TIMING", "0") == "1" else None)
         self.init_s = time.time() - t0
         log.info("engine ready: %d KV blocks x %d tokens, graphs %.1fs", nb, cfg.block_size,
                  self.graph_s)
@@ -161,16 +164,46 @@ class LLMEngine:
         if not self.async_mode:
             return self._step_sync()
         launched = None
+        ht = self._host_t
+        h0 = time.perf_counter() if ht is not None else 0.0
         batch = self.scheduler.schedule()
         if not batch.is_empty:
             t0 = time.monotonic()
+            h1 = time.perf_counter() if ht is not None else 0.0
             plan, samplers = self.executor.runner.build_plan(batch.prefills, batch.decodes,
                                                              self.bm.table, device_tokens=True)
+            h2 = time.perf_counter() if ht is not None else 0.0
             fut = self.executor.execute_async(plan)
+            h3 = time.perf_counter() if ht is not None else 0.0
             launched = self._launched(batch, plan, samplers, fut, t0)
-        outs = self._process(self._inflight) if self._inflight is not None else []
+            if ht is not None:
+                ht["schedule"] += h1 - h0
+                ht["build_plan"] += h2 - h1
+                ht["launch"] += h3 - h2
+                h0 = time.perf_counter()
+        if self._inflight is not None:
+            if ht is not None:
+                w0 = time.perf_counter()
+                self._inflight[0].result()
+                ht["wait"] += time.perf_counter() - w0
+                h0b = time.perf_counter()
+            outs = self._process(self._inflight)
+            if ht is not None:
+                ht["process"] += time.perf_counter() - h0b
+                ht["steps"] += 1
+        else:
+            outs = []
         self._inflight = launched
         return outs
+
+    def host_timing(self) -> Optional[dict]:
+        """KGC_HOST_TIMING=1: seconds the host spent per engine step in scheduling,
+        building the step plan, launching (upload + graph replay + sampler enqueue),
+        waiting for the previous step's tokens, and processing them (async mode)."""
+        if self._host_t is None:
+            return None
+        n = max(1, self._host_t["steps"])
+        return {k: (round(v / n * 1e6, 1) if k != "steps" else v) for k, v in self._host_t.items()}
 
     def _step_pipelined(self) -> list[RequestOutput]:
         """PP > 1: micro-batch v = this step's turn.  Its previous step's tokens are read

@@ -419,15 +419,24 @@ def dg_table_path(model: str, tp: int = 1) -> str:
 
 
 def dg_fingerprint() -> dict:
-    """What an offline K9m table's (cfg, S) picks depend on: the GPU architecture and
-    device name, and the id -> tile map of the loaded kernel library (ids index kCfg in
-    gemm_decode.hip; a renumbered or retiled id would silently mean another kernel)."""
+    """What an offline K9m table's (cfg, S) picks depend on: the GPU architecture and its
+    compute-unit count, and the id -> tile map of the loaded kernel library (ids index kCfg
+    in gemm_decode.hip; a renumbered or retiled id would silently mean another kernel).
+    The marketing name is recorded (``device``) but not compared: it comes from libdrm's
+    amdgpu.ids, which the same MI355X resolves differently with and without rocprofv3
+    preloaded ("AMD Radeon Graphics" vs the product name), and a run under the profiler
+    then dropped the table and profiled other kernels than the service runs."""
     from . import _k
     props = torch.cuda.get_device_properties(torch.cuda.current_device())
     n = int(_k().dgemm_num_cfgs())
     return {"arch": str(getattr(props, "gcnArchName", "")).split(":")[0], "device": props.name,
+            "cus": int(props.multi_processor_count),
             "num_cfgs": n, "cfgs": [list(_dg_info(c)[:2]) + [int(_dg_info(c)[2])]
                                     for c in range(n)]}
+
+
+# fingerprint keys that must match (``device`` is informational, see dg_fingerprint)
+_DG_FP_KEYS = ("arch", "cus", "num_cfgs", "cfgs")
 
 
 def load_dg_table(model: str, tp: int = 1) -> int:
@@ -448,8 +457,8 @@ def load_dg_table(model: str, tp: int = 1) -> int:
     if fp is None:
         log.warning("K9m: %s has no fingerprint; ignored (start-up tuning runs)", path)
         return 0
-    if fp != cur:
-        diff = sorted(k for k in set(fp) | set(cur) if fp.get(k) != cur.get(k))
+    diff = sorted(k for k in _DG_FP_KEYS if fp.get(k) != cur.get(k))
+    if diff:
         log.warning("K9m: %s was tuned for another GPU or kernel library (%s differ); "
                     "ignored, start-up tuning runs", path, ", ".join(diff))
         return 0

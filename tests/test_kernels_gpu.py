@@ -1374,7 +1374,7 @@ def test_sampler_health_async_steps_keep_their_flags(gpu):
 
 def test_dg_table_fingerprint_guards_stale_tables(gpu, tmp_path, monkeypatch):
     """an offline K9m table is trusted only when its fingerprint (GPU arch and
-    name, the library's tile-config list) matches the running build; a mismatching or
+    CU count, the library's tile-config list) matches the running build; a mismatching or
     unfingerprinted table is dropped whole (start-up tuning runs), and an entry whose tile
     does not divide its N or whose split exceeds K / 64 is dropped alone."""
     import json
@@ -1396,6 +1396,13 @@ def test_dg_table_fingerprint_guards_stale_tables(gpu, tmp_path, monkeypatch):
         assert gemm.load_dg_table("x") == 0
         path.write_text(json.dumps({"fingerprint": dict(fp, arch="gfx942"), "entries": ent}))
         assert gemm.load_dg_table("x") == 0
+        path.write_text(json.dumps({"fingerprint": dict(fp, cus=fp["cus"] // 2), "entries": ent}))
+        assert gemm.load_dg_table("x") == 0
+        # the marketing name is informational: libdrm resolves it differently under
+        # rocprofv3, and a profiled run must load the same table as the service runs
+        path.write_text(json.dumps({"fingerprint": dict(fp, device="AMD Radeon Graphics (x)"),
+                                    "entries": ent}))
+        assert gemm.load_dg_table("x") == 3
         path.write_text(json.dumps({"entries": ent}))
         assert gemm.load_dg_table("x") == 0
         # the committed table matches this library

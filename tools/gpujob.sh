@@ -23,6 +23,7 @@
 #   dgemm8    K9m microbench at M = 256 on the Llama-3-70B TP = 8 shard shapes
 #   prof_mix  rocprofv3 anatomy of one Mixtral 8x7B engine wave (DETAIL=1)
 #   phantom_mix  Mixtral 8x7B EP = 8 rank-0 stand-in (one GPU), engine mode + anatomy
+#   py        python $PY (a probe / microbench; limit $PYT seconds, default 300)
 set -o pipefail
 TAG="${TAG:-job}"
 K="${K:-}"
@@ -50,6 +51,7 @@ for r in "$@"; do
     b70)     steps+=("b70|1100|env $ENVS python bench.py --model llama-3-70b --steps 1 --warmup 1 > ${O}_b70.json 2> ${O}_b70.err") ;;
     mixtral) steps+=("mixtral|1000|env $ENVS python bench.py --model mixtral-8x7b --steps 1 --warmup 1 > ${O}_mixtral.json 2> ${O}_mixtral.err") ;;
     phantom) steps+=("phantom|600|env $ENVS KGC_TP_PHANTOM=8 DETAIL=1 bash tools/profile.sh /tmp/ph_${TAG} -- python bench.py --mode engine --model llama-3-70b --steps 1 --warmup 1 > ${O}_phantom.log 2>&1 && cp /tmp/ph_${TAG}/summary.txt ${O}_phantom_summary.txt") ;;
+    py)      steps+=("py|${PYT:-300}|python $PY > ${O}_py.jsonl 2> ${O}_py.err") ;;
     *) echo "unknown recipe $r" >&2; exit 2 ;;
   esac
 done

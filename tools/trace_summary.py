@@ -105,6 +105,41 @@ def main():
             agg.update(s[3])
         for k, v in agg.most_common(16):
             print(f"   {k:38} {v / len(dec) / 1e3:9.1f} us/step")
+        # where the span - busy time goes: the lead gap (previous step's sampler -> this
+        # step's first kernel: host-side scheduling / launch) and the gaps between the
+        # step's own kernels, summed per (previous family -> next family) boundary
+        lead, inner = [], []
+        sites = collections.Counter()
+        for a, b in zip(samp, samp[1:]):
+            seg = ev[a + 1:b + 1]
+            if len(seg) != nk:
+                continue
+            lead.append(max(0, seg[0][0] - ev[a][1]))
+            g = 0
+            for (s0, e0, n0), (s1, e1, n1) in zip(seg, seg[1:]):
+                d = max(0, s1 - e0)
+                g += d
+                sites[(family(n0), family(n1))] += d
+            inner.append(g)
+        if lead:
+            print(f"gaps: lead (host) median {statistics.median(lead) / 1e3:.1f} us, "
+                  f"between the step's kernels median {statistics.median(inner) / 1e3:.1f} us")
+            for (f0, f1), v in sites.most_common(8):
+                print(f"   {f0[:30]:30} -> {f1[:30]:30} {v / len(lead) / 1e3:8.1f} us/step")
+            # one steady-state step's first and last kernels: offset from the previous
+            # sampler's end, duration and the gap before each
+            mid = [(a, b) for a, b in zip(samp, samp[1:]) if b - a == nk]
+            if mid:
+                a, b = mid[len(mid) // 2]
+                seg = ev[a + 1:b + 1]
+                t0, prev = ev[a][1], ev[a][1]
+                print("one decode step (offset us, dur us, gap before us, kernel):")
+                for i, (s, e, n) in enumerate(seg):
+                    if i < 10 or i >= len(seg) - 4:
+                        print(f"   {(s - t0) / 1e3:9.1f} {(e - s) / 1e3:7.1f} {(s - prev) / 1e3:7.1f}  {n[:70]}")
+                    elif i == 10:
+                        print("   ...")
+                    prev = e
         if "--detail" in sys.argv:
             # per kernel instantiation (template arguments kept): calls per step, us per call
             # an instantiation called k times per layer (o and down share one) is split by
