@@ -21,6 +21,7 @@
 //   V^T [D][64 keys]   chunk c of dim d stored at c ^ ((d>>1)&7)
 #include "common.h"
 #include "launch.h"
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -507,9 +508,236 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_gqa_kernel(
   }
 }
 
+// Persistent GQA variant: ONE workgroup per CU walks the work list (items = (128-row work
+// item, kv-head group, QB-row sub-block), heaviest first, dealt round-robin), with the K / V
+// tile stream running ACROSS items: the last tile of an item loads the next item's first
+// tile into the free LDS buffer, so a new item starts with its tile already staged.
+// Per-wave math, tile order and rounding are those of prefill_attn_gqa_kernel (results are
+// bit-identical).  Why: at short prompts every workgroup of the one-shot grid paid its own
+// pipeline fill -- the work_seq -> qsl / seq_lens -> block table -> K / V chain of dependent
+// loads, the q load and the first LDS store, ~10 us -- against 1-8 tiles of ~2.5 us of
+// work each (32 x 512 causal: 8 workgroups per CU, 0.40 PF/s against 0.84 PF/s at 16K).
+template <typename T, int D, bool KV8, int GH>
+__global__ __launch_bounds__(512, 1) void prefill_attn_gqa_persist_kernel(
+    const T* __restrict__ q, T* __restrict__ out, const void* __restrict__ kc_,
+    const void* __restrict__ vc_, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ qsl, const int* __restrict__ seq_lens,
+    const int* __restrict__ work_seq, const int* __restrict__ work_mblk, int nq, int nkv,
+    int bs_log2, float scale_log2, float v_scale, int num_blocks, int64_t q_stride,
+    const float* __restrict__ cos_sin, int cs_rows, int n_items) {
+  typedef typename Vec8<T>::type V8;
+  typedef std::conditional_t<KV8, uint8_t, T> C;
+  typedef std::conditional_t<KV8, u32x2, u32x4> R;
+  const C* __restrict__ kc = reinterpret_cast<const C*>(kc_);
+  const C* __restrict__ vc = reinterpret_cast<const C*>(vc_);
+  auto widen = [](R r) -> u32x4 {
+    if constexpr (KV8) return fp8x8_widen<T>(r);
+    else return r;
+  };
+  constexpr int NT_ = 512;
+  constexpr int QB = 256 / GH;
+  constexpr int ZS = PF_BM / QB;                       // sub-blocks per 128-row work item
+  constexpr int NCH = D / 8, KS = D / 32, DT = D / 16;
+  constexpr int KPT = PF_BN * NCH / NT_;
+  constexpr int VPT = D * (PF_BN / 8) / NT_;
+  constexpr int TILE = PF_BN * D;
+  static_assert(KPT * NT_ == PF_BN * NCH && VPT * NT_ == D * (PF_BN / 8), "staging split");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* lds = reinterpret_cast<T*>(smem);
+
+  const int G = nq / nkv;
+  const int Y = nkv * (G / GH);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r16 = lane & 15, qd = lane >> 4;
+  const int bsm = (1 << bs_log2) - 1;
+  const int64_t hs = (int64_t)D << bs_log2;
+  const int cap = bt_stride << bs_log2;
+
+  // an item's workgroup-uniform geometry (scalar registers); the per-wave values (q-head,
+  // first row, last tile) are derived for the current item only (VGPRs are the limit
+  // here: 256 at one workgroup of 8 waves per CU)
+  struct Item {
+    int q0, qlen, L, ctx0, qbase, hg0, h, n_tiles;
+    const int* bt;
+  };
+  // item idx -> its geometry; false: nothing to do (empty / out-of-range sub-block)
+  auto decode = [&](int idx, Item& I) -> bool {
+    const int w = idx / (Y * ZS), r = idx - w * (Y * ZS);
+    const int y = r / ZS, z = r - y * ZS;
+    const int seq = work_seq[w], mb = work_mblk[w];
+    I.h = y / (G / GH);
+    I.hg0 = I.h * G + (y % (G / GH)) * GH;
+    I.q0 = qsl[seq];
+    I.qlen = qsl[seq + 1] - I.q0;
+    int L_in = seq_lens[seq];
+    KGC_DCHECK_RANGE(L_in, 0, cap + 1, "prefill seq_len");
+    I.L = min(L_in, cap);
+    I.ctx0 = I.L - I.qlen;
+    I.qbase = mb * PF_BM + z * QB;
+    if (I.qlen <= 0 || I.ctx0 < 0 || I.qbase >= I.qlen) return false;
+    I.n_tiles = (I.ctx0 + min(I.qbase + QB, I.qlen) - 1) / PF_BN + 1;
+    I.bt = block_tables + (int64_t)seq * bt_stride;
+    return true;
+  };
+  // the first item to do at or after idx on this workgroup's stride, or n_items
+  auto next_valid = [&](int idx, Item& I) -> int {
+    while (idx < n_items && !decode(idx, I)) idx += gridDim.x;
+    return idx;
+  };
+
+  V8 qf[2][KS];
+  int qpos[2];
+  const int wrow = (wave / GH) * 32, whead = wave % GH;    // this wave's rows / head
+  auto load_q = [&](const Item& I) {
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const int qi = I.qbase + wrow + qt * 16 + r16;
+      const int qc = min(qi, I.qlen - 1);
+      qpos[qt] = I.ctx0 + qc;
+      pf_load_q<T, D>(q + (int64_t)(I.q0 + qc) * q_stride + (int64_t)(I.hg0 + whead) * D,
+                      cos_sin, cs_rows, qpos[qt], qd, qf[qt]);
+    }
+  };
+  R kreg[KPT], vreg[VPT];
+  int kblk[KPT], vblk[VPT];
+  auto fetch_bt = [&](const int* bt, int L, int kt) {
+#pragma unroll
+    for (int u = 0; u < KPT; ++u) {
+      const int key = (threadIdx.x + NT_ * u) / NCH;
+      kblk[u] = kgc_bt(bt, min(kt * PF_BN + key, L - 1) >> bs_log2, bt_stride, num_blocks);
+    }
+#pragma unroll
+    for (int u = 0; u < VPT; ++u) {
+      const int c = (threadIdx.x + NT_ * u) / D;
+      vblk[u] = kgc_bt(bt, (min(kt * PF_BN + 8 * c, L - 1) & ~7) >> bs_log2, bt_stride, num_blocks);
+    }
+  };
+  auto load_tile = [&](int L, int h, int kt) {
+#pragma unroll
+    for (int u = 0; u < KPT; ++u) {
+      const int ci = threadIdx.x + NT_ * u;
+      const int key = ci / NCH, c = ci % NCH;
+      const int ka = min(kt * PF_BN + key, L - 1);
+      const C* src = kc + ((int64_t)kblk[u] * nkv + h) * hs + (int64_t)(ka & bsm) * D + c * 8;
+      kreg[u] = *reinterpret_cast<const R*>(src);
+    }
+#pragma unroll
+    for (int u = 0; u < VPT; ++u) {
+      const int ci = threadIdx.x + NT_ * u;
+      const int c = ci / D, d = ci % D;
+      const int ka = min(kt * PF_BN + 8 * c, L - 1) & ~7;
+      const C* src = vc + ((int64_t)vblk[u] * nkv + h) * hs + ((ka & bsm) >> 3) * (D * 8) + d * 8;
+      vreg[u] = *reinterpret_cast<const R*>(src);
+    }
+  };
+  auto store_tile = [&](int buf) {
+    T* K = lds + buf * 2 * TILE;
+    T* V = K + TILE;
+#pragma unroll
+    for (int u = 0; u < KPT; ++u) {
+      const int ci = threadIdx.x + NT_ * u;
+      const int key = ci / NCH, c = ci % NCH;
+      *reinterpret_cast<u32x4*>(K + key * D + ((c ^ (kswz(key) & (NCH - 1))) * 8)) = widen(kreg[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < VPT; ++u) {
+      const int ci = threadIdx.x + NT_ * u;
+      const int c = ci / D, d = ci % D;
+      *reinterpret_cast<u32x4*>(V + d * PF_BN + ((c ^ ((d >> 1) & 7)) * 8)) = widen(vreg[u]);
+    }
+  };
+
+  Item cur, nxt;
+  int it = next_valid(blockIdx.x, cur);
+  if (it >= n_items) return;                      // uniform: the whole workgroup leaves
+  fetch_bt(cur.bt, cur.L, 0);
+  load_tile(cur.L, cur.h, 0);
+  load_q(cur);
+  store_tile(0);
+  __syncthreads();
+  int buf = 0;
+  bool kb_ready = false;     // kblk / vblk already hold the block ids of this item's tile 1
+  for (;;) {
+    const int nit = next_valid(it + gridDim.x, nxt);
+    const bool has_next = nit < n_items;
+    // the block ids of the tile loaded next: this item's tile 1, or the next item's tile 0
+    if (!kb_ready) {
+      if (cur.n_tiles > 1) fetch_bt(cur.bt, cur.L, 1);
+      else if (has_next) fetch_bt(nxt.bt, nxt.L, 0);
+    }
+    kb_ready = false;
+    const int wq0 = cur.qbase + wrow;
+    const int wave_tiles = (cur.ctx0 + min(wq0 + 31, cur.qlen - 1)) / PF_BN + 1;
+    f32x4 o[2][DT];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int t = 0; t < DT; ++t) o[qt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+    for (int kt = 0; kt < cur.n_tiles; ++kt) {
+      // the tile after this one in the stream (this item's kt + 1, else the next item's
+      // tile 0) is loaded while this one computes; then the block ids of the one after it
+      bool loaded = false;
+      if (kt + 1 < cur.n_tiles) {
+        load_tile(cur.L, cur.h, kt + 1);
+        if (kt + 2 < cur.n_tiles) fetch_bt(cur.bt, cur.L, kt + 2);
+        else if (has_next) fetch_bt(nxt.bt, nxt.L, 0);
+        loaded = true;
+      } else if (has_next) {
+        load_tile(nxt.L, nxt.h, 0);
+        if (nxt.n_tiles > 1) {
+          fetch_bt(nxt.bt, nxt.L, 1);
+          kb_ready = true;
+        }
+        loaded = true;
+      }
+      if (kt < wave_tiles) {
+        const T* K = lds + buf * 2 * TILE;
+        const T* V = K + TILE;
+        if ((kt + 1) * PF_BN - 1 > cur.ctx0 + wq0)
+          pf_wave_tile<T, D, true>(K, V, qf, o, m, l, qpos, kt * PF_BN, scale_log2, r16, qd);
+        else
+          pf_wave_tile<T, D, false>(K, V, qf, o, m, l, qpos, kt * PF_BN, scale_log2, r16, qd);
+      }
+      if (loaded) store_tile(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      float tot = l[qt];
+      tot += __shfl_xor(tot, 16, 64);
+      tot += __shfl_xor(tot, 32, 64);
+      const float inv = v_scale / tot;
+      const int qi = wq0 + qt * 16 + r16;
+      if (qi < cur.qlen && qi < cur.qbase + QB) {
+        T* orow = out + ((int64_t)(cur.q0 + qi) * nq + cur.hg0 + whead) * D + 4 * qd;
+#pragma unroll
+        for (int t = 0; t < DT; ++t) {
+          Pack4<T> pk;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) pk.h[i] = from_f<T>(o[qt][t][i] * inv);
+          *reinterpret_cast<u32x2*>(orow + 16 * t) = pk.u;
+        }
+      }
+    }
+    if (!has_next) break;
+    // the next item's first tile is already staged in LDS buffer `buf`
+    cur = nxt;
+    it = nit;
+    load_q(cur);
+  }
+}
+
 // KGC_PREFILL_GQA=0: the one-head-per-workgroup kernel everywhere (A/B and tests)
 static int prefill_gqa_enabled() {
   const char* e = getenv("KGC_PREFILL_GQA");
+  return e ? atoi(e) : 1;
+}
+
+// KGC_PREFILL_PERSIST=0: the one-shot GQA grid instead of the persistent walk (A/B, tests)
+static int prefill_persist_enabled() {
+  const char* e = getenv("KGC_PREFILL_PERSIST");
   return e ? atoi(e) : 1;
 }
 
@@ -522,6 +750,21 @@ static void prefill_gqa_dispatch(const void* q, void* out, const void* kc, const
   const size_t lds = 2 * 2 * PF_BN * D * sizeof(T);
   const int G = nq / nkv;
   const dim3 grid(n_work, nkv * (G / GH), PF_BM / (256 / GH));
+  const int64_t n_items = (int64_t)grid.x * grid.y * grid.z;
+  if (prefill_persist_enabled() && n_items < ((int64_t)1 << 30)) {
+    // one workgroup per CU (launch_bounds(512, 1), 64 KB of LDS), never more than items
+    static const int n_cu = [] {
+      int dev = 0, cu = 256;
+      if (hipGetDevice(&dev) == hipSuccess)
+        hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev);
+      return cu > 0 ? cu : 256;
+    }();
+    const int g = (int)std::min<int64_t>(n_items, n_cu);
+    prefill_attn_gqa_persist_kernel<T, D, KV8, GH><<<g, 512, lds, s>>>(
+        (const T*)q, (T*)out, kc, vc, bt, bt_stride, qsl, sl, ws, wm, nq, nkv, bs_log2,
+        scale_log2, v_scale, num_blocks, q_stride, cos_sin, cs_rows, (int)n_items);
+    return;
+  }
   prefill_attn_gqa_kernel<T, D, KV8, GH><<<grid, 512, lds, s>>>(
       (const T*)q, (T*)out, kc, vc, bt, bt_stride, qsl, sl, ws, wm, nq, nkv, bs_log2,
       scale_log2, v_scale, num_blocks, q_stride, cos_sin, cs_rows);

@@ -453,6 +453,62 @@ def test_prefill_lazy_rescale_growing_scores(gpu, monkeypatch, gqa, shape):
         torch.testing.assert_close(out[qsl[i]:qsl[i + 1]][rows], exp, atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("nq,nkv,d", [(32, 8, 128), (64, 8, 128), (8, 1, 128), (16, 4, 64)])
+@pytest.mark.parametrize("shape", ["short_many", "mixed_chunked", "one_item"])
+def test_prefill_persistent_walk_bit_identical(gpu, monkeypatch, dt, nq, nkv, d, shape):
+    """K2's persistent GQA walk (one workgroup per CU over the work list, the K / V tile
+    stream running across items; KGC_PREFILL_PERSIST=1, the default) against the one-shot
+    GQA grid (=0): the same tiles in the same order per wave, so the outputs must agree bit
+    for bit -- on many short prompts (more items than CUs, 1-8 tiles each), on mixed fresh
+    prompts and chunked continuations (empty sub-blocks, single-tile items next to long
+    ones), and on a single item -- and both within tolerance of the fp32 reference; the
+    walk also replays correctly from a captured graph."""
+    monkeypatch.setenv("KGC_PREFILL_GQA", "1")
+    torch.manual_seed(21)
+    bs = 16
+    if shape == "short_many":
+        seq_lens = [512] * 24 + [96, 33, 64, 1, 200]
+        query_lens = list(seq_lens)
+    elif shape == "mixed_chunked":
+        seq_lens = [5, 130, 300, 64, 700, 1030, 17]
+        query_lens = [5, 130, 100, 1, 257, 1030, 3]
+    else:
+        seq_lens, query_lens = [40], [40]
+    kc, vc, bt = _fill_random_cache(len(seq_lens), seq_lens, nkv, bs, d, dt, gpu)
+    qsl = [0]
+    for ql in query_lens:
+        qsl.append(qsl[-1] + ql)
+    q = torch.randn(qsl[-1], nq, d, dtype=dt, device=gpu)
+    qsl_t = torch.tensor(qsl, dtype=torch.int32, device=gpu)
+    sl_t = torch.tensor(seq_lens, dtype=torch.int32, device=gpu)
+    outs = {}
+    for persist in ("0", "1"):
+        monkeypatch.setenv("KGC_PREFILL_PERSIST", persist)
+        outs[persist] = ops.prefill_attention(q, kc, vc, bt, qsl_t, sl_t, d ** -0.5)
+    torch.cuda.synchronize()
+    assert torch.equal(outs["0"], outs["1"])
+    if shape != "short_many" or nq == 32:
+        exp = ref.prefill_attention(q.cpu(), kc.cpu(), vc.cpu(), bt.cpu(), qsl_t.cpu(),
+                                    sl_t.cpu(), d ** -0.5)
+        torch.testing.assert_close(outs["1"].cpu().float(), exp.float(), **_tol(dt))
+    # graph replay of the persistent walk
+    monkeypatch.setenv("KGC_PREFILL_PERSIST", "1")
+    ws, wm = ops.prefill_work_list(query_lens, seq_lens)
+    ws_t = torch.tensor(ws, dtype=torch.int32, device=gpu)
+    wm_t = torch.tensor(wm, dtype=torch.int32, device=gpu)
+    out = torch.empty_like(q)
+    ops.prefill_attention(q, kc, vc, bt, qsl_t, sl_t, d ** -0.5, ws_t, wm_t, out)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ops.prefill_attention(q, kc, vc, bt, qsl_t, sl_t, d ** -0.5, ws_t, wm_t, out)
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, outs["0"])
+
+
 def test_prefill_matches_dense(gpu):
     """End-to-end: rope_kv_write -> prefill kernel == dense causal attention."""
     torch.manual_seed(5)

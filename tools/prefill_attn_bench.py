@@ -1,6 +1,7 @@
 """K2 prefill attention microbenchmark: causal prefill over the paged KV cache at
 prompt lengths 512 .. 32K (Llama-3-8B heads: 32 q / 8 kv x 128), one-head-per-workgroup
-kernel (KGC_PREFILL_GQA=0) vs the GQA-shared kernel (=1).
+kernel (KGC_PREFILL_GQA=0) vs the GQA-shared kernel (=1), one-shot grid
+(KGC_PREFILL_PERSIST=0) and persistent walk (=1).
 
     python tools/prefill_attn_bench.py [--nq 32 --nkv 8] [--shapes 32x512,8x2048,2x8192,1x16384]
                                        [--chunked 32768]
@@ -82,17 +83,20 @@ def main():
         keys = sum(sum(s - ql + i + 1 for i in range(ql)) for s, ql in zip(seq_lens, qlens))
         flop = 4.0 * a.d * a.nq * keys
         res = {}
-        for gqa in ("0", "1"):
+        for gqa, persist in (("0", "0"), ("1", "0"), ("1", "1")):
             os.environ["KGC_PREFILL_GQA"] = gqa
+            os.environ["KGC_PREFILL_PERSIST"] = persist
 
             def run():
                 ops.prefill_attention(q, kc, vc, bt, qsl_t, sl_t, a.d ** -0.5, ws_t, wm_t, out)
             t = timeit(run)
-            res[gqa] = t
+            res[gqa + persist] = t
             print(json.dumps({"case": name, "nq": a.nq, "nkv": a.nkv, "gqa_kernel": gqa == "1",
+                              "persistent": persist == "1",
                               "ms": round(t * 1e3, 3), "TFLOPs": round(flop / t / 1e12, 1)}),
                   flush=True)
-        print(json.dumps({"case": name, "speedup_gqa": round(res["0"] / res["1"], 3)}), flush=True)
+        print(json.dumps({"case": name, "speedup_gqa": round(res["00"] / res["10"], 3),
+                          "speedup_persistent": round(res["10"] / res["11"], 3)}), flush=True)
         del kc, vc, q, out
         torch.cuda.empty_cache()
 
