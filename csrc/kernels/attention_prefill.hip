@@ -579,10 +579,21 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_gqa_persist_kernel(
     I.bt = block_tables + (int64_t)seq * bt_stride;
     return true;
   };
-  // the first item to do at or after idx on this workgroup's stride, or n_items
-  auto next_valid = [&](int idx, Item& I) -> int {
-    while (idx < n_items && !decode(idx, I)) idx += gridDim.x;
-    return idx;
+  // Items are dealt in rounds of gridDim.x, heaviest first (the host's work-list order),
+  // alternating direction round to round: workgroup b takes item r * G + b in even rounds
+  // and r * G + G - 1 - b in odd ones, so the workgroup dealt a round's heaviest item gets
+  // the next round's lightest (plain round-robin left long prompts ~10 % imbalanced).
+  const int G_ = gridDim.x, b_ = blockIdx.x;
+  auto item_of = [&](int r) -> int { return r * G_ + ((r & 1) ? G_ - 1 - b_ : b_); };
+  // the first round >= r whose item this workgroup has work in (its item in `I`), or a
+  // round past the list
+  auto next_valid = [&](int r, Item& I) -> int {
+    while (r * G_ < n_items) {
+      const int idx = item_of(r);
+      if (idx < n_items && decode(idx, I)) break;
+      ++r;
+    }
+    return r;
   };
 
   V8 qf[2][KS];
@@ -648,8 +659,8 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_gqa_persist_kernel(
   };
 
   Item cur, nxt;
-  int it = next_valid(blockIdx.x, cur);
-  if (it >= n_items) return;                      // uniform: the whole workgroup leaves
+  int it = next_valid(0, cur);                    // `it`: the current item's round
+  if (it * G_ >= n_items) return;                 // uniform: the whole workgroup leaves
   fetch_bt(cur.bt, cur.L, 0);
   load_tile(cur.L, cur.h, 0);
   load_q(cur);
@@ -658,8 +669,8 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_gqa_persist_kernel(
   int buf = 0;
   bool kb_ready = false;     // kblk / vblk already hold the block ids of this item's tile 1
   for (;;) {
-    const int nit = next_valid(it + gridDim.x, nxt);
-    const bool has_next = nit < n_items;
+    const int nit = next_valid(it + 1, nxt);
+    const bool has_next = nit * G_ < n_items;
     // the block ids of the tile loaded next: this item's tile 1, or the next item's tile 0
     if (!kb_ready) {
       if (cur.n_tiles > 1) fetch_bt(cur.bt, cur.L, 1);
