@@ -71,6 +71,57 @@ __device__ __forceinline__ void pf_load_q(const T* qrow, const float* __restrict
   for (int s = 0; s < KS; ++s) qf[s] = t[s].v;
 }
 
+// pf_load_q in two halves, so the loads can be issued early and the rotation done later:
+// the persistent walk issues the next item's q (and cos / sin) loads BEFORE the current
+// item's output stores -- on gfx9 stores count in vmcnt too, so loads issued after the
+// stores would wait for the stores' completion at their first use.
+template <typename T, int D>
+struct PfQRaw {
+  Pack8<T> t[D / 32];
+  float4 c[D / 64][4];       // per rotated fragment pair: cos lo / hi, sin lo / hi
+};
+// cs_row: the row's cos / sin (always a readable row -- the caller passes a dummy one
+// without RoPE -- so every register of r is written here and none stays live across the
+// caller's loop)
+template <typename T, int D>
+__device__ __forceinline__ void pf_issue_q(const T* qrow, const float* __restrict__ cs_row,
+                                           int qd, PfQRaw<T, D>& r) {
+  constexpr int KS = D / 32;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) r.t[s].u = *reinterpret_cast<const u32x4*>(qrow + 32 * s + 8 * qd);
+#pragma unroll
+  for (int s = 0; s < KS / 2; ++s) {
+    const int col = 32 * s + 8 * qd;
+    r.c[s][0] = *reinterpret_cast<const float4*>(cs_row + col);
+    r.c[s][1] = *reinterpret_cast<const float4*>(cs_row + col + 4);
+    r.c[s][2] = *reinterpret_cast<const float4*>(cs_row + D / 2 + col);
+    r.c[s][3] = *reinterpret_cast<const float4*>(cs_row + D / 2 + col + 4);
+  }
+}
+template <typename T, int D>
+__device__ __forceinline__ void pf_finish_q(PfQRaw<T, D>& r, bool rope,
+                                            typename Vec8<T>::type (&qf)[D / 32]) {
+  constexpr int KS = D / 32;
+  if (rope) {
+#pragma unroll
+    for (int s = 0; s < KS / 2; ++s) {
+      const float cc[8] = {r.c[s][0].x, r.c[s][0].y, r.c[s][0].z, r.c[s][0].w,
+                           r.c[s][1].x, r.c[s][1].y, r.c[s][1].z, r.c[s][1].w};
+      const float sn[8] = {r.c[s][2].x, r.c[s][2].y, r.c[s][2].z, r.c[s][2].w,
+                           r.c[s][3].x, r.c[s][3].y, r.c[s][3].z, r.c[s][3].w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float ra, rb;
+        neox_rot(to_f(r.t[s].h[j]), to_f(r.t[s + KS / 2].h[j]), cc[j], sn[j], ra, rb);
+        r.t[s].h[j] = from_f<T>(ra);
+        r.t[s + KS / 2].h[j] = from_f<T>(rb);
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < KS; ++s) qf[s] = r.t[s].v;
+}
+
 // Lazy O rescale (log2 units): the running max m only moves when some row's tile max
 // exceeds it by more than this, so P = exp2(s - m) stays <= 2^8 and the O / l rescale
 // (DT*8 + 2 VALU per lane) runs on a few tiles per row instead of on every tile.  The
@@ -609,6 +660,29 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_gqa_persist_kernel(
                       cos_sin, cs_rows, qpos[qt], qd, qf[qt]);
     }
   };
+  PfQRaw<T, D> qraw[2];
+  int qpos_n[2];
+  auto issue_q = [&](const Item& I) {
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const int qi = I.qbase + wrow + qt * 16 + r16;
+      const int qc = min(qi, I.qlen - 1);
+      qpos_n[qt] = I.ctx0 + qc;
+      // without RoPE the (unused) cos / sin come from a fixed readable row: q's first
+      const float* csr = cos_sin != nullptr
+                             ? cos_sin + (int64_t)min(qpos_n[qt], cs_rows - 1) * D
+                             : reinterpret_cast<const float*>(q);
+      pf_issue_q<T, D>(q + (int64_t)(I.q0 + qc) * q_stride + (int64_t)(I.hg0 + whead) * D,
+                       csr, qd, qraw[qt]);
+    }
+  };
+  auto finish_q = [&]() {
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      qpos[qt] = qpos_n[qt];
+      pf_finish_q<T, D>(qraw[qt], cos_sin != nullptr, qf[qt]);
+    }
+  };
   R kreg[KPT], vreg[VPT];
   int kblk[KPT], vblk[VPT];
   auto fetch_bt = [&](const int* bt, int L, int kt) {
@@ -714,6 +788,10 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_gqa_persist_kernel(
       __syncthreads();
       buf ^= 1;
     }
+    // the next item's q loads go out before this item's output stores (see PfQRaw);
+    // unconditional (the current item's rows again at the end of the walk) so the raw
+    // registers are written every iteration and not kept live around the loop
+    issue_q(has_next ? nxt : cur);
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       float tot = l[qt];
@@ -736,7 +814,7 @@ __global__ __launch_bounds__(512, 1) void prefill_attn_gqa_persist_kernel(
     // the next item's first tile is already staged in LDS buffer `buf`
     cur = nxt;
     it = nit;
-    load_q(cur);
+    finish_q();
   }
 }
 
