@@ -137,6 +137,44 @@ class LLMEngine:
         self.metrics.on_arrival()
         return seq
 
+    def coalescing(self) -> bool:
+        """A burst is being admitted: nothing is running or in flight, and the waiting
+        prompts fill less than one step's token budget (the engine-core loop then keeps
+        admitting arrivals for a moment before it steps: entrypoints/engine_core.py)."""
+        s = self.scheduler
+        if self.pp_depth > 1 or not s.waiting or s.running or self._inflight is not None:
+            return False
+        budget, tot = self.cfg.token_budget(), 0
+        for seq in s.waiting:
+            tot += seq.num_tokens - seq.num_computed
+            if tot >= budget:
+                return False
+        return True
+
+    def inflight_coalescing(self) -> bool:
+        """A prefill-only step of at least half the token budget is still running on the
+        GPU, and the prompts waiting now (possibly none) fill less than the next step's
+        budget: under a burst the rest is still arriving, so the engine-core loop may
+        keep admitting arrivals before it launches the next step (a partial prefill, or
+        with nothing waiting at that instant, a decode step the prefill-first policy would
+        then interleave with the burst's remaining chunks)."""
+        inf = self._inflight
+        if inf is None or self.pp_depth > 1:
+            return False
+        fut, _, plan, _, _ = inf
+        budget = self.cfg.token_budget()
+        if plan.D or plan.Tp < budget // 2 or fut.done():
+            return False
+        s = self.scheduler
+        if len(s.running) >= self.cfg.max_num_seqs:
+            return False
+        tot = 0
+        for seq in s.waiting:
+            tot += seq.num_tokens - seq.num_computed
+            if tot >= budget:
+                return False
+        return True
+
     def abort(self, request_id: str) -> None:
         s = self.scheduler.abort(request_id)
         self.seqs.pop(request_id, None)

@@ -372,6 +372,10 @@ class TokenFuture:
         self.buf, self.ev, self.values, self._lp = buf, ev, values, lp
         self._on_done = on_done
 
+    def done(self) -> bool:
+        """Non-blocking: has the step (and its token copy) completed?"""
+        return self.values is not None or self.ev is None or self.ev.query()
+
     def result(self) -> list[int]:
         if self.values is None:
             if self.ev is not None:
@@ -397,6 +401,10 @@ class PipelinedTokenFuture:
     def __init__(self, work, buf: torch.Tensor, on_done):
         self.work, self.buf, self._on_done = work, buf, on_done
         self.values: Optional[list[int]] = None
+
+    def done(self) -> bool:
+        """Non-blocking: have the last stage's ids arrived?"""
+        return self.values is not None or self.work.is_completed()
 
     def result(self) -> list[int]:
         if self.values is None:

@@ -73,6 +73,43 @@ class _Intake(threading.Thread):
         self.wake.set()
 
 
+def _drain(intake: "_Intake", eng, conns: list, owner: dict, adds, done) -> bool:
+    """Handle every message the intake thread queued.  Returns False on shutdown.
+    ``adds`` gets (receive time, frontend stamp) per admitted request."""
+    while intake.q:
+        c, msg, t_recv = intake.q.popleft()
+        if c is None:
+            conns.clear()
+            return True
+        if msg is None:
+            if c in conns:
+                conns.remove(c)        # a frontend went away: drop its requests
+            for rid in [r for r, oc in owner.items() if oc is c]:
+                owner.pop(rid)
+                eng.abort(rid)
+            continue
+        kind = msg[0]
+        if kind == "add":
+            _, rid, ids, params, arrival = msg
+            adds.append((t_recv, arrival))
+            try:
+                eng.add_request(ids, params, request_id=rid, arrival_time=arrival)
+                owner[rid] = c
+            except Exception as e:  # noqa: BLE001 - reported to that request
+                c.send(("reject", rid, f"{type(e).__name__}: {e}"))
+        elif kind == "abort":
+            owner.pop(msg[1], None)
+            eng.abort(msg[1])
+        elif kind == "metrics":
+            from prometheus_client import generate_latest
+            c.send(("metrics", msg[1], generate_latest(eng.metrics.registry).decode()))
+        elif kind == "stats":
+            c.send(("stats", msg[1], done.snapshot(msg[2])))
+        elif kind == "shutdown":
+            return False
+    return True
+
+
 def _make_engine(cfg: EngineConfig):
     if os.environ.get("KGC_FAKE_ENGINE"):
         # GPU-free timing model of the engine (engine/fake.py): load-tests the
@@ -123,7 +160,23 @@ def _core_main(cfg: EngineConfig, conn, listen: Optional[tuple] = None) -> None:
     owner: dict = {}          # request id -> connection of the frontend that submitted it
     # host-time accounting of the core loop, logged at exit: where a step's host time goes
     # besides the engine step itself (inbox handling, output fan-out to the frontends)
-    st = {"iters": 0, "steps": 0, "step_s": 0.0, "send_s": 0.0, "inbox_s": 0.0}
+    st = {"iters": 0, "steps": 0, "step_s": 0.0, "send_s": 0.0, "inbox_s": 0.0,
+          "coalesce_waits": 0}
+    # Burst admission (KGC_COALESCE_MS, default 40; KGC_COALESCE_GAP_MS, default 3): when
+    # an idle engine receives a burst (a wave of requests through the router: 256 arrive
+    # over ~50 ms), stepping at once ran the first 1, 6 and 7 requests as three small
+    # prefill steps and left a 19-request remainder after the full 16K-token chunks: 11
+    # prefill steps instead of 8, plus a decode step forced into a chunk by the prefill-
+    # first deferral bound (profiles/README.md "Round 6: burst admission").  While
+    # nothing is running and the waiting prompts fill less than one step's token budget,
+    # the loop keeps admitting as long as requests keep arriving (gaps under GAP ms), for
+    # at most COALESCE ms.  Under continuous load something is always running, so this
+    # never delays a step there.
+    coalesce_s = float(os.environ.get("KGC_COALESCE_MS", "40")) / 1e3
+    gap_s = float(os.environ.get("KGC_COALESCE_GAP_MS", "3")) / 1e3
+    coalescing = getattr(eng, "coalescing", lambda: False)
+    inflight_coalescing = getattr(eng, "inflight_coalescing", lambda: False)
+    gap_inflight_s = float(os.environ.get("KGC_COALESCE_INFLIGHT_GAP_MS", "10")) / 1e3
     # (core receive time, frontend stamp) of the latest requests (bounded: a server runs
     # for weeks)
     adds: collections.deque = collections.deque(maxlen=1 << 16)
@@ -140,38 +193,38 @@ def _core_main(cfg: EngineConfig, conn, listen: Optional[tuple] = None) -> None:
             if idle and not intake.q:
                 intake.wake.wait(0.05)
             intake.wake.clear()
-            while intake.q and running:
-                c, msg, t_recv = intake.q.popleft()
-                if c is None:
-                    conns.clear()
-                    break
-                if msg is None:
-                    if c in conns:
-                        conns.remove(c)        # a frontend went away: drop its requests
-                    for rid in [r for r, oc in owner.items() if oc is c]:
-                        owner.pop(rid)
-                        eng.abort(rid)
-                    continue
-                kind = msg[0]
-                if kind == "add":
-                    _, rid, ids, params, arrival = msg
-                    adds.append((t_recv, arrival))
-                    try:
-                        eng.add_request(ids, params, request_id=rid, arrival_time=arrival)
-                        owner[rid] = c
-                    except Exception as e:  # noqa: BLE001 - reported to that request
-                        c.send(("reject", rid, f"{type(e).__name__}: {e}"))
-                elif kind == "abort":
-                    owner.pop(msg[1], None)
-                    eng.abort(msg[1])
-                elif kind == "metrics":
-                    from prometheus_client import generate_latest
-                    c.send(("metrics", msg[1], generate_latest(eng.metrics.registry).decode()))
-                elif kind == "stats":
-                    c.send(("stats", msg[1], done.snapshot(msg[2])))
-                elif kind == "shutdown":
-                    running = False
-                    break
+            running = _drain(intake, eng, conns, owner, adds, done) and running
+            # a burst is being admitted (nothing runs yet and the waiting prompts fill
+            # less than one prefill step): keep admitting while requests keep arriving
+            if running and coalesce_s > 0 and coalescing():
+                t_end = time.monotonic() + coalesce_s
+                while running and coalescing():
+                    rem = t_end - time.monotonic()
+                    if rem <= 0:
+                        break
+                    if not intake.q and not intake.wake.wait(min(gap_s, rem)):
+                        break                  # the arrivals paused: start the step
+                    intake.wake.clear()
+                    running = _drain(intake, eng, conns, owner, adds, done) and running
+                    st["coalesce_waits"] += 1
+            # ... and while a large prefill step is on the GPU: the next step would be a
+            # partial prefill of what has arrived so far, so admit further arrivals until
+            # the step's budget fills, the arrivals pause (GAP_INFLIGHT ms since the last
+            # one) or the GPU step completes -- the next step is launched before the GPU
+            # goes idle, except when the in-flight step finishes first
+            if (running and coalesce_s > 0 and adds
+                    and time.monotonic() - adds[-1][0] < gap_inflight_s
+                    and inflight_coalescing()):
+                t_end = time.monotonic() + 0.5
+                while running and inflight_coalescing():
+                    now = time.monotonic()
+                    if now >= t_end or (adds and now - adds[-1][0] > gap_inflight_s):
+                        break
+                    if not intake.q and not intake.wake.wait(0.001):
+                        continue               # re-check: the GPU step may have completed
+                    intake.wake.clear()
+                    running = _drain(intake, eng, conns, owner, adds, done) and running
+                    st["coalesce_waits"] += 1
             if not idle:
                 st["inbox_s"] += time.perf_counter() - ti
             if running and eng.has_unfinished():
@@ -214,8 +267,8 @@ def _core_main(cfg: EngineConfig, conn, listen: Optional[tuple] = None) -> None:
         os._exit(1)
     intake.stop = True
     log.info("core loop: %d iterations, %d engine steps; host time: step %.2f s, output "
-             "fan-out %.2f s, inbox %.2f s", st["iters"], st["steps"], st["step_s"],
-             st["send_s"], st["inbox_s"])
+             "fan-out %.2f s, inbox %.2f s; burst-admission waits %d", st["iters"],
+             st["steps"], st["step_s"], st["send_s"], st["inbox_s"], st["coalesce_waits"])
     if adds:
         lat = sorted(r - a for r, a in adds)
         log.info("core intake (last %d requests): %.3f s first -> last receive; frontend -> core "
