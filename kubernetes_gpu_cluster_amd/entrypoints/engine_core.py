@@ -198,11 +198,15 @@ def _core_main(cfg: EngineConfig, conn, listen: Optional[tuple] = None) -> None:
             # less than one prefill step): keep admitting while requests keep arriving
             if running and coalesce_s > 0 and coalescing():
                 t_end = time.monotonic() + coalesce_s
+                n0 = len(adds)
                 while running and coalescing():
                     rem = t_end - time.monotonic()
                     if rem <= 0:
                         break
-                    if not intake.q and not intake.wake.wait(min(gap_s, rem)):
+                    # a lone request waits at most GAP for a follower; once followers
+                    # come (a burst), pauses of up to INFLIGHT_GAP are tolerated
+                    gap = gap_s if len(adds) - n0 < 2 else gap_inflight_s
+                    if not intake.q and not intake.wake.wait(min(gap, rem)):
                         break                  # the arrivals paused: start the step
                     intake.wake.clear()
                     running = _drain(intake, eng, conns, owner, adds, done) and running
